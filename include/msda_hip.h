@@ -1,0 +1,109 @@
+/*
+ * msda_hip.h — C-ABI of the MI355X (gfx950) multi-scale temporal deformable
+ * attention (MSDA) kernels.
+ *
+ * This is the drop-in boundary for the reference's native op
+ *   module `MultiScaleDeformableAttention`            (reference: models/ops/setup.py:53)
+ *   ms_deform_attn_forward / ms_deform_attn_backward   (reference: models/ops/src/vision.cpp:14-15,
+ *                                                       models/ops/src/ms_deform_attn.h:20-61)
+ * and for the live pure-PyTorch core it shadows
+ *   ms_deform_attn_core_pytorch                        (reference: models/modules/attention.py:331-383)
+ *
+ * Differences from the reference's pybind signature, all deliberate:
+ *   - plain device pointers + sizes, no torch types;
+ *   - level shapes / start indices are HOST arrays (the reference passes device
+ *     tensors and syncs on them at models/modules/attention.py:346,458);
+ *   - the 1-D temporal layout is native: sampling_loc is (B, Lq, M, L, P) and
+ *     spatial_shapes holds T_l (the 2-D (H=1, W=T) form of
+ *     models/ops/modules/ms_deform_attn.py:114-117 is unpacked by the host shim);
+ *   - a padding-mode tag picks the live semantics (BORDER: grid_sample
+ *     bilinear/border/align_corners=False, models/modules/attention.py:367-368)
+ *     or the dormant CUDA kernel's zero padding
+ *     (models/ops/src/cuda/ms_deform_im2col_cuda.cuh:34-85,289);
+ *   - errors come back as a non-zero status + msda_hip_last_error() text instead
+ *     of the reference's printf (ms_deform_im2col_cuda.cuh:949-953,1322-1326).
+ *
+ * Ownership: inputs are borrowed, read-only and must be contiguous (as asserted at
+ * models/ops/src/cuda/ms_deform_attn_cuda.cu:28-38,93-105). Outputs are caller
+ * allocated (the shim allocates them through the framework allocator). All work is
+ * enqueued asynchronously on `stream`; nothing in here synchronises the host.
+ */
+#ifndef MSDA_HIP_H_
+#define MSDA_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* dtype tags for value / output / grad_value / grad_output storage */
+#define MSDA_DTYPE_F32 0
+#define MSDA_DTYPE_F64 1
+#define MSDA_DTYPE_BF16 2
+#define MSDA_DTYPE_F16 3
+
+/* padding-mode tags */
+#define MSDA_PAD_BORDER 0 /* live path: grid_sample(border, align_corners=False) */
+#define MSDA_PAD_ZEROS 1  /* dormant CUDA kernel: taps outside the map read 0    */
+
+/* status codes */
+#define MSDA_OK 0
+#define MSDA_ERR_ARG 1    /* bad size / dtype / pointer                          */
+#define MSDA_ERR_LAUNCH 2 /* hipGetLastError after a launch                       */
+
+#define MSDA_MAX_LEVELS 16
+
+/* Coordinate dtype rule: sampling_loc / attn_weight / grad_loc / grad_attn are
+ * f64 when value_dtype == MSDA_DTYPE_F64 and f32 otherwise (bf16/f16 values keep
+ * fp32 locations: loc*T_l up to 4096 needs a 24-bit mantissa). */
+
+/* Forward.  Replaces ms_deform_attn_cuda_forward
+ * (reference: models/ops/src/cuda/ms_deform_attn_cuda.cu:20-80) and
+ * ms_deform_attn_core_pytorch (models/modules/attention.py:331-383).
+ *   value          (batch, spatial_size, num_heads, channels)   value_dtype
+ *   sampling_loc   (batch, num_query, num_heads, num_levels, num_point)  in [0,1] (any real accepted)
+ *   attn_weight    (batch, num_query, num_heads, num_levels, num_point)
+ *   output         (batch, num_query, num_heads*channels)        value_dtype (written, not accumulated)
+ * spatial_shapes[l] = T_l, level_start[l] = offset of level l along spatial_size (host arrays). */
+int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                     const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                     const void* attn_weight, void* output, int64_t batch, int64_t spatial_size,
+                     int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
+                     int padding_mode, void* stream);
+
+/* Bytes of fp32 scratch msda_hip_backward needs for grad_value accumulation:
+ * 0 for f32/f64 values (accumulated in place), batch*spatial*heads*channels*4 for bf16/f16. */
+size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,
+                                         int64_t num_heads, int64_t channels);
+
+/* Backward.  Replaces ms_deform_attn_cuda_backward
+ * (reference: models/ops/src/cuda/ms_deform_attn_cuda.cu:83-153) and the autograd
+ * graph of ms_deform_attn_core_pytorch (grid_sampler_2d_backward + stack/mul/sum).
+ *   grad_output    (batch, num_query, num_heads*channels)        value_dtype
+ *   grad_value     (batch, spatial_size, num_heads, channels)    value_dtype (overwritten)
+ *   grad_loc       (batch, num_query, num_heads, num_levels, num_point)  coord dtype (overwritten)
+ *   grad_attn      (batch, num_query, num_heads, num_levels, num_point)  coord dtype (overwritten)
+ *   workspace      msda_hip_backward_workspace_bytes(...) bytes of device memory (NULL if 0)
+ * Any of grad_value / grad_loc / grad_attn may be NULL to skip it.
+ * BORDER mode: grad_loc is 0 where loc*T_l-0.5 is clamped (<=0 or >=T_l-1), exactly
+ * as ATen's clip_coordinates_set_grad treats the border as out of bounds. */
+int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                      const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                      const void* attn_weight, const void* grad_output, void* grad_value,
+                      void* grad_loc, void* grad_attn, void* workspace, int64_t batch,
+                      int64_t spatial_size, int64_t num_heads, int64_t channels,
+                      int64_t num_query, int64_t num_point, int padding_mode, void* stream);
+
+/* Text of the last error raised on the calling thread ("" if none). */
+const char* msda_hip_last_error(void);
+
+/* ABI version (bumped on any signature change). */
+int msda_hip_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MSDA_HIP_H_ */

@@ -1,0 +1,43 @@
+"""MI355X-native multi-scale temporal deformable attention (MSDA) for the
+SAGA-DVC/multimodal-feature-learning deformable DVC path.
+
+Layout:
+  csrc/msda.hip        HIP kernels (gfx950) + the extern "C" entry points of include/msda_hip.h
+  lib/libmsda_hip.so   built by __graft_entry__.build()
+  _native.py           ctypes binding of the C-ABI (no fallback)
+  msda.py              host checks, layout normalisation, autograd.Function
+  MultiScaleDeformableAttention.py   mirror of the reference's pybind extension API
+  models/...           mirror of the reference modules on the path (same names / signatures)
+
+The directory name is not a Python identifier; import it with
+``importlib.import_module("multimodal-feature-learning_amd")``.  The import registers
+``mfl_amd`` (and ``mfl_amd.<submodule>``) as aliases of the same module objects.
+"""
+import sys as _sys
+
+__version__ = "0.1.0"
+
+from . import _native  # noqa: E402
+from . import msda  # noqa: E402
+from . import MultiScaleDeformableAttention  # noqa: E402
+from . import models  # noqa: E402
+from .models.modules import attention, embedding_layers, misc_modules  # noqa: E402,F401
+from .models import base_encoder  # noqa: E402,F401
+from .models.deformable import unimodal_deformable_transformer  # noqa: E402,F401
+from .models.deformable import multimodal_deformable_transformer  # noqa: E402,F401
+from .models.ops.functions import ms_deform_attn_func  # noqa: E402,F401
+from .models.ops.modules import ms_deform_attn  # noqa: E402,F401
+from . import dvc_core  # noqa: E402,F401
+
+ALIAS = "mfl_amd"
+
+
+def _register_alias():
+    prefix = __name__ + "."
+    _sys.modules.setdefault(ALIAS, _sys.modules[__name__])
+    for name, mod in list(_sys.modules.items()):
+        if name.startswith(prefix):
+            _sys.modules.setdefault(ALIAS + "." + name[len(prefix):], mod)
+
+
+_register_alias()

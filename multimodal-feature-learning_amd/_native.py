@@ -1,0 +1,88 @@
+"""ctypes binding of the C-ABI in include/msda_hip.h (libmsda_hip.so, built for gfx950).
+
+This is the only place that touches the shared library.  There is no fallback: if the
+library is missing or fails to load, every MSDA call raises ``RuntimeError`` (the
+reference's native op likewise raises ``AT_ERROR("Not implemented on the CPU")`` for
+CPU tensors, models/ops/src/cpu/ms_deform_attn_cpu.cpp:17-41).
+"""
+import ctypes
+import os
+import threading
+
+import torch
+
+LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libmsda_hip.so")
+
+# keep in sync with include/msda_hip.h
+DTYPE_TAGS = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2, torch.float16: 3}
+PAD_TAGS = {"border": 0, "zeros": 1}
+MAX_LEVELS = 16
+ABI_VERSION = 1
+
+# every symbol include/msda_hip.h declares (checked by tests/test_capi.py)
+EXPORTED_SYMBOLS = (
+    "msda_hip_forward",
+    "msda_hip_backward",
+    "msda_hip_backward_workspace_bytes",
+    "msda_hip_last_error",
+    "msda_hip_abi_version",
+)
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib):
+    i64, vp, i32 = ctypes.c_int64, ctypes.c_void_p, ctypes.c_int
+    p64 = ctypes.POINTER(ctypes.c_int64)
+    lib.msda_hip_forward.restype = i32
+    lib.msda_hip_forward.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp,
+                                     i64, i64, i64, i64, i64, i64, i32, vp]
+    lib.msda_hip_backward.restype = i32
+    lib.msda_hip_backward.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp, vp, vp, vp,
+                                      i64, i64, i64, i64, i64, i64, i32, vp]
+    lib.msda_hip_backward_workspace_bytes.restype = ctypes.c_size_t
+    lib.msda_hip_backward_workspace_bytes.argtypes = [i32, i64, i64, i64, i64]
+    lib.msda_hip_last_error.restype = ctypes.c_char_p
+    lib.msda_hip_last_error.argtypes = []
+    lib.msda_hip_abi_version.restype = i32
+    lib.msda_hip_abi_version.argtypes = []
+    return lib
+
+
+def load_library():
+    """Load (once) and return the ctypes handle of libmsda_hip.so; raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(
+                    f"MSDA HIP library not built: {LIB_PATH} is missing. "
+                    "Run `python -c 'import __graft_entry__ as g; g.build()'` first.")
+            lib = _declare(ctypes.CDLL(LIB_PATH))
+            ver = lib.msda_hip_abi_version()
+            if ver != ABI_VERSION:
+                raise RuntimeError(f"libmsda_hip.so ABI {ver} != expected {ABI_VERSION}; rebuild")
+            _lib = lib
+    return _lib
+
+
+def last_error():
+    return load_library().msda_hip_last_error().decode(errors="replace")
+
+
+def check(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (status {rc}): {last_error()}")
+
+
+def host_i64_array(values):
+    arr = (ctypes.c_int64 * len(values))(*[int(v) for v in values])
+    return arr
+
+
+def stream_handle(device):
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

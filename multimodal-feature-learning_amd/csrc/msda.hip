@@ -1,0 +1,572 @@
+// msda.hip — multi-scale temporal deformable attention (MSDA) for MI355X / gfx950.
+//
+// What it computes (the live semantics of the reference):
+//   out[b,q,m,:] = sum_l sum_p aw[b,q,m,l,p] * lerp(V_l[b,:,m,:], y)
+//   y = clamp(fma((2*loc-1)+1, T_l/2, -0.5), 0, T_l-1)           (BORDER)
+// i.e. F.grid_sample(bilinear, border, align_corners=False) on a (B*M, D, T_l, 1)
+// image at grid x=-1 — reference models/modules/attention.py:349-383 — and its
+// autograd backward (ATen grid_sampler_2d_backward + stack/mul/sum).  The dormant
+// CUDA extension's zero padding (models/ops/src/cuda/ms_deform_im2col_cuda.cuh:34-85,
+// 238-300) is available as MSDA_PAD_ZEROS for the models/ops API.
+//
+// Layout in HBM (all row-major, contiguous):
+//   value  (B, S, M, D)   one (b,s,m) row = D channels, rows of one token are M*D apart
+//   loc/aw (B, Lq, M, L, P) fp32 (fp64 for fp64 values)
+//   out    (B, Lq, M*D)
+//
+// Work decomposition: one "item" = one (b, q, m) output row.  G = D/VEC lanes of a
+// 64-wide wavefront own one item (VEC channels per lane, 16-byte loads), so every
+// tap is one coalesced G*16-byte row read; 64/G items share a wavefront.  The
+// per-sample coordinate arithmetic is uniform inside a lane group.
+// Backward: grad_aw / grad_loc are reductions over the item's D channels = a
+// butterfly over the G lanes of the group (__shfl_xor, no LDS, no barriers);
+// grad_value is a scatter-add of the two taps with fp32/fp64 global atomics
+// (bf16/fp16 values accumulate in an fp32 workspace, converted once at the end).
+//
+// Coordinates are computed with FP contraction OFF in exactly the operation order of
+// ATen's CPU grid sampler (g = 2*loc-1, then y = fma(g+1, T/2, -0.5)), so the tap index
+// and the clamp decision are bit-identical to the CPU reference: the loc-gradient jumps
+// at integer positions, and a one-ulp different y would flip the segment.
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string.h>
+
+#include "msda_hip.h"
+
+namespace {
+
+thread_local char g_last_error[512] = {0};
+
+template <typename... A>
+void set_error(const char* fmt, A... a) {
+  snprintf(g_last_error, sizeof(g_last_error), fmt, a...);
+}
+void set_error(const char* msg) { snprintf(g_last_error, sizeof(g_last_error), "%s", msg); }
+
+struct Levels {
+  int T[MSDA_MAX_LEVELS];
+  int start[MSDA_MAX_LEVELS];
+};
+
+// ---------------------------------------------------------------------------------
+// storage types and 16-byte vector I/O
+// ---------------------------------------------------------------------------------
+struct bf16_t { uint16_t x; };
+struct f16_t { uint16_t x; };
+
+template <typename scalar_t> struct AccOf { using type = float; };
+template <> struct AccOf<double> { using type = double; };
+
+__device__ __forceinline__ float to_acc(float v) { return v; }
+__device__ __forceinline__ double to_acc(double v) { return v; }
+__device__ __forceinline__ float to_acc(bf16_t v) { return __uint_as_float(((uint32_t)v.x) << 16); }
+__device__ __forceinline__ float to_acc(f16_t v) {
+  return __half2float(__ushort_as_half(v.x));
+}
+
+__device__ __forceinline__ void from_acc(float a, float* d) { *d = a; }
+__device__ __forceinline__ void from_acc(double a, double* d) { *d = a; }
+__device__ __forceinline__ void from_acc(float a, bf16_t* d) {
+  __hip_bfloat16 h = __float2bfloat16(a);  // RNE, NaN stays NaN
+  d->x = *reinterpret_cast<uint16_t*>(&h);
+}
+__device__ __forceinline__ void from_acc(float a, f16_t* d) {
+  d->x = __half_as_ushort(__float2half(a));
+}
+
+// Load VEC consecutive elements (16 B when VEC*sizeof == 16) into the accumulator type.
+template <typename scalar_t, int VEC>
+__device__ __forceinline__ void load_vec(const scalar_t* __restrict__ p,
+                                         typename AccOf<scalar_t>::type (&r)[VEC]) {
+  if constexpr (VEC * sizeof(scalar_t) == 16) {
+    const uint4 raw = *reinterpret_cast<const uint4*>(p);
+    const scalar_t* e = reinterpret_cast<const scalar_t*>(&raw);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) r[i] = to_acc(e[i]);
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) r[i] = to_acc(p[i]);
+  }
+}
+
+template <typename scalar_t, int VEC>
+__device__ __forceinline__ void store_vec(scalar_t* __restrict__ p,
+                                          const typename AccOf<scalar_t>::type (&r)[VEC]) {
+  if constexpr (VEC * sizeof(scalar_t) == 16) {
+    uint4 raw;
+    scalar_t* e = reinterpret_cast<scalar_t*>(&raw);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) from_acc(r[i], &e[i]);
+    *reinterpret_cast<uint4*>(p) = raw;
+  } else {
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) from_acc(r[i], &p[i]);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// sampling coordinates
+// ---------------------------------------------------------------------------------
+template <typename coord_t>
+struct Taps {
+  int i0, i1;      // tap rows inside the level (always valid addresses)
+  coord_t w0, w1;  // interpolation weights (0 for a tap outside the map)
+  bool ok0, ok1;   // tap inside the map
+  coord_t gmul;    // d(y)/d(loc) with the clamp folded in (0 where clamped / skipped)
+};
+
+// BORDER: grid_sample(bilinear, padding_mode='border', align_corners=False) along a
+// T-long axis at normalized grid coordinate g = 2*loc-1 (attention.py:349,367-368).
+template <typename coord_t>
+__device__ __forceinline__ Taps<coord_t> taps_border(coord_t loc, int T) {
+#pragma clang fp contract(off)
+  Taps<coord_t> t;
+  const coord_t g = loc * (coord_t)2 - (coord_t)1;
+  // ATen's CPU sampler fuses the unnormalize into one FMA (pinned in tests/test_oracle.py)
+  const coord_t y = fma(g + (coord_t)1, (coord_t)T * (coord_t)0.5, (coord_t)-0.5);
+  const coord_t ymax = (coord_t)(T - 1);
+  // ATen clip_coordinates_get_grad: the border itself counts as out of bounds.
+  const bool inb = (y > (coord_t)0) && (y < ymax);
+  const coord_t yc = y > (coord_t)0 ? (y < ymax ? y : ymax) : (coord_t)0;
+  const coord_t y0 = floor(yc);
+  const coord_t n = yc - y0;
+  t.i0 = (int)y0;
+  t.i1 = t.i0 + 1;
+  t.ok0 = true;
+  t.ok1 = t.i1 <= T - 1;
+  if (!t.ok1) t.i1 = t.i0;
+  t.w0 = (coord_t)1 - n;
+  t.w1 = n;
+  // dy/dloc = 2 (from g) * T/2 (unnormalize)
+  t.gmul = inb ? (coord_t)T : (coord_t)0;
+  return t;
+}
+
+// ZEROS: the dormant CUDA kernel's 1-D (H=1) semantics: w_im = loc*T - 0.5, the sample is
+// skipped unless -1 < w_im < T, taps outside [0, T-1] read 0
+// (ms_deform_im2col_cuda.cuh:34-85 and :276-290; ms_deform_attn.py:114-117 lift).
+template <typename coord_t>
+__device__ __forceinline__ Taps<coord_t> taps_zeros(coord_t loc, int T) {
+#pragma clang fp contract(off)
+  Taps<coord_t> t;
+  const coord_t x = loc * (coord_t)T - (coord_t)0.5;
+  const bool live = (x > (coord_t)-1) && (x < (coord_t)T);
+  const coord_t x0 = floor(live ? x : (coord_t)0);
+  const coord_t lw = (live ? x : (coord_t)0) - x0;
+  const int lo = (int)x0;
+  t.ok0 = live && lo >= 0;
+  t.ok1 = live && lo + 1 <= T - 1;
+  t.i0 = t.ok0 ? lo : 0;
+  t.i1 = t.ok1 ? lo + 1 : 0;
+  t.w0 = t.ok0 ? (coord_t)1 - lw : (coord_t)0;
+  t.w1 = t.ok1 ? lw : (coord_t)0;
+  t.gmul = live ? (coord_t)T : (coord_t)0;
+  return t;
+}
+
+template <typename coord_t, bool ZEROS>
+__device__ __forceinline__ Taps<coord_t> make_taps(coord_t loc, int T) {
+  if constexpr (ZEROS) return taps_zeros(loc, T);
+  else return taps_border(loc, T);
+}
+
+// ---------------------------------------------------------------------------------
+// forward
+// ---------------------------------------------------------------------------------
+template <typename scalar_t, typename coord_t, int VEC, bool ZEROS>
+__global__ __launch_bounds__(256) void msda_fwd_kernel(
+    const scalar_t* __restrict__ value, const coord_t* __restrict__ loc,
+    const coord_t* __restrict__ aw, scalar_t* __restrict__ out, const Levels lv, const int L,
+    const int P, const int S, const int M, const int D, const int Lq, const long long n_items,
+    const int gshift) {
+  using acc_t = typename AccOf<scalar_t>::type;
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long item = tid >> gshift;
+  if (item >= n_items) return;
+  const int G = 1 << gshift;
+  const int lg = (int)(tid & (G - 1));
+  const int m = (int)(item % M);
+  const long long b = item / M / Lq;
+  const long long rowstride = (long long)M * D;
+  const coord_t* __restrict__ locp = loc + item * (L * P);
+  const coord_t* __restrict__ awp = aw + item * (L * P);
+  const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D;
+  scalar_t* __restrict__ op = out + item * D;
+  const int nchunk = D / VEC;
+  for (int ck = lg; ck < nchunk; ck += G) {
+    acc_t acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[e] = (acc_t)0;
+    for (int l = 0; l < L; ++l) {
+      const int T = lv.T[l];
+      const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rowstride + ck * VEC;
+      for (int p = 0; p < P; ++p) {
+        const coord_t a = awp[l * P + p];
+        const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locp[l * P + p], T);
+        acc_t v0[VEC], v1[VEC];
+        load_vec<scalar_t, VEC>(vl + t.i0 * rowstride, v0);
+        load_vec<scalar_t, VEC>(vl + t.i1 * rowstride, v1);
+        const acc_t w0 = (acc_t)t.w0, w1 = (acc_t)t.w1, aa = (acc_t)a;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          const acc_t x0 = t.ok0 ? v0[e] : (acc_t)0;
+          const acc_t x1 = t.ok1 ? v1[e] : (acc_t)0;
+          acc[e] += aa * (x0 * w0 + x1 * w1);
+        }
+      }
+    }
+    store_vec<scalar_t, VEC>(op + ck * VEC, acc);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// backward
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void atomic_add_acc(float* p, float v) { unsafeAtomicAdd(p, v); }
+__device__ __forceinline__ void atomic_add_acc(double* p, double v) { unsafeAtomicAdd(p, v); }
+
+template <typename scalar_t, typename coord_t, typename gacc_t, int VEC, bool ZEROS>
+__global__ __launch_bounds__(256) void msda_bwd_kernel(
+    const scalar_t* __restrict__ value, const coord_t* __restrict__ loc,
+    const coord_t* __restrict__ aw, const scalar_t* __restrict__ gout,
+    gacc_t* __restrict__ gval, coord_t* __restrict__ gloc, coord_t* __restrict__ gaw,
+    const Levels lv, const int L, const int P, const int S, const int M, const int D,
+    const int Lq, const long long n_items, const int gshift) {
+  using acc_t = typename AccOf<scalar_t>::type;
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long item_raw = tid >> gshift;
+  // every lane stays alive for the butterfly reductions below
+  const bool active = item_raw < n_items;
+  const long long item = active ? item_raw : 0;
+  const int G = 1 << gshift;
+  const int lg = (int)(tid & (G - 1));
+  const int m = (int)(item % M);
+  const long long b = item / M / Lq;
+  const long long rowstride = (long long)M * D;
+  const coord_t* __restrict__ locp = loc + item * (L * P);
+  const coord_t* __restrict__ awp = aw + item * (L * P);
+  const long long vrow0 = (b * S * M + m) * (long long)D;
+  const scalar_t* __restrict__ vb = value + vrow0;
+  const scalar_t* __restrict__ gp = gout + item * D;
+  const int nchunk = D / VEC;
+  for (int l = 0; l < L; ++l) {
+    const int T = lv.T[l];
+    const long long lbase = (long long)lv.start[l] * rowstride;
+    for (int p = 0; p < P; ++p) {
+      const coord_t a = awp[l * P + p];
+      const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locp[l * P + p], T);
+      const acc_t w0 = (acc_t)t.w0, w1 = (acc_t)t.w1, aa = (acc_t)a;
+      acc_t pa = (acc_t)0;  // d out / d aw
+      acc_t pl = (acc_t)0;  // sum_c g * (v1 - v0)
+      if (active) {
+        for (int ck = lg; ck < nchunk; ck += G) {
+          acc_t g[VEC], v0[VEC], v1[VEC];
+          load_vec<scalar_t, VEC>(gp + ck * VEC, g);
+          load_vec<scalar_t, VEC>(vb + lbase + t.i0 * rowstride + ck * VEC, v0);
+          load_vec<scalar_t, VEC>(vb + lbase + t.i1 * rowstride + ck * VEC, v1);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            const acc_t x0 = t.ok0 ? v0[e] : (acc_t)0;
+            const acc_t x1 = t.ok1 ? v1[e] : (acc_t)0;
+            pa += g[e] * (x0 * w0 + x1 * w1);
+            pl += g[e] * (x1 - x0);
+          }
+          if (gval != nullptr) {
+            gacc_t* gv = gval + vrow0 + lbase + ck * VEC;
+            if (t.ok0 && t.w0 != (coord_t)0) {
+              const acc_t s0 = aa * w0;
+#pragma unroll
+              for (int e = 0; e < VEC; ++e) atomic_add_acc(gv + t.i0 * rowstride + e, (gacc_t)(s0 * g[e]));
+            }
+            if (t.ok1 && t.w1 != (coord_t)0) {
+              const acc_t s1 = aa * w1;
+#pragma unroll
+              for (int e = 0; e < VEC; ++e) atomic_add_acc(gv + t.i1 * rowstride + e, (gacc_t)(s1 * g[e]));
+            }
+          }
+        }
+      }
+      // butterfly over the G lanes of this item (G divides 64, groups are aligned)
+      for (int off = G >> 1; off > 0; off >>= 1) {
+        pa += __shfl_xor(pa, off);
+        pl += __shfl_xor(pl, off);
+      }
+      if (active && lg == 0) {
+        const long long o = item * (L * P) + l * P + p;
+        if (gaw != nullptr) gaw[o] = (coord_t)pa;
+        if (gloc != nullptr) gloc[o] = (coord_t)(pl * aa) * t.gmul;
+      }
+    }
+  }
+}
+
+// fp32 accumulator -> bf16/fp16 grad_value
+template <typename scalar_t>
+__global__ __launch_bounds__(256) void cast_from_f32_kernel(const float* __restrict__ src,
+                                                           scalar_t* __restrict__ dst,
+                                                           long long n) {
+  const long long i0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (i0 + 3 < n) {
+    const float4 v = *reinterpret_cast<const float4*>(src + i0);
+    from_acc(v.x, dst + i0);
+    from_acc(v.y, dst + i0 + 1);
+    from_acc(v.z, dst + i0 + 2);
+    from_acc(v.w, dst + i0 + 3);
+  } else {
+    for (long long i = i0; i < n; ++i) from_acc(src[i], dst + i);
+  }
+}
+
+// ---------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------
+struct Problem {
+  long long B, S, M, D, Lq, L, P;
+  Levels lv;
+};
+
+int check_problem(const int64_t* shapes, const int64_t* starts, int64_t L, int64_t B,
+                  int64_t S, int64_t M, int64_t D, int64_t Lq, int64_t P, Problem* pr) {
+  if (L < 1 || L > MSDA_MAX_LEVELS) {
+    set_error("msda: num_levels=%lld must be in [1, %d]", (long long)L, MSDA_MAX_LEVELS);
+    return MSDA_ERR_ARG;
+  }
+  if (B < 0 || S < 0 || M < 1 || D < 1 || Lq < 0 || P < 1) {
+    set_error("msda: bad sizes (B=%lld S=%lld M=%lld D=%lld Lq=%lld P=%lld)", (long long)B, (long long)S, (long long)M, (long long)D, (long long)Lq, (long long)P);
+    return MSDA_ERR_ARG;
+  }
+  if (shapes == nullptr || starts == nullptr) {
+    set_error("msda: spatial_shapes / level_start must be host arrays");
+    return MSDA_ERR_ARG;
+  }
+  for (int64_t l = 0; l < L; ++l) {
+    if (shapes[l] < 1 || starts[l] < 0 || starts[l] + shapes[l] > S) {
+      set_error("msda: level %lld (T=%lld, start=%lld) does not fit spatial_size=%lld", (long long)l,
+                (long long)shapes[l], (long long)starts[l], (long long)S);
+      return MSDA_ERR_ARG;
+    }
+    pr->lv.T[l] = (int)shapes[l];
+    pr->lv.start[l] = (int)starts[l];
+  }
+  if (S > (1LL << 30) || D > (1LL << 20) || M * D * S > (1LL << 40)) {
+    set_error("msda: problem too large");
+    return MSDA_ERR_ARG;
+  }
+  pr->B = B; pr->S = S; pr->M = M; pr->D = D; pr->Lq = Lq; pr->L = L; pr->P = P;
+  return MSDA_OK;
+}
+
+int pick_vec(int dtype, long long D) {
+  const int elt = dtype == MSDA_DTYPE_F64 ? 8 : (dtype == MSDA_DTYPE_F32 ? 4 : 2);
+  const int v = 16 / elt;
+  return (D % v == 0) ? v : 1;
+}
+
+int group_shift_for(long long nchunk) {
+  int s = 0;
+  while ((1LL << s) < nchunk && s < 6) ++s;
+  return s;
+}
+
+int launch_status(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    set_error("msda: %s launch failed: %s", what, hipGetErrorString(e));
+    return MSDA_ERR_LAUNCH;
+  }
+  return MSDA_OK;
+}
+
+template <typename scalar_t, typename coord_t, int VEC>
+int run_forward(const Problem& pr, const void* value, const void* loc, const void* aw, void* out,
+                int pad, hipStream_t st) {
+  const long long n_items = pr.B * pr.Lq * pr.M;
+  if (n_items == 0) return MSDA_OK;
+  const int gshift = group_shift_for(pr.D / VEC);
+  const long long threads = n_items << gshift;
+  const unsigned blocks = (unsigned)((threads + 255) / 256);
+  auto* v = static_cast<const scalar_t*>(value);
+  auto* lc = static_cast<const coord_t*>(loc);
+  auto* a = static_cast<const coord_t*>(aw);
+  auto* o = static_cast<scalar_t*>(out);
+  if (pad == MSDA_PAD_ZEROS)
+    hipLaunchKernelGGL((msda_fwd_kernel<scalar_t, coord_t, VEC, true>), dim3(blocks), dim3(256), 0,
+                       st, v, lc, a, o, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M,
+                       (int)pr.D, (int)pr.Lq, n_items, gshift);
+  else
+    hipLaunchKernelGGL((msda_fwd_kernel<scalar_t, coord_t, VEC, false>), dim3(blocks), dim3(256),
+                       0, st, v, lc, a, o, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M,
+                       (int)pr.D, (int)pr.Lq, n_items, gshift);
+  return launch_status("forward");
+}
+
+template <typename scalar_t, typename coord_t, typename gacc_t, int VEC>
+int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
+                 const void* gout, gacc_t* gacc, void* gloc, void* gaw, int pad, hipStream_t st) {
+  const long long n_items = pr.B * pr.Lq * pr.M;
+  if (n_items == 0) return MSDA_OK;
+  const int gshift = group_shift_for(pr.D / VEC);
+  const long long threads = n_items << gshift;
+  const unsigned blocks = (unsigned)((threads + 255) / 256);
+  auto* v = static_cast<const scalar_t*>(value);
+  auto* lc = static_cast<const coord_t*>(loc);
+  auto* a = static_cast<const coord_t*>(aw);
+  auto* g = static_cast<const scalar_t*>(gout);
+  auto* gl = static_cast<coord_t*>(gloc);
+  auto* ga = static_cast<coord_t*>(gaw);
+  if (pad == MSDA_PAD_ZEROS)
+    hipLaunchKernelGGL((msda_bwd_kernel<scalar_t, coord_t, gacc_t, VEC, true>), dim3(blocks),
+                       dim3(256), 0, st, v, lc, a, g, gacc, gl, ga, pr.lv, (int)pr.L, (int)pr.P,
+                       (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, n_items, gshift);
+  else
+    hipLaunchKernelGGL((msda_bwd_kernel<scalar_t, coord_t, gacc_t, VEC, false>), dim3(blocks),
+                       dim3(256), 0, st, v, lc, a, g, gacc, gl, ga, pr.lv, (int)pr.L, (int)pr.P,
+                       (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, n_items, gshift);
+  return launch_status("backward");
+}
+
+}  // namespace
+
+extern "C" {
+
+int msda_hip_abi_version(void) { return 1; }
+
+const char* msda_hip_last_error(void) { return g_last_error; }
+
+size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,
+                                         int64_t num_heads, int64_t channels) {
+  if (value_dtype == MSDA_DTYPE_BF16 || value_dtype == MSDA_DTYPE_F16)
+    return (size_t)batch * spatial_size * num_heads * channels * sizeof(float);
+  return 0;
+}
+
+int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                     const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                     const void* attn_weight, void* output, int64_t batch, int64_t spatial_size,
+                     int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
+                     int padding_mode, void* stream) {
+  g_last_error[0] = 0;
+  Problem pr;
+  int rc = check_problem(spatial_shapes, level_start, num_levels, batch, spatial_size, num_heads,
+                         channels, num_query, num_point, &pr);
+  if (rc) return rc;
+  if (padding_mode != MSDA_PAD_BORDER && padding_mode != MSDA_PAD_ZEROS) {
+    set_error("msda: unknown padding_mode %d", padding_mode);
+    return MSDA_ERR_ARG;
+  }
+  const long long n_out = pr.B * pr.Lq * pr.M * pr.D;
+  if (n_out > 0 && (output == nullptr || sampling_loc == nullptr || attn_weight == nullptr ||
+                    (pr.S > 0 && value == nullptr))) {
+    set_error("msda_hip_forward: null pointer");
+    return MSDA_ERR_ARG;
+  }
+  if (pr.S == 0 && n_out > 0) {
+    set_error("msda_hip_forward: empty value with non-empty query");
+    return MSDA_ERR_ARG;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const int vec = pick_vec(value_dtype, pr.D);
+  switch (value_dtype) {
+    case MSDA_DTYPE_F32:
+      return vec == 4 ? run_forward<float, float, 4>(pr, value, sampling_loc, attn_weight, output, padding_mode, st)
+                      : run_forward<float, float, 1>(pr, value, sampling_loc, attn_weight, output, padding_mode, st);
+    case MSDA_DTYPE_F64:
+      return vec == 2 ? run_forward<double, double, 2>(pr, value, sampling_loc, attn_weight, output, padding_mode, st)
+                      : run_forward<double, double, 1>(pr, value, sampling_loc, attn_weight, output, padding_mode, st);
+    case MSDA_DTYPE_BF16:
+      return vec == 8 ? run_forward<bf16_t, float, 8>(pr, value, sampling_loc, attn_weight, output, padding_mode, st)
+                      : run_forward<bf16_t, float, 1>(pr, value, sampling_loc, attn_weight, output, padding_mode, st);
+    case MSDA_DTYPE_F16:
+      return vec == 8 ? run_forward<f16_t, float, 8>(pr, value, sampling_loc, attn_weight, output, padding_mode, st)
+                      : run_forward<f16_t, float, 1>(pr, value, sampling_loc, attn_weight, output, padding_mode, st);
+    default:
+      set_error("msda_hip_forward: unknown value dtype %d", value_dtype);
+      return MSDA_ERR_ARG;
+  }
+}
+
+int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                      const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                      const void* attn_weight, const void* grad_output, void* grad_value,
+                      void* grad_loc, void* grad_attn, void* workspace, int64_t batch,
+                      int64_t spatial_size, int64_t num_heads, int64_t channels,
+                      int64_t num_query, int64_t num_point, int padding_mode, void* stream) {
+  g_last_error[0] = 0;
+  Problem pr;
+  int rc = check_problem(spatial_shapes, level_start, num_levels, batch, spatial_size, num_heads,
+                         channels, num_query, num_point, &pr);
+  if (rc) return rc;
+  if (padding_mode != MSDA_PAD_BORDER && padding_mode != MSDA_PAD_ZEROS) {
+    set_error("msda: unknown padding_mode %d", padding_mode);
+    return MSDA_ERR_ARG;
+  }
+  const bool half_like = value_dtype == MSDA_DTYPE_BF16 || value_dtype == MSDA_DTYPE_F16;
+  const long long n_val = pr.B * pr.S * pr.M * pr.D;
+  const long long n_items = pr.B * pr.Lq * pr.M;
+  const size_t coord_sz = value_dtype == MSDA_DTYPE_F64 ? 8 : 4;
+  const size_t elt = value_dtype == MSDA_DTYPE_F64 ? 8 : (value_dtype == MSDA_DTYPE_F32 ? 4 : 2);
+  if (n_items > 0 && (sampling_loc == nullptr || attn_weight == nullptr ||
+                      grad_output == nullptr || (pr.S > 0 && value == nullptr))) {
+    set_error("msda_hip_backward: null input pointer");
+    return MSDA_ERR_ARG;
+  }
+  if (half_like && grad_value != nullptr && n_val > 0 && workspace == nullptr) {
+    set_error("msda_hip_backward: bf16/f16 values need an fp32 workspace");
+    return MSDA_ERR_ARG;
+  }
+  if (pr.S == 0 && n_items > 0) {
+    set_error("msda_hip_backward: empty value with non-empty query");
+    return MSDA_ERR_ARG;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // zero-init like at::zeros / zeros_like (ms_deform_attn_cuda.cu:121-123)
+  void* gacc = half_like ? workspace : grad_value;
+  if (grad_value != nullptr && n_val > 0) {
+    if (hipMemsetAsync(gacc, 0, (size_t)n_val * (half_like ? 4 : elt), st) != hipSuccess) {
+      set_error("msda_hip_backward: hipMemsetAsync failed");
+      return MSDA_ERR_LAUNCH;
+    }
+  }
+  if (grad_value == nullptr) gacc = nullptr;
+  const int vec = pick_vec(value_dtype, pr.D);
+  switch (value_dtype) {
+    case MSDA_DTYPE_F32:
+      rc = vec == 4 ? run_backward<float, float, float, 4>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st)
+                    : run_backward<float, float, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st);
+      break;
+    case MSDA_DTYPE_F64:
+      rc = vec == 2 ? run_backward<double, double, double, 2>(pr, value, sampling_loc, attn_weight, grad_output, (double*)gacc, grad_loc, grad_attn, padding_mode, st)
+                    : run_backward<double, double, double, 1>(pr, value, sampling_loc, attn_weight, grad_output, (double*)gacc, grad_loc, grad_attn, padding_mode, st);
+      break;
+    case MSDA_DTYPE_BF16:
+      rc = vec == 8 ? run_backward<bf16_t, float, float, 8>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st)
+                    : run_backward<bf16_t, float, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st);
+      break;
+    case MSDA_DTYPE_F16:
+      rc = vec == 8 ? run_backward<f16_t, float, float, 8>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st)
+                    : run_backward<f16_t, float, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st);
+      break;
+    default:
+      set_error("msda_hip_backward: unknown value dtype %d", value_dtype);
+      return MSDA_ERR_ARG;
+  }
+  if (rc) return rc;
+  if (half_like && grad_value != nullptr && n_val > 0) {
+    const unsigned blocks = (unsigned)(((n_val + 3) / 4 + 255) / 256);
+    if (value_dtype == MSDA_DTYPE_BF16)
+      hipLaunchKernelGGL(cast_from_f32_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st,
+                         (const float*)workspace, (bf16_t*)grad_value, n_val);
+    else
+      hipLaunchKernelGGL(cast_from_f32_kernel<f16_t>, dim3(blocks), dim3(256), 0, st,
+                         (const float*)workspace, (f16_t*)grad_value, n_val);
+    rc = launch_status("grad_value cast");
+  }
+  (void)coord_sz;
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,97 @@
+"""The measured workload: the proposal path of the reference's ``UnimodalDeformableDVC``
+(models/deformable/unimodal_deformable_dvc.py:26-203) — sine position + duration embedding,
+Conv1d pyramid (BaseEncoder), deformable encoder / decoder, and the per-decoder-level
+class / segment / count heads — without the Hungarian matching and caption decoder
+(host-side / out of scope; the reference wrapper crashes past the
+heads at HEAD).
+
+Submodule names follow the reference wrapper (``pos_embed``, ``base_encoder``,
+``unimodal_deformable_transformer``, ``query_embedding``, ``class_embedding``,
+``segment_embedding``, ``count_head``) so its state_dict keys map one to one.
+"""
+import math
+
+import torch
+from torch import nn
+
+from .models.base_encoder import BaseEncoder
+from .models.deformable.unimodal_deformable_transformer import DeformableTransformer
+from .models.modules.embedding_layers import FFN, PositionEmbeddingVideoSine
+from .models.modules.misc_modules import predict_event_num
+
+__all__ = ["DeformableDVCCore", "synthetic_clips", "workload_loss"]
+
+
+class DeformableDVCCore(nn.Module):
+    def __init__(self, d_model=512, num_queries=100, num_classes=200, max_eseq_length=10, feature_dim=512,
+                 num_heads=8, num_feature_levels=4, enc_layers=6, dec_layers=6, ff_dim=2048, dropout=0.1,
+                 enc_n_points=4, dec_n_points=4):
+        super().__init__()
+        self.num_queries = num_queries
+        self.query_embedding = nn.Embedding(num_queries, d_model * 2)
+        class_embedding = nn.Linear(d_model, num_classes + 1)
+        segment_embedding = FFN(in_dim=d_model, hidden_dim=d_model, out_dim=2, num_layers=3)
+        count_head = nn.Linear(d_model, max_eseq_length + 1)
+        self.pos_embed = PositionEmbeddingVideoSine(d_model // 2, normalize=True)
+        self.base_encoder = BaseEncoder(num_feature_levels, feature_dim, d_model)
+        # head init of unimodal_deformable_dvc.py:59-71
+        prior_prob = 0.01
+        class_embedding.bias.data = torch.ones(num_classes + 1) * -math.log((1 - prior_prob) / prior_prob)
+        nn.init.constant_(segment_embedding.layers[-1].weight.data, 0)
+        nn.init.constant_(segment_embedding.layers[-1].bias.data, 0)
+        self.unimodal_deformable_transformer = DeformableTransformer(
+            d_model=d_model, num_head=num_heads, num_encoder_layers=enc_layers, num_decoder_layers=dec_layers,
+            dim_feedforward=ff_dim, dropout=dropout, activation="relu", return_intermediate_dec=True,
+            num_feature_levels=num_feature_levels, dec_n_points=dec_n_points, enc_n_points=enc_n_points)
+        nn.init.constant_(segment_embedding.layers[-1].bias.data[2:], -2.0)
+        # heads shared across decoder levels, as the reference does (:72-74)
+        self.class_embedding = nn.ModuleList([class_embedding for _ in range(dec_layers)])
+        self.count_head = nn.ModuleList([count_head for _ in range(dec_layers)])
+        self.segment_embedding = nn.ModuleList([segment_embedding for _ in range(dec_layers)])
+
+    def forward(self, video, video_mask, durations):
+        """video (B, T, feature_dim), video_mask (B, T) bool True = pad, durations (B,)
+        -> dict with pred_logits / pred_segments / pred_count (last level), the stacked
+        per-level head outputs, hs (dec_layers, B, Q, d) and memory (B, S, d)."""
+        tr = self.unimodal_deformable_transformer
+        B = video.shape[0]
+        srcs, masks, pos = self.base_encoder(video, video_mask, durations, self.pos_embed)
+        src_flatten, shapes, starts, valid, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(srcs, masks, pos)
+        memory = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten)
+        qw = self.query_embedding.weight
+        query_mask = torch.ones(B, qw.shape[0], dtype=torch.bool, device=qw.device)
+        _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qw)
+        hs, inter = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten, query_mask,
+                                       False)
+        classes, segments, counts = [], [], []
+        for lvl in range(hs.shape[0]):
+            classes.append(self.class_embedding[lvl](hs[lvl]).softmax(dim=-1))
+            segments.append(self.segment_embedding[lvl](hs[lvl]).sigmoid())
+            counts.append(predict_event_num(self.count_head[lvl], hs[lvl]))
+        cls, seg, cnt = torch.stack(classes), torch.stack(segments), torch.stack(counts)
+        return {"pred_logits": cls[-1], "pred_segments": seg[-1], "pred_count": cnt[-1],
+                "all_logits": cls, "all_segments": seg, "all_counts": cnt,
+                "hs": hs, "inter_references": inter, "memory": memory}
+
+
+def synthetic_clips(batch, T=1024, feature_dim=512, padded=False, seed=0, device="cpu", dtype=torch.float32):
+    """ActivityNet-shaped synthetic inputs (BASELINE.md / SURVEY §8(d)): features ~ N(0,1)
+    (seed), masks all valid or valid length U[T/2, T] (seed+1), durations U(30, 240) s (seed+2)."""
+    g = torch.Generator().manual_seed(seed)
+    video = torch.randn((batch, T, feature_dim), generator=g).to(dtype)
+    mask = torch.zeros(batch, T, dtype=torch.bool)
+    if padded:
+        gm = torch.Generator().manual_seed(seed + 1)
+        for b in range(batch):
+            valid = int(torch.randint(T // 2, T + 1, (1,), generator=gm))
+            mask[b, valid:] = True
+    gd = torch.Generator().manual_seed(seed + 2)
+    durations = torch.rand(batch, generator=gd, dtype=torch.float64) * 210.0 + 30.0
+    return video.to(device), mask.to(device), durations.to(device)
+
+
+def workload_loss(out):
+    """hs.sum() + memory.sum() (isolates the path from matcher / criterion)
+    plus the heads' outputs, so every head and decoder level carries gradient."""
+    return (out["hs"].float().sum() + out["memory"].float().sum() + out["all_segments"].float().sum()
+            + out["all_counts"].float().sum() + (out["all_logits"].float() * 1e-2).square().sum())

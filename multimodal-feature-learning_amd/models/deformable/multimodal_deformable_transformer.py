@@ -1,0 +1,279 @@
+"""Video + audio deformable encoder/decoder, same interface as the reference's
+``models/deformable/multimodal_deformable_transformer.py``.
+
+Every encoder layer makes four MSDA calls with ONE shared ``self_attn`` module
+(video->video, audio->audio, audio queries over video values, video queries over
+audio values; reference :256-270); every decoder layer two MSDA cross-attentions
+(video, audio) followed by the concat / LayerNorm(2d) / Linear / ReLU bridge
+(:410-428).  All MSDA calls run on the HIP kernel through ``MSDeformAttn``.
+"""
+import math
+
+import torch
+from torch import nn
+from torch.nn.init import constant_, normal_, xavier_uniform_
+
+from ..modules.attention import MSDeformAttn
+from ..modules.misc_modules import inverse_sigmoid
+from .unimodal_deformable_transformer import (_get_activation_fn, _get_clones, encoder_reference_points,
+                                              level_metadata)
+
+__all__ = [
+    "MultimodalDeformableTransformer", "MultimodalDeformableTransformerEncoderLayer",
+    "MultimodalDeformableTransformerEncoder", "MultimodalDeformableTransformerDecoderLayer",
+    "MultimodalDeformableTransformerDecoder", "build_multimodal_deformable_transformer",
+]
+
+
+class MultimodalDeformableTransformer(nn.Module):
+    """reference multimodal_deformable_transformer.py:11-218 (same constructor, submodule
+    names and init; ``pos_trans`` / ``pos_trans_norm`` exist here as in the reference)."""
+
+    def __init__(self, d_model=256, num_head=8, num_encoder_layers=6, num_decoder_layers=6,
+                 dim_feedforward=1024, dropout=0.1, activation="relu", return_intermediate_dec=False,
+                 num_feature_levels=4, dec_n_points=4, enc_n_points=4):
+        super().__init__()
+        self.d_model = d_model
+        self.num_head = num_head
+        self.no_encoder = num_encoder_layers == 0
+        self.num_feature_levels = num_feature_levels
+        self.encoder = MultimodalDeformableTransformerEncoder(
+            MultimodalDeformableTransformerEncoderLayer(d_model, dim_feedforward, dropout, activation,
+                                                        num_feature_levels, num_head, enc_n_points),
+            num_encoder_layers)
+        self.decoder = MultimodalDeformableTransformerDecoder(
+            MultimodalDeformableTransformerDecoderLayer(d_model, dim_feedforward, dropout, activation,
+                                                        num_feature_levels, num_head, dec_n_points),
+            num_decoder_layers, return_intermediate_dec)
+        self.level_embed = nn.Parameter(torch.Tensor(num_feature_levels, d_model))
+        self.pos_trans = nn.Linear(d_model, d_model * 2)
+        self.pos_trans_norm = nn.LayerNorm(d_model * 2)
+        self.reference_points = nn.Linear(d_model, 1)
+        self._reset_parameters()
+
+    def _reset_parameters(self):
+        for p in self.parameters():
+            if p.dim() > 1:
+                nn.init.xavier_uniform_(p)
+        for m in self.modules():
+            if isinstance(m, MSDeformAttn):
+                m._reset_parameters()
+        xavier_uniform_(self.reference_points.weight.data, gain=1.0)
+        constant_(self.reference_points.bias.data, 0.)
+        normal_(self.level_embed)
+
+    def get_proposal_pos_embed(self, proposals):
+        num_pos_feats, temperature, scale = 256, 10000, 2 * math.pi
+        dim_t = torch.arange(num_pos_feats, dtype=torch.float32, device=proposals.device)
+        dim_t = temperature ** (2 * (dim_t // 2) / num_pos_feats)
+        pos = (proposals.sigmoid() * scale)[:, :, :, None] / dim_t
+        return torch.stack((pos[:, :, :, 0::2].sin(), pos[:, :, :, 1::2].cos()), dim=4).flatten(2)
+
+    def get_valid_ratio(self, mask):
+        return torch.sum(~mask, 1).float() / mask.shape[1]
+
+    def prepare_encoder_inputs(self, srcs, masks, pos_embeds):
+        """One modality's pyramid -> flattened inputs (reference :87-131)."""
+        src_flatten = torch.cat([s.transpose(1, 2) for s in srcs], 1)
+        lvl_pos_embed_flatten = torch.cat(
+            [p.transpose(1, 2) + self.level_embed[lvl].view(1, 1, -1) for lvl, p in enumerate(pos_embeds)], 1)
+        mask_flatten = torch.cat(list(masks), 1)
+        temporal_shapes, level_start_index = level_metadata([s.shape[-1] for s in srcs], src_flatten.device)
+        valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
+        return src_flatten, temporal_shapes, level_start_index, valid_ratios, lvl_pos_embed_flatten, mask_flatten
+
+    def forward_encoder(self, video_src_flatten, video_temporal_shapes, video_level_start_index, video_valid_ratios,
+                        video_lvl_pos_embed_flatten, video_mask_flatten, audio_src_flatten, audio_temporal_shapes,
+                        audio_level_start_index, audio_valid_ratios, audio_lvl_pos_embed_flatten, audio_mask_flatten):
+        """:return (audio_attended_visual (B, S_v, d), visual_attended_audio (B, S_a, d)) (reference :133-166)"""
+        if self.no_encoder:
+            return video_src_flatten, audio_src_flatten
+        return self.encoder(video_src_flatten, video_temporal_shapes, video_level_start_index, video_valid_ratios,
+                            video_lvl_pos_embed_flatten, video_mask_flatten, audio_src_flatten, audio_temporal_shapes,
+                            audio_level_start_index, audio_valid_ratios, audio_lvl_pos_embed_flatten,
+                            audio_mask_flatten)
+
+    def prepare_decoder_input_query(self, batch_size, query_embed):
+        query_embed, tgt = torch.chunk(query_embed, 2, dim=1)
+        query_embed = query_embed.unsqueeze(0).expand(batch_size, -1, -1)
+        tgt = tgt.unsqueeze(0).expand(batch_size, -1, -1)
+        reference_points = self.reference_points(query_embed).sigmoid()
+        return reference_points, tgt, reference_points, query_embed
+
+    def prepare_decoder_input_proposal(self, gt_reference_points):
+        topk_coords_unact = inverse_sigmoid(gt_reference_points)
+        pos_trans_out = self.pos_trans_norm(self.pos_trans(self.get_proposal_pos_embed(topk_coords_unact)))
+        query_embed, tgt = torch.chunk(pos_trans_out, 2, dim=2)
+        return gt_reference_points, tgt, gt_reference_points, query_embed
+
+    def forward_decoder(self, *kargs):
+        return self.decoder(*kargs)
+
+
+class MultimodalDeformableTransformerEncoderLayer(nn.Module):
+    """reference :221-277.  Returns ``(audio_attended_visual, visual_attended_audio)``."""
+
+    def __init__(self, d_model=256, d_ffn=1024, dropout=0.1, activation="relu", n_levels=4, n_heads=8, n_points=4):
+        super().__init__()
+        self.self_attn = MSDeformAttn(d_model, n_levels, n_heads, n_points)
+        self.dropout1 = nn.Dropout(dropout)
+        self.norm1 = nn.LayerNorm(d_model)
+        self.linear1 = nn.Linear(d_model, d_ffn)
+        self.activation = _get_activation_fn(activation)
+        self.dropout2 = nn.Dropout(dropout)
+        self.linear2 = nn.Linear(d_ffn, d_model)
+        self.dropout3 = nn.Dropout(dropout)
+        self.norm2 = nn.LayerNorm(d_model)
+
+    @staticmethod
+    def with_pos_embed(tensor, pos):
+        return tensor if pos is None else tensor + pos
+
+    def forward_ffn(self, src):
+        hidden = self.dropout2(self.activation(self.linear1(src)))
+        return self.norm2(src + self.dropout3(self.linear2(hidden)))
+
+    def _self_block(self, src, pos, ref, shapes, starts, mask):
+        attn = self.self_attn(self.with_pos_embed(src, pos), ref, src, shapes, starts, mask)
+        return self.norm1(src + self.dropout1(attn))
+
+    def forward(self, video_src, video_pos, video_reference_points, video_temporal_shapes, video_level_start_index,
+                video_padding_mask, audio_src, audio_pos, audio_reference_points, audio_temporal_shapes,
+                audio_level_start_index, audio_padding_mask):
+        video_src = self._self_block(video_src, video_pos, video_reference_points, video_temporal_shapes,
+                                     video_level_start_index, video_padding_mask)
+        audio_src = self._self_block(audio_src, audio_pos, audio_reference_points, audio_temporal_shapes,
+                                     audio_level_start_index, audio_padding_mask)
+        # cross-modal: queries of one stream sample the other stream's values (no residual, no pos)
+        visual_attended_audio = self.self_attn(audio_src, audio_reference_points, video_src, video_temporal_shapes,
+                                               video_level_start_index, video_padding_mask)
+        audio_attended_visual = self.self_attn(video_src, video_reference_points, audio_src, audio_temporal_shapes,
+                                               audio_level_start_index, audio_padding_mask)
+        return self.forward_ffn(audio_attended_visual), self.forward_ffn(visual_attended_audio)
+
+
+class MultimodalDeformableTransformerEncoder(nn.Module):
+    """reference :280-335"""
+
+    def __init__(self, encoder_layer, num_layers):
+        super().__init__()
+        self.layers = _get_clones(encoder_layer, num_layers)
+        self.num_layers = num_layers
+
+    @staticmethod
+    def get_reference_points(temporal_shapes, valid_ratios, device):
+        return encoder_reference_points(temporal_shapes, valid_ratios, device)
+
+    def forward(self, video_src, video_temporal_shapes, video_level_start_index, video_valid_ratios, video_pos,
+                video_padding_mask, audio_src, audio_temporal_shapes, audio_level_start_index, audio_valid_ratios,
+                audio_pos, audio_padding_mask):
+        video_ref = self.get_reference_points(video_temporal_shapes, video_valid_ratios, device=video_src.device)
+        audio_ref = self.get_reference_points(audio_temporal_shapes, audio_valid_ratios, device=audio_src.device)
+        output = video_src, audio_src
+        for layer in self.layers:
+            v, a = output
+            output = layer(v, video_pos, video_ref, video_temporal_shapes, video_level_start_index, video_padding_mask,
+                           a, audio_pos, audio_ref, audio_temporal_shapes, audio_level_start_index, audio_padding_mask)
+        return output
+
+
+class MultimodalDeformableTransformerDecoderLayer(nn.Module):
+    """reference :338-432"""
+
+    def __init__(self, d_model=256, d_ffn=1024, dropout=0.1, activation="relu", n_levels=4, n_heads=8, n_points=4):
+        super().__init__()
+        self.cross_attn = MSDeformAttn(d_model, n_levels, n_heads, n_points)
+        self.dropout1 = nn.Dropout(dropout)
+        self.norm1 = nn.LayerNorm(d_model)
+        self.self_attn = nn.MultiheadAttention(d_model, n_heads, dropout=dropout)
+        self.dropout2 = nn.Dropout(dropout)
+        self.norm2 = nn.LayerNorm(d_model)
+        self.linear1 = nn.Linear(d_model, d_ffn)
+        self.activation = _get_activation_fn(activation)
+        self.dropout3 = nn.Dropout(dropout)
+        self.linear2 = nn.Linear(d_ffn, d_model)
+        self.dropout4 = nn.Dropout(dropout)
+        self.norm3 = nn.LayerNorm(d_model)
+        self.norm4 = nn.LayerNorm(2 * d_model)
+        self.linear3 = nn.Linear(2 * d_model, d_model)
+        self.dropout5 = nn.Dropout(dropout)
+
+    @staticmethod
+    def with_pos_embed(tensor, pos):
+        return tensor if pos is None else tensor + pos
+
+    def forward_ffn(self, tgt):
+        hidden = self.dropout3(self.activation(self.linear1(tgt)))
+        return self.norm3(tgt + self.dropout4(self.linear2(hidden)))
+
+    def _cross_block(self, tgt, query_pos, ref, src, shapes, starts, mask):
+        attn = self.cross_attn(self.with_pos_embed(tgt, query_pos), ref, src, shapes, starts, mask)
+        return self.norm1(tgt + self.dropout1(attn))
+
+    def forward(self, tgt, query_pos, reference_points_input_video, reference_points_input_audio, query_mask,
+                video_src, video_temporal_shapes, video_level_start_index, video_src_padding_mask, audio_src,
+                audio_temporal_shapes, audio_level_start_index, audio_src_padding_mask):
+        qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
+        sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
+        tgt = self.norm2(tgt + self.dropout2(sa))
+        tgt_video = self._cross_block(tgt, query_pos, reference_points_input_video, video_src, video_temporal_shapes,
+                                      video_level_start_index, video_src_padding_mask)
+        tgt_audio = self._cross_block(tgt, query_pos, reference_points_input_audio, audio_src, audio_temporal_shapes,
+                                      audio_level_start_index, audio_src_padding_mask)
+        bridged = self.linear3(self.norm4(torch.cat([tgt_video, tgt_audio], dim=-1)))
+        tgt = self.activation(self.dropout5(bridged))
+        return self.forward_ffn(tgt)
+
+
+class MultimodalDeformableTransformerDecoder(nn.Module):
+    """reference :435-512"""
+
+    def __init__(self, decoder_layer, num_layers, return_intermediate=False):
+        super().__init__()
+        self.layers = _get_clones(decoder_layer, num_layers)
+        self.num_layers = num_layers
+        self.return_intermediate = return_intermediate
+        self.bbox_head = None
+
+    @staticmethod
+    def _per_level(reference_points, valid_ratios):
+        if reference_points.shape[-1] == 2:
+            return reference_points[:, :, None] * torch.stack([valid_ratios, valid_ratios], -1)[:, None]
+        assert reference_points.shape[-1] == 1
+        return reference_points[:, :, None] * valid_ratios[:, None, :, None]
+
+    def forward(self, tgt, reference_points, query_pos, query_padding_mask, video_src, video_temporal_shapes,
+                video_level_start_index, video_valid_ratios, video_padding_mask, audio_src, audio_temporal_shapes,
+                audio_level_start_index, audio_valid_ratios, audio_padding_mask, disable_iterative_refine=False):
+        output = tgt
+        hs, refs = [], []
+        for lid, layer in enumerate(self.layers):
+            ref_v = self._per_level(reference_points, video_valid_ratios)
+            ref_a = self._per_level(reference_points, audio_valid_ratios)
+            output = layer(output, query_pos, ref_v, ref_a, query_padding_mask, video_src, video_temporal_shapes,
+                           video_level_start_index, video_padding_mask, audio_src, audio_temporal_shapes,
+                           audio_level_start_index, audio_padding_mask)
+            if not disable_iterative_refine and self.bbox_head is not None:
+                delta = self.bbox_head[lid](output)
+                if reference_points.shape[-1] == 2:
+                    refined = (delta + inverse_sigmoid(reference_points)).sigmoid()
+                else:
+                    refined = delta
+                    refined[..., :1] = delta[..., :1] + inverse_sigmoid(reference_points)
+                    refined = refined.sigmoid()
+                reference_points = refined.detach()
+            if self.return_intermediate:
+                hs.append(output)
+                refs.append(reference_points)
+        if self.return_intermediate:
+            return torch.stack(hs), torch.stack(refs)
+        return output, reference_points
+
+
+def build_multimodal_deformable_transformer(args):
+    return MultimodalDeformableTransformer(
+        d_model=args.d_model, num_head=args.num_heads, num_encoder_layers=args.enc_layers,
+        num_decoder_layers=args.dec_layers, dim_feedforward=args.transformer_ff_dim,
+        dropout=args.transformer_dropout_prob, activation="relu",
+        return_intermediate_dec=args.return_intermediate, num_feature_levels=args.num_feature_levels,
+        dec_n_points=args.dec_n_points, enc_n_points=args.enc_n_points)

@@ -1,0 +1,162 @@
+"""MSDA interface of the reference's ``models/modules/attention.py``, backed by the HIP kernel.
+
+Drop-in for the three MSDA symbols the reference's transformers import
+(``from ..modules.attention import MSDeformAttn`` — reference
+models/deformable/unimodal_deformable_transformer.py:10 and friends):
+
+* ``ms_deform_attn_core_pytorch``  — reference attention.py:331-383 (live core).
+  Same signature and result; computed by ``msda_hip_forward`` / ``msda_hip_backward``
+  in border mode instead of per-level ``F.grid_sample``.
+* ``MSDeformAttnFunction``          — reference attention.py:310-328 (dormant call
+  into the CUDA extension).  Same ``apply`` signature; zero-padding semantics of the
+  extension kernel (ms_deform_im2col_cuda.cuh:34-85).
+* ``MSDeformAttn``                  — reference attention.py:394-511.  Same constructor,
+  parameter names / init and forward signature, including ``is_sparse``.
+
+There is no CPU path (see ``msda.py``).
+"""
+import math
+import warnings
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+from torch.nn.init import constant_, xavier_uniform_
+
+from ... import msda as _msda
+from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
+from ..ops.modules.ms_deform_attn import stack_sampled_values
+
+__all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn"]
+
+
+def _loc5(sampling_locations):
+    """(B,Lq,M,L,P) or the live module's (B,Lq,M,L,P,1) form -> (B,Lq,M,L,P)."""
+    if sampling_locations.dim() == 6 and sampling_locations.shape[-1] == 1:
+        return sampling_locations[..., 0]
+    if sampling_locations.dim() == 5:
+        return sampling_locations
+    raise ValueError(f"sampling_locations must be (B,Lq,M,L,P[,1]); got {tuple(sampling_locations.shape)}")
+
+
+def ms_deform_attn_core_pytorch(value, value_temporal_shapes, sampling_locations, attention_weights,
+                                return_value=False):
+    """Live MSDA core, reference attention.py:331-383 (border padding, align_corners=False).
+
+    :param value (batch_size, sum of tokens over levels, n_heads, d_model/n_heads)
+    :param value_temporal_shapes (n_levels,) or (n_levels, 1)
+    :param sampling_locations (batch_size, Lq, n_heads, n_levels, n_points[, 1])
+    :param attention_weights (batch_size, Lq, n_heads, n_levels, n_points)
+    :return (batch_size, Lq, n_heads * d_model/n_heads), contiguous
+    """
+    shapes, starts = _msda.host_levels(value_temporal_shapes)
+    loc = _loc5(sampling_locations)
+    if return_value:
+        # reference attention.py:376-378: per-sample values stacked (B*M, D, Lq, L, P); unused by the models
+        return stack_sampled_values(value, shapes, starts, loc, attention_weights, "border")
+    return _msda.msda_apply(value, shapes, starts, loc, attention_weights, "border")
+
+
+def _is_power_of_2(n):
+    if (not isinstance(n, int)) or (n < 0):
+        raise ValueError("invalid input for _is_power_of_2: {} (type: {})".format(n, type(n)))
+    return (n & (n - 1) == 0) and n != 0
+
+
+class MSDeformAttn(nn.Module):
+    """Multi-scale temporal deformable attention, reference attention.py:394-511.
+
+    Parameters, their names (``sampling_offsets``, ``attention_weights``,
+    ``value_proj``, ``output_proj``) and their initialisation follow the reference
+    (attention.py:426-442: xavier attention weights, not the ops module's zero init),
+    so reference state_dicts load unchanged.
+    """
+
+    def __init__(self, d_model=256, n_levels=4, n_heads=8, n_points=4):
+        super().__init__()
+        if d_model % n_heads != 0:
+            raise ValueError('d_model must be divisible by n_heads, but got {} and {}'.format(d_model, n_heads))
+        _d_per_head = d_model // n_heads
+        if not _is_power_of_2(_d_per_head):
+            warnings.warn("You'd better set d_model in MSDeformAttn to make the dimension of each attention "
+                          "head a power of 2 which is more efficient in our CUDA implementation.")
+        self.im2col_step = 64
+        self.d_model = d_model
+        self.n_levels = n_levels
+        self.n_heads = n_heads
+        self.n_points = n_points
+        self.sampling_offsets = nn.Linear(d_model, n_heads * n_levels * n_points)
+        self.attention_weights = nn.Linear(d_model, n_heads * n_levels * n_points)
+        self.value_proj = nn.Linear(d_model, d_model)
+        self.output_proj = nn.Linear(d_model, d_model)
+        self._reset_parameters()
+
+    def _reset_parameters(self):
+        constant_(self.sampling_offsets.weight.data, 0.)
+        thetas = torch.arange(self.n_heads, dtype=torch.float32) * (2 * math.pi / self.n_heads)
+        grid_init = torch.stack([thetas.cos(), thetas.sin()], -1)
+        grid_init = (grid_init / grid_init.abs().max(-1, keepdim=True)[0]).view(self.n_heads, 1, 1, 2)
+        grid_init = grid_init[..., 0].repeat(1, self.n_levels, self.n_points)
+        for i in range(self.n_points):
+            grid_init[:, :, i] *= i + 1
+        with torch.no_grad():
+            self.sampling_offsets.bias = nn.Parameter(grid_init.view(-1))
+        xavier_uniform_(self.attention_weights.weight.data)
+        constant_(self.attention_weights.bias.data, 0.)
+        xavier_uniform_(self.value_proj.weight.data)
+        constant_(self.value_proj.bias.data, 0.)
+        xavier_uniform_(self.output_proj.weight.data)
+        constant_(self.output_proj.bias.data, 0.)
+
+    def forward(self, query, reference_points, input_flatten, input_spatial_shapes,
+                input_level_start_index, input_padding_mask=None, is_sparse=False):
+        """
+        :param query                   (N, Len_q, C)
+        :param reference_points        (N, Len_q, n_levels, 1) in [0, 1], or (N, Len_q, n_levels, 2) (centre, length)
+        :param input_flatten           (N, sum_l T_l, C)
+        :param input_spatial_shapes    (n_levels,) [T_0, ..., T_{L-1}]
+        :param input_level_start_index (n_levels,)
+        :param input_padding_mask      (N, sum_l T_l) bool, True = padding
+        :return output (N, Len_q, C)  [, sampling_locations (N,Len_q,M,L,P,1), attention_weights (N,Len_q,M,L,P)]
+        """
+        N, Len_q, _ = query.shape
+        N, Len_in, _ = input_flatten.shape
+        shapes, starts = _msda.host_levels(input_spatial_shapes, input_level_start_index)
+        assert sum(shapes) == Len_in  # attention.py:458, without the device sync
+
+        value = self.value_proj(input_flatten)
+        if input_padding_mask is not None:
+            value = value.masked_fill(input_padding_mask[..., None], float(0))
+        value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
+
+        sampling_offsets = self.sampling_offsets(query).view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
+        attention_weights = self.attention_weights(query).view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
+        attention_weights = F.softmax(attention_weights, -1).view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
+
+        if reference_points.shape[-1] == 1:
+            normalizer = _shape_tensor(input_spatial_shapes, shapes, query.device)
+            sampling_locations = reference_points[:, :, None, :, None, 0] \
+                + sampling_offsets / normalizer[None, None, None, :, None]
+        elif reference_points.shape[-1] == 2:
+            sampling_locations = reference_points[:, :, None, :, None, 0] \
+                + sampling_offsets / self.n_points * reference_points[:, :, None, :, None, 1] * 0.5
+        else:
+            raise ValueError(
+                'Last dim of reference_points must be 1 or 2, but get {} instead.'.format(reference_points.shape[-1]))
+
+        # host-side T_l tuple: no (L,1) device tensor, no .split() sync (attention.py:346,495)
+        output = ms_deform_attn_core_pytorch(value, shapes, sampling_locations, attention_weights)
+        output = self.output_proj(output)
+        if is_sparse:
+            return output, sampling_locations.unsqueeze(-1), attention_weights
+        return output
+
+
+def _shape_tensor(input_spatial_shapes, shapes, device):
+    """The int64 (L,) T_l tensor the reference divides offsets by (attention.py:474-476).
+
+    Dividing by the integer tensor keeps the reference's dtype promotion (bf16 offsets
+    under autocast stay bf16)."""
+    if isinstance(input_spatial_shapes, torch.Tensor) and input_spatial_shapes.device == device:
+        return input_spatial_shapes.reshape(-1)
+    return torch.as_tensor(shapes, dtype=torch.long, device=device)

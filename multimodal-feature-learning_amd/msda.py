@@ -1,0 +1,241 @@
+"""Host side of the MSDA hot path: tensor checks, layout normalisation, the C-ABI calls
+and the autograd.Function.
+
+Semantics follow the reference's live core ``ms_deform_attn_core_pytorch``
+(models/modules/attention.py:331-383, padding "border") or its dormant CUDA extension
+(models/ops/src/cuda/ms_deform_im2col_cuda.cuh, padding "zeros").  There is no CPU
+path: a non-ROCm tensor raises, like the reference extension's CPU stub
+(models/ops/src/cpu/ms_deform_attn_cpu.cpp:17-41).
+"""
+import torch
+from torch.autograd import Function
+from torch.autograd.function import once_differentiable
+
+from . import _native
+
+__all__ = [
+    "host_levels", "msda_forward", "msda_backward", "MSDAFunction", "msda_apply", "KernelTimer",
+    "algorithmic_bytes",
+]
+
+_timer = None  # KernelTimer while bench.py measures; None otherwise
+
+
+def algorithmic_bytes(kind, B, S, M, D, Lq, L, P, value_bytes):
+    """Algorithmic HBM bytes of one launch: every value / loc / aw / out
+    element once; backward adds grad_out, the fp32 grad_value and grad_loc / grad_aw."""
+    vals = B * S * M * D
+    coords = 2 * B * Lq * M * L * P * 4
+    rows = B * Lq * M * D
+    if kind == "fwd":
+        return vals * value_bytes + coords + rows * value_bytes
+    return vals * value_bytes + rows * value_bytes + coords + vals * 4 + coords
+
+
+class KernelTimer:
+    """Brackets every MSDA C-ABI call with HIP events on the stream the kernel runs on
+    (torch's current stream, which is what the C-ABI is given).  Records
+    (kind, Lq, algorithmic bytes, start, end); read after a synchronize."""
+
+    def __init__(self):
+        self.records = []
+
+    def __enter__(self):
+        global _timer
+        _timer = self
+        return self
+
+    def __exit__(self, *exc):
+        global _timer
+        _timer = None
+        return False
+
+    def _begin(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def _end(self, kind, key, nbytes, ev0):
+        ev1 = torch.cuda.Event(enable_timing=True)
+        ev1.record()
+        self.records.append((kind, key, nbytes, ev0, ev1))
+
+    def summary(self):
+        """{(kind, key): {"launches", "total_ms", "avg_ms", "bytes_per_launch"}}"""
+        out = {}
+        for kind, key, nbytes, e0, e1 in self.records:
+            d = out.setdefault((kind, key), {"launches": 0, "total_ms": 0.0, "bytes_per_launch": nbytes})
+            d["launches"] += 1
+            d["total_ms"] += e0.elapsed_time(e1)
+        for d in out.values():
+            d["avg_ms"] = d["total_ms"] / d["launches"]
+        return out
+
+
+def _as_int_list(x):
+    if isinstance(x, torch.Tensor):
+        return [int(v) for v in x.reshape(-1).tolist()]  # device tensor => one host sync
+    return [int(v) for v in x]
+
+
+def host_levels(spatial_shapes, level_start_index=None):
+    """Normalise level metadata to host tuples ``(T_l...), (start_l...)``.
+
+    Accepts the forms the reference passes around: a (L,) tensor of T_l
+    (unimodal_deformable_transformer.py:129), the (L,1) form of attention.py:495, the
+    (L,2) ``[H, W]`` form of the 2-D extension API with H == 1
+    (models/ops/modules/ms_deform_attn.py:117), or plain Python sequences.  A tensor
+    carrying a ``_mfl_host`` attribute (set by this package's transformer) is read
+    without touching the device.
+    """
+    cached = getattr(spatial_shapes, "_mfl_host", None)
+    if cached is not None:
+        shapes = tuple(cached)
+    elif isinstance(spatial_shapes, torch.Tensor) and spatial_shapes.dim() == 2:
+        if spatial_shapes.shape[1] == 1:
+            shapes = tuple(_as_int_list(spatial_shapes[:, 0]))
+        elif spatial_shapes.shape[1] == 2:
+            hw = spatial_shapes.tolist()
+            if any(int(h) != 1 for h, _ in hw):
+                raise NotImplementedError(
+                    "MSDA HIP kernel is temporal (1-D): 2-D spatial_shapes must have H == 1, got "
+                    f"{hw}")
+            shapes = tuple(int(w) for _, w in hw)
+        else:
+            raise ValueError(f"spatial_shapes must be (L,), (L,1) or (L,2); got {tuple(spatial_shapes.shape)}")
+    else:
+        shapes = tuple(_as_int_list(spatial_shapes))
+    if level_start_index is None:
+        starts, acc = [], 0
+        for t in shapes:
+            starts.append(acc)
+            acc += t
+        starts = tuple(starts)
+    else:
+        cached = getattr(level_start_index, "_mfl_host", None)
+        starts = tuple(cached) if cached is not None else tuple(_as_int_list(level_start_index))
+    if len(starts) != len(shapes):
+        raise ValueError(f"level_start_index has {len(starts)} levels, spatial_shapes {len(shapes)}")
+    return shapes, starts
+
+
+def _coord_dtype(value):
+    return torch.float64 if value.dtype == torch.float64 else torch.float32
+
+
+def _check_inputs(value, loc, aw, shapes, starts):
+    if value.dtype not in _native.DTYPE_TAGS:
+        raise TypeError(f"MSDA: unsupported value dtype {value.dtype}")
+    for name, t in (("value", value), ("sampling_loc", loc), ("attn_weight", aw)):
+        if not t.is_cuda:
+            raise RuntimeError(f"MSDA HIP kernel: {name} must be a ROCm device tensor (got {t.device}); "
+                               "there is no CPU implementation")
+        if not t.is_contiguous():
+            raise ValueError(f"MSDA: {name} must be contiguous")
+    if value.dim() != 4:
+        raise ValueError(f"value must be (B, S, M, D); got {tuple(value.shape)}")
+    B, S, M, D = value.shape
+    if loc.dim() != 5 or aw.dim() != 5:
+        raise ValueError(f"sampling_loc / attn_weight must be (B, Lq, M, L, P); got "
+                         f"{tuple(loc.shape)} / {tuple(aw.shape)}")
+    if tuple(loc.shape) != tuple(aw.shape):
+        raise ValueError(f"sampling_loc {tuple(loc.shape)} and attn_weight {tuple(aw.shape)} differ")
+    if loc.shape[0] != B or loc.shape[2] != M or loc.shape[3] != len(shapes):
+        raise ValueError(f"shape mismatch: value {tuple(value.shape)}, loc {tuple(loc.shape)}, "
+                         f"{len(shapes)} levels")
+    if len(shapes) > _native.MAX_LEVELS:
+        raise ValueError(f"at most {_native.MAX_LEVELS} levels supported")
+    cd = _coord_dtype(value)
+    if loc.dtype != cd or aw.dtype != cd:
+        raise TypeError(f"MSDA: sampling_loc / attn_weight must be {cd} for {value.dtype} values")
+    if len(shapes) and max(s + t for s, t in zip(starts, shapes)) > S:
+        raise ValueError(f"levels {shapes} starting at {starts} exceed spatial size {S}")
+
+
+def msda_forward(value, shapes, starts, loc, aw, padding_mode="border"):
+    """out (B, Lq, M*D) = MSDA(value (B,S,M,D), loc/aw (B,Lq,M,L,P)) on the HIP kernel."""
+    _check_inputs(value, loc, aw, shapes, starts)
+    lib = _native.load_library()
+    B, S, M, D = value.shape
+    Lq, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
+    out = torch.empty((B, Lq, M * D), dtype=value.dtype, device=value.device)
+    timer = _timer
+    if timer is not None:
+        ev0 = timer._begin()
+    rc = lib.msda_hip_forward(
+        value.data_ptr(), _native.DTYPE_TAGS[value.dtype],
+        _native.host_i64_array(shapes), _native.host_i64_array(starts), L,
+        loc.data_ptr(), aw.data_ptr(), out.data_ptr(),
+        B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
+    _native.check(rc, "msda_hip_forward")
+    if timer is not None:
+        timer._end("fwd", (S, Lq), algorithmic_bytes("fwd", B, S, M, D, Lq, L, P, value.element_size()), ev0)
+    return out
+
+
+def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="border",
+                  need_value=True, need_loc=True, need_aw=True):
+    """(grad_value, grad_loc, grad_aw) of msda_forward; unneeded ones come back None."""
+    _check_inputs(value, loc, aw, shapes, starts)
+    grad_output = grad_output.to(value.dtype).contiguous()
+    B, S, M, D = value.shape
+    Lq, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
+    if tuple(grad_output.shape) != (B, Lq, M * D):
+        raise ValueError(f"grad_output must be {(B, Lq, M * D)}, got {tuple(grad_output.shape)}")
+    lib = _native.load_library()
+    gv = torch.empty_like(value) if need_value else None
+    gl = torch.empty_like(loc) if need_loc else None
+    ga = torch.empty_like(aw) if need_aw else None
+    ws = None
+    if need_value:
+        nbytes = lib.msda_hip_backward_workspace_bytes(_native.DTYPE_TAGS[value.dtype], B, S, M, D)
+        if nbytes:
+            ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=value.device)
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    timer = _timer
+    if timer is not None:
+        ev0 = timer._begin()
+    rc = lib.msda_hip_backward(
+        value.data_ptr(), _native.DTYPE_TAGS[value.dtype],
+        _native.host_i64_array(shapes), _native.host_i64_array(starts), L,
+        loc.data_ptr(), aw.data_ptr(), grad_output.data_ptr(),
+        ptr(gv), ptr(gl), ptr(ga), ptr(ws),
+        B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
+    _native.check(rc, "msda_hip_backward")
+    if timer is not None:
+        timer._end("bwd", (S, Lq), algorithmic_bytes("bwd", B, S, M, D, Lq, L, P, value.element_size()), ev0)
+    return gv, gl, ga
+
+
+class MSDAFunction(Function):
+    """autograd wrapper (shape of the reference's MSDeformAttnFunction,
+    models/modules/attention.py:310-328): saves the inputs, backward returns
+    grads for value / loc / aw, ``once_differentiable`` like the reference."""
+
+    @staticmethod
+    def forward(ctx, value, loc, aw, shapes, starts, padding_mode):
+        ctx.meta = (shapes, starts, padding_mode)
+        ctx.save_for_backward(value, loc, aw)
+        return msda_forward(value, shapes, starts, loc, aw, padding_mode)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_output):
+        value, loc, aw = ctx.saved_tensors
+        shapes, starts, padding_mode = ctx.meta
+        nv, nl, na = ctx.needs_input_grad[:3]
+        gv, gl, ga = msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode,
+                                   need_value=nv, need_loc=nl, need_aw=na)
+        return gv, gl, ga, None, None, None
+
+
+def msda_apply(value, shapes, starts, loc, aw, padding_mode="border"):
+    """Differentiable MSDA on normalised inputs: value (B,S,M,D); loc, aw (B,Lq,M,L,P).
+
+    Casts loc / aw to the coordinate dtype (fp32, or fp64 for fp64 values) and makes
+    everything contiguous outside the Function, so autograd tracks those copies."""
+    cd = _coord_dtype(value)
+    value = value.contiguous()
+    loc = loc.to(cd).contiguous()
+    aw = aw.to(cd).contiguous()
+    return MSDAFunction.apply(value, loc, aw, tuple(shapes), tuple(starts), padding_mode)

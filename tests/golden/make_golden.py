@@ -1,0 +1,263 @@
+"""Generate the golden vectors under tests/golden/ by running the REAL reference on CPU.
+
+Run in the build container (where /root/reference exists):
+    PYTHONDONTWRITEBYTECODE=1 python3 -B tests/golden/make_golden.py
+
+The reference is imported read-only from /root/reference (no bytecode written there),
+with stub modules for packages it imports but never uses on this path (torchvision,
+torchaudio, timm, wandb, ml_collections) and a namespace shim for ``models`` that skips
+``models/__init__.py`` (which imports timm).  Only tensors are written (torch.save of a
+dict of tensors, loadable with ``weights_only=True``); no reference source is copied.
+
+Fixtures:
+  op_border_{f64,f32}.pt     ms_deform_attn_core_pytorch (attention.py:331) fwd + grads,
+                             small shapes, locations in U(-0.2, 1.2) + exact border /
+                             integer-position points.
+  op_border_f32_enc.pt       same at the T=1024 encoder level shapes [1024,512,256,128]
+                             (B=1, M=8, D=64, 48 queries); inputs regenerated from a seed,
+                             grad_value stored as per-row channel sums + 256 full rows.
+  module_f64.pt              MSDeformAttn(d=64, L=4, M=4, P=4) (attention.py:394) fwd + grads,
+                             encoder shape (+ padding mask) and decoder shape, is_sparse outputs.
+  transformer_f64.pt         PositionEmbeddingVideoSine + BaseEncoder + DeformableTransformer
+                             (2 enc + 2 dec, d=64, dropout 0) at T=64, B=2 (one padded clip).
+  multimodal_f64.pt          MultimodalDeformableTransformer (1 enc + 1 dec, d=64), video
+                             T=32 / audio T=16 pyramids, B=2.
+"""
+import os
+import sys
+import types
+
+import torch
+
+REF = "/root/reference"
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.dont_write_bytecode = True
+
+
+def _stub(name, **attrs):
+    mod = types.ModuleType(name)
+    for k, v in attrs.items():
+        setattr(mod, k, v)
+    sys.modules[name] = mod
+    return mod
+
+
+def import_reference():
+    for name in ("torchvision", "torchaudio", "timm", "wandb", "ml_collections"):
+        _stub(name, __version__="0.0.0")
+    _stub("torchaudio.compliance")
+    _stub("torchaudio.compliance.kaldi")
+    models = types.ModuleType("models")
+    models.__path__ = [os.path.join(REF, "models")]
+    sys.modules["models"] = models
+    sys.path.insert(0, REF)
+    import models.modules.attention as attention  # noqa: E402
+    import models.base_encoder as base_encoder  # noqa: E402
+    import models.modules.embedding_layers as embedding_layers  # noqa: E402
+    import models.deformable.unimodal_deformable_transformer as uni  # noqa: E402
+    import models.deformable.multimodal_deformable_transformer as mm  # noqa: E402
+    return types.SimpleNamespace(attention=attention, base_encoder=base_encoder,
+                                 embedding_layers=embedding_layers, uni=uni, mm=mm)
+
+
+def _compact(state_dict):
+    """fp64 copies of fp32-initialised weights are exactly fp32: store them as fp32."""
+    out = {}
+    for k, v in state_dict.items():
+        if v.dtype == torch.float64 and torch.equal(v.float().double(), v):
+            v = v.float()
+        out[k] = v.clone()
+    return out
+
+
+def _locations(gen, shape, dtype):
+    return (torch.rand(shape, generator=gen, dtype=torch.float64) * 1.4 - 0.2).to(dtype)
+
+
+def _attn(gen, shape, dtype):
+    a = torch.rand(shape, generator=gen, dtype=torch.float64) + 1e-5
+    a = a / a.sum(-1, keepdim=True).sum(-2, keepdim=True)
+    return a.to(dtype)
+
+
+def _edge_points(loc, shapes):
+    """Exact border / integer-position locations for query 0 (binary fractions: exact in fp32)."""
+    for l, T in enumerate(shapes):
+        pts = [0.5 / T, (T - 0.5) / T, 5.5 / T if T > 6 else 1.5 / T, 0.0, 1.0, -0.5, 1.5]
+        flat = loc[:, 0, :, l].reshape(-1)
+        for i, v in enumerate(pts):
+            if i < flat.numel():
+                flat[i] = v
+        loc[:, 0, :, l] = flat.view(loc[:, 0, :, l].shape)
+    return loc
+
+
+def op_case(ref, dtype, shapes, B, M, D, Lq, P, seed, edge=True):
+    gen = torch.Generator().manual_seed(seed)
+    L, S = len(shapes), sum(shapes)
+    value = torch.randn((B, S, M, D), generator=gen, dtype=torch.float64).to(dtype)
+    loc = _locations(gen, (B, Lq, M, L, P), dtype)
+    if edge:
+        loc = _edge_points(loc, shapes)
+    aw = _attn(gen, (B, Lq, M, L, P), dtype)
+    gout = torch.randn((B, Lq, M * D), generator=gen, dtype=torch.float64).to(dtype)
+    v, lc, a = (t.clone().requires_grad_(True) for t in (value, loc, aw))
+    shp = torch.tensor(shapes, dtype=torch.long).unsqueeze(-1)
+    out = ref.attention.ms_deform_attn_core_pytorch(v, shp, lc.unsqueeze(-1), a)
+    out.backward(gout)
+    return dict(value=value, loc=loc, aw=aw, grad_out=gout, shapes=torch.tensor(shapes), out=out.detach(),
+                grad_value=v.grad, grad_loc=lc.grad, grad_aw=a.grad)
+
+
+def op_enc_case(ref, seed=7):
+    shapes, B, M, D, Lq, P = [1024, 512, 256, 128], 1, 8, 64, 48, 4
+    d = op_case(ref, torch.float32, shapes, B, M, D, Lq, P, seed, edge=True)
+    gv = d.pop("grad_value")
+    rows = torch.randperm(sum(shapes), generator=torch.Generator().manual_seed(seed + 1))[:256]
+    # keep only rows that matter + make the inputs regenerable from the seed
+    for k in ("value", "loc", "aw", "grad_out"):
+        d.pop(k)
+    d.update(seed=torch.tensor(seed), B=torch.tensor(B), M=torch.tensor(M), D=torch.tensor(D),
+             Lq=torch.tensor(Lq), P=torch.tensor(P), grad_value_rowsum=gv.sum(-1),
+             grad_value_rows=rows, grad_value_at_rows=gv[:, rows])
+    return d
+
+
+def module_case(ref, seed=11):
+    torch.manual_seed(seed)
+    d_model, L, M, P, B = 64, 4, 4, 4, 2
+    shapes = [32, 16, 8, 4]
+    S = sum(shapes)
+    attn = ref.attention.MSDeformAttn(d_model, L, M, P).double()
+    gen = torch.Generator().manual_seed(seed)
+    out = {"state_dict": _compact(attn.state_dict()), "shapes": torch.tensor(shapes)}
+    shp = torch.tensor(shapes, dtype=torch.long)
+    start = torch.cat((shp.new_zeros(1), shp.cumsum(0)[:-1]))
+    valid = torch.ones(B, 4)
+    valid[1] = torch.tensor([0.75, 0.75, 0.75, 0.75])
+    mask = torch.zeros(B, S, dtype=torch.bool)
+    for l, (T, s0) in enumerate(zip(shapes, start.tolist())):
+        mask[1, s0 + int(T * 0.75):s0 + T] = True
+    enc_ref = ref.uni.DeformableTransformerEncoder.get_reference_points(shp, valid.double(), "cpu")
+    cases = {
+        "enc": (S, enc_ref, None),
+        "enc_masked": (S, enc_ref, mask),
+        "dec": (20, torch.rand((B, 20, 1), generator=gen, dtype=torch.float64)[:, :, None] * valid.double()[:, None, :, None], None),
+    }
+    flat0 = torch.randn((B, S, d_model), generator=gen, dtype=torch.float64)
+    for name, (Lq, refp, m) in cases.items():
+        query = torch.randn((B, Lq, d_model), generator=gen, dtype=torch.float64).requires_grad_(True)
+        flat = flat0.clone().requires_grad_(True)
+        gout = torch.randn((B, Lq, d_model), generator=gen, dtype=torch.float64)
+        attn.zero_grad()
+        y, sl, sa = attn(query, refp, flat, shp, start, m, is_sparse=True)
+        y.backward(gout)
+        out[name] = dict(query=query.detach(), reference_points=refp, input_flatten=flat.detach(),
+                         padding_mask=(m if m is not None else torch.zeros(0, dtype=torch.bool)),
+                         grad_out=gout, output=y.detach(), sampling_locations=sl.detach(),
+                         attention_weights=sa.detach(), grad_query=query.grad, grad_input_flatten=flat.grad,
+                         param_grads={k: p.grad.clone() for k, p in attn.named_parameters()})
+    return out
+
+
+def transformer_case(ref, seed=23):
+    torch.manual_seed(seed)
+    d_model, heads, Q = 64, 4, 20
+    pos_embed = ref.embedding_layers.PositionEmbeddingVideoSine(d_model // 2, normalize=True).double()
+    base = ref.base_encoder.BaseEncoder(4, d_model, d_model).double()
+    tr = ref.uni.DeformableTransformer(d_model=d_model, num_head=heads, num_encoder_layers=2, num_decoder_layers=2,
+                                       dim_feedforward=128, dropout=0.0, return_intermediate_dec=True,
+                                       num_feature_levels=4, dec_n_points=4, enc_n_points=4).double()
+    query_embedding = torch.nn.Embedding(Q, d_model * 2).double()
+    # the reference's duration embedding allocates with the default dtype
+    # (embedding_layers.py:222): run the forward with float64 as the default dtype
+    torch.set_default_dtype(torch.float64)
+    try:
+        return _transformer_run(ref, seed, pos_embed, base, tr, query_embedding)
+    finally:
+        torch.set_default_dtype(torch.float32)
+
+
+def _transformer_run(ref, seed, pos_embed, base, tr, query_embedding):
+    d_model, B, T, Q = 64, 2, 64, 20
+    gen = torch.Generator().manual_seed(seed)
+    video = torch.randn((B, T, d_model), generator=gen, dtype=torch.float64).requires_grad_(True)
+    mask = torch.zeros(B, T, dtype=torch.bool)
+    mask[1, 48:] = True
+    durations = torch.tensor([37.5, 120.2], dtype=torch.float64)
+    srcs, masks, pos = base(video, mask, durations, pos_embed)
+    src_flatten, shapes, starts, valid, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(srcs, masks, pos)
+    memory = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten)
+    qmask = torch.ones(B, Q, dtype=torch.bool)
+    init_ref, tgt, refp, qe = tr.prepare_decoder_input_query(B, query_embedding.weight)
+    hs, inter = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qe, mask_flatten, qmask, False)
+    w_hs = torch.randn(hs.shape, generator=gen, dtype=torch.float64)
+    w_mem = torch.randn(memory.shape, generator=gen, dtype=torch.float64)
+    loss = (hs * w_hs).sum() + (memory * w_mem).sum()
+    loss.backward()
+    named = {"pos_embed": pos_embed, "base_encoder": base, "transformer": tr, "query_embedding": query_embedding}
+    return dict(
+        video=video.detach(), mask=mask, durations=durations, w_hs=w_hs, w_mem=w_mem,
+        memory=memory.detach(), hs=hs.detach(), inter_references=inter.detach(), loss=loss.detach(),
+        grad_video=video.grad,
+        state_dicts={n: _compact(m.state_dict()) for n, m in named.items()},
+        param_grads={n: {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+                     for n, m in named.items()})
+
+
+def multimodal_case(ref, seed=31):
+    torch.manual_seed(seed)
+    d_model, heads, B, Q = 64, 4, 2, 12
+    tr = ref.mm.MultimodalDeformableTransformer(d_model=d_model, num_head=heads, num_encoder_layers=1,
+                                                num_decoder_layers=1, dim_feedforward=128, dropout=0.0,
+                                                return_intermediate_dec=True, num_feature_levels=4,
+                                                dec_n_points=4, enc_n_points=4).double()
+    query_embedding = torch.nn.Embedding(Q, d_model * 2).double()
+    gen = torch.Generator().manual_seed(seed)
+    inputs = {}
+    prepared = {}
+    for name, lens in (("video", [32, 16, 8, 4]), ("audio", [16, 8, 4, 2])):
+        srcs = [torch.randn((B, d_model, t), generator=gen, dtype=torch.float64).requires_grad_(True) for t in lens]
+        pos = [torch.randn((B, d_model, t), generator=gen, dtype=torch.float64) for t in lens]
+        masks = [torch.zeros(B, t, dtype=torch.bool) for t in lens]
+        masks = [m.clone() for m in masks]
+        for m, t in zip(masks, lens):
+            m[1, (3 * t) // 4:] = True
+        inputs[name] = dict(srcs=srcs, pos=pos, masks=masks)
+        prepared[name] = tr.prepare_encoder_inputs(srcs, masks, pos)
+    v, a = prepared["video"], prepared["audio"]
+    mem_v, mem_a = tr.forward_encoder(*v, *a)
+    qmask = torch.ones(B, Q, dtype=torch.bool)
+    init_ref, tgt, refp, qe = tr.prepare_decoder_input_query(B, query_embedding.weight)
+    hs, inter = tr.forward_decoder(tgt, refp, qe, qmask, mem_v, v[1], v[2], v[3], v[5], mem_a, a[1], a[2], a[3], a[5],
+                                   False)
+    w = [torch.randn(t.shape, generator=gen, dtype=torch.float64) for t in (hs, mem_v, mem_a)]
+    loss = (hs * w[0]).sum() + (mem_v * w[1]).sum() + (mem_a * w[2]).sum()
+    loss.backward()
+    return dict(
+        inputs={n: dict(srcs=[s.detach() for s in d["srcs"]], pos=d["pos"], masks=d["masks"]) for n, d in inputs.items()},
+        grad_srcs={n: [s.grad for s in d["srcs"]] for n, d in inputs.items()},
+        weights=w, hs=hs.detach(), inter_references=inter.detach(), memory_video=mem_v.detach(),
+        memory_audio=mem_a.detach(), loss=loss.detach(),
+        state_dicts={"transformer": _compact(tr.state_dict()), "query_embedding": _compact(query_embedding.state_dict())},
+        param_grads={"transformer": {k: p.grad.clone() for k, p in tr.named_parameters() if p.grad is not None},
+                     "query_embedding": {k: p.grad.clone() for k, p in query_embedding.named_parameters()}})
+
+
+def main():
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    ref = import_reference()
+    small = dict(shapes=[32, 16, 8, 4], B=2, M=4, D=8, Lq=20, P=4)
+    torch.save(op_case(ref, torch.float64, seed=1, **small), os.path.join(HERE, "op_border_f64.pt"))
+    torch.save(op_case(ref, torch.float32, seed=2, **small), os.path.join(HERE, "op_border_f32.pt"))
+    torch.save(op_enc_case(ref), os.path.join(HERE, "op_border_f32_enc.pt"))
+    torch.save(module_case(ref), os.path.join(HERE, "module_f64.pt"))
+    torch.save(transformer_case(ref), os.path.join(HERE, "transformer_f64.pt"))
+    torch.save(multimodal_case(ref), os.path.join(HERE, "multimodal_f64.pt"))
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".pt"):
+            print(f, os.path.getsize(os.path.join(HERE, f)))
+
+
+if __name__ == "__main__":
+    main()

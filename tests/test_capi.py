@@ -1,0 +1,60 @@
+"""The C-ABI library: loads without a GPU, exports every symbol include/msda_hip.h
+declares, and rejects bad arguments with a status + message before touching a device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+from conftest import PKG, ROOT
+
+HEADER = os.path.join(ROOT, "include", "msda_hip.h")
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(msda_hip_\w+)\s*\(", text, re.M)))
+
+
+def test_header_symbols_match_binding():
+    assert declared_symbols() == sorted(PKG._native.EXPORTED_SYMBOLS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = ctypes.CDLL(PKG._native.LIB_PATH)
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_abi_version_and_workspace():
+    lib = PKG._native.load_library()
+    assert lib.msda_hip_abi_version() == PKG._native.ABI_VERSION
+    assert lib.msda_hip_backward_workspace_bytes(0, 8, 1920, 8, 64) == 0          # f32 accumulates in place
+    assert lib.msda_hip_backward_workspace_bytes(1, 8, 1920, 8, 64) == 0          # f64 too
+    assert lib.msda_hip_backward_workspace_bytes(2, 8, 1920, 8, 64) == 8 * 1920 * 8 * 64 * 4  # bf16 -> fp32 scratch
+
+
+@pytest.mark.parametrize("bad", ["levels0", "levels17", "level_overflow", "bad_pad", "bad_dtype", "null_out"])
+def test_argument_errors_return_status(bad):
+    nat = PKG._native
+    lib = nat.load_library()
+    shapes, starts, L = [4, 2], [0, 4], 2
+    kw = dict(dtype=0, pad=0, S=6, out=ctypes.c_void_p(16), L=L)
+    if bad == "levels0":
+        kw["L"] = 0
+    elif bad == "levels17":
+        shapes, starts, kw["L"] = [1] * 17, list(range(17)), 17
+        kw["S"] = 17
+    elif bad == "level_overflow":
+        starts = [0, 5]
+    elif bad == "bad_pad":
+        kw["pad"] = 7
+    elif bad == "bad_dtype":
+        kw["dtype"] = 9
+    elif bad == "null_out":
+        kw["out"] = None
+    fake = ctypes.c_void_p(16)  # never dereferenced: validation fails first
+    rc = lib.msda_hip_forward(fake, kw["dtype"], nat.host_i64_array(shapes), nat.host_i64_array(starts), kw["L"],
+                              fake, fake, kw["out"], 1, kw["S"], 1, 4, 3, 2, kw["pad"], None)
+    assert rc == 1
+    assert "msda" in nat.last_error()

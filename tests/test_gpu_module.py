@@ -1,0 +1,124 @@
+"""Module / transformer-level parity on the GPU (``-m gpu``): the mirrored modules running
+the HIP kernel reproduce the reference's golden outputs and gradients — fp64 to ~1e-9,
+fp32 within the north_star tolerance (1e-3 relative) — and the bf16-autocast training
+step agrees with fp32."""
+import pytest
+import torch
+
+from conftest import PKG
+from test_host_modules import (_load, build_multimodal, build_transformer_stack, run_multimodal,
+                               run_transformer_stack)
+
+pytestmark = pytest.mark.gpu
+M = PKG.models
+
+
+def _close(a, b, rtol, atol):
+    torch.testing.assert_close(a.detach().cpu().to(b.dtype), b, rtol=rtol, atol=atol)
+
+
+def _rel_close(a, b, rel):
+    """max |a-b| <= rel * max |b| (north_star '1e-3 rel fp32' read on the tensor scale)."""
+    a = a.detach().cpu().double()
+    b = b.double()
+    err = (a - b).abs().max().item()
+    assert err <= rel * b.abs().max().item() + 1e-12, (err, b.abs().max().item())
+
+
+@pytest.mark.parametrize("case", ["enc", "enc_masked", "dec"])
+def test_msdeformattn_fp64_matches_reference(golden, dev, case):
+    g = golden("module_f64")
+    d = g[case]
+    sd = g["state_dict"]
+    attn = _load(M.modules.attention.MSDeformAttn(sd["value_proj.weight"].shape[0], 4, 4, 4).double(), sd).to(dev)
+    shapes = g["shapes"].to(dev)
+    start = torch.cat((shapes.new_zeros(1), shapes.cumsum(0)[:-1]))
+    q = d["query"].to(dev).requires_grad_(True)
+    x = d["input_flatten"].to(dev).requires_grad_(True)
+    mask = d["padding_mask"].to(dev) if d["padding_mask"].numel() else None
+    y, sl, sa = attn(q, d["reference_points"].to(dev), x, shapes, start, mask, is_sparse=True)
+    y.backward(d["grad_out"].to(dev))
+    _close(y, d["output"], 1e-10, 1e-11)
+    _close(sl, d["sampling_locations"], 1e-12, 1e-12)
+    _close(q.grad, d["grad_query"], 1e-9, 1e-10)
+    _close(x.grad, d["grad_input_flatten"], 1e-9, 1e-10)
+    for k, p in attn.named_parameters():
+        _close(p.grad, d["param_grads"][k], 1e-9, 1e-10)
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+def test_transformer_stack_matches_reference(golden, dev, dtype):
+    g = golden("transformer_f64")
+    mods = build_transformer_stack(g, device=dev)
+    if dtype == torch.float32:
+        for m in mods.values():
+            m.float()
+    video = g["video"].to(dev, dtype).requires_grad_(True)
+    torch.set_default_dtype(dtype)
+    try:
+        memory, hs, inter = run_transformer_stack(mods, video, g["mask"].to(dev), g["durations"].to(dev, dtype))
+        loss = (hs * g["w_hs"].to(dev, dtype)).sum() + (memory * g["w_mem"].to(dev, dtype)).sum()
+        loss.backward()
+    finally:
+        torch.set_default_dtype(torch.float32)
+    if dtype == torch.float64:
+        _close(memory, g["memory"], 1e-9, 1e-10)
+        _close(hs, g["hs"], 1e-9, 1e-10)
+        _close(video.grad, g["grad_video"], 1e-8, 1e-9)
+        for n, m in mods.items():
+            for k, p in m.named_parameters():
+                if k in g["param_grads"][n]:
+                    _close(p.grad, g["param_grads"][n][k], 1e-7, 1e-9)
+    else:  # fp32 end to end vs the fp64 reference: north_star's 1e-3 relative
+        _rel_close(memory, g["memory"], 1e-3)
+        _rel_close(hs, g["hs"], 1e-3)
+        _rel_close(video.grad, g["grad_video"], 1e-3)
+        for n, m in mods.items():
+            for k, p in m.named_parameters():
+                if k in g["param_grads"][n]:
+                    _rel_close(p.grad, g["param_grads"][n][k], 2e-3)
+
+
+def test_multimodal_fp64_matches_reference(golden, dev):
+    g = golden("multimodal_f64")
+    tr, qe = build_multimodal(g, device=dev)
+    inputs = {n: dict(srcs=[s.to(dev).requires_grad_(True) for s in d["srcs"]], pos=[p.to(dev) for p in d["pos"]],
+                      masks=[m.to(dev) for m in d["masks"]]) for n, d in g["inputs"].items()}
+    mem_v, mem_a, hs, inter = run_multimodal(tr, qe, inputs)
+    w = [t.to(dev) for t in g["weights"]]
+    ((hs * w[0]).sum() + (mem_v * w[1]).sum() + (mem_a * w[2]).sum()).backward()
+    _close(hs, g["hs"], 1e-9, 1e-10)
+    _close(mem_v, g["memory_video"], 1e-9, 1e-10)
+    _close(mem_a, g["memory_audio"], 1e-9, 1e-10)
+    for n in ("video", "audio"):
+        for s, ref in zip(inputs[n]["srcs"], g["grad_srcs"][n]):
+            _close(s.grad, ref, 1e-8, 1e-9)
+    for k, p in tr.named_parameters():
+        if k in g["param_grads"]["transformer"]:
+            _close(p.grad, g["param_grads"]["transformer"][k], 1e-7, 1e-9)
+
+
+def test_bf16_autocast_step_tracks_fp32(dev):
+    """The bench's bf16 step (value bf16, loc/aw fp32) stays close to the fp32 step."""
+    torch.manual_seed(0)
+    model = PKG.dvc_core.DeformableDVCCore(d_model=256, num_queries=20, feature_dim=256, enc_layers=2, dec_layers=2,
+                                           ff_dim=512, dropout=0.0).to(dev)
+    video, mask, dur = PKG.dvc_core.synthetic_clips(2, T=128, feature_dim=256, padded=True, device=dev)
+    out32 = model(video, mask, dur)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out16 = model(video, mask, dur)
+    for k in ("hs", "memory"):
+        a, b = out16[k].float(), out32[k].float()
+        assert ((a - b).norm() / b.norm()).item() < 3e-2, k
+    loss = PKG.dvc_core.workload_loss(out16)
+    loss.backward()
+    assert all(p.grad is None or torch.isfinite(p.grad).all() for p in model.parameters())
+
+
+def test_module_runs_no_host_sync_for_levels(dev):
+    """Level metadata from prepare_encoder_inputs carries its host copy: the MSDA call does
+    not read the device tensor (the reference syncs at attention.py:346,458)."""
+    tr = M.deformable.unimodal_deformable_transformer
+    shapes, starts = tr.level_metadata([64, 32, 16, 8], dev)
+    assert shapes._mfl_host == (64, 32, 16, 8) and starts._mfl_host == (0, 64, 96, 112)
+    assert PKG.msda.host_levels(shapes, starts) == ((64, 32, 16, 8), (0, 64, 96, 112))

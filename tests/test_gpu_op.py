@@ -1,0 +1,198 @@
+"""HIP kernel parity (``-m gpu``): libmsda_hip.so through the C-ABI vs the reference's golden
+vectors and vs the oracle restatement, over dtypes, channel counts, level layouts, both
+padding modes and the edge cases (clamp borders, near-integer positions, empty inputs).
+
+Tolerances: fp64 1e-12 (only the grad_value atomic-add order differs); fp32 outputs /
+grads within 1e-5 / 1e-4 relative of the fp32 reference (north_star asks 1e-3);
+bf16 / fp16 values against the oracle on the same rounded inputs in fp32.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import PKG
+from oracle import msda_oracle as O
+from test_oracle import near_integer_locations, regenerate_enc_inputs
+
+pytestmark = pytest.mark.gpu
+msda = PKG.msda
+
+
+def _np(t):
+    return t.detach().float().cpu().numpy() if t.dtype in (torch.bfloat16, torch.float16) else t.detach().cpu().numpy()
+
+
+def run_hip(value, shapes, loc, aw, gout, padding="border", dev="cuda"):
+    starts = O.level_starts(shapes)
+    v, lc, a, g = (t.to(dev) for t in (value, loc, aw, gout))
+    out = msda.msda_forward(v, shapes, starts, lc, a, padding)
+    gv, gl, ga = msda.msda_backward(v, shapes, starts, lc, a, g, padding)
+    torch.cuda.synchronize()
+    return out.cpu(), gv.cpu(), gl.cpu(), ga.cpu()
+
+
+def rand_case(shapes, B, M, D, Lq, P, dtype, seed, lo=-0.2, hi=1.2):
+    gen = torch.Generator().manual_seed(seed)
+    S = sum(shapes)
+    value = torch.randn((B, S, M, D), generator=gen).to(dtype)
+    cd = torch.float64 if dtype == torch.float64 else torch.float32
+    loc = (torch.rand((B, Lq, M, len(shapes), P), generator=gen, dtype=torch.float64) * (hi - lo) + lo).to(cd)
+    aw = torch.rand((B, Lq, M, len(shapes), P), generator=gen, dtype=torch.float64).to(cd)
+    gout = torch.randn((B, Lq, M * D), generator=gen).to(dtype)
+    return value, loc, aw, gout
+
+
+@pytest.mark.parametrize("name,rtol,atol", [("op_border_f64", 1e-12, 1e-12), ("op_border_f32", 1e-5, 1e-6)])
+def test_kernel_matches_reference_golden(golden, dev, name, rtol, atol):
+    g = golden(name)
+    shapes = g["shapes"].tolist()
+    out, gv, gl, ga = run_hip(g["value"], shapes, g["loc"], g["aw"], g["grad_out"])
+    torch.testing.assert_close(out, g["out"], rtol=rtol, atol=atol)
+    torch.testing.assert_close(gv, g["grad_value"], rtol=rtol * 10, atol=atol * 10)
+    torch.testing.assert_close(ga, g["grad_aw"], rtol=rtol * 10, atol=atol * 10)
+    torch.testing.assert_close(gl, g["grad_loc"], rtol=rtol * 10, atol=atol * 64)
+
+
+def test_kernel_matches_reference_golden_enc_shape(golden, dev):
+    g = golden("op_border_f32_enc")
+    shapes, value, loc, aw, gout = regenerate_enc_inputs(g)
+    out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout)
+    torch.testing.assert_close(out, g["out"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(ga, g["grad_aw"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(gl, g["grad_loc"], rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gv.sum(-1), g["grad_value_rowsum"], rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(gv[:, g["grad_value_rows"]], g["grad_value_at_rows"], rtol=1e-4, atol=1e-5)
+
+
+CASES = [
+    # shapes,               B, M, D,    Lq, P
+    ([32, 16, 8, 4],        2, 4, 8,    20, 4),
+    ([1024, 512, 256, 128], 1, 8, 64,   64, 4),
+    ([50, 25, 13, 7],       3, 8, 64,   95, 4),    # audio pyramid of config 3
+    ([300, 150, 75, 38],    2, 8, 32,   40, 2),    # video_rescale_len = 300
+    ([17],                  2, 2, 30,   9, 3),
+    ([1, 1, 1],             1, 1, 16,   5, 1),     # T = 1 levels
+    ([64, 32],              1, 2, 71,   7, 4),     # odd channel count (scalar path)
+    ([40, 20, 10],          1, 1, 1025, 3, 2),     # D > 64 lanes: chunked lanes
+    ([40, 20, 10],          1, 2, 256,  6, 2),
+]
+
+
+@pytest.mark.parametrize("dtype", [torch.float64, torch.float32])
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("case", range(len(CASES)))
+def test_kernel_matches_oracle(dev, case, padding, dtype):
+    shapes, B, M, D, Lq, P = CASES[case]
+    value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, dtype, seed=100 + case)
+    out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout, padding)
+    r_out = O.msda_forward(_np(value), shapes, _np(loc), _np(aw), padding=padding)
+    r_gv, r_gl, r_ga = O.msda_backward(_np(value), shapes, _np(loc), _np(aw), _np(gout), padding=padding)
+    tol = dict(rtol=1e-11, atol=1e-11) if dtype == torch.float64 else dict(rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(_np(out), r_out, **tol)
+    np.testing.assert_allclose(_np(ga), r_ga, **tol)
+    np.testing.assert_allclose(_np(gv), r_gv, rtol=tol["rtol"] * 10, atol=tol["atol"] * 10)
+    scale = max(shapes)
+    np.testing.assert_allclose(_np(gl), r_gl, rtol=tol["rtol"] * 10, atol=tol["atol"] * scale)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("D", [64, 30])
+def test_half_values_match_oracle_on_rounded_inputs(dev, dtype, D):
+    shapes, B, M, Lq, P = [256, 128, 64, 32], 2, 8, 96, 4
+    value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, dtype, seed=7)
+    out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout)
+    assert out.dtype == dtype and gv.dtype == dtype and gl.dtype == torch.float32
+    v32, g32 = value.float(), gout.float()
+    r_out = O.msda_forward(_np(v32), shapes, _np(loc), _np(aw))
+    r_gv, r_gl, r_ga = O.msda_backward(_np(v32), shapes, _np(loc), _np(aw), _np(g32))
+    eps = 2 ** -8 if dtype == torch.bfloat16 else 2 ** -11        # output rounding of the storage type
+    np.testing.assert_allclose(_np(out), r_out, rtol=eps, atol=eps * np.abs(r_out).max())
+    np.testing.assert_allclose(_np(ga), r_ga, rtol=1e-4, atol=1e-4)   # fp32 math on exact inputs
+    np.testing.assert_allclose(_np(gl), r_gl, rtol=1e-4, atol=1e-2)
+    np.testing.assert_allclose(_np(gv), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
+
+
+@pytest.mark.parametrize("T", [1024, 1000, 300, 75, 50])
+def test_tap_segment_bit_identical_near_integers(dev, T):
+    """Same construction as the oracle's pin: the fp32 kernel picks ATen's segment."""
+    loc = torch.from_numpy(near_integer_locations(T)).view(1, -1, 1, 1, 1)
+    value = (torch.arange(T, dtype=torch.float32) ** 2).view(1, T, 1, 1)
+    aw = torch.ones_like(loc)
+    gout = torch.ones(1, loc.shape[1], 1)
+    _, _, gl, _ = run_hip(value, [T], loc, aw, gout)
+    _, r_gl, _ = O.msda_backward(value.numpy(), [T], loc.numpy(), aw.numpy(), gout.numpy())
+    np.testing.assert_allclose(gl.numpy(), r_gl, rtol=1e-6)
+
+
+def test_border_gradient_exactly_zero_at_clamp(golden, dev):
+    g = golden("op_border_f32")
+    shapes = g["shapes"].tolist()
+    _, _, gl, _ = run_hip(g["value"], shapes, g["loc"], g["aw"], g["grad_out"])
+    ref = g["grad_loc"]
+    assert torch.equal(gl == 0, ref == 0)
+
+
+@pytest.mark.parametrize("B,Lq", [(0, 5), (2, 0)])
+def test_empty_inputs(dev, B, Lq):
+    shapes = [8, 4]
+    value, loc, aw, gout = rand_case(shapes, max(B, 1), 2, 16, max(Lq, 1), 2, torch.float32, seed=1)
+    value, loc, aw, gout = value[:B], loc[:B, :Lq], aw[:B, :Lq], gout[:B, :Lq]
+    out, gv, gl, ga = run_hip(value.contiguous(), shapes, loc.contiguous(), aw.contiguous(), gout.contiguous())
+    assert out.shape == (B, Lq, 32) and gv.shape == value.shape
+    assert gv.abs().sum() == 0
+
+
+def test_needs_input_grad_subsets(dev):
+    shapes = [32, 16]
+    value, loc, aw, gout = rand_case(shapes, 2, 4, 16, 10, 2, torch.float64, seed=5)
+    v, lc, a = value.cuda().requires_grad_(True), loc.cuda(), aw.cuda().requires_grad_(True)
+    out = msda.msda_apply(v, shapes, O.level_starts(shapes), lc, a)
+    out.backward(gout.cuda())
+    _, r_gl, r_ga = O.msda_backward(_np(value), shapes, _np(loc), _np(aw), _np(gout))
+    assert lc.grad is None
+    np.testing.assert_allclose(a.grad.cpu().numpy(), r_ga, rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.parametrize("channels", [30, 32, 64, 71, 1025, 2048, 3096])
+def test_gradcheck_fp64(dev, channels):
+    """torch.autograd.gradcheck in fp64 over the channel counts of the reference's own
+    test (models/ops/test.py:85-86), locations kept off the interpolation kinks."""
+    N, M, Lq, L, P = 1, 2, 2, 2, 2
+    shapes = [6, 3]
+    gen = torch.Generator().manual_seed(3)
+    value = (torch.rand(N, sum(shapes), M, channels, generator=gen, dtype=torch.float64) * 0.01)
+    loc = torch.rand(N, Lq, M, L, P, generator=gen, dtype=torch.float64) * 0.8 + 0.1
+    for l, T in enumerate(shapes):
+        y = loc[:, :, :, l] * T - 0.5
+        frac = y - y.floor()
+        loc[:, :, :, l] += torch.where((frac < 1e-3) | (frac > 1 - 1e-3), 5e-3 / T, 0.0)
+    aw = torch.rand(N, Lq, M, L, P, generator=gen, dtype=torch.float64) + 1e-5
+    aw = aw / aw.sum(-1, keepdim=True).sum(-2, keepdim=True)
+    starts = O.level_starts(shapes)
+    for padding in ("border", "zeros"):
+        f = lambda v, lc, a: msda.MSDAFunction.apply(v, lc, a, tuple(shapes), tuple(starts), padding)  # noqa: E731
+        inputs = tuple(t.cuda().requires_grad_(True) for t in (value, loc, aw))
+        assert torch.autograd.gradcheck(f, inputs, eps=1e-6, atol=1e-5, rtol=1e-4)
+
+
+def test_full_size_properties(dev):
+    """At the bench's size (B=8, T=1024 encoder call) where the oracle is too slow to run
+    whole: linearity in value and the grad_value checksum
+    sum_s grad_value[b,s,m,:] = sum_q (sum_{l,p} aw[b,q,m,l,p]) grad_out[b,q,m,:] (border
+    weights of a sample sum to 1); plus oracle parity on one clip."""
+    shapes, B, M, D, P = [1024, 512, 256, 128], 8, 8, 64, 4
+    Lq = sum(shapes)
+    v1, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.float32, seed=11, lo=0.0, hi=1.0)
+    v2 = torch.randn_like(v1)
+    starts = O.level_starts(shapes)
+    c = lambda t: t.cuda()  # noqa: E731
+    o1 = msda.msda_forward(c(v1), shapes, starts, c(loc), c(aw))
+    o2 = msda.msda_forward(c(v2), shapes, starts, c(loc), c(aw))
+    o12 = msda.msda_forward(c(2 * v1 - 3 * v2), shapes, starts, c(loc), c(aw))
+    torch.testing.assert_close(o12, 2 * o1 - 3 * o2, rtol=1e-4, atol=1e-4)
+    gv, _, _ = msda.msda_backward(c(v1), shapes, starts, c(loc), c(aw), c(gout))
+    lhs = gv.double().sum(1)                                               # (B, M, D)
+    rhs = (aw.double().sum((-1, -2))[..., None] * gout.double().view(B, Lq, M, D)).sum(1)
+    torch.testing.assert_close(lhs.cpu(), rhs, rtol=1e-4, atol=1e-3)
+    r_out = O.msda_forward(_np(v1[:1]), shapes, _np(loc[:1]), _np(aw[:1]))
+    np.testing.assert_allclose(o1[:1].cpu().numpy(), r_out, rtol=2e-5, atol=2e-5)

@@ -1,0 +1,158 @@
+"""Host logic of the mirrored modules, on CPU, with the MSDA core swapped for the oracle
+(oracle.cpu_model.oracle_core): MSDeformAttn, PositionEmbeddingVideoSine + BaseEncoder +
+DeformableTransformer and MultimodalDeformableTransformer must reproduce the reference's
+golden outputs and gradients (fp64), and the product path must refuse host tensors."""
+import pytest
+import torch
+
+from conftest import PKG
+from oracle.cpu_model import oracle_core
+
+M = PKG.models
+
+
+def _load(module, sd):
+    module.load_state_dict({k: v.double() if v.is_floating_point() else v for k, v in sd.items()})
+    return module
+
+
+def _close(a, b, rtol=1e-9, atol=1e-10):
+    torch.testing.assert_close(a, b.to(a.dtype), rtol=rtol, atol=atol)
+
+
+def test_product_core_refuses_cpu_tensors():
+    v = torch.zeros(1, 6, 1, 4)
+    loc = torch.zeros(1, 2, 1, 2, 1)
+    aw = torch.ones(1, 2, 1, 2, 1)
+    with pytest.raises(RuntimeError, match="ROCm device"):
+        M.modules.attention.ms_deform_attn_core_pytorch(v, torch.tensor([4, 2]), loc, aw)
+    with pytest.raises(RuntimeError, match="Not implemented on the CPU"):
+        PKG.MultiScaleDeformableAttention.ms_deform_attn_forward(v, torch.tensor([[1, 4], [1, 2]]),
+                                                                torch.tensor([0, 4]),
+                                                                torch.stack([loc, loc * 0 + 0.5], -1), aw, 64)
+
+
+def test_host_levels_forms():
+    hl = PKG.msda.host_levels
+    assert hl(torch.tensor([8, 4, 2])) == ((8, 4, 2), (0, 8, 12))
+    assert hl(torch.tensor([[8], [4]])) == ((8, 4), (0, 8))
+    assert hl(torch.tensor([[1, 8], [1, 4]]), torch.tensor([0, 8])) == ((8, 4), (0, 8))
+    with pytest.raises(NotImplementedError):
+        hl(torch.tensor([[2, 8]]))
+    t = torch.tensor([5, 3])
+    t._mfl_host = (5, 3)
+    assert hl(t) == ((5, 3), (0, 5))
+
+
+@pytest.mark.parametrize("case", ["enc", "enc_masked", "dec"])
+def test_msdeformattn_matches_reference(golden, case):
+    g = golden("module_f64")
+    d = g[case]
+    sd = g["state_dict"]
+    d_model = sd["value_proj.weight"].shape[0]
+    attn = _load(M.modules.attention.MSDeformAttn(d_model, 4, 4, 4).double(), sd)
+    shapes = g["shapes"]
+    start = torch.cat((shapes.new_zeros(1), shapes.cumsum(0)[:-1]))
+    q = d["query"].clone().requires_grad_(True)
+    x = d["input_flatten"].clone().requires_grad_(True)
+    mask = d["padding_mask"] if d["padding_mask"].numel() else None
+    with oracle_core(PKG):
+        y, sl, sa = attn(q, d["reference_points"], x, shapes, start, mask, is_sparse=True)
+        y.backward(d["grad_out"])
+    _close(y, d["output"])
+    _close(sl, d["sampling_locations"])
+    _close(sa, d["attention_weights"])
+    _close(q.grad, d["grad_query"], rtol=1e-8, atol=1e-9)
+    _close(x.grad, d["grad_input_flatten"], rtol=1e-8, atol=1e-9)
+    for k, p in attn.named_parameters():
+        _close(p.grad, d["param_grads"][k], rtol=1e-8, atol=1e-9)
+
+
+def build_transformer_stack(g, device="cpu"):
+    d_model, heads, Q = 64, 4, 20
+    pos = M.modules.embedding_layers.PositionEmbeddingVideoSine(d_model // 2, normalize=True)
+    base = M.base_encoder.BaseEncoder(4, d_model, d_model)
+    tr = M.deformable.unimodal_deformable_transformer.DeformableTransformer(
+        d_model=d_model, num_head=heads, num_encoder_layers=2, num_decoder_layers=2, dim_feedforward=128,
+        dropout=0.0, return_intermediate_dec=True, num_feature_levels=4, dec_n_points=4, enc_n_points=4)
+    qe = torch.nn.Embedding(Q, 2 * d_model)
+    mods = {"pos_embed": pos, "base_encoder": base, "transformer": tr, "query_embedding": qe}
+    for n, m in mods.items():
+        _load(m.double().to(device), g["state_dicts"][n])
+    return mods
+
+
+def run_transformer_stack(mods, video, mask, durations):
+    pos, base, tr, qe = (mods[k] for k in ("pos_embed", "base_encoder", "transformer", "query_embedding"))
+    B = video.shape[0]
+    srcs, masks, poses = base(video, mask, durations, pos)
+    src_flatten, shapes, starts, valid, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(srcs, masks, poses)
+    memory = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten)
+    qmask = torch.ones(B, qe.weight.shape[0], dtype=torch.bool, device=video.device)
+    _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qe.weight)
+    hs, inter = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten, qmask, False)
+    return memory, hs, inter
+
+
+def test_transformer_stack_matches_reference(golden):
+    g = golden("transformer_f64")
+    mods = build_transformer_stack(g)
+    video = g["video"].clone().requires_grad_(True)
+    torch.set_default_dtype(torch.float64)
+    try:
+        with oracle_core(PKG):
+            memory, hs, inter = run_transformer_stack(mods, video, g["mask"], g["durations"])
+            loss = (hs * g["w_hs"]).sum() + (memory * g["w_mem"]).sum()
+            loss.backward()
+    finally:
+        torch.set_default_dtype(torch.float32)
+    _close(memory, g["memory"])
+    _close(hs, g["hs"])
+    _close(inter, g["inter_references"])
+    _close(video.grad, g["grad_video"], rtol=1e-8, atol=1e-9)
+    for n, m in mods.items():
+        for k, p in m.named_parameters():
+            if k in g["param_grads"][n]:
+                _close(p.grad, g["param_grads"][n][k], rtol=1e-7, atol=1e-9)
+
+
+def build_multimodal(g, device="cpu"):
+    tr = M.deformable.multimodal_deformable_transformer.MultimodalDeformableTransformer(
+        d_model=64, num_head=4, num_encoder_layers=1, num_decoder_layers=1, dim_feedforward=128, dropout=0.0,
+        return_intermediate_dec=True, num_feature_levels=4, dec_n_points=4, enc_n_points=4)
+    qe = torch.nn.Embedding(g["state_dicts"]["query_embedding"]["weight"].shape[0], 128)
+    _load(tr.double().to(device), g["state_dicts"]["transformer"])
+    _load(qe.double().to(device), g["state_dicts"]["query_embedding"])
+    return tr, qe
+
+
+def run_multimodal(tr, qe, inputs):
+    prepared = {n: tr.prepare_encoder_inputs(d["srcs"], d["masks"], d["pos"]) for n, d in inputs.items()}
+    v, a = prepared["video"], prepared["audio"]
+    mem_v, mem_a = tr.forward_encoder(*v, *a)
+    B = mem_v.shape[0]
+    qmask = torch.ones(B, qe.weight.shape[0], dtype=torch.bool, device=mem_v.device)
+    _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qe.weight)
+    hs, inter = tr.forward_decoder(tgt, refp, qpos, qmask, mem_v, v[1], v[2], v[3], v[5], mem_a, a[1], a[2], a[3],
+                                   a[5], False)
+    return mem_v, mem_a, hs, inter
+
+
+def test_multimodal_matches_reference(golden):
+    g = golden("multimodal_f64")
+    tr, qe = build_multimodal(g)
+    inputs = {n: dict(srcs=[s.clone().requires_grad_(True) for s in d["srcs"]], pos=d["pos"], masks=d["masks"])
+              for n, d in g["inputs"].items()}
+    with oracle_core(PKG):
+        mem_v, mem_a, hs, inter = run_multimodal(tr, qe, inputs)
+        w = g["weights"]
+        ((hs * w[0]).sum() + (mem_v * w[1]).sum() + (mem_a * w[2]).sum()).backward()
+    _close(hs, g["hs"])
+    _close(mem_v, g["memory_video"])
+    _close(mem_a, g["memory_audio"])
+    for n in ("video", "audio"):
+        for s, ref in zip(inputs[n]["srcs"], g["grad_srcs"][n]):
+            _close(s.grad, ref, rtol=1e-8, atol=1e-9)
+    for k, p in tr.named_parameters():
+        if k in g["param_grads"]["transformer"]:
+            _close(p.grad, g["param_grads"]["transformer"][k], rtol=1e-7, atol=1e-9)
