@@ -20,8 +20,8 @@
 // per-sample coordinate arithmetic is uniform inside a lane group.
 // Backward: grad_aw / grad_loc are reductions over the item's D channels = a
 // butterfly over the G lanes of the group (__shfl_xor, no LDS, no barriers);
-// grad_value is a scatter-add of the two taps with fp32/fp64 global atomics
-// (bf16/fp16 values accumulate in an fp32 workspace, converted once at the end).
+// grad_value is NOT scattered with global atomics: msda_gvalue_kernel gives every
+// (b, head, level, row-range) slab one owner workgroup that accumulates it in LDS.
 //
 // Coordinates are computed with FP contraction OFF in exactly the operation order of
 // ATen's CPU grid sampler (g = 2*loc-1, then y = fma(g+1, T/2, -0.5)), so the tap index
@@ -226,14 +226,11 @@ __global__ __launch_bounds__(256) void msda_fwd_kernel(
 // ---------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------
-__device__ __forceinline__ void atomic_add_acc(float* p, float v) { unsafeAtomicAdd(p, v); }
-__device__ __forceinline__ void atomic_add_acc(double* p, double v) { unsafeAtomicAdd(p, v); }
-
-template <typename scalar_t, typename coord_t, typename gacc_t, int VEC, bool ZEROS>
+template <typename scalar_t, typename coord_t, int VEC, bool ZEROS>
 __global__ __launch_bounds__(256) void msda_bwd_kernel(
     const scalar_t* __restrict__ value, const coord_t* __restrict__ loc,
     const coord_t* __restrict__ aw, const scalar_t* __restrict__ gout,
-    gacc_t* __restrict__ gval, coord_t* __restrict__ gloc, coord_t* __restrict__ gaw,
+    coord_t* __restrict__ gloc, coord_t* __restrict__ gaw,
     const Levels lv, const int L, const int P, const int S, const int M, const int D,
     const int Lq, const long long n_items, const int gshift) {
   using acc_t = typename AccOf<scalar_t>::type;
@@ -275,19 +272,6 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(
             pa += g[e] * (x0 * w0 + x1 * w1);
             pl += g[e] * (x1 - x0);
           }
-          if (gval != nullptr) {
-            gacc_t* gv = gval + vrow0 + lbase + ck * VEC;
-            if (t.ok0 && t.w0 != (coord_t)0) {
-              const acc_t s0 = aa * w0;
-#pragma unroll
-              for (int e = 0; e < VEC; ++e) atomic_add_acc(gv + t.i0 * rowstride + e, (gacc_t)(s0 * g[e]));
-            }
-            if (t.ok1 && t.w1 != (coord_t)0) {
-              const acc_t s1 = aa * w1;
-#pragma unroll
-              for (int e = 0; e < VEC; ++e) atomic_add_acc(gv + t.i1 * rowstride + e, (gacc_t)(s1 * g[e]));
-            }
-          }
         }
       }
       // butterfly over the G lanes of this item (G divides 64, groups are aligned)
@@ -304,26 +288,135 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(
   }
 }
 
-// fp32 accumulator -> bf16/fp16 grad_value
-template <typename scalar_t>
-__global__ __launch_bounds__(256) void cast_from_f32_kernel(const float* __restrict__ src,
-                                                           scalar_t* __restrict__ dst,
-                                                           long long n) {
-  const long long i0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (i0 + 3 < n) {
-    const float4 v = *reinterpret_cast<const float4*>(src + i0);
-    from_acc(v.x, dst + i0);
-    from_acc(v.y, dst + i0 + 1);
-    from_acc(v.z, dst + i0 + 2);
-    from_acc(v.w, dst + i0 + 3);
-  } else {
-    for (long long i = i0; i < n; ++i) from_acc(src[i], dst + i);
+// ---------------------------------------------------------------------------------
+// backward, grad_value: atomic-free scatter through LDS
+// ---------------------------------------------------------------------------------
+// One workgroup owns rows [r0, r1) of one (b, head m, level l) slab of grad_value and keeps
+// them in LDS (acc type).  It scans every sample (q, p) of level l for (b, m), recomputes
+// its two taps, and adds aw*w*grad_out[b,q,m,:] for each tap that falls in its rows
+// (lane = channel: one ds_add per 64 channels, conflict-free).  Every grad_value row has
+// exactly one owner, so the slab is written once with plain stores: no global atomics,
+// no memset, no fp32 workspace for bf16/fp16 values.
+struct RangePlan {
+  int rows;                      // rows per workgroup
+  int cum[MSDA_MAX_LEVELS + 1];  // prefix sum over levels of ceil(T_l / rows)
+};
+
+template <typename scalar_t, typename coord_t, bool ZEROS, bool ONE_CHUNK>
+__global__ __launch_bounds__(256) void msda_gvalue_kernel(
+    const coord_t* __restrict__ loc, const coord_t* __restrict__ aw,
+    const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, const Levels lv,
+    const RangePlan rp, const int L, const int P, const int S, const int M, const int D,
+    const int Lq) {
+  using acc_t = typename AccOf<scalar_t>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  acc_t* slab = reinterpret_cast<acc_t*>(smem_raw);
+
+  const int nr = rp.cum[L];
+  const int r = (int)(blockIdx.x % (unsigned)nr);
+  const long long bm = blockIdx.x / (unsigned)nr;
+  const int m = (int)(bm % M);
+  const long long b = bm / M;
+  int l = 0;
+  while (r >= rp.cum[l + 1]) ++l;
+  const int T = lv.T[l];
+  const int r0 = (r - rp.cum[l]) * rp.rows;
+  const int r1 = min(r0 + rp.rows, T);
+  const int nrows = r1 - r0;
+
+  for (int i = threadIdx.x; i < nrows * D; i += blockDim.x) slab[i] = (acc_t)0;
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int nwave = blockDim.x >> 6;
+  const int LP = L * P;
+  const long long qstride_c = (long long)M * LP;  // loc/aw stride between queries
+  const long long qstride_g = (long long)M * D;   // grad_out stride between queries
+  const coord_t* __restrict__ locb = loc + (b * Lq * M + m) * LP + l * P;
+  const coord_t* __restrict__ awb = aw + (b * Lq * M + m) * LP + l * P;
+  const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D;
+  const long long nsamp = (long long)Lq * P;
+
+  for (long long s0 = (long long)wave * 64; s0 < nsamp; s0 += (long long)nwave * 64) {
+    const long long sidx = s0 + lane;
+    int q = 0, i0 = 0, i1 = 0;
+    acc_t a0 = (acc_t)0, a1 = (acc_t)0;
+    bool in0 = false, in1 = false;
+    if (sidx < nsamp) {
+      q = (int)(sidx / P);
+      const int p = (int)(sidx - (long long)q * P);
+      const coord_t a = awb[q * qstride_c + p];
+      const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qstride_c + p], T);
+      in0 = t.ok0 && t.w0 != (coord_t)0 && t.i0 >= r0 && t.i0 < r1;
+      in1 = t.ok1 && t.w1 != (coord_t)0 && t.i1 >= r0 && t.i1 < r1;
+      a0 = (acc_t)a * (acc_t)t.w0;
+      a1 = (acc_t)a * (acc_t)t.w1;
+      i0 = t.i0 - r0;
+      i1 = t.i1 - r0;
+    }
+    // both taps of the 64 samples, as one list of (lane, tap) contributions
+    unsigned long long mk0 = __ballot(in0);
+    unsigned long long mk1 = __ballot(in1);
+    constexpr int BATCH = 8;
+    while (mk0 | mk1) {
+      int qs[BATCH], rows[BATCH];
+      acc_t ws[BATCH];
+#pragma unroll
+      for (int k = 0; k < BATCH; ++k) {
+        // pop one contribution (wave-uniform); empty slots get weight 0 on row 0 / q 0
+        const bool from0 = mk0 != 0ull;
+        const unsigned long long mk = from0 ? mk0 : mk1;
+        const bool have = mk != 0ull;
+        const int j = have ? __builtin_ctzll(mk) : 0;
+        if (from0) mk0 &= mk0 - 1; else if (have) mk1 &= mk1 - 1;
+        qs[k] = __builtin_amdgcn_readlane(q, j);
+        rows[k] = have ? __builtin_amdgcn_readlane(from0 ? i0 : i1, j) : 0;
+        const acc_t wsel = from0 ? a0 : a1;
+        acc_t wv;
+        if constexpr (sizeof(acc_t) == 8) {
+          const long long bits = __builtin_bit_cast(long long, wsel);
+          const int lo = __builtin_amdgcn_readlane((int)bits, j);
+          const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), j);
+          wv = __builtin_bit_cast(acc_t, ((long long)hi << 32) | (unsigned)lo);
+        } else {
+          wv = __builtin_bit_cast(acc_t, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wsel), j));
+        }
+        ws[k] = have ? wv : (acc_t)0;
+      }
+      if constexpr (ONE_CHUNK) {
+        acc_t g[BATCH];
+#pragma unroll
+        for (int k = 0; k < BATCH; ++k)
+          g[k] = lane < D ? to_acc(gb[qs[k] * qstride_g + lane]) : (acc_t)0;
+#pragma unroll
+        for (int k = 0; k < BATCH; ++k)
+          if (lane < D) atomicAdd(&slab[rows[k] * D + lane], ws[k] * g[k]);
+      } else {
+        for (int c = lane; c < D; c += 64) {
+          acc_t g[BATCH];
+#pragma unroll
+          for (int k = 0; k < BATCH; ++k) g[k] = to_acc(gb[qs[k] * qstride_g + c]);
+#pragma unroll
+          for (int k = 0; k < BATCH; ++k) atomicAdd(&slab[rows[k] * D + c], ws[k] * g[k]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  scalar_t* __restrict__ dst = gval + ((b * S + lv.start[l] + r0) * M + m) * (long long)D;
+  const long long rowstride = (long long)M * D;
+  for (int i = threadIdx.x; i < nrows * D; i += blockDim.x) {
+    const int row = i / D, c = i - row * D;
+    from_acc(slab[i], dst + row * rowstride + c);
   }
 }
 
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
+constexpr long long kSlabBytes = 48 * 1024;  // LDS per grad_value workgroup (3 per CU)
+
 struct Problem {
   long long B, S, M, D, Lq, L, P;
   Levels lv;
@@ -404,9 +497,9 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
   return launch_status("forward");
 }
 
-template <typename scalar_t, typename coord_t, typename gacc_t, int VEC>
+template <typename scalar_t, typename coord_t, int VEC>
 int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
-                 const void* gout, gacc_t* gacc, void* gloc, void* gaw, int pad, hipStream_t st) {
+                 const void* gout, void* gloc, void* gaw, int pad, hipStream_t st) {
   const long long n_items = pr.B * pr.Lq * pr.M;
   if (n_items == 0) return MSDA_OK;
   const int gshift = group_shift_for(pr.D / VEC);
@@ -419,14 +512,50 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
   auto* gl = static_cast<coord_t*>(gloc);
   auto* ga = static_cast<coord_t*>(gaw);
   if (pad == MSDA_PAD_ZEROS)
-    hipLaunchKernelGGL((msda_bwd_kernel<scalar_t, coord_t, gacc_t, VEC, true>), dim3(blocks),
-                       dim3(256), 0, st, v, lc, a, g, gacc, gl, ga, pr.lv, (int)pr.L, (int)pr.P,
+    hipLaunchKernelGGL((msda_bwd_kernel<scalar_t, coord_t, VEC, true>), dim3(blocks),
+                       dim3(256), 0, st, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P,
                        (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, n_items, gshift);
   else
-    hipLaunchKernelGGL((msda_bwd_kernel<scalar_t, coord_t, gacc_t, VEC, false>), dim3(blocks),
-                       dim3(256), 0, st, v, lc, a, g, gacc, gl, ga, pr.lv, (int)pr.L, (int)pr.P,
+    hipLaunchKernelGGL((msda_bwd_kernel<scalar_t, coord_t, VEC, false>), dim3(blocks),
+                       dim3(256), 0, st, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P,
                        (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, n_items, gshift);
   return launch_status("backward");
+}
+
+template <typename scalar_t, typename coord_t>
+int run_grad_value(const Problem& pr, const void* loc, const void* aw, const void* gout, void* gval,
+                   int pad, hipStream_t st) {
+  using acc_t = typename AccOf<scalar_t>::type;
+  if (pr.B * pr.M * pr.S * pr.D == 0) return MSDA_OK;
+  const long long row_bytes = pr.D * (long long)sizeof(acc_t);
+  if (row_bytes > kSlabBytes) {
+    set_error("msda_hip_backward: channels=%lld too large for the LDS grad_value slab", pr.D);
+    return MSDA_ERR_ARG;
+  }
+  int maxT = 1;
+  for (int l = 0; l < pr.L; ++l) maxT = max(maxT, pr.lv.T[l]);
+  RangePlan rp;
+  rp.rows = (int)min((long long)maxT, kSlabBytes / row_bytes);
+  rp.cum[0] = 0;
+  for (int l = 0; l < pr.L; ++l) rp.cum[l + 1] = rp.cum[l] + (pr.lv.T[l] + rp.rows - 1) / rp.rows;
+  const long long blocks = pr.B * pr.M * rp.cum[pr.L];
+  const size_t lds = (size_t)rp.rows * row_bytes;
+  auto* lc = static_cast<const coord_t*>(loc);
+  auto* a = static_cast<const coord_t*>(aw);
+  auto* g = static_cast<const scalar_t*>(gout);
+  auto* gv = static_cast<scalar_t*>(gval);
+#define MSDA_GV(Z, ONE)                                                                         \
+  hipLaunchKernelGGL((msda_gvalue_kernel<scalar_t, coord_t, Z, ONE>), dim3((unsigned)blocks),   \
+                     dim3(256), lds, st, lc, a, g, gv, pr.lv, rp, (int)pr.L, (int)pr.P,         \
+                     (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq)
+  const bool one = pr.D <= 64;
+  if (pad == MSDA_PAD_ZEROS) {
+    if (one) MSDA_GV(true, true); else MSDA_GV(true, false);
+  } else {
+    if (one) MSDA_GV(false, true); else MSDA_GV(false, false);
+  }
+#undef MSDA_GV
+  return launch_status("grad_value");
 }
 
 }  // namespace
@@ -439,9 +568,8 @@ const char* msda_hip_last_error(void) { return g_last_error; }
 
 size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,
                                          int64_t num_heads, int64_t channels) {
-  if (value_dtype == MSDA_DTYPE_BF16 || value_dtype == MSDA_DTYPE_F16)
-    return (size_t)batch * spatial_size * num_heads * channels * sizeof(float);
-  return 0;
+  (void)value_dtype; (void)batch; (void)spatial_size; (void)num_heads; (void)channels;
+  return 0;  // grad_value is accumulated in LDS slabs (msda_gvalue_kernel): no scratch
 }
 
 int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_shapes,
@@ -504,18 +632,10 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
     set_error("msda: unknown padding_mode %d", padding_mode);
     return MSDA_ERR_ARG;
   }
-  const bool half_like = value_dtype == MSDA_DTYPE_BF16 || value_dtype == MSDA_DTYPE_F16;
-  const long long n_val = pr.B * pr.S * pr.M * pr.D;
   const long long n_items = pr.B * pr.Lq * pr.M;
-  const size_t coord_sz = value_dtype == MSDA_DTYPE_F64 ? 8 : 4;
-  const size_t elt = value_dtype == MSDA_DTYPE_F64 ? 8 : (value_dtype == MSDA_DTYPE_F32 ? 4 : 2);
   if (n_items > 0 && (sampling_loc == nullptr || attn_weight == nullptr ||
                       grad_output == nullptr || (pr.S > 0 && value == nullptr))) {
     set_error("msda_hip_backward: null input pointer");
-    return MSDA_ERR_ARG;
-  }
-  if (half_like && grad_value != nullptr && n_val > 0 && workspace == nullptr) {
-    set_error("msda_hip_backward: bf16/f16 values need an fp32 workspace");
     return MSDA_ERR_ARG;
   }
   if (pr.S == 0 && n_items > 0) {
@@ -523,50 +643,47 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
     return MSDA_ERR_ARG;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-  // zero-init like at::zeros / zeros_like (ms_deform_attn_cuda.cu:121-123)
-  void* gacc = half_like ? workspace : grad_value;
-  if (grad_value != nullptr && n_val > 0) {
-    if (hipMemsetAsync(gacc, 0, (size_t)n_val * (half_like ? 4 : elt), st) != hipSuccess) {
-      set_error("msda_hip_backward: hipMemsetAsync failed");
-      return MSDA_ERR_LAUNCH;
-    }
-  }
-  if (grad_value == nullptr) gacc = nullptr;
   const int vec = pick_vec(value_dtype, pr.D);
+  (void)workspace;  // ABI v1 slot; grad_value no longer needs scratch (see msda_gvalue_kernel)
+  // grad_loc / grad_attn: per-item gathers + lane-group butterflies
+  if (grad_loc != nullptr || grad_attn != nullptr) {
+    switch (value_dtype) {
+      case MSDA_DTYPE_F32:
+        rc = vec == 4 ? run_backward<float, float, 4>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st)
+                      : run_backward<float, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st);
+        break;
+      case MSDA_DTYPE_F64:
+        rc = vec == 2 ? run_backward<double, double, 2>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st)
+                      : run_backward<double, double, 1>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st);
+        break;
+      case MSDA_DTYPE_BF16:
+        rc = vec == 8 ? run_backward<bf16_t, float, 8>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st)
+                      : run_backward<bf16_t, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st);
+        break;
+      case MSDA_DTYPE_F16:
+        rc = vec == 8 ? run_backward<f16_t, float, 8>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st)
+                      : run_backward<f16_t, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st);
+        break;
+      default:
+        set_error("msda_hip_backward: unknown value dtype %d", value_dtype);
+        return MSDA_ERR_ARG;
+    }
+    if (rc) return rc;
+  }
+  if (grad_value == nullptr) return MSDA_OK;
   switch (value_dtype) {
     case MSDA_DTYPE_F32:
-      rc = vec == 4 ? run_backward<float, float, float, 4>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st)
-                    : run_backward<float, float, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st);
-      break;
+      return run_grad_value<float, float>(pr, sampling_loc, attn_weight, grad_output, grad_value, padding_mode, st);
     case MSDA_DTYPE_F64:
-      rc = vec == 2 ? run_backward<double, double, double, 2>(pr, value, sampling_loc, attn_weight, grad_output, (double*)gacc, grad_loc, grad_attn, padding_mode, st)
-                    : run_backward<double, double, double, 1>(pr, value, sampling_loc, attn_weight, grad_output, (double*)gacc, grad_loc, grad_attn, padding_mode, st);
-      break;
+      return run_grad_value<double, double>(pr, sampling_loc, attn_weight, grad_output, grad_value, padding_mode, st);
     case MSDA_DTYPE_BF16:
-      rc = vec == 8 ? run_backward<bf16_t, float, float, 8>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st)
-                    : run_backward<bf16_t, float, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st);
-      break;
+      return run_grad_value<bf16_t, float>(pr, sampling_loc, attn_weight, grad_output, grad_value, padding_mode, st);
     case MSDA_DTYPE_F16:
-      rc = vec == 8 ? run_backward<f16_t, float, float, 8>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st)
-                    : run_backward<f16_t, float, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, (float*)gacc, grad_loc, grad_attn, padding_mode, st);
-      break;
+      return run_grad_value<f16_t, float>(pr, sampling_loc, attn_weight, grad_output, grad_value, padding_mode, st);
     default:
       set_error("msda_hip_backward: unknown value dtype %d", value_dtype);
       return MSDA_ERR_ARG;
   }
-  if (rc) return rc;
-  if (half_like && grad_value != nullptr && n_val > 0) {
-    const unsigned blocks = (unsigned)(((n_val + 3) / 4 + 255) / 256);
-    if (value_dtype == MSDA_DTYPE_BF16)
-      hipLaunchKernelGGL(cast_from_f32_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st,
-                         (const float*)workspace, (bf16_t*)grad_value, n_val);
-    else
-      hipLaunchKernelGGL(cast_from_f32_kernel<f16_t>, dim3(blocks), dim3(256), 0, st,
-                         (const float*)workspace, (f16_t*)grad_value, n_val);
-    rc = launch_status("grad_value cast");
-  }
-  (void)coord_sz;
-  return rc;
 }
 
 }  // extern "C"

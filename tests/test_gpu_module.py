@@ -62,13 +62,16 @@ def test_transformer_stack_matches_reference(golden, dev, dtype):
     finally:
         torch.set_default_dtype(torch.float32)
     if dtype == torch.float64:
-        _close(memory, g["memory"], 1e-9, 1e-10)
-        _close(hs, g["hs"], 1e-9, 1e-10)
-        _close(video.grad, g["grad_video"], 1e-8, 1e-9)
+        # the reference computes the sine position embedding in fp32 even in an fp64 model
+        # (embedding_layers.py:208, cumsum(dtype=float32)): GPU vs CPU fp32 sin/cos differ by
+        # an ulp, so the fp64 stack agrees to fp32 resolution, not 1e-9
+        _rel_close(memory, g["memory"], 1e-6)
+        _rel_close(hs, g["hs"], 1e-6)
+        _rel_close(video.grad, g["grad_video"], 1e-6)
         for n, m in mods.items():
             for k, p in m.named_parameters():
                 if k in g["param_grads"][n]:
-                    _close(p.grad, g["param_grads"][n][k], 1e-7, 1e-9)
+                    _rel_close(p.grad, g["param_grads"][n][k], 1e-6)
     else:  # fp32 end to end vs the fp64 reference: north_star's 1e-3 relative
         _rel_close(memory, g["memory"], 1e-3)
         _rel_close(hs, g["hs"], 1e-3)
