@@ -78,12 +78,17 @@ __device__ __forceinline__ void from_acc(float a, f16_t* d) {
   d->x = __half_as_ushort(__float2half(a));
 }
 
-// Load VEC consecutive elements (16 B when VEC*sizeof == 16) into the accumulator type.
+// Load VEC consecutive elements (one 16- or 8-byte access when VEC*sizeof is 16 or 8).
 template <typename scalar_t, int VEC>
 __device__ __forceinline__ void load_vec(const scalar_t* __restrict__ p,
                                          typename AccOf<scalar_t>::type (&r)[VEC]) {
   if constexpr (VEC * sizeof(scalar_t) == 16) {
     const uint4 raw = *reinterpret_cast<const uint4*>(p);
+    const scalar_t* e = reinterpret_cast<const scalar_t*>(&raw);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) r[i] = to_acc(e[i]);
+  } else if constexpr (VEC * sizeof(scalar_t) == 8) {
+    const uint2 raw = *reinterpret_cast<const uint2*>(p);
     const scalar_t* e = reinterpret_cast<const scalar_t*>(&raw);
 #pragma unroll
     for (int i = 0; i < VEC; ++i) r[i] = to_acc(e[i]);
@@ -102,6 +107,12 @@ __device__ __forceinline__ void store_vec(scalar_t* __restrict__ p,
 #pragma unroll
     for (int i = 0; i < VEC; ++i) from_acc(r[i], &e[i]);
     *reinterpret_cast<uint4*>(p) = raw;
+  } else if constexpr (VEC * sizeof(scalar_t) == 8) {
+    uint2 raw;
+    scalar_t* e = reinterpret_cast<scalar_t*>(&raw);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) from_acc(r[i], &e[i]);
+    *reinterpret_cast<uint2*>(p) = raw;
   } else {
 #pragma unroll
     for (int i = 0; i < VEC; ++i) from_acc(r[i], &p[i]);
@@ -289,26 +300,43 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(
 }
 
 // ---------------------------------------------------------------------------------
-// backward, grad_value: atomic-free scatter through LDS
+// backward, grad_value: scatter through LDS with plain (non-atomic) read-modify-write
 // ---------------------------------------------------------------------------------
 // One workgroup owns rows [r0, r1) of one (b, head m, level l) slab of grad_value and keeps
-// them in LDS (acc type).  It scans every sample (q, p) of level l for (b, m), recomputes
-// its two taps, and adds aw*w*grad_out[b,q,m,:] for each tap that falls in its rows
-// (lane = channel: one ds_add per 64 channels, conflict-free).  Every grad_value row has
-// exactly one owner, so the slab is written once with plain stores: no global atomics,
-// no memset, no fp32 workspace for bf16/fp16 values.
+// them in LDS as fp32 (fp64 for fp64 values).  It scans every sample (q, p) of level l for
+// (b, m), recomputes the two taps and adds aw*w*grad_out[b,q,m,:] to each tap row it owns.
+// Every grad_value row has exactly one owner workgroup, so the slab is written once with
+// plain stores: no global atomics, no memset, no fp32 staging buffer for bf16/fp16.
+//
+// No LDS atomics either: ds_add_f32 measured ~81 ns per wave-op per CU on gfx950 against
+// ~7 ns for a ds_read + ds_write pair (tools/lds_probe.hip).  Races are avoided by
+// ownership instead:
+//   * wave w of the workgroup owns the rows with (row - r0) % 4 == w (both taps of a sample
+//     are adjacent rows, so they always belong to different waves);
+//   * inside a wave, NSLOT contributions are applied per instruction, one per "slot" of
+//     64/NSLOT lanes (CPL channels per lane = one 16-byte ds_read/ds_write); slot =
+//     ((row - r0) / 4) % NSLOT, so the rows of one instruction are always distinct, and
+//     later rounds of the same slot are ordered by the wave's in-order LDS pipe.
+// NSLOT = 0 is the generic path (any channel count): one contribution per round, lane =
+// channel, 4-byte (8 for fp64) RMW.
 struct RangePlan {
   int rows;                      // rows per workgroup
   int cum[MSDA_MAX_LEVELS + 1];  // prefix sum over levels of ceil(T_l / rows)
 };
 
-template <typename scalar_t, typename coord_t, bool ZEROS, bool ONE_CHUNK>
+template <typename acc_t, int N>
+struct alignas(16) AccN {
+  acc_t v[N];
+};
+
+template <typename scalar_t, typename coord_t, bool ZEROS, int NSLOT>
 __global__ __launch_bounds__(256) void msda_gvalue_kernel(
     const coord_t* __restrict__ loc, const coord_t* __restrict__ aw,
     const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, const Levels lv,
     const RangePlan rp, const int L, const int P, const int S, const int M, const int D,
     const int Lq) {
   using acc_t = typename AccOf<scalar_t>::type;
+  constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(acc_t) : 1;  // channels per lane
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   acc_t* slab = reinterpret_cast<acc_t*>(smem_raw);
 
@@ -324,81 +352,104 @@ __global__ __launch_bounds__(256) void msda_gvalue_kernel(
   const int r1 = min(r0 + rp.rows, T);
   const int nrows = r1 - r0;
 
-  for (int i = threadIdx.x; i < nrows * D; i += blockDim.x) slab[i] = (acc_t)0;
+  for (int i = threadIdx.x * CPL; i < nrows * D; i += blockDim.x * CPL) {
+#pragma unroll
+    for (int e = 0; e < CPL; ++e) slab[i + e] = (acc_t)0;
+  }
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int nwave = blockDim.x >> 6;
   const int LP = L * P;
   const long long qstride_c = (long long)M * LP;  // loc/aw stride between queries
   const long long qstride_g = (long long)M * D;   // grad_out stride between queries
   const coord_t* __restrict__ locb = loc + (b * Lq * M + m) * LP + l * P;
   const coord_t* __restrict__ awb = aw + (b * Lq * M + m) * LP + l * P;
   const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D;
-  const long long nsamp = (long long)Lq * P;
+  const int nsamp = Lq * P;
+  constexpr int NS = NSLOT > 0 ? NSLOT : 1;
+  constexpr int LPR = 64 / NS;  // lanes per slot
+  const int slot = lane / LPR;
+  const int cl = lane - slot * LPR;
 
-  for (long long s0 = (long long)wave * 64; s0 < nsamp; s0 += (long long)nwave * 64) {
-    const long long sidx = s0 + lane;
-    int q = 0, i0 = 0, i1 = 0;
-    acc_t a0 = (acc_t)0, a1 = (acc_t)0;
-    bool in0 = false, in1 = false;
+  for (int s0 = 0; s0 < nsamp; s0 += 64) {
+    // --- one tap per lane at most: the one whose row this wave owns ---
+    const int sidx = s0 + lane;
+    int q = 0, rowl = 0;
+    acc_t wt = (acc_t)0;
+    bool has = false;
     if (sidx < nsamp) {
-      q = (int)(sidx / P);
-      const int p = (int)(sidx - (long long)q * P);
+      q = sidx / P;
+      const int p = sidx - q * P;
       const coord_t a = awb[q * qstride_c + p];
       const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qstride_c + p], T);
-      in0 = t.ok0 && t.w0 != (coord_t)0 && t.i0 >= r0 && t.i0 < r1;
-      in1 = t.ok1 && t.w1 != (coord_t)0 && t.i1 >= r0 && t.i1 < r1;
-      a0 = (acc_t)a * (acc_t)t.w0;
-      a1 = (acc_t)a * (acc_t)t.w1;
-      i0 = t.i0 - r0;
-      i1 = t.i1 - r0;
+      const bool c0 = t.ok0 && t.w0 != (coord_t)0 && t.i0 >= r0 && t.i0 < r1 && ((t.i0 - r0) & 3) == wave;
+      const bool c1 = t.ok1 && t.w1 != (coord_t)0 && t.i1 >= r0 && t.i1 < r1 && ((t.i1 - r0) & 3) == wave;
+      has = c0 || c1;
+      rowl = (c0 ? t.i0 : t.i1) - r0;
+      wt = (acc_t)a * (acc_t)(c0 ? t.w0 : t.w1);
     }
-    // both taps of the 64 samples, as one list of (lane, tap) contributions
-    unsigned long long mk0 = __ballot(in0);
-    unsigned long long mk1 = __ballot(in1);
-    constexpr int BATCH = 8;
-    while (mk0 | mk1) {
-      int qs[BATCH], rows[BATCH];
-      acc_t ws[BATCH];
+    unsigned long long mk[NS];
 #pragma unroll
-      for (int k = 0; k < BATCH; ++k) {
-        // pop one contribution (wave-uniform); empty slots get weight 0 on row 0 / q 0
-        const bool from0 = mk0 != 0ull;
-        const unsigned long long mk = from0 ? mk0 : mk1;
-        const bool have = mk != 0ull;
-        const int j = have ? __builtin_ctzll(mk) : 0;
-        if (from0) mk0 &= mk0 - 1; else if (have) mk1 &= mk1 - 1;
-        qs[k] = __builtin_amdgcn_readlane(q, j);
-        rows[k] = have ? __builtin_amdgcn_readlane(from0 ? i0 : i1, j) : 0;
-        const acc_t wsel = from0 ? a0 : a1;
-        acc_t wv;
-        if constexpr (sizeof(acc_t) == 8) {
-          const long long bits = __builtin_bit_cast(long long, wsel);
-          const int lo = __builtin_amdgcn_readlane((int)bits, j);
-          const int hi = __builtin_amdgcn_readlane((int)(bits >> 32), j);
-          wv = __builtin_bit_cast(acc_t, ((long long)hi << 32) | (unsigned)lo);
+    for (int sl = 0; sl < NS; ++sl) mk[sl] = __ballot(has && ((rowl >> 2) % NS) == sl);
+    unsigned long long any = 0;
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) any |= mk[sl];
+    constexpr int ROUNDS = 4;  // rounds whose grad_out loads are in flight together
+    while (any) {
+      int srow[ROUNDS], sq[ROUNDS];
+      acc_t sw[ROUNDS];
+#pragma unroll
+      for (int k = 0; k < ROUNDS; ++k) {
+        // pop one contribution per slot (wave-uniform), then each lane takes its slot's
+        if constexpr (NS == 1) {
+          const bool hv = mk[0] != 0ull;
+          const int j = hv ? __builtin_ctzll(mk[0]) : 0;  // wave-uniform
+          if (hv) mk[0] &= mk[0] - 1;
+          sq[k] = hv ? __builtin_amdgcn_readlane(q, j) : 0;
+          srow[k] = hv ? __builtin_amdgcn_readlane(rowl, j) : -1;
+          sw[k] = hv ? __shfl(wt, j) : (acc_t)0;
         } else {
-          wv = __builtin_bit_cast(acc_t, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wsel), j));
+          int my_j = 0;
+          bool my_have = false;
+#pragma unroll
+          for (int sl = 0; sl < NS; ++sl) {
+            const bool hv = mk[sl] != 0ull;
+            const int j = hv ? __builtin_ctzll(mk[sl]) : 0;
+            if (hv) mk[sl] &= mk[sl] - 1;
+            if (slot == sl) { my_j = j; my_have = hv; }
+          }
+          sq[k] = __shfl(q, my_j);
+          srow[k] = __shfl(rowl, my_j);
+          sw[k] = my_have ? __shfl(wt, my_j) : (acc_t)0;
+          if (!my_have) { sq[k] = 0; srow[k] = -1; }
         }
-        ws[k] = have ? wv : (acc_t)0;
       }
-      if constexpr (ONE_CHUNK) {
-        acc_t g[BATCH];
+      any = 0;
 #pragma unroll
-        for (int k = 0; k < BATCH; ++k)
-          g[k] = lane < D ? to_acc(gb[qs[k] * qstride_g + lane]) : (acc_t)0;
+      for (int sl = 0; sl < NS; ++sl) any |= mk[sl];
+      if constexpr (NSLOT > 0) {
+        acc_t g[ROUNDS][CPL];
 #pragma unroll
-        for (int k = 0; k < BATCH; ++k)
-          if (lane < D) atomicAdd(&slab[rows[k] * D + lane], ws[k] * g[k]);
+        for (int k = 0; k < ROUNDS; ++k) load_vec<scalar_t, CPL>(gb + sq[k] * qstride_g + cl * CPL, g[k]);
+#pragma unroll
+        for (int k = 0; k < ROUNDS; ++k) {
+          if (srow[k] >= 0) {
+            AccN<acc_t, CPL>* dst = reinterpret_cast<AccN<acc_t, CPL>*>(slab + srow[k] * D + cl * CPL);
+            AccN<acc_t, CPL> v = *dst;
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) v.v[e] += sw[k] * g[k][e];
+            *dst = v;
+          }
+        }
       } else {
         for (int c = lane; c < D; c += 64) {
-          acc_t g[BATCH];
+          acc_t g[ROUNDS];
 #pragma unroll
-          for (int k = 0; k < BATCH; ++k) g[k] = to_acc(gb[qs[k] * qstride_g + c]);
+          for (int k = 0; k < ROUNDS; ++k) g[k] = to_acc(gb[sq[k] * qstride_g + c]);
 #pragma unroll
-          for (int k = 0; k < BATCH; ++k) atomicAdd(&slab[rows[k] * D + c], ws[k] * g[k]);
+          for (int k = 0; k < ROUNDS; ++k)
+            if (srow[k] >= 0) slab[srow[k] * D + c] += sw[k] * g[k];
         }
       }
     }
@@ -406,9 +457,16 @@ __global__ __launch_bounds__(256) void msda_gvalue_kernel(
   __syncthreads();
   scalar_t* __restrict__ dst = gval + ((b * S + lv.start[l] + r0) * M + m) * (long long)D;
   const long long rowstride = (long long)M * D;
-  for (int i = threadIdx.x; i < nrows * D; i += blockDim.x) {
+  for (int i = threadIdx.x * CPL; i < nrows * D; i += blockDim.x * CPL) {
     const int row = i / D, c = i - row * D;
-    from_acc(slab[i], dst + row * rowstride + c);
+    if constexpr (CPL > 1) {
+      acc_t v[CPL];
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) v[e] = slab[i + e];
+      store_vec<scalar_t, CPL>(dst + row * rowstride + c, v);
+    } else {
+      from_acc(slab[i], dst + row * rowstride + c);
+    }
   }
 }
 
@@ -544,15 +602,23 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
   auto* a = static_cast<const coord_t*>(aw);
   auto* g = static_cast<const scalar_t*>(gout);
   auto* gv = static_cast<scalar_t*>(gval);
-#define MSDA_GV(Z, ONE)                                                                         \
-  hipLaunchKernelGGL((msda_gvalue_kernel<scalar_t, coord_t, Z, ONE>), dim3((unsigned)blocks),   \
+#define MSDA_GV(Z, NS)                                                                          \
+  hipLaunchKernelGGL((msda_gvalue_kernel<scalar_t, coord_t, Z, NS>), dim3((unsigned)blocks),    \
                      dim3(256), lds, st, lc, a, g, gv, pr.lv, rp, (int)pr.L, (int)pr.P,         \
                      (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq)
-  const bool one = pr.D <= 64;
-  if (pad == MSDA_PAD_ZEROS) {
-    if (one) MSDA_GV(true, true); else MSDA_GV(true, false);
-  } else {
-    if (one) MSDA_GV(false, true); else MSDA_GV(false, false);
+  // slots per instruction for 16-byte lanes: NSLOT = 64 / (D / CPL) when that is a power of 2
+  constexpr int CPL = 16 / (int)sizeof(acc_t);
+  int ns = 0;
+  if (pr.D % CPL == 0 && pr.D / CPL <= 64 && 64 % (pr.D / CPL) == 0) ns = (int)(64 / (pr.D / CPL));
+  if (ns > 16) ns = 0;  // tiny heads: generic path
+  const bool z = pad == MSDA_PAD_ZEROS;
+  switch (ns) {
+    case 1: if (z) MSDA_GV(true, 1); else MSDA_GV(false, 1); break;
+    case 2: if (z) MSDA_GV(true, 2); else MSDA_GV(false, 2); break;
+    case 4: if (z) MSDA_GV(true, 4); else MSDA_GV(false, 4); break;
+    case 8: if (z) MSDA_GV(true, 8); else MSDA_GV(false, 8); break;
+    case 16: if (z) MSDA_GV(true, 16); else MSDA_GV(false, 16); break;
+    default: if (z) MSDA_GV(true, 0); else MSDA_GV(false, 0); break;
   }
 #undef MSDA_GV
   return launch_status("grad_value");

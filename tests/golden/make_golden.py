@@ -19,9 +19,10 @@ Fixtures:
   module_f64.pt              MSDeformAttn(d=64, L=4, M=4, P=4) (attention.py:394) fwd + grads,
                              encoder shape (+ padding mask) and decoder shape, is_sparse outputs.
   transformer_f64.pt         PositionEmbeddingVideoSine + BaseEncoder + DeformableTransformer
-                             (2 enc + 2 dec, d=64, dropout 0) at T=64, B=2 (one padded clip).
+                             (2 enc + 2 dec, d=64, dropout 0) at T=64, B=2 (one padded clip),
+                             sampling_offsets weights jittered off their exact init.
   multimodal_f64.pt          MultimodalDeformableTransformer (1 enc + 1 dec, d=64), video
-                             T=32 / audio T=16 pyramids, B=2.
+                             T=32 / audio T=16 pyramids, B=2, offsets jittered likewise.
 """
 import os
 import sys
@@ -58,6 +59,20 @@ def import_reference():
     import models.deformable.multimodal_deformable_transformer as mm  # noqa: E402
     return types.SimpleNamespace(attention=attention, base_encoder=base_encoder,
                                  embedding_layers=embedding_layers, uni=uni, mm=mm)
+
+
+def _jitter_offsets(module, seed):
+    """Move every MSDeformAttn off its exact initialisation: at init all sampling offsets are
+    integers, so every encoder sample sits exactly on a map position, where the location
+    gradient is discontinuous and any rounding difference picks another segment.  A small
+    random sampling_offsets weight (as after a few training steps) puts samples at generic
+    positions, so fp32 vs fp64 comparisons of the transformer gradients are meaningful."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for mod in module.modules():
+            if type(mod).__name__ == "MSDeformAttn":
+                w = mod.sampling_offsets.weight
+                w.copy_((torch.randn(w.shape, generator=g, dtype=torch.float64) * 0.05).to(w.dtype))
 
 
 def _compact(state_dict):
@@ -169,6 +184,7 @@ def transformer_case(ref, seed=23):
                                        dim_feedforward=128, dropout=0.0, return_intermediate_dec=True,
                                        num_feature_levels=4, dec_n_points=4, enc_n_points=4).double()
     query_embedding = torch.nn.Embedding(Q, d_model * 2).double()
+    _jitter_offsets(tr, seed)
     # the reference's duration embedding allocates with the default dtype
     # (embedding_layers.py:222): run the forward with float64 as the default dtype
     torch.set_default_dtype(torch.float64)
@@ -213,6 +229,7 @@ def multimodal_case(ref, seed=31):
                                                 return_intermediate_dec=True, num_feature_levels=4,
                                                 dec_n_points=4, enc_n_points=4).double()
     query_embedding = torch.nn.Embedding(Q, d_model * 2).double()
+    _jitter_offsets(tr, seed)
     gen = torch.Generator().manual_seed(seed)
     inputs = {}
     prepared = {}

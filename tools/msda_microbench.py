@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""MSDA kernel microbenchmark: times each HIP kernel of the path through the C-ABI with
+HIP events, at the bench's encoder / decoder call shapes (B=8, T=1024 pyramid, M=8, D=64,
+L=4, P=4), for three location regimes:
+  init     — the reference's initial sampling (ref point + integer offsets: every sample
+             exactly on a map position),
+  trained  — ref point + N(0, 2 / T_l) jitter (taps spread around the reference),
+  uniform  — U(0, 1) locations (no locality at all).
+Prints one JSON line per (dtype, shape, regime, kernel) with avg µs and algorithmic GB/s.
+"""
+import argparse
+import importlib
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = importlib.import_module("multimodal-feature-learning_amd")
+msda = PKG.msda
+
+
+def make(regime, B, Lq, shapes, M, P, dtype, dev, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    S = sum(shapes)
+    L = len(shapes)
+    value = torch.randn(B, S, M, 64, generator=g).to(dev, dtype)
+    if Lq == S:  # encoder: the reference points of every token (valid ratio 1)
+        ref = torch.cat([(torch.arange(t, dtype=torch.float32) + 0.5) / t for t in shapes])
+    else:
+        ref = torch.rand(Lq, generator=g)
+    ref = ref.view(1, Lq, 1, 1, 1).expand(B, Lq, M, L, P)
+    T = torch.tensor(shapes, dtype=torch.float32).view(1, 1, 1, L, 1)
+    theta = torch.arange(M, dtype=torch.float32) * (2 * 3.141592653589793 / M)
+    d = torch.stack([theta.cos(), theta.sin()], -1)
+    d = (d / d.abs().max(-1, keepdim=True)[0])[:, 0].view(1, 1, M, 1, 1)
+    k = torch.arange(1, P + 1, dtype=torch.float32).view(1, 1, 1, 1, P)
+    if regime == "init":
+        loc = ref + d * k / T
+    elif regime == "trained":
+        loc = ref + d * k / T + torch.randn(B, Lq, M, L, P, generator=g) * 2.0 / T
+    else:
+        loc = torch.rand(B, Lq, M, L, P, generator=g)
+    aw = torch.softmax(torch.randn(B, Lq, M, L * P, generator=g), -1).view(B, Lq, M, L, P)
+    gout = torch.randn(B, Lq, M * 64, generator=g).to(dev, dtype)
+    return value, loc.contiguous().to(dev), aw.to(dev), gout
+
+
+def timeit(fn, iters):
+    for _ in range(3):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--dtypes", default="bf16,fp32")
+    ap.add_argument("--regimes", default="init,trained,uniform")
+    ap.add_argument("--B", type=int, default=8)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    shapes = [1024, 512, 256, 128]
+    starts = [0, 1024, 1536, 1792]
+    S, M, L, P, D = sum(shapes), 8, 4, 4, 64
+    for dname in args.dtypes.split(","):
+        dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[dname]
+        vb = 2 if dtype == torch.bfloat16 else 4
+        for Lq, shape_name in ((S, "enc"), (100, "dec")):
+            for regime in args.regimes.split(","):
+                value, loc, aw, gout = make(regime, args.B, Lq, shapes, M, P, dtype, dev)
+                fwd_b = msda.algorithmic_bytes("fwd", args.B, S, M, D, Lq, L, P, vb)
+                bwd_b = msda.algorithmic_bytes("bwd", args.B, S, M, D, Lq, L, P, vb)
+                runs = {
+                    "fwd": (lambda: msda.msda_forward(value, shapes, starts, loc, aw), fwd_b),
+                    "bwd_loc_aw": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout,
+                                                              need_value=False), None),
+                    "bwd_value": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout,
+                                                             need_loc=False, need_aw=False), None),
+                    "bwd_all": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout), bwd_b),
+                }
+                for name, (fn, nbytes) in runs.items():
+                    us = timeit(fn, args.iters)
+                    rec = {"dtype": dname, "shape": shape_name, "regime": regime, "kernel": name,
+                           "us": round(us, 2)}
+                    if nbytes:
+                        rec["alg_GBps"] = round(nbytes / (us * 1e-6) / 1e9, 1)
+                    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
