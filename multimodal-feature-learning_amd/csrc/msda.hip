@@ -329,16 +329,31 @@ struct alignas(16) AccN {
   acc_t v[N];
 };
 
+constexpr int kGvThreads = 256;
+constexpr int kGvSampPerThread = 4;                             // samples per thread per step
+constexpr int kGvStep = kGvThreads * kGvSampPerThread;          // samples scanned per step
+constexpr int kGvQueue = 2 * kGvStep;                           // <= 2 taps per sample
+
 template <typename scalar_t, typename coord_t, bool ZEROS, int NSLOT>
-__global__ __launch_bounds__(256) void msda_gvalue_kernel(
+__global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
     const coord_t* __restrict__ loc, const coord_t* __restrict__ aw,
     const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, const Levels lv,
     const RangePlan rp, const int L, const int P, const int S, const int M, const int D,
     const int Lq) {
   using acc_t = typename AccOf<scalar_t>::type;
   constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(acc_t) : 1;  // channels per lane
+  constexpr int NS = NSLOT > 0 ? NSLOT : 1;
+  constexpr int LPR = 64 / NS;                                   // lanes per slot
+  constexpr int ROUNDS = 8;  // slot-rounds whose grad_out loads are in flight together
+
+  // LDS: [slab rows*D acc_t][queue: q int, rowl int, w acc_t][queue counter]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int rows_cap = rp.rows;
   acc_t* slab = reinterpret_cast<acc_t*>(smem_raw);
+  int* q_q = reinterpret_cast<int*>(smem_raw + (size_t)rows_cap * D * sizeof(acc_t));
+  int* q_row = q_q + kGvQueue;
+  acc_t* q_w = reinterpret_cast<acc_t*>(q_row + kGvQueue);
+  int* q_cnt = reinterpret_cast<int*>(q_w + kGvQueue);
 
   const int nr = rp.cum[L];
   const int r = (int)(blockIdx.x % (unsigned)nr);
@@ -352,10 +367,11 @@ __global__ __launch_bounds__(256) void msda_gvalue_kernel(
   const int r1 = min(r0 + rp.rows, T);
   const int nrows = r1 - r0;
 
-  for (int i = threadIdx.x * CPL; i < nrows * D; i += blockDim.x * CPL) {
+  for (int i = threadIdx.x * CPL; i < nrows * D; i += kGvThreads * CPL) {
 #pragma unroll
     for (int e = 0; e < CPL; ++e) slab[i + e] = (acc_t)0;
   }
+  if (threadIdx.x == 0) *q_cnt = 0;
   __syncthreads();
 
   const int lane = threadIdx.x & 63;
@@ -367,49 +383,77 @@ __global__ __launch_bounds__(256) void msda_gvalue_kernel(
   const coord_t* __restrict__ awb = aw + (b * Lq * M + m) * LP + l * P;
   const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D;
   const int nsamp = Lq * P;
-  constexpr int NS = NSLOT > 0 ? NSLOT : 1;
-  constexpr int LPR = 64 / NS;  // lanes per slot
   const int slot = lane / LPR;
   const int cl = lane - slot * LPR;
 
-  for (int s0 = 0; s0 < nsamp; s0 += 64) {
-    // --- one tap per lane at most: the one whose row this wave owns ---
-    const int sidx = s0 + lane;
-    int q = 0, rowl = 0;
-    acc_t wt = (acc_t)0;
-    bool has = false;
-    if (sidx < nsamp) {
-      q = sidx / P;
-      const int p = sidx - q * P;
-      const coord_t a = awb[q * qstride_c + p];
-      const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qstride_c + p], T);
-      const bool c0 = t.ok0 && t.w0 != (coord_t)0 && t.i0 >= r0 && t.i0 < r1 && ((t.i0 - r0) & 3) == wave;
-      const bool c1 = t.ok1 && t.w1 != (coord_t)0 && t.i1 >= r0 && t.i1 < r1 && ((t.i1 - r0) & 3) == wave;
-      has = c0 || c1;
-      rowl = (c0 ? t.i0 : t.i1) - r0;
-      wt = (acc_t)a * (acc_t)(c0 ? t.w0 : t.w1);
+  for (int base = 0; base < nsamp; base += kGvStep) {
+    // ---- phase A: the whole workgroup scans kGvStep samples (loads issued together) ----
+    coord_t lc[kGvSampPerThread], av[kGvSampPerThread];
+#pragma unroll
+    for (int u = 0; u < kGvSampPerThread; ++u) {
+      const int sidx = base + u * kGvThreads + threadIdx.x;
+      const int qq = sidx / P, pp = sidx - (sidx / P) * P;
+      const bool live = sidx < nsamp;
+      lc[u] = live ? locb[qq * qstride_c + pp] : (coord_t)-1e30;
+      av[u] = live ? awb[qq * qstride_c + pp] : (coord_t)0;
     }
-    unsigned long long mk[NS];
 #pragma unroll
-    for (int sl = 0; sl < NS; ++sl) mk[sl] = __ballot(has && ((rowl >> 2) % NS) == sl);
-    unsigned long long any = 0;
+    for (int u = 0; u < kGvSampPerThread; ++u) {
+      const int sidx = base + u * kGvThreads + threadIdx.x;
+      const int qq = sidx / P;
+      bool c[2] = {false, false};
+      int rw[2] = {0, 0};
+      acc_t wv[2] = {(acc_t)0, (acc_t)0};
+      if (sidx < nsamp) {
+        const Taps<coord_t> t = make_taps<coord_t, ZEROS>(lc[u], T);
+        c[0] = t.ok0 && t.w0 != (coord_t)0 && t.i0 >= r0 && t.i0 < r1;
+        c[1] = t.ok1 && t.w1 != (coord_t)0 && t.i1 >= r0 && t.i1 < r1;
+        rw[0] = t.i0 - r0;
+        rw[1] = t.i1 - r0;
+        wv[0] = (acc_t)av[u] * (acc_t)t.w0;
+        wv[1] = (acc_t)av[u] * (acc_t)t.w1;
+      }
 #pragma unroll
-    for (int sl = 0; sl < NS; ++sl) any |= mk[sl];
-    constexpr int ROUNDS = 4;  // rounds whose grad_out loads are in flight together
-    while (any) {
-      int srow[ROUNDS], sq[ROUNDS];
-      acc_t sw[ROUNDS];
+      for (int k = 0; k < 2; ++k) {
+        // wave-level compaction, one LDS counter bump per wave
+        const unsigned long long mk = __ballot(c[k]);
+        if (mk == 0ull) continue;
+        const int before = __builtin_amdgcn_mbcnt_hi((unsigned)(mk >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk, 0u));
+        int start = 0;
+        if (lane == 0) start = atomicAdd(q_cnt, __popcll(mk));
+        start = __shfl(start, 0);
+        if (c[k]) {
+          q_q[start + before] = qq;
+          q_row[start + before] = rw[k];
+          q_w[start + before] = wv[k];
+        }
+      }
+    }
+    __syncthreads();
+    const int n = *q_cnt;
+    // ---- phase B: wave w applies the entries whose row it owns ((row & 3) == w) ----
+    for (int e0 = 0; e0 < n; e0 += 64) {
+      const int e = e0 + lane;
+      int eq = 0, er = 0;
+      acc_t ew = (acc_t)0;
+      bool mine = false;
+      if (e < n) {
+        er = q_row[e];
+        mine = (er & 3) == wave;
+        eq = q_q[e];
+        ew = q_w[e];
+      }
+      unsigned long long mk[NS];
 #pragma unroll
-      for (int k = 0; k < ROUNDS; ++k) {
-        // pop one contribution per slot (wave-uniform), then each lane takes its slot's
-        if constexpr (NS == 1) {
-          const bool hv = mk[0] != 0ull;
-          const int j = hv ? __builtin_ctzll(mk[0]) : 0;  // wave-uniform
-          if (hv) mk[0] &= mk[0] - 1;
-          sq[k] = hv ? __builtin_amdgcn_readlane(q, j) : 0;
-          srow[k] = hv ? __builtin_amdgcn_readlane(rowl, j) : -1;
-          sw[k] = hv ? __shfl(wt, j) : (acc_t)0;
-        } else {
+      for (int sl = 0; sl < NS; ++sl) mk[sl] = __ballot(mine && ((er >> 2) % NS) == sl);
+      unsigned long long any = 0;
+#pragma unroll
+      for (int sl = 0; sl < NS; ++sl) any |= mk[sl];
+      while (any) {
+        int srow[ROUNDS], sq[ROUNDS];
+        acc_t sw[ROUNDS];
+#pragma unroll
+        for (int k = 0; k < ROUNDS; ++k) {
           int my_j = 0;
           bool my_have = false;
 #pragma unroll
@@ -419,45 +463,51 @@ __global__ __launch_bounds__(256) void msda_gvalue_kernel(
             if (hv) mk[sl] &= mk[sl] - 1;
             if (slot == sl) { my_j = j; my_have = hv; }
           }
-          sq[k] = __shfl(q, my_j);
-          srow[k] = __shfl(rowl, my_j);
-          sw[k] = my_have ? __shfl(wt, my_j) : (acc_t)0;
-          if (!my_have) { sq[k] = 0; srow[k] = -1; }
+          // every lane executes the bpermutes (a masked-off source lane would read as 0)
+          const int qj = __shfl(eq, my_j);
+          const int rj = __shfl(er, my_j);
+          const acc_t wj = __shfl(ew, my_j);
+          sq[k] = my_have ? qj : 0;
+          srow[k] = my_have ? rj : -1;
+          sw[k] = my_have ? wj : (acc_t)0;
         }
-      }
-      any = 0;
+        any = 0;
 #pragma unroll
-      for (int sl = 0; sl < NS; ++sl) any |= mk[sl];
-      if constexpr (NSLOT > 0) {
-        acc_t g[ROUNDS][CPL];
+        for (int sl = 0; sl < NS; ++sl) any |= mk[sl];
+        if constexpr (NSLOT > 0) {
+          acc_t g[ROUNDS][CPL];
 #pragma unroll
-        for (int k = 0; k < ROUNDS; ++k) load_vec<scalar_t, CPL>(gb + sq[k] * qstride_g + cl * CPL, g[k]);
+          for (int k = 0; k < ROUNDS; ++k) load_vec<scalar_t, CPL>(gb + sq[k] * qstride_g + cl * CPL, g[k]);
 #pragma unroll
-        for (int k = 0; k < ROUNDS; ++k) {
-          if (srow[k] >= 0) {
-            AccN<acc_t, CPL>* dst = reinterpret_cast<AccN<acc_t, CPL>*>(slab + srow[k] * D + cl * CPL);
-            AccN<acc_t, CPL> v = *dst;
+          for (int k = 0; k < ROUNDS; ++k) {
+            if (srow[k] >= 0) {
+              AccN<acc_t, CPL>* dst = reinterpret_cast<AccN<acc_t, CPL>*>(slab + srow[k] * D + cl * CPL);
+              AccN<acc_t, CPL> v = *dst;
 #pragma unroll
-            for (int e = 0; e < CPL; ++e) v.v[e] += sw[k] * g[k][e];
-            *dst = v;
+              for (int c = 0; c < CPL; ++c) v.v[c] += sw[k] * g[k][c];
+              *dst = v;
+            }
           }
-        }
-      } else {
-        for (int c = lane; c < D; c += 64) {
-          acc_t g[ROUNDS];
+        } else {
+          for (int c = lane; c < D; c += 64) {
+            acc_t g[ROUNDS];
 #pragma unroll
-          for (int k = 0; k < ROUNDS; ++k) g[k] = to_acc(gb[sq[k] * qstride_g + c]);
+            for (int k = 0; k < ROUNDS; ++k) g[k] = to_acc(gb[sq[k] * qstride_g + c]);
 #pragma unroll
-          for (int k = 0; k < ROUNDS; ++k)
-            if (srow[k] >= 0) slab[srow[k] * D + c] += sw[k] * g[k];
+            for (int k = 0; k < ROUNDS; ++k)
+              if (srow[k] >= 0) slab[srow[k] * D + c] += sw[k] * g[k];
+          }
         }
       }
     }
+    __syncthreads();
+    if (threadIdx.x == 0) *q_cnt = 0;
+    __syncthreads();
   }
-  __syncthreads();
+
   scalar_t* __restrict__ dst = gval + ((b * S + lv.start[l] + r0) * M + m) * (long long)D;
   const long long rowstride = (long long)M * D;
-  for (int i = threadIdx.x * CPL; i < nrows * D; i += blockDim.x * CPL) {
+  for (int i = threadIdx.x * CPL; i < nrows * D; i += kGvThreads * CPL) {
     const int row = i / D, c = i - row * D;
     if constexpr (CPL > 1) {
       acc_t v[CPL];
@@ -473,7 +523,7 @@ __global__ __launch_bounds__(256) void msda_gvalue_kernel(
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
-constexpr long long kSlabBytes = 48 * 1024;  // LDS per grad_value workgroup (3 per CU)
+constexpr long long kSlabBytes = 32 * 1024;  // grad_value LDS slab per workgroup (+ queue: ~56 KB, 2 per CU)
 
 struct Problem {
   long long B, S, M, D, Lq, L, P;
@@ -597,14 +647,14 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
   rp.cum[0] = 0;
   for (int l = 0; l < pr.L; ++l) rp.cum[l + 1] = rp.cum[l] + (pr.lv.T[l] + rp.rows - 1) / rp.rows;
   const long long blocks = pr.B * pr.M * rp.cum[pr.L];
-  const size_t lds = (size_t)rp.rows * row_bytes;
+  const size_t lds = (size_t)rp.rows * row_bytes + (size_t)kGvQueue * (2 * sizeof(int) + sizeof(acc_t)) + 16;
   auto* lc = static_cast<const coord_t*>(loc);
   auto* a = static_cast<const coord_t*>(aw);
   auto* g = static_cast<const scalar_t*>(gout);
   auto* gv = static_cast<scalar_t*>(gval);
 #define MSDA_GV(Z, NS)                                                                          \
   hipLaunchKernelGGL((msda_gvalue_kernel<scalar_t, coord_t, Z, NS>), dim3((unsigned)blocks),    \
-                     dim3(256), lds, st, lc, a, g, gv, pr.lv, rp, (int)pr.L, (int)pr.P,         \
+                     dim3(kGvThreads), lds, st, lc, a, g, gv, pr.lv, rp, (int)pr.L, (int)pr.P,         \
                      (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq)
   // slots per instruction for 16-byte lanes: NSLOT = 64 / (D / CPL) when that is a power of 2
   constexpr int CPL = 16 / (int)sizeof(acc_t);
