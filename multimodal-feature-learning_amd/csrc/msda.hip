@@ -346,14 +346,17 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
   constexpr int LPR = 64 / NS;                                   // lanes per slot
   constexpr int ROUNDS = 8;  // slot-rounds whose grad_out loads are in flight together
 
-  // LDS: [slab rows*D acc_t][queue: q int, rowl int, w acc_t][queue counter]
+  // LDS: [slab rows*D acc_t][queue w acc_t][queue q int][queue row int]
+  //      [per-wave round tables: w acc_t x 4*64][q|row int x 4*64][queue counter]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int rows_cap = rp.rows;
   acc_t* slab = reinterpret_cast<acc_t*>(smem_raw);
-  int* q_q = reinterpret_cast<int*>(smem_raw + (size_t)rows_cap * D * sizeof(acc_t));
+  acc_t* q_w = slab + (size_t)rows_cap * D;
+  acc_t* t_w = q_w + kGvQueue;
+  int* q_q = reinterpret_cast<int*>(t_w + 4 * 64);
   int* q_row = q_q + kGvQueue;
-  acc_t* q_w = reinterpret_cast<acc_t*>(q_row + kGvQueue);
-  int* q_cnt = reinterpret_cast<int*>(q_w + kGvQueue);
+  int* t_qr = q_row + kGvQueue;
+  int* q_cnt = t_qr + 4 * 64;
 
   const int nr = rp.cum[L];
   const int r = (int)(blockIdx.x % (unsigned)nr);
@@ -432,9 +435,15 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
     __syncthreads();
     const int n = *q_cnt;
     // ---- phase B: wave w applies the entries whose row it owns ((row & 3) == w) ----
+    // Per group of 64 queue entries: each owned entry gets slot = (row/4) % NS and its rank
+    // among the wave's entries of that slot (mbcnt), and parks (q|row, w) in this wave's
+    // [rank][slot] table; round k then has the lanes of slot s read table entry [k][s]
+    // (an LDS broadcast) — no serial pop loop.  Rows of one round are distinct by slot.
+    int* tqr = t_qr + wave * 64;
+    acc_t* tw = t_w + wave * 64;
     for (int e0 = 0; e0 < n; e0 += 64) {
       const int e = e0 + lane;
-      int eq = 0, er = 0;
+      int er = 0, eq = 0;
       acc_t ew = (acc_t)0;
       bool mine = false;
       if (e < n) {
@@ -443,37 +452,35 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
         eq = q_q[e];
         ew = q_w[e];
       }
-      unsigned long long mk[NS];
+      const int es = (er >> 2) % NS;
+      int cnt_my = 0, rank = 0, nrounds = 0;
 #pragma unroll
-      for (int sl = 0; sl < NS; ++sl) mk[sl] = __ballot(mine && ((er >> 2) % NS) == sl);
-      unsigned long long any = 0;
-#pragma unroll
-      for (int sl = 0; sl < NS; ++sl) any |= mk[sl];
-      while (any) {
+      for (int sl = 0; sl < NS; ++sl) {
+        const unsigned long long mk = __ballot(mine && es == sl);
+        const int c = __popcll(mk);
+        nrounds = c > nrounds ? c : nrounds;
+        if (slot == sl) cnt_my = c;
+        if (es == sl)
+          rank = __builtin_amdgcn_mbcnt_hi((unsigned)(mk >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk, 0u));
+      }
+      if (nrounds == 0) continue;
+      if (mine) {
+        tqr[rank * NS + es] = (eq << 12) | er;  // row < 4096, q < 2^19 (checked on the host)
+        tw[rank * NS + es] = ew;
+      }
+      for (int k0 = 0; k0 < nrounds; k0 += ROUNDS) {
         int srow[ROUNDS], sq[ROUNDS];
         acc_t sw[ROUNDS];
 #pragma unroll
         for (int k = 0; k < ROUNDS; ++k) {
-          int my_j = 0;
-          bool my_have = false;
-#pragma unroll
-          for (int sl = 0; sl < NS; ++sl) {
-            const bool hv = mk[sl] != 0ull;
-            const int j = hv ? __builtin_ctzll(mk[sl]) : 0;
-            if (hv) mk[sl] &= mk[sl] - 1;
-            if (slot == sl) { my_j = j; my_have = hv; }
-          }
-          // every lane executes the bpermutes (a masked-off source lane would read as 0)
-          const int qj = __shfl(eq, my_j);
-          const int rj = __shfl(er, my_j);
-          const acc_t wj = __shfl(ew, my_j);
-          sq[k] = my_have ? qj : 0;
-          srow[k] = my_have ? rj : -1;
-          sw[k] = my_have ? wj : (acc_t)0;
+          const bool v = k0 + k < cnt_my;
+          const int idx = v ? (k0 + k) * NS + slot : 0;
+          const int qr = tqr[idx];
+          const acc_t w = tw[idx];
+          sq[k] = v ? (qr >> 12) : 0;
+          srow[k] = v ? (qr & 4095) : -1;
+          sw[k] = v ? w : (acc_t)0;
         }
-        any = 0;
-#pragma unroll
-        for (int sl = 0; sl < NS; ++sl) any |= mk[sl];
         if constexpr (NSLOT > 0) {
           acc_t g[ROUNDS][CPL];
 #pragma unroll
@@ -647,7 +654,12 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
   rp.cum[0] = 0;
   for (int l = 0; l < pr.L; ++l) rp.cum[l + 1] = rp.cum[l] + (pr.lv.T[l] + rp.rows - 1) / rp.rows;
   const long long blocks = pr.B * pr.M * rp.cum[pr.L];
-  const size_t lds = (size_t)rp.rows * row_bytes + (size_t)kGvQueue * (2 * sizeof(int) + sizeof(acc_t)) + 16;
+  const size_t lds = (size_t)rp.rows * row_bytes + (size_t)(kGvQueue + 256) * (sizeof(int) + sizeof(acc_t)) +
+                     (size_t)kGvQueue * sizeof(int) + 16;
+  if (rp.rows > 4096 || pr.Lq >= (1 << 19)) {  // packing of (q, row) in the round tables
+    set_error("msda_hip_backward: num_query=%lld too large for the grad_value kernel", pr.Lq);
+    return MSDA_ERR_ARG;
+  }
   auto* lc = static_cast<const coord_t*>(loc);
   auto* a = static_cast<const coord_t*>(aw);
   auto* g = static_cast<const scalar_t*>(gout);
