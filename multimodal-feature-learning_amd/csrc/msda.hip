@@ -437,8 +437,9 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
     // ---- phase B: wave w applies the entries whose row it owns ((row & 3) == w) ----
     // Per group of 64 queue entries: each owned entry gets slot = (row/4) % NS and its rank
     // among the wave's entries of that slot (mbcnt), and parks (q|row, w) in this wave's
-    // [rank][slot] table; round k then has the lanes of slot s read table entry [k][s]
-    // (an LDS broadcast) — no serial pop loop.  Rows of one round are distinct by slot.
+    // 64-entry table at base_slot + rank (slots packed back to back); round k then has the
+    // lanes of slot s read entry base_s + k (an LDS broadcast) — no serial pop loop.
+    // Rows of one round are distinct because their slots are.
     int* tqr = t_qr + wave * 64;
     acc_t* tw = t_w + wave * 64;
     for (int e0 = 0; e0 < n; e0 += 64) {
@@ -453,20 +454,24 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
         ew = q_w[e];
       }
       const int es = (er >> 2) % NS;
-      int cnt_my = 0, rank = 0, nrounds = 0;
+      // compact table: slot s occupies [base_s, base_s + count_s), sum of counts <= 64
+      int cnt_my = 0, my_base = 0, rank = 0, ebase = 0, nrounds = 0, acc_base = 0;
 #pragma unroll
       for (int sl = 0; sl < NS; ++sl) {
         const unsigned long long mk = __ballot(mine && es == sl);
         const int c = __popcll(mk);
         nrounds = c > nrounds ? c : nrounds;
-        if (slot == sl) cnt_my = c;
-        if (es == sl)
+        if (slot == sl) { cnt_my = c; my_base = acc_base; }
+        if (es == sl) {
           rank = __builtin_amdgcn_mbcnt_hi((unsigned)(mk >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk, 0u));
+          ebase = acc_base;
+        }
+        acc_base += c;
       }
       if (nrounds == 0) continue;
       if (mine) {
-        tqr[rank * NS + es] = (eq << 12) | er;  // row < 4096, q < 2^19 (checked on the host)
-        tw[rank * NS + es] = ew;
+        tqr[ebase + rank] = (eq << 12) | er;  // row < 4096, q < 2^19 (checked on the host)
+        tw[ebase + rank] = ew;
       }
       for (int k0 = 0; k0 < nrounds; k0 += ROUNDS) {
         int srow[ROUNDS], sq[ROUNDS];
@@ -474,7 +479,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
 #pragma unroll
         for (int k = 0; k < ROUNDS; ++k) {
           const bool v = k0 + k < cnt_my;
-          const int idx = v ? (k0 + k) * NS + slot : 0;
+          const int idx = v ? my_base + k0 + k : 0;  // < 64
           const int qr = tqr[idx];
           const acc_t w = tw[idx];
           sq[k] = v ? (qr >> 12) : 0;
@@ -530,7 +535,8 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
-constexpr long long kSlabBytes = 32 * 1024;  // grad_value LDS slab per workgroup (+ queue: ~56 KB, 2 per CU)
+constexpr long long kSlabBytes = 32 * 1024;  // grad_value LDS slab per workgroup (+ queue: ~58 KB, 2 per CU)
+constexpr long long kLdsLimit = 64 * 1024;   // dynamic LDS per workgroup we allow ourselves
 
 struct Problem {
   long long B, S, M, D, Lq, L, P;
@@ -642,20 +648,23 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
                    int pad, hipStream_t st) {
   using acc_t = typename AccOf<scalar_t>::type;
   if (pr.B * pr.M * pr.S * pr.D == 0) return MSDA_OK;
+  // LDS = slab (rows x D acc) + queue / round tables; stay within 64 KB per workgroup
   const long long row_bytes = pr.D * (long long)sizeof(acc_t);
-  if (row_bytes > kSlabBytes) {
+  const long long overhead = (long long)(kGvQueue + 256) * (sizeof(int) + sizeof(acc_t)) +
+                             (long long)kGvQueue * sizeof(int) + 16;
+  const long long slab_budget = min(kSlabBytes, kLdsLimit - overhead);
+  if (row_bytes > slab_budget) {
     set_error("msda_hip_backward: channels=%lld too large for the LDS grad_value slab", pr.D);
     return MSDA_ERR_ARG;
   }
   int maxT = 1;
   for (int l = 0; l < pr.L; ++l) maxT = max(maxT, pr.lv.T[l]);
   RangePlan rp;
-  rp.rows = (int)min((long long)maxT, kSlabBytes / row_bytes);
+  rp.rows = (int)min((long long)maxT, slab_budget / row_bytes);
   rp.cum[0] = 0;
   for (int l = 0; l < pr.L; ++l) rp.cum[l + 1] = rp.cum[l] + (pr.lv.T[l] + rp.rows - 1) / rp.rows;
   const long long blocks = pr.B * pr.M * rp.cum[pr.L];
-  const size_t lds = (size_t)rp.rows * row_bytes + (size_t)(kGvQueue + 256) * (sizeof(int) + sizeof(acc_t)) +
-                     (size_t)kGvQueue * sizeof(int) + 16;
+  const size_t lds = (size_t)(rp.rows * row_bytes + overhead);
   if (rp.rows > 4096 || pr.Lq >= (1 << 19)) {  // packing of (q, row) in the round tables
     set_error("msda_hip_backward: num_query=%lld too large for the grad_value kernel", pr.Lq);
     return MSDA_ERR_ARG;

@@ -12,15 +12,19 @@ step() {  # name timeout cmd...
   local rc=$?
   echo "rc=$rc"; tail -n 25 "gpurun_out/$name.log"
   if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)"; exit $rc; fi
+  if [ "$name" = smoke ] && [ $rc -ne 0 ]; then echo "STOP: smoke failed"; exit 1; fi
   return 0
 }
 MODE=${1:-all}
 if [ "$MODE" = all ] || [ "$MODE" = tests ]; then
-  step pytest_gpu 900 python -m pytest tests -m gpu -x -q
-  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step smoke 180 python -u -c "import __graft_entry__ as g; g.smoke()"
+  step pytest_gpu 480 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider
+fi
+if [ "$MODE" = micro ]; then
+  step micro 300 python -u tools/msda_microbench.py ${MICRO_ARGS:-}
 fi
 if [ "$MODE" = all ] || [ "$MODE" = bench ]; then
-  step bench 900 python bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-3}
-  step rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0
+  step bench 600 python -u bench.py --steps ${STEPS:-10} --warmup ${WARMUP:-3}
+  step rocprof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --cpu-baseline 0
   find gpurun_out/prof -name "*kernel_stats.csv" | head -3
 fi
