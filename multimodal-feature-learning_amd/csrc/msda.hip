@@ -333,6 +333,7 @@ constexpr int kGvThreads = 256;
 constexpr int kGvSampPerThread = 4;                             // samples per thread per step
 constexpr int kGvStep = kGvThreads * kGvSampPerThread;          // samples scanned per step
 constexpr int kGvQueue = 2 * kGvStep;                           // <= 2 taps per sample
+constexpr int kGvSlotCap = 64;                                  // entries per (wave, slot) table
 
 template <typename scalar_t, typename coord_t, bool ZEROS, int NSLOT>
 __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
@@ -344,19 +345,19 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
   constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(acc_t) : 1;  // channels per lane
   constexpr int NS = NSLOT > 0 ? NSLOT : 1;
   constexpr int LPR = 64 / NS;                                   // lanes per slot
-  constexpr int ROUNDS = 8;  // slot-rounds whose grad_out loads are in flight together
+  constexpr int ROUNDS = 16;  // slot-rounds whose grad_out loads are in flight together
 
   // LDS: [slab rows*D acc_t][queue w acc_t][queue q int][queue row int]
-  //      [per-wave round tables: w acc_t x 4*64][q|row int x 4*64][queue counter]
+  //      [per-wave slot tables: w acc_t x 4*NS*cap][q|row int x 4*NS*cap][queue counter]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int rows_cap = rp.rows;
   acc_t* slab = reinterpret_cast<acc_t*>(smem_raw);
   acc_t* q_w = slab + (size_t)rows_cap * D;
   acc_t* t_w = q_w + kGvQueue;
-  int* q_q = reinterpret_cast<int*>(t_w + 4 * 64);
+  int* q_q = reinterpret_cast<int*>(t_w + 4 * NS * kGvSlotCap);
   int* q_row = q_q + kGvQueue;
   int* t_qr = q_row + kGvQueue;
-  int* q_cnt = t_qr + 4 * 64;
+  int* q_cnt = t_qr + 4 * NS * kGvSlotCap;
 
   const int nr = rp.cum[L];
   const int r = (int)(blockIdx.x % (unsigned)nr);
@@ -388,6 +389,61 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
   const int nsamp = Lq * P;
   const int slot = lane / LPR;
   const int cl = lane - slot * LPR;
+
+  // per-wave slot tables: tw / tqr [NS][kGvSlotCap]; counts are wave-uniform
+  int* tqr = t_qr + wave * (NS * kGvSlotCap);
+  acc_t* tw = t_w + wave * (NS * kGvSlotCap);
+  int tcnt[NS];
+#pragma unroll
+  for (int sl = 0; sl < NS; ++sl) tcnt[sl] = 0;
+  auto flush = [&]() {
+    int nr = 0, my_cnt = 0;
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) {
+      nr = tcnt[sl] > nr ? tcnt[sl] : nr;
+      if (slot == sl) my_cnt = tcnt[sl];
+    }
+    for (int k0 = 0; k0 < nr; k0 += ROUNDS) {
+      int srow[ROUNDS], sq[ROUNDS];
+      acc_t sw[ROUNDS];
+#pragma unroll
+      for (int k = 0; k < ROUNDS; ++k) {
+        const bool v = k0 + k < my_cnt;
+        const int idx = slot * kGvSlotCap + (v ? k0 + k : 0);
+        const int qr = tqr[idx];
+        const acc_t w = tw[idx];
+        sq[k] = v ? (qr >> 12) : 0;
+        srow[k] = v ? (qr & 4095) : -1;
+        sw[k] = v ? w : (acc_t)0;
+      }
+      if constexpr (NSLOT > 0) {
+        acc_t g[ROUNDS][CPL];
+#pragma unroll
+        for (int k = 0; k < ROUNDS; ++k) load_vec<scalar_t, CPL>(gb + sq[k] * qstride_g + cl * CPL, g[k]);
+#pragma unroll
+        for (int k = 0; k < ROUNDS; ++k) {
+          if (srow[k] >= 0) {
+            AccN<acc_t, CPL>* dst = reinterpret_cast<AccN<acc_t, CPL>*>(slab + srow[k] * D + cl * CPL);
+            AccN<acc_t, CPL> v = *dst;
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) v.v[c] += sw[k] * g[k][c];
+            *dst = v;
+          }
+        }
+      } else {
+        for (int c = lane; c < D; c += 64) {
+          acc_t g[ROUNDS];
+#pragma unroll
+          for (int k = 0; k < ROUNDS; ++k) g[k] = to_acc(gb[sq[k] * qstride_g + c]);
+#pragma unroll
+          for (int k = 0; k < ROUNDS; ++k)
+            if (srow[k] >= 0) slab[srow[k] * D + c] += sw[k] * g[k];
+        }
+      }
+    }
+#pragma unroll
+    for (int sl = 0; sl < NS; ++sl) tcnt[sl] = 0;
+  };
 
   for (int base = 0; base < nsamp; base += kGvStep) {
     // ---- phase A: the whole workgroup scans kGvStep samples (loads issued together) ----
@@ -434,14 +490,10 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
     }
     __syncthreads();
     const int n = *q_cnt;
-    // ---- phase B: wave w applies the entries whose row it owns ((row & 3) == w) ----
-    // Per group of 64 queue entries: each owned entry gets slot = (row/4) % NS and its rank
-    // among the wave's entries of that slot (mbcnt), and parks (q|row, w) in this wave's
-    // 64-entry table at base_slot + rank (slots packed back to back); round k then has the
-    // lanes of slot s read entry base_s + k (an LDS broadcast) — no serial pop loop.
-    // Rows of one round are distinct because their slots are.
-    int* tqr = t_qr + wave * 64;
-    acc_t* tw = t_w + wave * 64;
+    // ---- phase B: wave w moves the entries whose row it owns ((row & 3) == w) into its
+    // per-slot tables (slot = (row/4) % NS, kGvSlotCap entries each); a table that would
+    // overflow is first drained by flush().  Tables persist across steps (the slab rows are
+    // private to the wave), so drains run in long batches with ROUNDS loads in flight.
     for (int e0 = 0; e0 < n; e0 += 64) {
       const int e = e0 + lane;
       int er = 0, eq = 0;
@@ -454,68 +506,33 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
         ew = q_w[e];
       }
       const int es = (er >> 2) % NS;
-      // compact table: slot s occupies [base_s, base_s + count_s), sum of counts <= 64
-      int cnt_my = 0, my_base = 0, rank = 0, ebase = 0, nrounds = 0, acc_base = 0;
+      unsigned long long mk[NS];
+      bool full = false;
 #pragma unroll
       for (int sl = 0; sl < NS; ++sl) {
-        const unsigned long long mk = __ballot(mine && es == sl);
-        const int c = __popcll(mk);
-        nrounds = c > nrounds ? c : nrounds;
-        if (slot == sl) { cnt_my = c; my_base = acc_base; }
-        if (es == sl) {
-          rank = __builtin_amdgcn_mbcnt_hi((unsigned)(mk >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk, 0u));
-          ebase = acc_base;
-        }
-        acc_base += c;
+        mk[sl] = __ballot(mine && es == sl);
+        full |= tcnt[sl] + __popcll(mk[sl]) > kGvSlotCap;
       }
-      if (nrounds == 0) continue;
+      if (full) flush();
       if (mine) {
-        tqr[ebase + rank] = (eq << 12) | er;  // row < 4096, q < 2^19 (checked on the host)
-        tw[ebase + rank] = ew;
+        int pos = 0;
+#pragma unroll
+        for (int sl = 0; sl < NS; ++sl)
+          if (es == sl)
+            pos = sl * kGvSlotCap + tcnt[sl] +
+                  __builtin_amdgcn_mbcnt_hi((unsigned)(mk[sl] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk[sl], 0u));
+        tqr[pos] = (eq << 12) | er;  // row < 4096, q < 2^19 (checked on the host)
+        tw[pos] = ew;
       }
-      for (int k0 = 0; k0 < nrounds; k0 += ROUNDS) {
-        int srow[ROUNDS], sq[ROUNDS];
-        acc_t sw[ROUNDS];
 #pragma unroll
-        for (int k = 0; k < ROUNDS; ++k) {
-          const bool v = k0 + k < cnt_my;
-          const int idx = v ? my_base + k0 + k : 0;  // < 64
-          const int qr = tqr[idx];
-          const acc_t w = tw[idx];
-          sq[k] = v ? (qr >> 12) : 0;
-          srow[k] = v ? (qr & 4095) : -1;
-          sw[k] = v ? w : (acc_t)0;
-        }
-        if constexpr (NSLOT > 0) {
-          acc_t g[ROUNDS][CPL];
-#pragma unroll
-          for (int k = 0; k < ROUNDS; ++k) load_vec<scalar_t, CPL>(gb + sq[k] * qstride_g + cl * CPL, g[k]);
-#pragma unroll
-          for (int k = 0; k < ROUNDS; ++k) {
-            if (srow[k] >= 0) {
-              AccN<acc_t, CPL>* dst = reinterpret_cast<AccN<acc_t, CPL>*>(slab + srow[k] * D + cl * CPL);
-              AccN<acc_t, CPL> v = *dst;
-#pragma unroll
-              for (int c = 0; c < CPL; ++c) v.v[c] += sw[k] * g[k][c];
-              *dst = v;
-            }
-          }
-        } else {
-          for (int c = lane; c < D; c += 64) {
-            acc_t g[ROUNDS];
-#pragma unroll
-            for (int k = 0; k < ROUNDS; ++k) g[k] = to_acc(gb[sq[k] * qstride_g + c]);
-#pragma unroll
-            for (int k = 0; k < ROUNDS; ++k)
-              if (srow[k] >= 0) slab[srow[k] * D + c] += sw[k] * g[k];
-          }
-        }
-      }
+      for (int sl = 0; sl < NS; ++sl) tcnt[sl] += __popcll(mk[sl]);
     }
     __syncthreads();
     if (threadIdx.x == 0) *q_cnt = 0;
     __syncthreads();
   }
+  flush();
+  __syncthreads();
 
   scalar_t* __restrict__ dst = gval + ((b * S + lv.start[l] + r0) * M + m) * (long long)D;
   const long long rowstride = (long long)M * D;
@@ -648,9 +665,16 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
                    int pad, hipStream_t st) {
   using acc_t = typename AccOf<scalar_t>::type;
   if (pr.B * pr.M * pr.S * pr.D == 0) return MSDA_OK;
-  // LDS = slab (rows x D acc) + queue / round tables; stay within 64 KB per workgroup
+  // slots per instruction for 16-byte lanes: NSLOT = 64 / (D / CPL) when that is a power of 2
+  constexpr int CPL = 16 / (int)sizeof(acc_t);
+  int ns = 0;
+  if (pr.D % CPL == 0 && pr.D / CPL <= 64 && 64 % (pr.D / CPL) == 0) ns = (int)(64 / (pr.D / CPL));
+  if (ns > 16) ns = 0;  // tiny heads: generic path
+  const int ns_eff = ns > 0 ? ns : 1;
+  // LDS = slab (rows x D acc) + queue + slot tables; stay within 64 KB per workgroup
   const long long row_bytes = pr.D * (long long)sizeof(acc_t);
-  const long long overhead = (long long)(kGvQueue + 256) * (sizeof(int) + sizeof(acc_t)) +
+  const long long table = 4LL * ns_eff * kGvSlotCap;
+  const long long overhead = (long long)(kGvQueue + table) * (sizeof(int) + sizeof(acc_t)) +
                              (long long)kGvQueue * sizeof(int) + 16;
   const long long slab_budget = min(kSlabBytes, kLdsLimit - overhead);
   if (row_bytes > slab_budget) {
@@ -665,7 +689,7 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
   for (int l = 0; l < pr.L; ++l) rp.cum[l + 1] = rp.cum[l] + (pr.lv.T[l] + rp.rows - 1) / rp.rows;
   const long long blocks = pr.B * pr.M * rp.cum[pr.L];
   const size_t lds = (size_t)(rp.rows * row_bytes + overhead);
-  if (rp.rows > 4096 || pr.Lq >= (1 << 19)) {  // packing of (q, row) in the round tables
+  if (rp.rows > 4096 || pr.Lq >= (1 << 19)) {  // packing of (q, row) in the slot tables
     set_error("msda_hip_backward: num_query=%lld too large for the grad_value kernel", pr.Lq);
     return MSDA_ERR_ARG;
   }
@@ -677,11 +701,6 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
   hipLaunchKernelGGL((msda_gvalue_kernel<scalar_t, coord_t, Z, NS>), dim3((unsigned)blocks),    \
                      dim3(kGvThreads), lds, st, lc, a, g, gv, pr.lv, rp, (int)pr.L, (int)pr.P,         \
                      (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq)
-  // slots per instruction for 16-byte lanes: NSLOT = 64 / (D / CPL) when that is a power of 2
-  constexpr int CPL = 16 / (int)sizeof(acc_t);
-  int ns = 0;
-  if (pr.D % CPL == 0 && pr.D / CPL <= 64 && 64 % (pr.D / CPL) == 0) ns = (int)(64 / (pr.D / CPL));
-  if (ns > 16) ns = 0;  // tiny heads: generic path
   const bool z = pad == MSDA_PAD_ZEROS;
   switch (ns) {
     case 1: if (z) MSDA_GV(true, 1); else MSDA_GV(false, 1); break;
