@@ -317,8 +317,8 @@ __global__ __launch_bounds__(256) void msda_bwd_kernel(
 //     64/NSLOT lanes (CPL channels per lane = one 16-byte ds_read/ds_write); slot =
 //     ((row - r0) / 4) % NSLOT, so the rows of one instruction are always distinct, and
 //     later rounds of the same slot are ordered by the wave's in-order LDS pipe.
-// NSLOT = 0 is the generic path (any channel count): one contribution per round, lane =
-// channel, 4-byte (8 for fp64) RMW.
+// NSLOT (1, 2 or 4) needs D % CPL == 0 and D <= 64/NSLOT*CPL; NSLOT = 0 is the generic
+// path (any channel count): one contribution per round, lane = channel, 4/8-byte RMW.
 struct RangePlan {
   int rows;                      // rows per workgroup
   int cum[MSDA_MAX_LEVELS + 1];  // prefix sum over levels of ceil(T_l / rows)
@@ -417,12 +417,15 @@ __global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
         sw[k] = v ? w : (acc_t)0;
       }
       if constexpr (NSLOT > 0) {
+        const bool lane_on = cl * CPL < D;  // narrow heads leave the slot's upper lanes idle
         acc_t g[ROUNDS][CPL];
 #pragma unroll
-        for (int k = 0; k < ROUNDS; ++k) load_vec<scalar_t, CPL>(gb + sq[k] * qstride_g + cl * CPL, g[k]);
+        for (int k = 0; k < ROUNDS; ++k) {
+          if (lane_on) load_vec<scalar_t, CPL>(gb + sq[k] * qstride_g + cl * CPL, g[k]);
+        }
 #pragma unroll
         for (int k = 0; k < ROUNDS; ++k) {
-          if (srow[k] >= 0) {
+          if (srow[k] >= 0 && lane_on) {
             AccN<acc_t, CPL>* dst = reinterpret_cast<AccN<acc_t, CPL>*>(slab + srow[k] * D + cl * CPL);
             AccN<acc_t, CPL> v = *dst;
 #pragma unroll
@@ -667,9 +670,14 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
   if (pr.B * pr.M * pr.S * pr.D == 0) return MSDA_OK;
   // slots per instruction for 16-byte lanes: NSLOT = 64 / (D / CPL) when that is a power of 2
   constexpr int CPL = 16 / (int)sizeof(acc_t);
+  // (at most 4 slots: a slot's table must hold a whole 64-entry group; lanes whose chunk
+  //  is past D idle for narrow heads)
   int ns = 0;
-  if (pr.D % CPL == 0 && pr.D / CPL <= 64 && 64 % (pr.D / CPL) == 0) ns = (int)(64 / (pr.D / CPL));
-  if (ns > 16) ns = 0;  // tiny heads: generic path
+  if (pr.D % CPL == 0) {
+    if (pr.D <= 16 * CPL) ns = 4;
+    else if (pr.D <= 32 * CPL) ns = 2;
+    else if (pr.D <= 64 * CPL) ns = 1;
+  }
   const int ns_eff = ns > 0 ? ns : 1;
   // LDS = slab (rows x D acc) + queue + slot tables; stay within 64 KB per workgroup
   const long long row_bytes = pr.D * (long long)sizeof(acc_t);
@@ -706,8 +714,6 @@ int run_grad_value(const Problem& pr, const void* loc, const void* aw, const voi
     case 1: if (z) MSDA_GV(true, 1); else MSDA_GV(false, 1); break;
     case 2: if (z) MSDA_GV(true, 2); else MSDA_GV(false, 2); break;
     case 4: if (z) MSDA_GV(true, 4); else MSDA_GV(false, 4); break;
-    case 8: if (z) MSDA_GV(true, 8); else MSDA_GV(false, 8); break;
-    case 16: if (z) MSDA_GV(true, 16); else MSDA_GV(false, 16); break;
     default: if (z) MSDA_GV(true, 0); else MSDA_GV(false, 0); break;
   }
 #undef MSDA_GV

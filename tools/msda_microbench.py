@@ -67,6 +67,8 @@ def main():
     ap.add_argument("--dtypes", default="bf16,fp32")
     ap.add_argument("--regimes", default="init,trained,uniform")
     ap.add_argument("--B", type=int, default=8)
+    ap.add_argument("--shapes", default="enc,dec")
+    ap.add_argument("--kernels", default="fwd,bwd_loc_aw,bwd_value,bwd_all")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     shapes = [1024, 512, 256, 128]
@@ -76,6 +78,8 @@ def main():
         dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[dname]
         vb = 2 if dtype == torch.bfloat16 else 4
         for Lq, shape_name in ((S, "enc"), (100, "dec")):
+            if shape_name not in args.shapes.split(","):
+                continue
             for regime in args.regimes.split(","):
                 value, loc, aw, gout = make(regime, args.B, Lq, shapes, M, P, dtype, dev)
                 fwd_b = msda.algorithmic_bytes("fwd", args.B, S, M, D, Lq, L, P, vb)
@@ -89,6 +93,8 @@ def main():
                     "bwd_all": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout), bwd_b),
                 }
                 for name, (fn, nbytes) in runs.items():
+                    if name not in args.kernels.split(","):
+                        continue
                     us = timeit(fn, args.iters)
                     rec = {"dtype": dname, "shape": shape_name, "regime": regime, "kernel": name,
                            "us": round(us, 2)}
