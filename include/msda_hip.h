@@ -73,11 +73,13 @@ int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_
                      int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
                      int padding_mode, void* stream);
 
-/* Bytes of device scratch msda_hip_backward needs.  Always 0 since grad_value is
- * accumulated in LDS slabs owned by one workgroup each (no global atomics, no fp32
- * staging for bf16/f16); kept so callers written against ABI v1 stay valid. */
+/* Bytes of device scratch msda_hip_backward needs (ABI v2: depends on the query side).
+ * Holds the per-row tap lists of the backward's sort pass (B*M*L*2*Lq*P entries), the row
+ * table (B*M*S) and the per-tap dot products (B*Lq*M*L*P*2); no floating-point atomics
+ * are used, so the backward is bitwise reproducible. */
 size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,
-                                         int64_t num_heads, int64_t channels);
+                                         int64_t num_heads, int64_t channels, int64_t num_query,
+                                         int64_t num_levels, int64_t num_point);
 
 /* Backward.  Replaces ms_deform_attn_cuda_backward
  * (reference: models/ops/src/cuda/ms_deform_attn_cuda.cu:83-153) and the autograd
@@ -86,7 +88,7 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
  *   grad_value     (batch, spatial_size, num_heads, channels)    value_dtype (overwritten)
  *   grad_loc       (batch, num_query, num_heads, num_levels, num_point)  coord dtype (overwritten)
  *   grad_attn      (batch, num_query, num_heads, num_levels, num_point)  coord dtype (overwritten)
- *   workspace      msda_hip_backward_workspace_bytes(...) bytes of device memory (may be NULL)
+ *   workspace      msda_hip_backward_workspace_bytes(...) bytes of device memory, 256-B aligned
  * Any of grad_value / grad_loc / grad_attn may be NULL to skip it.
  * BORDER mode: grad_loc is 0 where loc*T_l-0.5 is clamped (<=0 or >=T_l-1), exactly
  * as ATen's clip_coordinates_set_grad treats the border as out of bounds. */

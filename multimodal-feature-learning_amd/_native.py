@@ -18,7 +18,7 @@ LIB_PATH = os.path.join(LIB_DIR, "libmsda_hip.so")
 DTYPE_TAGS = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2, torch.float16: 3}
 PAD_TAGS = {"border": 0, "zeros": 1}
 MAX_LEVELS = 16
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # every symbol include/msda_hip.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
@@ -43,7 +43,7 @@ def _declare(lib):
     lib.msda_hip_backward.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp, vp, vp, vp,
                                       i64, i64, i64, i64, i64, i64, i32, vp]
     lib.msda_hip_backward_workspace_bytes.restype = ctypes.c_size_t
-    lib.msda_hip_backward_workspace_bytes.argtypes = [i32, i64, i64, i64, i64]
+    lib.msda_hip_backward_workspace_bytes.argtypes = [i32, i64, i64, i64, i64, i64, i64, i64]
     lib.msda_hip_last_error.restype = ctypes.c_char_p
     lib.msda_hip_last_error.argtypes = []
     lib.msda_hip_abi_version.restype = i32

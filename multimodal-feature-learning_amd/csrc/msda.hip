@@ -237,326 +237,271 @@ __global__ __launch_bounds__(256) void msda_fwd_kernel(
 // ---------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------
-template <typename scalar_t, typename coord_t, int VEC, bool ZEROS>
-__global__ __launch_bounds__(256) void msda_bwd_kernel(
-    const scalar_t* __restrict__ value, const coord_t* __restrict__ loc,
-    const coord_t* __restrict__ aw, const scalar_t* __restrict__ gout,
-    coord_t* __restrict__ gloc, coord_t* __restrict__ gaw,
-    const Levels lv, const int L, const int P, const int S, const int M, const int D,
-    const int Lq, const long long n_items, const int gshift) {
-  using acc_t = typename AccOf<scalar_t>::type;
-  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long item_raw = tid >> gshift;
-  // every lane stays alive for the butterfly reductions below
-  const bool active = item_raw < n_items;
-  const long long item = active ? item_raw : 0;
-  const int G = 1 << gshift;
-  const int lg = (int)(tid & (G - 1));
-  const int m = (int)(item % M);
-  const long long b = item / M / Lq;
-  const long long rowstride = (long long)M * D;
-  const coord_t* __restrict__ locp = loc + item * (L * P);
-  const coord_t* __restrict__ awp = aw + item * (L * P);
-  const long long vrow0 = (b * S * M + m) * (long long)D;
-  const scalar_t* __restrict__ vb = value + vrow0;
-  const scalar_t* __restrict__ gp = gout + item * D;
-  const int nchunk = D / VEC;
-  for (int l = 0; l < L; ++l) {
-    const int T = lv.T[l];
-    const long long lbase = (long long)lv.start[l] * rowstride;
-    for (int p = 0; p < P; ++p) {
-      const coord_t a = awp[l * P + p];
-      const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locp[l * P + p], T);
-      const acc_t w0 = (acc_t)t.w0, w1 = (acc_t)t.w1, aa = (acc_t)a;
-      acc_t pa = (acc_t)0;  // d out / d aw
-      acc_t pl = (acc_t)0;  // sum_c g * (v1 - v0)
-      if (active) {
-        for (int ck = lg; ck < nchunk; ck += G) {
-          acc_t g[VEC], v0[VEC], v1[VEC];
-          load_vec<scalar_t, VEC>(gp + ck * VEC, g);
-          load_vec<scalar_t, VEC>(vb + lbase + t.i0 * rowstride + ck * VEC, v0);
-          load_vec<scalar_t, VEC>(vb + lbase + t.i1 * rowstride + ck * VEC, v1);
+// The backward is the transpose of the forward's sparse gather.  Every tap (sample, k)
+// adds aw*w_k*grad_out[b,q,m,:] to value row (b, level_start + i_k, m) and needs the dot
+// product d_k = <grad_out[b,q,m,:], value row> for grad_aw / grad_loc.  Three kernels and
+// no floating-point atomics anywhere (ds_add_f32 measured ~12x slower than a plain LDS
+// read+write pair on gfx950, tools/lds_probe.hip; global fp32 atomics ~1.3 TB/s):
+//   1. msda_bwd_sort_kernel  — one workgroup per (b, m, level): histogram of the in-map
+//      taps per row with LDS integer atomics, exclusive scan, per-row entry lists
+//      {tap id, aw*w} (staged in LDS and written contiguously when they fit) and a row
+//      table {first entry, count}.  Entries of a row are then sorted by tap id, so every
+//      sum below has a fixed order: the backward is bitwise reproducible.
+//   2. msda_bwd_pull_kernel  — the forward's mirror: a slot of 64/NS lanes (CPL channels
+//      each, one 16-byte access per lane) per destination value row walks the row's
+//      entries, gathers grad_out rows, accumulates in registers and writes the row once;
+//      the same loop reduces each entry's dot product with the row's values (butterfly
+//      over the slot's lanes) into the per-tap buffer d.
+//   3. msda_bwd_coord_kernel — per sample: grad_aw = w0 d0 + w1 d1,
+//      grad_loc = aw * dy/dloc * (d1 - d0)   (d_k = 0 for a tap outside the map).
+template <typename coord_t>
+struct Entry {
+  int tap;    // ((q * P + p) << 1) | k
+  coord_t w;  // aw * w_k
+};
+
+constexpr int kSortThreads = 512;
+constexpr long long kSortLdsMax = 150 * 1024;  // LDS staging of a level's entry lists
+
+// exclusive scan of one value per thread over the workgroup; returns the thread's prefix,
+// *total gets the sum.  scratch: >= kSortThreads/64 + 1 ints of LDS.
+__device__ __forceinline__ int block_exclusive_scan(int x, int* scratch, int* total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = x;
 #pragma unroll
-          for (int e = 0; e < VEC; ++e) {
-            const acc_t x0 = t.ok0 ? v0[e] : (acc_t)0;
-            const acc_t x1 = t.ok1 ? v1[e] : (acc_t)0;
-            pa += g[e] * (x0 * w0 + x1 * w1);
-            pl += g[e] * (x1 - x0);
-          }
+  for (int off = 1; off < 64; off <<= 1) {
+    const int y = __shfl_up(incl, off);
+    if (lane >= off) incl += y;
+  }
+  if (lane == 63) scratch[wave] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) {
+      const int t = scratch[w];
+      scratch[w] = run;
+      run += t;
+    }
+    scratch[blockDim.x >> 6] = run;
+  }
+  __syncthreads();
+  const int res = scratch[wave] + incl - x;
+  *total = scratch[blockDim.x >> 6];
+  __syncthreads();
+  return res;
+}
+
+template <typename coord_t, bool ZEROS, bool STAGE>
+__global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
+    const coord_t* __restrict__ loc, const coord_t* __restrict__ aw, int2* __restrict__ rowinfo,
+    Entry<coord_t>* __restrict__ entries, const Levels lv, const int L, const int P, const int S,
+    const int M, const int Lq) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const int l = (int)(blockIdx.x % (unsigned)L);
+  const long long bm = blockIdx.x / (unsigned)L;
+  const int m = (int)(bm % M);
+  const long long b = bm / M;
+  const int T = lv.T[l];
+  // LDS: [stage entries (STAGE)][cursor T ints][scan scratch 16 ints]
+  const int ncap = 2 * Lq * P;
+  Entry<coord_t>* stage = reinterpret_cast<Entry<coord_t>*>(smem_raw);
+  int* cur = reinterpret_cast<int*>(smem_raw + (STAGE ? (size_t)ncap * sizeof(Entry<coord_t>) : 0));
+  int* scratch = cur + T;
+
+  for (int i = threadIdx.x; i < T; i += kSortThreads) cur[i] = 0;
+  __syncthreads();
+
+  const int LP = L * P;
+  const long long qs = (long long)M * LP;
+  const coord_t* __restrict__ locb = loc + (b * Lq * M + m) * LP + l * P;
+  const coord_t* __restrict__ awb = aw + (b * Lq * M + m) * LP + l * P;
+  const int nsamp = Lq * P;
+
+  // pass 1: taps per row
+  for (int s = threadIdx.x; s < nsamp; s += kSortThreads) {
+    const int q = s / P, p = s - (s / P) * P;
+    const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qs + p], T);
+    if (t.ok0) atomicAdd(&cur[t.i0], 1);
+    if (t.ok1) atomicAdd(&cur[t.i1], 1);
+  }
+  __syncthreads();
+
+  // exclusive scan over rows: thread i owns rows [i*chunk, (i+1)*chunk)
+  const int chunk = (T + kSortThreads - 1) / kSortThreads;
+  const int lo = min((int)threadIdx.x * chunk, T), hi = min(lo + chunk, T);
+  int mine = 0;
+  for (int i = lo; i < hi; ++i) mine += cur[i];
+  int total = 0;
+  int run = block_exclusive_scan(mine, scratch, &total);
+  const long long base = (bm * L + l) * (long long)ncap;  // this (b, m, level)'s entry region
+  int2* __restrict__ rinfo = rowinfo + bm * S + lv.start[l];
+  for (int i = lo; i < hi; ++i) {
+    const int c = cur[i];
+    rinfo[i] = make_int2((int)(base + run), c);  // base + run < 2^31 (checked on the host)
+    cur[i] = run;
+    run += c;
+  }
+  __syncthreads();
+
+  // pass 2: place the entries
+  for (int s = threadIdx.x; s < nsamp; s += kSortThreads) {
+    const int q = s / P, p = s - (s / P) * P;
+    const coord_t a = awb[q * qs + p];
+    const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qs + p], T);
+    if (t.ok0) {
+      const int pos = atomicAdd(&cur[t.i0], 1);
+      Entry<coord_t> e{(s << 1), a * t.w0};
+      if constexpr (STAGE) stage[pos] = e; else entries[base + pos] = e;
+    }
+    if (t.ok1) {
+      const int pos = atomicAdd(&cur[t.i1], 1);
+      Entry<coord_t> e{(s << 1) | 1, a * t.w1};
+      if constexpr (STAGE) stage[pos] = e; else entries[base + pos] = e;
+    }
+  }
+  __syncthreads();
+  // cur[i] now = end of row i.  Sort each row's list by tap id (insertion sort; lists are
+  // short) so the pull kernel sums in a fixed order, then write out.
+  if constexpr (STAGE) {
+    for (int i = lo; i < hi; ++i) {
+      const int e1 = cur[i], e0 = (i == 0 ? 0 : cur[i - 1]);
+      for (int x = e0 + 1; x < e1; ++x) {
+        const Entry<coord_t> key = stage[x];
+        int y = x - 1;
+        while (y >= e0 && stage[y].tap > key.tap) {
+          stage[y + 1] = stage[y];
+          --y;
         }
+        stage[y + 1] = key;
       }
-      // butterfly over the G lanes of this item (G divides 64, groups are aligned)
-      for (int off = G >> 1; off > 0; off >>= 1) {
-        pa += __shfl_xor(pa, off);
-        pl += __shfl_xor(pl, off);
-      }
-      if (active && lg == 0) {
-        const long long o = item * (L * P) + l * P + p;
-        if (gaw != nullptr) gaw[o] = (coord_t)pa;
-        if (gloc != nullptr) gloc[o] = (coord_t)(pl * aa) * t.gmul;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < total; i += kSortThreads) entries[base + i] = stage[i];
+  } else {
+    __threadfence_block();
+    for (int i = lo; i < hi; ++i) {
+      const int e1 = cur[i], e0 = (i == 0 ? 0 : cur[i - 1]);
+      for (int x = e0 + 1; x < e1; ++x) {
+        const Entry<coord_t> key = entries[base + x];
+        int y = x - 1;
+        while (y >= e0 && entries[base + y].tap > key.tap) {
+          entries[base + y + 1] = entries[base + y];
+          --y;
+        }
+        entries[base + y + 1] = key;
       }
     }
   }
 }
-
-// ---------------------------------------------------------------------------------
-// backward, grad_value: scatter through LDS with plain (non-atomic) read-modify-write
-// ---------------------------------------------------------------------------------
-// One workgroup owns rows [r0, r1) of one (b, head m, level l) slab of grad_value and keeps
-// them in LDS as fp32 (fp64 for fp64 values).  It scans every sample (q, p) of level l for
-// (b, m), recomputes the two taps and adds aw*w*grad_out[b,q,m,:] to each tap row it owns.
-// Every grad_value row has exactly one owner workgroup, so the slab is written once with
-// plain stores: no global atomics, no memset, no fp32 staging buffer for bf16/fp16.
-//
-// No LDS atomics either: ds_add_f32 measured ~81 ns per wave-op per CU on gfx950 against
-// ~7 ns for a ds_read + ds_write pair (tools/lds_probe.hip).  Races are avoided by
-// ownership instead:
-//   * wave w of the workgroup owns the rows with (row - r0) % 4 == w (both taps of a sample
-//     are adjacent rows, so they always belong to different waves);
-//   * inside a wave, NSLOT contributions are applied per instruction, one per "slot" of
-//     64/NSLOT lanes (CPL channels per lane = one 16-byte ds_read/ds_write); slot =
-//     ((row - r0) / 4) % NSLOT, so the rows of one instruction are always distinct, and
-//     later rounds of the same slot are ordered by the wave's in-order LDS pipe.
-// NSLOT (1, 2 or 4) needs D % CPL == 0 and D <= 64/NSLOT*CPL; NSLOT = 0 is the generic
-// path (any channel count): one contribution per round, lane = channel, 4/8-byte RMW.
-struct RangePlan {
-  int rows;                      // rows per workgroup
-  int cum[MSDA_MAX_LEVELS + 1];  // prefix sum over levels of ceil(T_l / rows)
-};
 
 template <typename acc_t, int N>
 struct alignas(16) AccN {
   acc_t v[N];
 };
 
-constexpr int kGvThreads = 256;
-constexpr int kGvSampPerThread = 4;                             // samples per thread per step
-constexpr int kGvStep = kGvThreads * kGvSampPerThread;          // samples scanned per step
-constexpr int kGvQueue = 2 * kGvStep;                           // <= 2 taps per sample
-constexpr int kGvSlotCap = 64;                                  // entries per (wave, slot) table
+constexpr int kPullThreads = 256;
 
-template <typename scalar_t, typename coord_t, bool ZEROS, int NSLOT>
-__global__ __launch_bounds__(kGvThreads) void msda_gvalue_kernel(
-    const coord_t* __restrict__ loc, const coord_t* __restrict__ aw,
-    const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, const Levels lv,
-    const RangePlan rp, const int L, const int P, const int S, const int M, const int D,
-    const int Lq) {
+template <typename scalar_t, typename coord_t, int NSLOT, bool NEED_D>
+__global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
+    const scalar_t* __restrict__ value, const scalar_t* __restrict__ gout,
+    const int2* __restrict__ rowinfo, const Entry<coord_t>* __restrict__ entries,
+    scalar_t* __restrict__ gval, coord_t* __restrict__ dbuf, const Levels lv, const int L,
+    const int P, const int S, const int M, const int D, const int Lq, const long long nrows) {
   using acc_t = typename AccOf<scalar_t>::type;
-  constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(acc_t) : 1;  // channels per lane
+  constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(acc_t) : 1;  // channels per lane per pass
   constexpr int NS = NSLOT > 0 ? NSLOT : 1;
-  constexpr int LPR = 64 / NS;                                   // lanes per slot
-  constexpr int ROUNDS = 16;  // slot-rounds whose grad_out loads are in flight together
-
-  // LDS: [slab rows*D acc_t][queue w acc_t][queue q int][queue row int]
-  //      [per-wave slot tables: w acc_t x 4*NS*cap][q|row int x 4*NS*cap][queue counter]
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const int rows_cap = rp.rows;
-  acc_t* slab = reinterpret_cast<acc_t*>(smem_raw);
-  acc_t* q_w = slab + (size_t)rows_cap * D;
-  acc_t* t_w = q_w + kGvQueue;
-  int* q_q = reinterpret_cast<int*>(t_w + 4 * NS * kGvSlotCap);
-  int* q_row = q_q + kGvQueue;
-  int* t_qr = q_row + kGvQueue;
-  int* q_cnt = t_qr + 4 * NS * kGvSlotCap;
-
-  const int nr = rp.cum[L];
-  const int r = (int)(blockIdx.x % (unsigned)nr);
-  const long long bm = blockIdx.x / (unsigned)nr;
+  constexpr int LPR = 64 / NS;                                   // lanes per slot (row)
+  constexpr int U = 4;                                           // entries in flight per slot
+  const int lane = threadIdx.x & 63;
+  const int slot = lane / LPR;
+  const int cl = lane - slot * LPR;
+  const long long wave_id = ((long long)blockIdx.x * kPullThreads + threadIdx.x) >> 6;
+  const long long row = wave_id * NS + slot;  // (b, m, s) flattened as (b*M + m)*S + s
+  const bool valid = row < nrows;
+  const long long rr = valid ? row : 0;
+  const int s = (int)(rr % S);
+  const long long bm = rr / S;
   const int m = (int)(bm % M);
   const long long b = bm / M;
   int l = 0;
-  while (r >= rp.cum[l + 1]) ++l;
-  const int T = lv.T[l];
-  const int r0 = (r - rp.cum[l]) * rp.rows;
-  const int r1 = min(r0 + rp.rows, T);
-  const int nrows = r1 - r0;
-
-  for (int i = threadIdx.x * CPL; i < nrows * D; i += kGvThreads * CPL) {
-#pragma unroll
-    for (int e = 0; e < CPL; ++e) slab[i + e] = (acc_t)0;
-  }
-  if (threadIdx.x == 0) *q_cnt = 0;
-  __syncthreads();
-
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int LP = L * P;
-  const long long qstride_c = (long long)M * LP;  // loc/aw stride between queries
-  const long long qstride_g = (long long)M * D;   // grad_out stride between queries
-  const coord_t* __restrict__ locb = loc + (b * Lq * M + m) * LP + l * P;
-  const coord_t* __restrict__ awb = aw + (b * Lq * M + m) * LP + l * P;
+  while (l + 1 < L && s >= lv.start[l + 1]) ++l;
+  const int2 info = valid ? rowinfo[rr] : make_int2(0, 0);
+  const int start = info.x, count = valid ? info.y : 0;
+  const long long vrow = ((b * S + s) * M + m) * (long long)D;
+  const long long gq = (long long)M * D;
   const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D;
-  const int nsamp = Lq * P;
-  const int slot = lane / LPR;
-  const int cl = lane - slot * LPR;
 
-  // per-wave slot tables: tw / tqr [NS][kGvSlotCap]; counts are wave-uniform
-  int* tqr = t_qr + wave * (NS * kGvSlotCap);
-  acc_t* tw = t_w + wave * (NS * kGvSlotCap);
-  int tcnt[NS];
+  // channel passes: NSLOT > 0 covers D with one CPL-wide chunk per lane; generic loops
+  const int npass = NSLOT > 0 ? 1 : (D + 63) / 64;
+  for (int pass = 0; pass < npass; ++pass) {
+    const int c0 = NSLOT > 0 ? cl * CPL : pass * 64 + lane;
+    const bool on = valid && c0 < D;
+    acc_t v[CPL], acc[CPL];
 #pragma unroll
-  for (int sl = 0; sl < NS; ++sl) tcnt[sl] = 0;
-  auto flush = [&]() {
-    int nr = 0, my_cnt = 0;
+    for (int e = 0; e < CPL; ++e) { v[e] = (acc_t)0; acc[e] = (acc_t)0; }
+    if (NEED_D && on) load_vec<scalar_t, CPL>(value + vrow + c0, v);
+    for (int j = 0; __ballot(j < count) != 0ull; j += U) {
+      Entry<coord_t> en[U];
+      acc_t g[U][CPL];
 #pragma unroll
-    for (int sl = 0; sl < NS; ++sl) {
-      nr = tcnt[sl] > nr ? tcnt[sl] : nr;
-      if (slot == sl) my_cnt = tcnt[sl];
-    }
-    for (int k0 = 0; k0 < nr; k0 += ROUNDS) {
-      int srow[ROUNDS], sq[ROUNDS];
-      acc_t sw[ROUNDS];
+      for (int u = 0; u < U; ++u) {
+        const bool have = j + u < count;
+        en[u] = have ? entries[start + j + u] : Entry<coord_t>{0, (coord_t)0};
+        const int q = (en[u].tap >> 1) / P;
+        if (have && on) load_vec<scalar_t, CPL>(gb + q * gq + c0, g[u]);
+        else {
 #pragma unroll
-      for (int k = 0; k < ROUNDS; ++k) {
-        const bool v = k0 + k < my_cnt;
-        const int idx = slot * kGvSlotCap + (v ? k0 + k : 0);
-        const int qr = tqr[idx];
-        const acc_t w = tw[idx];
-        sq[k] = v ? (qr >> 12) : 0;
-        srow[k] = v ? (qr & 4095) : -1;
-        sw[k] = v ? w : (acc_t)0;
-      }
-      if constexpr (NSLOT > 0) {
-        const bool lane_on = cl * CPL < D;  // narrow heads leave the slot's upper lanes idle
-        acc_t g[ROUNDS][CPL];
-#pragma unroll
-        for (int k = 0; k < ROUNDS; ++k) {
-          if (lane_on) load_vec<scalar_t, CPL>(gb + sq[k] * qstride_g + cl * CPL, g[k]);
+          for (int e = 0; e < CPL; ++e) g[u][e] = (acc_t)0;
         }
+      }
 #pragma unroll
-        for (int k = 0; k < ROUNDS; ++k) {
-          if (srow[k] >= 0 && lane_on) {
-            AccN<acc_t, CPL>* dst = reinterpret_cast<AccN<acc_t, CPL>*>(slab + srow[k] * D + cl * CPL);
-            AccN<acc_t, CPL> v = *dst;
+      for (int u = 0; u < U; ++u) {
+        const acc_t w = (acc_t)en[u].w;
+        acc_t dp = (acc_t)0;
 #pragma unroll
-            for (int c = 0; c < CPL; ++c) v.v[c] += sw[k] * g[k][c];
-            *dst = v;
+        for (int e = 0; e < CPL; ++e) {
+          acc[e] += w * g[u][e];
+          dp += g[u][e] * v[e];
+        }
+        if constexpr (NEED_D) {
+          // butterfly over the slot's lanes (every lane participates)
+#pragma unroll
+          for (int off = LPR >> 1; off > 0; off >>= 1) dp += __shfl_xor(dp, off);
+          if (j + u < count && cl == 0) {
+            const int tap = en[u].tap;
+            const int sidx = tap >> 1, q = sidx / P, p = sidx - (sidx / P) * P;
+            const long long di = ((((b * Lq + q) * M + m) * L + l) * (long long)P + p) * 2 + (tap & 1);
+            if (NSLOT > 0 || pass == 0) dbuf[di] = (coord_t)dp;
+            else dbuf[di] += (coord_t)dp;  // generic path: later channel passes add on
           }
         }
-      } else {
-        for (int c = lane; c < D; c += 64) {
-          acc_t g[ROUNDS];
-#pragma unroll
-          for (int k = 0; k < ROUNDS; ++k) g[k] = to_acc(gb[sq[k] * qstride_g + c]);
-#pragma unroll
-          for (int k = 0; k < ROUNDS; ++k)
-            if (srow[k] >= 0) slab[srow[k] * D + c] += sw[k] * g[k];
-        }
       }
     }
-#pragma unroll
-    for (int sl = 0; sl < NS; ++sl) tcnt[sl] = 0;
-  };
-
-  for (int base = 0; base < nsamp; base += kGvStep) {
-    // ---- phase A: the whole workgroup scans kGvStep samples (loads issued together) ----
-    coord_t lc[kGvSampPerThread], av[kGvSampPerThread];
-#pragma unroll
-    for (int u = 0; u < kGvSampPerThread; ++u) {
-      const int sidx = base + u * kGvThreads + threadIdx.x;
-      const int qq = sidx / P, pp = sidx - (sidx / P) * P;
-      const bool live = sidx < nsamp;
-      lc[u] = live ? locb[qq * qstride_c + pp] : (coord_t)-1e30;
-      av[u] = live ? awb[qq * qstride_c + pp] : (coord_t)0;
-    }
-#pragma unroll
-    for (int u = 0; u < kGvSampPerThread; ++u) {
-      const int sidx = base + u * kGvThreads + threadIdx.x;
-      const int qq = sidx / P;
-      bool c[2] = {false, false};
-      int rw[2] = {0, 0};
-      acc_t wv[2] = {(acc_t)0, (acc_t)0};
-      if (sidx < nsamp) {
-        const Taps<coord_t> t = make_taps<coord_t, ZEROS>(lc[u], T);
-        c[0] = t.ok0 && t.w0 != (coord_t)0 && t.i0 >= r0 && t.i0 < r1;
-        c[1] = t.ok1 && t.w1 != (coord_t)0 && t.i1 >= r0 && t.i1 < r1;
-        rw[0] = t.i0 - r0;
-        rw[1] = t.i1 - r0;
-        wv[0] = (acc_t)av[u] * (acc_t)t.w0;
-        wv[1] = (acc_t)av[u] * (acc_t)t.w1;
-      }
-#pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        // wave-level compaction, one LDS counter bump per wave
-        const unsigned long long mk = __ballot(c[k]);
-        if (mk == 0ull) continue;
-        const int before = __builtin_amdgcn_mbcnt_hi((unsigned)(mk >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk, 0u));
-        int start = 0;
-        if (lane == 0) start = atomicAdd(q_cnt, __popcll(mk));
-        start = __shfl(start, 0);
-        if (c[k]) {
-          q_q[start + before] = qq;
-          q_row[start + before] = rw[k];
-          q_w[start + before] = wv[k];
-        }
-      }
-    }
-    __syncthreads();
-    const int n = *q_cnt;
-    // ---- phase B: wave w moves the entries whose row it owns ((row & 3) == w) into its
-    // per-slot tables (slot = (row/4) % NS, kGvSlotCap entries each); a table that would
-    // overflow is first drained by flush().  Tables persist across steps (the slab rows are
-    // private to the wave), so drains run in long batches with ROUNDS loads in flight.
-    for (int e0 = 0; e0 < n; e0 += 64) {
-      const int e = e0 + lane;
-      int er = 0, eq = 0;
-      acc_t ew = (acc_t)0;
-      bool mine = false;
-      if (e < n) {
-        er = q_row[e];
-        mine = (er & 3) == wave;
-        eq = q_q[e];
-        ew = q_w[e];
-      }
-      const int es = (er >> 2) % NS;
-      unsigned long long mk[NS];
-      bool full = false;
-#pragma unroll
-      for (int sl = 0; sl < NS; ++sl) {
-        mk[sl] = __ballot(mine && es == sl);
-        full |= tcnt[sl] + __popcll(mk[sl]) > kGvSlotCap;
-      }
-      if (full) flush();
-      if (mine) {
-        int pos = 0;
-#pragma unroll
-        for (int sl = 0; sl < NS; ++sl)
-          if (es == sl)
-            pos = sl * kGvSlotCap + tcnt[sl] +
-                  __builtin_amdgcn_mbcnt_hi((unsigned)(mk[sl] >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mk[sl], 0u));
-        tqr[pos] = (eq << 12) | er;  // row < 4096, q < 2^19 (checked on the host)
-        tw[pos] = ew;
-      }
-#pragma unroll
-      for (int sl = 0; sl < NS; ++sl) tcnt[sl] += __popcll(mk[sl]);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) *q_cnt = 0;
-    __syncthreads();
-  }
-  flush();
-  __syncthreads();
-
-  scalar_t* __restrict__ dst = gval + ((b * S + lv.start[l] + r0) * M + m) * (long long)D;
-  const long long rowstride = (long long)M * D;
-  for (int i = threadIdx.x * CPL; i < nrows * D; i += kGvThreads * CPL) {
-    const int row = i / D, c = i - row * D;
-    if constexpr (CPL > 1) {
-      acc_t v[CPL];
-#pragma unroll
-      for (int e = 0; e < CPL; ++e) v[e] = slab[i + e];
-      store_vec<scalar_t, CPL>(dst + row * rowstride + c, v);
-    } else {
-      from_acc(slab[i], dst + row * rowstride + c);
+    if (gval != nullptr && on) {
+      if constexpr (NSLOT > 0) store_vec<scalar_t, CPL>(gval + vrow + c0, acc);
+      else from_acc(acc[0], gval + vrow + c0);
     }
   }
+}
+
+template <typename coord_t, bool ZEROS>
+__global__ __launch_bounds__(256) void msda_bwd_coord_kernel(
+    const coord_t* __restrict__ loc, const coord_t* __restrict__ aw,
+    const coord_t* __restrict__ dbuf, coord_t* __restrict__ gloc, coord_t* __restrict__ gaw,
+    const Levels lv, const int L, const int P, const long long n) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int l = (int)((i / P) % L);
+  const Taps<coord_t> t = make_taps<coord_t, ZEROS>(loc[i], lv.T[l]);
+  const coord_t d0 = t.ok0 ? dbuf[2 * i] : (coord_t)0;
+  const coord_t d1 = t.ok1 ? dbuf[2 * i + 1] : (coord_t)0;
+  if (gaw != nullptr) gaw[i] = t.w0 * d0 + t.w1 * d1;
+  if (gloc != nullptr) gloc[i] = aw[i] * t.gmul * (d1 - d0);
 }
 
 // ---------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------
-constexpr long long kSlabBytes = 32 * 1024;  // grad_value LDS slab per workgroup (+ queue: ~58 KB, 2 per CU)
-constexpr long long kLdsLimit = 64 * 1024;   // dynamic LDS per workgroup we allow ourselves
 
 struct Problem {
   long long B, S, M, D, Lq, L, P;
@@ -638,100 +583,142 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
   return launch_status("forward");
 }
 
-template <typename scalar_t, typename coord_t, int VEC>
-int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
-                 const void* gout, void* gloc, void* gaw, int pad, hipStream_t st) {
-  const long long n_items = pr.B * pr.Lq * pr.M;
-  if (n_items == 0) return MSDA_OK;
-  const int gshift = group_shift_for(pr.D / VEC);
-  const long long threads = n_items << gshift;
-  const unsigned blocks = (unsigned)((threads + 255) / 256);
-  auto* v = static_cast<const scalar_t*>(value);
-  auto* lc = static_cast<const coord_t*>(loc);
-  auto* a = static_cast<const coord_t*>(aw);
-  auto* g = static_cast<const scalar_t*>(gout);
-  auto* gl = static_cast<coord_t*>(gloc);
-  auto* ga = static_cast<coord_t*>(gaw);
-  if (pad == MSDA_PAD_ZEROS)
-    hipLaunchKernelGGL((msda_bwd_kernel<scalar_t, coord_t, VEC, true>), dim3(blocks),
-                       dim3(256), 0, st, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P,
-                       (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, n_items, gshift);
-  else
-    hipLaunchKernelGGL((msda_bwd_kernel<scalar_t, coord_t, VEC, false>), dim3(blocks),
-                       dim3(256), 0, st, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P,
-                       (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, n_items, gshift);
-  return launch_status("backward");
+// backward workspace: [rowinfo int2 x B*M*S][entries Entry x B*M*L*2*Lq*P][d coord x B*Lq*M*L*P*2]
+struct BwdLayout {
+  size_t rowinfo, entries, dbuf, total;
+};
+
+size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+BwdLayout bwd_layout(int value_dtype, long long B, long long S, long long M, long long Lq,
+                     long long L, long long P) {
+  const size_t cs = value_dtype == MSDA_DTYPE_F64 ? 8 : 4;
+  const size_t es = value_dtype == MSDA_DTYPE_F64 ? sizeof(Entry<double>) : sizeof(Entry<float>);
+  BwdLayout w;
+  w.rowinfo = 0;
+  w.entries = align_up((size_t)B * M * S * sizeof(int2));
+  w.dbuf = w.entries + align_up((size_t)B * M * L * 2 * Lq * P * es);
+  w.total = w.dbuf + align_up((size_t)B * Lq * M * L * P * 2 * cs);
+  return w;
+}
+
+template <typename K>
+int allow_lds(K kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return MSDA_OK;
+  if (hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) != hipSuccess) {
+    set_error("msda: cannot raise dynamic LDS to %zu bytes", bytes);
+    return MSDA_ERR_LAUNCH;
+  }
+  return MSDA_OK;
 }
 
 template <typename scalar_t, typename coord_t>
-int run_grad_value(const Problem& pr, const void* loc, const void* aw, const void* gout, void* gval,
-                   int pad, hipStream_t st) {
+int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
+                 const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
+                 int value_dtype, int pad, hipStream_t st) {
   using acc_t = typename AccOf<scalar_t>::type;
-  if (pr.B * pr.M * pr.S * pr.D == 0) return MSDA_OK;
-  // slots per instruction for 16-byte lanes: NSLOT = 64 / (D / CPL) when that is a power of 2
-  constexpr int CPL = 16 / (int)sizeof(acc_t);
-  // (at most 4 slots: a slot's table must hold a whole 64-entry group; lanes whose chunk
-  //  is past D idle for narrow heads)
-  int ns = 0;
-  if (pr.D % CPL == 0) {
-    if (pr.D <= 16 * CPL) ns = 4;
-    else if (pr.D <= 32 * CPL) ns = 2;
-    else if (pr.D <= 64 * CPL) ns = 1;
-  }
-  const int ns_eff = ns > 0 ? ns : 1;
-  // LDS = slab (rows x D acc) + queue + slot tables; stay within 64 KB per workgroup
-  const long long row_bytes = pr.D * (long long)sizeof(acc_t);
-  const long long table = 4LL * ns_eff * kGvSlotCap;
-  const long long overhead = (long long)(kGvQueue + table) * (sizeof(int) + sizeof(acc_t)) +
-                             (long long)kGvQueue * sizeof(int) + 16;
-  const long long slab_budget = min(kSlabBytes, kLdsLimit - overhead);
-  if (row_bytes > slab_budget) {
-    set_error("msda_hip_backward: channels=%lld too large for the LDS grad_value slab", pr.D);
-    return MSDA_ERR_ARG;
-  }
-  int maxT = 1;
-  for (int l = 0; l < pr.L; ++l) maxT = max(maxT, pr.lv.T[l]);
-  RangePlan rp;
-  rp.rows = (int)min((long long)maxT, slab_budget / row_bytes);
-  rp.cum[0] = 0;
-  for (int l = 0; l < pr.L; ++l) rp.cum[l + 1] = rp.cum[l] + (pr.lv.T[l] + rp.rows - 1) / rp.rows;
-  const long long blocks = pr.B * pr.M * rp.cum[pr.L];
-  const size_t lds = (size_t)(rp.rows * row_bytes + overhead);
-  if (rp.rows > 4096 || pr.Lq >= (1 << 19)) {  // packing of (q, row) in the slot tables
-    set_error("msda_hip_backward: num_query=%lld too large for the grad_value kernel", pr.Lq);
-    return MSDA_ERR_ARG;
-  }
+  const long long nrows = pr.B * pr.M * pr.S;
+  if (nrows == 0) return MSDA_OK;
+  const BwdLayout wl = bwd_layout(value_dtype, pr.B, pr.S, pr.M, pr.Lq, pr.L, pr.P);
+  auto* ws = static_cast<unsigned char*>(workspace);
+  auto* rowinfo = reinterpret_cast<int2*>(ws + wl.rowinfo);
+  auto* entries = reinterpret_cast<Entry<coord_t>*>(ws + wl.entries);
+  auto* dbuf = reinterpret_cast<coord_t*>(ws + wl.dbuf);
   auto* lc = static_cast<const coord_t*>(loc);
   auto* a = static_cast<const coord_t*>(aw);
-  auto* g = static_cast<const scalar_t*>(gout);
-  auto* gv = static_cast<scalar_t*>(gval);
-#define MSDA_GV(Z, NS)                                                                          \
-  hipLaunchKernelGGL((msda_gvalue_kernel<scalar_t, coord_t, Z, NS>), dim3((unsigned)blocks),    \
-                     dim3(kGvThreads), lds, st, lc, a, g, gv, pr.lv, rp, (int)pr.L, (int)pr.P,         \
-                     (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq)
   const bool z = pad == MSDA_PAD_ZEROS;
-  switch (ns) {
-    case 1: if (z) MSDA_GV(true, 1); else MSDA_GV(false, 1); break;
-    case 2: if (z) MSDA_GV(true, 2); else MSDA_GV(false, 2); break;
-    case 4: if (z) MSDA_GV(true, 4); else MSDA_GV(false, 4); break;
-    default: if (z) MSDA_GV(true, 0); else MSDA_GV(false, 0); break;
+  const bool need_d = gloc != nullptr || gaw != nullptr;
+  int rc;
+
+  // 1. sort: one workgroup per (b, m, level)
+  {
+    int maxT = 1;
+    for (int l = 0; l < pr.L; ++l) maxT = max(maxT, pr.lv.T[l]);
+    const size_t tail = (size_t)(maxT + 16) * sizeof(int);
+    const size_t stage = (size_t)2 * pr.Lq * pr.P * sizeof(Entry<coord_t>);
+    const bool use_stage = stage + tail <= (size_t)kSortLdsMax;
+    const size_t lds = (use_stage ? stage : 0) + tail;
+    if (lds > (size_t)kSortLdsMax + tail) {
+      set_error("msda_hip_backward: level of %d rows too long for the sort kernel", maxT);
+      return MSDA_ERR_ARG;
+    }
+    const unsigned blocks = (unsigned)(pr.B * pr.M * pr.L);
+#define MSDA_SORT(Z, STG)                                                                         \
+  do {                                                                                          \
+    if ((rc = allow_lds(msda_bwd_sort_kernel<coord_t, Z, STG>, lds))) return rc;               \
+    hipLaunchKernelGGL((msda_bwd_sort_kernel<coord_t, Z, STG>), dim3(blocks), dim3(kSortThreads), \
+                       lds, st, lc, a, rowinfo, entries, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, \
+                       (int)pr.M, (int)pr.Lq);                                                  \
+  } while (0)
+    if (z) { if (use_stage) MSDA_SORT(true, true); else MSDA_SORT(true, false); }
+    else { if (use_stage) MSDA_SORT(false, true); else MSDA_SORT(false, false); }
+#undef MSDA_SORT
+    if ((rc = launch_status("backward sort"))) return rc;
   }
-#undef MSDA_GV
-  return launch_status("grad_value");
+
+  // 2. pull: NS rows per wave, 64/NS lanes x CPL channels per row
+  {
+    constexpr int CPL = 16 / (int)sizeof(acc_t);
+    int ns = 0;
+    if (pr.D % CPL == 0) {
+      if (pr.D <= 16 * CPL) ns = 4;
+      else if (pr.D <= 32 * CPL) ns = 2;
+      else if (pr.D <= 64 * CPL) ns = 1;
+    }
+    const int nse = ns > 0 ? ns : 1;
+    const long long waves = (nrows + nse - 1) / nse;
+    const unsigned blocks = (unsigned)((waves + 3) / 4);
+    auto* v = static_cast<const scalar_t*>(value);
+    auto* g = static_cast<const scalar_t*>(gout);
+    auto* gv = static_cast<scalar_t*>(gval);
+#define MSDA_PULL(NSL, ND)                                                                         \
+  hipLaunchKernelGGL((msda_bwd_pull_kernel<scalar_t, coord_t, NSL, ND>), dim3(blocks),            \
+                     dim3(kPullThreads), 0, st, v, g, rowinfo, entries, gv, dbuf, pr.lv, (int)pr.L, \
+                     (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, nrows)
+    switch (ns) {
+      case 4: if (need_d) MSDA_PULL(4, true); else MSDA_PULL(4, false); break;
+      case 2: if (need_d) MSDA_PULL(2, true); else MSDA_PULL(2, false); break;
+      case 1: if (need_d) MSDA_PULL(1, true); else MSDA_PULL(1, false); break;
+      default: if (need_d) MSDA_PULL(0, true); else MSDA_PULL(0, false); break;
+    }
+#undef MSDA_PULL
+    if ((rc = launch_status("backward pull"))) return rc;
+  }
+
+  // 3. coordinates
+  if (need_d) {
+    const long long n = pr.B * pr.Lq * pr.M * pr.L * pr.P;
+    if (n > 0) {
+      const unsigned blocks = (unsigned)((n + 255) / 256);
+      auto* gl = static_cast<coord_t*>(gloc);
+      auto* ga = static_cast<coord_t*>(gaw);
+      if (z)
+        hipLaunchKernelGGL((msda_bwd_coord_kernel<coord_t, true>), dim3(blocks), dim3(256), 0, st,
+                           lc, a, dbuf, gl, ga, pr.lv, (int)pr.L, (int)pr.P, n);
+      else
+        hipLaunchKernelGGL((msda_bwd_coord_kernel<coord_t, false>), dim3(blocks), dim3(256), 0, st,
+                           lc, a, dbuf, gl, ga, pr.lv, (int)pr.L, (int)pr.P, n);
+      if ((rc = launch_status("backward coord"))) return rc;
+    }
+  }
+  return MSDA_OK;
 }
 
 }  // namespace
 
 extern "C" {
 
-int msda_hip_abi_version(void) { return 1; }
+int msda_hip_abi_version(void) { return 2; }
 
 const char* msda_hip_last_error(void) { return g_last_error; }
 
 size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,
-                                         int64_t num_heads, int64_t channels) {
-  (void)value_dtype; (void)batch; (void)spatial_size; (void)num_heads; (void)channels;
-  return 0;  // grad_value is accumulated in LDS slabs (msda_gvalue_kernel): no scratch
+                                         int64_t num_heads, int64_t channels, int64_t num_query,
+                                         int64_t num_levels, int64_t num_point) {
+  (void)channels;
+  if (batch <= 0 || spatial_size <= 0 || num_heads <= 0) return 0;
+  return bwd_layout(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point).total;
 }
 
 int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_shapes,
@@ -804,47 +791,49 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
     set_error("msda_hip_backward: empty value with non-empty query");
     return MSDA_ERR_ARG;
   }
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  const int vec = pick_vec(value_dtype, pr.D);
-  (void)workspace;  // ABI v1 slot; grad_value no longer needs scratch (see msda_gvalue_kernel)
-  // grad_loc / grad_attn: per-item gathers + lane-group butterflies
-  if (grad_loc != nullptr || grad_attn != nullptr) {
-    switch (value_dtype) {
-      case MSDA_DTYPE_F32:
-        rc = vec == 4 ? run_backward<float, float, 4>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st)
-                      : run_backward<float, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st);
-        break;
-      case MSDA_DTYPE_F64:
-        rc = vec == 2 ? run_backward<double, double, 2>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st)
-                      : run_backward<double, double, 1>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st);
-        break;
-      case MSDA_DTYPE_BF16:
-        rc = vec == 8 ? run_backward<bf16_t, float, 8>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st)
-                      : run_backward<bf16_t, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st);
-        break;
-      case MSDA_DTYPE_F16:
-        rc = vec == 8 ? run_backward<f16_t, float, 8>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st)
-                      : run_backward<f16_t, float, 1>(pr, value, sampling_loc, attn_weight, grad_output, grad_loc, grad_attn, padding_mode, st);
-        break;
-      default:
-        set_error("msda_hip_backward: unknown value dtype %d", value_dtype);
-        return MSDA_ERR_ARG;
+  // the backward's row table covers [0, S) level by level: levels must tile it in order
+  // (as the reference's level_start_index = cumsum of the shapes does)
+  for (int l = 0, run = 0; l < pr.L; ++l) {
+    if (pr.lv.start[l] != run) {
+      set_error("msda_hip_backward: level_start must be the running sum of spatial_shapes");
+      return MSDA_ERR_ARG;
     }
-    if (rc) return rc;
+    run += pr.lv.T[l];
+    if (l == pr.L - 1 && run != pr.S) {
+      set_error("msda_hip_backward: spatial_shapes must sum to spatial_size (%lld != %lld)",
+                (long long)run, pr.S);
+      return MSDA_ERR_ARG;
+    }
   }
-  if (grad_value == nullptr) return MSDA_OK;
+  if (2 * pr.Lq * pr.P >= (1LL << 30) || pr.B * pr.M * pr.L * 2 * pr.Lq * pr.P >= (1LL << 31)) {
+    set_error("msda_hip_backward: too many taps for 32-bit entry indices");
+    return MSDA_ERR_ARG;
+  }
+  if (value_dtype < MSDA_DTYPE_F32 || value_dtype > MSDA_DTYPE_F16) {
+    set_error("msda_hip_backward: unknown value dtype %d", value_dtype);
+    return MSDA_ERR_ARG;
+  }
+  const size_t need = msda_hip_backward_workspace_bytes(value_dtype, batch, spatial_size, num_heads,
+                                                        channels, num_query, num_levels, num_point);
+  if (need > 0 && workspace == nullptr) {
+    set_error("msda_hip_backward: workspace of %zu bytes required", need);
+    return MSDA_ERR_ARG;
+  }
+  if (grad_value == nullptr && grad_loc == nullptr && grad_attn == nullptr) return MSDA_OK;
+  hipStream_t st = static_cast<hipStream_t>(stream);
   switch (value_dtype) {
     case MSDA_DTYPE_F32:
-      return run_grad_value<float, float>(pr, sampling_loc, attn_weight, grad_output, grad_value, padding_mode, st);
+      return run_backward<float, float>(pr, value, sampling_loc, attn_weight, grad_output, grad_value,
+                                        grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
     case MSDA_DTYPE_F64:
-      return run_grad_value<double, double>(pr, sampling_loc, attn_weight, grad_output, grad_value, padding_mode, st);
+      return run_backward<double, double>(pr, value, sampling_loc, attn_weight, grad_output, grad_value,
+                                          grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
     case MSDA_DTYPE_BF16:
-      return run_grad_value<bf16_t, float>(pr, sampling_loc, attn_weight, grad_output, grad_value, padding_mode, st);
-    case MSDA_DTYPE_F16:
-      return run_grad_value<f16_t, float>(pr, sampling_loc, attn_weight, grad_output, grad_value, padding_mode, st);
+      return run_backward<bf16_t, float>(pr, value, sampling_loc, attn_weight, grad_output, grad_value,
+                                         grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
     default:
-      set_error("msda_hip_backward: unknown value dtype %d", value_dtype);
-      return MSDA_ERR_ARG;
+      return run_backward<f16_t, float>(pr, value, sampling_loc, attn_weight, grad_output, grad_value,
+                                        grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
   }
 }
 

@@ -187,10 +187,9 @@ def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="bor
     gl = torch.empty_like(loc) if need_loc else None
     ga = torch.empty_like(aw) if need_aw else None
     ws = None
-    if need_value:
-        nbytes = lib.msda_hip_backward_workspace_bytes(_native.DTYPE_TAGS[value.dtype], B, S, M, D)
-        if nbytes:
-            ws = torch.empty((nbytes + 3) // 4, dtype=torch.float32, device=value.device)
+    nbytes = lib.msda_hip_backward_workspace_bytes(_native.DTYPE_TAGS[value.dtype], B, S, M, D, Lq, L, P)
+    if nbytes:  # through the caching allocator: no hipMalloc on the hot path, graph-capturable
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=value.device)
     ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     timer = _timer
     if timer is not None:
