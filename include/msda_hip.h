@@ -75,8 +75,9 @@ int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_
 
 /* Bytes of device scratch msda_hip_backward needs (ABI v2: depends on the query side).
  * Holds the per-row tap lists of the backward's sort pass (B*M*L*2*Lq*P entries), the row
- * table (B*M*S) and the per-tap dot products (B*Lq*M*L*P*2); no floating-point atomics
- * are used, so the backward is bitwise reproducible. */
+ * table (B*M*S) and the per-tap dot products (B*Lq*M*L*P*2).  No floating-point atomics
+ * are used; with MSDA_HIP_DETERMINISTIC=1 in the environment every sum also has a fixed
+ * order (bitwise reproducible backward, slower sort pass). */
 size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,
                                          int64_t num_heads, int64_t channels, int64_t num_query,
                                          int64_t num_levels, int64_t num_point);

@@ -33,6 +33,7 @@
 #include <hip/hip_fp16.h>
 #include <stdint.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include "msda_hip.h"
@@ -245,8 +246,9 @@ __global__ __launch_bounds__(256) void msda_fwd_kernel(
 //   1. msda_bwd_sort_kernel  — one workgroup per (b, m, level): histogram of the in-map
 //      taps per row with LDS integer atomics, exclusive scan, per-row entry lists
 //      {tap id, aw*w} (staged in LDS and written contiguously when they fit) and a row
-//      table {first entry, count}.  Entries of a row are then sorted by tap id, so every
-//      sum below has a fixed order: the backward is bitwise reproducible.
+//      table {first entry, count}.  With MSDA_HIP_DETERMINISTIC=1 the entries of a row are
+//      sorted by tap id, so every sum below has a fixed order (bitwise reproducible
+//      backward); by default their order is the LDS-atomic arrival order.
 //   2. msda_bwd_pull_kernel  — the forward's mirror: a slot of 64/NS lanes (CPL channels
 //      each, one 16-byte access per lane) per destination value row walks the row's
 //      entries, gathers grad_out rows, accumulates in registers and writes the row once;
@@ -295,7 +297,7 @@ template <typename coord_t, bool ZEROS, bool STAGE>
 __global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
     const coord_t* __restrict__ loc, const coord_t* __restrict__ aw, int2* __restrict__ rowinfo,
     Entry<coord_t>* __restrict__ entries, const Levels lv, const int L, const int P, const int S,
-    const int M, const int Lq) {
+    const int M, const int Lq, const int sort_rows) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const int l = (int)(blockIdx.x % (unsigned)L);
   const long long bm = blockIdx.x / (unsigned)L;
@@ -360,10 +362,11 @@ __global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
     }
   }
   __syncthreads();
-  // cur[i] now = end of row i.  Sort each row's list by tap id (insertion sort; lists are
-  // short) so the pull kernel sums in a fixed order, then write out.
+  // cur[i] now = end of row i.  In deterministic mode each row's list is sorted by tap id
+  // (insertion sort by the row's owner thread: O(n^2) in the row length, so off by
+  // default) so the pull kernel sums in a fixed order; then write out.
   if constexpr (STAGE) {
-    for (int i = lo; i < hi; ++i) {
+    for (int i = lo; i < hi && sort_rows; ++i) {
       const int e1 = cur[i], e0 = (i == 0 ? 0 : cur[i - 1]);
       for (int x = e0 + 1; x < e1; ++x) {
         const Entry<coord_t> key = stage[x];
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
     for (int i = threadIdx.x; i < total; i += kSortThreads) entries[base + i] = stage[i];
   } else {
     __threadfence_block();
-    for (int i = lo; i < hi; ++i) {
+    for (int i = lo; i < hi && sort_rows; ++i) {
       const int e1 = cur[i], e0 = (i == 0 ? 0 : cur[i - 1]);
       for (int x = e0 + 1; x < e1; ++x) {
         const Entry<coord_t> key = entries[base + x];
@@ -633,6 +636,10 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
 
   // 1. sort: one workgroup per (b, m, level)
   {
+    static const int deterministic = [] {
+      const char* e = getenv("MSDA_HIP_DETERMINISTIC");
+      return (e != nullptr && e[0] == '1') ? 1 : 0;
+    }();
     int maxT = 1;
     for (int l = 0; l < pr.L; ++l) maxT = max(maxT, pr.lv.T[l]);
     const size_t tail = (size_t)(maxT + 16) * sizeof(int);
@@ -649,7 +656,7 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     if ((rc = allow_lds(msda_bwd_sort_kernel<coord_t, Z, STG>, lds))) return rc;               \
     hipLaunchKernelGGL((msda_bwd_sort_kernel<coord_t, Z, STG>), dim3(blocks), dim3(kSortThreads), \
                        lds, st, lc, a, rowinfo, entries, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, \
-                       (int)pr.M, (int)pr.Lq);                                                  \
+                       (int)pr.M, (int)pr.Lq, deterministic);                                   \
   } while (0)
     if (z) { if (use_stage) MSDA_SORT(true, true); else MSDA_SORT(true, false); }
     else { if (use_stage) MSDA_SORT(false, true); else MSDA_SORT(false, false); }
