@@ -414,7 +414,7 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
   constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(acc_t) : 1;  // channels per lane per pass
   constexpr int NS = NSLOT > 0 ? NSLOT : 1;
   constexpr int LPR = 64 / NS;                                   // lanes per slot (row)
-  constexpr int U = 4;                                           // entries in flight per slot
+  constexpr int U = LPR < 16 ? LPR : 16;                         // grad_out loads in flight per slot
   const int lane = threadIdx.x & 63;
   const int slot = lane / LPR;
   const int cl = lane - slot * LPR;
@@ -443,39 +443,49 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
 #pragma unroll
     for (int e = 0; e < CPL; ++e) { v[e] = (acc_t)0; acc[e] = (acc_t)0; }
     if (NEED_D && on) load_vec<scalar_t, CPL>(value + vrow + c0, v);
-    for (int j = 0; __ballot(j < count) != 0ull; j += U) {
-      Entry<coord_t> en[U];
-      acc_t g[U][CPL];
+    // entries come in chunks of LPR: lane cl of a slot loads entry j0 + cl (one coalesced
+    // access per slot), the next chunk is prefetched, and each entry is broadcast to the
+    // slot's lanes with a shuffle, so U grad_out loads are in flight at once.
+    Entry<coord_t> nxt = (cl < count) ? entries[start + cl] : Entry<coord_t>{0, (coord_t)0};
+    for (int j0 = 0; __ballot(j0 < count) != 0ull; j0 += LPR) {
+      const Entry<coord_t> cur = nxt;
+      nxt = (j0 + LPR + cl < count) ? entries[start + j0 + LPR + cl] : Entry<coord_t>{0, (coord_t)0};
+      const int nchunk = min(LPR, count - j0);  // may be <= 0 for a finished slot
+      for (int u0 = 0; __ballot(u0 < nchunk) != 0ull; u0 += U) {
+        int tap[U];
+        acc_t w[U], g[U][CPL];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const bool have = j + u < count;
-        en[u] = have ? entries[start + j + u] : Entry<coord_t>{0, (coord_t)0};
-        const int q = (en[u].tap >> 1) / P;
-        if (have && on) load_vec<scalar_t, CPL>(gb + q * gq + c0, g[u]);
-        else {
+        for (int u = 0; u < U; ++u) {
+          const int src = slot * LPR + ((u0 + u) & (LPR - 1));
+          tap[u] = __shfl(cur.tap, src);
+          w[u] = (acc_t)__shfl(cur.w, src);
+          const bool have = u0 + u < nchunk;
+          const int q = (tap[u] >> 1) / P;
+          if (have && on) load_vec<scalar_t, CPL>(gb + q * gq + c0, g[u]);
+          else {
 #pragma unroll
-          for (int e = 0; e < CPL; ++e) g[u][e] = (acc_t)0;
+            for (int e = 0; e < CPL; ++e) g[u][e] = (acc_t)0;
+          }
+          if (!have) w[u] = (acc_t)0;
         }
-      }
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const acc_t w = (acc_t)en[u].w;
-        acc_t dp = (acc_t)0;
+        for (int u = 0; u < U; ++u) {
+          acc_t dp = (acc_t)0;
 #pragma unroll
-        for (int e = 0; e < CPL; ++e) {
-          acc[e] += w * g[u][e];
-          dp += g[u][e] * v[e];
-        }
-        if constexpr (NEED_D) {
-          // butterfly over the slot's lanes (every lane participates)
+          for (int e = 0; e < CPL; ++e) {
+            acc[e] += w[u] * g[u][e];
+            dp += g[u][e] * v[e];
+          }
+          if constexpr (NEED_D) {
+            // butterfly over the slot's lanes (every lane participates)
 #pragma unroll
-          for (int off = LPR >> 1; off > 0; off >>= 1) dp += __shfl_xor(dp, off);
-          if (j + u < count && cl == 0) {
-            const int tap = en[u].tap;
-            const int sidx = tap >> 1, q = sidx / P, p = sidx - (sidx / P) * P;
-            const long long di = ((((b * Lq + q) * M + m) * L + l) * (long long)P + p) * 2 + (tap & 1);
-            if (NSLOT > 0 || pass == 0) dbuf[di] = (coord_t)dp;
-            else dbuf[di] += (coord_t)dp;  // generic path: later channel passes add on
+            for (int off = LPR >> 1; off > 0; off >>= 1) dp += __shfl_xor(dp, off);
+            if (u0 + u < nchunk && cl == 0) {
+              const int sidx = tap[u] >> 1, q = sidx / P, p = sidx - (sidx / P) * P;
+              const long long di = ((((b * Lq + q) * M + m) * L + l) * (long long)P + p) * 2 + (tap[u] & 1);
+              if (NSLOT > 0 || pass == 0) dbuf[di] = (coord_t)dp;
+              else dbuf[di] += (coord_t)dp;  // generic path: later channel passes add on
+            }
           }
         }
       }
