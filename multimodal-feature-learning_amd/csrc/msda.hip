@@ -249,11 +249,11 @@ __global__ __launch_bounds__(256) void msda_fwd_kernel(
 //      table {first entry, count}.  With MSDA_HIP_DETERMINISTIC=1 the entries of a row are
 //      sorted by tap id, so every sum below has a fixed order (bitwise reproducible
 //      backward); by default their order is the LDS-atomic arrival order.
-//   2. msda_bwd_pull_kernel  — the forward's mirror: a slot of 64/NS lanes (CPL channels
-//      each, one 16-byte access per lane) per destination value row walks the row's
-//      entries, gathers grad_out rows, accumulates in registers and writes the row once;
-//      the same loop reduces each entry's dot product with the row's values (butterfly
-//      over the slot's lanes) into the per-tap buffer d.
+//   2. msda_bwd_pull_kernel  — the forward's mirror: 64/NS lanes (one 16-byte access per
+//      lane, as the forward) per destination value row walk the row's entries, gather
+//      grad_out rows, accumulate in registers and write the row once; the same loop reduces
+//      each entry's dot product with the row's values (DPP butterfly over the row's
+//      lanes) into the per-tap buffer d.
 //   3. msda_bwd_coord_kernel — per sample: grad_aw = w0 d0 + w1 d1,
 //      grad_loc = aw * dy/dloc * (d1 - d0)   (d_k = 0 for a tap outside the map).
 template <typename coord_t>
@@ -397,13 +397,31 @@ __global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
   }
 }
 
-template <typename acc_t, int N>
-struct alignas(16) AccN {
-  acc_t v[N];
-};
+// Sum of x over aligned groups of N lanes (N = 2..64), result in every lane of the group.
+// Up to 16 lanes with DPP (quad_perm / row_half_mirror / row_mirror: VALU only, no LDS
+// crossbar); beyond that ds_bpermute.
+template <int N>
+__device__ __forceinline__ float group_sum(float x) {
+  if constexpr (N >= 2) x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xF, 0xF, false));
+  if constexpr (N >= 4) x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xF, 0xF, false));
+  if constexpr (N >= 8) x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x141, 0xF, 0xF, false));
+  if constexpr (N >= 16) x += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x140, 0xF, 0xF, false));
+  if constexpr (N >= 32) x += __shfl_xor(x, 16);
+  if constexpr (N >= 64) x += __shfl_xor(x, 32);
+  return x;
+}
+template <int N>
+__device__ __forceinline__ double group_sum(double x) {
+#pragma unroll
+  for (int off = N >> 1; off > 0; off >>= 1) x += __shfl_xor(x, off);
+  return x;
+}
 
 constexpr int kPullThreads = 256;
 
+// NSLOT rows per wave, LPR = 64/NSLOT lanes per row, CPL = 16 B / sizeof(scalar_t) channels
+// per lane (one 16-byte load per lane per row, as the forward); NSLOT = 0: generic path,
+// one row per wave, lane = channel, D in passes of 64.
 template <typename scalar_t, typename coord_t, int NSLOT, bool NEED_D>
 __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
     const scalar_t* __restrict__ value, const scalar_t* __restrict__ gout,
@@ -411,10 +429,10 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
     scalar_t* __restrict__ gval, coord_t* __restrict__ dbuf, const Levels lv, const int L,
     const int P, const int S, const int M, const int D, const int Lq, const long long nrows) {
   using acc_t = typename AccOf<scalar_t>::type;
-  constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(acc_t) : 1;  // channels per lane per pass
+  constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(scalar_t) : 1;
   constexpr int NS = NSLOT > 0 ? NSLOT : 1;
-  constexpr int LPR = 64 / NS;                                   // lanes per slot (row)
-  constexpr int U = LPR < 16 ? LPR : 16;                         // grad_out loads in flight per slot
+  constexpr int LPR = 64 / NS;                            // lanes per row
+  constexpr int U = NSLOT > 0 ? (64 / CPL < LPR ? 64 / CPL : LPR) : 16;  // loads in flight
   const int lane = threadIdx.x & 63;
   const int slot = lane / LPR;
   const int cl = lane - slot * LPR;
@@ -434,7 +452,6 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
   const long long gq = (long long)M * D;
   const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D;
 
-  // channel passes: NSLOT > 0 covers D with one CPL-wide chunk per lane; generic loops
   const int npass = NSLOT > 0 ? 1 : (D + 63) / 64;
   for (int pass = 0; pass < npass; ++pass) {
     const int c0 = NSLOT > 0 ? cl * CPL : pass * 64 + lane;
@@ -443,20 +460,20 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
 #pragma unroll
     for (int e = 0; e < CPL; ++e) { v[e] = (acc_t)0; acc[e] = (acc_t)0; }
     if (NEED_D && on) load_vec<scalar_t, CPL>(value + vrow + c0, v);
-    // entries come in chunks of LPR: lane cl of a slot loads entry j0 + cl (one coalesced
-    // access per slot), the next chunk is prefetched, and each entry is broadcast to the
-    // slot's lanes with a shuffle, so U grad_out loads are in flight at once.
+    // entries in chunks of LPR: lane cl of a row loads entry j0 + cl (coalesced), the next
+    // chunk is prefetched, each entry is broadcast to the row's lanes with a shuffle, and U
+    // grad_out row loads are in flight at once.
     Entry<coord_t> nxt = (cl < count) ? entries[start + cl] : Entry<coord_t>{0, (coord_t)0};
     for (int j0 = 0; __ballot(j0 < count) != 0ull; j0 += LPR) {
       const Entry<coord_t> cur = nxt;
       nxt = (j0 + LPR + cl < count) ? entries[start + j0 + LPR + cl] : Entry<coord_t>{0, (coord_t)0};
-      const int nchunk = min(LPR, count - j0);  // may be <= 0 for a finished slot
+      const int nchunk = min(LPR, count - j0);  // <= 0 for a finished row
       for (int u0 = 0; __ballot(u0 < nchunk) != 0ull; u0 += U) {
         int tap[U];
         acc_t w[U], g[U][CPL];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          const int src = slot * LPR + ((u0 + u) & (LPR - 1));
+          const int src = slot * LPR + u0 + u;
           tap[u] = __shfl(cur.tap, src);
           w[u] = (acc_t)__shfl(cur.w, src);
           const bool have = u0 + u < nchunk;
@@ -477,9 +494,7 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
             dp += g[u][e] * v[e];
           }
           if constexpr (NEED_D) {
-            // butterfly over the slot's lanes (every lane participates)
-#pragma unroll
-            for (int off = LPR >> 1; off > 0; off >>= 1) dp += __shfl_xor(dp, off);
+            dp = group_sum<LPR>(dp);  // every lane participates
             if (u0 + u < nchunk && cl == 0) {
               const int sidx = tap[u] >> 1, q = sidx / P, p = sidx - (sidx / P) * P;
               const long long di = ((((b * Lq + q) * M + m) * L + l) * (long long)P + p) * 2 + (tap[u] & 1);
@@ -674,14 +689,17 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     if ((rc = launch_status("backward sort"))) return rc;
   }
 
-  // 2. pull: NS rows per wave, 64/NS lanes x CPL channels per row
+  // 2. pull: NS rows per wave, 64/NS lanes x 16 bytes per row
   {
-    constexpr int CPL = 16 / (int)sizeof(acc_t);
+    constexpr int CPL = 16 / (int)sizeof(scalar_t);
     int ns = 0;
     if (pr.D % CPL == 0) {
-      if (pr.D <= 16 * CPL) ns = 4;
-      else if (pr.D <= 32 * CPL) ns = 2;
-      else if (pr.D <= 64 * CPL) ns = 1;
+      const long long lpr = pr.D / CPL;
+      if (lpr == 8) ns = 8;
+      else if (lpr == 16) ns = 4;
+      else if (lpr == 32) ns = 2;
+      else if (lpr == 64) ns = 1;
+      else if (lpr < 8) ns = 0;  // narrow heads: generic
     }
     const int nse = ns > 0 ? ns : 1;
     const long long waves = (nrows + nse - 1) / nse;
@@ -694,6 +712,7 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
                      dim3(kPullThreads), 0, st, v, g, rowinfo, entries, gv, dbuf, pr.lv, (int)pr.L, \
                      (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, nrows)
     switch (ns) {
+      case 8: if (need_d) MSDA_PULL(8, true); else MSDA_PULL(8, false); break;
       case 4: if (need_d) MSDA_PULL(4, true); else MSDA_PULL(4, false); break;
       case 2: if (need_d) MSDA_PULL(2, true); else MSDA_PULL(2, false); break;
       case 1: if (need_d) MSDA_PULL(1, true); else MSDA_PULL(1, false); break;
