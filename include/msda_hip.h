@@ -74,8 +74,8 @@ int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_
                      int padding_mode, void* stream);
 
 /* Bytes of device scratch msda_hip_backward needs (ABI v2: depends on the query side).
- * Holds the per-row tap lists of the backward's sort pass (B*M*L*2*Lq*P entries), the row
- * table (B*M*S) and the per-tap dot products (B*Lq*M*L*P*2).  No floating-point atomics
+ * Holds the per-row tap lists of the backward's sort pass (B*M*L*2*Lq*P entries) and the
+ * row table (B*M*S).  No floating-point atomics
  * are used; with MSDA_HIP_DETERMINISTIC=1 in the environment every sum also has a fixed
  * order (bitwise reproducible backward, slower sort pass). */
 size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,

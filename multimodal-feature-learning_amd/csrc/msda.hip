@@ -29,6 +29,8 @@
 // at integer positions, and a one-ulp different y would flip the segment.
 
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include <stdint.h>
@@ -419,15 +421,23 @@ __device__ __forceinline__ double group_sum(double x) {
 
 constexpr int kPullThreads = 256;
 
+// Row order of the pull: levels by decreasing taps per row (T ascending: a level's rows all
+// receive ~2*Lq*P/T_l taps), so the longest-running waves start first instead of forming the
+// tail of the launch.  Rows of level lvl[i] occupy [cum[i], cum[i+1]) as (b*M + m, s).
+struct PullOrder {
+  int lvl[MSDA_MAX_LEVELS];
+  long long cum[MSDA_MAX_LEVELS + 1];
+};
+
 // NSLOT rows per wave, LPR = 64/NSLOT lanes per row, CPL = 16 B / sizeof(scalar_t) channels
 // per lane (one 16-byte load per lane per row, as the forward); NSLOT = 0: generic path,
 // one row per wave, lane = channel, D in passes of 64.
-template <typename scalar_t, typename coord_t, int NSLOT, bool NEED_D>
+template <typename scalar_t, typename coord_t, int NSLOT>
 __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
-    const scalar_t* __restrict__ value, const scalar_t* __restrict__ gout,
-    const int2* __restrict__ rowinfo, const Entry<coord_t>* __restrict__ entries,
-    scalar_t* __restrict__ gval, coord_t* __restrict__ dbuf, const Levels lv, const int L,
-    const int P, const int S, const int M, const int D, const int Lq, const long long nrows) {
+    const scalar_t* __restrict__ gout, const int2* __restrict__ rowinfo,
+    const Entry<coord_t>* __restrict__ entries, scalar_t* __restrict__ gval, const int S,
+    const int M, const int D, const int Lq, const int P, const long long nrows, const Levels lv,
+    const PullOrder po) {
   using acc_t = typename AccOf<scalar_t>::type;
   constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(scalar_t) : 1;
   constexpr int NS = NSLOT > 0 ? NSLOT : 1;
@@ -439,13 +449,16 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
   const long long wave_id = ((long long)blockIdx.x * kPullThreads + threadIdx.x) >> 6;
   const long long row = wave_id * NS + slot;  // (b, m, s) flattened as (b*M + m)*S + s
   const bool valid = row < nrows;
-  const long long rr = valid ? row : 0;
-  const int s = (int)(rr % S);
-  const long long bm = rr / S;
+  const long long ro = valid ? row : 0;
+  int i = 0;
+  while (ro >= po.cum[i + 1]) ++i;
+  const int l = po.lvl[i];
+  const long long off = ro - po.cum[i];
+  const long long bm = off / lv.T[l];
+  const int s = lv.start[l] + (int)(off - bm * lv.T[l]);
+  const long long rr = bm * S + s;
   const int m = (int)(bm % M);
   const long long b = bm / M;
-  int l = 0;
-  while (l + 1 < L && s >= lv.start[l + 1]) ++l;
   const int2 info = valid ? rowinfo[rr] : make_int2(0, 0);
   const int start = info.x, count = valid ? info.y : 0;
   const long long vrow = ((b * S + s) * M + m) * (long long)D;
@@ -456,10 +469,9 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
   for (int pass = 0; pass < npass; ++pass) {
     const int c0 = NSLOT > 0 ? cl * CPL : pass * 64 + lane;
     const bool on = valid && c0 < D;
-    acc_t v[CPL], acc[CPL];
+    acc_t acc[CPL];
 #pragma unroll
-    for (int e = 0; e < CPL; ++e) { v[e] = (acc_t)0; acc[e] = (acc_t)0; }
-    if (NEED_D && on) load_vec<scalar_t, CPL>(value + vrow + c0, v);
+    for (int e = 0; e < CPL; ++e) acc[e] = (acc_t)0;
     // entries in chunks of LPR: lane cl of a row loads entry j0 + cl (coalesced), the next
     // chunk is prefetched, each entry is broadcast to the row's lanes with a shuffle, and U
     // grad_out row loads are in flight at once.
@@ -487,44 +499,100 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          acc_t dp = (acc_t)0;
 #pragma unroll
-          for (int e = 0; e < CPL; ++e) {
-            acc[e] += w[u] * g[u][e];
-            dp += g[u][e] * v[e];
-          }
-          if constexpr (NEED_D) {
-            dp = group_sum<LPR>(dp);  // every lane participates
-            if (u0 + u < nchunk && cl == 0) {
-              const int sidx = tap[u] >> 1, q = sidx / P, p = sidx - (sidx / P) * P;
-              const long long di = ((((b * Lq + q) * M + m) * L + l) * (long long)P + p) * 2 + (tap[u] & 1);
-              if (NSLOT > 0 || pass == 0) dbuf[di] = (coord_t)dp;
-              else dbuf[di] += (coord_t)dp;  // generic path: later channel passes add on
-            }
-          }
+          for (int e = 0; e < CPL; ++e) acc[e] += w[u] * g[u][e];
         }
       }
     }
-    if (gval != nullptr && on) {
+    if (on) {
       if constexpr (NSLOT > 0) store_vec<scalar_t, CPL>(gval + vrow + c0, acc);
       else from_acc(acc[0], gval + vrow + c0);
     }
   }
 }
 
-template <typename coord_t, bool ZEROS>
+// grad_aw / grad_loc: the forward's item decomposition (G lanes x VEC channels own one
+// (b, q, m) row).  grad_out of the item is loaded once; per sample the two taps are
+// gathered like the forward, the two partial dot products are reduced over the G lanes with
+// DPP, and lane j % G writes sample j, so each item's 2*L*P outputs leave as coalesced
+// stores.  ONE: D/VEC <= G (every lane owns exactly one chunk; the common case).
+template <typename scalar_t, typename coord_t, int VEC, int G, bool ZEROS, bool ONE>
 __global__ __launch_bounds__(256) void msda_bwd_coord_kernel(
-    const coord_t* __restrict__ loc, const coord_t* __restrict__ aw,
-    const coord_t* __restrict__ dbuf, coord_t* __restrict__ gloc, coord_t* __restrict__ gaw,
-    const Levels lv, const int L, const int P, const long long n) {
-  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const int l = (int)((i / P) % L);
-  const Taps<coord_t> t = make_taps<coord_t, ZEROS>(loc[i], lv.T[l]);
-  const coord_t d0 = t.ok0 ? dbuf[2 * i] : (coord_t)0;
-  const coord_t d1 = t.ok1 ? dbuf[2 * i + 1] : (coord_t)0;
-  if (gaw != nullptr) gaw[i] = t.w0 * d0 + t.w1 * d1;
-  if (gloc != nullptr) gloc[i] = aw[i] * t.gmul * (d1 - d0);
+    const scalar_t* __restrict__ value, const coord_t* __restrict__ loc,
+    const coord_t* __restrict__ aw, const scalar_t* __restrict__ gout,
+    coord_t* __restrict__ gloc, coord_t* __restrict__ gaw, const Levels lv, const int L,
+    const int P, const int S, const int M, const int D, const int Lq, const long long n_items) {
+  using acc_t = typename AccOf<scalar_t>::type;
+  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long item_raw = tid / G;
+  const bool active = item_raw < n_items;  // every lane stays for the reductions
+  const long long item = active ? item_raw : 0;
+  const int lg = (int)(tid % G);
+  const int m = (int)(item % M);
+  const long long b = item / M / Lq;
+  const long long rowstride = (long long)M * D;
+  const coord_t* __restrict__ locp = loc + item * (L * P);
+  const coord_t* __restrict__ awp = aw + item * (L * P);
+  const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D;
+  const scalar_t* __restrict__ gp = gout + item * D;
+  const int nchunk = D / VEC;
+  const bool on = active && lg < nchunk;
+  acc_t g1[VEC];
+  if constexpr (ONE) {
+    if (on) load_vec<scalar_t, VEC>(gp + lg * VEC, g1);
+    else {
+#pragma unroll
+      for (int e = 0; e < VEC; ++e) g1[e] = (acc_t)0;
+    }
+  }
+  for (int l = 0; l < L; ++l) {
+    const int T = lv.T[l];
+    const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rowstride;
+    for (int p = 0; p < P; ++p) {
+      const int j = l * P + p;
+      const coord_t a = awp[j];
+      const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locp[j], T);
+      const acc_t w0 = (acc_t)t.w0, w1 = (acc_t)t.w1;
+      acc_t pa = (acc_t)0, pl = (acc_t)0;
+      if constexpr (ONE) {
+        if (on) {
+          acc_t v0[VEC], v1[VEC];
+          load_vec<scalar_t, VEC>(vl + t.i0 * rowstride + lg * VEC, v0);
+          load_vec<scalar_t, VEC>(vl + t.i1 * rowstride + lg * VEC, v1);
+#pragma unroll
+          for (int e = 0; e < VEC; ++e) {
+            const acc_t x0 = t.ok0 ? v0[e] : (acc_t)0;
+            const acc_t x1 = t.ok1 ? v1[e] : (acc_t)0;
+            pa += g1[e] * (x0 * w0 + x1 * w1);
+            pl += g1[e] * (x1 - x0);
+          }
+        }
+      } else {
+        if (active) {
+          for (int ck = lg; ck < nchunk; ck += G) {
+            acc_t g[VEC], v0[VEC], v1[VEC];
+            load_vec<scalar_t, VEC>(gp + ck * VEC, g);
+            load_vec<scalar_t, VEC>(vl + t.i0 * rowstride + ck * VEC, v0);
+            load_vec<scalar_t, VEC>(vl + t.i1 * rowstride + ck * VEC, v1);
+#pragma unroll
+            for (int e = 0; e < VEC; ++e) {
+              const acc_t x0 = t.ok0 ? v0[e] : (acc_t)0;
+              const acc_t x1 = t.ok1 ? v1[e] : (acc_t)0;
+              pa += g[e] * (x0 * w0 + x1 * w1);
+              pl += g[e] * (x1 - x0);
+            }
+          }
+        }
+      }
+      pa = group_sum<G>(pa);
+      pl = group_sum<G>(pl);
+      if (active && lg == j % G) {
+        const long long o = item * (L * P) + j;
+        if (gaw != nullptr) gaw[o] = (coord_t)pa;
+        if (gloc != nullptr) gloc[o] = (coord_t)(pl * (acc_t)a) * t.gmul;
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -611,9 +679,9 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
   return launch_status("forward");
 }
 
-// backward workspace: [rowinfo int2 x B*M*S][entries Entry x B*M*L*2*Lq*P][d coord x B*Lq*M*L*P*2]
+// backward workspace: [rowinfo int2 x B*M*S][entries Entry x B*M*L*2*Lq*P]
 struct BwdLayout {
-  size_t rowinfo, entries, dbuf, total;
+  size_t rowinfo, entries, total;
 };
 
 size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -625,8 +693,8 @@ BwdLayout bwd_layout(int value_dtype, long long B, long long S, long long M, lon
   BwdLayout w;
   w.rowinfo = 0;
   w.entries = align_up((size_t)B * M * S * sizeof(int2));
-  w.dbuf = w.entries + align_up((size_t)B * M * L * 2 * Lq * P * es);
-  w.total = w.dbuf + align_up((size_t)B * Lq * M * L * P * 2 * cs);
+  w.total = w.entries + align_up((size_t)B * M * L * 2 * Lq * P * es);
+  (void)cs;
   return w;
 }
 
@@ -652,12 +720,54 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
   auto* ws = static_cast<unsigned char*>(workspace);
   auto* rowinfo = reinterpret_cast<int2*>(ws + wl.rowinfo);
   auto* entries = reinterpret_cast<Entry<coord_t>*>(ws + wl.entries);
-  auto* dbuf = reinterpret_cast<coord_t*>(ws + wl.dbuf);
   auto* lc = static_cast<const coord_t*>(loc);
   auto* a = static_cast<const coord_t*>(aw);
   const bool z = pad == MSDA_PAD_ZEROS;
-  const bool need_d = gloc != nullptr || gaw != nullptr;
   int rc;
+
+  // grad_loc / grad_attn: item kernel (independent of the sort / pull pair)
+  if (gloc != nullptr || gaw != nullptr) {
+    const long long n_items = pr.B * pr.Lq * pr.M;
+    if (n_items > 0) {
+      constexpr int VEC = 16 / (int)sizeof(scalar_t);
+      const bool vec_ok = pr.D % VEC == 0;
+      const long long nchunk = vec_ok ? pr.D / VEC : pr.D;
+      int G = 1;
+      while (G < nchunk && G < 64) G <<= 1;
+      const bool one = nchunk <= G;
+      const long long threads = n_items * G;
+      const unsigned blocks = (unsigned)((threads + 255) / 256);
+      auto* v = static_cast<const scalar_t*>(value);
+      auto* g = static_cast<const scalar_t*>(gout);
+      auto* gl = static_cast<coord_t*>(gloc);
+      auto* ga = static_cast<coord_t*>(gaw);
+#define MSDA_CO(V, GG, Z, ONE)                                                                     \
+  hipLaunchKernelGGL((msda_bwd_coord_kernel<scalar_t, coord_t, V, GG, Z, ONE>), dim3(blocks),        \
+                     dim3(256), 0, st, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, \
+                     (int)pr.M, (int)pr.D, (int)pr.Lq, n_items)
+#define MSDA_CO_G(V, Z, ONE)                                                                       \
+  switch (G) {                                                                                   \
+    case 1: MSDA_CO(V, 1, Z, ONE); break;                                                        \
+    case 2: MSDA_CO(V, 2, Z, ONE); break;                                                        \
+    case 4: MSDA_CO(V, 4, Z, ONE); break;                                                        \
+    case 8: MSDA_CO(V, 8, Z, ONE); break;                                                        \
+    case 16: MSDA_CO(V, 16, Z, ONE); break;                                                      \
+    case 32: MSDA_CO(V, 32, Z, ONE); break;                                                      \
+    default: MSDA_CO(V, 64, Z, ONE); break;                                                      \
+  }
+      if (vec_ok) {
+        if (z) { if (one) { MSDA_CO_G(VEC, true, true) } else { MSDA_CO_G(VEC, true, false) } }
+        else { if (one) { MSDA_CO_G(VEC, false, true) } else { MSDA_CO_G(VEC, false, false) } }
+      } else {
+        if (z) { if (one) { MSDA_CO_G(1, true, true) } else { MSDA_CO_G(1, true, false) } }
+        else { if (one) { MSDA_CO_G(1, false, true) } else { MSDA_CO_G(1, false, false) } }
+      }
+#undef MSDA_CO_G
+#undef MSDA_CO
+      if ((rc = launch_status("backward coords"))) return rc;
+    }
+  }
+  if (gval == nullptr) return MSDA_OK;
 
   // 1. sort: one workgroup per (b, m, level)
   {
@@ -701,43 +811,32 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
       else if (lpr == 64) ns = 1;
       else if (lpr < 8) ns = 0;  // narrow heads: generic
     }
+    PullOrder po;
+    for (int l = 0; l < pr.L; ++l) po.lvl[l] = l;
+    std::stable_sort(po.lvl, po.lvl + pr.L, [&](int x, int y) { return pr.lv.T[x] < pr.lv.T[y]; });
+    po.cum[0] = 0;
+    for (int i = 0; i < pr.L; ++i) po.cum[i + 1] = po.cum[i] + pr.B * pr.M * pr.lv.T[po.lvl[i]];
+    for (int i = pr.L; i < MSDA_MAX_LEVELS; ++i) po.cum[i + 1] = 0x7fffffffffffffffll;
     const int nse = ns > 0 ? ns : 1;
     const long long waves = (nrows + nse - 1) / nse;
     const unsigned blocks = (unsigned)((waves + 3) / 4);
-    auto* v = static_cast<const scalar_t*>(value);
     auto* g = static_cast<const scalar_t*>(gout);
     auto* gv = static_cast<scalar_t*>(gval);
-#define MSDA_PULL(NSL, ND)                                                                         \
-  hipLaunchKernelGGL((msda_bwd_pull_kernel<scalar_t, coord_t, NSL, ND>), dim3(blocks),            \
-                     dim3(kPullThreads), 0, st, v, g, rowinfo, entries, gv, dbuf, pr.lv, (int)pr.L, \
-                     (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, nrows)
+#define MSDA_PULL(NSL)                                                                          \
+  hipLaunchKernelGGL((msda_bwd_pull_kernel<scalar_t, coord_t, NSL>), dim3(blocks),               \
+                     dim3(kPullThreads), 0, st, g, rowinfo, entries, gv, (int)pr.S, (int)pr.M,     \
+                     (int)pr.D, (int)pr.Lq, (int)pr.P, nrows, pr.lv, po)
     switch (ns) {
-      case 8: if (need_d) MSDA_PULL(8, true); else MSDA_PULL(8, false); break;
-      case 4: if (need_d) MSDA_PULL(4, true); else MSDA_PULL(4, false); break;
-      case 2: if (need_d) MSDA_PULL(2, true); else MSDA_PULL(2, false); break;
-      case 1: if (need_d) MSDA_PULL(1, true); else MSDA_PULL(1, false); break;
-      default: if (need_d) MSDA_PULL(0, true); else MSDA_PULL(0, false); break;
+      case 8: MSDA_PULL(8); break;
+      case 4: MSDA_PULL(4); break;
+      case 2: MSDA_PULL(2); break;
+      case 1: MSDA_PULL(1); break;
+      default: MSDA_PULL(0); break;
     }
 #undef MSDA_PULL
     if ((rc = launch_status("backward pull"))) return rc;
   }
 
-  // 3. coordinates
-  if (need_d) {
-    const long long n = pr.B * pr.Lq * pr.M * pr.L * pr.P;
-    if (n > 0) {
-      const unsigned blocks = (unsigned)((n + 255) / 256);
-      auto* gl = static_cast<coord_t*>(gloc);
-      auto* ga = static_cast<coord_t*>(gaw);
-      if (z)
-        hipLaunchKernelGGL((msda_bwd_coord_kernel<coord_t, true>), dim3(blocks), dim3(256), 0, st,
-                           lc, a, dbuf, gl, ga, pr.lv, (int)pr.L, (int)pr.P, n);
-      else
-        hipLaunchKernelGGL((msda_bwd_coord_kernel<coord_t, false>), dim3(blocks), dim3(256), 0, st,
-                           lc, a, dbuf, gl, ga, pr.lv, (int)pr.L, (int)pr.P, n);
-      if ((rc = launch_status("backward coord"))) return rc;
-    }
-  }
   return MSDA_OK;
 }
 
