@@ -8,11 +8,14 @@
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = one training iteration over one synthetic batch per GPU (8 clips): bf16 autocast
-forward, backward, DDP gradient all-reduce over RCCL (N > 1), clip_grad_norm_(0.1) and
-AdamW (reference engine.py:86-134, main.py:98).  Inputs are resident in HBM before timing.
+forward, backward, gradient all-reduce over RCCL (N > 1, one flat fp32 buffer),
+clip_grad_norm_(0.1) and AdamW (reference engine.py:86-134, main.py:98), replayed as two
+HIP graphs around the all-reduce (train_step.py; --graph 0 runs it eagerly).  Inputs are
+resident in HBM before timing.
 Prints ONE JSON line on rank 0, including
-  roofline     — the dominant MSDA kernel's algorithmic bytes / its average launch time,
-                 timed with HIP events on the launch stream over the timed region;
+  roofline     — the dominant MSDA launch's algorithmic bytes / its average duration, timed
+                 with HIP events on the launch stream around every MSDA C-ABI call of
+                 --timer-steps eager steps run right after the timed graph replays;
   cpu_baseline — the reference's pure-PyTorch CPU path (oracle: per-level grid_sample core
                  + the same stock-PyTorch layers, fp32) timed on this host, rank 0, N=1.
 """
@@ -47,6 +50,8 @@ def parse():
     p.add_argument("--dropout", type=float, default=0.1)
     p.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU reference path (rank 0, N=1)")
     p.add_argument("--cpu-clips", type=int, default=3)
+    p.add_argument("--graph", type=int, default=1, help="1: replay the step as HIP graphs (train_step.py)")
+    p.add_argument("--timer-steps", type=int, default=2, help="eager steps timed per MSDA launch (roofline)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                    help="per-launch HBM bytes from rocprofv3 PMC passes (profiles/), if present")
     return p.parse_args()
@@ -74,18 +79,6 @@ def usable_cores():
 def build_model(args, device):
     torch.manual_seed(0)
     return PKG.dvc_core.DeformableDVCCore(d_model=512, num_queries=args.queries, dropout=args.dropout).to(device)
-
-
-def train_step(model, opt, batch, use_bf16):
-    video, mask, durations = batch
-    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=use_bf16):
-        out = model(video, mask, durations)
-        loss = PKG.dvc_core.workload_loss(out)
-    loss.backward()
-    torch.nn.utils.clip_grad_norm_(model.parameters(), 0.1)
-    opt.step()
-    opt.zero_grad(set_to_none=True)
-    return loss
 
 
 def cpu_baseline(args):
@@ -124,7 +117,9 @@ def roofline(summary, traffic):
     achieved = d["bytes_per_launch"] / (d["avg_ms"] * 1e-3) / 1e9
     name = f"msda_{kind}_S{key[0]}_Lq{key[1]}"
     tr = traffic.get(name) if traffic else None
-    return {"bound": "hbm", "kernel": name, "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+    return {"bound": "hbm", "kernel": name,
+            "timing": "HIP events around each MSDA C-ABI call (sort+pull+coord kernels for bwd) on its "
+                      "launch stream, eager steps after the timed region", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": tr,
             "algorithmic_bytes_per_launch": d["bytes_per_launch"], "avg_launch_ms": round(d["avg_ms"], 5),
             "launches": d["launches"],
@@ -145,24 +140,24 @@ def main():
     PKG._native.load_library()  # fail loudly before anything else if the HIP library is missing
 
     model = build_model(args, device)
-    if world > 1:
-        model = torch.nn.parallel.DistributedDataParallel(model, device_ids=[local_rank], gradient_as_bucket_view=True,
-                                                          bucket_cap_mb=64)
-    opt = torch.optim.AdamW(model.parameters(), lr=1e-4, weight_decay=1e-4)
-    batch = PKG.dvc_core.synthetic_clips(args.batch, T=args.T, seed=1000 + rank, device=device)
+    if world > 1:  # identical initial weights on every rank (the reference's DDP broadcast)
+        for t in list(model.parameters()) + list(model.buffers()):
+            dist.broadcast(t.data, src=0)
     use_bf16 = args.dtype == "bf16"
+    trainer = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, lr=1e-4, weight_decay=1e-4,
+                                             max_norm=0.1, use_bf16=use_bf16, graph=bool(args.graph))
+    batch = PKG.dvc_core.synthetic_clips(args.batch, T=args.T, seed=1000 + rank, device=device)
 
+    trainer.capture(batch)  # eager warm-up steps + graph capture (no-op without --graph)
     for _ in range(args.warmup):
-        train_step(model, opt, batch, use_bf16)
+        trainer.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    timer = PKG.msda.KernelTimer()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with timer:
-        for _ in range(args.steps):
-            train_step(model, opt, batch, use_bf16)
+    for _ in range(args.steps):
+        trainer.step(batch)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -172,6 +167,14 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    # MSDA launch durations: HIP events around every C-ABI call, on the launch stream, over
+    # eager steps of the same workload (events cannot bracket kernels inside a graph replay;
+    # the kernels and their inputs are the same ones the graph replays)
+    timer = PKG.msda.KernelTimer()
+    with timer:
+        for _ in range(args.timer_steps):
+            trainer.eager_step(batch)
+    torch.cuda.synchronize()
     summary = timer.summary()
     if rank == 0:
         traffic = {}
@@ -191,7 +194,8 @@ def main():
                                    "100 queries; BaseEncoder + 6 enc + 6 dec + heads, AdamW step",
                        "model": "DeformableDVCCore (UnimodalDeformableDVC proposal path)",
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch, "seq_len": args.T,
-                       "d_model": 512, "levels": 4, "queries": args.queries, "parallelism": f"dp{world}"},
+                       "d_model": 512, "levels": 4, "queries": args.queries, "parallelism": f"dp{world}",
+                       "execution": "hip_graph" if args.graph else "eager"},
             "roofline": roofline(summary, traffic),
             "cpu_baseline": None,
         }

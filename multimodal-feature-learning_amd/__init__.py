@@ -8,6 +8,7 @@ Layout:
   msda.py              host checks, layout normalisation, autograd.Function
   MultiScaleDeformableAttention.py   mirror of the reference's pybind extension API
   models/...           mirror of the reference modules on the path (same names / signatures)
+  train_step.py        flat-gradient data-parallel step, HIP-graph captured (bench.py)
 
 The directory name is not a Python identifier; import it with
 ``importlib.import_module("multimodal-feature-learning_amd")``.  The import registers
@@ -28,6 +29,7 @@ from .models.deformable import multimodal_deformable_transformer  # noqa: E402,F
 from .models.ops.functions import ms_deform_attn_func  # noqa: E402,F401
 from .models.ops.modules import ms_deform_attn  # noqa: E402,F401
 from . import dvc_core  # noqa: E402,F401
+from . import train_step  # noqa: E402,F401
 
 ALIAS = "mfl_amd"
 

@@ -26,10 +26,19 @@ __all__ = [
 ]
 
 
+_LEVEL_CACHE = {}
+
+
 def level_metadata(lengths, device):
     """(temporal_shapes, level_start_index) as int64 device tensors tagged with host tuples
-    (reference unimodal_deformable_transformer.py:129-130 builds the same two tensors)."""
+    (reference unimodal_deformable_transformer.py:129-130 builds the same two tensors).
+    Cached per (lengths, device): read-only, and no host->device copy inside a step (so the
+    step can be captured in a HIP graph)."""
     lengths = tuple(int(t) for t in lengths)
+    key = (lengths, str(torch.device(device)))
+    hit = _LEVEL_CACHE.get(key)
+    if hit is not None:
+        return hit
     starts, run = [], 0
     for t in lengths:
         starts.append(run)
@@ -38,6 +47,7 @@ def level_metadata(lengths, device):
     starts_t = torch.tensor(starts, dtype=torch.long, device=device)
     shapes_t._mfl_host = lengths
     starts_t._mfl_host = tuple(starts)
+    _LEVEL_CACHE[key] = (shapes_t, starts_t)
     return shapes_t, starts_t
 
 

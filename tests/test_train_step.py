@@ -1,0 +1,141 @@
+"""The bench's training step (train_step.FlatGradTrainer): flat-gradient fwd+bwd, gradient
+all-reduce, clip_grad_norm_ + AdamW.
+
+CPU (no marker): the eager step equals the textbook PyTorch step (model.backward, clip,
+AdamW), and the world_size-2 gloo run — each rank one clip, one flat all-reduce — equals the
+single-process step on both clips, i.e. the reference's DDP semantics (gradients averaged
+over ranks, main.py:55,98).  The MSDA core runs through the oracle on the CPU.
+GPU (-m gpu): the HIP-graph replay of the step equals the eager step.
+"""
+import copy
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import PKG, ROOT
+
+SMALL = dict(d_model=64, num_queries=6, feature_dim=64, enc_layers=1, dec_layers=1, ff_dim=128, dropout=0.0,
+             num_classes=5)
+
+
+def _model(device="cpu"):
+    torch.manual_seed(0)
+    return PKG.dvc_core.DeformableDVCCore(**SMALL).to(device)
+
+
+def _batch(n, device="cpu"):
+    return PKG.dvc_core.synthetic_clips(n, T=32, feature_dim=64, padded=True, seed=3, device=device)
+
+
+def _params(model):
+    return {k: v.detach().clone().cpu() for k, v in model.named_parameters()}
+
+
+def test_eager_step_matches_textbook_step():
+    from oracle.cpu_model import oracle_core
+    batch = _batch(2)
+    ref = _model()
+    opt = torch.optim.AdamW(ref.parameters(), lr=1e-3, weight_decay=1e-4)
+    mine = copy.deepcopy(ref)
+    tr = PKG.train_step.FlatGradTrainer(mine, PKG.dvc_core.workload_loss, lr=1e-3, weight_decay=1e-4,
+                                        max_norm=0.1, use_bf16=False, graph=False)
+    with oracle_core(PKG):
+        for _ in range(2):
+            PKG.dvc_core.workload_loss(ref(*batch)).backward()
+            torch.nn.utils.clip_grad_norm_(ref.parameters(), 0.1)
+            opt.step()
+            opt.zero_grad(set_to_none=True)
+            tr.eager_step(batch)
+    a, b = _params(ref), _params(mine)
+    for k in a:
+        torch.testing.assert_close(b[k], a[k], rtol=1e-5, atol=1e-6, msg=k)
+    # every parameter got a gradient view into the single flat buffer
+    assert all(p.grad.data_ptr() >= tr.flat_grad.data_ptr() for p in tr.params)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_main(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import importlib
+    pkg = importlib.import_module("multimodal-feature-learning_amd")
+    from oracle.cpu_model import oracle_core
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        model = pkg.dvc_core.DeformableDVCCore(**SMALL)
+        video, mask, dur = pkg.dvc_core.synthetic_clips(2, T=32, feature_dim=64, padded=True, seed=3)
+        shard = (video[rank:rank + 1], mask[rank:rank + 1], dur[rank:rank + 1])
+        tr = pkg.train_step.FlatGradTrainer(model, pkg.dvc_core.workload_loss, lr=1e-3, weight_decay=1e-4,
+                                            max_norm=0.1, use_bf16=False, graph=False)
+        assert tr.world == world
+        with oracle_core(pkg):
+            tr._forward_backward(shard)
+            tr._allreduce()
+            grad = tr.flat_grad.clone()
+            tr._update()
+            tr.eager_step(shard)
+        torch.save({"grad": grad, "params": {k: v.detach() for k, v in model.named_parameters()}},
+                   f"{out_path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_two_ranks_equal_full_batch_step():
+    """Each rank one clip; after the flat all-reduce every rank holds the gradient of the
+    two-clip batch averaged over ranks (compared before AdamW, whose sign-like first steps
+    would amplify fp32 summation-order noise), and the ranks' parameters stay identical."""
+    from oracle.cpu_model import oracle_core
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "params")
+        mp.start_processes(_rank_main, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+        r0 = torch.load(out + ".0", weights_only=True)
+        r1 = torch.load(out + ".1", weights_only=True)
+    ref = _model()
+    tr = PKG.train_step.FlatGradTrainer(ref, lambda o: PKG.dvc_core.workload_loss(o) / 2, lr=1e-3,
+                                        weight_decay=1e-4, max_norm=0.1, use_bf16=False, graph=False)
+    with oracle_core(PKG):
+        tr._forward_backward(_batch(2))
+    full = tr.flat_grad
+    assert torch.equal(r0["grad"], r1["grad"])
+    err = (r0["grad"] - full).abs().max().item()
+    assert err <= 1e-5 * full.abs().max().item(), (err, full.abs().max().item())
+    for k in r0["params"]:
+        assert torch.equal(r0["params"][k], r1["params"][k]), k
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bf16", [False, True])
+def test_graph_replay_matches_eager_step(dev, bf16):
+    """The captured fwd+bwd graph produces the eager step's loss and flat gradient on the
+    same parameters; the update graph then applies clip + AdamW like the eager update."""
+    batch = _batch(2, dev)
+    model = _model(dev)
+    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, lr=1e-3, max_norm=0.1, use_bf16=bf16,
+                                        graph=True)
+    tr.capture(batch, warmup=1)
+    tr._g_fb.replay()
+    loss_g, grad_g = tr._loss.clone(), tr.flat_grad.clone()
+    loss_e = tr._forward_backward(batch)
+    grad_e = tr.flat_grad.clone()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss_g, loss_e, rtol=1e-5, atol=1e-5)
+    err = (grad_g - grad_e).abs().max().item()
+    assert err <= 1e-4 * grad_e.abs().max().item(), (err, grad_e.abs().max().item())
+    before = _params(model)
+    tr._g_up.replay()
+    torch.cuda.synchronize()
+    after = _params(model)
+    assert any(not torch.equal(before[k], after[k]) for k in before)
+    assert all(torch.isfinite(v).all() for v in after.values())
