@@ -177,7 +177,8 @@ def test_gradcheck_fp64(dev, channels):
 
 def test_full_size_properties(dev):
     """At the bench's size (B=8, T=1024 encoder call) where the oracle is too slow to run
-    whole: linearity in value and the grad_value checksum
+    whole: linearity in value and in aw, the adjoint identity <g, fwd(v)> = <bwd_value(g), v>,
+    and the grad_value checksum
     sum_s grad_value[b,s,m,:] = sum_q (sum_{l,p} aw[b,q,m,l,p]) grad_out[b,q,m,:] (border
     weights of a sample sum to 1); plus oracle parity on one clip."""
     shapes, B, M, D, P = [1024, 512, 256, 128], 8, 8, 64, 4
@@ -194,5 +195,14 @@ def test_full_size_properties(dev):
     lhs = gv.double().sum(1)                                               # (B, M, D)
     rhs = (aw.double().sum((-1, -2))[..., None] * gout.double().view(B, Lq, M, D)).sum(1)
     torch.testing.assert_close(lhs.cpu(), rhs, rtol=1e-4, atol=1e-3)
+    # adjoint: grad_value is the transpose of the forward's linear map in value
+    dot_fwd = (o1.double() * c(gout).double()).sum().item()
+    dot_bwd = (gv.double() * c(v1).double()).sum().item()
+    assert abs(dot_fwd - dot_bwd) <= 1e-4 * abs(dot_fwd) + 1e-3, (dot_fwd, dot_bwd)
+    # linearity in the attention weights
+    aw2 = torch.rand_like(aw)
+    oa = msda.msda_forward(c(v1), shapes, starts, c(loc), c(aw2))
+    oab = msda.msda_forward(c(v1), shapes, starts, c(loc), c(aw + 0.5 * aw2))
+    torch.testing.assert_close(oab, o1 + 0.5 * oa, rtol=1e-4, atol=1e-4)
     r_out = O.msda_forward(_np(v1[:1]), shapes, _np(loc[:1]), _np(aw[:1]))
     np.testing.assert_allclose(o1[:1].cpu().numpy(), r_out, rtol=2e-5, atol=2e-5)
