@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include <stdint.h>
@@ -54,6 +55,16 @@ struct Levels {
   int T[MSDA_MAX_LEVELS];
   int start[MSDA_MAX_LEVELS];
 };
+
+// XCD-aware block order (MI355X_MICROARCH.md, workgroup dispatch; cdna guide T1): blocks are
+// dealt round-robin over the 8 XCDs, each with a private 4 MB L2.  Renumber so that the
+// blocks sharing an XCD get one contiguous range of logical ids: a clip's value / grad_out
+// rows (2 MB in bf16 at the bench shape) then stay in one XCD's L2 instead of being fetched
+// by all eight.  Bijective for any block count; speed only, never correctness.
+__device__ __forceinline__ unsigned xcd_block(unsigned orig, unsigned nwg) {
+  const unsigned xcd = orig % 8u, q = nwg / 8u, r = nwg % 8u;
+  return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + orig / 8u;
+}
 
 // ---------------------------------------------------------------------------------
 // storage types and 16-byte vector I/O
@@ -120,6 +131,19 @@ __device__ __forceinline__ void store_vec(scalar_t* __restrict__ p,
 #pragma unroll
     for (int i = 0; i < VEC; ++i) from_acc(r[i], &p[i]);
   }
+}
+
+// One 16-byte row fragment kept raw (4 VGPRs) until it is consumed; zero when not loaded.
+template <typename scalar_t>
+__device__ __forceinline__ uint4 load16_if(bool ok, const scalar_t* __restrict__ p) {
+  return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
+}
+template <typename scalar_t, int VEC>
+__device__ __forceinline__ void cvt16(const uint4& raw, typename AccOf<scalar_t>::type (&r)[VEC]) {
+  static_assert(VEC * sizeof(scalar_t) == 16, "16-byte fragment");
+  const scalar_t* e = reinterpret_cast<const scalar_t*>(&raw);
+#pragma unroll
+  for (int i = 0; i < VEC; ++i) r[i] = to_acc(e[i]);
 }
 
 // ---------------------------------------------------------------------------------
@@ -198,7 +222,7 @@ __global__ __launch_bounds__(256) void msda_fwd_kernel(
     const int P, const int S, const int M, const int D, const int Lq, const long long n_items,
     const int gshift) {
   using acc_t = typename AccOf<scalar_t>::type;
-  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long tid = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const long long item = tid >> gshift;
   if (item >= n_items) return;
   const int G = 1 << gshift;
@@ -235,6 +259,75 @@ __global__ __launch_bounds__(256) void msda_fwd_kernel(
     }
     store_vec<scalar_t, VEC>(op + ck * VEC, acc);
   }
+}
+
+// Forward fast path: fp32 coordinates, L*P <= 16 with L*P % 4 == 0 (the reference's 4 levels
+// x 4 points), D = G * VEC (every lane owns one 16-byte chunk).  The item's 2*L*P coordinates
+// are loaded up front as float4s (one dependent round trip instead of one per sample), and
+// the 8 row fragments of 4 samples are in flight together, kept raw until use.
+constexpr int kLPMax = 16;
+
+template <int N>
+__device__ __forceinline__ void load_coords16(const float* __restrict__ p, int LP, float (&r)[N]) {
+#pragma unroll
+  for (int c = 0; c < N / 4; ++c) {
+    if (4 * c < LP) {
+      const float4 x = reinterpret_cast<const float4*>(p)[c];
+      r[4 * c] = x.x; r[4 * c + 1] = x.y; r[4 * c + 2] = x.z; r[4 * c + 3] = x.w;
+    } else {
+      r[4 * c] = r[4 * c + 1] = r[4 * c + 2] = r[4 * c + 3] = 0.f;
+    }
+  }
+}
+
+template <typename scalar_t, int VEC, int G, bool ZEROS>
+__global__ __launch_bounds__(256) void msda_fwd16_kernel(
+    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    scalar_t* __restrict__ out, const Levels lv, const int L, const int P, const int S, const int M,
+    const int D, const int Lq, const long long n_items) {
+  using acc_t = float;
+  const long long tid = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const long long item = tid / G;
+  if (item >= n_items) return;
+  const int lg = (int)(tid % G);
+  const int m = (int)(item % M);
+  const long long b = item / M / Lq;
+  const long long rowstride = (long long)M * D;
+  const int LP = L * P;
+  float lr[kLPMax], ar[kLPMax];
+  load_coords16(loc + item * LP, LP, lr);
+  load_coords16(aw + item * LP, LP, ar);
+  const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D + lg * VEC;
+  acc_t acc[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+#pragma unroll
+  for (int j0 = 0; j0 < kLPMax; j0 += 4) {
+    if (j0 < LP) {
+      uint4 r0[4], r1[4];
+      float w0[4], w1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int l = (j0 + u) / P;
+        const Taps<float> t = make_taps<float, ZEROS>(lr[j0 + u], lv.T[l]);
+        const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rowstride;
+        r0[u] = load16_if(t.ok0, vl + t.i0 * rowstride);
+        r1[u] = load16_if(t.ok1, vl + t.i1 * rowstride);
+        w0[u] = t.w0;
+        w1[u] = t.w1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        acc_t x0[VEC], x1[VEC];
+        cvt16<scalar_t, VEC>(r0[u], x0);
+        cvt16<scalar_t, VEC>(r1[u], x1);
+        const float aa = ar[j0 + u];
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) acc[e] += aa * (x0[e] * w0[u] + x1[e] * w1[u]);
+      }
+    }
+  }
+  store_vec<scalar_t, VEC>(out + item * D + lg * VEC, acc);
 }
 
 // ---------------------------------------------------------------------------------
@@ -301,8 +394,9 @@ __global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
     Entry<coord_t>* __restrict__ entries, const Levels lv, const int L, const int P, const int S,
     const int M, const int Lq, const int sort_rows) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
-  const int l = (int)(blockIdx.x % (unsigned)L);
-  const long long bm = blockIdx.x / (unsigned)L;
+  const unsigned blk = xcd_block(blockIdx.x, gridDim.x);
+  const int l = (int)(blk % (unsigned)L);
+  const long long bm = blk / (unsigned)L;
   const int m = (int)(bm % M);
   const long long b = bm / M;
   const int T = lv.T[l];
@@ -421,9 +515,10 @@ __device__ __forceinline__ double group_sum(double x) {
 
 constexpr int kPullThreads = 256;
 
-// Row order of the pull: levels by decreasing taps per row (T ascending: a level's rows all
-// receive ~2*Lq*P/T_l taps), so the longest-running waves start first instead of forming the
-// tail of the launch.  Rows of level lvl[i] occupy [cum[i], cum[i+1]) as (b*M + m, s).
+// Row order of the pull: clip-major (with the XCD block order, a clip's grad_out rows stay in
+// one L2), then levels by decreasing taps per row (T ascending: a level's rows all receive
+// ~2*Lq*P/T_l taps), so the longest-running waves start first instead of forming the tail.
+// Inside a clip, rows of level lvl[i] occupy [cum[i], cum[i+1]) as (m, s).
 struct PullOrder {
   int lvl[MSDA_MAX_LEVELS];
   long long cum[MSDA_MAX_LEVELS + 1];
@@ -446,16 +541,20 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
   const int lane = threadIdx.x & 63;
   const int slot = lane / LPR;
   const int cl = lane - slot * LPR;
-  const long long wave_id = ((long long)blockIdx.x * kPullThreads + threadIdx.x) >> 6;
+  const long long wave_id = ((long long)xcd_block(blockIdx.x, gridDim.x) * kPullThreads + threadIdx.x) >> 6;
   const long long row = wave_id * NS + slot;  // (b, m, s) flattened as (b*M + m)*S + s
   const bool valid = row < nrows;
   const long long ro = valid ? row : 0;
+  const long long ms = (long long)M * S;
+  const long long bq = ro / ms;
+  const long long rem = ro - bq * ms;
   int i = 0;
-  while (ro >= po.cum[i + 1]) ++i;
+  while (rem >= po.cum[i + 1]) ++i;
   const int l = po.lvl[i];
-  const long long off = ro - po.cum[i];
-  const long long bm = off / lv.T[l];
-  const int s = lv.start[l] + (int)(off - bm * lv.T[l]);
+  const long long off = rem - po.cum[i];
+  const long long mq = off / lv.T[l];
+  const int s = lv.start[l] + (int)(off - mq * lv.T[l]);
+  const long long bm = bq * M + mq;
   const long long rr = bm * S + s;
   const int m = (int)(bm % M);
   const long long b = bm / M;
@@ -511,6 +610,249 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
   }
 }
 
+// Fused sort + pull: one 1024-thread workgroup per (b, m, level) builds the level's per-row
+// entry lists in LDS exactly as msda_bwd_sort_kernel does, then pulls every value row of the
+// level from them (the pull kernel's lane layout: NS rows per wave, 16 B per lane).  The entry
+// lists never leave LDS, there is no row table, and a single launch replaces two.  Used when
+// the lists fit in LDS (2*Lq*P entries + T_l cursors <= kGvLdsMax) and there are enough
+// (b, m, level) workgroups to fill the chip; otherwise sort + pull.
+constexpr int kGvThreads = 1024;
+constexpr long long kGvLdsMax = 160 * 1024;
+constexpr int kGvCache = 8;  // samples per thread whose loc / aw stay in registers between passes
+
+template <typename scalar_t, typename coord_t, int NSLOT, bool ZEROS>
+__global__ __launch_bounds__(kGvThreads) void msda_bwd_gvalue_kernel(
+    const coord_t* __restrict__ loc, const coord_t* __restrict__ aw,
+    const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, const Levels lv,
+    const int L, const int P, const int S, const int M, const int D, const int Lq,
+    const int sort_rows) {
+  using acc_t = typename AccOf<scalar_t>::type;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const unsigned blk = xcd_block(blockIdx.x, gridDim.x);
+  const int l = (int)(blk % (unsigned)L);
+  const long long bm = blk / (unsigned)L;
+  const int m = (int)(bm % M);
+  const long long b = bm / M;
+  const int T = lv.T[l];
+  const int ncap = 2 * Lq * P;
+#ifdef MSDA_PHASE_TIMING  // debug build only: per-phase wall clock of two workgroups
+  unsigned long long tph[6];
+  tph[0] = wall_clock64();
+#define MSDA_PH(i) do { __syncthreads(); tph[i] = wall_clock64(); } while (0)
+#else
+#define MSDA_PH(i) do { } while (0)
+#endif
+  Entry<coord_t>* ent = reinterpret_cast<Entry<coord_t>*>(smem_raw);
+  int* cur = reinterpret_cast<int*>(smem_raw + (size_t)ncap * sizeof(Entry<coord_t>));
+  int* scratch = cur + T;
+
+  for (int i = threadIdx.x; i < T; i += kGvThreads) cur[i] = 0;
+  __syncthreads();
+  MSDA_PH(1);
+
+  const int LP = L * P;
+  const long long qs = (long long)M * LP;
+  const coord_t* __restrict__ locb = loc + (b * Lq * M + m) * LP + l * P;
+  const coord_t* __restrict__ awb = aw + (b * Lq * M + m) * LP + l * P;
+  const int nsamp = Lq * P;
+
+  // pass 1: taps per row; the first kGvCache samples of every thread keep loc / aw in registers
+  coord_t cl[kGvCache], ca[kGvCache];
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) {
+      const int q = s / P, p = s - (s / P) * P;
+      cl[k] = locb[q * qs + p];
+      ca[k] = awb[q * qs + p];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) {
+      const Taps<coord_t> t = make_taps<coord_t, ZEROS>(cl[k], T);
+      if (t.ok0) atomicAdd(&cur[t.i0], 1);
+      if (t.ok1) atomicAdd(&cur[t.i1], 1);
+    }
+  }
+  for (int s = threadIdx.x + kGvCache * kGvThreads; s < nsamp; s += kGvThreads) {
+    const int q = s / P, p = s - (s / P) * P;
+    const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qs + p], T);
+    if (t.ok0) atomicAdd(&cur[t.i0], 1);
+    if (t.ok1) atomicAdd(&cur[t.i1], 1);
+  }
+  __syncthreads();
+  MSDA_PH(2);
+
+  // exclusive scan over rows: thread i owns rows [i*chunk, (i+1)*chunk)
+  const int chunk = (T + kGvThreads - 1) / kGvThreads;
+  const int lo = min((int)threadIdx.x * chunk, T), hi = min(lo + chunk, T);
+  int mine = 0;
+  for (int i = lo; i < hi; ++i) mine += cur[i];
+  int total = 0;
+  int run = block_exclusive_scan(mine, scratch, &total);
+  for (int i = lo; i < hi; ++i) {
+    const int c = cur[i];
+    cur[i] = run;
+    run += c;
+  }
+  __syncthreads();
+  MSDA_PH(3);
+
+  // pass 2: place the entries (cur[i] ends at the end of row i)
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) {
+      const Taps<coord_t> t = make_taps<coord_t, ZEROS>(cl[k], T);
+      if (t.ok0) ent[atomicAdd(&cur[t.i0], 1)] = Entry<coord_t>{(s << 1), ca[k] * t.w0};
+      if (t.ok1) ent[atomicAdd(&cur[t.i1], 1)] = Entry<coord_t>{(s << 1) | 1, ca[k] * t.w1};
+    }
+  }
+  for (int s = threadIdx.x + kGvCache * kGvThreads; s < nsamp; s += kGvThreads) {
+    const int q = s / P, p = s - (s / P) * P;
+    const coord_t a = awb[q * qs + p];
+    const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qs + p], T);
+    if (t.ok0) ent[atomicAdd(&cur[t.i0], 1)] = Entry<coord_t>{(s << 1), a * t.w0};
+    if (t.ok1) ent[atomicAdd(&cur[t.i1], 1)] = Entry<coord_t>{(s << 1) | 1, a * t.w1};
+  }
+  __syncthreads();
+  MSDA_PH(4);
+  if (sort_rows) {  // deterministic mode: each row's list in tap order (insertion sort)
+    for (int i = lo; i < hi; ++i) {
+      const int e1 = cur[i], e0 = (i == 0 ? 0 : cur[i - 1]);
+      for (int x = e0 + 1; x < e1; ++x) {
+        const Entry<coord_t> key = ent[x];
+        int y = x - 1;
+        while (y >= e0 && ent[y].tap > key.tap) {
+          ent[y + 1] = ent[y];
+          --y;
+        }
+        ent[y + 1] = key;
+      }
+    }
+    __syncthreads();
+  }
+
+  // pull: NS rows per wave-iteration, LPR lanes x CPL channels per row
+  constexpr int CPL = NSLOT > 0 ? 16 / (int)sizeof(scalar_t) : 1;
+  constexpr int NS = NSLOT > 0 ? NSLOT : 1;
+  constexpr int LPR = 64 / NS;
+  constexpr int U = 8;  // grad_out loads in flight per lane
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = lane / LPR;
+  const int c_l = lane - slot * LPR;
+  const long long gq = (long long)M * D;
+  const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D;
+  scalar_t* __restrict__ gvl = gval + ((b * S + lv.start[l]) * M + m) * (long long)D;
+  const int npass = NSLOT > 0 ? 1 : (D + 63) / 64;
+  for (int r0 = wave * NS; r0 < T; r0 += (kGvThreads / 64) * NS) {
+    const int row = r0 + slot;
+    const bool valid = row < T;
+    const int e0 = valid ? (row == 0 ? 0 : cur[row - 1]) : 0;
+    const int count = valid ? cur[row] - e0 : 0;
+    for (int pass = 0; pass < npass; ++pass) {
+      const int c0 = NSLOT > 0 ? c_l * CPL : pass * 64 + lane;
+      const bool on = valid && c0 < D;
+      acc_t acc[CPL];
+#pragma unroll
+      for (int e = 0; e < CPL; ++e) acc[e] = (acc_t)0;
+      for (int j0 = 0; __ballot(j0 < count) != 0ull; j0 += U) {
+        acc_t w[U], g[U][CPL];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool have = j0 + u < count;
+          const Entry<coord_t> e = have ? ent[e0 + j0 + u] : Entry<coord_t>{0, (coord_t)0};
+          w[u] = (acc_t)e.w;
+          const int q = (e.tap >> 1) / P;
+          if (have && on) load_vec<scalar_t, CPL>(gb + q * gq + c0, g[u]);
+          else {
+#pragma unroll
+            for (int x = 0; x < CPL; ++x) g[u][x] = (acc_t)0;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int x = 0; x < CPL; ++x) acc[x] += w[u] * g[u][x];
+        }
+      }
+      if (on) {
+        if constexpr (NSLOT > 0) store_vec<scalar_t, CPL>(gvl + (long long)row * gq + c0, acc);
+        else from_acc(acc[0], gvl + (long long)row * gq + c0);
+      }
+    }
+  }
+#ifdef MSDA_PHASE_TIMING
+  MSDA_PH(5);
+  if (threadIdx.x == 0 && bm == 0)
+    printf("gvalue l=%d T=%d ncap=%d zero=%llu pass1=%llu scan=%llu pass2=%llu pull=%llu (x10ns)\n", l, T,
+           ncap, tph[1] - tph[0], tph[2] - tph[1], tph[3] - tph[2], tph[4] - tph[3], tph[5] - tph[4]);
+#endif
+#undef MSDA_PH
+}
+
+// grad_aw / grad_loc fast path (conditions of msda_fwd16_kernel): coordinates and the
+// item's grad_out chunk loaded once, 4 samples' fragments in flight, DPP reductions.
+template <typename scalar_t, int VEC, int G, bool ZEROS>
+__global__ __launch_bounds__(256) void msda_bwd_coord16_kernel(
+    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    const scalar_t* __restrict__ gout, float* __restrict__ gloc, float* __restrict__ gaw,
+    const Levels lv, const int L, const int P, const int S, const int M, const int D, const int Lq,
+    const long long n_items) {
+  const long long tid = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const long long item_raw = tid / G;
+  const bool active = item_raw < n_items;  // every lane stays for the reductions
+  const long long item = active ? item_raw : 0;
+  const int lg = (int)(tid % G);
+  const int m = (int)(item % M);
+  const long long b = item / M / Lq;
+  const long long rowstride = (long long)M * D;
+  const int LP = L * P;
+  float lr[kLPMax], ar[kLPMax];
+  load_coords16(loc + item * LP, LP, lr);
+  load_coords16(aw + item * LP, LP, ar);
+  float g1[VEC];
+  cvt16<scalar_t, VEC>(load16_if(active, gout + item * D + lg * VEC), g1);
+  const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D + lg * VEC;
+#pragma unroll
+  for (int j0 = 0; j0 < kLPMax; j0 += 4) {
+    if (j0 < LP) {
+      uint4 r0[4], r1[4];
+      Taps<float> t[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int l = (j0 + u) / P;
+        t[u] = make_taps<float, ZEROS>(lr[j0 + u], lv.T[l]);
+        const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rowstride;
+        r0[u] = load16_if(active && t[u].ok0, vl + t[u].i0 * rowstride);
+        r1[u] = load16_if(active && t[u].ok1, vl + t[u].i1 * rowstride);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float x0[VEC], x1[VEC];
+        cvt16<scalar_t, VEC>(r0[u], x0);
+        cvt16<scalar_t, VEC>(r1[u], x1);
+        float pa = 0.f, pl = 0.f;
+#pragma unroll
+        for (int e = 0; e < VEC; ++e) {
+          pa += g1[e] * (x0[e] * t[u].w0 + x1[e] * t[u].w1);
+          pl += g1[e] * (x1[e] - x0[e]);
+        }
+        pa = group_sum<G>(pa);
+        pl = group_sum<G>(pl);
+        const int j = j0 + u;
+        if (active && lg == j % G) {
+          const long long o = item * LP + j;
+          if (gaw != nullptr) gaw[o] = pa;
+          if (gloc != nullptr) gloc[o] = (pl * ar[j]) * t[u].gmul;
+        }
+      }
+    }
+  }
+}
+
 // grad_aw / grad_loc: the forward's item decomposition (G lanes x VEC channels own one
 // (b, q, m) row).  grad_out of the item is loaded once; per sample the two taps are
 // gathered like the forward, the two partial dot products are reduced over the G lanes with
@@ -523,7 +865,7 @@ __global__ __launch_bounds__(256) void msda_bwd_coord_kernel(
     coord_t* __restrict__ gloc, coord_t* __restrict__ gaw, const Levels lv, const int L,
     const int P, const int S, const int M, const int D, const int Lq, const long long n_items) {
   using acc_t = typename AccOf<scalar_t>::type;
-  const long long tid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long tid = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
   const long long item_raw = tid / G;
   const bool active = item_raw < n_items;  // every lane stays for the reductions
   const long long item = active ? item_raw : 0;
@@ -656,6 +998,18 @@ int launch_status(const char* what) {
   return MSDA_OK;
 }
 
+// Lanes per item of the fast (fwd16 / coord16) kernels, or 0 when they do not apply: fp32
+// coordinates, L*P <= 16 and a multiple of 4, D an exact power-of-two number of 16-byte chunks.
+template <typename scalar_t>
+int fast16_group(const Problem& pr) {
+  constexpr int VEC = 16 / (int)sizeof(scalar_t);
+  const long long LP = pr.L * pr.P;
+  if (LP > kLPMax || LP % 4 != 0 || pr.D % VEC != 0) return 0;
+  const long long g = pr.D / VEC;
+  if (g < 1 || g > 64 || (g & (g - 1)) != 0) return 0;
+  return (int)g;
+}
+
 template <typename scalar_t, typename coord_t, int VEC>
 int run_forward(const Problem& pr, const void* value, const void* loc, const void* aw, void* out,
                 int pad, hipStream_t st) {
@@ -668,6 +1022,30 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
   auto* lc = static_cast<const coord_t*>(loc);
   auto* a = static_cast<const coord_t*>(aw);
   auto* o = static_cast<scalar_t*>(out);
+  if constexpr (!std::is_same<coord_t, double>::value && VEC * sizeof(scalar_t) == 16) {
+    const int G = fast16_group<scalar_t>(pr);
+    if (G > 0) {
+      const unsigned fblocks = (unsigned)((n_items * G + 255) / 256);
+#define MSDA_F16(GG, Z)                                                                            \
+  hipLaunchKernelGGL((msda_fwd16_kernel<scalar_t, VEC, GG, Z>), dim3(fblocks), dim3(256), 0, st, v,  \
+                     lc, a, o, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D,        \
+                     (int)pr.Lq, n_items)
+#define MSDA_F16_G(Z)                                                                              \
+  switch (G) {                                                                                   \
+    case 1: MSDA_F16(1, Z); break;                                                               \
+    case 2: MSDA_F16(2, Z); break;                                                               \
+    case 4: MSDA_F16(4, Z); break;                                                               \
+    case 8: MSDA_F16(8, Z); break;                                                               \
+    case 16: MSDA_F16(16, Z); break;                                                             \
+    case 32: MSDA_F16(32, Z); break;                                                             \
+    default: MSDA_F16(64, Z); break;                                                             \
+  }
+      if (pad == MSDA_PAD_ZEROS) { MSDA_F16_G(true) } else { MSDA_F16_G(false) }
+#undef MSDA_F16_G
+#undef MSDA_F16
+      return launch_status("forward");
+    }
+  }
   if (pad == MSDA_PAD_ZEROS)
     hipLaunchKernelGGL((msda_fwd_kernel<scalar_t, coord_t, VEC, true>), dim3(blocks), dim3(256), 0,
                        st, v, lc, a, o, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M,
@@ -698,6 +1076,19 @@ BwdLayout bwd_layout(int value_dtype, long long B, long long S, long long M, lon
   return w;
 }
 
+// Backward path choice, shared by the workspace query and the launcher: the fused gvalue kernel
+// needs no workspace.  MSDA_HIP_BWD_PATH=split forces sort + pull (A/B measurements).
+bool use_fused_gvalue(int value_dtype, long long B, long long S, long long M, long long Lq,
+                      long long L, long long P) {
+  static const int force_split = [] {
+    const char* e = getenv("MSDA_HIP_BWD_PATH");
+    return (e != nullptr && strcmp(e, "split") == 0) ? 1 : 0;
+  }();
+  if (force_split || value_dtype == MSDA_DTYPE_F64) return false;
+  const long long lds = 2 * Lq * P * (long long)sizeof(Entry<float>) + (S + 32) * 4;
+  return lds <= kGvLdsMax && B * M * L >= 256;
+}
+
 template <typename K>
 int allow_lds(K kernel, size_t bytes) {
   if (bytes <= 64 * 1024) return MSDA_OK;
@@ -726,7 +1117,39 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
   int rc;
 
   // grad_loc / grad_attn: item kernel (independent of the sort / pull pair)
-  if (gloc != nullptr || gaw != nullptr) {
+  bool coords_done = gloc == nullptr && gaw == nullptr;
+  if constexpr (!std::is_same<coord_t, double>::value) {
+    const int G = coords_done ? 0 : fast16_group<scalar_t>(pr);
+    const long long n_items = pr.B * pr.Lq * pr.M;
+    if (G > 0 && n_items > 0) {
+      constexpr int VEC = 16 / (int)sizeof(scalar_t);
+      const unsigned cblocks = (unsigned)((n_items * G + 255) / 256);
+      auto* v = static_cast<const scalar_t*>(value);
+      auto* g = static_cast<const scalar_t*>(gout);
+      auto* gl = static_cast<float*>(gloc);
+      auto* ga = static_cast<float*>(gaw);
+#define MSDA_C16(GG, Z)                                                                            \
+  hipLaunchKernelGGL((msda_bwd_coord16_kernel<scalar_t, VEC, GG, Z>), dim3(cblocks), dim3(256), 0,  \
+                     st, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M,    \
+                     (int)pr.D, (int)pr.Lq, n_items)
+#define MSDA_C16_G(Z)                                                                              \
+  switch (G) {                                                                                   \
+    case 1: MSDA_C16(1, Z); break;                                                               \
+    case 2: MSDA_C16(2, Z); break;                                                               \
+    case 4: MSDA_C16(4, Z); break;                                                               \
+    case 8: MSDA_C16(8, Z); break;                                                               \
+    case 16: MSDA_C16(16, Z); break;                                                             \
+    case 32: MSDA_C16(32, Z); break;                                                             \
+    default: MSDA_C16(64, Z); break;                                                             \
+  }
+      if (z) { MSDA_C16_G(true) } else { MSDA_C16_G(false) }
+#undef MSDA_C16_G
+#undef MSDA_C16
+      if ((rc = launch_status("backward coords"))) return rc;
+      coords_done = true;
+    }
+  }
+  if (!coords_done) {
     const long long n_items = pr.B * pr.Lq * pr.M;
     if (n_items > 0) {
       constexpr int VEC = 16 / (int)sizeof(scalar_t);
@@ -768,6 +1191,47 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     }
   }
   if (gval == nullptr) return MSDA_OK;
+
+  static const int deterministic_rows = [] {
+    const char* e = getenv("MSDA_HIP_DETERMINISTIC");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }();
+  if (use_fused_gvalue(value_dtype, pr.B, pr.S, pr.M, pr.Lq, pr.L, pr.P)) {
+    int maxT = 1;
+    for (int l = 0; l < pr.L; ++l) maxT = max(maxT, pr.lv.T[l]);
+    const size_t lds = (size_t)2 * pr.Lq * pr.P * sizeof(Entry<coord_t>) + (size_t)(maxT + 32) * 4;
+    constexpr int CPL = 16 / (int)sizeof(scalar_t);
+    int ns = 0;
+    if (pr.D % CPL == 0) {
+      const long long lpr = pr.D / CPL;
+      if (lpr == 8) ns = 8;
+      else if (lpr == 16) ns = 4;
+      else if (lpr == 32) ns = 2;
+      else if (lpr == 64) ns = 1;
+    }
+    const unsigned blocks = (unsigned)(pr.B * pr.M * pr.L);
+    auto* g = static_cast<const scalar_t*>(gout);
+    auto* gv = static_cast<scalar_t*>(gval);
+#define MSDA_GV(NSL, Z)                                                                             \
+  do {                                                                                            \
+    if ((rc = allow_lds(msda_bwd_gvalue_kernel<scalar_t, coord_t, NSL, Z>, lds))) return rc;      \
+    hipLaunchKernelGGL((msda_bwd_gvalue_kernel<scalar_t, coord_t, NSL, Z>), dim3(blocks),          \
+                       dim3(kGvThreads), lds, st, lc, a, g, gv, pr.lv, (int)pr.L, (int)pr.P,        \
+                       (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, deterministic_rows);          \
+  } while (0)
+#define MSDA_GV_NS(Z)                                                                               \
+  switch (ns) {                                                                                   \
+    case 8: MSDA_GV(8, Z); break;                                                                 \
+    case 4: MSDA_GV(4, Z); break;                                                                 \
+    case 2: MSDA_GV(2, Z); break;                                                                 \
+    case 1: MSDA_GV(1, Z); break;                                                                 \
+    default: MSDA_GV(0, Z); break;                                                                \
+  }
+    if (z) { MSDA_GV_NS(true) } else { MSDA_GV_NS(false) }
+#undef MSDA_GV_NS
+#undef MSDA_GV
+    return launch_status("backward gvalue");
+  }
 
   // 1. sort: one workgroup per (b, m, level)
   {
@@ -815,7 +1279,7 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     for (int l = 0; l < pr.L; ++l) po.lvl[l] = l;
     std::stable_sort(po.lvl, po.lvl + pr.L, [&](int x, int y) { return pr.lv.T[x] < pr.lv.T[y]; });
     po.cum[0] = 0;
-    for (int i = 0; i < pr.L; ++i) po.cum[i + 1] = po.cum[i] + pr.B * pr.M * pr.lv.T[po.lvl[i]];
+    for (int i = 0; i < pr.L; ++i) po.cum[i + 1] = po.cum[i] + pr.M * pr.lv.T[po.lvl[i]];
     for (int i = pr.L; i < MSDA_MAX_LEVELS; ++i) po.cum[i + 1] = 0x7fffffffffffffffll;
     const int nse = ns > 0 ? ns : 1;
     const long long waves = (nrows + nse - 1) / nse;
@@ -853,6 +1317,8 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
                                          int64_t num_levels, int64_t num_point) {
   (void)channels;
   if (batch <= 0 || spatial_size <= 0 || num_heads <= 0) return 0;
+  if (use_fused_gvalue(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point))
+    return 0;
   return bwd_layout(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point).total;
 }
 

@@ -29,13 +29,18 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_workspace():
     lib = PKG._native.load_library()
     assert lib.msda_hip_abi_version() == PKG._native.ABI_VERSION
-    # sort-pass workspace: row table + per-row tap lists
-    B, S, M, D, Lq, L, P = 8, 1920, 8, 64, 1920, 4, 4
+    # split path (sort + pull, few (b, m, level) workgroups): row table + per-row tap lists
+    B, S, M, D, Lq, L, P = 2, 1920, 8, 64, 1920, 4, 4
     f32 = lib.msda_hip_backward_workspace_bytes(0, B, S, M, D, Lq, L, P)
     f64 = lib.msda_hip_backward_workspace_bytes(1, B, S, M, D, Lq, L, P)
     assert f32 >= B * M * S * 8 + B * M * L * 2 * Lq * P * 8
     assert f64 > f32
     assert lib.msda_hip_backward_workspace_bytes(2, B, S, M, D, Lq, L, P) == f32  # bf16 keeps fp32 coords
+    # fused path (entry lists live in LDS, >= 256 (b, m, level) workgroups): no workspace,
+    # except fp64 (16-byte entries do not fit) and lists beyond the LDS budget
+    assert lib.msda_hip_backward_workspace_bytes(2, 8, S, M, D, Lq, L, P) == 0
+    assert lib.msda_hip_backward_workspace_bytes(1, 8, S, M, D, Lq, L, P) > 0
+    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) > 0
     assert lib.msda_hip_backward_workspace_bytes(0, 0, S, M, D, Lq, L, P) == 0
 
 

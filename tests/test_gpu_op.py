@@ -75,6 +75,12 @@ CASES = [
     ([64, 32],              1, 2, 71,   7, 4),     # odd channel count (scalar path)
     ([40, 20, 10],          1, 1, 1025, 3, 2),     # D > 64 lanes: chunked lanes
     ([40, 20, 10],          1, 2, 256,  6, 2),
+    # >= 256 (b, m, level) workgroups: fused sort+pull backward (entry lists in LDS)
+    ([32, 16, 8, 4],        8, 8, 64,   60, 4),
+    ([32, 16, 8, 4],        4, 16, 32,  30, 4),    # 8 rows per wave (fp32 D=32)
+    ([16, 8, 4, 2],         8, 8, 30,   20, 2),    # odd channel count: lane-per-channel pull
+    ([8, 4, 2, 1],          8, 8, 16,   200, 4),   # 800 taps on one row
+    ([64, 32, 16, 8],       8, 8, 16,   4000, 2),  # 16000 entries: near the LDS budget
 ]
 
 
@@ -97,8 +103,9 @@ def test_kernel_matches_oracle(dev, case, padding, dtype):
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("D", [64, 30])
-def test_half_values_match_oracle_on_rounded_inputs(dev, dtype, D):
-    shapes, B, M, Lq, P = [256, 128, 64, 32], 2, 8, 96, 4
+@pytest.mark.parametrize("B", [2, 8])  # 8: fused sort+pull backward
+def test_half_values_match_oracle_on_rounded_inputs(dev, dtype, D, B):
+    shapes, M, Lq, P = [256, 128, 64, 32], 8, 96, 4
     value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, dtype, seed=7)
     out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout)
     assert out.dtype == dtype and gv.dtype == dtype and gl.dtype == torch.float32
