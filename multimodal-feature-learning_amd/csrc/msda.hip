@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <mutex>
 #include <type_traits>
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
@@ -144,6 +145,28 @@ __device__ __forceinline__ void cvt16(const uint4& raw, typename AccOf<scalar_t>
   const scalar_t* e = reinterpret_cast<const scalar_t*>(&raw);
 #pragma unroll
   for (int i = 0; i < VEC; ++i) r[i] = to_acc(e[i]);
+}
+
+// Packed fp32 pairs: the fast kernels' channel math runs as v_pk_fma_f32 (two channels per
+// instruction); a bf16 pair unpacks with one shift and one mask.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+template <typename scalar_t, int VEC>
+__device__ __forceinline__ void cvt16x2(const uint4& raw, f32x2 (&r)[VEC / 2]) {
+  static_assert(VEC * sizeof(scalar_t) == 16, "16-byte fragment");
+  if constexpr (std::is_same<scalar_t, bf16_t>::value) {
+    const uint32_t d[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) r[i] = f32x2{__uint_as_float(d[i] << 16), __uint_as_float(d[i] & 0xffff0000u)};
+  } else {
+    const scalar_t* e = reinterpret_cast<const scalar_t*>(&raw);
+#pragma unroll
+    for (int i = 0; i < VEC / 2; ++i) r[i] = f32x2{(float)to_acc(e[2 * i]), (float)to_acc(e[2 * i + 1])};
+  }
+}
+
+__device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
+  return __builtin_elementwise_fma(a, b, c);
 }
 
 // ---------------------------------------------------------------------------------
@@ -298,34 +321,41 @@ __global__ __launch_bounds__(256) void msda_fwd16_kernel(
   load_coords16(loc + item * LP, LP, lr);
   load_coords16(aw + item * LP, LP, ar);
   const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D + lg * VEC;
-  acc_t acc[VEC];
+  const int rs = M * D;  // row stride; tap offsets inside one clip fit 32 bits
+  f32x2 acc2[VEC / 2];
 #pragma unroll
-  for (int e = 0; e < VEC; ++e) acc[e] = 0.f;
+  for (int e = 0; e < VEC / 2; ++e) acc2[e] = f32x2{0.f, 0.f};
 #pragma unroll
   for (int j0 = 0; j0 < kLPMax; j0 += 4) {
     if (j0 < LP) {
       uint4 r0[4], r1[4];
-      float w0[4], w1[4];
+      float c0[4], c1[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int l = (j0 + u) / P;
         const Taps<float> t = make_taps<float, ZEROS>(lr[j0 + u], lv.T[l]);
-        const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rowstride;
-        r0[u] = load16_if(t.ok0, vl + t.i0 * rowstride);
-        r1[u] = load16_if(t.ok1, vl + t.i1 * rowstride);
-        w0[u] = t.w0;
-        w1[u] = t.w1;
+        const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rs;
+        r0[u] = load16_if(t.ok0, vl + t.i0 * rs);
+        r1[u] = load16_if(t.ok1, vl + t.i1 * rs);
+        c0[u] = ar[j0 + u] * t.w0;
+        c1[u] = ar[j0 + u] * t.w1;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        acc_t x0[VEC], x1[VEC];
-        cvt16<scalar_t, VEC>(r0[u], x0);
-        cvt16<scalar_t, VEC>(r1[u], x1);
-        const float aa = ar[j0 + u];
+        f32x2 x0[VEC / 2], x1[VEC / 2];
+        cvt16x2<scalar_t, VEC>(r0[u], x0);
+        cvt16x2<scalar_t, VEC>(r1[u], x1);
+        const f32x2 k0{c0[u], c0[u]}, k1{c1[u], c1[u]};
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) acc[e] += aa * (x0[e] * w0[u] + x1[e] * w1[u]);
+        for (int e = 0; e < VEC / 2; ++e) acc2[e] = pk_fma(x1[e], k1, pk_fma(x0[e], k0, acc2[e]));
       }
     }
+  }
+  acc_t acc[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC / 2; ++e) {
+    acc[2 * e] = acc2[e].x;
+    acc[2 * e + 1] = acc2[e].y;
   }
   store_vec<scalar_t, VEC>(out + item * D + lg * VEC, acc);
 }
@@ -353,9 +383,16 @@ __global__ __launch_bounds__(256) void msda_fwd16_kernel(
 //      grad_loc = aw * dy/dloc * (d1 - d0)   (d_k = 0 for a tap outside the map).
 template <typename coord_t>
 struct Entry {
-  int tap;    // ((q * P + p) << 1) | k
+  int q;      // query whose grad_out row this tap pulls
   coord_t w;  // aw * w_k
 };
+
+// Deterministic mode's order of a row's list: by query, then weight.  Entries that tie on
+// both add the same product, so any order of them gives the same sum.
+template <typename coord_t>
+__device__ __forceinline__ bool entry_after(const Entry<coord_t>& a, const Entry<coord_t>& b) {
+  return a.q > b.q || (a.q == b.q && a.w > b.w);
+}
 
 constexpr int kSortThreads = 512;
 constexpr long long kSortLdsMax = 150 * 1024;  // LDS staging of a level's entry lists
@@ -448,12 +485,12 @@ __global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
     const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qs + p], T);
     if (t.ok0) {
       const int pos = atomicAdd(&cur[t.i0], 1);
-      Entry<coord_t> e{(s << 1), a * t.w0};
+      Entry<coord_t> e{q, a * t.w0};
       if constexpr (STAGE) stage[pos] = e; else entries[base + pos] = e;
     }
     if (t.ok1) {
       const int pos = atomicAdd(&cur[t.i1], 1);
-      Entry<coord_t> e{(s << 1) | 1, a * t.w1};
+      Entry<coord_t> e{q, a * t.w1};
       if constexpr (STAGE) stage[pos] = e; else entries[base + pos] = e;
     }
   }
@@ -467,7 +504,7 @@ __global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
       for (int x = e0 + 1; x < e1; ++x) {
         const Entry<coord_t> key = stage[x];
         int y = x - 1;
-        while (y >= e0 && stage[y].tap > key.tap) {
+        while (y >= e0 && entry_after(stage[y], key)) {
           stage[y + 1] = stage[y];
           --y;
         }
@@ -483,7 +520,7 @@ __global__ __launch_bounds__(kSortThreads) void msda_bwd_sort_kernel(
       for (int x = e0 + 1; x < e1; ++x) {
         const Entry<coord_t> key = entries[base + x];
         int y = x - 1;
-        while (y >= e0 && entries[base + y].tap > key.tap) {
+        while (y >= e0 && entry_after(entries[base + y], key)) {
           entries[base + y + 1] = entries[base + y];
           --y;
         }
@@ -580,16 +617,15 @@ __global__ __launch_bounds__(kPullThreads) void msda_bwd_pull_kernel(
       nxt = (j0 + LPR + cl < count) ? entries[start + j0 + LPR + cl] : Entry<coord_t>{0, (coord_t)0};
       const int nchunk = min(LPR, count - j0);  // <= 0 for a finished row
       for (int u0 = 0; __ballot(u0 < nchunk) != 0ull; u0 += U) {
-        int tap[U];
+        int qq[U];
         acc_t w[U], g[U][CPL];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int src = slot * LPR + u0 + u;
-          tap[u] = __shfl(cur.tap, src);
+          qq[u] = __shfl(cur.q, src);
           w[u] = (acc_t)__shfl(cur.w, src);
           const bool have = u0 + u < nchunk;
-          const int q = (tap[u] >> 1) / P;
-          if (have && on) load_vec<scalar_t, CPL>(gb + q * gq + c0, g[u]);
+          if (have && on) load_vec<scalar_t, CPL>(gb + qq[u] * gq + c0, g[u]);
           else {
 #pragma unroll
             for (int e = 0; e < CPL; ++e) g[u][e] = (acc_t)0;
@@ -706,16 +742,17 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_gvalue_kernel(
     const int s = threadIdx.x + k * kGvThreads;
     if (s < nsamp) {
       const Taps<coord_t> t = make_taps<coord_t, ZEROS>(cl[k], T);
-      if (t.ok0) ent[atomicAdd(&cur[t.i0], 1)] = Entry<coord_t>{(s << 1), ca[k] * t.w0};
-      if (t.ok1) ent[atomicAdd(&cur[t.i1], 1)] = Entry<coord_t>{(s << 1) | 1, ca[k] * t.w1};
+      const int q = s / P;
+      if (t.ok0) ent[atomicAdd(&cur[t.i0], 1)] = Entry<coord_t>{q, ca[k] * t.w0};
+      if (t.ok1) ent[atomicAdd(&cur[t.i1], 1)] = Entry<coord_t>{q, ca[k] * t.w1};
     }
   }
   for (int s = threadIdx.x + kGvCache * kGvThreads; s < nsamp; s += kGvThreads) {
     const int q = s / P, p = s - (s / P) * P;
     const coord_t a = awb[q * qs + p];
     const Taps<coord_t> t = make_taps<coord_t, ZEROS>(locb[q * qs + p], T);
-    if (t.ok0) ent[atomicAdd(&cur[t.i0], 1)] = Entry<coord_t>{(s << 1), a * t.w0};
-    if (t.ok1) ent[atomicAdd(&cur[t.i1], 1)] = Entry<coord_t>{(s << 1) | 1, a * t.w1};
+    if (t.ok0) ent[atomicAdd(&cur[t.i0], 1)] = Entry<coord_t>{q, a * t.w0};
+    if (t.ok1) ent[atomicAdd(&cur[t.i1], 1)] = Entry<coord_t>{q, a * t.w1};
   }
   __syncthreads();
   MSDA_PH(4);
@@ -725,7 +762,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_gvalue_kernel(
       for (int x = e0 + 1; x < e1; ++x) {
         const Entry<coord_t> key = ent[x];
         int y = x - 1;
-        while (y >= e0 && ent[y].tap > key.tap) {
+        while (y >= e0 && entry_after(ent[y], key)) {
           ent[y + 1] = ent[y];
           --y;
         }
@@ -765,8 +802,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_gvalue_kernel(
           const bool have = j0 + u < count;
           const Entry<coord_t> e = have ? ent[e0 + j0 + u] : Entry<coord_t>{0, (coord_t)0};
           w[u] = (acc_t)e.w;
-          const int q = (e.tap >> 1) / P;
-          if (have && on) load_vec<scalar_t, CPL>(gb + q * gq + c0, g[u]);
+          if (have && on) load_vec<scalar_t, CPL>(gb + e.q * gq + c0, g[u]);
           else {
 #pragma unroll
             for (int x = 0; x < CPL; ++x) g[u][x] = (acc_t)0;
@@ -813,9 +849,10 @@ __global__ __launch_bounds__(256) void msda_bwd_coord16_kernel(
   float lr[kLPMax], ar[kLPMax];
   load_coords16(loc + item * LP, LP, lr);
   load_coords16(aw + item * LP, LP, ar);
-  float g1[VEC];
-  cvt16<scalar_t, VEC>(load16_if(active, gout + item * D + lg * VEC), g1);
+  f32x2 g2[VEC / 2];
+  cvt16x2<scalar_t, VEC>(load16_if(active, gout + item * D + lg * VEC), g2);
   const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D + lg * VEC;
+  const int rs = M * D;
 #pragma unroll
   for (int j0 = 0; j0 < kLPMax; j0 += 4) {
     if (j0 < LP) {
@@ -825,28 +862,29 @@ __global__ __launch_bounds__(256) void msda_bwd_coord16_kernel(
       for (int u = 0; u < 4; ++u) {
         const int l = (j0 + u) / P;
         t[u] = make_taps<float, ZEROS>(lr[j0 + u], lv.T[l]);
-        const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rowstride;
-        r0[u] = load16_if(active && t[u].ok0, vl + t[u].i0 * rowstride);
-        r1[u] = load16_if(active && t[u].ok1, vl + t[u].i1 * rowstride);
+        const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rs;
+        r0[u] = load16_if(active && t[u].ok0, vl + t[u].i0 * rs);
+        r1[u] = load16_if(active && t[u].ok1, vl + t[u].i1 * rs);
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        float x0[VEC], x1[VEC];
-        cvt16<scalar_t, VEC>(r0[u], x0);
-        cvt16<scalar_t, VEC>(r1[u], x1);
-        float pa = 0.f, pl = 0.f;
+        // d_k = <grad_out, tap k row>: grad_aw = w0 d0 + w1 d1, grad_loc = aw dy/dloc (d1 - d0)
+        f32x2 x0[VEC / 2], x1[VEC / 2];
+        cvt16x2<scalar_t, VEC>(r0[u], x0);
+        cvt16x2<scalar_t, VEC>(r1[u], x1);
+        f32x2 s0{0.f, 0.f}, s1{0.f, 0.f};
 #pragma unroll
-        for (int e = 0; e < VEC; ++e) {
-          pa += g1[e] * (x0[e] * t[u].w0 + x1[e] * t[u].w1);
-          pl += g1[e] * (x1[e] - x0[e]);
+        for (int e = 0; e < VEC / 2; ++e) {
+          s0 = pk_fma(g2[e], x0[e], s0);
+          s1 = pk_fma(g2[e], x1[e], s1);
         }
-        pa = group_sum<G>(pa);
-        pl = group_sum<G>(pl);
+        const float d0 = group_sum<G>(s0.x + s0.y);
+        const float d1 = group_sum<G>(s1.x + s1.y);
         const int j = j0 + u;
         if (active && lg == j % G) {
           const long long o = item * LP + j;
-          if (gaw != nullptr) gaw[o] = pa;
-          if (gloc != nullptr) gloc[o] = (pl * ar[j]) * t[u].gmul;
+          if (gaw != nullptr) gaw[o] = d0 * t[u].w0 + d1 * t[u].w1;
+          if (gloc != nullptr) gloc[o] = ((d1 - d0) * ar[j]) * t[u].gmul;
         }
       }
     }
@@ -1101,9 +1139,9 @@ int allow_lds(K kernel, size_t bytes) {
 }
 
 template <typename scalar_t, typename coord_t>
-int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
-                 const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
-                 int value_dtype, int pad, hipStream_t st) {
+int run_backward_impl(const Problem& pr, const void* value, const void* loc, const void* aw,
+                      const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
+                      int value_dtype, int pad, hipStream_t st, hipStream_t cst) {
   using acc_t = typename AccOf<scalar_t>::type;
   const long long nrows = pr.B * pr.M * pr.S;
   if (nrows == 0) return MSDA_OK;
@@ -1130,7 +1168,7 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
       auto* ga = static_cast<float*>(gaw);
 #define MSDA_C16(GG, Z)                                                                            \
   hipLaunchKernelGGL((msda_bwd_coord16_kernel<scalar_t, VEC, GG, Z>), dim3(cblocks), dim3(256), 0,  \
-                     st, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M,    \
+                     cst, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M,    \
                      (int)pr.D, (int)pr.Lq, n_items)
 #define MSDA_C16_G(Z)                                                                              \
   switch (G) {                                                                                   \
@@ -1166,7 +1204,7 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
       auto* ga = static_cast<coord_t*>(gaw);
 #define MSDA_CO(V, GG, Z, ONE)                                                                     \
   hipLaunchKernelGGL((msda_bwd_coord_kernel<scalar_t, coord_t, V, GG, Z, ONE>), dim3(blocks),        \
-                     dim3(256), 0, st, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, \
+                     dim3(256), 0, cst, v, lc, a, g, gl, ga, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, \
                      (int)pr.M, (int)pr.D, (int)pr.Lq, n_items)
 #define MSDA_CO_G(V, Z, ONE)                                                                       \
   switch (G) {                                                                                   \
@@ -1302,6 +1340,66 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
   }
 
   return MSDA_OK;
+}
+
+// Side stream of the calling device: grad_loc / grad_attn (coordinate kernel) and grad_value
+// (sort / pull) read the same inputs and write disjoint outputs, so with all three requested
+// the coordinate kernel runs beside the grad_value kernel, forked from and joined back into
+// the caller's stream with events (both capture into a HIP graph as parallel branches).
+// MSDA_HIP_SIDE_STREAM=0 serialises them on the caller's stream.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  bool ok = false;
+};
+
+SideStream* side_stream() {
+  static const int enabled = [] {
+    const char* e = getenv("MSDA_HIP_SIDE_STREAM");
+    return (e != nullptr && e[0] == '0') ? 0 : 1;
+  }();
+  if (!enabled) return nullptr;
+  constexpr int kMaxDev = 64;
+  static std::mutex mu;
+  static SideStream per_dev[kMaxDev];
+  static bool tried[kMaxDev] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  SideStream& ss = per_dev[dev];
+  if (!tried[dev]) {
+    tried[dev] = true;
+    ss.ok = hipStreamCreateWithFlags(&ss.s, hipStreamNonBlocking) == hipSuccess &&
+            hipEventCreateWithFlags(&ss.fork, hipEventDisableTiming) == hipSuccess &&
+            hipEventCreateWithFlags(&ss.join, hipEventDisableTiming) == hipSuccess;
+  }
+  return ss.ok ? &ss : nullptr;
+}
+
+template <typename scalar_t, typename coord_t>
+int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
+                 const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
+                 int value_dtype, int pad, hipStream_t st) {
+  SideStream* side = nullptr;
+  // worth a fork / join (~5 us) only when the coordinate kernel is long (encoder-sized calls)
+  if (gval != nullptr && (gloc != nullptr || gaw != nullptr) && pr.B * pr.M * pr.S > 0 &&
+      pr.B * pr.Lq * pr.M >= 32768) {
+    side = side_stream();
+    if (side != nullptr && (hipEventRecord(side->fork, st) != hipSuccess ||
+                            hipStreamWaitEvent(side->s, side->fork, 0) != hipSuccess))
+      side = nullptr;
+  }
+  const int rc = run_backward_impl<scalar_t, coord_t>(pr, value, loc, aw, gout, gval, gloc, gaw,
+                                                      workspace, value_dtype, pad, st,
+                                                      side != nullptr ? side->s : st);
+  if (side != nullptr) {
+    if (hipEventRecord(side->join, side->s) != hipSuccess ||
+        hipStreamWaitEvent(st, side->join, 0) != hipSuccess) {
+      set_error("msda_hip_backward: side-stream join failed");
+      return MSDA_ERR_LAUNCH;
+    }
+  }
+  return rc;
 }
 
 }  // namespace
