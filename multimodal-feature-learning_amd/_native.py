@@ -13,6 +13,8 @@ import torch
 
 LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 LIB_PATH = os.path.join(LIB_DIR, "libmsda_hip.so")
+# tools only (e.g. a phase-timing debug build); never set by the product path or the tests
+LIB_PATH = os.environ.get("MSDA_HIP_LIB", LIB_PATH)
 
 # keep in sync with include/msda_hip.h
 DTYPE_TAGS = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2, torch.float16: 3}

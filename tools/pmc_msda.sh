@@ -5,7 +5,7 @@
 # by tools/pmc_summary.py.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out/pmc; export TMPDIR=/tmp
-ARGS=${MICRO_ARGS:-"--dtypes bf16 --regimes init --iters 3 --kernels fwd,bwd_all"}
+ARGS=${MICRO_ARGS:-"--dtypes bf16 --regimes init --iters 3 --shapes enc --kernels fwd,bwd_all"}
 run() { # name counters...
   local name=$1; shift
   rm -rf gpurun_out/pmc/$name
@@ -17,4 +17,5 @@ run fetch FETCH_SIZE
 run write WRITE_SIZE
 run l2 TCC_HIT_sum TCC_MISS_sum
 run sq SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU
-python3 tools/pmc_summary.py gpurun_out/pmc > gpurun_out/pmc/summary.json && cat gpurun_out/pmc/summary.json
+python3 tools/pmc_summary.py gpurun_out/pmc gpurun_out/pmc/traffic_latest.json > gpurun_out/pmc/summary.json &&
+  cat gpurun_out/pmc/summary.json gpurun_out/pmc/traffic_latest.json

@@ -43,7 +43,31 @@ def main(root):
             rec["l2_hit_rate"] = rec["TCC_HIT_sum"] / tot if tot else None
         out[f"{k}@grid{grid}"] = {c: (round(v, 4) if isinstance(v, float) else v) for c, v in rec.items()}
     json.dump(out, sys.stdout, indent=1)
+    return out
+
+
+# bench.py's launch names -> the kernels of that C-ABI call at the encoder shape (B=8, T=1024
+# pyramid, bf16; tools/pmc_msda.sh runs the encoder shape only, so one grid per kernel)
+CALL_KERNELS = {
+    "msda_fwd_S1920_Lq1920": ("msda_fwd16_kernel",),
+    "msda_bwd_S1920_Lq1920": ("msda_bwd_gvalue_kernel", "msda_bwd_coord16_kernel"),
+}
+
+
+def traffic_per_call(out):
+    res = {}
+    for call, kernels in CALL_KERNELS.items():
+        parts = {}
+        for key, rec in out.items():
+            kname = key.split("<", 1)[0]
+            if kname in kernels and "traffic_bytes" in rec:
+                parts[kname] = rec["traffic_bytes"]
+        if len(parts) == len(kernels):
+            res[call] = round(sum(parts.values()))
+    return res
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    summary = main(sys.argv[1])
+    if len(sys.argv) > 2:  # also write bench.py's --traffic-json (HBM bytes per C-ABI call)
+        json.dump(traffic_per_call(summary), open(sys.argv[2], "w"), indent=1)

@@ -1,17 +1,16 @@
 #!/usr/bin/env python3
-"""Per-launch-shape summary of the MSDA kernels in a rocprofv3 --kernel-trace CSV.
+"""Split a rocprofv3 kernel trace (run_kernel_trace.csv) per MSDA kernel and launch shape.
 
-rocprofv3 --stats aggregates every dispatch of a kernel symbol, which mixes the encoder
-(Lq = S) and decoder (Lq = 100) calls of the same template instance.  This groups the
-dispatches of each msda_* kernel by grid size (one grid size per call shape) and prints
-count / avg / min / max duration plus VGPRs and LDS, so the bench's HIP-event
-`avg_launch_ms` can be checked against the profiler per shape.
+rocprof's --stats table averages a kernel over every launch shape (encoder and decoder calls
+share a kernel), so bench.py's per-call HIP-event timings cannot be checked against it
+directly.  This groups the trace by (kernel, grid size, LDS bytes), and also prints the
+step-level top kernels of the whole trace.
 
-usage: tools/rocprof_msda_summary.py <run_kernel_trace.csv> [> profiles/<round>_msda_kernels.csv]
+usage: rocprof_msda_summary.py <run_kernel_trace.csv> [--steps N]  -> CSV on stdout
 """
+import argparse
 import csv
 import re
-import sys
 from collections import defaultdict
 
 
@@ -19,27 +18,29 @@ def short(name):
     m = re.search(r"(msda_\w+?)<(.*?)>\(", name)
     if not m:
         return None
-    args = m.group(2).replace("(anonymous namespace)::", "")
-    return f"{m.group(1)}<{args}>"
+    return f"{m.group(1)}<{m.group(2).replace('(anonymous namespace)::', '')}>"
 
 
-def main(path):
-    groups = defaultdict(list)
-    meta = {}
-    for r in csv.DictReader(open(path)):
-        s = short(r["Kernel_Name"])
-        if s is None:
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("trace")
+    args = ap.parse_args()
+    acc = defaultdict(list)
+    for r in csv.DictReader(open(args.trace)):
+        k = short(r["Kernel_Name"])
+        if k is None:
             continue
-        key = (s, int(r["Grid_Size_X"]), int(r["Workgroup_Size_X"]))
-        groups[key].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-        meta[key] = (r["VGPR_Count"], r["Accum_VGPR_Count"], r["LDS_Block_Size"])
-    w = csv.writer(sys.stdout)
-    w.writerow(["kernel", "grid_x", "block_x", "calls", "avg_us", "min_us", "max_us", "vgpr", "agpr", "lds_bytes"])
-    for key in sorted(groups, key=lambda k: -sum(groups[k])):
-        d = groups[key]
-        w.writerow([key[0], key[1], key[2], len(d), round(sum(d) / len(d) / 1e3, 2), round(min(d) / 1e3, 2),
-                    round(max(d) / 1e3, 2), *meta[key]])
+        grid = int(r["Grid_Size_X"]) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        wg = int(r["Workgroup_Size_X"])
+        key = (k, grid // max(wg, 1), wg, int(r["LDS_Block_Size"]), int(r["VGPR_Count"]))
+        acc[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    w = csv.writer(__import__("sys").stdout)
+    w.writerow(["kernel", "workgroups", "wg_size", "lds_bytes", "vgprs", "launches", "avg_us", "min_us",
+                "max_us", "total_us"])
+    for key, ts in sorted(acc.items(), key=lambda kv: -sum(kv[1])):
+        w.writerow(list(key) + [len(ts), round(sum(ts) / len(ts), 2), round(min(ts), 2), round(max(ts), 2),
+                                round(sum(ts), 1)])
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main()
