@@ -829,6 +829,206 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_gvalue_kernel(
 #undef MSDA_PH
 }
 
+// Fused backward: grad_value, grad_loc and grad_attn in ONE launch, one 1024-thread workgroup
+// per (b, m, level).  Both taps of a sample lie in the same level, so everything a sample's
+// coordinate gradients need is produced inside its level's workgroup:
+//   1-3. histogram / scan / place (as msda_bwd_gvalue_kernel): per-row lists of the level's
+//        in-map taps, key = q << 8 | (2p + k), in LDS; wd[tap] = aw * w_k (0 off the map);
+//   4.   pull: the owner lanes of a value row hold that row of `value` in registers and walk
+//        its list; every gathered grad_out row is used twice — accumulated into grad_value
+//        (aw * w_k * g) and dotted with the value row, d_k = <g, v_row> (DPP reduction over the
+//        row's lanes), which overwrites wd[tap] (each tap has exactly one entry);
+//   5.   epilogue: per sample, grad_attn = w0 d0 + w1 d1, grad_loc = aw dy/dloc (d1 - d0).
+// So the backward gathers grad_out once per tap and never gathers value rows — half the row
+// fragments of the sort/pull + coordinate-kernel pair (tools/msda_microbench.py).
+// LDS: 8 B per tap (key, wd) + 4 B per row.  COORDS=false: grad_value only.
+template <typename scalar_t, int NSLOT, bool ZEROS, bool COORDS, int U>
+__global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
+    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, float* __restrict__ gloc,
+    float* __restrict__ gaw, const Levels lv, const int L, const int P, const int S, const int M,
+    const int D, const int Lq, const int sort_rows) {
+  static_assert(NSLOT > 0, "fused backward needs whole 16-byte chunks per lane");
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const unsigned blk = xcd_block(blockIdx.x, gridDim.x);
+  const int l = (int)(blk % (unsigned)L);
+  const long long bm = blk / (unsigned)L;
+  const int m = (int)(bm % M);
+  const long long b = bm / M;
+  const int T = lv.T[l];
+  const int nsamp = Lq * P;
+  const int ncap = 2 * nsamp;
+  unsigned* ent = reinterpret_cast<unsigned*>(smem_raw);
+  float* wd = reinterpret_cast<float*>(smem_raw + (size_t)ncap * 4);
+  int* cur = reinterpret_cast<int*>(smem_raw + (size_t)ncap * 8);
+  int* scratch = cur + T;
+
+  for (int i = threadIdx.x; i < T; i += kGvThreads) cur[i] = 0;
+  __syncthreads();
+
+  const int LP = L * P;
+  const long long qs = (long long)M * LP;
+  const float* __restrict__ locb = loc + (b * Lq * M + m) * LP + l * P;
+  const float* __restrict__ awb = aw + (b * Lq * M + m) * LP + l * P;
+
+  // 1. taps per row; the first kGvCache samples of every thread keep loc / aw in registers
+  float cl[kGvCache], ca[kGvCache];
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) {
+      const int q = s / P, p = s - (s / P) * P;
+      cl[k] = locb[q * qs + p];
+      ca[k] = awb[q * qs + p];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) {
+      const Taps<float> t = make_taps<float, ZEROS>(cl[k], T);
+      if (t.ok0) atomicAdd(&cur[t.i0], 1);
+      if (t.ok1) atomicAdd(&cur[t.i1], 1);
+    }
+  }
+  for (int s = threadIdx.x + kGvCache * kGvThreads; s < nsamp; s += kGvThreads) {
+    const int q = s / P, p = s - (s / P) * P;
+    const Taps<float> t = make_taps<float, ZEROS>(locb[q * qs + p], T);
+    if (t.ok0) atomicAdd(&cur[t.i0], 1);
+    if (t.ok1) atomicAdd(&cur[t.i1], 1);
+  }
+  __syncthreads();
+
+  // 2. exclusive scan over rows: thread i owns rows [i*chunk, (i+1)*chunk)
+  const int chunk = (T + kGvThreads - 1) / kGvThreads;
+  const int lo = min((int)threadIdx.x * chunk, T), hi = min(lo + chunk, T);
+  {
+    int mine = 0;
+    for (int i = lo; i < hi; ++i) mine += cur[i];
+    int total = 0;
+    int run = block_exclusive_scan(mine, scratch, &total);
+    for (int i = lo; i < hi; ++i) {
+      const int c = cur[i];
+      cur[i] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+
+  // 3. place the keys (cur[i] ends at the end of row i) and the tap weights
+  auto place = [&](int s, float lc, float a) {
+    const Taps<float> t = make_taps<float, ZEROS>(lc, T);
+    const int q = s / P, p = s - q * P;
+    const unsigned key = ((unsigned)q << 8) | (unsigned)(2 * p);
+    if (t.ok0) ent[atomicAdd(&cur[t.i0], 1)] = key;
+    if (t.ok1) ent[atomicAdd(&cur[t.i1], 1)] = key | 1u;
+    wd[2 * s] = t.ok0 ? a * t.w0 : 0.f;
+    wd[2 * s + 1] = t.ok1 ? a * t.w1 : 0.f;
+  };
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) place(s, cl[k], ca[k]);
+  }
+  for (int s = threadIdx.x + kGvCache * kGvThreads; s < nsamp; s += kGvThreads) {
+    const int q = s / P, p = s - q * P;
+    place(s, locb[q * qs + p], awb[q * qs + p]);
+  }
+  __syncthreads();
+  if (sort_rows) {  // deterministic mode: each row's list in tap order (insertion sort)
+    for (int i = lo; i < hi; ++i) {
+      const int e1 = cur[i], e0 = (i == 0 ? 0 : cur[i - 1]);
+      for (int x = e0 + 1; x < e1; ++x) {
+        const unsigned key = ent[x];
+        int y = x - 1;
+        while (y >= e0 && ent[y] > key) {
+          ent[y + 1] = ent[y];
+          --y;
+        }
+        ent[y + 1] = key;
+      }
+    }
+    __syncthreads();
+  }
+
+  // 4. pull: NS rows per wave-iteration, LPR lanes x CPL channels (16 bytes) per row
+  constexpr int CPL = 16 / (int)sizeof(scalar_t);
+  constexpr int NS = NSLOT;
+  constexpr int LPR = 64 / NS;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = lane / LPR;
+  const int c_l = lane - slot * LPR;
+  const int rs = M * D;  // row stride; offsets inside one clip fit 32 bits
+  const int twoP = 2 * P;
+  const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D + c_l * CPL;
+  const long long vofs = ((b * S + lv.start[l]) * M + m) * (long long)D + c_l * CPL;
+  const scalar_t* __restrict__ vl = value + vofs;
+  scalar_t* __restrict__ gvl = gval + vofs;
+  for (int r0 = wave * NS; r0 < T; r0 += (kGvThreads / 64) * NS) {
+    const int row = r0 + slot;
+    const bool valid = row < T;
+    const int e0 = valid ? (row == 0 ? 0 : cur[row - 1]) : 0;
+    const int count = valid ? cur[row] - e0 : 0;
+    f32x2 v2[CPL / 2];
+    if constexpr (COORDS) cvt16x2<scalar_t, CPL>(load16_if(count > 0, vl + row * rs), v2);
+    f32x2 acc[CPL / 2];
+#pragma unroll
+    for (int e = 0; e < CPL / 2; ++e) acc[e] = f32x2{0.f, 0.f};
+    for (int j0 = 0; __ballot(j0 < count) != 0ull; j0 += U) {
+      uint4 g[U];
+      float w[U];
+      int tt[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool have = j0 + u < count;
+        const unsigned key = have ? ent[e0 + j0 + u] : 0u;
+        const int q = (int)(key >> 8);
+        tt[u] = have ? q * twoP + (int)(key & 0xffu) : -1;
+        w[u] = have ? wd[tt[u]] : 0.f;
+        g[u] = load16_if(have, gb + q * rs);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        f32x2 x[CPL / 2];
+        cvt16x2<scalar_t, CPL>(g[u], x);
+        const f32x2 k2{w[u], w[u]};
+#pragma unroll
+        for (int e = 0; e < CPL / 2; ++e) acc[e] = pk_fma(x[e], k2, acc[e]);
+        if constexpr (COORDS) {
+          f32x2 sd{0.f, 0.f};
+#pragma unroll
+          for (int e = 0; e < CPL / 2; ++e) sd = pk_fma(x[e], v2[e], sd);
+          const float d = group_sum<LPR>(sd.x + sd.y);
+          if (tt[u] >= 0 && c_l == 0) wd[tt[u]] = d;
+        }
+      }
+    }
+    if (valid) {
+      float a[CPL];
+#pragma unroll
+      for (int e = 0; e < CPL / 2; ++e) {
+        a[2 * e] = acc[e].x;
+        a[2 * e + 1] = acc[e].y;
+      }
+      store_vec<scalar_t, CPL>(gvl + row * rs, a);
+    }
+  }
+  if constexpr (COORDS) {
+    __syncthreads();
+    // 5. coordinate gradients of the level's samples: d_k = wd[2s + k] (0 off the map)
+    float* __restrict__ gab = gaw == nullptr ? nullptr : gaw + (b * Lq * M + m) * LP + l * P;
+    float* __restrict__ glb = gloc == nullptr ? nullptr : gloc + (b * Lq * M + m) * LP + l * P;
+    for (int s = threadIdx.x; s < nsamp; s += kGvThreads) {
+      const int q = s / P, p = s - q * P;
+      const long long o = q * qs + p;
+      const Taps<float> t = make_taps<float, ZEROS>(locb[o], T);
+      const float d0 = wd[2 * s], d1 = wd[2 * s + 1];
+      if (gab != nullptr) gab[o] = d0 * t.w0 + d1 * t.w1;
+      if (glb != nullptr) glb[o] = ((d1 - d0) * awb[o]) * t.gmul;
+    }
+  }
+}
+
 // grad_aw / grad_loc fast path (conditions of msda_fwd16_kernel): coordinates and the
 // item's grad_out chunk loaded once, 4 samples' fragments in flight, DPP reductions.
 template <typename scalar_t, int VEC, int G, bool ZEROS>
@@ -1376,10 +1576,85 @@ SideStream* side_stream() {
   return ss.ok ? &ss : nullptr;
 }
 
+// Rows per wave of the fused backward (msda_bwd_fused_kernel), or 0 when it does not apply:
+// fp32 coordinates, grad_value requested, the level's lists fit in LDS with enough
+// (b, m, level) workgroups to fill the chip (use_fused_gvalue), D a power-of-two number of
+// 16-byte chunks of at least 8 lanes, 2P <= 256 (key layout) and Lq < 2^23.
+// MSDA_HIP_BWD_PATH=unfused forces the gvalue + coordinate kernel pair (A/B measurements).
+template <typename scalar_t, typename coord_t>
+int fused_bwd_rows(const Problem& pr, int value_dtype, const void* gval) {
+  static const int force_unfused = [] {
+    const char* e = getenv("MSDA_HIP_BWD_PATH");
+    return (e != nullptr && strcmp(e, "unfused") == 0) ? 1 : 0;
+  }();
+  if (force_unfused || gval == nullptr || !std::is_same<coord_t, float>::value) return 0;
+  if (2 * pr.P > 256 || pr.Lq >= (1LL << 23)) return 0;
+  if (!use_fused_gvalue(value_dtype, pr.B, pr.S, pr.M, pr.Lq, pr.L, pr.P)) return 0;
+  constexpr int CPL = 16 / (int)sizeof(scalar_t);
+  if (pr.D % CPL != 0) return 0;
+  const long long lpr = pr.D / CPL;
+  if (lpr == 8) return 8;
+  if (lpr == 16) return 4;
+  if (lpr == 32) return 2;
+  if (lpr == 64) return 1;
+  return 0;
+}
+
+template <typename scalar_t>
+int run_backward_fused(const Problem& pr, int ns, const void* value, const void* loc, const void* aw,
+                       const void* gout, void* gval, void* gloc, void* gaw, int pad, hipStream_t st) {
+  static const int deterministic_rows = [] {
+    const char* e = getenv("MSDA_HIP_DETERMINISTIC");
+    return (e != nullptr && e[0] == '1') ? 1 : 0;
+  }();
+  int maxT = 1;
+  for (int l = 0; l < pr.L; ++l) maxT = max(maxT, pr.lv.T[l]);
+  const size_t lds = (size_t)2 * pr.Lq * pr.P * 8 + (size_t)(maxT + 32) * 4;
+  const unsigned blocks = (unsigned)(pr.B * pr.M * pr.L);
+  const bool coords = gloc != nullptr || gaw != nullptr;
+  const bool z = pad == MSDA_PAD_ZEROS;
+  auto* v = static_cast<const scalar_t*>(value);
+  auto* lc = static_cast<const float*>(loc);
+  auto* a = static_cast<const float*>(aw);
+  auto* g = static_cast<const scalar_t*>(gout);
+  auto* gv = static_cast<scalar_t*>(gval);
+  auto* gl = static_cast<float*>(gloc);
+  auto* ga = static_cast<float*>(gaw);
+  int rc;
+#define MSDA_FU(NSL, Z, C)                                                                        \
+  do {                                                                                          \
+    if ((rc = allow_lds(msda_bwd_fused_kernel<scalar_t, NSL, Z, C, 8>, lds))) return rc;        \
+    hipLaunchKernelGGL((msda_bwd_fused_kernel<scalar_t, NSL, Z, C, 8>), dim3(blocks),           \
+                       dim3(kGvThreads), lds, st, v, lc, a, g, gv, gl, ga, pr.lv, (int)pr.L,      \
+                       (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq,                  \
+                       deterministic_rows);                                                     \
+  } while (0)
+#define MSDA_FU_NS(Z, C)                                                                          \
+  switch (ns) {                                                                                 \
+    case 8: MSDA_FU(8, Z, C); break;                                                            \
+    case 4: MSDA_FU(4, Z, C); break;                                                            \
+    case 2: MSDA_FU(2, Z, C); break;                                                            \
+    default: MSDA_FU(1, Z, C); break;                                                           \
+  }
+  if (z) {
+    if (coords) { MSDA_FU_NS(true, true) } else { MSDA_FU_NS(true, false) }
+  } else {
+    if (coords) { MSDA_FU_NS(false, true) } else { MSDA_FU_NS(false, false) }
+  }
+#undef MSDA_FU_NS
+#undef MSDA_FU
+  return launch_status("backward fused");
+}
+
 template <typename scalar_t, typename coord_t>
 int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
                  const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
                  int value_dtype, int pad, hipStream_t st) {
+  if constexpr (std::is_same<coord_t, float>::value) {
+    const int ns = pr.B * pr.M * pr.S > 0 ? fused_bwd_rows<scalar_t, coord_t>(pr, value_dtype, gval) : 0;
+    if (ns > 0)
+      return run_backward_fused<scalar_t>(pr, ns, value, loc, aw, gout, gval, gloc, gaw, pad, st);
+  }
   SideStream* side = nullptr;
   // worth a fork / join (~5 us) only when the coordinate kernel is long (encoder-sized calls)
   if (gval != nullptr && (gloc != nullptr || gaw != nullptr) && pr.B * pr.M * pr.S > 0 &&
