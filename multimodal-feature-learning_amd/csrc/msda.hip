@@ -134,10 +134,40 @@ __device__ __forceinline__ void store_vec(scalar_t* __restrict__ p,
   }
 }
 
+template <typename scalar_t, int VEC>
+__device__ __forceinline__ void store_vec_nt(scalar_t* __restrict__ p,
+                                             const typename AccOf<scalar_t>::type (&r)[VEC]) {
+#ifdef MSDA_NT
+  if constexpr (VEC * sizeof(scalar_t) == 16) {
+    uint4 raw;
+    scalar_t* e = reinterpret_cast<scalar_t*>(&raw);
+#pragma unroll
+    for (int i = 0; i < VEC; ++i) from_acc(r[i], &e[i]);
+    typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(u32x4_t{raw.x, raw.y, raw.z, raw.w}, reinterpret_cast<u32x4_t*>(p));
+    return;
+  }
+#endif
+  store_vec<scalar_t, VEC>(p, r);
+}
+
 // One 16-byte row fragment kept raw (4 VGPRs) until it is consumed; zero when not loaded.
 template <typename scalar_t>
 __device__ __forceinline__ uint4 load16_if(bool ok, const scalar_t* __restrict__ p) {
   return ok ? *reinterpret_cast<const uint4*>(p) : make_uint4(0u, 0u, 0u, 0u);
+}
+// Streaming variants (MSDA_NT builds): data touched once per kernel (value rows of the fused
+// backward, grad_value) marked non-temporal so it does not evict the gathered grad_out rows.
+template <typename scalar_t>
+__device__ __forceinline__ uint4 load16_if_nt(bool ok, const scalar_t* __restrict__ p) {
+#ifdef MSDA_NT
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  if (!ok) return make_uint4(0u, 0u, 0u, 0u);
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return load16_if(ok, p);
+#endif
 }
 template <typename scalar_t, int VEC>
 __device__ __forceinline__ void cvt16(const uint4& raw, typename AccOf<scalar_t>::type (&r)[VEC]) {
@@ -150,6 +180,7 @@ __device__ __forceinline__ void cvt16(const uint4& raw, typename AccOf<scalar_t>
 // Packed fp32 pairs: the fast kernels' channel math runs as v_pk_fma_f32 (two channels per
 // instruction); a bf16 pair unpacks with one shift and one mask.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 template <typename scalar_t, int VEC>
 __device__ __forceinline__ void cvt16x2(const uint4& raw, f32x2 (&r)[VEC / 2]) {
@@ -167,6 +198,30 @@ __device__ __forceinline__ void cvt16x2(const uint4& raw, f32x2 (&r)[VEC / 2]) {
 
 __device__ __forceinline__ f32x2 pk_fma(f32x2 a, f32x2 b, f32x2 c) {
   return __builtin_elementwise_fma(a, b, c);
+}
+
+// Dot product of two raw 16-byte fragments, fp32 accumulation: v_dot2_f32_bf16 / v_dot2_f32_f16
+// on the packed pairs (no unpacking), plain FMAs for fp32.
+typedef _Float16 f16x2_t __attribute__((ext_vector_type(2)));
+template <typename scalar_t>
+__device__ __forceinline__ float dot16(const uint4& a, const uint4& b) {
+  const uint32_t x[4] = {a.x, a.y, a.z, a.w}, y[4] = {b.x, b.y, b.z, b.w};
+  float r = 0.f;
+  if constexpr (std::is_same<scalar_t, bf16_t>::value) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      r = __builtin_amdgcn_fdot2_f32_bf16(__builtin_bit_cast(bf16x2_t, x[e]), __builtin_bit_cast(bf16x2_t, y[e]), r,
+                                          false);
+  } else if constexpr (std::is_same<scalar_t, f16_t>::value) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      r = __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2_t, x[e]), __builtin_bit_cast(f16x2_t, y[e]), r, false);
+  } else {
+    static_assert(std::is_same<scalar_t, float>::value, "dot16: 16-bit or fp32 fragments");
+#pragma unroll
+    for (int e = 0; e < 4; ++e) r = fmaf(__uint_as_float(x[e]), __uint_as_float(y[e]), r);
+  }
+  return r;
 }
 
 // ---------------------------------------------------------------------------------
@@ -862,9 +917,17 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
   float* wd = reinterpret_cast<float*>(smem_raw + (size_t)ncap * 4);
   int* cur = reinterpret_cast<int*>(smem_raw + (size_t)ncap * 8);
   int* scratch = cur + T;
+#ifdef MSDA_PHASE_TIMING  // debug build only: per-phase wall clock of the (b=0, m=0) workgroups
+  unsigned long long tph[7];
+  tph[0] = wall_clock64();
+#define MSDA_PH(i) do { __syncthreads(); tph[i] = wall_clock64(); } while (0)
+#else
+#define MSDA_PH(i) do { } while (0)
+#endif
 
   for (int i = threadIdx.x; i < T; i += kGvThreads) cur[i] = 0;
   __syncthreads();
+  MSDA_PH(1);
 
   const int LP = L * P;
   const long long qs = (long long)M * LP;
@@ -898,6 +961,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
     if (t.ok1) atomicAdd(&cur[t.i1], 1);
   }
   __syncthreads();
+  MSDA_PH(2);
 
   // 2. exclusive scan over rows: thread i owns rows [i*chunk, (i+1)*chunk)
   const int chunk = (T + kGvThreads - 1) / kGvThreads;
@@ -914,6 +978,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
     }
   }
   __syncthreads();
+  MSDA_PH(3);
 
   // 3. place the keys (cur[i] ends at the end of row i) and the tap weights
   auto place = [&](int s, float lc, float a) {
@@ -950,6 +1015,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
     }
     __syncthreads();
   }
+  MSDA_PH(4);
 
   // 4. pull: NS rows per wave-iteration, LPR lanes x CPL channels (16 bytes) per row
   constexpr int CPL = 16 / (int)sizeof(scalar_t);
@@ -964,42 +1030,43 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
   const long long vofs = ((b * S + lv.start[l]) * M + m) * (long long)D + c_l * CPL;
   const scalar_t* __restrict__ vl = value + vofs;
   scalar_t* __restrict__ gvl = gval + vofs;
+  // NS rows per wave-iteration; per batch U grad_out fragments in flight.  (A software-
+  // pipelined variant that kept the next batch in flight while consuming this one measured
+  // slower: 93 vs 81 us at the bench's encoder shape.)
   for (int r0 = wave * NS; r0 < T; r0 += (kGvThreads / 64) * NS) {
     const int row = r0 + slot;
     const bool valid = row < T;
     const int e0 = valid ? (row == 0 ? 0 : cur[row - 1]) : 0;
     const int count = valid ? cur[row] - e0 : 0;
-    f32x2 v2[CPL / 2];
-    if constexpr (COORDS) cvt16x2<scalar_t, CPL>(load16_if(count > 0, vl + row * rs), v2);
+    uint4 vr = make_uint4(0u, 0u, 0u, 0u);
+    if constexpr (COORDS) vr = load16_if_nt(count > 0, vl + row * rs);
     f32x2 acc[CPL / 2];
 #pragma unroll
     for (int e = 0; e < CPL / 2; ++e) acc[e] = f32x2{0.f, 0.f};
     for (int j0 = 0; __ballot(j0 < count) != 0ull; j0 += U) {
+      // registers hold only the U gathered fragments; the keys and tap weights are read
+      // from LDS again when consumed (a ds_read is ~50 cycles, a gather thousands)
       uint4 g[U];
-      float w[U];
-      int tt[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const bool have = j0 + u < count;
         const unsigned key = have ? ent[e0 + j0 + u] : 0u;
-        const int q = (int)(key >> 8);
-        tt[u] = have ? q * twoP + (int)(key & 0xffu) : -1;
-        w[u] = have ? wd[tt[u]] : 0.f;
-        g[u] = load16_if(have, gb + q * rs);
+        g[u] = load16_if(have, gb + (int)(key >> 8) * rs);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
+        const bool have = j0 + u < count;
+        const unsigned key = have ? ent[e0 + j0 + u] : 0u;
+        const int tt = (int)(key >> 8) * twoP + (int)(key & 0xffu);
+        const float w = have ? wd[tt] : 0.f;
         f32x2 x[CPL / 2];
         cvt16x2<scalar_t, CPL>(g[u], x);
-        const f32x2 k2{w[u], w[u]};
+        const f32x2 k2{w, w};
 #pragma unroll
         for (int e = 0; e < CPL / 2; ++e) acc[e] = pk_fma(x[e], k2, acc[e]);
         if constexpr (COORDS) {
-          f32x2 sd{0.f, 0.f};
-#pragma unroll
-          for (int e = 0; e < CPL / 2; ++e) sd = pk_fma(x[e], v2[e], sd);
-          const float d = group_sum<LPR>(sd.x + sd.y);
-          if (tt[u] >= 0 && c_l == 0) wd[tt[u]] = d;
+          const float d = group_sum<LPR>(dot16<scalar_t>(g[u], vr));
+          if (have && c_l == 0) wd[tt] = d;
         }
       }
     }
@@ -1010,23 +1077,61 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
         a[2 * e] = acc[e].x;
         a[2 * e + 1] = acc[e].y;
       }
-      store_vec<scalar_t, CPL>(gvl + row * rs, a);
+      store_vec_nt<scalar_t, CPL>(gvl + row * rs, a);
     }
   }
+  MSDA_PH(5);
   if constexpr (COORDS) {
     __syncthreads();
     // 5. coordinate gradients of the level's samples: d_k = wd[2s + k] (0 off the map)
     float* __restrict__ gab = gaw == nullptr ? nullptr : gaw + (b * Lq * M + m) * LP + l * P;
     float* __restrict__ glb = gloc == nullptr ? nullptr : gloc + (b * Lq * M + m) * LP + l * P;
-    for (int s = threadIdx.x; s < nsamp; s += kGvThreads) {
-      const int q = s / P, p = s - q * P;
-      const long long o = q * qs + p;
-      const Taps<float> t = make_taps<float, ZEROS>(locb[o], T);
-      const float d0 = wd[2 * s], d1 = wd[2 * s + 1];
-      if (gab != nullptr) gab[o] = d0 * t.w0 + d1 * t.w1;
-      if (glb != nullptr) glb[o] = ((d1 - d0) * awb[o]) * t.gmul;
+    // the first kGvCache samples of every thread still have loc / aw in registers (pass 1)
+#pragma unroll
+    for (int k = 0; k < kGvCache; ++k) {
+      const int s = threadIdx.x + k * kGvThreads;
+      if (s < nsamp) {
+        const int q = s / P, p = s - q * P;
+        const long long o = q * qs + p;
+        const Taps<float> t = make_taps<float, ZEROS>(cl[k], T);
+        const float d0 = wd[2 * s], d1 = wd[2 * s + 1];
+        if (gab != nullptr) gab[o] = d0 * t.w0 + d1 * t.w1;
+        if (glb != nullptr) glb[o] = ((d1 - d0) * ca[k]) * t.gmul;
+      }
+    }
+    for (int s0 = kGvThreads * kGvCache; s0 < nsamp; s0 += kGvThreads * kGvCache) {
+      float lc[kGvCache], ac[kGvCache];  // all loads of the batch in flight together
+#pragma unroll
+      for (int k = 0; k < kGvCache; ++k) {
+        const int s = s0 + threadIdx.x + k * kGvThreads;
+        if (s < nsamp) {
+          const int q = s / P, p = s - q * P;
+          lc[k] = locb[q * qs + p];
+          ac[k] = awb[q * qs + p];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kGvCache; ++k) {
+        const int s = s0 + threadIdx.x + k * kGvThreads;
+        if (s < nsamp) {
+          const int q = s / P, p = s - q * P;
+          const long long o = q * qs + p;
+          const Taps<float> t = make_taps<float, ZEROS>(lc[k], T);
+          const float d0 = wd[2 * s], d1 = wd[2 * s + 1];
+          if (gab != nullptr) gab[o] = d0 * t.w0 + d1 * t.w1;
+          if (glb != nullptr) glb[o] = ((d1 - d0) * ac[k]) * t.gmul;
+        }
+      }
     }
   }
+#ifdef MSDA_PHASE_TIMING
+  MSDA_PH(6);
+  if (threadIdx.x == 0 && bm == 0)
+    printf("fused l=%d T=%d ncap=%d zero=%llu pass1=%llu scan=%llu place=%llu pull=%llu coords=%llu (x10ns)\n", l, T,
+           ncap, tph[1] - tph[0], tph[2] - tph[1], tph[3] - tph[2], tph[4] - tph[3], tph[5] - tph[4],
+           tph[6] - tph[5]);
+#endif
+#undef MSDA_PH
 }
 
 // grad_aw / grad_loc fast path (conditions of msda_fwd16_kernel): coordinates and the
@@ -1621,13 +1726,23 @@ int run_backward_fused(const Problem& pr, int ns, const void* value, const void*
   auto* gl = static_cast<float*>(gloc);
   auto* ga = static_cast<float*>(gaw);
   int rc;
-#define MSDA_FU(NSL, Z, C)                                                                        \
+  // gathers per batch: 8 when the finest level's rows average >= 8 taps (encoder-like
+  // calls), 4 for sparse levels (decoder-like: few taps per row, row-set changes dominate)
+  const bool wide = (long long)2 * pr.Lq * pr.P >= 8LL * maxT;
+#ifndef MSDA_FUSED_UW
+#define MSDA_FUSED_UW 8
+#endif
+#define MSDA_FU_U(NSL, Z, C, UU)                                                                  \
   do {                                                                                          \
-    if ((rc = allow_lds(msda_bwd_fused_kernel<scalar_t, NSL, Z, C, 8>, lds))) return rc;        \
-    hipLaunchKernelGGL((msda_bwd_fused_kernel<scalar_t, NSL, Z, C, 8>), dim3(blocks),           \
+    if ((rc = allow_lds(msda_bwd_fused_kernel<scalar_t, NSL, Z, C, UU>, lds))) return rc;       \
+    hipLaunchKernelGGL((msda_bwd_fused_kernel<scalar_t, NSL, Z, C, UU>), dim3(blocks),          \
                        dim3(kGvThreads), lds, st, v, lc, a, g, gv, gl, ga, pr.lv, (int)pr.L,      \
                        (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq,                  \
                        deterministic_rows);                                                     \
+  } while (0)
+#define MSDA_FU(NSL, Z, C)                                                                        \
+  do {                                                                                          \
+    if (wide) MSDA_FU_U(NSL, Z, C, MSDA_FUSED_UW); else MSDA_FU_U(NSL, Z, C, 4);                            \
   } while (0)
 #define MSDA_FU_NS(Z, C)                                                                          \
   switch (ns) {                                                                                 \
@@ -1643,6 +1758,7 @@ int run_backward_fused(const Problem& pr, int ns, const void* value, const void*
   }
 #undef MSDA_FU_NS
 #undef MSDA_FU
+#undef MSDA_FU_U
   return launch_status("backward fused");
 }
 
