@@ -18,6 +18,7 @@ from .models.base_encoder import BaseEncoder
 from .models.deformable.unimodal_deformable_transformer import DeformableTransformer
 from .models.modules.embedding_layers import FFN, PositionEmbeddingVideoSine
 from .models.modules.misc_modules import predict_event_num
+from .models.modules.linear import Linear
 
 __all__ = ["DeformableDVCCore", "synthetic_clips", "workload_loss"]
 
@@ -29,9 +30,9 @@ class DeformableDVCCore(nn.Module):
         super().__init__()
         self.num_queries = num_queries
         self.query_embedding = nn.Embedding(num_queries, d_model * 2)
-        class_embedding = nn.Linear(d_model, num_classes + 1)
+        class_embedding = Linear(d_model, num_classes + 1)
         segment_embedding = FFN(in_dim=d_model, hidden_dim=d_model, out_dim=2, num_layers=3)
-        count_head = nn.Linear(d_model, max_eseq_length + 1)
+        count_head = Linear(d_model, max_eseq_length + 1)
         self.pos_embed = PositionEmbeddingVideoSine(d_model // 2, normalize=True)
         self.base_encoder = BaseEncoder(num_feature_levels, feature_dim, d_model)
         # head init of unimodal_deformable_dvc.py:59-71

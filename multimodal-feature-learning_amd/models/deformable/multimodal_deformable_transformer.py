@@ -15,6 +15,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from ..modules.attention import MSDeformAttn
 from ..modules.misc_modules import inverse_sigmoid
+from ..modules.linear import Linear
 from .unimodal_deformable_transformer import (_get_activation_fn, _get_clones, encoder_reference_points,
                                               level_metadata)
 
@@ -46,9 +47,9 @@ class MultimodalDeformableTransformer(nn.Module):
                                                         num_feature_levels, num_head, dec_n_points),
             num_decoder_layers, return_intermediate_dec)
         self.level_embed = nn.Parameter(torch.Tensor(num_feature_levels, d_model))
-        self.pos_trans = nn.Linear(d_model, d_model * 2)
+        self.pos_trans = Linear(d_model, d_model * 2)
         self.pos_trans_norm = nn.LayerNorm(d_model * 2)
-        self.reference_points = nn.Linear(d_model, 1)
+        self.reference_points = Linear(d_model, 1)
         self._reset_parameters()
 
     def _reset_parameters(self):
@@ -118,10 +119,10 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
         self.self_attn = MSDeformAttn(d_model, n_levels, n_heads, n_points)
         self.dropout1 = nn.Dropout(dropout)
         self.norm1 = nn.LayerNorm(d_model)
-        self.linear1 = nn.Linear(d_model, d_ffn)
+        self.linear1 = Linear(d_model, d_ffn)
         self.activation = _get_activation_fn(activation)
         self.dropout2 = nn.Dropout(dropout)
-        self.linear2 = nn.Linear(d_ffn, d_model)
+        self.linear2 = Linear(d_ffn, d_model)
         self.dropout3 = nn.Dropout(dropout)
         self.norm2 = nn.LayerNorm(d_model)
 
@@ -188,14 +189,14 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
         self.self_attn = nn.MultiheadAttention(d_model, n_heads, dropout=dropout)
         self.dropout2 = nn.Dropout(dropout)
         self.norm2 = nn.LayerNorm(d_model)
-        self.linear1 = nn.Linear(d_model, d_ffn)
+        self.linear1 = Linear(d_model, d_ffn)
         self.activation = _get_activation_fn(activation)
         self.dropout3 = nn.Dropout(dropout)
-        self.linear2 = nn.Linear(d_ffn, d_model)
+        self.linear2 = Linear(d_ffn, d_model)
         self.dropout4 = nn.Dropout(dropout)
         self.norm3 = nn.LayerNorm(d_model)
         self.norm4 = nn.LayerNorm(2 * d_model)
-        self.linear3 = nn.Linear(2 * d_model, d_model)
+        self.linear3 = Linear(2 * d_model, d_model)
         self.dropout5 = nn.Dropout(dropout)
 
     @staticmethod

@@ -7,6 +7,7 @@ import torch
 from torch import nn
 
 from .misc_modules import NestedTensor
+from .linear import Linear
 
 __all__ = ["PositionEmbeddingVideoSine", "FFN"]
 
@@ -32,7 +33,7 @@ class PositionEmbeddingVideoSine(nn.Module):
         if scale is None:
             scale = 2 * math.pi
         self.scale = scale
-        self.duration_embed_layer = nn.Linear(self.num_pos_feats, self.num_pos_feats)
+        self.duration_embed_layer = Linear(self.num_pos_feats, self.num_pos_feats)
 
     def forward(self, tensor_list: NestedTensor):
         x = tensor_list.tensors
@@ -66,7 +67,7 @@ class FFN(nn.Module):
         super().__init__()
         self.num_layers = num_layers
         h = [hidden_dim] * (num_layers - 1)
-        self.layers = nn.ModuleList(nn.Linear(n, k) for n, k in zip([in_dim] + h, h + [out_dim]))
+        self.layers = nn.ModuleList(Linear(n, k) for n, k in zip([in_dim] + h, h + [out_dim]))
         self.relu = nn.ReLU()
 
     def forward(self, x):

@@ -1,0 +1,85 @@
+"""``nn.Linear`` with an MI355X-shaped backward under bf16/fp16 autocast.
+
+Same parameters, state_dict keys, init and forward math as ``torch.nn.Linear`` (every Linear
+of the reference's deformable stack, e.g. ``models/modules/attention.py:417-420`` and the
+FFNs of ``unimodal_deformable_transformer.py:174-177``).  Only the autocast backward differs:
+
+* autograd computes ``dW = dY^T X`` as ONE hipBLASLt GEMM with a bf16 output.  At the bench
+  step's shapes (K = 15,360 tokens, 512x512 or 128x512 outputs) that GEMM has 16-64 output
+  tiles for 256 CUs and no split-K: ~100-125 us each (tools/gemm_probe.py).  Then it casts
+  the bf16 result to fp32 and adds it into ``p.grad`` (two more kernels, bf16 rounding
+  of the whole gradient).
+* here the K dimension is split into ``s`` chunks, one strided-batched GEMM writes the fp32
+  partial products (fp32 accumulate and output, ``out_dtype``), and their sum is the fp32
+  gradient: 30-55 us at the same shapes and ~1000x less rounding error; short K (decoder
+  queries) uses a single GEMM with fp32 output.  The bias gradient is one fp32-output
+  reduction.
+
+Outside autocast on a GPU (fp32 / fp64 parity runs) and on the CPU it is exactly
+``F.linear``.
+"""
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+__all__ = ["Linear", "split_k_chunks"]
+
+
+def split_k_chunks(k, min_chunk=1024, max_split=8):
+    """Number of K chunks for the weight-gradient GEMM: the largest s <= max_split dividing K
+    with K / s >= min_chunk (1 = no split)."""
+    s = max_split
+    while s > 1:
+        if k % s == 0 and k // s >= min_chunk:
+            return s
+        s //= 2
+    return 1
+
+
+class _AutocastLinear(torch.autograd.Function):
+    """y = x W^T + b with x already in the autocast dtype; W, b fp32 masters."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias):
+        dt = x.dtype
+        wc = weight.to(dt)
+        x2 = x.reshape(-1, x.shape[-1])
+        if bias is not None:
+            y = torch.addmm(bias.to(dt), x2, wc.t())
+        else:
+            y = torch.mm(x2, wc.t())
+        ctx.save_for_backward(x2, wc)
+        ctx.has_bias = bias is not None
+        ctx.x_shape = x.shape
+        return y.view(*x.shape[:-1], wc.shape[0])
+
+    @staticmethod
+    def backward(ctx, gy):
+        x2, wc = ctx.saved_tensors
+        g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype)
+        gx = gw = gb = None
+        if ctx.needs_input_grad[0]:
+            gx = torch.mm(g2, wc).view(ctx.x_shape)
+        if ctx.needs_input_grad[1]:
+            k, n_out, n_in = x2.shape[0], g2.shape[1], x2.shape[1]
+            s = split_k_chunks(k)
+            if s > 1:
+                part = torch.empty(s, n_out, n_in, device=g2.device, dtype=torch.float32)
+                torch.baddbmm(part, g2.view(s, k // s, n_out).transpose(1, 2), x2.view(s, k // s, n_in),
+                              beta=0, out_dtype=torch.float32, out=part)
+                gw = part.sum(0)
+            else:
+                gw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
+        if ctx.has_bias and ctx.needs_input_grad[2]:
+            gb = g2.sum(0, dtype=torch.float32)
+        return gx, gw, gb
+
+
+class Linear(nn.Linear):
+    def forward(self, x):
+        if (x.is_cuda and torch.is_autocast_enabled("cuda") and self.weight.dtype == torch.float32
+                and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16)):
+            dt = torch.get_autocast_dtype("cuda")
+            with torch.autocast("cuda", enabled=False):
+                return _AutocastLinear.apply(x.to(dt), self.weight, self.bias)
+        return F.linear(x, self.weight, self.bias)

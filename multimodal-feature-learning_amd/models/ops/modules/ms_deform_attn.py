@@ -12,6 +12,7 @@ from torch.nn.init import constant_, xavier_uniform_
 
 from .... import msda as _msda
 from ..functions import MSDeformAttnFunction, ms_deform_attn_core_pytorch
+from ...modules.linear import Linear
 
 __all__ = ["MSDeformAttn", "MSDeformAttnCap", "stack_sampled_values"]
 
@@ -51,10 +52,10 @@ class MSDeformAttn(nn.Module):
         self.n_levels = n_levels
         self.n_heads = n_heads
         self.n_points = n_points
-        self.sampling_offsets = nn.Linear(d_model, n_heads * n_levels * n_points)
-        self.attention_weights = nn.Linear(d_model, n_heads * n_levels * n_points)
-        self.value_proj = nn.Linear(d_model, d_model)
-        self.output_proj = nn.Linear(d_model, d_model)
+        self.sampling_offsets = Linear(d_model, n_heads * n_levels * n_points)
+        self.attention_weights = Linear(d_model, n_heads * n_levels * n_points)
+        self.value_proj = Linear(d_model, d_model)
+        self.output_proj = Linear(d_model, d_model)
         self._reset_parameters()
 
     def _reset_parameters(self):

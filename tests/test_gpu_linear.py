@@ -1,0 +1,72 @@
+"""The package Linear (models/modules/linear.py): same forward as nn.Linear, split-K fp32
+weight gradient under bf16 autocast.  GPU cases compare with an fp64 reference computed from
+the same bf16-rounded operands (the only rounding left is the bf16 forward output and the
+fp32 accumulation order), and with stock autograd's bf16 gradient."""
+import pytest
+import torch
+
+from conftest import PKG
+
+linear_mod = PKG.models.modules.linear
+
+
+def test_split_k_chunks():
+    f = linear_mod.split_k_chunks
+    assert f(15360) == 8
+    assert f(8192) == 8
+    assert f(4096) == 4
+    assert f(2048) == 2
+    assert f(800) == 1
+    assert f(15361) == 1
+    assert f(0) == 1
+
+
+def test_cpu_is_plain_linear():
+    torch.manual_seed(0)
+    lin = linear_mod.Linear(16, 8)
+    ref = torch.nn.Linear(16, 8)
+    ref.load_state_dict(lin.state_dict())
+    x = torch.randn(3, 5, 16)
+    torch.testing.assert_close(lin(x), ref(x), rtol=0, atol=0)
+    assert set(lin.state_dict()) == {"weight", "bias"}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tokens,n_in,n_out", [(15360, 512, 512), (15360, 512, 128), (800, 512, 2048),
+                                               (7, 64, 30)])
+def test_autocast_grads_match_fp64(dev, tokens, n_in, n_out):
+    torch.manual_seed(0)
+    lin = linear_mod.Linear(n_in, n_out).to(dev)
+    x = torch.randn(1, tokens, n_in, device=dev, requires_grad=True)
+    gy = torch.randn(1, tokens, n_out, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = lin(x)
+    assert y.dtype == torch.bfloat16
+    y.backward(gy.to(torch.bfloat16))
+    # fp64 reference on the bf16-rounded operands autocast feeds the GEMMs
+    xb = x.detach().to(torch.bfloat16).double().reshape(-1, n_in)
+    wb = lin.weight.detach().to(torch.bfloat16).double()
+    gb = gy.to(torch.bfloat16).double().reshape(-1, n_out)
+    y_ref = xb @ wb.t() + lin.bias.detach().to(torch.bfloat16).double()
+    torch.testing.assert_close(y.double().reshape(-1, n_out), y_ref, rtol=1e-2, atol=1e-2)
+    gw_ref = gb.t() @ xb
+    gbias_ref = gb.sum(0)
+    assert lin.weight.grad.dtype == torch.float32
+    torch.testing.assert_close(lin.weight.grad.double(), gw_ref, rtol=1e-5, atol=1e-5 * gw_ref.abs().max().item())
+    torch.testing.assert_close(lin.bias.grad.double(), gbias_ref, rtol=1e-5, atol=1e-5 * gbias_ref.abs().max().item())
+    gx_ref = (gb @ wb).reshape(x.shape)
+    torch.testing.assert_close(x.grad.double(), gx_ref, rtol=2e-2, atol=2e-2 * gx_ref.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_accumulates_into_existing_grad(dev):
+    """Shared heads (the DVC wrapper reuses one Linear per decoder level) accumulate."""
+    torch.manual_seed(1)
+    lin = linear_mod.Linear(64, 32).to(dev)
+    x = torch.randn(4096, 64, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        (lin(x).float().sum() + lin(x * 2).float().sum()).backward()
+    xb = x.to(torch.bfloat16).double()
+    x2b = (x * 2).to(torch.bfloat16).double()
+    ref = xb.sum(0) + x2b.sum(0)
+    torch.testing.assert_close(lin.weight.grad.double(), ref.expand(32, 64), rtol=1e-5, atol=1e-3)
