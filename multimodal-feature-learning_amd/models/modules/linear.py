@@ -37,15 +37,17 @@ def split_k_chunks(k, min_chunk=1024, max_split=8):
 
 
 class _AutocastLinear(torch.autograd.Function):
-    """y = x W^T + b with x already in the autocast dtype; W, b fp32 masters."""
+    """y = x W^T + b with x already in the autocast dtype; W, b fp32 masters; wc / bc optional
+    low-precision copies of W / b (the trainer's shadow) used instead of casting."""
 
     @staticmethod
-    def forward(ctx, x, weight, bias):
+    def forward(ctx, x, weight, bias, wc, bc):
         dt = x.dtype
-        wc = weight.to(dt)
+        if wc is None:
+            wc = weight.to(dt)
         x2 = x.reshape(-1, x.shape[-1])
         if bias is not None:
-            y = torch.addmm(bias.to(dt), x2, wc.t())
+            y = torch.addmm(bias.to(dt) if bc is None else bc, x2, wc.t())
         else:
             y = torch.mm(x2, wc.t())
         ctx.save_for_backward(x2, wc)
@@ -72,14 +74,26 @@ class _AutocastLinear(torch.autograd.Function):
                 gw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
         if ctx.has_bias and ctx.needs_input_grad[2]:
             gb = g2.sum(0, dtype=torch.float32)
-        return gx, gw, gb
+        return gx, gw, gb, None, None
 
 
 class Linear(nn.Linear):
+    _shadow = None  # (weight copy, bias copy, weight version) set by set_bf16_shadow
+
+    def set_bf16_shadow(self, weight_bf16, bias_bf16):
+        """Use these bf16 copies of weight / bias under bf16 autocast for as long as the fp32
+        weight is not modified in place (its version counter is recorded now).  The training
+        step refreshes them after every optimizer step (train_step.FlatGradTrainer)."""
+        self._shadow = (weight_bf16, bias_bf16, self.weight._version)
+
     def forward(self, x):
         if (x.is_cuda and torch.is_autocast_enabled("cuda") and self.weight.dtype == torch.float32
                 and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16)):
             dt = torch.get_autocast_dtype("cuda")
+            wc = bc = None
+            sh = self._shadow
+            if sh is not None and dt == torch.bfloat16 and sh[2] == self.weight._version:
+                wc, bc = sh[0], sh[1]
             with torch.autocast("cuda", enabled=False):
-                return _AutocastLinear.apply(x.to(dt), self.weight, self.bias)
+                return _AutocastLinear.apply(x.to(dt), self.weight, self.bias, wc, bc)
         return F.linear(x, self.weight, self.bias)

@@ -5,8 +5,13 @@ forward, ``loss.backward()`` with the bucketed NCCL all-reduce overlapped, then
 ``clip_grad_norm_(max_norm)`` and the optimizer step.  Here the step is restructured for
 the MI355X the way the hardware wants it:
 
-* every gradient lives in ONE flat fp32 buffer (``p.grad`` are views into it, so autograd
-  accumulates in place and there is nothing to copy in or out of buckets);
+* parameters and gradients each live in ONE flat fp32 buffer (``p`` and ``p.grad`` are views
+  into them).  The backward starts with ``p.grad = None``, so autograd hands each parameter
+  its freshly computed gradient without an accumulate kernel, and one multi-tensor copy
+  moves them into the flat gradient buffer (instead of ~260 per-parameter add kernels);
+* under bf16 autocast a bf16 shadow of the flat parameters is refreshed by ONE cast kernel
+  after every optimizer step, and the Linear layers read their bf16 weights from it
+  (instead of ~200 per-use weight / bias casts, models/modules/linear.py);
 * the forward+backward and the clip+AdamW halves are each captured once into a HIP graph
   and replayed — the ~1500 kernels of a step are launched by two ``hipGraphLaunch`` calls
   instead of ~1500 Python-driven launches (the eager step is launch-bound: its GPU is idle
@@ -20,6 +25,8 @@ the MI355X the way the hardware wants it:
 """
 import torch
 import torch.distributed as dist
+
+from .models.modules.linear import Linear
 
 __all__ = ["FlatGradTrainer"]
 
@@ -37,14 +44,34 @@ class FlatGradTrainer:
         self.params = [p for p in model.parameters() if p.requires_grad]
         dev = self.params[0].device
         self.device = dev
-        n = sum(p.numel() for p in self.params)
-        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
-        off = 0
         for p in self.params:
             if p.dtype != torch.float32:
                 raise TypeError("FlatGradTrainer keeps fp32 master parameters; got " + str(p.dtype))
-            p.grad = self.flat_grad[off:off + p.numel()].view_as(p)
-            off += p.numel()
+        n = sum(p.numel() for p in self.params)
+        self.flat_param = torch.empty(n, dtype=torch.float32, device=dev)
+        self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
+        self.grad_views = []
+        off = 0
+        for p in self.params:
+            k = p.numel()
+            self.flat_param[off:off + k].copy_(p.detach().reshape(-1))
+            p.data = self.flat_param[off:off + k].view_as(p)
+            self.grad_views.append(self.flat_grad[off:off + k].view_as(p))
+            off += k
+        self._attach_grads()
+        # bf16 weight shadow for the autocast Linear layers (one cast per step, _refresh_shadow)
+        self.flat_bf16 = None
+        self._linears = []
+        if use_bf16 and dev.type == "cuda":
+            self.flat_bf16 = self.flat_param.to(torch.bfloat16)
+            index = {id(p): v for p, v in zip(self.params, self._views(self.flat_bf16))}
+            for mod in model.modules():
+                if isinstance(mod, Linear) and id(mod.weight) in index:
+                    b = index.get(id(mod.bias)) if mod.bias is not None else None
+                    if mod.bias is not None and b is None:
+                        continue
+                    self._linears.append((mod, index[id(mod.weight)], b))
+            self._refresh_shadow()
         self.opt = torch.optim.AdamW(self.params, lr=lr, weight_decay=weight_decay, capturable=graph,
                                      foreach=True)
         self._g_fb = None
@@ -52,13 +79,41 @@ class FlatGradTrainer:
         self._loss = None
 
     # --- the three phases ------------------------------------------------------------
+    def _views(self, flat):
+        out, off = [], 0
+        for p in self.params:
+            out.append(flat[off:off + p.numel()].view_as(p))
+            off += p.numel()
+        return out
+
+    def _attach_grads(self):
+        for p, g in zip(self.params, self.grad_views):
+            p.grad = g
+
+    def _refresh_shadow(self):
+        """bf16 copy of every parameter (one kernel); Linear layers use it while their fp32
+        weight's version counter still matches (any other in-place change disables it)."""
+        if self.flat_bf16 is None:
+            return
+        self.flat_bf16.copy_(self.flat_param)
+        for mod, w, b in self._linears:
+            mod.set_bf16_shadow(w, b)
+
     def _forward_backward(self, batch, cache_casts=True):
-        self.flat_grad.zero_()
+        for p in self.params:  # autograd then hands over fresh gradients (no accumulate kernels)
+            p.grad = None
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_bf16,
                             cache_enabled=cache_casts):
             out = self.model(*batch)
             loss = self.loss_fn(out)
         loss.backward()
+        got = [(v, p.grad) for p, v in zip(self.params, self.grad_views) if p.grad is not None]
+        missing = [v for p, v in zip(self.params, self.grad_views) if p.grad is None]
+        if got:
+            torch._foreach_copy_([v for v, _ in got], [g for _, g in got])
+        if missing:
+            torch._foreach_zero_(missing)
+        self._attach_grads()
         return loss.detach()
 
     def _allreduce(self):
@@ -69,6 +124,7 @@ class FlatGradTrainer:
     def _update(self):
         torch.nn.utils.clip_grad_norm_(self.params, self.max_norm, foreach=True)
         self.opt.step()
+        self._refresh_shadow()
 
     # --- public -------------------------------------------------------------------------
     def eager_step(self, batch):

@@ -70,3 +70,21 @@ def test_accumulates_into_existing_grad(dev):
     x2b = (x * 2).to(torch.bfloat16).double()
     ref = xb.sum(0) + x2b.sum(0)
     torch.testing.assert_close(lin.weight.grad.double(), ref.expand(32, 64), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_bf16_shadow_is_bitwise_the_cast_and_expires(dev):
+    torch.manual_seed(2)
+    lin = linear_mod.Linear(64, 48).to(dev)
+    x = torch.randn(300, 64, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y_cast = lin(x)
+    lin.set_bf16_shadow(lin.weight.detach().to(torch.bfloat16), lin.bias.detach().to(torch.bfloat16))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y_shadow = lin(x)
+    torch.testing.assert_close(y_shadow, y_cast, rtol=0, atol=0)
+    with torch.no_grad():  # an in-place change to the master weight retires the shadow
+        lin.weight.mul_(2)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y_new = lin(x)
+    torch.testing.assert_close(y_new.float(), (x @ (lin.weight.t())).float() + lin.bias, rtol=2e-2, atol=5e-2)
