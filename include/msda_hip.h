@@ -100,6 +100,33 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
                       int64_t spatial_size, int64_t num_heads, int64_t channels,
                       int64_t num_query, int64_t num_point, int padding_mode, void* stream);
 
+/* MSDA prologue.  Replaces the elementwise chain of MSDeformAttn.forward
+ * between its two query projections and the core (reference models/modules/attention.py:468-483):
+ *   attn_weight  = softmax(attn_logits over num_levels*num_point)                 (coord dtype)
+ *   sampling_loc = ref[..., 0] + sampling_offsets / T_l                          (ref_dim == 1)
+ *   sampling_loc = ref[..., 0] + sampling_offsets / num_point * ref[..., 1] * 0.5 (ref_dim == 2)
+ *   sampling_offsets, attn_logits  (batch, num_query, num_heads, num_levels, num_point)  dtype
+ *   reference_points               (batch, num_query, num_levels, ref_dim)          coord dtype
+ *   sampling_loc, attn_weight      (batch, num_query, num_heads, num_levels, num_point)  coord dtype
+ * 16-bit dtypes reproduce PyTorch's promotion under autocast (offsets / T_l rounded to the
+ * 16-bit dtype once; the softmax in fp32).  num_heads must be a power of two <= 64 and
+ * num_levels*num_point <= 64. */
+int msda_hip_prologue_forward(const void* sampling_offsets, const void* attn_logits, int dtype,
+                              const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
+                              int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,
+                              int64_t num_point, void* sampling_loc, void* attn_weight, void* stream);
+
+/* Backward of msda_hip_prologue_forward: from grad_loc / grad_attn (coord dtype, the outputs of
+ * msda_hip_backward) and the forward's attn_weight, writes grad_offsets and grad_logits (dtype)
+ * and grad_ref (coord dtype, (batch, num_query, num_levels, ref_dim), summed over heads and
+ * points).  Any output may be NULL to skip it; sampling_offsets / reference_points are read
+ * only for ref_dim == 2. */
+int msda_hip_prologue_backward(const void* grad_loc, const void* grad_attn, const void* attn_weight,
+                               const void* sampling_offsets, int dtype, const void* reference_points,
+                               int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
+                               int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
+                               void* grad_offsets, void* grad_logits, void* grad_ref, void* stream);
+
 /* Text of the last error raised on the calling thread ("" if none). */
 const char* msda_hip_last_error(void);
 

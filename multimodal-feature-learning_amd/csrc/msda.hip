@@ -1793,13 +1793,279 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
   return rc;
 }
 
+
+// ---------------------------------------------------------------------------------
+// MSDA prologue: the elementwise chain of MSDeformAttn.forward between
+// the sampling_offsets / attention_weights projections and the core
+// (reference models/modules/attention.py:468-483):
+//   aw  = softmax(attention_weights(query).view(..., L*P))            (fp32 under autocast)
+//   loc = ref[..., 0] + off / T_l                         (ref_dim 1)
+//   loc = ref[..., 0] + off / P * ref[..., 1] * 0.5       (ref_dim 2, the box form)
+// in ONE kernel per direction instead of ~5 PyTorch kernels each.  The 16-bit cases keep
+// PyTorch's type promotion exactly: off / T_l and off / P are 16-bit tensors (computed in
+// fp32, rounded once), everything after the promotion to the fp32 reference is fp32; the
+// backward rounds where autograd casts back to the 16-bit inputs.
+// One thread per (b, q, m) item; M a power of two <= 64 so that the M items of one query are
+// aligned lanes of one wave (grad_ref is a DPP sum over them).
+// ---------------------------------------------------------------------------------
+template <typename scalar_t> struct Is16 { static constexpr bool value = false; };
+template <> struct Is16<bf16_t> { static constexpr bool value = true; };
+template <> struct Is16<f16_t> { static constexpr bool value = true; };
+
+// value rounded to scalar_t and back (identity for fp32 / fp64)
+template <typename scalar_t, typename coord_t>
+__device__ __forceinline__ coord_t round_to(coord_t v) {
+  if constexpr (Is16<scalar_t>::value) {
+    scalar_t h;
+    from_acc((float)v, &h);
+    return (coord_t)to_acc(h);
+  } else {
+    return v;
+  }
+}
+
+template <typename coord_t>
+__device__ __forceinline__ coord_t lanes_sum(coord_t x, int M) {
+  switch (M) {
+    case 1: return x;
+    case 2: return group_sum<2>(x);
+    case 4: return group_sum<4>(x);
+    case 8: return group_sum<8>(x);
+    case 16: return group_sum<16>(x);
+    case 32: return group_sum<32>(x);
+    default: return group_sum<64>(x);
+  }
+}
+
+template <typename scalar_t, typename coord_t, int LPMAX>
+__global__ __launch_bounds__(256) void msda_prologue_fwd_kernel(
+    const scalar_t* __restrict__ off, const scalar_t* __restrict__ logits,
+    const coord_t* __restrict__ ref, const int ref_dim, coord_t* __restrict__ loc,
+    coord_t* __restrict__ aw, const Levels lv, const int L, const int P, const int M,
+    const long long n_items) {
+  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= n_items) return;
+  const int LP = L * P;
+  const long long bq = item / M;
+  const scalar_t* __restrict__ o = off + item * LP;
+  const scalar_t* __restrict__ a = logits + item * LP;
+  coord_t x[LPMAX];
+  coord_t mx = -INFINITY;
+#pragma unroll
+  for (int j = 0; j < LPMAX; ++j) {
+    if (j < LP) {
+      x[j] = (coord_t)to_acc(a[j]);
+      mx = x[j] > mx ? x[j] : mx;
+    }
+  }
+  coord_t sum = 0;
+#pragma unroll
+  for (int j = 0; j < LPMAX; ++j) {
+    if (j < LP) {
+      x[j] = exp(x[j] - mx);
+      sum += x[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < LPMAX; ++j)
+    if (j < LP) aw[item * LP + j] = x[j] / sum;
+  for (int l = 0; l < L; ++l) {
+    const coord_t T = (coord_t)lv.T[l];
+    const coord_t r0 = ref[(bq * L + l) * ref_dim];
+    const coord_t r1 = ref_dim == 2 ? ref[(bq * L + l) * 2 + 1] : (coord_t)0;
+    for (int p = 0; p < P; ++p) {
+      const int j = l * P + p;
+      const coord_t v = (coord_t)to_acc(o[j]);
+      coord_t lc;
+      if (ref_dim == 1) {
+        lc = r0 + round_to<scalar_t>(v / T);
+      } else {
+        lc = r0 + (round_to<scalar_t>(v / (coord_t)P) * r1) * (coord_t)0.5;
+      }
+      loc[item * LP + j] = lc;
+    }
+  }
+}
+
+template <typename scalar_t, typename coord_t, int LPMAX>
+__global__ __launch_bounds__(256) void msda_prologue_bwd_kernel(
+    const coord_t* __restrict__ grad_loc, const coord_t* __restrict__ grad_aw,
+    const coord_t* __restrict__ aw, const scalar_t* __restrict__ off, const coord_t* __restrict__ ref,
+    const int ref_dim, scalar_t* __restrict__ grad_off, scalar_t* __restrict__ grad_logits,
+    coord_t* __restrict__ grad_ref, const Levels lv, const int L, const int P, const int M,
+    const long long n_items) {
+  const long long item_raw = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = item_raw < n_items;  // all lanes stay for the grad_ref reduction
+  const long long item = active ? item_raw : 0;
+  const int LP = L * P;
+  const long long bq = item / M;
+  const int m = (int)(item % M);
+  if (grad_logits != nullptr && active) {
+    coord_t g[LPMAX], y[LPMAX];
+    coord_t dot = 0;
+#pragma unroll
+    for (int j = 0; j < LPMAX; ++j) {
+      if (j < LP) {
+        g[j] = grad_aw[item * LP + j];
+        y[j] = aw[item * LP + j];
+        dot += g[j] * y[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < LPMAX; ++j)
+      if (j < LP) from_acc((typename AccOf<scalar_t>::type)(y[j] * (g[j] - dot)), &grad_logits[item * LP + j]);
+  }
+  if (grad_off == nullptr && grad_ref == nullptr) return;
+  for (int l = 0; l < L; ++l) {
+    const coord_t T = (coord_t)lv.T[l];
+    const coord_t r1 = ref_dim == 2 ? ref[(bq * L + l) * 2 + 1] : (coord_t)0;
+    coord_t s0 = 0, s1 = 0;
+    for (int p = 0; p < P; ++p) {
+      const int j = l * P + p;
+      const coord_t gl = active ? grad_loc[item * LP + j] : (coord_t)0;
+      s0 += gl;
+      if (ref_dim == 1) {
+        if (grad_off != nullptr && active)
+          from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gl) / T), &grad_off[item * LP + j]);
+      } else {
+        const coord_t gh = gl * (coord_t)0.5;
+        if (grad_off != nullptr && active)
+          from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gh * r1) / (coord_t)P),
+                   &grad_off[item * LP + j]);
+        const coord_t u = active ? round_to<scalar_t>((coord_t)to_acc(off[item * LP + j]) / (coord_t)P) : (coord_t)0;
+        s1 += gh * u;
+      }
+    }
+    if (grad_ref != nullptr) {
+      s0 = lanes_sum(s0, M);
+      if (ref_dim == 2) s1 = lanes_sum(s1, M);
+      if (active && m == 0) {
+        grad_ref[(bq * L + l) * ref_dim] = s0;
+        if (ref_dim == 2) grad_ref[(bq * L + l) * 2 + 1] = s1;
+      }
+    }
+  }
+}
+
+template <typename scalar_t, typename coord_t>
+int run_prologue(bool fwd, const Problem& pr, int ref_dim, const void* off, const void* logits,
+                 const void* ref, void* loc, void* aw, const void* grad_loc, const void* grad_aw,
+                 void* grad_off, void* grad_logits, void* grad_ref, hipStream_t st) {
+  const long long n_items = pr.B * pr.Lq * pr.M;
+  if (n_items == 0) return MSDA_OK;
+  const unsigned blocks = (unsigned)((n_items + 255) / 256);
+  const int LP = (int)(pr.L * pr.P);
+  auto* o = static_cast<const scalar_t*>(off);
+  auto* r = static_cast<const coord_t*>(ref);
+#define MSDA_PRO(LPM)                                                                              \
+  do {                                                                                           \
+    if (fwd)                                                                                     \
+      hipLaunchKernelGGL((msda_prologue_fwd_kernel<scalar_t, coord_t, LPM>), dim3(blocks), dim3(256), 0, \
+                         st, o, static_cast<const scalar_t*>(logits), r, ref_dim,               \
+                         static_cast<coord_t*>(loc), static_cast<coord_t*>(aw), pr.lv, (int)pr.L, \
+                         (int)pr.P, (int)pr.M, n_items);                                         \
+    else                                                                                         \
+      hipLaunchKernelGGL((msda_prologue_bwd_kernel<scalar_t, coord_t, LPM>), dim3(blocks), dim3(256), 0, \
+                         st, static_cast<const coord_t*>(grad_loc), static_cast<const coord_t*>(grad_aw), \
+                         static_cast<const coord_t*>(aw), o, r, ref_dim,                          \
+                         static_cast<scalar_t*>(grad_off), static_cast<scalar_t*>(grad_logits),  \
+                         static_cast<coord_t*>(grad_ref), pr.lv, (int)pr.L, (int)pr.P, (int)pr.M, n_items); \
+  } while (0)
+  if (LP <= 16) MSDA_PRO(16);
+  else MSDA_PRO(64);
+#undef MSDA_PRO
+  return launch_status(fwd ? "prologue forward" : "prologue backward");
+}
+
+int check_prologue(const int64_t* shapes, int64_t L, int64_t B, int64_t Lq, int64_t M, int64_t P,
+                   int ref_dim, Problem* pr) {
+  if (L < 1 || L > MSDA_MAX_LEVELS || B < 0 || Lq < 0 || M < 1 || M > 64 || (M & (M - 1)) != 0 ||
+      P < 1 || L * P > 64 || (ref_dim != 1 && ref_dim != 2) || shapes == nullptr) {
+    set_error("msda prologue: bad arguments (L=%lld M=%lld P=%lld ref_dim=%d; M must be a power of two "
+              "<= 64, L*P <= 64)", (long long)L, (long long)M, (long long)P, ref_dim);
+    return MSDA_ERR_ARG;
+  }
+  for (int64_t l = 0; l < L; ++l) {
+    if (shapes[l] < 1) {
+      set_error("msda prologue: level %lld has T=%lld", (long long)l, (long long)shapes[l]);
+      return MSDA_ERR_ARG;
+    }
+    pr->lv.T[l] = (int)shapes[l];
+    pr->lv.start[l] = 0;
+  }
+  pr->B = B; pr->S = 0; pr->M = M; pr->D = 1; pr->Lq = Lq; pr->L = L; pr->P = P;
+  return MSDA_OK;
+}
+
+int dispatch_prologue(bool fwd, int dtype, const Problem& pr, int ref_dim, const void* off,
+                      const void* logits, const void* ref, void* loc, void* aw, const void* grad_loc,
+                      const void* grad_aw, void* grad_off, void* grad_logits, void* grad_ref,
+                      hipStream_t st) {
+  switch (dtype) {
+    case MSDA_DTYPE_F32:
+      return run_prologue<float, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw, grad_off,
+                                        grad_logits, grad_ref, st);
+    case MSDA_DTYPE_F64:
+      return run_prologue<double, double>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
+                                          grad_off, grad_logits, grad_ref, st);
+    case MSDA_DTYPE_BF16:
+      return run_prologue<bf16_t, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
+                                         grad_off, grad_logits, grad_ref, st);
+    case MSDA_DTYPE_F16:
+      return run_prologue<f16_t, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
+                                        grad_off, grad_logits, grad_ref, st);
+    default:
+      set_error("msda prologue: unknown dtype %d", dtype);
+      return MSDA_ERR_ARG;
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
-int msda_hip_abi_version(void) { return 2; }
+int msda_hip_abi_version(void) { return 3; }
 
 const char* msda_hip_last_error(void) { return g_last_error; }
+
+int msda_hip_prologue_forward(const void* sampling_offsets, const void* attn_logits, int dtype,
+                              const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
+                              int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,
+                              int64_t num_point, void* sampling_loc, void* attn_weight, void* stream) {
+  g_last_error[0] = 0;
+  Problem pr;
+  int rc = check_prologue(spatial_shapes, num_levels, batch, num_query, num_heads, num_point, ref_dim, &pr);
+  if (rc) return rc;
+  if (batch * num_query > 0 && (sampling_offsets == nullptr || attn_logits == nullptr ||
+                                reference_points == nullptr || sampling_loc == nullptr || attn_weight == nullptr)) {
+    set_error("msda_hip_prologue_forward: null pointer");
+    return MSDA_ERR_ARG;
+  }
+  return dispatch_prologue(true, dtype, pr, ref_dim, sampling_offsets, attn_logits, reference_points,
+                           sampling_loc, attn_weight, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           static_cast<hipStream_t>(stream));
+}
+
+int msda_hip_prologue_backward(const void* grad_loc, const void* grad_attn, const void* attn_weight,
+                               const void* sampling_offsets, int dtype, const void* reference_points,
+                               int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
+                               int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
+                               void* grad_offsets, void* grad_logits, void* grad_ref, void* stream) {
+  g_last_error[0] = 0;
+  Problem pr;
+  int rc = check_prologue(spatial_shapes, num_levels, batch, num_query, num_heads, num_point, ref_dim, &pr);
+  if (rc) return rc;
+  const bool need_loc_side = grad_offsets != nullptr || grad_ref != nullptr;
+  if (batch * num_query > 0 &&
+      ((need_loc_side && grad_loc == nullptr) || (grad_logits != nullptr && (grad_attn == nullptr || attn_weight == nullptr)) ||
+       (ref_dim == 2 && need_loc_side && (reference_points == nullptr || sampling_offsets == nullptr)))) {
+    set_error("msda_hip_prologue_backward: null pointer");
+    return MSDA_ERR_ARG;
+  }
+  return dispatch_prologue(false, dtype, pr, ref_dim, sampling_offsets, nullptr, reference_points, nullptr,
+                           const_cast<void*>(attn_weight), grad_loc, grad_attn, grad_offsets, grad_logits,
+                           grad_ref, static_cast<hipStream_t>(stream));
+}
 
 size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,
                                          int64_t num_heads, int64_t channels, int64_t num_query,

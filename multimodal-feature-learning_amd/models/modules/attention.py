@@ -132,6 +132,17 @@ class MSDeformAttn(nn.Module):
 
         sampling_offsets = self.sampling_offsets(query).view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
         attention_weights = self.attention_weights(query).view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
+        if (query.is_cuda and reference_points.shape[-1] in (1, 2)
+                and attention_weights.dtype == sampling_offsets.dtype
+                and _msda.prologue_supported(self.n_heads, self.n_levels, self.n_points)):
+            # softmax + location arithmetic in one HIP kernel each way
+            sampling_locations, attention_weights = _msda.msda_prologue_apply(
+                sampling_offsets, attention_weights, reference_points, shapes)
+            output = ms_deform_attn_core_pytorch(value, shapes, sampling_locations, attention_weights)
+            output = self.output_proj(output)
+            if is_sparse:
+                return output, sampling_locations.unsqueeze(-1), attention_weights
+            return output
         attention_weights = F.softmax(attention_weights, -1).view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
 
         if reference_points.shape[-1] == 1:

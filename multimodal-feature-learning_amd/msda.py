@@ -15,7 +15,8 @@ from . import _native
 
 __all__ = [
     "host_levels", "msda_forward", "msda_backward", "MSDAFunction", "msda_apply", "KernelTimer",
-    "algorithmic_bytes",
+    "algorithmic_bytes", "prologue_supported", "prologue_forward", "prologue_backward", "MSDAPrologueFunction",
+    "msda_prologue_apply",
 ]
 
 _timer = None  # KernelTimer while bench.py measures; None otherwise
@@ -238,3 +239,91 @@ def msda_apply(value, shapes, starts, loc, aw, padding_mode="border"):
     loc = loc.to(cd).contiguous()
     aw = aw.to(cd).contiguous()
     return MSDAFunction.apply(value, loc, aw, tuple(shapes), tuple(starts), padding_mode)
+
+
+# --- MSDA prologue -------------------------------------------------------
+
+def prologue_supported(n_heads, n_levels, n_points):
+    """The fused prologue kernel's shape limits (include/msda_hip.h)."""
+    return 1 <= n_heads <= 64 and (n_heads & (n_heads - 1)) == 0 and n_levels * n_points <= 64
+
+
+def prologue_forward(offsets, logits, ref, shapes):
+    """(sampling_loc, attn_weight) of the reference's MSDeformAttn prologue
+    (models/modules/attention.py:468-483) in one HIP kernel.
+
+    offsets (B, Lq, M, L, P) and logits (B, Lq, M, L*P) in one dtype (bf16 under autocast);
+    ref (B, Lq, L, 1 or 2) in the coordinate dtype; outputs (B, Lq, M, L, P) coord dtype."""
+    if not (offsets.is_cuda and logits.is_cuda and ref.is_cuda):
+        raise RuntimeError("MSDA prologue: ROCm device tensors required (no CPU implementation)")
+    if offsets.dtype not in _native.DTYPE_TAGS or logits.dtype != offsets.dtype:
+        raise TypeError(f"MSDA prologue: offsets / logits dtypes {offsets.dtype} / {logits.dtype}")
+    B, Lq, M, L, P = offsets.shape
+    cd = torch.float64 if offsets.dtype == torch.float64 else torch.float32
+    if ref.dtype != cd or ref.dim() != 4 or tuple(ref.shape[:3]) != (B, Lq, L) or ref.shape[3] not in (1, 2):
+        raise ValueError(f"MSDA prologue: reference_points {tuple(ref.shape)} {ref.dtype} does not match "
+                         f"offsets {tuple(offsets.shape)}")
+    if len(shapes) != L:
+        raise ValueError(f"MSDA prologue: {len(shapes)} level shapes for {L} levels")
+    for name, t in (("offsets", offsets), ("logits", logits), ("reference_points", ref)):
+        if not t.is_contiguous():
+            raise ValueError(f"MSDA prologue: {name} must be contiguous")
+    lib = _native.load_library()
+    loc = torch.empty((B, Lq, M, L, P), dtype=cd, device=offsets.device)
+    aw = torch.empty_like(loc)
+    rc = lib.msda_hip_prologue_forward(
+        offsets.data_ptr(), logits.data_ptr(), _native.DTYPE_TAGS[offsets.dtype], ref.data_ptr(), ref.shape[3],
+        _native.host_i64_array(shapes), L, B, Lq, M, P, loc.data_ptr(), aw.data_ptr(),
+        _native.stream_handle(offsets.device))
+    _native.check(rc, "msda_hip_prologue_forward")
+    return loc, aw
+
+
+def prologue_backward(grad_loc, grad_aw, aw, offsets, ref, shapes, need_off=True, need_logits=True,
+                      need_ref=True):
+    """(grad_offsets, grad_logits, grad_ref) of prologue_forward; unneeded ones are None."""
+    B, Lq, M, L, P = offsets.shape
+    cd = aw.dtype
+    lib = _native.load_library()
+    if grad_loc is None:
+        grad_loc = torch.zeros_like(aw)
+    if grad_aw is None:
+        grad_aw = torch.zeros_like(aw)
+    grad_loc = grad_loc.to(cd).contiguous()
+    grad_aw = grad_aw.to(cd).contiguous()
+    g_off = torch.empty_like(offsets) if need_off else None
+    g_log = torch.empty((B, Lq, M, L * P), dtype=offsets.dtype, device=offsets.device) if need_logits else None
+    g_ref = torch.empty_like(ref) if need_ref else None
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    rc = lib.msda_hip_prologue_backward(
+        grad_loc.data_ptr(), grad_aw.data_ptr(), aw.data_ptr(), offsets.data_ptr(),
+        _native.DTYPE_TAGS[offsets.dtype], ref.data_ptr(), ref.shape[3], _native.host_i64_array(shapes), L,
+        B, Lq, M, P, ptr(g_off), ptr(g_log), ptr(g_ref), _native.stream_handle(offsets.device))
+    _native.check(rc, "msda_hip_prologue_backward")
+    return g_off, g_log, g_ref
+
+
+class MSDAPrologueFunction(Function):
+    @staticmethod
+    def forward(ctx, offsets, logits, ref, shapes):
+        loc, aw = prologue_forward(offsets, logits, ref, shapes)
+        ctx.shapes = shapes
+        ctx.save_for_backward(aw, offsets, ref)
+        return loc, aw
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_loc, grad_aw):
+        aw, offsets, ref = ctx.saved_tensors
+        n_off, n_log, n_ref = ctx.needs_input_grad[:3]
+        g_off, g_log, g_ref = prologue_backward(grad_loc, grad_aw, aw, offsets, ref, ctx.shapes, n_off, n_log,
+                                                n_ref)
+        return g_off, g_log, g_ref, None
+
+
+def msda_prologue_apply(offsets, logits, ref, shapes):
+    """Differentiable fused prologue: offsets (B,Lq,M,L,P), logits (B,Lq,M,L*P) (same dtype),
+    ref (B,Lq,L,1|2) -> (sampling_loc, attn_weight) (B,Lq,M,L,P) in the coordinate dtype."""
+    cd = torch.float64 if offsets.dtype == torch.float64 else torch.float32
+    return MSDAPrologueFunction.apply(offsets.contiguous(), logits.to(offsets.dtype).contiguous(),
+                                      ref.to(cd).contiguous(), tuple(int(t) for t in shapes))

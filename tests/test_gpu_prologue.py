@@ -1,0 +1,118 @@
+"""Fused MSDA prologue (msda_hip_prologue_forward / _backward through the C-ABI) against the
+reference's own PyTorch composition of the same step (models/modules/attention.py:468-483:
+softmax over L*P, loc = ref + off / T_l or the box form ref0 + off / P * ref1 * 0.5), in
+fp64 / fp32 and under bf16 autocast, forward and backward.
+
+Tolerances: fp64 1e-12; fp32 locations bitwise (same two operations), softmax and its
+gradient 1e-6; bf16 autocast: locations bitwise (the kernel rounds off / T_l to bf16 exactly
+where PyTorch's promotion does), gradients within one bf16 ulp."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import PKG
+
+pytestmark = pytest.mark.gpu
+msda = PKG.msda
+
+
+def reference_prologue(off, logits, ref, shapes):
+    """attention.py:468-483 restated (the module's composite path)."""
+    B, Lq, M, L, P = off.shape
+    aw = F.softmax(logits, -1).view(B, Lq, M, L, P)
+    if ref.shape[-1] == 1:
+        normalizer = torch.tensor(shapes, device=off.device)
+        loc = ref[:, :, None, :, None, 0] + off / normalizer[None, None, None, :, None]
+    else:
+        loc = ref[:, :, None, :, None, 0] + off / P * ref[:, :, None, :, None, 1] * 0.5
+    return loc, aw
+
+
+def make(B, Lq, M, L, P, ref_dim, dtype, dev, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    off = (torch.randn(B, Lq, M, L, P, generator=g, dtype=torch.float64) * 3).to(dev, dtype)
+    logits = torch.randn(B, Lq, M, L * P, generator=g, dtype=torch.float64).to(dev, dtype)
+    cd = torch.float64 if dtype == torch.float64 else torch.float32
+    ref = torch.rand(B, Lq, L, ref_dim, generator=g, dtype=torch.float64).to(dev, cd)
+    gl = torch.randn(B, Lq, M, L, P, generator=g, dtype=torch.float64).to(dev, cd)
+    ga = torch.randn(B, Lq, M, L, P, generator=g, dtype=torch.float64).to(dev, cd)
+    return off, logits, ref, gl, ga
+
+
+def run_both(off, logits, ref, gl, ga, shapes):
+    outs = []
+    for fused in (True, False):
+        o = off.detach().clone().requires_grad_(True)
+        lg = logits.detach().clone().requires_grad_(True)
+        r = ref.detach().clone().requires_grad_(True)
+        if fused:
+            loc, aw = msda.msda_prologue_apply(o, lg, r, shapes)
+        else:
+            loc, aw = reference_prologue(o, lg, r, shapes)
+        (loc * gl).sum().backward(retain_graph=True)
+        (aw * ga).sum().backward()
+        outs.append((loc.detach(), aw.detach(), o.grad, lg.grad, r.grad))
+    return outs
+
+
+@pytest.mark.parametrize("ref_dim", [1, 2])
+@pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-12), (torch.float32, 1e-6)])
+@pytest.mark.parametrize("B,Lq,M,L,P,shapes", [(2, 37, 8, 4, 4, [1024, 512, 256, 128]),
+                                              (1, 5, 2, 3, 2, [17, 9, 5]), (3, 11, 16, 1, 4, [64])])
+def test_matches_reference_composition(dev, ref_dim, dtype, tol, B, Lq, M, L, P, shapes):
+    off, logits, ref, gl, ga = make(B, Lq, M, L, P, ref_dim, dtype, dev)
+    (loc, aw, go, glg, gr), (loc_r, aw_r, go_r, glg_r, gr_r) = run_both(off, logits, ref, gl, ga, shapes)
+    assert loc.dtype == loc_r.dtype and aw.dtype == aw_r.dtype
+    if dtype == torch.float32:
+        assert torch.equal(loc, loc_r)
+    torch.testing.assert_close(loc, loc_r, rtol=tol, atol=tol)
+    torch.testing.assert_close(aw, aw_r, rtol=tol, atol=tol)
+    torch.testing.assert_close(go, go_r, rtol=tol, atol=tol)
+    torch.testing.assert_close(glg, glg_r, rtol=tol, atol=tol)
+    torch.testing.assert_close(gr, gr_r, rtol=tol * 10, atol=tol * 10)
+
+
+@pytest.mark.parametrize("ref_dim", [1, 2])
+def test_bf16_autocast_promotion(dev, ref_dim):
+    """Under autocast the projections emit bf16: off / T_l is a bf16 tensor, the softmax runs in
+    fp32 and the sum with the fp32 reference is fp32 (the module's composite path)."""
+    B, Lq, M, L, P, shapes = 2, 64, 8, 4, 4, [1024, 512, 256, 128]
+    off, logits, ref, gl, ga = make(B, Lq, M, L, P, ref_dim, torch.bfloat16, dev, seed=1)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        (loc, aw, go, glg, gr), (loc_r, aw_r, go_r, glg_r, gr_r) = run_both(off, logits, ref, gl, ga, shapes)
+    assert loc.dtype == torch.float32 and aw.dtype == torch.float32
+    assert go.dtype == torch.bfloat16 and glg.dtype == torch.bfloat16
+    assert torch.equal(loc, loc_r)
+    torch.testing.assert_close(aw, aw_r, rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(go.float(), go_r.float(), rtol=8e-3, atol=1e-6)
+    torch.testing.assert_close(glg.float(), glg_r.float(), rtol=8e-3, atol=1e-6)
+    torch.testing.assert_close(gr, gr_r, rtol=1e-5, atol=1e-5)
+
+
+def test_module_uses_fused_prologue_and_matches_composite(dev):
+    """MSDeformAttn on the GPU takes the fused path; the CPU composite (reference math) gives
+    the same output and gradients in fp64."""
+    torch.manual_seed(0)
+    attn = PKG.models.modules.attention.MSDeformAttn(64, 4, 8, 4).double()
+    shapes = [32, 16, 8, 4]
+    S = sum(shapes)
+    q = torch.randn(2, 20, 64, dtype=torch.float64)
+    ref = torch.rand(2, 20, 4, 1, dtype=torch.float64)
+    x = torch.randn(2, S, 64, dtype=torch.float64)
+    st = torch.tensor(shapes)
+    lsi = torch.tensor([0, 32, 48, 56])
+    from oracle.cpu_model import oracle_core
+    outs = []
+    for device in ("cpu", dev):
+        a = attn.to(device)
+        qq, rr, xx = (t.detach().to(device).requires_grad_(True) for t in (q, ref, x))
+        if device == "cpu":
+            with oracle_core(PKG):
+                y = a(qq, rr, xx, st, lsi)
+        else:
+            y = a(qq, rr, xx, st.to(device), lsi.to(device))
+        y.square().sum().backward()
+        outs.append([t.detach().cpu() for t in (y, qq.grad, rr.grad, xx.grad)])
+        a.zero_grad()
+    for u, v in zip(*outs):
+        torch.testing.assert_close(u, v, rtol=1e-10, atol=1e-10)
