@@ -109,8 +109,7 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
  *   reference_points               (batch, num_query, num_levels, ref_dim)          coord dtype
  *   sampling_loc, attn_weight      (batch, num_query, num_heads, num_levels, num_point)  coord dtype
  * 16-bit dtypes reproduce PyTorch's promotion under autocast (offsets / T_l rounded to the
- * 16-bit dtype once; the softmax in fp32).  num_heads must be a power of two <= 64 and
- * num_levels*num_point <= 64. */
+ * 16-bit dtype once; the softmax in fp32).  num_heads*num_levels*num_point must be <= 1024. */
 int msda_hip_prologue_forward(const void* sampling_offsets, const void* attn_logits, int dtype,
                               const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
                               int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,

@@ -1805,8 +1805,6 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
 // PyTorch's type promotion exactly: off / T_l and off / P are 16-bit tensors (computed in
 // fp32, rounded once), everything after the promotion to the fp32 reference is fp32; the
 // backward rounds where autograd casts back to the 16-bit inputs.
-// One thread per (b, q, m) item; M a power of two <= 64 so that the M items of one query are
-// aligned lanes of one wave (grad_ref is a DPP sum over them).
 // ---------------------------------------------------------------------------------
 template <typename scalar_t> struct Is16 { static constexpr bool value = false; };
 template <> struct Is16<bf16_t> { static constexpr bool value = true; };
@@ -1824,124 +1822,284 @@ __device__ __forceinline__ coord_t round_to(coord_t v) {
   }
 }
 
-template <typename coord_t>
-__device__ __forceinline__ coord_t lanes_sum(coord_t x, int M) {
-  switch (M) {
-    case 1: return x;
-    case 2: return group_sum<2>(x);
-    case 4: return group_sum<4>(x);
-    case 8: return group_sum<8>(x);
-    case 16: return group_sum<16>(x);
-    case 32: return group_sum<32>(x);
-    default: return group_sum<64>(x);
+// One thread per sample (b, q, m, l, p): loads and stores are contiguous across the block.  A
+// block holds G whole queries (G*M*L*P threads, M*L*P <= 1024); the 16-way softmax sums and the
+// grad_ref sums over (m, p) go through LDS.
+// Sum / max over the item's LP samples.  LP a power of two <= 64: the samples of one item are
+// aligned lanes of one wave (QS = M*LP and blocks start at wave boundaries), so a butterfly of
+// __shfl_xor does it without LDS or barriers; otherwise through LDS.
+template <typename coord_t, bool MAXOP>
+__device__ __forceinline__ coord_t item_reduce(coord_t v, int LP, bool pow2, coord_t* sx, int t, int t0) {
+  if (pow2) {
+    for (int o = 1; o < LP; o <<= 1) {
+      const coord_t w = __shfl_xor(v, o);
+      v = MAXOP ? (w > v ? w : v) : v + w;
+    }
+    return v;
   }
+  __syncthreads();
+  sx[t] = v;
+  __syncthreads();
+  coord_t r = MAXOP ? (coord_t)-INFINITY : (coord_t)0;
+  for (int k = 0; k < LP; ++k) r = MAXOP ? (sx[t0 + k] > r ? sx[t0 + k] : r) : r + sx[t0 + k];
+  return r;
 }
 
-template <typename scalar_t, typename coord_t, int LPMAX>
-__global__ __launch_bounds__(256) void msda_prologue_fwd_kernel(
+// Thread -> (query in block, sample j, level l): shifts when P, L*P and M*L*P are powers of
+// two (the reference's 4 x 4 x 8), integer division otherwise (runtime divisions cost ~40
+// VALU each and made the kernel ALU-bound).
+struct PrologueIdx {
+  int g, r, j, l;
+};
+template <bool POW2>
+__device__ __forceinline__ PrologueIdx prologue_idx(int t, int QS, int LP, int P, int sQS, int sLP, int sP) {
+  PrologueIdx x;
+  if constexpr (POW2) {
+    x.g = t >> sQS;
+    x.r = t & (QS - 1);
+    x.j = x.r & (LP - 1);
+    x.l = x.j >> sP;
+  } else {
+    x.g = t / QS;
+    x.r = t - x.g * QS;
+    x.j = x.r % LP;
+    x.l = x.j / P;
+  }
+  (void)sLP;
+  return x;
+}
+
+// T_l for a per-lane level index without a dynamically indexed kernel-argument load (which
+// costs one extra dependent memory round trip): a select chain over the uniform table.
+__device__ __forceinline__ int level_T(const Levels& lv, int l, int L) {
+  int T = lv.T[0];
+#pragma unroll
+  for (int k = 1; k < MSDA_MAX_LEVELS; ++k)
+    if (k < L && l == k) T = lv.T[k];
+  return T;
+}
+
+template <typename scalar_t, typename coord_t, bool POW2>
+__global__ __launch_bounds__(1024) void msda_prologue_fwd_kernel(
     const scalar_t* __restrict__ off, const scalar_t* __restrict__ logits,
     const coord_t* __restrict__ ref, const int ref_dim, coord_t* __restrict__ loc,
     coord_t* __restrict__ aw, const Levels lv, const int L, const int P, const int M,
-    const long long n_items) {
-  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (item >= n_items) return;
-  const int LP = L * P;
-  const long long bq = item / M;
-  const scalar_t* __restrict__ o = off + item * LP;
-  const scalar_t* __restrict__ a = logits + item * LP;
-  coord_t x[LPMAX];
-  coord_t mx = -INFINITY;
-#pragma unroll
-  for (int j = 0; j < LPMAX; ++j) {
-    if (j < LP) {
-      x[j] = (coord_t)to_acc(a[j]);
-      mx = x[j] > mx ? x[j] : mx;
-    }
-  }
-  coord_t sum = 0;
-#pragma unroll
-  for (int j = 0; j < LPMAX; ++j) {
-    if (j < LP) {
-      x[j] = exp(x[j] - mx);
-      sum += x[j];
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < LPMAX; ++j)
-    if (j < LP) aw[item * LP + j] = x[j] / sum;
-  for (int l = 0; l < L; ++l) {
-    const coord_t T = (coord_t)lv.T[l];
-    const coord_t r0 = ref[(bq * L + l) * ref_dim];
-    const coord_t r1 = ref_dim == 2 ? ref[(bq * L + l) * 2 + 1] : (coord_t)0;
-    for (int p = 0; p < P; ++p) {
-      const int j = l * P + p;
-      const coord_t v = (coord_t)to_acc(o[j]);
-      coord_t lc;
-      if (ref_dim == 1) {
-        lc = r0 + round_to<scalar_t>(v / T);
-      } else {
-        lc = r0 + (round_to<scalar_t>(v / (coord_t)P) * r1) * (coord_t)0.5;
-      }
-      loc[item * LP + j] = lc;
-    }
-  }
+    const long long n_queries, const int G, const int sQS, const int sLP, const int sP) {
+#pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  coord_t* sx = reinterpret_cast<coord_t*>(smem_raw);
+  const int LP = L * P, QS = M * LP;
+  const bool pow2 = POW2 || (LP & (LP - 1)) == 0;
+  const int t = threadIdx.x;
+  const PrologueIdx ix = prologue_idx<POW2>(t, QS, LP, P, sQS, sLP, sP);
+  const long long bq_raw = (long long)blockIdx.x * G + ix.g;
+  const bool active = bq_raw < n_queries;
+  const long long bq = active ? bq_raw : 0;  // clamped: every load below is unconditional
+  const int r = ix.r, j = ix.j, l = ix.l;
+  const long long e = bq * QS + r;
+  // all global loads of the thread issued together: one round trip
+  const coord_t x = (coord_t)to_acc(logits[e]);
+  const coord_t v = (coord_t)to_acc(off[e]);
+  const coord_t r0 = ref[(bq * L + l) * ref_dim];
+  const coord_t r1 = ref[(bq * L + l) * ref_dim + (ref_dim - 1)];
+  const coord_t T = (coord_t)level_T(lv, l, L);
+  const int t0 = t - j;
+  const coord_t mx = item_reduce<coord_t, true>(x, LP, pow2, sx, t, t0);
+  const coord_t ex = exp(x - mx);  // one exp per sample
+  const coord_t sum = item_reduce<coord_t, false>(ex, LP, pow2, sx, t, t0);
+  if (!active) return;
+  aw[e] = ex / sum;
+  if (ref_dim == 1)
+    loc[e] = r0 + round_to<scalar_t>(v / T);
+  else
+    loc[e] = r0 + (round_to<scalar_t>(v / (coord_t)P) * r1) * (coord_t)0.5;
 }
 
-template <typename scalar_t, typename coord_t, int LPMAX>
-__global__ __launch_bounds__(256) void msda_prologue_bwd_kernel(
+template <typename scalar_t, typename coord_t, bool POW2>
+__global__ __launch_bounds__(1024) void msda_prologue_bwd_kernel(
     const coord_t* __restrict__ grad_loc, const coord_t* __restrict__ grad_aw,
     const coord_t* __restrict__ aw, const scalar_t* __restrict__ off, const coord_t* __restrict__ ref,
     const int ref_dim, scalar_t* __restrict__ grad_off, scalar_t* __restrict__ grad_logits,
     coord_t* __restrict__ grad_ref, const Levels lv, const int L, const int P, const int M,
+    const long long n_queries, const int G, const int sQS, const int sLP, const int sP) {
+#pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  coord_t* s0 = reinterpret_cast<coord_t*>(smem_raw);  // g*y, then grad_loc
+  coord_t* s1 = s0 + blockDim.x;                        // box form: grad of ref[..., 1]
+  const int LP = L * P, QS = M * LP;
+  const int t = threadIdx.x;
+  const PrologueIdx ix = prologue_idx<POW2>(t, QS, LP, P, sQS, sLP, sP);
+  const long long bq_raw = (long long)blockIdx.x * G + ix.g;
+  const bool active = bq_raw < n_queries;
+  const long long bq = active ? bq_raw : 0;  // clamped: loads below are unconditional
+  const int r = ix.r, j = ix.j, l = ix.l;
+  const long long e = bq * QS + r;
+  const bool pow2 = (LP & (LP - 1)) == 0;
+  const bool loc_side = grad_off != nullptr || grad_ref != nullptr;
+  const bool box = ref_dim == 2;
+  const coord_t T = (coord_t)level_T(lv, l, L);
+  const coord_t gl = loc_side ? (active ? grad_loc[e] : (coord_t)0) : (coord_t)0;
+  const coord_t r1 = box ? ref[(bq * L + l) * 2 + 1] : (coord_t)0;
+  const coord_t ov = box ? (coord_t)to_acc(off[e]) : (coord_t)0;
+  if (grad_logits != nullptr) {  // uniform
+    const coord_t g = active ? grad_aw[e] : (coord_t)0;
+    const coord_t y = active ? aw[e] : (coord_t)0;
+    const coord_t dot = item_reduce<coord_t, false>(g * y, LP, pow2, s0, t, t - j);
+    if (active) from_acc((typename AccOf<scalar_t>::type)(y * (g - dot)), &grad_logits[e]);
+  }
+  if (!loc_side) return;
+  coord_t gu = 0;  // box form: d loc / d ref1 contribution
+  if (!box) {
+    if (grad_off != nullptr && active)
+      from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gl) / T), &grad_off[e]);
+  } else if (active) {
+    const coord_t gh = gl * (coord_t)0.5;
+    if (grad_off != nullptr)
+      from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gh * r1) / (coord_t)P), &grad_off[e]);
+    gu = gh * round_to<scalar_t>(ov / (coord_t)P);
+  }
+  if (grad_ref == nullptr) return;  // uniform
+  __syncthreads();
+  s0[t] = gl;
+  s1[t] = gu;
+  __syncthreads();
+  // grad_ref[bq, l, c]: sum over (m, p) of the block's G queries
+  for (int o = t; o < G * L * ref_dim; o += blockDim.x) {
+    const int c = o % ref_dim, ql = o / ref_dim;
+    const int lq = ql % L, g = ql / L;
+    const long long bqo = (long long)blockIdx.x * G + g;
+    if (bqo >= n_queries) continue;
+    const coord_t* src = c == 0 ? s0 : s1;
+    coord_t acc = 0;
+    for (int m = 0; m < M; ++m)
+      for (int p = 0; p < P; ++p) acc += src[g * QS + m * LP + lq * P + p];
+    grad_ref[(bqo * L + lq) * ref_dim + c] = acc;
+  }
+}
+
+// Fast path for the reference's shape (L*P == 16, M a power of two <= 64, fp32 coordinates):
+// one thread per (b, q, m) item, all of its 16 samples in registers, 16-byte loads and stores
+// (the per-sample kernels above spend most of their time on per-lane address arithmetic).
+template <typename scalar_t>
+__device__ __forceinline__ void load16s(const scalar_t* __restrict__ p, float (&r)[16]) {
+  constexpr int V = 16 / (int)sizeof(scalar_t);
+#pragma unroll
+  for (int c = 0; c < 16 / V; ++c) {
+    float t[V];
+    load_vec<scalar_t, V>(p + c * V, t);
+#pragma unroll
+    for (int i = 0; i < V; ++i) r[c * V + i] = t[i];
+  }
+}
+template <typename scalar_t>
+__device__ __forceinline__ void store16s(scalar_t* __restrict__ p, const float (&r)[16]) {
+  constexpr int V = 16 / (int)sizeof(scalar_t);
+#pragma unroll
+  for (int c = 0; c < 16 / V; ++c) {
+    float t[V];
+#pragma unroll
+    for (int i = 0; i < V; ++i) t[i] = r[c * V + i];
+    store_vec<scalar_t, V>(p + c * V, t);
+  }
+}
+
+template <typename scalar_t, int M, int P>
+__global__ __launch_bounds__(256) void msda_prologue16_fwd_kernel(
+    const scalar_t* __restrict__ off, const scalar_t* __restrict__ logits, const float* __restrict__ ref,
+    const int ref_dim, float* __restrict__ loc, float* __restrict__ aw, const Levels lv,
     const long long n_items) {
+#pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
+  constexpr int L = 16 / P;
+  const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (item >= n_items) return;
+  const long long bq = item / M;
+  float x[16], v[16];
+  load16s<scalar_t>(logits + item * 16, x);
+  load16s<scalar_t>(off + item * 16, v);
+  float mx = x[0];
+#pragma unroll
+  for (int j = 1; j < 16; ++j) mx = x[j] > mx ? x[j] : mx;
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    x[j] = expf(x[j] - mx);
+    sum += x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] = x[j] / sum;
+  store16s<float>(aw + item * 16, x);
+  const float* __restrict__ rb = ref + bq * L * ref_dim;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int l = j / P;
+    const float r0 = rb[l * ref_dim];
+    if (ref_dim == 1) {
+      v[j] = r0 + round_to<scalar_t>(v[j] / (float)lv.T[l]);
+    } else {
+      v[j] = r0 + (round_to<scalar_t>(v[j] / (float)P) * rb[l * 2 + 1]) * 0.5f;
+    }
+  }
+  store16s<float>(loc + item * 16, v);
+}
+
+template <typename scalar_t, int M, int P>
+__global__ __launch_bounds__(256) void msda_prologue16_bwd_kernel(
+    const float* __restrict__ grad_loc, const float* __restrict__ grad_aw, const float* __restrict__ aw,
+    const scalar_t* __restrict__ off, const float* __restrict__ ref, const int ref_dim,
+    scalar_t* __restrict__ grad_off, scalar_t* __restrict__ grad_logits, float* __restrict__ grad_ref,
+    const Levels lv, const long long n_items) {
+#pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
+  constexpr int L = 16 / P;
   const long long item_raw = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = item_raw < n_items;  // all lanes stay for the grad_ref reduction
+  const bool active = item_raw < n_items;  // every lane stays for the grad_ref lane sums
   const long long item = active ? item_raw : 0;
-  const int LP = L * P;
   const long long bq = item / M;
   const int m = (int)(item % M);
-  if (grad_logits != nullptr && active) {
-    coord_t g[LPMAX], y[LPMAX];
-    coord_t dot = 0;
+  if (grad_logits != nullptr) {
+    float g[16], y[16];
+    load16s<float>(grad_aw + item * 16, g);
+    load16s<float>(aw + item * 16, y);
+    float dot = 0.f;
 #pragma unroll
-    for (int j = 0; j < LPMAX; ++j) {
-      if (j < LP) {
-        g[j] = grad_aw[item * LP + j];
-        y[j] = aw[item * LP + j];
-        dot += g[j] * y[j];
-      }
-    }
+    for (int j = 0; j < 16; ++j) dot += g[j] * y[j];
 #pragma unroll
-    for (int j = 0; j < LPMAX; ++j)
-      if (j < LP) from_acc((typename AccOf<scalar_t>::type)(y[j] * (g[j] - dot)), &grad_logits[item * LP + j]);
+    for (int j = 0; j < 16; ++j) g[j] = y[j] * (g[j] - dot);
+    if (active) store16s<scalar_t>(grad_logits + item * 16, g);
   }
   if (grad_off == nullptr && grad_ref == nullptr) return;
-  for (int l = 0; l < L; ++l) {
-    const coord_t T = (coord_t)lv.T[l];
-    const coord_t r1 = ref_dim == 2 ? ref[(bq * L + l) * 2 + 1] : (coord_t)0;
-    coord_t s0 = 0, s1 = 0;
-    for (int p = 0; p < P; ++p) {
-      const int j = l * P + p;
-      const coord_t gl = active ? grad_loc[item * LP + j] : (coord_t)0;
-      s0 += gl;
-      if (ref_dim == 1) {
-        if (grad_off != nullptr && active)
-          from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gl) / T), &grad_off[item * LP + j]);
-      } else {
-        const coord_t gh = gl * (coord_t)0.5;
-        if (grad_off != nullptr && active)
-          from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gh * r1) / (coord_t)P),
-                   &grad_off[item * LP + j]);
-        const coord_t u = active ? round_to<scalar_t>((coord_t)to_acc(off[item * LP + j]) / (coord_t)P) : (coord_t)0;
-        s1 += gh * u;
-      }
+  float gl[16], o[16];
+  load16s<float>(grad_loc + item * 16, gl);
+  const bool box = ref_dim == 2;
+  if (box) load16s<scalar_t>(off + item * 16, o);
+  const float* __restrict__ rb = ref + bq * L * ref_dim;
+  float go[16], s1[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int l = j / P;
+    if (!box) {
+      go[j] = round_to<scalar_t>(gl[j]) / (float)lv.T[l];
+      s1[j] = 0.f;
+    } else {
+      const float gh = gl[j] * 0.5f;
+      go[j] = round_to<scalar_t>(gh * rb[l * 2 + 1]) / (float)P;
+      s1[j] = gh * round_to<scalar_t>(o[j] / (float)P);
     }
-    if (grad_ref != nullptr) {
-      s0 = lanes_sum(s0, M);
-      if (ref_dim == 2) s1 = lanes_sum(s1, M);
+  }
+  if (grad_off != nullptr && active) store16s<scalar_t>(grad_off + item * 16, go);
+  if (grad_ref != nullptr) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+      for (int p = 0; p < P; ++p) {
+        a0 += active ? gl[l * P + p] : 0.f;
+        a1 += active ? s1[l * P + p] : 0.f;
+      }
+      a0 = group_sum<M>(a0);
+      if (box) a1 = group_sum<M>(a1);
       if (active && m == 0) {
-        grad_ref[(bq * L + l) * ref_dim] = s0;
-        if (ref_dim == 2) grad_ref[(bq * L + l) * 2 + 1] = s1;
+        grad_ref[(bq * L + l) * ref_dim] = a0;
+        if (box) grad_ref[(bq * L + l) * 2 + 1] = a1;
       }
     }
   }
@@ -1951,38 +2109,91 @@ template <typename scalar_t, typename coord_t>
 int run_prologue(bool fwd, const Problem& pr, int ref_dim, const void* off, const void* logits,
                  const void* ref, void* loc, void* aw, const void* grad_loc, const void* grad_aw,
                  void* grad_off, void* grad_logits, void* grad_ref, hipStream_t st) {
-  const long long n_items = pr.B * pr.Lq * pr.M;
-  if (n_items == 0) return MSDA_OK;
-  const unsigned blocks = (unsigned)((n_items + 255) / 256);
-  const int LP = (int)(pr.L * pr.P);
-  auto* o = static_cast<const scalar_t*>(off);
-  auto* r = static_cast<const coord_t*>(ref);
-#define MSDA_PRO(LPM)                                                                              \
+  const long long n_queries = pr.B * pr.Lq;
+  if (n_queries == 0) return MSDA_OK;
+  if constexpr (!std::is_same<coord_t, double>::value) {
+    const int Mi = (int)pr.M;
+    // item-per-thread kernels need enough items to fill the chip (encoder-sized calls: 10.6 / 7.2 us
+    // vs 11.6 / 13.7 us per-sample at B=8, Lq=1920); small calls (decoder queries) take the
+    // per-sample kernels (3.2 / 4.8 us vs 5.5 / 5.0 us at Lq=100)
+    if (pr.L * pr.P == 16 && 16 % pr.P == 0 && Mi <= 64 && (Mi & (Mi - 1)) == 0 &&
+        n_queries * pr.M >= 65536) {
+      const long long n_items = n_queries * pr.M;
+      const unsigned blocks = (unsigned)((n_items + 255) / 256);
+      auto* o = static_cast<const scalar_t*>(off);
+      auto* rf = static_cast<const float*>(ref);
+#define MSDA_P16_(MM, PP)                                                                          \
   do {                                                                                           \
     if (fwd)                                                                                     \
-      hipLaunchKernelGGL((msda_prologue_fwd_kernel<scalar_t, coord_t, LPM>), dim3(blocks), dim3(256), 0, \
-                         st, o, static_cast<const scalar_t*>(logits), r, ref_dim,               \
-                         static_cast<coord_t*>(loc), static_cast<coord_t*>(aw), pr.lv, (int)pr.L, \
-                         (int)pr.P, (int)pr.M, n_items);                                         \
+      hipLaunchKernelGGL((msda_prologue16_fwd_kernel<scalar_t, MM, PP>), dim3(blocks), dim3(256), 0, st, o, \
+                         static_cast<const scalar_t*>(logits), rf, ref_dim, static_cast<float*>(loc), \
+                         static_cast<float*>(aw), pr.lv, n_items);                               \
     else                                                                                         \
-      hipLaunchKernelGGL((msda_prologue_bwd_kernel<scalar_t, coord_t, LPM>), dim3(blocks), dim3(256), 0, \
-                         st, static_cast<const coord_t*>(grad_loc), static_cast<const coord_t*>(grad_aw), \
-                         static_cast<const coord_t*>(aw), o, r, ref_dim,                          \
-                         static_cast<scalar_t*>(grad_off), static_cast<scalar_t*>(grad_logits),  \
-                         static_cast<coord_t*>(grad_ref), pr.lv, (int)pr.L, (int)pr.P, (int)pr.M, n_items); \
+      hipLaunchKernelGGL((msda_prologue16_bwd_kernel<scalar_t, MM, PP>), dim3(blocks), dim3(256), 0, st, \
+                         static_cast<const float*>(grad_loc), static_cast<const float*>(grad_aw), \
+                         static_cast<const float*>(aw), o, rf, ref_dim, static_cast<scalar_t*>(grad_off), \
+                         static_cast<scalar_t*>(grad_logits), static_cast<float*>(grad_ref), pr.lv, n_items); \
   } while (0)
-  if (LP <= 16) MSDA_PRO(16);
-  else MSDA_PRO(64);
+#define MSDA_P16(MM)                                                                               \
+  do {                                                                                           \
+    switch (pr.P) {                                                                              \
+      case 1: MSDA_P16_(MM, 1); break;                                                           \
+      case 2: MSDA_P16_(MM, 2); break;                                                           \
+      case 4: MSDA_P16_(MM, 4); break;                                                           \
+      case 8: MSDA_P16_(MM, 8); break;                                                           \
+      default: MSDA_P16_(MM, 16); break;                                                         \
+    }                                                                                            \
+  } while (0)
+      switch (Mi) {
+        case 1: MSDA_P16(1); break;
+        case 2: MSDA_P16(2); break;
+        case 4: MSDA_P16(4); break;
+        case 8: MSDA_P16(8); break;
+        case 16: MSDA_P16(16); break;
+        case 32: MSDA_P16(32); break;
+        default: MSDA_P16(64); break;
+      }
+#undef MSDA_P16
+#undef MSDA_P16_
+      return launch_status(fwd ? "prologue forward" : "prologue backward");
+    }
+  }
+  const int QS = (int)(pr.M * pr.L * pr.P);
+  const int G = max(1, 256 / QS);
+  const int threads = G * QS;
+  const unsigned blocks = (unsigned)((n_queries + G - 1) / G);
+  const size_t lds = (size_t)threads * sizeof(coord_t) * (fwd ? 1 : 2);
+  auto* o = static_cast<const scalar_t*>(off);
+  auto* r = static_cast<const coord_t*>(ref);
+  auto lg2 = [](long long v) { int k = 0; while ((1LL << k) < v) ++k; return (1LL << k) == v ? k : -1; };
+  const int sQS = lg2(QS), sLP = lg2(pr.L * pr.P), sP = lg2(pr.P);
+  const bool pow2 = sQS >= 0 && sLP >= 0 && sP >= 0;
+#define MSDA_PRO(PW)                                                                                  \
+  do {                                                                                              \
+    if (fwd)                                                                                        \
+      hipLaunchKernelGGL((msda_prologue_fwd_kernel<scalar_t, coord_t, PW>), dim3(blocks), dim3(threads), lds, \
+                         st, o, static_cast<const scalar_t*>(logits), r, ref_dim, static_cast<coord_t*>(loc), \
+                         static_cast<coord_t*>(aw), pr.lv, (int)pr.L, (int)pr.P, (int)pr.M, n_queries, G, \
+                         sQS, sLP, sP);                                                              \
+    else                                                                                            \
+      hipLaunchKernelGGL((msda_prologue_bwd_kernel<scalar_t, coord_t, PW>), dim3(blocks), dim3(threads), lds, \
+                         st, static_cast<const coord_t*>(grad_loc), static_cast<const coord_t*>(grad_aw), \
+                         static_cast<const coord_t*>(aw), o, r, ref_dim, static_cast<scalar_t*>(grad_off), \
+                         static_cast<scalar_t*>(grad_logits), static_cast<coord_t*>(grad_ref), pr.lv,   \
+                         (int)pr.L, (int)pr.P, (int)pr.M, n_queries, G, sQS, sLP, sP);              \
+  } while (0)
+  if (pow2) MSDA_PRO(true);
+  else MSDA_PRO(false);
 #undef MSDA_PRO
   return launch_status(fwd ? "prologue forward" : "prologue backward");
 }
 
 int check_prologue(const int64_t* shapes, int64_t L, int64_t B, int64_t Lq, int64_t M, int64_t P,
                    int ref_dim, Problem* pr) {
-  if (L < 1 || L > MSDA_MAX_LEVELS || B < 0 || Lq < 0 || M < 1 || M > 64 || (M & (M - 1)) != 0 ||
-      P < 1 || L * P > 64 || (ref_dim != 1 && ref_dim != 2) || shapes == nullptr) {
-    set_error("msda prologue: bad arguments (L=%lld M=%lld P=%lld ref_dim=%d; M must be a power of two "
-              "<= 64, L*P <= 64)", (long long)L, (long long)M, (long long)P, ref_dim);
+  if (L < 1 || L > MSDA_MAX_LEVELS || B < 0 || Lq < 0 || M < 1 || P < 1 || M * L * P > 1024 ||
+      (ref_dim != 1 && ref_dim != 2) || shapes == nullptr) {
+    set_error("msda prologue: bad arguments (L=%lld M=%lld P=%lld ref_dim=%d; M*L*P must be <= 1024)",
+              (long long)L, (long long)M, (long long)P, ref_dim);
     return MSDA_ERR_ARG;
   }
   for (int64_t l = 0; l < L; ++l) {

@@ -15,11 +15,17 @@ from . import _native
 
 __all__ = [
     "host_levels", "msda_forward", "msda_backward", "MSDAFunction", "msda_apply", "KernelTimer",
-    "algorithmic_bytes", "prologue_supported", "prologue_forward", "prologue_backward", "MSDAPrologueFunction",
+    "algorithmic_bytes", "gathered_bytes", "prologue_supported", "prologue_forward", "prologue_backward", "MSDAPrologueFunction",
     "msda_prologue_apply",
 ]
 
 _timer = None  # KernelTimer while bench.py measures; None otherwise
+
+
+def gathered_bytes(B, M, D, Lq, L, P, value_bytes):
+    """Row-fragment bytes one forward or fused-backward launch gathers: two taps of D values per
+    sample (value rows in the forward, grad_out rows in the backward's pull)."""
+    return B * Lq * M * L * P * 2 * D * value_bytes
 
 
 def algorithmic_bytes(kind, B, S, M, D, Lq, L, P, value_bytes):
@@ -56,16 +62,17 @@ class KernelTimer:
         ev.record()
         return ev
 
-    def _end(self, kind, key, nbytes, ev0):
+    def _end(self, kind, key, nbytes, ev0, gathered=0):
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
-        self.records.append((kind, key, nbytes, ev0, ev1))
+        self.records.append((kind, key, nbytes, gathered, ev0, ev1))
 
     def summary(self):
-        """{(kind, key): {"launches", "total_ms", "avg_ms", "bytes_per_launch"}}"""
+        """{(kind, key): {"launches", "total_ms", "avg_ms", "bytes_per_launch", "gather_bytes_per_launch"}}"""
         out = {}
-        for kind, key, nbytes, e0, e1 in self.records:
-            d = out.setdefault((kind, key), {"launches": 0, "total_ms": 0.0, "bytes_per_launch": nbytes})
+        for kind, key, nbytes, gathered, e0, e1 in self.records:
+            d = out.setdefault((kind, key), {"launches": 0, "total_ms": 0.0, "bytes_per_launch": nbytes,
+                                             "gather_bytes_per_launch": gathered})
             d["launches"] += 1
             d["total_ms"] += e0.elapsed_time(e1)
         for d in out.values():
@@ -170,7 +177,8 @@ def msda_forward(value, shapes, starts, loc, aw, padding_mode="border"):
         B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
     _native.check(rc, "msda_hip_forward")
     if timer is not None:
-        timer._end("fwd", (S, Lq), algorithmic_bytes("fwd", B, S, M, D, Lq, L, P, value.element_size()), ev0)
+        timer._end("fwd", (S, Lq), algorithmic_bytes("fwd", B, S, M, D, Lq, L, P, value.element_size()), ev0,
+                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()))
     return out
 
 
@@ -203,7 +211,8 @@ def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="bor
         B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
     _native.check(rc, "msda_hip_backward")
     if timer is not None:
-        timer._end("bwd", (S, Lq), algorithmic_bytes("bwd", B, S, M, D, Lq, L, P, value.element_size()), ev0)
+        timer._end("bwd", (S, Lq), algorithmic_bytes("bwd", B, S, M, D, Lq, L, P, value.element_size()), ev0,
+                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()))
     return gv, gl, ga
 
 
@@ -245,7 +254,7 @@ def msda_apply(value, shapes, starts, loc, aw, padding_mode="border"):
 
 def prologue_supported(n_heads, n_levels, n_points):
     """The fused prologue kernel's shape limits (include/msda_hip.h)."""
-    return 1 <= n_heads <= 64 and (n_heads & (n_heads - 1)) == 0 and n_levels * n_points <= 64
+    return n_heads * n_levels * n_points <= 1024
 
 
 def prologue_forward(offsets, logits, ref, shapes):

@@ -57,8 +57,12 @@ def run_both(off, logits, ref, gl, ga, shapes):
 
 @pytest.mark.parametrize("ref_dim", [1, 2])
 @pytest.mark.parametrize("dtype,tol", [(torch.float64, 1e-12), (torch.float32, 1e-6)])
-@pytest.mark.parametrize("B,Lq,M,L,P,shapes", [(2, 37, 8, 4, 4, [1024, 512, 256, 128]),
-                                              (1, 5, 2, 3, 2, [17, 9, 5]), (3, 11, 16, 1, 4, [64])])
+@pytest.mark.parametrize("B,Lq,M,L,P,shapes", [(2, 37, 8, 4, 4, [1024, 512, 256, 128]),  # per-sample kernels
+                                              (1, 9, 4, 2, 8, [300, 150]),
+                                              (1, 5, 2, 3, 2, [17, 9, 5]),                 # generic kernels
+                                              (3, 11, 16, 1, 4, [64]), (2, 7, 3, 4, 4, [40, 20, 10, 5]),
+                                              (8, 1030, 8, 4, 4, [1024, 512, 256, 128]),   # item-per-thread path
+                                              (4, 2050, 8, 2, 8, [300, 150])])
 def test_matches_reference_composition(dev, ref_dim, dtype, tol, B, Lq, M, L, P, shapes):
     off, logits, ref, gl, ga = make(B, Lq, M, L, P, ref_dim, dtype, dev)
     (loc, aw, go, glg, gr), (loc_r, aw_r, go_r, glg_r, gr_r) = run_both(off, logits, ref, gl, ga, shapes)
@@ -73,10 +77,13 @@ def test_matches_reference_composition(dev, ref_dim, dtype, tol, B, Lq, M, L, P,
 
 
 @pytest.mark.parametrize("ref_dim", [1, 2])
-def test_bf16_autocast_promotion(dev, ref_dim):
+@pytest.mark.parametrize("L,P", [(4, 4), (3, 2)])
+@pytest.mark.parametrize("Lq", [64, 1200])  # per-sample / item-per-thread kernels
+def test_bf16_autocast_promotion(dev, ref_dim, L, P, Lq):
     """Under autocast the projections emit bf16: off / T_l is a bf16 tensor, the softmax runs in
     fp32 and the sum with the fp32 reference is fp32 (the module's composite path)."""
-    B, Lq, M, L, P, shapes = 2, 64, 8, 4, 4, [1024, 512, 256, 128]
+    B, M = 8, 8
+    shapes = [1024, 512, 256, 128][:L]
     off, logits, ref, gl, ga = make(B, Lq, M, L, P, ref_dim, torch.bfloat16, dev, seed=1)
     with torch.autocast("cuda", dtype=torch.bfloat16):
         (loc, aw, go, glg, gr), (loc_r, aw_r, go_r, glg_r, gr_r) = run_both(off, logits, ref, gl, ga, shapes)

@@ -68,7 +68,7 @@ def main():
     ap.add_argument("--regimes", default="init,trained,uniform")
     ap.add_argument("--B", type=int, default=8)
     ap.add_argument("--shapes", default="enc,dec")
-    ap.add_argument("--kernels", default="fwd,bwd_loc_aw,bwd_value,bwd_all")
+    ap.add_argument("--kernels", default="fwd,bwd_loc_aw,bwd_value,bwd_all,prologue_fwd,prologue_bwd")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     shapes = [1024, 512, 256, 128]
@@ -92,6 +92,14 @@ def main():
                                                              need_loc=False, need_aw=False), None),
                     "bwd_all": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout), bwd_b),
                 }
+                off = (torch.randn(args.B, Lq, M, L, P) * 2).to(dev, dtype)
+                logits = torch.randn(args.B, Lq, M, L * P).to(dev, dtype)
+                refp = torch.rand(args.B, Lq, L, 1, device=dev)
+                ploc, paw = msda.prologue_forward(off, logits, refp, shapes)
+                pro_b = args.B * Lq * M * L * P * (2 * vb + 2 * 4) + args.B * Lq * L * 4
+                runs["prologue_fwd"] = (lambda: msda.prologue_forward(off, logits, refp, shapes), pro_b)
+                runs["prologue_bwd"] = (lambda: msda.prologue_backward(loc, aw, paw, off, refp, shapes, True, True,
+                                                                       True), pro_b + args.B * Lq * M * L * P * 4)
                 for name, (fn, nbytes) in runs.items():
                     if name not in args.kernels.split(","):
                         continue

@@ -50,7 +50,7 @@ def main(root):
 # pyramid, bf16; tools/pmc_msda.sh runs the encoder shape only, so one grid per kernel)
 CALL_KERNELS = {
     "msda_fwd_S1920_Lq1920": ("msda_fwd16_kernel",),
-    "msda_bwd_S1920_Lq1920": ("msda_bwd_gvalue_kernel", "msda_bwd_coord16_kernel"),
+    "msda_bwd_S1920_Lq1920": ("msda_bwd_fused_kernel",),
 }
 
 
