@@ -126,6 +126,18 @@ int msda_hip_prologue_backward(const void* grad_loc, const void* grad_attn, cons
                                int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
                                void* grad_offsets, void* grad_logits, void* grad_ref, void* stream);
 
+/* Sparse-DETR decoder attention map.  Replaces attn_map_to_flat_grid
+ * (reference utils/dam.py:20-73): per (row, head), the attention weight of every sample is
+ * scattered onto the two tokens around loc * T_l of its level with the reference's margins
+ * (floor token: loc*T_l - floor - 1, next token: loc*T_l - floor), in-level tokens only.
+ *   sampling_loc, attn_weight  (rows, num_query, num_heads, num_levels, num_point)  fp32
+ *                              (rows = batch * decoder layers)
+ *   flat_grid                  (rows, num_heads, sum_l T_l) fp32 (overwritten)
+ * Float atomics in LDS: the summation order is not fixed (as the reference's scatter_add_). */
+int msda_hip_dam_flat_grid(const void* sampling_loc, const void* attn_weight, const int64_t* spatial_shapes,
+                           const int64_t* level_start, int64_t num_levels, int64_t rows, int64_t num_query,
+                           int64_t num_heads, int64_t num_point, void* flat_grid, void* stream);
+
 /* Text of the last error raised on the calling thread ("" if none). */
 const char* msda_hip_last_error(void);
 

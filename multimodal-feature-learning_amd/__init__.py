@@ -8,6 +8,7 @@ Layout:
   msda.py              host checks, layout normalisation, autograd.Function
   MultiScaleDeformableAttention.py   mirror of the reference's pybind extension API
   models/...           mirror of the reference modules on the path (same names / signatures)
+  utils/dam.py         Sparse-DETR decoder attention map (HIP scatter kernel)
   train_step.py        flat-gradient data-parallel step, HIP-graph captured (bench.py)
 
 The directory name is not a Python identifier; import it with
@@ -28,6 +29,8 @@ from .models.deformable import unimodal_deformable_transformer  # noqa: E402,F40
 from .models.deformable import multimodal_deformable_transformer  # noqa: E402,F401
 from .models.ops.functions import ms_deform_attn_func  # noqa: E402,F401
 from .models.ops.modules import ms_deform_attn  # noqa: E402,F401
+from . import utils  # noqa: E402,F401
+from .utils import dam  # noqa: E402,F401
 from . import dvc_core  # noqa: E402,F401
 from . import train_step  # noqa: E402,F401
 

@@ -20,7 +20,7 @@ LIB_PATH = os.environ.get("MSDA_HIP_LIB", LIB_PATH)
 DTYPE_TAGS = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2, torch.float16: 3}
 PAD_TAGS = {"border": 0, "zeros": 1}
 MAX_LEVELS = 16
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # every symbol include/msda_hip.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
@@ -29,6 +29,7 @@ EXPORTED_SYMBOLS = (
     "msda_hip_backward_workspace_bytes",
     "msda_hip_prologue_forward",
     "msda_hip_prologue_backward",
+    "msda_hip_dam_flat_grid",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -53,6 +54,8 @@ def _declare(lib):
     lib.msda_hip_prologue_backward.restype = i32
     lib.msda_hip_prologue_backward.argtypes = [vp, vp, vp, vp, i32, vp, i32, p64, i64, i64, i64, i64, i64,
                                                vp, vp, vp, vp]
+    lib.msda_hip_dam_flat_grid.restype = i32
+    lib.msda_hip_dam_flat_grid.argtypes = [vp, vp, p64, p64, i64, i64, i64, i64, i64, vp, vp]
     lib.msda_hip_last_error.restype = ctypes.c_char_p
     lib.msda_hip_last_error.argtypes = []
     lib.msda_hip_abi_version.restype = i32

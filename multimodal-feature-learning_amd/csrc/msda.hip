@@ -2231,13 +2231,110 @@ int dispatch_prologue(bool fwd, int dtype, const Problem& pr, int ref_dim, const
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Sparse-DETR decoder attention map (reference utils/dam.py:20-73,
+// attn_map_to_flat_grid): for every (batch*layer, head) row, scatter-add each sample's
+// attention weight onto the two tokens around x = loc * T_l of its level:
+//   token start_l + floor(x)     += aw * (x - floor(x) - 1)   (the reference's margin_end, <= 0)
+//   token start_l + floor(x) + 1 += aw * (x - floor(x))
+// each only if the token lies inside the level.  One workgroup per row accumulates the row in
+// LDS (S fp32 words) and writes it once; rows too long for LDS accumulate with global atomics
+// into the zeroed output.
+// ---------------------------------------------------------------------------------
+constexpr int kDamThreads = 256;
+constexpr long long kDamLdsMax = 128 * 1024;
+
+template <bool LDS>
+__global__ __launch_bounds__(kDamThreads) void msda_dam_kernel(
+    const float* __restrict__ loc, const float* __restrict__ aw, float* __restrict__ out, const Levels lv,
+    const int L, const int P, const int M, const int Lq, const int S) {
+#pragma clang fp contract(off)  // the reference's separate mul / sub kernels
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  float* acc = reinterpret_cast<float*>(smem_raw);
+  const long long row = blockIdx.x;  // (batch*layer) * M + m
+  const int m = (int)(row % M);
+  const long long bn = row / M;
+  float* __restrict__ orow = out + row * S;
+  if constexpr (LDS) {
+    for (int i = threadIdx.x; i < S; i += kDamThreads) acc[i] = 0.f;
+    __syncthreads();
+  }
+  const int LP = L * P;
+  const long long nsamp = (long long)Lq * LP;
+  for (long long s = threadIdx.x; s < nsamp; s += kDamThreads) {
+    const int q = (int)(s / LP), j = (int)(s - (long long)q * LP);
+    const int l = j / P;
+    const long long e = ((bn * Lq + q) * M + m) * LP + j;
+    const int T = level_T(lv, l, L);
+    int st = lv.start[0];
+#pragma unroll
+    for (int k = 1; k < MSDA_MAX_LEVELS; ++k)
+      if (k < L && l == k) st = lv.start[k];
+    const float x = loc[e] * (float)T;
+    const float a = aw[e];
+    const float f = floorf(x);
+    const long long i0 = (long long)f;
+    const float m_start = x - (float)i0;
+    const float m_end = x - (float)(i0 + 1);
+    if (i0 >= 0 && i0 < T) {
+      if constexpr (LDS) atomicAdd(&acc[st + (int)i0], a * m_end);
+      else atomicAdd(&orow[st + (int)i0], a * m_end);
+    }
+    if (i0 + 1 >= 0 && i0 + 1 < T) {
+      if constexpr (LDS) atomicAdd(&acc[st + (int)i0 + 1], a * m_start);
+      else atomicAdd(&orow[st + (int)i0 + 1], a * m_start);
+    }
+  }
+  if constexpr (LDS) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < S; i += kDamThreads) orow[i] = acc[i];
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
-int msda_hip_abi_version(void) { return 3; }
+int msda_hip_abi_version(void) { return 4; }
 
 const char* msda_hip_last_error(void) { return g_last_error; }
+
+int msda_hip_dam_flat_grid(const void* sampling_loc, const void* attn_weight, const int64_t* spatial_shapes,
+                           const int64_t* level_start, int64_t num_levels, int64_t rows, int64_t num_query,
+                           int64_t num_heads, int64_t num_point, void* flat_grid, void* stream) {
+  g_last_error[0] = 0;
+  Problem pr;
+  long long S = 0;
+  if (spatial_shapes != nullptr && num_levels >= 1 && num_levels <= MSDA_MAX_LEVELS)
+    for (int64_t l = 0; l < num_levels; ++l) S += spatial_shapes[l];
+  int rc = check_problem(spatial_shapes, level_start, num_levels, rows, S, num_heads, 1, num_query, num_point, &pr);
+  if (rc) return rc;
+  const long long nrows = rows * num_heads;
+  if (nrows == 0 || S == 0) return MSDA_OK;
+  if (flat_grid == nullptr || (num_query > 0 && (sampling_loc == nullptr || attn_weight == nullptr))) {
+    set_error("msda_hip_dam_flat_grid: null pointer");
+    return MSDA_ERR_ARG;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* lc = static_cast<const float*>(sampling_loc);
+  auto* a = static_cast<const float*>(attn_weight);
+  auto* out = static_cast<float*>(flat_grid);
+  const size_t lds = (size_t)S * 4;
+  if ((long long)lds <= kDamLdsMax) {
+    if ((rc = allow_lds(msda_dam_kernel<true>, lds))) return rc;
+    hipLaunchKernelGGL((msda_dam_kernel<true>), dim3((unsigned)nrows), dim3(kDamThreads), lds, st, lc, a, out,
+                       pr.lv, (int)pr.L, (int)pr.P, (int)pr.M, (int)pr.Lq, (int)S);
+  } else {
+    if (hipMemsetAsync(out, 0, (size_t)nrows * S * 4, st) != hipSuccess) {
+      set_error("msda_hip_dam_flat_grid: memset failed");
+      return MSDA_ERR_LAUNCH;
+    }
+    hipLaunchKernelGGL((msda_dam_kernel<false>), dim3((unsigned)nrows), dim3(kDamThreads), 0, st, lc, a, out, pr.lv,
+                       (int)pr.L, (int)pr.P, (int)pr.M, (int)pr.Lq, (int)S);
+  }
+  return launch_status("dam flat grid");
+}
 
 int msda_hip_prologue_forward(const void* sampling_offsets, const void* attn_logits, int dtype,
                               const void* reference_points, int ref_dim, const int64_t* spatial_shapes,

@@ -23,6 +23,14 @@ Fixtures:
                              sampling_offsets weights jittered off their exact init.
   multimodal_f64.pt          MultimodalDeformableTransformer (1 enc + 1 dec, d=64), video
                              T=32 / audio T=16 pyramids, B=2, offsets jittered likewise.
+  dam_f32.pt                 utils/dam.py attn_map_to_flat_grid / idx_to_flat_grid / compute_corr
+                             (Sparse-DETR decoder attention map), B=2, 3 layers, M=4, [32,16,8,4],
+                             locations in U(-0.2, 1.2) plus integer / border points.
+  sparse_f64.pt              SparseDeformableTransformer (rho=0.3: mask predictor, top-k encoder
+                             queries scattered back; 2 enc + 2 dec, d=64) fwd + grads, with the
+                             decoder attention map of its own sampling locations.
+
+usage: make_golden.py [case ...]   (default: every case; e.g. ``make_golden.py dam sparse``)
 """
 import os
 import sys
@@ -57,8 +65,13 @@ def import_reference():
     import models.modules.embedding_layers as embedding_layers  # noqa: E402
     import models.deformable.unimodal_deformable_transformer as uni  # noqa: E402
     import models.deformable.multimodal_deformable_transformer as mm  # noqa: E402
+    import models.sparse.unimodal_sparse_deformable_transformer as sparse  # noqa: E402
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("_ref_dam", os.path.join(REF, "utils", "dam.py"))
+    dam = importlib.util.module_from_spec(spec)  # utils/dam.py alone: numpy + torch only
+    spec.loader.exec_module(dam)
     return types.SimpleNamespace(attention=attention, base_encoder=base_encoder,
-                                 embedding_layers=embedding_layers, uni=uni, mm=mm)
+                                 embedding_layers=embedding_layers, uni=uni, mm=mm, sparse=sparse, dam=dam)
 
 
 def _jitter_offsets(module, seed):
@@ -261,16 +274,82 @@ def multimodal_case(ref, seed=31):
                      "query_embedding": {k: p.grad.clone() for k, p in query_embedding.named_parameters()}})
 
 
+def dam_case(ref, seed=41):
+    gen = torch.Generator().manual_seed(seed)
+    shapes, B, NL, Lq, M, P = [32, 16, 8, 4], 2, 3, 20, 4, 4
+    L = len(shapes)
+    loc = _locations(gen, (B, NL, Lq, M, L, P), torch.float32)
+    for l, T in enumerate(shapes):  # integer and border positions (loc * T exact in fp32)
+        loc[0, 0, 0, :, l, :] = torch.tensor([0.0, 1.0 / T, (T - 1.0) / T, 1.0]).view(1, 4).expand(M, 4)
+    aw = torch.rand((B, NL, Lq, M, L, P), generator=gen, dtype=torch.float32)
+    shp = torch.tensor(shapes, dtype=torch.long)
+    start = torch.cat((shp.new_zeros(1), shp.cumsum(0)[:-1]))
+    grid = ref.dam.attn_map_to_flat_grid(shp, start, loc.unsqueeze(-1), aw)
+    summed = grid.sum(dim=(1, 2))
+    topk = torch.topk(summed, 10)[1]
+    flat_topk = ref.dam.idx_to_flat_grid(shp, topk)
+    corr = ref.dam.compute_corr(flat_topk, summed, shp)
+    return dict(shapes=shp, level_start=start, loc=loc, aw=aw, flat_grid=grid, topk=topk, flat_topk=flat_topk,
+                corr=torch.stack(corr))
+
+
+def sparse_case(ref, seed=53):
+    torch.manual_seed(seed)
+    d_model, heads, B, Q = 64, 4, 2, 12
+    tr = ref.sparse.SparseDeformableTransformer(d_model=d_model, num_head=heads, num_encoder_layers=2,
+                                                num_decoder_layers=2, dim_feedforward=128, dropout=0.0,
+                                                return_intermediate_dec=True, num_feature_levels=4,
+                                                dec_n_points=4, enc_n_points=4, rho=0.3).double()
+    query_embedding = torch.nn.Embedding(Q, d_model * 2).double()
+    _jitter_offsets(tr, seed)
+    gen = torch.Generator().manual_seed(seed)
+    lens = [32, 16, 8, 4]
+    srcs = [torch.randn((B, d_model, t), generator=gen, dtype=torch.float64).requires_grad_(True) for t in lens]
+    pos = [torch.randn((B, d_model, t), generator=gen, dtype=torch.float64) for t in lens]
+    masks = [torch.zeros(B, t, dtype=torch.bool) for t in lens]
+    for m, t in zip(masks, lens):
+        m[1, (3 * t) // 4:] = True
+    (src_flatten, shapes, starts, valid, lvl_pos, mask_flatten, proposals, topk, mask_pred,
+     sparse_token_nums) = tr.prepare_encoder_inputs(srcs, masks, pos)
+    memory, sl_enc, aw_enc, _, _ = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten,
+                                                      proposals, topk, sparse_token_nums)
+    qmask = torch.ones(B, Q, dtype=torch.bool)
+    init_ref, tgt, refp, qe = tr.prepare_decoder_input_query(B, query_embedding.weight)
+    hs, inter, sl_dec, aw_dec = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qe, mask_flatten, qmask,
+                                                   False)
+    dam = ref.dam.attn_map_to_flat_grid(shapes, starts, sl_dec.detach().float(), aw_dec.detach().float())
+    w = [torch.randn(t.shape, generator=gen, dtype=torch.float64) for t in (hs, memory, mask_pred)]
+    loss = (hs * w[0]).sum() + (memory * w[1]).sum() + (mask_pred * w[2]).sum()
+    loss.backward()
+    return dict(
+        srcs=[s.detach() for s in srcs], pos=pos, masks=masks, weights=w, hs=hs.detach(), memory=memory.detach(),
+        mask_prediction=mask_pred.detach(), topk=topk, sparse_token_nums=sparse_token_nums,
+        sampling_locations_enc=sl_enc.detach(), attn_weights_enc=aw_enc.detach(),
+        sampling_locations_dec=sl_dec.detach(), attn_weights_dec=aw_dec.detach(), dam_flat_grid=dam,
+        grad_srcs=[s.grad for s in srcs], loss=loss.detach(),
+        state_dicts={"transformer": _compact(tr.state_dict()), "query_embedding": _compact(query_embedding.state_dict())},
+        param_grads={"transformer": {k: p.grad.clone() for k, p in tr.named_parameters() if p.grad is not None},
+                     "query_embedding": {k: p.grad.clone() for k, p in query_embedding.named_parameters()}})
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = import_reference()
     small = dict(shapes=[32, 16, 8, 4], B=2, M=4, D=8, Lq=20, P=4)
-    torch.save(op_case(ref, torch.float64, seed=1, **small), os.path.join(HERE, "op_border_f64.pt"))
-    torch.save(op_case(ref, torch.float32, seed=2, **small), os.path.join(HERE, "op_border_f32.pt"))
-    torch.save(op_enc_case(ref), os.path.join(HERE, "op_border_f32_enc.pt"))
-    torch.save(module_case(ref), os.path.join(HERE, "module_f64.pt"))
-    torch.save(transformer_case(ref), os.path.join(HERE, "transformer_f64.pt"))
-    torch.save(multimodal_case(ref), os.path.join(HERE, "multimodal_f64.pt"))
+    cases = {
+        "op_border_f64": lambda: op_case(ref, torch.float64, seed=1, **small),
+        "op_border_f32": lambda: op_case(ref, torch.float32, seed=2, **small),
+        "op_border_f32_enc": lambda: op_enc_case(ref),
+        "module_f64": lambda: module_case(ref),
+        "transformer_f64": lambda: transformer_case(ref),
+        "multimodal_f64": lambda: multimodal_case(ref),
+        "dam_f32": lambda: dam_case(ref),
+        "sparse_f64": lambda: sparse_case(ref),
+    }
+    wanted = sys.argv[1:] or list(cases)
+    for name, fn in cases.items():
+        if any(name.startswith(w) for w in wanted):
+            torch.save(fn(), os.path.join(HERE, name + ".pt"))
     for f in sorted(os.listdir(HERE)):
         if f.endswith(".pt"):
             print(f, os.path.getsize(os.path.join(HERE, f)))
