@@ -27,6 +27,7 @@ from .models.modules import attention, embedding_layers, misc_modules  # noqa: E
 from .models import base_encoder  # noqa: E402,F401
 from .models.deformable import unimodal_deformable_transformer  # noqa: E402,F401
 from .models.deformable import multimodal_deformable_transformer  # noqa: E402,F401
+from .models.sparse import unimodal_sparse_deformable_transformer  # noqa: E402,F401
 from .models.ops.functions import ms_deform_attn_func  # noqa: E402,F401
 from .models.ops.modules import ms_deform_attn  # noqa: E402,F401
 from . import utils  # noqa: E402,F401

@@ -1,0 +1,85 @@
+"""Sparse-DETR transformer mirror (models/sparse/unimodal_sparse_deformable_transformer.py)
+against the reference's own run (tests/golden/sparse_f64.pt: rho = 0.3, mask predictor,
+top-k encoder queries over the full pyramid scattered back, 2 enc + 2 dec layers, fp64).
+
+CPU: the module logic with the MSDA core replaced by the oracle (oracle/cpu_model.oracle_core).
+GPU: the same on the HIP kernels (MSDA fwd/bwd with Lq = top-k, fused prologue), plus the
+decoder attention map of its own sampling locations through the DAM kernel.
+Tolerance: fp64; the reference's sine/cos position terms are not involved here, so 1e-9."""
+import pytest
+import torch
+
+from conftest import PKG
+
+SP = PKG.models.sparse.unimodal_sparse_deformable_transformer
+
+
+def _build(g, device):
+    torch.manual_seed(0)
+    tr = SP.SparseDeformableTransformer(d_model=64, num_head=4, num_encoder_layers=2, num_decoder_layers=2,
+                                        dim_feedforward=128, dropout=0.0, return_intermediate_dec=True,
+                                        num_feature_levels=4, dec_n_points=4, enc_n_points=4, rho=0.3).double()
+    tr.load_state_dict({k: v.double() for k, v in g["state_dicts"]["transformer"].items()})
+    qe = torch.nn.Embedding(12, 128).double()
+    qe.load_state_dict({k: v.double() for k, v in g["state_dicts"]["query_embedding"].items()})
+    return tr.to(device), qe.to(device)
+
+
+def _run(g, device):
+    tr, qe = _build(g, device)
+    srcs = [s.to(device).requires_grad_(True) for s in g["srcs"]]
+    pos = [p.to(device) for p in g["pos"]]
+    masks = [m.to(device) for m in g["masks"]]
+    (src_flatten, shapes, starts, valid, lvl_pos, mask_flatten, proposals, topk, mask_pred,
+     sparse_token_nums) = tr.prepare_encoder_inputs(srcs, masks, pos)
+    memory, sl_enc, aw_enc, _, _ = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten,
+                                                      proposals, topk, sparse_token_nums)
+    B = srcs[0].shape[0]
+    qmask = torch.ones(B, 12, dtype=torch.bool, device=device)
+    _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qe.weight)
+    hs, inter, sl_dec, aw_dec = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten,
+                                                   qmask, False)
+    w = [t.to(device) for t in g["weights"]]
+    ((hs * w[0]).sum() + (memory * w[1]).sum() + (mask_pred * w[2]).sum()).backward()
+    return dict(tr=tr, qe=qe, srcs=srcs, hs=hs, memory=memory, mask_pred=mask_pred, topk=topk,
+                sparse_token_nums=sparse_token_nums, sl_enc=sl_enc, aw_enc=aw_enc, sl_dec=sl_dec, aw_dec=aw_dec,
+                shapes=shapes, starts=starts)
+
+
+def _check(r, g, tol):
+    def close(a, b):
+        torch.testing.assert_close(a.detach().cpu().to(b.dtype), b, rtol=tol, atol=tol)
+    assert torch.equal(r["topk"].cpu(), g["topk"])
+    assert torch.equal(r["sparse_token_nums"].cpu(), g["sparse_token_nums"])
+    close(r["mask_pred"], g["mask_prediction"])
+    close(r["memory"], g["memory"])
+    close(r["hs"], g["hs"])
+    close(r["sl_enc"], g["sampling_locations_enc"])
+    close(r["aw_enc"], g["attn_weights_enc"])
+    close(r["sl_dec"], g["sampling_locations_dec"])
+    close(r["aw_dec"], g["attn_weights_dec"])
+    for s, ref in zip(r["srcs"], g["grad_srcs"]):
+        close(s.grad, ref)
+    for k, p in r["tr"].named_parameters():
+        if k in g["param_grads"]["transformer"]:
+            torch.testing.assert_close(p.grad.detach().cpu(), g["param_grads"]["transformer"][k], rtol=tol * 10,
+                                       atol=tol * 10, msg=k)
+
+
+def test_sparse_transformer_matches_reference_cpu(golden):
+    from oracle.cpu_model import oracle_core
+    g = golden("sparse_f64")
+    with oracle_core(PKG):
+        r = _run(g, "cpu")
+    _check(r, g, 1e-9)
+
+
+@pytest.mark.gpu
+def test_sparse_transformer_matches_reference_gpu(golden, dev):
+    g = golden("sparse_f64")
+    r = _run(g, dev)
+    _check(r, g, 1e-9)
+    # the criterion's decoder attention map of the model's own sampling locations (DAM kernel)
+    dam = PKG.utils.dam.attn_map_to_flat_grid(r["shapes"], r["starts"], r["sl_dec"].detach(), r["aw_dec"].detach())
+    ref = g["dam_flat_grid"]
+    torch.testing.assert_close(dam.cpu(), ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
