@@ -39,6 +39,19 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH
 GATHER_CEIL_TBPS = 18.8  # L2-resident indexed-row gather, chip-wide (same guide, "Indexed rows")
 
 
+WORKLOADS = {
+    "video": "configs[1]: models/deformable video-only, 4-level pyramid T=1024 d=512, 100 queries; "
+             "BaseEncoder + 6 enc + 6 dec + heads, AdamW step",
+    "multimodal": "configs[2]: multimodal video T=1024 + audio T=50 deformable fusion (4 MSDA calls per encoder "
+                  "layer, 2 per decoder layer), d=512, 100 queries, 6 + 6 layers + heads, AdamW step",
+    "sparse": "Sparse-DETR DVC (models/sparse, rho=0.3) T=1024 d=512, 100 queries, 6 + 6 layers, segment / count "
+              "heads + mask-prediction loss through the DAM kernel, AdamW step, eager",
+}
+MODELS = {"video": "DeformableDVCCore (UnimodalDeformableDVC proposal path)",
+          "multimodal": "MultimodalDVCCore (MultimodalDeformableDVC proposal path)",
+          "sparse": "SparseDVCCore (UnimodalSparseDVC proposal path)"}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -48,6 +61,11 @@ def parse():
     p.add_argument("--T", type=int, default=1024)
     p.add_argument("--queries", type=int, default=100)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--config", default="video", choices=["video", "multimodal", "sparse"],
+                   help="video: configs[1], the headline line.  multimodal: configs[2] (video + audio T_a=50, "
+                        "SURVEY 8(d)); sparse: the Sparse-DETR DVC (rho=0.3, eager: its top-k sizes are host "
+                        "values).  Only 'video' is the BASELINE metric's workload.")
+    p.add_argument("--audio-T", type=int, default=50, help="audio length (reference audio_rescale_len)")
     p.add_argument("--dropout", type=float, default=0.1)
     p.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU reference path (rank 0, N=1)")
     p.add_argument("--cpu-clips", type=int, default=3)
@@ -79,7 +97,22 @@ def usable_cores():
 
 def build_model(args, device):
     torch.manual_seed(0)
-    return PKG.dvc_core.DeformableDVCCore(d_model=512, num_queries=args.queries, dropout=args.dropout).to(device)
+    core = {"video": PKG.dvc_core.DeformableDVCCore, "multimodal": PKG.dvc_core.MultimodalDVCCore,
+            "sparse": PKG.dvc_core.SparseDVCCore}[args.config]
+    return core(d_model=512, num_queries=args.queries, dropout=args.dropout).to(device)
+
+
+def build_batch(args, rank, device):
+    video, mask, dur = PKG.dvc_core.synthetic_clips(args.batch, T=args.T, seed=1000 + rank, device=device)
+    if args.config == "multimodal":
+        audio, amask, _ = PKG.dvc_core.synthetic_clips(args.batch, T=args.audio_T, seed=2000 + rank, device=device)
+        return video, mask, audio, amask, dur
+    return video, mask, dur
+
+
+def loss_fn(args):
+    return {"video": PKG.dvc_core.workload_loss, "multimodal": PKG.dvc_core.multimodal_workload_loss,
+            "sparse": PKG.dvc_core.sparse_workload_loss}[args.config]
 
 
 def cpu_baseline(args):
@@ -154,9 +187,11 @@ def main():
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, src=0)
     use_bf16 = args.dtype == "bf16"
-    trainer = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, lr=1e-4, weight_decay=1e-4,
+    if args.config == "sparse":
+        args.graph = 0  # host-side top-k sizes (reference :212, criterion.py:271): not capturable
+    trainer = PKG.train_step.FlatGradTrainer(model, loss_fn(args), lr=1e-4, weight_decay=1e-4,
                                              max_norm=0.1, use_bf16=use_bf16, graph=bool(args.graph))
-    batch = PKG.dvc_core.synthetic_clips(args.batch, T=args.T, seed=1000 + rank, device=device)
+    batch = build_batch(args, rank, device)
 
     trainer.capture(batch)  # eager warm-up steps + graph capture (no-op without --graph)
     for _ in range(args.warmup):
@@ -200,16 +235,14 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if use_bf16 else "fp32",
             "data": "synthetic (ActivityNet-shaped features N(0,1), random-init weights)",
-            "config": {"workload": "configs[1]: models/deformable video-only, 4-level pyramid T=1024 d=512, "
-                                   "100 queries; BaseEncoder + 6 enc + 6 dec + heads, AdamW step",
-                       "model": "DeformableDVCCore (UnimodalDeformableDVC proposal path)",
+            "config": {"workload": WORKLOADS[args.config], "model": MODELS[args.config],
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch, "seq_len": args.T,
                        "d_model": 512, "levels": 4, "queries": args.queries, "parallelism": f"dp{world}",
                        "execution": "hip_graph" if args.graph else "eager"},
             "roofline": roofline(summary, traffic),
             "cpu_baseline": None,
         }
-        if args.cpu_baseline and world == 1:
+        if args.cpu_baseline and world == 1 and args.config == "video":
             result["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -15,12 +15,16 @@ import torch
 from torch import nn
 
 from .models.base_encoder import BaseEncoder
+from .models.deformable.multimodal_deformable_transformer import MultimodalDeformableTransformer
 from .models.deformable.unimodal_deformable_transformer import DeformableTransformer
+from .models.sparse.unimodal_sparse_deformable_transformer import SparseDeformableTransformer
 from .models.modules.embedding_layers import FFN, PositionEmbeddingVideoSine
-from .models.modules.misc_modules import predict_event_num
+from .models.modules.misc_modules import inverse_sigmoid, predict_event_num, predict_event_num_with_depth
+from .utils.dam import attn_map_to_flat_grid
 from .models.modules.linear import Linear
 
-__all__ = ["DeformableDVCCore", "synthetic_clips", "workload_loss"]
+__all__ = ["DeformableDVCCore", "MultimodalDVCCore", "SparseDVCCore", "synthetic_clips", "workload_loss",
+           "multimodal_workload_loss", "sparse_workload_loss"]
 
 
 class DeformableDVCCore(nn.Module):
@@ -96,3 +100,128 @@ def workload_loss(out):
     plus the heads' outputs, so every head and decoder level carries gradient."""
     return (out["hs"].float().sum() + out["memory"].float().sum() + out["all_segments"].float().sum()
             + out["all_counts"].float().sum() + (out["all_logits"].float() * 1e-2).square().sum())
+
+
+class MultimodalDVCCore(nn.Module):
+    """Config 3: the proposal path of the reference's ``MultimodalDeformableDVC``
+    (models/deformable/multimodal_deformable_dvc.py:112-230) — one BaseEncoder shared by the video
+    and audio streams (:155-156), the multimodal deformable encoder (4 MSDA calls per layer:
+    video->video, audio->audio and both cross-modal directions) and decoder (2 MSDA
+    cross-attentions per layer + the fusion bridge), and the shared per-level heads.  Audio
+    features are 512-d (the shared base encoder needs it; a 128-d VGGish input would need a
+    projection the reference lacks)."""
+
+    def __init__(self, d_model=512, num_queries=100, num_classes=200, max_eseq_length=10, feature_dim=512,
+                 num_heads=8, num_feature_levels=4, enc_layers=6, dec_layers=6, ff_dim=2048, dropout=0.1,
+                 enc_n_points=4, dec_n_points=4):
+        super().__init__()
+        self.query_embedding = nn.Embedding(num_queries, d_model * 2)
+        class_embedding = Linear(d_model, num_classes + 1)
+        segment_embedding = FFN(in_dim=d_model, hidden_dim=d_model, out_dim=2, num_layers=3)
+        count_head = Linear(d_model, max_eseq_length + 1)
+        self.pos_embed = PositionEmbeddingVideoSine(d_model // 2, normalize=True)
+        self.base_encoder = BaseEncoder(num_feature_levels, feature_dim, d_model)
+        prior_prob = 0.01
+        class_embedding.bias.data = torch.ones(num_classes + 1) * -math.log((1 - prior_prob) / prior_prob)
+        nn.init.constant_(segment_embedding.layers[-1].weight.data, 0)
+        nn.init.constant_(segment_embedding.layers[-1].bias.data, 0)
+        self.multimodal_deformable_transformer = MultimodalDeformableTransformer(
+            d_model=d_model, num_head=num_heads, num_encoder_layers=enc_layers, num_decoder_layers=dec_layers,
+            dim_feedforward=ff_dim, dropout=dropout, activation="relu", return_intermediate_dec=True,
+            num_feature_levels=num_feature_levels, dec_n_points=dec_n_points, enc_n_points=enc_n_points)
+        nn.init.constant_(segment_embedding.layers[-1].bias.data[2:], -2.0)
+        self.class_embedding = nn.ModuleList([class_embedding for _ in range(dec_layers)])
+        self.count_head = nn.ModuleList([count_head for _ in range(dec_layers)])
+        self.segment_embedding = nn.ModuleList([segment_embedding for _ in range(dec_layers)])
+
+    def forward(self, video, video_mask, audio, audio_mask, durations):
+        tr = self.multimodal_deformable_transformer
+        B = video.shape[0]
+        v_srcs, v_masks, v_pos = self.base_encoder(video, video_mask, durations, self.pos_embed)
+        a_srcs, a_masks, a_pos = self.base_encoder(audio, audio_mask, durations, self.pos_embed)
+        v = tr.prepare_encoder_inputs(v_srcs, v_masks, v_pos)
+        a = tr.prepare_encoder_inputs(a_srcs, a_masks, a_pos)
+        mem_v, mem_a = tr.forward_encoder(*v, *a)
+        qw = self.query_embedding.weight
+        query_mask = torch.ones(B, qw.shape[0], dtype=torch.bool, device=qw.device)
+        _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qw)
+        hs, inter = tr.forward_decoder(tgt, refp, qpos, query_mask, mem_v, v[1], v[2], v[3], v[5], mem_a, a[1], a[2],
+                                       a[3], a[5], False)
+        classes, segments, counts = [], [], []
+        for lvl in range(hs.shape[0]):
+            classes.append(self.class_embedding[lvl](hs[lvl]).softmax(dim=-1))
+            segments.append(self.segment_embedding[lvl](hs[lvl]).sigmoid())
+            counts.append(predict_event_num(self.count_head[lvl], hs[lvl]))
+        return {"all_logits": torch.stack(classes), "all_segments": torch.stack(segments),
+                "all_counts": torch.stack(counts), "hs": hs, "memory_video": mem_v, "memory_audio": mem_a}
+
+
+def multimodal_workload_loss(out):
+    return (out["hs"].float().sum() + out["memory_video"].float().sum() + out["memory_audio"].float().sum()
+            + out["all_segments"].float().sum() + out["all_counts"].float().sum()
+            + (out["all_logits"].float() * 1e-2).square().sum())
+
+
+class SparseDVCCore(nn.Module):
+    """The proposal path of the reference's ``UnimodalSparseDVC``
+    (models/sparse/unimodal_sparse_dvc.py:111-230): BaseEncoder, Sparse-DETR transformer
+    (rho = 0.3: only the top 30 % encoder tokens are refined, over the full pyramid), decoder with
+    reference-point-relative segments and the count head.  The output also carries what the
+    criterion's mask-prediction loss needs (models/criterion.py:246-280)."""
+
+    def __init__(self, d_model=512, num_queries=100, max_eseq_length=10, feature_dim=512, num_heads=8,
+                 num_feature_levels=4, enc_layers=6, dec_layers=6, ff_dim=2048, dropout=0.1, enc_n_points=4,
+                 dec_n_points=4, rho=0.3):
+        super().__init__()
+        self.query_embedding = nn.Embedding(num_queries, d_model * 2)
+        self.segment_embedding_decoder = FFN(in_dim=d_model, hidden_dim=d_model, out_dim=2, num_layers=3)
+        self.count_head_decoder = Linear(d_model, max_eseq_length + 1)
+        self.pos_embed = PositionEmbeddingVideoSine(d_model // 2, normalize=True)
+        self.base_encoder = BaseEncoder(num_feature_levels, feature_dim, d_model)
+        nn.init.constant_(self.segment_embedding_decoder.layers[-1].weight.data, 0.)
+        nn.init.constant_(self.segment_embedding_decoder.layers[-1].bias.data[:2], 0.)
+        nn.init.constant_(self.segment_embedding_decoder.layers[-1].bias.data[2:], -2.0)
+        self.unimodal_sparse_transformer = SparseDeformableTransformer(
+            d_model=d_model, num_head=num_heads, num_encoder_layers=enc_layers, num_decoder_layers=dec_layers,
+            dim_feedforward=ff_dim, dropout=dropout, activation="relu", return_intermediate_dec=True,
+            num_feature_levels=num_feature_levels, dec_n_points=dec_n_points, enc_n_points=enc_n_points, rho=rho)
+
+    def forward(self, video, video_mask, durations):
+        tr = self.unimodal_sparse_transformer
+        B = video.shape[0]
+        srcs, masks, pos = self.base_encoder(video, video_mask, durations, self.pos_embed)
+        (src_flatten, shapes, starts, valid, lvl_pos, mask_flatten, proposals, topk, mask_pred,
+         sparse_token_nums) = tr.prepare_encoder_inputs(srcs, masks, pos)
+        memory, sl_enc, aw_enc, _, _ = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten,
+                                                          proposals, topk, sparse_token_nums)
+        qw = self.query_embedding.weight
+        query_mask = torch.ones(B, qw.shape[0], dtype=torch.bool, device=qw.device)
+        init_ref, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qw)
+        hs, inter, sl_dec, aw_dec = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten,
+                                                       query_mask, False)
+        segments = self.segment_embedding_decoder(hs)
+        counts = predict_event_num_with_depth(self.count_head_decoder, hs)
+        reference = torch.cat([init_ref[None], inter[:-1]], 0)  # reference :194-196
+        # (depth, B, Q, 1) broadcast over both segment terms, as ``outputs_segment[..., :2] += reference`` (:203)
+        segments = (segments + inverse_sigmoid(reference)).sigmoid()
+        return {"all_segments": segments, "all_counts": counts, "hs": hs, "memory": memory,
+                "backbone_mask_prediction": mask_pred, "sparse_token_nums": sparse_token_nums,
+                "sampling_locations_dec": sl_dec, "attn_weights_dec": aw_dec, "temporal_shapes": shapes,
+                "level_start_index": starts, "mask_flatten": mask_flatten}
+
+
+def sparse_workload_loss(out):
+    """hs / memory / heads as workload_loss, plus the criterion's mask-prediction loss
+    (models/criterion.py:246-280): the decoder attention map (DAM kernel) summed over layers and
+    heads, its top sparse_token_nums tokens as the target of the mask predictor."""
+    dam = attn_map_to_flat_grid(out["temporal_shapes"], out["level_start_index"],
+                                out["sampling_locations_dec"].detach(), out["attn_weights_dec"].detach()).sum(dim=(1, 2))
+    dam = dam.masked_fill(out["mask_flatten"], dam.min() - 1)
+    nums = out["sparse_token_nums"]
+    topk = torch.topk(dam, int(nums.max()))[1]
+    keep = torch.arange(topk.shape[1], device=topk.device)[None, :] < nums[:, None]
+    pred = out["backbone_mask_prediction"]
+    target = torch.zeros_like(pred).scatter_(1, topk, keep.to(pred.dtype))
+    mask_loss = torch.nn.functional.multilabel_soft_margin_loss(pred.float(), target.float())
+    return (out["hs"].float().sum() + out["memory"].float().sum() + out["all_segments"].float().sum()
+            + out["all_counts"].float().sum() + mask_loss)

@@ -139,3 +139,29 @@ def test_graph_replay_matches_eager_step(dev, bf16):
     after = _params(model)
     assert any(not torch.equal(before[k], after[k]) for k in before)
     assert all(torch.isfinite(v).all() for v in after.values())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["multimodal", "sparse"])
+def test_other_dvc_cores_train_one_step(config):
+    """configs[2] (video + audio) and the Sparse-DETR DVC: one bf16 training step through the
+    trainer is finite and moves every parameter that receives a gradient."""
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    small = dict(d_model=64, num_queries=6, feature_dim=64, enc_layers=1, dec_layers=2, ff_dim=128, dropout=0.0)
+    video, vmask, dur = PKG.dvc_core.synthetic_clips(2, T=64, feature_dim=64, padded=True, device=dev)
+    if config == "multimodal":
+        model = PKG.dvc_core.MultimodalDVCCore(num_classes=5, **small).to(dev)
+        audio, amask, _ = PKG.dvc_core.synthetic_clips(2, T=16, feature_dim=64, padded=True, seed=9, device=dev)
+        batch, loss_fn = (video, vmask, audio, amask, dur), PKG.dvc_core.multimodal_workload_loss
+    else:
+        model = PKG.dvc_core.SparseDVCCore(**small).to(dev)
+        batch, loss_fn = (video, vmask, dur), PKG.dvc_core.sparse_workload_loss
+    before = {k: v.detach().clone() for k, v in model.named_parameters()}
+    tr = PKG.train_step.FlatGradTrainer(model, loss_fn, lr=1e-3, use_bf16=True, graph=False)
+    loss = tr.eager_step(batch)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).item()
+    assert torch.isfinite(tr.flat_grad).all().item() and tr.flat_grad.abs().sum().item() > 0
+    moved = sum(int(not torch.equal(before[k], v.detach())) for k, v in model.named_parameters())
+    assert moved > len(before) // 2
