@@ -1,0 +1,38 @@
+/*
+ * flat_adamw.h — C-ABI of the training step's fused optimizer over one flat fp32 parameter
+ * buffer (multimodal-feature-learning_amd/csrc/flat_adamw.hip, built into libmsda_hip.so).
+ *
+ * Runtime component, not part of the MSDA boundary: it replaces, for the flat-buffer trainer
+ * (train_step.py), the reference step's clip_grad_norm_ + AdamW
+ * (reference engine.py:125-127, main.py:113) with the semantics of
+ * torch.nn.utils.clip_grad_norm_(max_norm) followed by torch.optim.AdamW(lr, (beta1, beta2), eps,
+ * weight_decay), and refreshes the bf16 shadow of the parameters in the same pass.
+ * Graph-capturable: the step count (`step`, one fp32 device scalar) and the clip coefficient
+ * stay on the device.  Gradients are read, not modified (the clip is applied on the fly).
+ */
+#ifndef FLAT_ADAMW_H_
+#define FLAT_ADAMW_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Bytes of device scratch flat_adamw_step needs (8-byte aligned). */
+size_t flat_adamw_workspace_bytes(void);
+
+/* One optimizer step over n parameters (16-byte aligned fp32 buffers; bf16_shadow may be NULL).
+ * max_norm <= 0 disables clipping.  Returns 0, or non-zero with flat_adamw_last_error(). */
+int flat_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, uint16_t* bf16_shadow,
+                    int64_t n, float* step, void* workspace, float lr, float beta1, float beta2, float eps,
+                    float weight_decay, float max_norm, void* stream);
+
+const char* flat_adamw_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* FLAT_ADAMW_H_ */

@@ -30,6 +30,10 @@ EXPORTED_SYMBOLS = (
     "msda_hip_prologue_forward",
     "msda_hip_prologue_backward",
     "msda_hip_dam_flat_grid",
+    # include/flat_adamw.h (training-step runtime, same library)
+    "flat_adamw_workspace_bytes",
+    "flat_adamw_step",
+    "flat_adamw_last_error",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -56,6 +60,13 @@ def _declare(lib):
                                                vp, vp, vp, vp]
     lib.msda_hip_dam_flat_grid.restype = i32
     lib.msda_hip_dam_flat_grid.argtypes = [vp, vp, p64, p64, i64, i64, i64, i64, i64, vp, vp]
+    f32 = ctypes.c_float
+    lib.flat_adamw_workspace_bytes.restype = ctypes.c_size_t
+    lib.flat_adamw_workspace_bytes.argtypes = []
+    lib.flat_adamw_step.restype = i32
+    lib.flat_adamw_step.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, f32, f32, f32, f32, f32, f32, vp]
+    lib.flat_adamw_last_error.restype = ctypes.c_char_p
+    lib.flat_adamw_last_error.argtypes = []
     lib.msda_hip_last_error.restype = ctypes.c_char_p
     lib.msda_hip_last_error.argtypes = []
     lib.msda_hip_abi_version.restype = i32

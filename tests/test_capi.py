@@ -1,5 +1,6 @@
-"""The C-ABI library: loads without a GPU, exports every symbol include/msda_hip.h
-declares, and rejects bad arguments with a status + message before touching a device."""
+"""The C-ABI library: loads without a GPU, exports every symbol include/msda_hip.h and
+include/flat_adamw.h declare, and rejects bad arguments with a status + message before
+touching a device."""
 import ctypes
 import os
 import re
@@ -8,12 +9,16 @@ import pytest
 
 from conftest import PKG, ROOT
 
-HEADER = os.path.join(ROOT, "include", "msda_hip.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("msda_hip.h", "flat_adamw.h")]
 
 
 def declared_symbols():
-    text = open(HEADER).read()
-    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(msda_hip_\w+)\s*\(", text, re.M)))
+    names = set()
+    for h in HEADERS:
+        text = open(h).read()
+        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*((?:msda_hip|flat_adamw)_\w+)\s*\(", text,
+                                re.M))
+    return sorted(names)
 
 
 def test_header_symbols_match_binding():

@@ -165,3 +165,33 @@ def test_other_dvc_cores_train_one_step(config):
     assert torch.isfinite(tr.flat_grad).all().item() and tr.flat_grad.abs().sum().item() > 0
     moved = sum(int(not torch.equal(before[k], v.detach())) for k, v in model.named_parameters())
     assert moved > len(before) // 2
+
+
+@pytest.mark.gpu
+def test_fused_flat_adamw_matches_torch_adamw():
+    """csrc/flat_adamw.hip (clip_grad_norm_ + AdamW over the flat buffers, bf16 shadow in the
+    same pass) against torch.nn.utils.clip_grad_norm_ + torch.optim.AdamW on the same model,
+    fp32, three steps with the clip active (max_norm 0.1) and inactive (max_norm 1e6).
+    Tolerance: fp32 (the two order their norm sums differently)."""
+    dev = torch.device("cuda", 0)
+    batch = _batch(2, dev)
+    for max_norm in (0.1, 1e6):
+        ref, mine = _model(dev), _model(dev)
+        t_ref = PKG.train_step.FlatGradTrainer(ref, PKG.dvc_core.workload_loss, lr=1e-3, weight_decay=1e-2,
+                                               max_norm=max_norm, use_bf16=False, graph=False, fused_optimizer=False)
+        t_mine = PKG.train_step.FlatGradTrainer(mine, PKG.dvc_core.workload_loss, lr=1e-3, weight_decay=1e-2,
+                                                max_norm=max_norm, use_bf16=False, graph=False, fused_optimizer=True)
+        for _ in range(3):  # the same gradients into both optimizers (the MSDA backward's LDS-atomic
+            t_ref._forward_backward(batch)  # list order would otherwise flip Adam's sign on ~0 grads)
+            t_mine.flat_grad.copy_(t_ref.flat_grad)
+            t_ref._update()
+            t_mine._update()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(t_mine.flat_param, t_ref.flat_param, rtol=2e-5, atol=2e-6)
+        assert float(t_mine.opt_step.item()) == 3.0
+    # bf16 trainer: the shadow written by the optimizer pass is exactly the cast of the new weights
+    m = _model(dev)
+    t = PKG.train_step.FlatGradTrainer(m, PKG.dvc_core.workload_loss, lr=1e-3, use_bf16=True, graph=False)
+    t.eager_step(batch)
+    torch.cuda.synchronize()
+    assert torch.equal(t.flat_bf16, t.flat_param.to(torch.bfloat16))
