@@ -1030,33 +1030,45 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
   const long long vofs = ((b * S + lv.start[l]) * M + m) * (long long)D + c_l * CPL;
   const scalar_t* __restrict__ vl = value + vofs;
   scalar_t* __restrict__ gvl = gval + vofs;
-  // NS rows per wave-iteration; per batch U grad_out fragments in flight.  (A software-
-  // pipelined variant that kept the next batch in flight while consuming this one measured
-  // slower: 93 vs 81 us at the bench's encoder shape.)
-  for (int r0 = wave * NS; r0 < T; r0 += (kGvThreads / 64) * NS) {
-    const int row = r0 + slot;
+  // Per wave iteration NS slots of LPR lanes; SPR consecutive slots share one value row
+  // (slots-per-row, from the level's average taps per row: 1 for the fine levels, up to NS for
+  // the coarsest), each taking every SPR-th entry of the row's list, so a long row is not walked
+  // by one slot while the others idle; the SPR partial sums meet through lane shuffles.  Per
+  // batch U grad_out fragments in flight.  (A software-pipelined variant that kept the next batch
+  // in flight while consuming this one measured slower: 93 vs 81 us at the encoder shape.)
+  const int avg_taps = ncap / T;
+  int SPR = avg_taps >= 96 ? 8 : avg_taps >= 48 ? 4 : avg_taps >= 24 ? 2 : 1;
+  SPR = SPR > NS ? NS : SPR;
+#ifdef MSDA_NO_SPR  // A/B builds only
+  SPR = 1;
+#endif
+  const int rpi = NS / SPR;  // value rows per wave iteration
+  const int sub = slot % SPR;
+  for (int r0 = wave * rpi; r0 < T; r0 += (kGvThreads / 64) * rpi) {
+    const int row = r0 + slot / SPR;
     const bool valid = row < T;
     const int e0 = valid ? (row == 0 ? 0 : cur[row - 1]) : 0;
     const int count = valid ? cur[row] - e0 : 0;
+    const int csub = count > sub ? (count - sub + SPR - 1) / SPR : 0;  // entries sub, sub+SPR, ...
     uint4 vr = make_uint4(0u, 0u, 0u, 0u);
-    if constexpr (COORDS) vr = load16_if_nt(count > 0, vl + row * rs);
+    if constexpr (COORDS) vr = load16_if_nt(csub > 0, vl + row * rs);
     f32x2 acc[CPL / 2];
 #pragma unroll
     for (int e = 0; e < CPL / 2; ++e) acc[e] = f32x2{0.f, 0.f};
-    for (int j0 = 0; __ballot(j0 < count) != 0ull; j0 += U) {
+    for (int j0 = 0; __ballot(j0 < csub) != 0ull; j0 += U) {
       // registers hold only the U gathered fragments; the keys and tap weights are read
       // from LDS again when consumed (a ds_read is ~50 cycles, a gather thousands)
       uint4 g[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const bool have = j0 + u < count;
-        const unsigned key = have ? ent[e0 + j0 + u] : 0u;
+        const bool have = j0 + u < csub;
+        const unsigned key = have ? ent[e0 + sub + (j0 + u) * SPR] : 0u;
         g[u] = load16_if(have, gb + (int)(key >> 8) * rs);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const bool have = j0 + u < count;
-        const unsigned key = have ? ent[e0 + j0 + u] : 0u;
+        const bool have = j0 + u < csub;
+        const unsigned key = have ? ent[e0 + sub + (j0 + u) * SPR] : 0u;
         const int tt = (int)(key >> 8) * twoP + (int)(key & 0xffu);
         const float w = have ? wd[tt] : 0.f;
         f32x2 x[CPL / 2];
@@ -1070,7 +1082,14 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
         }
       }
     }
-    if (valid) {
+    for (int o = LPR; o < LPR * SPR; o <<= 1) {  // sum the row's SPR partials (wave-uniform)
+#pragma unroll
+      for (int e = 0; e < CPL / 2; ++e) {
+        acc[e].x += __shfl_xor(acc[e].x, o);
+        acc[e].y += __shfl_xor(acc[e].y, o);
+      }
+    }
+    if (valid && sub == 0) {
       float a[CPL];
 #pragma unroll
       for (int e = 0; e < CPL / 2; ++e) {
