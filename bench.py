@@ -28,7 +28,9 @@ import subprocess
 import sys
 import time
 
-import torch
+# before torch touches HIP: see multimodal-feature-learning_amd/__init__.py (graph packet capture)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+import torch  # noqa: E402
 import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))

@@ -9,6 +9,7 @@
  * weight_decay), and refreshes the bf16 shadow of the parameters in the same pass.
  * Graph-capturable: the step count (`step`, one fp32 device scalar) and the clip coefficient
  * stay on the device.  Gradients are read, not modified (the clip is applied on the fly).
+ * Also the bias-gradient column sum of the autocast Linear (mfl_colsum).
  */
 #ifndef FLAT_ADAMW_H_
 #define FLAT_ADAMW_H_
@@ -29,6 +30,14 @@ int flat_adamw_step(float* params, const float* grads, float* exp_avg, float* ex
                     int64_t n, float* step, void* workspace, float lr, float beta1, float beta2, float eps,
                     float weight_decay, float max_norm, void* stream);
 
+/* Column sums in fp32 of a row-major (K, N) matrix x (dtype tag as msda_hip.h: 0 fp32, 2 bf16,
+ * 3 fp16; N*elt a multiple of 16 bytes, x 16-byte aligned): the bias gradient of the autocast
+ * Linear (models/modules/linear.py), sum over the K token rows of dY.  Fixed summation order.
+ * workspace: mfl_colsum_workspace_bytes(K, N) bytes. */
+size_t mfl_colsum_workspace_bytes(int64_t K, int64_t N);
+int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void* workspace, void* stream);
+
+/* Text of the last error of flat_adamw_step / mfl_colsum on the calling thread. */
 const char* flat_adamw_last_error(void);
 
 #ifdef __cplusplus

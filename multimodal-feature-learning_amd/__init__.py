@@ -15,7 +15,15 @@ The directory name is not a Python identifier; import it with
 ``importlib.import_module("multimodal-feature-learning_amd")``.  The import registers
 ``mfl_amd`` (and ``mfl_amd.<submodule>``) as aliases of the same module objects.
 """
+import os as _os
 import sys as _sys
+
+# HIP runtime setting, read once when the process initialises HIP (so it must be set before the
+# first device call): with the CLR's graph packet capture (the default), a captured bf16 training
+# step replayed after eager work that allocates device memory produced corrupted gradients
+# (tools/step_diag.py --graph 1; exact again with the capture off, see DESIGN.md §6).  Replays
+# with nothing allocating between them were exact either way.
+_os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 
 __version__ = "0.1.0"
 

@@ -34,6 +34,8 @@ EXPORTED_SYMBOLS = (
     "flat_adamw_workspace_bytes",
     "flat_adamw_step",
     "flat_adamw_last_error",
+    "mfl_colsum_workspace_bytes",
+    "mfl_colsum",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -65,6 +67,10 @@ def _declare(lib):
     lib.flat_adamw_workspace_bytes.argtypes = []
     lib.flat_adamw_step.restype = i32
     lib.flat_adamw_step.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, f32, f32, f32, f32, f32, f32, vp]
+    lib.mfl_colsum_workspace_bytes.restype = ctypes.c_size_t
+    lib.mfl_colsum_workspace_bytes.argtypes = [i64, i64]
+    lib.mfl_colsum.restype = i32
+    lib.mfl_colsum.argtypes = [vp, i32, i64, i64, vp, vp, vp]
     lib.flat_adamw_last_error.restype = ctypes.c_char_p
     lib.flat_adamw_last_error.argtypes = []
     lib.msda_hip_last_error.restype = ctypes.c_char_p

@@ -143,6 +143,102 @@ __global__ __launch_bounds__(kThreads) void flat_adamw_update(float* __restrict_
   }
 }
 
+
+// ---------------------------------------------------------------------------------
+// Bias gradient of the autocast Linear (models/modules/linear.py): db = sum over the K token
+// rows of dY (K x N, 16-bit or fp32) in fp32.  torch's column reduction of a (15360, 512) bf16
+// tensor takes ~14 us; here one pass of 16-byte loads: block (column strip of 32x16 B, row
+// chunk) partial sums in LDS -> partials[chunk][N], then a fixed-order sum over chunks
+// (deterministic).
+// ---------------------------------------------------------------------------------
+constexpr int kColRows = 8;    // row lanes per block
+constexpr int kColLanes = 32;  // 16-byte column lanes per block
+
+template <typename T>
+__device__ __forceinline__ void cvt16(const uint4& raw, float (&f)[16 / sizeof(T)]);
+template <>
+__device__ __forceinline__ void cvt16<uint16_t>(const uint4& raw, float (&f)[8]) {  // bf16
+  const uint32_t d[4] = {raw.x, raw.y, raw.z, raw.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(d[i] << 16);
+    f[2 * i + 1] = __uint_as_float(d[i] & 0xffff0000u);
+  }
+}
+template <>
+__device__ __forceinline__ void cvt16<_Float16>(const uint4& raw, float (&f)[8]) {
+  const _Float16* h = reinterpret_cast<const _Float16*>(&raw);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)h[i];
+}
+template <>
+__device__ __forceinline__ void cvt16<float>(const uint4& raw, float (&f)[4]) {
+  f[0] = __uint_as_float(raw.x); f[1] = __uint_as_float(raw.y);
+  f[2] = __uint_as_float(raw.z); f[3] = __uint_as_float(raw.w);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kColRows * kColLanes) void colsum_partial(const T* __restrict__ x, long long K, int N,
+                                                                      int rows_per_chunk, float* __restrict__ part) {
+  constexpr int V = 16 / sizeof(T);
+  __shared__ float red[kColRows][kColLanes * V];
+  const int cl = threadIdx.x % kColLanes, rl = threadIdx.x / kColLanes;
+  const int c0 = (blockIdx.x * kColLanes + cl) * V;
+  const long long r_begin = (long long)blockIdx.y * rows_per_chunk;
+  const long long r_end = min(K, r_begin + rows_per_chunk);
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = 0.f;
+  if (c0 < N) {
+    for (long long r = r_begin + rl; r < r_end; r += kColRows) {
+      float f[V];
+      cvt16<T>(*reinterpret_cast<const uint4*>(x + r * N + c0), f);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] += f[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) red[rl][cl * V + i] = acc[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < kColLanes * V; c += kColRows * kColLanes) {
+    float s = 0.f;
+#pragma unroll
+    for (int r = 0; r < kColRows; ++r) s += red[r][c];
+    const int col = blockIdx.x * kColLanes * V + c;
+    if (col < N) part[(long long)blockIdx.y * N + col] = s;
+  }
+}
+
+// out[c] = sum over chunks of part[k][c]: 16 chunk groups x 64 columns per 1024-thread block,
+// each thread a strided quarter-unrolled run over its chunks, then an LDS reduction over the
+// groups (fixed order: deterministic).
+constexpr int kFinGroups = 16;
+__global__ __launch_bounds__(kFinGroups * 64) void colsum_final(const float* __restrict__ part, int nchunks, int N,
+                                                               float* __restrict__ out) {
+  __shared__ float red[kFinGroups][64];
+  const int c_l = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + c_l;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (c < N) {
+    int k = g;
+    for (; k + 3 * kFinGroups < nchunks; k += 4 * kFinGroups) {
+      s0 += part[(long long)k * N + c];
+      s1 += part[(long long)(k + kFinGroups) * N + c];
+      s2 += part[(long long)(k + 2 * kFinGroups) * N + c];
+      s3 += part[(long long)(k + 3 * kFinGroups) * N + c];
+    }
+    for (; k < nchunks; k += kFinGroups) s0 += part[(long long)k * N + c];
+  }
+  red[g][c_l] = (s0 + s1) + (s2 + s3);
+  __syncthreads();
+  if (g == 0 && c < N) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < kFinGroups; ++i) t += red[i][c_l];
+    out[c] = t;
+  }
+}
+
 int status(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -191,6 +287,45 @@ int flat_adamw_step(float* params, const float* grads, float* exp_avg, float* ex
   hipLaunchKernelGGL(flat_adamw_update, dim3(blocks), dim3(kThreads), 0, st, params, grads, exp_avg, exp_avg_sq,
                      bf16_shadow, (long long)n, state, lr, weight_decay, beta1, beta2, eps);
   return status("update");
+}
+
+
+size_t mfl_colsum_workspace_bytes(int64_t K, int64_t N) {
+  const long long chunks = std::min<long long>(256, std::max<long long>(1, (K + 63) / 64));
+  return (size_t)chunks * (size_t)std::max<int64_t>(N, 1) * sizeof(float);
+}
+
+int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void* workspace, void* stream) {
+  g_err[0] = 0;
+  const int elt = dtype == 0 ? 4 : 2;
+  if (K < 0 || N <= 0 || out == nullptr || (K > 0 && (x == nullptr || workspace == nullptr)) ||
+      (dtype != 0 && dtype != 2 && dtype != 3) || (N * elt) % 16 != 0 || reinterpret_cast<uintptr_t>(x) % 16 != 0) {
+    snprintf(g_err, sizeof(g_err), "mfl_colsum: bad arguments (N*elt must be a multiple of 16 B, x 16-B aligned)");
+    return 1;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (K == 0) {
+    return hipMemsetAsync(out, 0, (size_t)N * 4, st) == hipSuccess ? 0 : 2;
+  }
+  const long long chunks = std::min<long long>(256, std::max<long long>(1, (K + 63) / 64));
+  const int rows_per_chunk = (int)((K + chunks - 1) / chunks);
+  const int V = 16 / elt;
+  const dim3 grid((unsigned)((N / V + kColLanes - 1) / kColLanes), (unsigned)chunks);
+  auto* part = static_cast<float*>(workspace);
+  if (dtype == 0)
+    hipLaunchKernelGGL(colsum_partial<float>, grid, dim3(kColRows * kColLanes), 0, st, static_cast<const float*>(x),
+                       (long long)K, (int)N, rows_per_chunk, part);
+  else if (dtype == 2)
+    hipLaunchKernelGGL(colsum_partial<uint16_t>, grid, dim3(kColRows * kColLanes), 0, st,
+                       static_cast<const uint16_t*>(x), (long long)K, (int)N, rows_per_chunk, part);
+  else
+    hipLaunchKernelGGL(colsum_partial<_Float16>, grid, dim3(kColRows * kColLanes), 0, st,
+                       static_cast<const _Float16*>(x), (long long)K, (int)N, rows_per_chunk, part);
+  int rc;
+  if ((rc = status("colsum partial"))) return rc;
+  hipLaunchKernelGGL(colsum_final, dim3((unsigned)((N + 63) / 64)), dim3(kFinGroups * 64), 0, st, part, (int)chunks,
+                     (int)N, out);
+  return status("colsum final");
 }
 
 const char* flat_adamw_last_error(void) { return g_err; }

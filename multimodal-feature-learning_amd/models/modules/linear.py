@@ -36,6 +36,36 @@ def split_k_chunks(k, min_chunk=1024, max_split=8):
     return 1
 
 
+def _bias_grad(g2):
+    """fp32 column sum of dY (K, N) through mfl_colsum (one streaming pass, fixed order);
+    torch's column reduction where the kernel's layout conditions do not hold."""
+    if g2.dtype not in (torch.bfloat16, torch.float16) or (g2.shape[1] * 2) % 16 or not g2.is_contiguous():
+        return g2.sum(0, dtype=torch.float32)
+    from ... import _native
+    lib = _native.load_library()
+    K, N = g2.shape
+    out = torch.empty(N, dtype=torch.float32, device=g2.device)
+    ws = torch.empty(lib.mfl_colsum_workspace_bytes(K, N), dtype=torch.uint8, device=g2.device)
+    rc = lib.mfl_colsum(g2.data_ptr(), _native.DTYPE_TAGS[g2.dtype], K, N, out.data_ptr(), ws.data_ptr(),
+                        _native.stream_handle(g2.device))
+    if rc != 0:
+        raise RuntimeError("mfl_colsum failed: " + lib.flat_adamw_last_error().decode())
+    return out
+
+
+def _weight_grad(g2, x2):
+    """fp32 dW = dY^T X of 16-bit dY (K, N) and X (K, C): K split into chunks, one strided-batched
+    GEMM with fp32 partial outputs, then their sum."""
+    k, n_out, n_in = x2.shape[0], g2.shape[1], x2.shape[1]
+    s = split_k_chunks(k)
+    if s > 1:
+        part = torch.empty(s, n_out, n_in, device=g2.device, dtype=torch.float32)
+        torch.baddbmm(part, g2.view(s, k // s, n_out).transpose(1, 2), x2.view(s, k // s, n_in),
+                      beta=0, out_dtype=torch.float32, out=part)
+        return part.sum(0)
+    return torch.mm(g2.t(), x2, out_dtype=torch.float32)
+
+
 class _AutocastLinear(torch.autograd.Function):
     """y = x W^T + b with x already in the autocast dtype; W, b fp32 masters; wc / bc optional
     low-precision copies of W / b (the trainer's shadow) used instead of casting."""
@@ -63,17 +93,9 @@ class _AutocastLinear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             gx = torch.mm(g2, wc).view(ctx.x_shape)
         if ctx.needs_input_grad[1]:
-            k, n_out, n_in = x2.shape[0], g2.shape[1], x2.shape[1]
-            s = split_k_chunks(k)
-            if s > 1:
-                part = torch.empty(s, n_out, n_in, device=g2.device, dtype=torch.float32)
-                torch.baddbmm(part, g2.view(s, k // s, n_out).transpose(1, 2), x2.view(s, k // s, n_in),
-                              beta=0, out_dtype=torch.float32, out=part)
-                gw = part.sum(0)
-            else:
-                gw = torch.mm(g2.t(), x2, out_dtype=torch.float32)
+            gw = _weight_grad(g2, x2)
         if ctx.has_bias and ctx.needs_input_grad[2]:
-            gb = g2.sum(0, dtype=torch.float32)
+            gb = _bias_grad(g2)
         return gx, gw, gb, None, None
 
 

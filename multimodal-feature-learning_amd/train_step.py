@@ -36,7 +36,8 @@ __all__ = ["FlatGradTrainer"]
 
 class FlatGradTrainer:
     def __init__(self, model, loss_fn, lr=1e-4, weight_decay=1e-4, max_norm=0.1, use_bf16=True, graph=True,
-                 process_group=None, fused_optimizer=None, betas=(0.9, 0.999), eps=1e-8):
+                 process_group=None, fused_optimizer=None, betas=(0.9, 0.999), eps=1e-8, handover=True,
+                 shadow=True):
         self.model = model
         self.loss_fn = loss_fn
         self.max_norm = max_norm
@@ -65,7 +66,8 @@ class FlatGradTrainer:
         # bf16 weight shadow for the autocast Linear layers (one cast per step, _refresh_shadow)
         self.flat_bf16 = None
         self._linears = []
-        if use_bf16 and dev.type == "cuda":
+        self.handover = handover
+        if use_bf16 and dev.type == "cuda" and shadow:
             self.flat_bf16 = self.flat_param.to(torch.bfloat16)
             index = {id(p): v for p, v in zip(self.params, self._views(self.flat_bf16))}
             for mod in model.modules():
@@ -116,6 +118,13 @@ class FlatGradTrainer:
             mod.set_bf16_shadow(w, b)
 
     def _forward_backward(self, batch, cache_casts=True):
+        if not self.handover:  # accumulate into the zeroed flat buffer (one add kernel per parameter)
+            self.flat_grad.zero_()
+            with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_bf16,
+                                cache_enabled=cache_casts):
+                loss = self.loss_fn(self.model(*batch))
+            loss.backward()
+            return loss.detach()
         for p in self.params:  # autograd then hands over fresh gradients (no accumulate kernels)
             p.grad = None
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_bf16,

@@ -16,7 +16,7 @@ def declared_symbols():
     names = set()
     for h in HEADERS:
         text = open(h).read()
-        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*((?:msda_hip|flat_adamw)_\w+)\s*\(", text,
+        names |= set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*((?:msda_hip|flat_adamw|mfl)_\w+)\s*\(", text,
                                 re.M))
     return sorted(names)
 

@@ -88,3 +88,15 @@ def test_bf16_shadow_is_bitwise_the_cast_and_expires(dev):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         y_new = lin(x)
     torch.testing.assert_close(y_new.float(), (x @ (lin.weight.t())).float() + lin.bias, rtol=2e-2, atol=5e-2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,N,dtype", [(15360, 512, torch.bfloat16), (800, 128, torch.bfloat16),
+                                       (15360, 2048, torch.float16), (37, 8, torch.bfloat16), (0, 64, torch.bfloat16)])
+def test_bias_grad_column_sum(dev, K, N, dtype):
+    """mfl_colsum (the Linear's bias gradient): fp32 column sums of a 16-bit (K, N) matrix vs fp64."""
+    g = torch.randn(K, N, device=dev).to(dtype)
+    out = linear_mod._bias_grad(g)
+    ref = g.double().sum(0)
+    assert out.dtype == torch.float32
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)

@@ -142,6 +142,33 @@ def test_graph_replay_matches_eager_step(dev, bf16):
 
 
 @pytest.mark.gpu
+def test_graph_steps_track_eager_steps_at_bench_shape(dev):
+    """Five graph-replayed steps at the bench shape (configs[1], bf16) follow five eager steps
+    from the same initial weights, with allocating device work (norms, maxima) between the
+    replays.  With the HIP runtime's graph packet capture on, this sequence corrupted the
+    second replay's gradients (inf / NaN); the package turns it off (__init__.py)."""
+    assert os.environ.get("DEBUG_CLR_GRAPH_PACKET_CAPTURE") == "0"
+    torch.manual_seed(0)
+    base = PKG.dvc_core.DeformableDVCCore(d_model=512, num_queries=100, dropout=0.0)
+    batch = PKG.dvc_core.synthetic_clips(8, T=1024, seed=1000, device=dev)
+    mk = lambda graph: PKG.train_step.FlatGradTrainer(  # noqa: E731
+        copy.deepcopy(base).to(dev), PKG.dvc_core.workload_loss, lr=1e-4, weight_decay=1e-4, max_norm=0.1,
+        use_bf16=True, graph=graph)
+    tg, te = mk(True), mk(False)
+    tg.capture(batch)
+    for _ in range(3):  # capture() ran three eager warm-up steps: same starting point
+        te.step(batch)
+    for i in range(5):
+        lg = tg.step(batch).item()
+        gnorm_g = tg.flat_grad.norm().item()  # allocating eager work between replays
+        assert bool(torch.isfinite(tg.flat_param).all()) and gnorm_g == gnorm_g, i
+        le = te.step(batch).item()
+        gnorm_e = te.flat_grad.norm().item()
+        assert abs(lg - le) <= 1e-2 * abs(le) + 1.0, (i, lg, le)
+        assert abs(gnorm_g - gnorm_e) <= 1e-2 * gnorm_e, (i, gnorm_g, gnorm_e)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("config", ["multimodal", "sparse"])
 def test_other_dvc_cores_train_one_step(config):
     """configs[2] (video + audio) and the Sparse-DETR DVC: one bf16 training step through the
