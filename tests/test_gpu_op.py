@@ -182,13 +182,15 @@ def test_gradcheck_fp64(dev, channels):
         assert torch.autograd.gradcheck(f, inputs, eps=1e-6, atol=1e-5, rtol=1e-4)
 
 
-def test_full_size_properties(dev):
-    """At the bench's size (B=8, T=1024 encoder call) where the oracle is too slow to run
-    whole: linearity in value and in aw, the adjoint identity <g, fwd(v)> = <bwd_value(g), v>,
-    and the grad_value checksum
+@pytest.mark.parametrize("shapes,B", [([1024, 512, 256, 128], 8),     # configs[1] encoder call (fused backward)
+                                      ([4096, 2048, 1024, 512], 2)])  # configs[3]: S = 7680 (sort + pull)
+def test_full_size_properties(dev, shapes, B):
+    """At full encoder-call sizes (the bench's B=8, T=1024; and T=4096, S=7680) where the oracle
+    is too slow to run whole: linearity in value and in aw, the adjoint identity
+    <g, fwd(v)> = <bwd_value(g), v>, and the grad_value checksum
     sum_s grad_value[b,s,m,:] = sum_q (sum_{l,p} aw[b,q,m,l,p]) grad_out[b,q,m,:] (border
     weights of a sample sum to 1); plus oracle parity on one clip."""
-    shapes, B, M, D, P = [1024, 512, 256, 128], 8, 8, 64, 4
+    M, D, P = 8, 64, 4
     Lq = sum(shapes)
     v1, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.float32, seed=11, lo=0.0, hi=1.0)
     v2 = torch.randn_like(v1)
