@@ -26,7 +26,7 @@ from torch.nn.init import constant_, xavier_uniform_
 from ... import msda as _msda
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
-from .linear import Linear
+from .linear import Linear, linear_pair
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn"]
 
@@ -130,8 +130,10 @@ class MSDeformAttn(nn.Module):
             value = value.masked_fill(input_padding_mask[..., None], float(0))
         value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
 
-        sampling_offsets = self.sampling_offsets(query).view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
-        attention_weights = self.attention_weights(query).view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
+        # one input cast and one fused backward for the two query projections
+        sampling_offsets, attention_weights = linear_pair(query, self.sampling_offsets, self.attention_weights)
+        sampling_offsets = sampling_offsets.view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
+        attention_weights = attention_weights.view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
         if (query.is_cuda and reference_points.shape[-1] in (1, 2)
                 and attention_weights.dtype == sampling_offsets.dtype
                 and _msda.prologue_supported(self.n_heads, self.n_levels, self.n_points)):

@@ -22,7 +22,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-__all__ = ["Linear", "split_k_chunks"]
+__all__ = ["Linear", "split_k_chunks", "linear_pair"]
 
 
 def split_k_chunks(k, min_chunk=1024, max_split=8):
@@ -99,8 +99,75 @@ class _AutocastLinear(torch.autograd.Function):
         return gx, gw, gb, None, None
 
 
+class _AutocastLinearPair(torch.autograd.Function):
+    """(x A^T + a, x B^T + b) of ONE 16-bit input: two forward GEMMs on the shared cast, and a
+    backward on the concatenated output gradient — one dgrad GEMM (no second input-gradient
+    cast and add), one split-K weight-gradient GEMM and one column sum for both layers."""
+
+    @staticmethod
+    def forward(ctx, x, wa, ba, wb, bb, wca, bca, wcb, bcb):
+        dt = x.dtype
+        wca = wa.to(dt) if wca is None else wca
+        wcb = wb.to(dt) if wcb is None else wcb
+        x2 = x.reshape(-1, x.shape[-1])
+        ya = torch.addmm(ba.to(dt) if bca is None else bca, x2, wca.t())
+        yb = torch.addmm(bb.to(dt) if bcb is None else bcb, x2, wcb.t())
+        ctx.save_for_backward(x2, wca, wcb)
+        ctx.x_shape = x.shape
+        lead = x.shape[:-1]
+        return ya.view(*lead, wca.shape[0]), yb.view(*lead, wcb.shape[0])
+
+    @staticmethod
+    def backward(ctx, gya, gyb):
+        x2, wca, wcb = ctx.saved_tensors
+        na, nb = wca.shape[0], wcb.shape[0]
+        k = x2.shape[0]
+        ga = gya.reshape(k, na).to(wca.dtype) if gya is not None else x2.new_zeros(k, na)
+        gb_ = gyb.reshape(k, nb).to(wca.dtype) if gyb is not None else x2.new_zeros(k, nb)
+        g2 = torch.cat((ga, gb_), 1)
+        nig = ctx.needs_input_grad
+        gx = torch.mm(g2, torch.cat((wca, wcb), 0)).view(ctx.x_shape) if nig[0] else None
+        gwa = gwb = gba = gbb = None
+        if nig[1] or nig[3]:
+            gw = _weight_grad(g2, x2)
+            gwa, gwb = gw[:na], gw[na:]
+        if nig[2] or nig[4]:
+            gbias = _bias_grad(g2)
+            gba, gbb = gbias[:na], gbias[na:]
+        return gx, gwa, gba, gwb, gbb, None, None, None, None
+
+
+def linear_pair(x, a, b):
+    """``(a(x), b(x))`` for two Linear layers with biases that read the same input (the
+    ``sampling_offsets`` / ``attention_weights`` projections of MSDeformAttn,
+    attention.py:468-470).  Under 16-bit autocast on the GPU: one input cast and a fused
+    backward (_AutocastLinearPair); elsewhere the two layers as they are."""
+    if not (isinstance(a, Linear) and isinstance(b, Linear) and a.bias is not None and b.bias is not None
+            and a._autocast_dtype(x) is not None):
+        return a(x), b(x)
+    dt = a._autocast_dtype(x)
+    wca, bca = a._low(dt)
+    wcb, bcb = b._low(dt)
+    with torch.autocast("cuda", enabled=False):
+        return _AutocastLinearPair.apply(x.to(dt), a.weight, a.bias, b.weight, b.bias, wca, bca, wcb, bcb)
+
+
 class Linear(nn.Linear):
     _shadow = None  # (weight copy, bias copy, weight version) set by set_bf16_shadow
+
+    def _autocast_dtype(self, x):
+        """The 16-bit autocast dtype this layer computes in for input x, or None (F.linear)."""
+        if (x.is_cuda and torch.is_autocast_enabled("cuda") and self.weight.dtype == torch.float32
+                and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16)):
+            return torch.get_autocast_dtype("cuda")
+        return None
+
+    def _low(self, dt):
+        """(weight, bias) 16-bit copies from the trainer's shadow while it is current, else None."""
+        sh = self._shadow
+        if sh is not None and dt == torch.bfloat16 and sh[2] == self.weight._version:
+            return sh[0], sh[1]
+        return None, None
 
     def set_bf16_shadow(self, weight_bf16, bias_bf16):
         """Use these bf16 copies of weight / bias under bf16 autocast for as long as the fp32

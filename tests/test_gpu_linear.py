@@ -100,3 +100,35 @@ def test_bias_grad_column_sum(dev, K, N, dtype):
     ref = g.double().sum(0)
     assert out.dtype == torch.float32
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tokens", [15360, 800, 7])
+@pytest.mark.parametrize("shadow", [False, True])
+def test_linear_pair_matches_two_linears(dev, tokens, shadow):
+    """linear_pair (the MSDA query projections: one input cast, one fused backward) gives the
+    two layers' outputs and the same gradients as calling them one after the other; with the
+    trainer's bf16 shadow too.  The input gradient sums the two layers' contributions inside
+    one GEMM instead of adding two bf16 products, so it agrees to bf16 rounding."""
+    torch.manual_seed(1)
+    a, b = linear_mod.Linear(512, 128).to(dev), linear_mod.Linear(512, 128).to(dev)
+    a2, b2 = linear_mod.Linear(512, 128).to(dev), linear_mod.Linear(512, 128).to(dev)
+    a2.load_state_dict(a.state_dict())
+    b2.load_state_dict(b.state_dict())
+    if shadow:
+        for m in (a, b, a2, b2):
+            m.set_bf16_shadow(m.weight.detach().to(torch.bfloat16), m.bias.detach().to(torch.bfloat16))
+    x = torch.randn(2, tokens // 2 if tokens > 7 else tokens, 512, device=dev)
+    x1, x2 = x.clone().requires_grad_(True), x.clone().requires_grad_(True)
+    ga, gb = torch.randn(*x.shape[:-1], 128, device=dev), torch.randn(*x.shape[:-1], 128, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        ya, yb = linear_mod.linear_pair(x1, a, b)
+        za, zb = a2(x2), b2(x2)
+    torch.testing.assert_close(ya, za, rtol=0, atol=0)
+    torch.testing.assert_close(yb, zb, rtol=0, atol=0)
+    ((ya.float() * ga).sum() + (yb.float() * gb).sum()).backward()
+    ((za.float() * ga).sum() + (zb.float() * gb).sum()).backward()
+    for p, q in ((a.weight, a2.weight), (a.bias, a2.bias), (b.weight, b2.weight), (b.bias, b2.bias)):
+        assert p.grad.dtype == torch.float32
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-5 * q.grad.abs().max().item())
+    torch.testing.assert_close(x1.grad, x2.grad, rtol=2e-2, atol=2e-2 * x2.grad.abs().max().item())
