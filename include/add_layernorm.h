@@ -1,0 +1,45 @@
+/*
+ * add_layernorm.h — C-ABI of the fused residual add + LayerNorm of the deformable transformer
+ * layers (multimodal-feature-learning_amd/csrc/add_layernorm.hip, built into libmsda_hip.so).
+ *
+ * Replaces, under bf16 autocast, `norm(x + dropout(y))` of the reference's encoder / decoder
+ * layers (models/deformable/unimodal_deformable_transformer.py:238-249, 362-373;
+ * multimodal_deformable_transformer.py and sparse/unimodal_sparse_deformable_transformer.py:
+ * the same pattern): ATen's fp32 add, layer_norm forward, layer_norm backward (input and
+ * gamma/beta kernels) and the cast of the branch gradient.
+ *
+ * Rows of d elements, row-major, contiguous.  r (residual) and y (branch) are fp32 (tag 0) or
+ * bf16 (tag 2); gamma, beta, out, mean, rstd, dout, dgamma, dbeta are fp32.  d % 256 == 0 and
+ * d <= 1024.  All calls are asynchronous on `stream` and return 0, or non-zero with
+ * mfl_add_layernorm_last_error().
+ */
+#ifndef MFL_ADD_LAYERNORM_H
+#define MFL_ADD_LAYERNORM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Scratch bytes of mfl_add_layernorm_backward (gamma / beta partials). */
+size_t mfl_add_layernorm_workspace_bytes(int64_t rows, int64_t d);
+
+/* out = LayerNorm(r + y) * gamma + beta (eps as nn.LayerNorm); mean / rstd per row for the backward. */
+int mfl_add_layernorm_forward(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,
+                              const float* beta, int64_t rows, int64_t d, float eps, float* out, float* mean,
+                              float* rstd, void* stream);
+
+/* dr (r's dtype) and dy (y's dtype) = d out / d (r + y); dgamma, dbeta summed over rows. */
+int mfl_add_layernorm_backward(const float* dout, const void* r, int r_dtype, const void* y, int y_dtype,
+                               const float* gamma, const float* mean, const float* rstd, int64_t rows, int64_t d,
+                               void* dr, void* dy, float* dgamma, float* dbeta, void* workspace, void* stream);
+
+const char* mfl_add_layernorm_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MFL_ADD_LAYERNORM_H */

@@ -36,6 +36,11 @@ EXPORTED_SYMBOLS = (
     "flat_adamw_last_error",
     "mfl_colsum_workspace_bytes",
     "mfl_colsum",
+    # include/add_layernorm.h
+    "mfl_add_layernorm_workspace_bytes",
+    "mfl_add_layernorm_forward",
+    "mfl_add_layernorm_backward",
+    "mfl_add_layernorm_last_error",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -71,6 +76,14 @@ def _declare(lib):
     lib.mfl_colsum_workspace_bytes.argtypes = [i64, i64]
     lib.mfl_colsum.restype = i32
     lib.mfl_colsum.argtypes = [vp, i32, i64, i64, vp, vp, vp]
+    lib.mfl_add_layernorm_workspace_bytes.restype = ctypes.c_size_t
+    lib.mfl_add_layernorm_workspace_bytes.argtypes = [i64, i64]
+    lib.mfl_add_layernorm_forward.restype = i32
+    lib.mfl_add_layernorm_forward.argtypes = [vp, i32, vp, i32, vp, vp, i64, i64, f32, vp, vp, vp, vp]
+    lib.mfl_add_layernorm_backward.restype = i32
+    lib.mfl_add_layernorm_backward.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, vp, vp, vp, vp, vp]
+    lib.mfl_add_layernorm_last_error.restype = ctypes.c_char_p
+    lib.mfl_add_layernorm_last_error.argtypes = []
     lib.flat_adamw_last_error.restype = ctypes.c_char_p
     lib.flat_adamw_last_error.argtypes = []
     lib.msda_hip_last_error.restype = ctypes.c_char_p

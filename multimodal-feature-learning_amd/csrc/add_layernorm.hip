@@ -1,0 +1,313 @@
+// Residual add + LayerNorm of the deformable transformer layers, forward and backward
+// (reference unimodal_deformable_transformer.py:238-249 / 362-373: norm(x + dropout(y)), and the
+// same pattern in the multimodal and sparse layers).  Under bf16 autocast the reference runs an
+// fp32 add of the residual stream and the 16-bit branch output, then an fp32 LayerNorm; the
+// backward is LayerNorm's input-gradient and gamma/beta kernels plus a cast of the gradient back
+// to the branch's 16-bit dtype.  Here:
+//   forward : z = r + y and out = (z - mean) * rstd * gamma + beta in one pass; mean / rstd kept;
+//   backward: dz from (dout, z recomputed from r and y), written once as dr (r's dtype) and dy
+//             (y's dtype); per-block gamma / beta partials, summed by a second small kernel.
+// One wave per row, d % 256 == 0 and d <= 1024 (4 consecutive elements per lane per 256-wide
+// chunk): the row stays in registers between the statistics and the output.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/add_layernorm.h"
+
+namespace {
+
+thread_local char g_err[256];
+
+constexpr int kWaves = 4;     // rows in flight per block (one per wave)
+constexpr int kBwdRows = 16;  // rows per backward block (kWaves waves x 4 rows): gamma/beta partials
+
+template <typename T> struct Vec4;
+template <> struct Vec4<float> {
+  __device__ static void load(const float* p, float (&v)[4]) {
+    const float4 x = *reinterpret_cast<const float4*>(p);
+    v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+  }
+  __device__ static void store(float* p, const float (&v)[4]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+template <> struct Vec4<uint16_t> {  // bf16
+  __device__ static void load(const uint16_t* p, float (&v)[4]) {
+    const uint2 x = *reinterpret_cast<const uint2*>(p);
+    v[0] = __uint_as_float(x.x << 16); v[1] = __uint_as_float(x.x & 0xffff0000u);
+    v[2] = __uint_as_float(x.y << 16); v[3] = __uint_as_float(x.y & 0xffff0000u);
+  }
+  __device__ static uint32_t rne(float f) {  // round to nearest even, NaN kept quiet
+    const uint32_t u = __float_as_uint(f);
+    if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+  }
+  __device__ static void store(uint16_t* p, const float (&v)[4]) {
+    *reinterpret_cast<uint2*>(p) = make_uint2(rne(v[0]) | (rne(v[1]) << 16), rne(v[2]) | (rne(v[3]) << 16));
+  }
+};
+
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+template <typename RT, typename YT, int CH>
+__global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__ r, const YT* __restrict__ y,
+                                                         const float* __restrict__ gamma,
+                                                         const float* __restrict__ beta, long long rows, int d,
+                                                         float eps, float* __restrict__ out,
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const long long row = (long long)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;  // wave-uniform
+  const long long base = row * d;
+  float z[CH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = c * 256 + lane * 4;
+    float a[4], b[4];
+    Vec4<RT>::load(r + base + col, a);
+    Vec4<YT>::load(y + base + col, b);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      z[c][k] = a[k] + b[k];
+      s += z[c][k];
+    }
+  }
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float t = z[c][k] - mean;
+      q += t * t;
+    }
+  const float rstd = rsqrtf(wave_sum(q) / (float)d + eps);
+#pragma unroll
+  for (int c = 0; c < CH; ++c) {
+    const int col = c * 256 + lane * 4;
+    float g[4], bb[4], o[4];
+    Vec4<float>::load(gamma + col, g);
+    Vec4<float>::load(beta + col, bb);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) o[k] = (z[c][k] - mean) * rstd * g[k] + bb[k];
+    Vec4<float>::store(out + base + col, o);
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+template <typename RT, typename YT, int CH>
+__global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
+    const float* __restrict__ dout, const RT* __restrict__ r, const YT* __restrict__ y,
+    const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+    long long rows, int d, RT* __restrict__ dr, YT* __restrict__ dy, float* __restrict__ part) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float dg[CH][4], db[CH][4];
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dg[c][k] = db[c][k] = 0.f;
+  for (int i = 0; i < kBwdRows / kWaves; ++i) {
+    const long long row = (long long)blockIdx.x * kBwdRows + i * kWaves + wave;
+    if (row >= rows) break;  // wave-uniform
+    const long long base = row * d;
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[CH][4], g[CH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = c * 256 + lane * 4;
+      float a[4], b[4], go[4], ga[4];
+      Vec4<RT>::load(r + base + col, a);
+      Vec4<YT>::load(y + base + col, b);
+      Vec4<float>::load(dout + base + col, go);
+      Vec4<float>::load(gamma + col, ga);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        xh[c][k] = (a[k] + b[k] - mean) * rstd;
+        g[c][k] = go[k] * ga[k];
+        s1 += g[c][k];
+        s2 += g[c][k] * xh[c][k];
+        dg[c][k] += go[k] * xh[c][k];
+        db[c][k] += go[k];
+      }
+    }
+    const float m1 = wave_sum(s1) / (float)d, m2 = wave_sum(s2) / (float)d;
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int col = c * 256 + lane * 4;
+      float dx[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dx[k] = rstd * (g[c][k] - m1 - xh[c][k] * m2);
+      Vec4<RT>::store(dr + base + col, dx);
+      Vec4<YT>::store(dy + base + col, dx);
+    }
+  }
+  // gamma / beta partials of the block: waves meet in LDS, fixed order
+  __shared__ float red[kWaves][2][CH * 256];
+#pragma unroll
+  for (int c = 0; c < CH; ++c)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[wave][0][c * 256 + lane * 4 + k] = dg[c][k];
+      red[wave][1][c * 256 + lane * 4 + k] = db[c][k];
+    }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 2 * d; j += kWaves * 64) {
+    const int which = j / d, col = j - which * d;
+    float t = 0.f;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) t += red[w][which][col];
+    part[(long long)blockIdx.x * 2 * d + j] = t;
+  }
+}
+
+// dgamma / dbeta = sum over the backward blocks' partials (16 groups x 64 columns per block)
+__global__ __launch_bounds__(1024) void add_ln_param_final(const float* __restrict__ part, int nblk, int d2,
+                                                          float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red[16][64];
+  const int c_l = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + c_l;
+  float s = 0.f;
+  if (c < d2)
+    for (int k = grp; k < nblk; k += 16) s += part[(long long)k * d2 + c];
+  red[grp][c_l] = s;
+  __syncthreads();
+  if (grp == 0 && c < d2) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][c_l];
+    const int half = d2 / 2;
+    if (c < half) dgamma[c] = t; else dbeta[c - half] = t;
+  }
+}
+
+int status(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "add_layernorm: %s launch failed: %s", what, hipGetErrorString(e));
+    return 2;
+  }
+  return 0;
+}
+
+bool shape_ok(int64_t rows, int64_t d) { return rows >= 0 && d > 0 && d % 256 == 0 && d <= 1024; }
+
+#define MFL_ALN_FWD(CHN)                                                                                   \
+  hipLaunchKernelGGL((add_ln_fwd<RT, YT, CHN>), dim3(blocks), dim3(kWaves * 64), 0, st, rp, yp, gamma, beta, \
+                     (long long)rows, (int)d, eps, out, mean, rstd)
+
+template <typename RT, typename YT>
+int fwd(const void* r, const void* y, const float* gamma, const float* beta, int64_t rows, int64_t d, float eps,
+        float* out, float* mean, float* rstd, hipStream_t st) {
+  const unsigned blocks = (unsigned)((rows + kWaves - 1) / kWaves);
+  auto* rp = static_cast<const RT*>(r);
+  auto* yp = static_cast<const YT*>(y);
+  switch (d / 256) {
+    case 1: MFL_ALN_FWD(1); break;
+    case 2: MFL_ALN_FWD(2); break;
+    case 3: MFL_ALN_FWD(3); break;
+    default: MFL_ALN_FWD(4); break;
+  }
+  return status("forward");
+}
+#undef MFL_ALN_FWD
+
+#define MFL_ALN_BWD(CHN)                                                                                   \
+  hipLaunchKernelGGL((add_ln_bwd<RT, YT, CHN>), dim3(blocks), dim3(kWaves * 64), 0, st, dout, rp, yp, gamma, \
+                     mean, rstd, (long long)rows, (int)d, drp, dyp, part)
+
+template <typename RT, typename YT>
+int bwd(const float* dout, const void* r, const void* y, const float* gamma, const float* mean, const float* rstd,
+        int64_t rows, int64_t d, void* dr, void* dy, float* dgamma, float* dbeta, void* workspace, hipStream_t st) {
+  const unsigned blocks = (unsigned)((rows + kBwdRows - 1) / kBwdRows);
+  auto* rp = static_cast<const RT*>(r);
+  auto* yp = static_cast<const YT*>(y);
+  auto* drp = static_cast<RT*>(dr);
+  auto* dyp = static_cast<YT*>(dy);
+  auto* part = static_cast<float*>(workspace);
+  switch (d / 256) {
+    case 1: MFL_ALN_BWD(1); break;
+    case 2: MFL_ALN_BWD(2); break;
+    case 3: MFL_ALN_BWD(3); break;
+    default: MFL_ALN_BWD(4); break;
+  }
+  int rc;
+  if ((rc = status("backward"))) return rc;
+  const int d2 = (int)(2 * d);
+  hipLaunchKernelGGL(add_ln_param_final, dim3((unsigned)((d2 + 63) / 64)), dim3(1024), 0, st, part, (int)blocks, d2,
+                     dgamma, dbeta);
+  return status("backward params");
+}
+#undef MFL_ALN_BWD
+
+}  // namespace
+
+extern "C" {
+
+size_t mfl_add_layernorm_workspace_bytes(int64_t rows, int64_t d) {
+  if (rows <= 0 || d <= 0) return 0;
+  return (size_t)((rows + kBwdRows - 1) / kBwdRows) * 2 * (size_t)d * sizeof(float);
+}
+
+int mfl_add_layernorm_forward(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,
+                              const float* beta, int64_t rows, int64_t d, float eps, float* out, float* mean,
+                              float* rstd, void* stream) {
+  g_err[0] = 0;
+  if (!shape_ok(rows, d) || (r_dtype != 0 && r_dtype != 2) || (y_dtype != 0 && y_dtype != 2)) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_forward: needs d %% 256 == 0, d <= 1024, fp32/bf16 inputs");
+    return 1;
+  }
+  if (rows == 0) return 0;
+  if (!r || !y || !gamma || !beta || !out || !mean || !rstd) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_forward: null pointer");
+    return 1;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (r_dtype == 0)
+    return y_dtype == 0 ? fwd<float, float>(r, y, gamma, beta, rows, d, eps, out, mean, rstd, st)
+                        : fwd<float, uint16_t>(r, y, gamma, beta, rows, d, eps, out, mean, rstd, st);
+  return y_dtype == 0 ? fwd<uint16_t, float>(r, y, gamma, beta, rows, d, eps, out, mean, rstd, st)
+                      : fwd<uint16_t, uint16_t>(r, y, gamma, beta, rows, d, eps, out, mean, rstd, st);
+}
+
+int mfl_add_layernorm_backward(const float* dout, const void* r, int r_dtype, const void* y, int y_dtype,
+                               const float* gamma, const float* mean, const float* rstd, int64_t rows, int64_t d,
+                               void* dr, void* dy, float* dgamma, float* dbeta, void* workspace, void* stream) {
+  g_err[0] = 0;
+  if (!shape_ok(rows, d) || (r_dtype != 0 && r_dtype != 2) || (y_dtype != 0 && y_dtype != 2)) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: needs d %% 256 == 0, d <= 1024, fp32/bf16 inputs");
+    return 1;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (rows == 0) {
+    if (hipMemsetAsync(dgamma, 0, (size_t)d * 4, st) != hipSuccess ||
+        hipMemsetAsync(dbeta, 0, (size_t)d * 4, st) != hipSuccess)
+      return 2;
+    return 0;
+  }
+  if (!dout || !r || !y || !gamma || !mean || !rstd || !dr || !dy || !dgamma || !dbeta || !workspace) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: null pointer");
+    return 1;
+  }
+  if (r_dtype == 0)
+    return y_dtype == 0
+               ? bwd<float, float>(dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, st)
+               : bwd<float, uint16_t>(dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, st);
+  return y_dtype == 0
+             ? bwd<uint16_t, float>(dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, st)
+             : bwd<uint16_t, uint16_t>(dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, st);
+}
+
+const char* mfl_add_layernorm_last_error(void) { return g_err; }
+
+}  // extern "C"

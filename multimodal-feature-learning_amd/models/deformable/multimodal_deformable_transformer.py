@@ -16,6 +16,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..modules.attention import MSDeformAttn
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
+from ..modules.add_norm import add_layer_norm
 from .unimodal_deformable_transformer import (_get_activation_fn, _get_clones, encoder_reference_points,
                                               level_metadata)
 
@@ -132,11 +133,11 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src):
         hidden = self.dropout2(self.activation(self.linear1(src)))
-        return self.norm2(src + self.dropout3(self.linear2(hidden)))
+        return add_layer_norm(src, self.dropout3(self.linear2(hidden)), self.norm2)
 
     def _self_block(self, src, pos, ref, shapes, starts, mask):
         attn = self.self_attn(self.with_pos_embed(src, pos), ref, src, shapes, starts, mask)
-        return self.norm1(src + self.dropout1(attn))
+        return add_layer_norm(src, self.dropout1(attn), self.norm1)
 
     def forward(self, video_src, video_pos, video_reference_points, video_temporal_shapes, video_level_start_index,
                 video_padding_mask, audio_src, audio_pos, audio_reference_points, audio_temporal_shapes,
@@ -205,18 +206,18 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
 
     def forward_ffn(self, tgt):
         hidden = self.dropout3(self.activation(self.linear1(tgt)))
-        return self.norm3(tgt + self.dropout4(self.linear2(hidden)))
+        return add_layer_norm(tgt, self.dropout4(self.linear2(hidden)), self.norm3)
 
     def _cross_block(self, tgt, query_pos, ref, src, shapes, starts, mask):
         attn = self.cross_attn(self.with_pos_embed(tgt, query_pos), ref, src, shapes, starts, mask)
-        return self.norm1(tgt + self.dropout1(attn))
+        return add_layer_norm(tgt, self.dropout1(attn), self.norm1)
 
     def forward(self, tgt, query_pos, reference_points_input_video, reference_points_input_audio, query_mask,
                 video_src, video_temporal_shapes, video_level_start_index, video_src_padding_mask, audio_src,
                 audio_temporal_shapes, audio_level_start_index, audio_src_padding_mask):
         qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
         sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
-        tgt = self.norm2(tgt + self.dropout2(sa))
+        tgt = add_layer_norm(tgt, self.dropout2(sa), self.norm2)
         tgt_video = self._cross_block(tgt, query_pos, reference_points_input_video, video_src, video_temporal_shapes,
                                       video_level_start_index, video_src_padding_mask)
         tgt_audio = self._cross_block(tgt, query_pos, reference_points_input_audio, audio_src, audio_temporal_shapes,

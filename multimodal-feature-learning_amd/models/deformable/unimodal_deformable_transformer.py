@@ -19,6 +19,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..modules.attention import MSDeformAttn
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
+from ..modules.add_norm import add_layer_norm
 
 __all__ = [
     "DeformableTransformer", "DeformableTransformerEncoderLayer", "DeformableTransformerEncoder",
@@ -185,12 +186,12 @@ class DeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src):
         hidden = self.dropout2(self.activation(self.linear1(src)))
-        return self.norm2(src + self.dropout3(self.linear2(hidden)))
+        return add_layer_norm(src, self.dropout3(self.linear2(hidden)), self.norm2)
 
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None):
         attn = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, temporal_shapes,
                               level_start_index, padding_mask)
-        src = self.norm1(src + self.dropout1(attn))
+        src = add_layer_norm(src, self.dropout1(attn), self.norm1)
         return self.forward_ffn(src)
 
 
@@ -241,16 +242,16 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward_ffn(self, tgt):
         hidden = self.dropout3(self.activation(self.linear1(tgt)))
-        return self.norm3(tgt + self.dropout4(self.linear2(hidden)))
+        return add_layer_norm(tgt, self.dropout4(self.linear2(hidden)), self.norm3)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None):
         qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
         sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
-        tgt = self.norm2(tgt + self.dropout2(sa))
+        tgt = add_layer_norm(tgt, self.dropout2(sa), self.norm2)
         ca = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_temporal_shapes,
                              level_start_index, src_padding_mask)
-        tgt = self.norm1(tgt + self.dropout1(ca))
+        tgt = add_layer_norm(tgt, self.dropout1(ca), self.norm1)
         return self.forward_ffn(tgt)
 
 

@@ -24,6 +24,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..deformable.unimodal_deformable_transformer import encoder_reference_points, level_metadata
 from ..modules.attention import MSDeformAttn
 from ..modules.linear import Linear
+from ..modules.add_norm import add_layer_norm
 from ..modules.misc_modules import inverse_sigmoid
 
 __all__ = [
@@ -187,14 +188,14 @@ class DeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src):
         hidden = self.dropout2(self.activation(self.linear1(src)))
-        return self.norm2(src + self.dropout3(self.linear2(hidden)))
+        return add_layer_norm(src, self.dropout3(self.linear2(hidden)), self.norm2)
 
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None, tgt=None):
         query = src if tgt is None else tgt
         attn, sampling_locations, attn_weights = self.self_attn(
             self.with_pos_embed(query, pos), reference_points, src, temporal_shapes, level_start_index, padding_mask,
             is_sparse=True)
-        out = self.norm1(query + self.dropout1(attn))
+        out = add_layer_norm(query, self.dropout1(attn), self.norm1)
         return self.forward_ffn(out), sampling_locations, attn_weights
 
 
@@ -288,17 +289,17 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward_ffn(self, tgt):
         hidden = self.dropout3(self.activation(self.linear1(tgt)))
-        return self.norm3(tgt + self.dropout4(self.linear2(hidden)))
+        return add_layer_norm(tgt, self.dropout4(self.linear2(hidden)), self.norm3)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None):
         qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
         sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
-        tgt = self.norm2(tgt + self.dropout2(sa))
+        tgt = add_layer_norm(tgt, self.dropout2(sa), self.norm2)
         ca, sampling_locations, attn_weights = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points,
                                                                src, src_temporal_shapes, level_start_index,
                                                                src_padding_mask, is_sparse=True)
-        tgt = self.norm1(tgt + self.dropout1(ca))
+        tgt = add_layer_norm(tgt, self.dropout1(ca), self.norm1)
         return self.forward_ffn(tgt), sampling_locations, attn_weights
 
 

@@ -1,5 +1,5 @@
-"""The C-ABI library: loads without a GPU, exports every symbol include/msda_hip.h and
-include/flat_adamw.h declare, and rejects bad arguments with a status + message before
+"""The C-ABI library: loads without a GPU, exports every symbol include/msda_hip.h,
+include/flat_adamw.h and include/add_layernorm.h declare, and rejects bad arguments with a status + message before
 touching a device."""
 import ctypes
 import os
@@ -9,7 +9,7 @@ import pytest
 
 from conftest import PKG, ROOT
 
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("msda_hip.h", "flat_adamw.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("msda_hip.h", "flat_adamw.h", "add_layernorm.h")]
 
 
 def declared_symbols():
