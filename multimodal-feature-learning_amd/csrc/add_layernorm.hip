@@ -60,7 +60,9 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__
                                                          const float* __restrict__ gamma,
                                                          const float* __restrict__ beta, long long rows, int d,
                                                          float eps, float* __restrict__ out,
-                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+                                                         float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                         uint16_t* __restrict__ out16, const float* __restrict__ pos,
+                                                         uint16_t* __restrict__ q16) {
   const int lane = threadIdx.x & 63;
   const long long row = (long long)blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (row >= rows) return;  // wave-uniform
@@ -98,6 +100,14 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__
 #pragma unroll
     for (int k = 0; k < 4; ++k) o[k] = (z[c][k] - mean) * rstd * g[k] + bb[k];
     Vec4<float>::store(out + base + col, o);
+    if (out16) Vec4<uint16_t>::store(out16 + base + col, o);  // the bf16 operand of the next GEMM
+    if (q16) {  // bf16(out + pos): the next MSDA query, rounded once from fp32 as autocast would
+      float p[4];
+      Vec4<float>::load(pos + base + col, p);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) p[k] += o[k];
+      Vec4<uint16_t>::store(q16 + base + col, p);
+    }
   }
   if (lane == 0) {
     mean_out[row] = mean;
@@ -109,7 +119,8 @@ template <typename RT, typename YT, int CH>
 __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
     const float* __restrict__ dout, const RT* __restrict__ r, const YT* __restrict__ y,
     const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-    long long rows, int d, RT* __restrict__ dr, YT* __restrict__ dy, float* __restrict__ part) {
+    long long rows, int d, RT* __restrict__ dr, YT* __restrict__ dy, float* __restrict__ part,
+    const uint16_t* __restrict__ dout16, const uint16_t* __restrict__ dq16, float* __restrict__ dpos) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   float dg[CH][4], db[CH][4];
 #pragma unroll
@@ -126,10 +137,24 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int col = c * 256 + lane * 4;
-      float a[4], b[4], go[4], ga[4];
+      float a[4], b[4], go[4] = {0.f, 0.f, 0.f, 0.f}, ga[4];
       Vec4<RT>::load(r + base + col, a);
       Vec4<YT>::load(y + base + col, b);
-      Vec4<float>::load(dout + base + col, go);
+      // d out = its fp32 gradient + the bf16 copy's + the (out + pos) copy's, summed in fp32
+      if (dout) Vec4<float>::load(dout + base + col, go);
+      if (dout16) {
+        float t[4];
+        Vec4<uint16_t>::load(dout16 + base + col, t);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) go[k] += t[k];
+      }
+      if (dq16) {
+        float t[4];
+        Vec4<uint16_t>::load(dq16 + base + col, t);
+        if (dpos) Vec4<float>::store(dpos + base + col, t);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) go[k] += t[k];
+      }
       Vec4<float>::load(gamma + col, ga);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -204,11 +229,11 @@ bool shape_ok(int64_t rows, int64_t d) { return rows >= 0 && d > 0 && d % 256 ==
 
 #define MFL_ALN_FWD(CHN)                                                                                   \
   hipLaunchKernelGGL((add_ln_fwd<RT, YT, CHN>), dim3(blocks), dim3(kWaves * 64), 0, st, rp, yp, gamma, beta, \
-                     (long long)rows, (int)d, eps, out, mean, rstd)
+                     (long long)rows, (int)d, eps, out, mean, rstd, out16, pos, q16)
 
 template <typename RT, typename YT>
 int fwd(const void* r, const void* y, const float* gamma, const float* beta, int64_t rows, int64_t d, float eps,
-        float* out, float* mean, float* rstd, hipStream_t st) {
+        float* out, float* mean, float* rstd, uint16_t* out16, const float* pos, uint16_t* q16, hipStream_t st) {
   const unsigned blocks = (unsigned)((rows + kWaves - 1) / kWaves);
   auto* rp = static_cast<const RT*>(r);
   auto* yp = static_cast<const YT*>(y);
@@ -224,11 +249,12 @@ int fwd(const void* r, const void* y, const float* gamma, const float* beta, int
 
 #define MFL_ALN_BWD(CHN)                                                                                   \
   hipLaunchKernelGGL((add_ln_bwd<RT, YT, CHN>), dim3(blocks), dim3(kWaves * 64), 0, st, dout, rp, yp, gamma, \
-                     mean, rstd, (long long)rows, (int)d, drp, dyp, part)
+                     mean, rstd, (long long)rows, (int)d, drp, dyp, part, dout16, dq16, dpos)
 
 template <typename RT, typename YT>
 int bwd(const float* dout, const void* r, const void* y, const float* gamma, const float* mean, const float* rstd,
-        int64_t rows, int64_t d, void* dr, void* dy, float* dgamma, float* dbeta, void* workspace, hipStream_t st) {
+        int64_t rows, int64_t d, void* dr, void* dy, float* dgamma, float* dbeta, void* workspace,
+        const uint16_t* dout16, const uint16_t* dq16, float* dpos, hipStream_t st) {
   const unsigned blocks = (unsigned)((rows + kBwdRows - 1) / kBwdRows);
   auto* rp = static_cast<const RT*>(r);
   auto* yp = static_cast<const YT*>(y);
@@ -259,30 +285,38 @@ size_t mfl_add_layernorm_workspace_bytes(int64_t rows, int64_t d) {
   return (size_t)((rows + kBwdRows - 1) / kBwdRows) * 2 * (size_t)d * sizeof(float);
 }
 
-int mfl_add_layernorm_forward(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,
-                              const float* beta, int64_t rows, int64_t d, float eps, float* out, float* mean,
-                              float* rstd, void* stream) {
+int mfl_add_layernorm_forward_ex(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,
+                                 const float* beta, int64_t rows, int64_t d, float eps, float* out, float* mean,
+                                 float* rstd, uint16_t* out16, const float* pos, uint16_t* q16, void* stream) {
   g_err[0] = 0;
   if (!shape_ok(rows, d) || (r_dtype != 0 && r_dtype != 2) || (y_dtype != 0 && y_dtype != 2)) {
     snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_forward: needs d %% 256 == 0, d <= 1024, fp32/bf16 inputs");
     return 1;
   }
   if (rows == 0) return 0;
-  if (!r || !y || !gamma || !beta || !out || !mean || !rstd) {
+  if (!r || !y || !gamma || !beta || !out || !mean || !rstd || (q16 && !pos)) {
     snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_forward: null pointer");
     return 1;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
+#define MFL_ALN_FWD_ARGS r, y, gamma, beta, rows, d, eps, out, mean, rstd, out16, pos, q16, st
   if (r_dtype == 0)
-    return y_dtype == 0 ? fwd<float, float>(r, y, gamma, beta, rows, d, eps, out, mean, rstd, st)
-                        : fwd<float, uint16_t>(r, y, gamma, beta, rows, d, eps, out, mean, rstd, st);
-  return y_dtype == 0 ? fwd<uint16_t, float>(r, y, gamma, beta, rows, d, eps, out, mean, rstd, st)
-                      : fwd<uint16_t, uint16_t>(r, y, gamma, beta, rows, d, eps, out, mean, rstd, st);
+    return y_dtype == 0 ? fwd<float, float>(MFL_ALN_FWD_ARGS) : fwd<float, uint16_t>(MFL_ALN_FWD_ARGS);
+  return y_dtype == 0 ? fwd<uint16_t, float>(MFL_ALN_FWD_ARGS) : fwd<uint16_t, uint16_t>(MFL_ALN_FWD_ARGS);
+#undef MFL_ALN_FWD_ARGS
 }
 
-int mfl_add_layernorm_backward(const float* dout, const void* r, int r_dtype, const void* y, int y_dtype,
-                               const float* gamma, const float* mean, const float* rstd, int64_t rows, int64_t d,
-                               void* dr, void* dy, float* dgamma, float* dbeta, void* workspace, void* stream) {
+int mfl_add_layernorm_forward(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,
+                              const float* beta, int64_t rows, int64_t d, float eps, float* out, float* mean,
+                              float* rstd, void* stream) {
+  return mfl_add_layernorm_forward_ex(r, r_dtype, y, y_dtype, gamma, beta, rows, d, eps, out, mean, rstd, nullptr,
+                                      nullptr, nullptr, stream);
+}
+
+int mfl_add_layernorm_backward_ex(const float* dout, const uint16_t* dout16, const uint16_t* dq16, const void* r,
+                                  int r_dtype, const void* y, int y_dtype, const float* gamma, const float* mean,
+                                  const float* rstd, int64_t rows, int64_t d, void* dr, void* dy, float* dgamma,
+                                  float* dbeta, float* dpos, void* workspace, void* stream) {
   g_err[0] = 0;
   if (!shape_ok(rows, d) || (r_dtype != 0 && r_dtype != 2) || (y_dtype != 0 && y_dtype != 2)) {
     snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: needs d %% 256 == 0, d <= 1024, fp32/bf16 inputs");
@@ -295,17 +329,28 @@ int mfl_add_layernorm_backward(const float* dout, const void* r, int r_dtype, co
       return 2;
     return 0;
   }
-  if (!dout || !r || !y || !gamma || !mean || !rstd || !dr || !dy || !dgamma || !dbeta || !workspace) {
+  if ((!dout && !dout16 && !dq16) || !r || !y || !gamma || !mean || !rstd || !dr || !dy || !dgamma || !dbeta ||
+      !workspace) {
     snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: null pointer");
     return 1;
   }
+#define MFL_ALN_BWD_ARGS dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, dout16, dq16, dpos, st
   if (r_dtype == 0)
-    return y_dtype == 0
-               ? bwd<float, float>(dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, st)
-               : bwd<float, uint16_t>(dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, st);
-  return y_dtype == 0
-             ? bwd<uint16_t, float>(dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, st)
-             : bwd<uint16_t, uint16_t>(dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, st);
+    return y_dtype == 0 ? bwd<float, float>(MFL_ALN_BWD_ARGS) : bwd<float, uint16_t>(MFL_ALN_BWD_ARGS);
+  return y_dtype == 0 ? bwd<uint16_t, float>(MFL_ALN_BWD_ARGS) : bwd<uint16_t, uint16_t>(MFL_ALN_BWD_ARGS);
+#undef MFL_ALN_BWD_ARGS
+}
+
+int mfl_add_layernorm_backward(const float* dout, const void* r, int r_dtype, const void* y, int y_dtype,
+                               const float* gamma, const float* mean, const float* rstd, int64_t rows, int64_t d,
+                               void* dr, void* dy, float* dgamma, float* dbeta, void* workspace, void* stream) {
+  if (!dout) {
+    g_err[0] = 0;
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: null pointer");
+    return 1;
+  }
+  return mfl_add_layernorm_backward_ex(dout, nullptr, nullptr, r, r_dtype, y, y_dtype, gamma, mean, rstd, rows, d, dr,
+                                       dy, dgamma, dbeta, nullptr, workspace, stream);
 }
 
 const char* mfl_add_layernorm_last_error(void) { return g_err; }

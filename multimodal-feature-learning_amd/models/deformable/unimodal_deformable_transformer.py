@@ -19,7 +19,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..modules.attention import MSDeformAttn
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
-from ..modules.add_norm import add_layer_norm
+from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 
 __all__ = [
     "DeformableTransformer", "DeformableTransformerEncoderLayer", "DeformableTransformerEncoder",
@@ -194,6 +194,17 @@ class DeformableTransformerEncoderLayer(nn.Module):
         src = add_layer_norm(src, self.dropout1(attn), self.norm1)
         return self.forward_ffn(src)
 
+    def forward_carry(self, src, value, query, next_pos, reference_points, temporal_shapes, level_start_index,
+                      padding_mask=None):
+        """``forward`` with the 16-bit operands carried between layers (bf16 autocast on the GPU):
+        ``value`` / ``query`` are this layer's MSDA inputs (``src`` and ``src + pos`` in bf16, or
+        the fp32 tensors themselves), and the fused add + LayerNorms hand back the next layer's
+        ``(src, value, query)`` (query = bf16(out + next_pos); None when next_pos is None)."""
+        attn = self.self_attn(query, reference_points, value, temporal_shapes, level_start_index, padding_mask)
+        src, src16, _ = add_layer_norm_carry(src, self.dropout1(attn), self.norm1)
+        hidden = self.dropout2(self.activation(self.linear1(src16)))
+        return add_layer_norm_carry(src, self.dropout3(self.linear2(hidden)), self.norm2, next_pos)
+
 
 class DeformableTransformerEncoder(nn.Module):
     """Stack of encoder layers sharing one set of reference points (reference :252-295)."""
@@ -210,6 +221,18 @@ class DeformableTransformerEncoder(nn.Module):
     def forward(self, src, temporal_shapes, level_start_index, valid_ratios, pos=None, padding_mask=None):
         reference_points = self.get_reference_points(temporal_shapes, valid_ratios, device=src.device)
         out = src
+        if (self.layers and all(type(layer) is DeformableTransformerEncoderLayer for layer in self.layers)
+                and carry_supported(src, self.layers[0].norm1)):
+            # bf16 operands carried from each fused add + LayerNorm to the next layer (no casts,
+            # no pos add, no gradient accumulation kernels between layers)
+            value, query = src, DeformableTransformerEncoderLayer.with_pos_embed(src, pos)
+            for i, layer in enumerate(self.layers):
+                next_pos = pos if i + 1 < len(self.layers) else None
+                out, value, query = layer.forward_carry(out, value, query, next_pos, reference_points,
+                                                        temporal_shapes, level_start_index, padding_mask)
+                if query is None:
+                    query = value
+            return out
         for layer in self.layers:
             out = layer(out, pos, reference_points, temporal_shapes, level_start_index, padding_mask)
         return out

@@ -14,7 +14,7 @@ import torch
 from torch import nn
 from torch.autograd import Function
 
-__all__ = ["add_layer_norm"]
+__all__ = ["add_layer_norm", "add_layer_norm_carry"]
 
 _TAGS = {torch.float32: 0, torch.bfloat16: 2}
 
@@ -69,3 +69,85 @@ def add_layer_norm(r, y, norm: nn.LayerNorm):
         with torch.autocast("cuda", enabled=False):
             return _AddLayerNorm.apply(r.contiguous(), y.contiguous(), norm.weight, norm.bias, norm.eps)
     return norm(r + y)
+
+
+class _AddLayerNormCarry(Function):
+    @staticmethod
+    def forward(ctx, r, y, weight, bias, pos, eps):
+        from ... import _native
+        lib = _native.load_library()
+        ctx.set_materialize_grads(False)
+        d = r.shape[-1]
+        rows = r.numel() // d
+        out = torch.empty(r.shape, dtype=torch.float32, device=r.device)
+        out16 = torch.empty(r.shape, dtype=torch.bfloat16, device=r.device)
+        q16 = torch.empty(r.shape, dtype=torch.bfloat16, device=r.device) if pos is not None else None
+        mean = torch.empty(rows, dtype=torch.float32, device=r.device)
+        rstd = torch.empty(rows, dtype=torch.float32, device=r.device)
+        rc = lib.mfl_add_layernorm_forward_ex(
+            r.data_ptr(), _TAGS[r.dtype], y.data_ptr(), _TAGS[y.dtype], weight.data_ptr(), bias.data_ptr(), rows, d,
+            float(eps), out.data_ptr(), mean.data_ptr(), rstd.data_ptr(), out16.data_ptr(),
+            pos.data_ptr() if pos is not None else None, q16.data_ptr() if q16 is not None else None,
+            _native.stream_handle(r.device))
+        if rc != 0:
+            raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
+        ctx.has_pos = pos is not None
+        ctx.pos_needs_grad = pos is not None and pos.requires_grad
+        ctx.save_for_backward(r, y, weight, mean, rstd)
+        return out, out16, q16
+
+    @staticmethod
+    def backward(ctx, dout, dout16, dq16):
+        from ... import _native
+        lib = _native.load_library()
+        r, y, weight, mean, rstd = ctx.saved_tensors
+        d = r.shape[-1]
+        rows = r.numel() // d
+        if dout is None and dout16 is None and dq16 is None:
+            return None, None, None, None, None, None
+        dout = dout.to(torch.float32).contiguous() if dout is not None else None
+        dout16 = dout16.to(torch.bfloat16).contiguous() if dout16 is not None else None
+        dq16 = dq16.to(torch.bfloat16).contiguous() if dq16 is not None else None
+        dr = torch.empty_like(r)
+        dy = torch.empty_like(y)
+        dw = torch.empty(d, dtype=torch.float32, device=r.device)
+        db = torch.empty(d, dtype=torch.float32, device=r.device)
+        dpos = None
+        if ctx.pos_needs_grad:
+            dpos = (torch.empty(r.shape, dtype=torch.float32, device=r.device) if dq16 is not None
+                    else torch.zeros(r.shape, dtype=torch.float32, device=r.device))
+        ws = torch.empty(max(lib.mfl_add_layernorm_workspace_bytes(rows, d), 4), dtype=torch.uint8, device=r.device)
+
+        def ptr(t):
+            return t.data_ptr() if t is not None else None
+        rc = lib.mfl_add_layernorm_backward_ex(
+            ptr(dout), ptr(dout16), ptr(dq16), r.data_ptr(), _TAGS[r.dtype], y.data_ptr(), _TAGS[y.dtype],
+            weight.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, d, dr.data_ptr(), dy.data_ptr(),
+            dw.data_ptr(), db.data_ptr(), ptr(dpos) if dq16 is not None else None, ws.data_ptr(),
+            _native.stream_handle(r.device))
+        if rc != 0:
+            raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
+        return dr, dy, dw, db, dpos, None
+
+
+def carry_supported(r, norm) -> bool:
+    """Whether ``add_layer_norm_carry`` runs fused for residual ``r`` and ``norm``."""
+    d = r.shape[-1]
+    return (r.is_cuda and torch.is_autocast_enabled("cuda")
+            and torch.get_autocast_dtype("cuda") == torch.bfloat16 and isinstance(norm, nn.LayerNorm)
+            and norm.elementwise_affine and norm.bias is not None and tuple(norm.normalized_shape) == (d,)
+            and norm.weight.dtype == torch.float32 and r.dtype in _TAGS and d % 256 == 0 and d <= 1024
+            and r.numel() > 0)
+
+
+def add_layer_norm_carry(r, y, norm: nn.LayerNorm, pos=None):
+    """``(out, out16, q16)`` with ``out = norm(r + y)`` (fp32 under autocast), ``out16`` its bf16
+    copy and ``q16 = bf16(out + pos)`` (None without ``pos``).  Fused on the GPU under bf16
+    autocast; elsewhere ``(out, out, out + pos)``, which every consumer treats exactly as before."""
+    if (carry_supported(r, norm) and r.shape == y.shape and y.dtype in _TAGS
+            and (pos is None or (pos.shape == r.shape and pos.dtype == torch.float32))):
+        with torch.autocast("cuda", enabled=False):
+            return _AddLayerNormCarry.apply(r.contiguous(), y.contiguous(), norm.weight, norm.bias,
+                                            pos.contiguous() if pos is not None else None, norm.eps)
+    out = add_layer_norm(r, y, norm)
+    return out, out, (out + pos if pos is not None else None)

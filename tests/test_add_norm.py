@@ -70,3 +70,93 @@ def test_unsupported_width_falls_back(dev):
         out = AN.add_layer_norm(r, y, norm)
         ref = norm(r + y)
     torch.testing.assert_close(out, ref, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,d,with_pos", [(15360, 512, True), (800, 512, False), (37, 1024, True)])
+def test_carry_matches_fp64(dev, rows, d, with_pos):
+    """add_layer_norm_carry: out (fp32), out16 = bf16(out), q16 = bf16(out + pos) and, with all three
+    gradients given, the input / pos / gamma / beta gradients against fp64."""
+    torch.manual_seed(rows)
+    norm = torch.nn.LayerNorm(d).to(dev)
+    with torch.no_grad():
+        norm.weight.uniform_(0.5, 1.5)
+        norm.bias.uniform_(-0.5, 0.5)
+    r = torch.randn(rows, d, device=dev).requires_grad_(True)
+    y = torch.randn(rows, d, device=dev).bfloat16().requires_grad_(True)
+    pos = torch.randn(rows, d, device=dev).requires_grad_(True) if with_pos else None
+    g0, g1, g2 = (torch.randn(rows, d, device=dev) for _ in range(3))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out, out16, q16 = AN.add_layer_norm_carry(r, y, norm, pos)
+    assert out.dtype == torch.float32 and out16.dtype == torch.bfloat16
+    torch.testing.assert_close(out16, out.bfloat16(), rtol=0, atol=0)
+    loss = (out * g0).sum() + (out16.float() * g1.bfloat16().float()).sum()
+    if with_pos:
+        torch.testing.assert_close(q16, (out + pos).bfloat16(), rtol=0, atol=0)
+        loss = loss + (q16.float() * g2.bfloat16().float()).sum()
+    else:
+        assert q16 is None
+    loss.backward()
+    dout = g0.double() + g1.bfloat16().double() + (g2.bfloat16().double() if with_pos else 0)
+    ro, rgr, rgy, rgw, rgb = _ref(r, y, norm.weight, norm.bias, norm.eps, dout)
+    torch.testing.assert_close(out.double(), ro, rtol=1e-5, atol=1e-5)
+    tol = 2 ** -8
+    torch.testing.assert_close(r.grad.double(), rgr, rtol=1e-5, atol=1e-5 * rgr.abs().max().item())
+    torch.testing.assert_close(y.grad.double(), rgy, rtol=tol, atol=tol * rgy.abs().max().item())
+    torch.testing.assert_close(norm.weight.grad.double(), rgw, rtol=1e-5, atol=1e-5 * rgw.abs().max().item())
+    torch.testing.assert_close(norm.bias.grad.double(), rgb, rtol=1e-5, atol=1e-5 * rgb.abs().max().item())
+    if with_pos:
+        torch.testing.assert_close(pos.grad, g2.bfloat16().float(), rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_carry_only_bf16_gradients(dev):
+    """The fp32 output unused (its gradient None): the backward runs on the 16-bit gradients alone."""
+    torch.manual_seed(3)
+    norm = torch.nn.LayerNorm(512).to(dev)
+    r = torch.randn(64, 512, device=dev).requires_grad_(True)
+    y = torch.randn(64, 512, device=dev).bfloat16().requires_grad_(True)
+    g1 = torch.randn(64, 512, device=dev).bfloat16()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        _, out16, _ = AN.add_layer_norm_carry(r, y, norm)
+    (out16.float() * g1.float()).sum().backward()
+    ro, rgr, rgy, rgw, rgb = _ref(r, y, norm.weight, norm.bias, norm.eps, g1.double())
+    torch.testing.assert_close(r.grad.double(), rgr, rtol=1e-5, atol=1e-5 * rgr.abs().max().item())
+    torch.testing.assert_close(norm.bias.grad.double(), rgb, rtol=1e-5, atol=1e-5 * rgb.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_encoder_carry_matches_uncarried(dev, monkeypatch):
+    """The encoder stack with carried bf16 operands against the same stack layer by layer (autocast
+    casts, pos adds): forward bit-identical (dropout 0: the same bf16 operands), gradients to
+    bf16-ulp tolerance elementwise and 1e-3 in norm."""
+    UT = PKG.models.deformable.unimodal_deformable_transformer
+    torch.manual_seed(0)
+    B, shapes, d = 2, [128, 64, 32, 16], 512
+    layer = UT.DeformableTransformerEncoderLayer(d, 1024, 0.0, "relu", 4, 8, 4)
+    enc = UT.DeformableTransformerEncoder(layer, 3).to(dev)
+    S = sum(shapes)
+    ts = torch.tensor(shapes, device=dev)
+    lsi = torch.cat([ts.new_zeros(1), ts.cumsum(0)[:-1]])
+    vr = torch.ones(B, 4, device=dev)
+    src0 = torch.randn(B, S, d, device=dev)
+    pos0 = torch.randn(B, S, d, device=dev)
+
+    def run():
+        enc.zero_grad(set_to_none=True)
+        src = src0.clone().requires_grad_(True)
+        pos = pos0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = enc(src, ts, lsi, vr, pos=pos)
+        (out * torch.linspace(-1, 1, d, device=dev)).sum().backward()
+        return out.detach(), src.grad, pos.grad, [p.grad.clone() for p in enc.parameters()]
+
+    o1, gs1, gp1, gw1 = run()
+    monkeypatch.setattr(UT, "carry_supported", lambda *a: False)
+    o2, gs2, gp2, gw2 = run()
+    torch.testing.assert_close(o1, o2, rtol=0, atol=0)
+    # the gradients cross bf16 GEMMs and bf16 branch gradients: a different fp32 summation order
+    # at the layer boundary moves a few elements by one bf16 ulp of their branch
+    for a, b in [(gs1, gs2), (gp1, gp2)] + list(zip(gw1, gw2)):
+        torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -8 * b.abs().max().item())
+        assert (a - b).norm() <= 1e-3 * b.norm()
