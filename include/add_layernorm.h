@@ -39,17 +39,23 @@ int mfl_add_layernorm_backward(const float* dout, const void* r, int r_dtype, co
 /* As mfl_add_layernorm_forward, plus optional 16-bit copies for the layer's next consumers (null = skip):
  * out16 = bf16(out) (the operand autocast would cast for value_proj / linear1) and, with pos (fp32, same
  * layout as out), q16 = bf16(out + pos) (the next MSDA query `with_pos_embed(src, pos)`,
- * unimodal_deformable_transformer.py:241).  Both rounded to nearest even from the fp32 values. */
+ * unimodal_deformable_transformer.py:241).  Both rounded to nearest even from the fp32 values.
+ * With `seed` (a device int64, read by the kernel; null = no dropout) the branch is dropped first:
+ * out = LN(r + dropout_p(y)) (nn.Dropout(p) training semantics, keep bits regenerated from the
+ * seed by the backward, which must get the same p and seed); 0 <= p_drop < 1. */
 int mfl_add_layernorm_forward_ex(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,
                                  const float* beta, int64_t rows, int64_t d, float eps, float* out, float* mean,
-                                 float* rstd, uint16_t* out16, const float* pos, uint16_t* q16, void* stream);
+                                 float* rstd, uint16_t* out16, const float* pos, uint16_t* q16, float p_drop,
+                                 const int64_t* seed, void* stream);
 
 /* As mfl_add_layernorm_backward with d out = dout (fp32) + dout16 + dq16 (bf16), each optional (at least one
- * non-null), summed in fp32; dpos (optional, fp32) = dq16 widened, the gradient of pos. */
+ * non-null), summed in fp32; dpos (optional, fp32) = dq16 widened, the gradient of pos.  p_drop / seed as
+ * given to the forward (dy is then the gradient through the dropout). */
 int mfl_add_layernorm_backward_ex(const float* dout, const uint16_t* dout16, const uint16_t* dq16, const void* r,
                                   int r_dtype, const void* y, int y_dtype, const float* gamma, const float* mean,
                                   const float* rstd, int64_t rows, int64_t d, void* dr, void* dy, float* dgamma,
-                                  float* dbeta, float* dpos, void* workspace, void* stream);
+                                  float* dbeta, float* dpos, float p_drop, const int64_t* seed, void* workspace,
+                                  void* stream);
 
 const char* mfl_add_layernorm_last_error(void);
 

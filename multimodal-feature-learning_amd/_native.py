@@ -85,10 +85,11 @@ def _declare(lib):
     lib.mfl_add_layernorm_backward.restype = i32
     lib.mfl_add_layernorm_backward.argtypes = [vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, vp, vp, vp, vp, vp]
     lib.mfl_add_layernorm_forward_ex.restype = i32
-    lib.mfl_add_layernorm_forward_ex.argtypes = [vp, i32, vp, i32, vp, vp, i64, i64, f32, vp, vp, vp, vp, vp, vp, vp]
+    lib.mfl_add_layernorm_forward_ex.argtypes = [vp, i32, vp, i32, vp, vp, i64, i64, f32, vp, vp, vp, vp, vp, vp, f32,
+                                                 vp, vp]
     lib.mfl_add_layernorm_backward_ex.restype = i32
     lib.mfl_add_layernorm_backward_ex.argtypes = [vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, vp, vp, vp,
-                                                  vp, vp, vp]
+                                                  vp, f32, vp, vp, vp]
     lib.mfl_add_layernorm_last_error.restype = ctypes.c_char_p
     lib.mfl_add_layernorm_last_error.argtypes = []
     lib.flat_adamw_last_error.restype = ctypes.c_char_p

@@ -55,6 +55,41 @@ __device__ __forceinline__ float wave_sum(float x) {
   return x;
 }
 
+// Dropout of the branch (nn.Dropout(p) in training, reference :238/:249): element e of the call is
+// kept when a 64-bit mix of (seed, e) clears p; the backward regenerates the same bits from the
+// same device-side seed (no mask in HBM).  Kept values are scaled by 1 / (1 - p) and, for a bf16
+// branch, rounded to bf16 as ATen's dropout of a bf16 tensor is.
+struct Drop {
+  const int64_t* seed_ptr;  // null: no dropout
+  float p, scale;
+};
+
+__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t e) {
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + e;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+template <typename YT>
+__device__ __forceinline__ void drop4(float (&b)[4], uint64_t seed, uint32_t thresh, float scale, long long e0,
+                                      float (&keep)[4]) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    keep[k] = (drop_bits(seed, (uint64_t)(e0 + k)) >> 8) >= thresh ? scale : 0.f;
+    float v = b[k] * keep[k];
+    if (sizeof(YT) == 2) v = __uint_as_float(Vec4<uint16_t>::rne(v) << 16);
+    b[k] = v;
+  }
+}
+
+__device__ __forceinline__ uint32_t drop_thresh(float p) {  // keep iff 24-bit draw >= p * 2^24
+  return (uint32_t)fminf(p * 16777216.f, 16777216.f);
+}
+
 template <typename RT, typename YT, int CH>
 __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__ r, const YT* __restrict__ y,
                                                          const float* __restrict__ gamma,
@@ -62,8 +97,10 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__
                                                          float eps, float* __restrict__ out,
                                                          float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                          uint16_t* __restrict__ out16, const float* __restrict__ pos,
-                                                         uint16_t* __restrict__ q16) {
+                                                         uint16_t* __restrict__ q16, Drop drop) {
   const int lane = threadIdx.x & 63;
+  const uint64_t seed = drop.seed_ptr ? (uint64_t)drop.seed_ptr[0] : 0;
+  const uint32_t thresh = drop_thresh(drop.p);
   const long long row = (long long)blockIdx.x * kWaves + (threadIdx.x >> 6);
   if (row >= rows) return;  // wave-uniform
   const long long base = row * d;
@@ -75,6 +112,10 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__
     float a[4], b[4];
     Vec4<RT>::load(r + base + col, a);
     Vec4<YT>::load(y + base + col, b);
+    if (drop.seed_ptr) {
+      float keep[4];
+      drop4<YT>(b, seed, thresh, drop.scale, base + col, keep);
+    }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       z[c][k] = a[k] + b[k];
@@ -120,8 +161,10 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
     const float* __restrict__ dout, const RT* __restrict__ r, const YT* __restrict__ y,
     const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     long long rows, int d, RT* __restrict__ dr, YT* __restrict__ dy, float* __restrict__ part,
-    const uint16_t* __restrict__ dout16, const uint16_t* __restrict__ dq16, float* __restrict__ dpos) {
+    const uint16_t* __restrict__ dout16, const uint16_t* __restrict__ dq16, float* __restrict__ dpos, Drop drop) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const uint64_t seed = drop.seed_ptr ? (uint64_t)drop.seed_ptr[0] : 0;
+  const uint32_t thresh = drop_thresh(drop.p);
   float dg[CH][4], db[CH][4];
 #pragma unroll
   for (int c = 0; c < CH; ++c)
@@ -132,7 +175,7 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
     if (row >= rows) break;  // wave-uniform
     const long long base = row * d;
     const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[CH][4], g[CH][4];
+    float xh[CH][4], g[CH][4], kp[CH][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
@@ -140,6 +183,12 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
       float a[4], b[4], go[4] = {0.f, 0.f, 0.f, 0.f}, ga[4];
       Vec4<RT>::load(r + base + col, a);
       Vec4<YT>::load(y + base + col, b);
+      if (drop.seed_ptr) {
+        drop4<YT>(b, seed, thresh, drop.scale, base + col, kp[c]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) kp[c][k] = 1.f;
+      }
       // d out = its fp32 gradient + the bf16 copy's + the (out + pos) copy's, summed in fp32
       if (dout) Vec4<float>::load(dout + base + col, go);
       if (dout16) {
@@ -174,6 +223,8 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
 #pragma unroll
       for (int k = 0; k < 4; ++k) dx[k] = rstd * (g[c][k] - m1 - xh[c][k] * m2);
       Vec4<RT>::store(dr + base + col, dx);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) dx[k] *= kp[c][k];
       Vec4<YT>::store(dy + base + col, dx);
     }
   }
@@ -229,11 +280,12 @@ bool shape_ok(int64_t rows, int64_t d) { return rows >= 0 && d > 0 && d % 256 ==
 
 #define MFL_ALN_FWD(CHN)                                                                                   \
   hipLaunchKernelGGL((add_ln_fwd<RT, YT, CHN>), dim3(blocks), dim3(kWaves * 64), 0, st, rp, yp, gamma, beta, \
-                     (long long)rows, (int)d, eps, out, mean, rstd, out16, pos, q16)
+                     (long long)rows, (int)d, eps, out, mean, rstd, out16, pos, q16, drop)
 
 template <typename RT, typename YT>
 int fwd(const void* r, const void* y, const float* gamma, const float* beta, int64_t rows, int64_t d, float eps,
-        float* out, float* mean, float* rstd, uint16_t* out16, const float* pos, uint16_t* q16, hipStream_t st) {
+        float* out, float* mean, float* rstd, uint16_t* out16, const float* pos, uint16_t* q16, Drop drop,
+        hipStream_t st) {
   const unsigned blocks = (unsigned)((rows + kWaves - 1) / kWaves);
   auto* rp = static_cast<const RT*>(r);
   auto* yp = static_cast<const YT*>(y);
@@ -249,12 +301,12 @@ int fwd(const void* r, const void* y, const float* gamma, const float* beta, int
 
 #define MFL_ALN_BWD(CHN)                                                                                   \
   hipLaunchKernelGGL((add_ln_bwd<RT, YT, CHN>), dim3(blocks), dim3(kWaves * 64), 0, st, dout, rp, yp, gamma, \
-                     mean, rstd, (long long)rows, (int)d, drp, dyp, part, dout16, dq16, dpos)
+                     mean, rstd, (long long)rows, (int)d, drp, dyp, part, dout16, dq16, dpos, drop)
 
 template <typename RT, typename YT>
 int bwd(const float* dout, const void* r, const void* y, const float* gamma, const float* mean, const float* rstd,
         int64_t rows, int64_t d, void* dr, void* dy, float* dgamma, float* dbeta, void* workspace,
-        const uint16_t* dout16, const uint16_t* dq16, float* dpos, hipStream_t st) {
+        const uint16_t* dout16, const uint16_t* dq16, float* dpos, Drop drop, hipStream_t st) {
   const unsigned blocks = (unsigned)((rows + kBwdRows - 1) / kBwdRows);
   auto* rp = static_cast<const RT*>(r);
   auto* yp = static_cast<const YT*>(y);
@@ -287,8 +339,13 @@ size_t mfl_add_layernorm_workspace_bytes(int64_t rows, int64_t d) {
 
 int mfl_add_layernorm_forward_ex(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,
                                  const float* beta, int64_t rows, int64_t d, float eps, float* out, float* mean,
-                                 float* rstd, uint16_t* out16, const float* pos, uint16_t* q16, void* stream) {
+                                 float* rstd, uint16_t* out16, const float* pos, uint16_t* q16, float p_drop,
+                                 const int64_t* seed, void* stream) {
   g_err[0] = 0;
+  if (seed && !(p_drop >= 0.f && p_drop < 1.f)) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_forward: dropout p must be in [0, 1)");
+    return 1;
+  }
   if (!shape_ok(rows, d) || (r_dtype != 0 && r_dtype != 2) || (y_dtype != 0 && y_dtype != 2)) {
     snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_forward: needs d %% 256 == 0, d <= 1024, fp32/bf16 inputs");
     return 1;
@@ -299,7 +356,8 @@ int mfl_add_layernorm_forward_ex(const void* r, int r_dtype, const void* y, int 
     return 1;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
-#define MFL_ALN_FWD_ARGS r, y, gamma, beta, rows, d, eps, out, mean, rstd, out16, pos, q16, st
+  const Drop drop{seed, p_drop, seed ? 1.f / (1.f - p_drop) : 1.f};
+#define MFL_ALN_FWD_ARGS r, y, gamma, beta, rows, d, eps, out, mean, rstd, out16, pos, q16, drop, st
   if (r_dtype == 0)
     return y_dtype == 0 ? fwd<float, float>(MFL_ALN_FWD_ARGS) : fwd<float, uint16_t>(MFL_ALN_FWD_ARGS);
   return y_dtype == 0 ? fwd<uint16_t, float>(MFL_ALN_FWD_ARGS) : fwd<uint16_t, uint16_t>(MFL_ALN_FWD_ARGS);
@@ -310,14 +368,19 @@ int mfl_add_layernorm_forward(const void* r, int r_dtype, const void* y, int y_d
                               const float* beta, int64_t rows, int64_t d, float eps, float* out, float* mean,
                               float* rstd, void* stream) {
   return mfl_add_layernorm_forward_ex(r, r_dtype, y, y_dtype, gamma, beta, rows, d, eps, out, mean, rstd, nullptr,
-                                      nullptr, nullptr, stream);
+                                      nullptr, nullptr, 0.f, nullptr, stream);
 }
 
 int mfl_add_layernorm_backward_ex(const float* dout, const uint16_t* dout16, const uint16_t* dq16, const void* r,
                                   int r_dtype, const void* y, int y_dtype, const float* gamma, const float* mean,
                                   const float* rstd, int64_t rows, int64_t d, void* dr, void* dy, float* dgamma,
-                                  float* dbeta, float* dpos, void* workspace, void* stream) {
+                                  float* dbeta, float* dpos, float p_drop, const int64_t* seed, void* workspace,
+                                  void* stream) {
   g_err[0] = 0;
+  if (seed && !(p_drop >= 0.f && p_drop < 1.f)) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: dropout p must be in [0, 1)");
+    return 1;
+  }
   if (!shape_ok(rows, d) || (r_dtype != 0 && r_dtype != 2) || (y_dtype != 0 && y_dtype != 2)) {
     snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: needs d %% 256 == 0, d <= 1024, fp32/bf16 inputs");
     return 1;
@@ -334,7 +397,9 @@ int mfl_add_layernorm_backward_ex(const float* dout, const uint16_t* dout16, con
     snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: null pointer");
     return 1;
   }
-#define MFL_ALN_BWD_ARGS dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, dout16, dq16, dpos, st
+  const Drop drop{seed, p_drop, seed ? 1.f / (1.f - p_drop) : 1.f};
+#define MFL_ALN_BWD_ARGS \
+  dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, dout16, dq16, dpos, drop, st
   if (r_dtype == 0)
     return y_dtype == 0 ? bwd<float, float>(MFL_ALN_BWD_ARGS) : bwd<float, uint16_t>(MFL_ALN_BWD_ARGS);
   return y_dtype == 0 ? bwd<uint16_t, float>(MFL_ALN_BWD_ARGS) : bwd<uint16_t, uint16_t>(MFL_ALN_BWD_ARGS);
@@ -350,7 +415,7 @@ int mfl_add_layernorm_backward(const float* dout, const void* r, int r_dtype, co
     return 1;
   }
   return mfl_add_layernorm_backward_ex(dout, nullptr, nullptr, r, r_dtype, y, y_dtype, gamma, mean, rstd, rows, d, dr,
-                                       dy, dgamma, dbeta, nullptr, workspace, stream);
+                                       dy, dgamma, dbeta, nullptr, 0.f, nullptr, workspace, stream);
 }
 
 const char* mfl_add_layernorm_last_error(void) { return g_err; }

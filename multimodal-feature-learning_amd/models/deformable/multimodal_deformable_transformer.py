@@ -133,11 +133,11 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src):
         hidden = self.dropout2(self.activation(self.linear1(src)))
-        return add_layer_norm(src, self.dropout3(self.linear2(hidden)), self.norm2)
+        return add_layer_norm(src, self.linear2(hidden), self.norm2, dropout=self.dropout3)
 
     def _self_block(self, src, pos, ref, shapes, starts, mask):
         attn = self.self_attn(self.with_pos_embed(src, pos), ref, src, shapes, starts, mask)
-        return add_layer_norm(src, self.dropout1(attn), self.norm1)
+        return add_layer_norm(src, attn, self.norm1, dropout=self.dropout1)
 
     def forward(self, video_src, video_pos, video_reference_points, video_temporal_shapes, video_level_start_index,
                 video_padding_mask, audio_src, audio_pos, audio_reference_points, audio_temporal_shapes,
@@ -206,18 +206,18 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
 
     def forward_ffn(self, tgt):
         hidden = self.dropout3(self.activation(self.linear1(tgt)))
-        return add_layer_norm(tgt, self.dropout4(self.linear2(hidden)), self.norm3)
+        return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
     def _cross_block(self, tgt, query_pos, ref, src, shapes, starts, mask):
         attn = self.cross_attn(self.with_pos_embed(tgt, query_pos), ref, src, shapes, starts, mask)
-        return add_layer_norm(tgt, self.dropout1(attn), self.norm1)
+        return add_layer_norm(tgt, attn, self.norm1, dropout=self.dropout1)
 
     def forward(self, tgt, query_pos, reference_points_input_video, reference_points_input_audio, query_mask,
                 video_src, video_temporal_shapes, video_level_start_index, video_src_padding_mask, audio_src,
                 audio_temporal_shapes, audio_level_start_index, audio_src_padding_mask):
         qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
         sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
-        tgt = add_layer_norm(tgt, self.dropout2(sa), self.norm2)
+        tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         tgt_video = self._cross_block(tgt, query_pos, reference_points_input_video, video_src, video_temporal_shapes,
                                       video_level_start_index, video_src_padding_mask)
         tgt_audio = self._cross_block(tgt, query_pos, reference_points_input_audio, audio_src, audio_temporal_shapes,

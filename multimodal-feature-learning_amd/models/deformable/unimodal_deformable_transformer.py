@@ -186,12 +186,12 @@ class DeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src):
         hidden = self.dropout2(self.activation(self.linear1(src)))
-        return add_layer_norm(src, self.dropout3(self.linear2(hidden)), self.norm2)
+        return add_layer_norm(src, self.linear2(hidden), self.norm2, dropout=self.dropout3)
 
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None):
         attn = self.self_attn(self.with_pos_embed(src, pos), reference_points, src, temporal_shapes,
                               level_start_index, padding_mask)
-        src = add_layer_norm(src, self.dropout1(attn), self.norm1)
+        src = add_layer_norm(src, attn, self.norm1, dropout=self.dropout1)
         return self.forward_ffn(src)
 
     def forward_carry(self, src, value, query, next_pos, reference_points, temporal_shapes, level_start_index,
@@ -201,9 +201,9 @@ class DeformableTransformerEncoderLayer(nn.Module):
         the fp32 tensors themselves), and the fused add + LayerNorms hand back the next layer's
         ``(src, value, query)`` (query = bf16(out + next_pos); None when next_pos is None)."""
         attn = self.self_attn(query, reference_points, value, temporal_shapes, level_start_index, padding_mask)
-        src, src16, _ = add_layer_norm_carry(src, self.dropout1(attn), self.norm1)
+        src, src16, _ = add_layer_norm_carry(src, attn, self.norm1, dropout=self.dropout1)
         hidden = self.dropout2(self.activation(self.linear1(src16)))
-        return add_layer_norm_carry(src, self.dropout3(self.linear2(hidden)), self.norm2, next_pos)
+        return add_layer_norm_carry(src, self.linear2(hidden), self.norm2, next_pos, self.dropout3)
 
 
 class DeformableTransformerEncoder(nn.Module):
@@ -265,16 +265,16 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward_ffn(self, tgt):
         hidden = self.dropout3(self.activation(self.linear1(tgt)))
-        return add_layer_norm(tgt, self.dropout4(self.linear2(hidden)), self.norm3)
+        return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None):
         qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
         sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
-        tgt = add_layer_norm(tgt, self.dropout2(sa), self.norm2)
+        tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         ca = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_temporal_shapes,
                              level_start_index, src_padding_mask)
-        tgt = add_layer_norm(tgt, self.dropout1(ca), self.norm1)
+        tgt = add_layer_norm(tgt, ca, self.norm1, dropout=self.dropout1)
         return self.forward_ffn(tgt)
 
 

@@ -19,9 +19,22 @@ __all__ = ["add_layer_norm", "add_layer_norm_carry"]
 _TAGS = {torch.float32: 0, torch.bfloat16: 2}
 
 
+def _ptr(t):
+    return t.data_ptr() if t is not None else None
+
+
+def _drop_args(dropout, device):
+    """(p, seed tensor) of an active nn.Dropout, else (0.0, None).  The seed is drawn on the device
+    from torch's generator (graph-capture safe: a fresh value on every replay) and kept for the
+    backward, which regenerates the keep bits from it."""
+    if isinstance(dropout, nn.Dropout) and dropout.training and dropout.p > 0:
+        return float(dropout.p), torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
+    return 0.0, None
+
+
 class _AddLayerNorm(Function):
     @staticmethod
-    def forward(ctx, r, y, weight, bias, eps):
+    def forward(ctx, r, y, weight, bias, eps, p_drop, seed):
         from ... import _native
         lib = _native.load_library()
         d = r.shape[-1]
@@ -29,19 +42,21 @@ class _AddLayerNorm(Function):
         out = torch.empty(r.shape, dtype=torch.float32, device=r.device)
         mean = torch.empty(rows, dtype=torch.float32, device=r.device)
         rstd = torch.empty(rows, dtype=torch.float32, device=r.device)
-        rc = lib.mfl_add_layernorm_forward(r.data_ptr(), _TAGS[r.dtype], y.data_ptr(), _TAGS[y.dtype],
-                                           weight.data_ptr(), bias.data_ptr(), rows, d, float(eps), out.data_ptr(),
-                                           mean.data_ptr(), rstd.data_ptr(), _native.stream_handle(r.device))
+        rc = lib.mfl_add_layernorm_forward_ex(r.data_ptr(), _TAGS[r.dtype], y.data_ptr(), _TAGS[y.dtype],
+                                              weight.data_ptr(), bias.data_ptr(), rows, d, float(eps), out.data_ptr(),
+                                              mean.data_ptr(), rstd.data_ptr(), None, None, None, p_drop, _ptr(seed),
+                                              _native.stream_handle(r.device))
         if rc != 0:
             raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
-        ctx.save_for_backward(r, y, weight, mean, rstd)
+        ctx.p_drop = p_drop
+        ctx.save_for_backward(r, y, weight, mean, rstd, seed)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         from ... import _native
         lib = _native.load_library()
-        r, y, weight, mean, rstd = ctx.saved_tensors
+        r, y, weight, mean, rstd, seed = ctx.saved_tensors
         dout = dout.to(torch.float32).contiguous()
         d = r.shape[-1]
         rows = r.numel() // d
@@ -50,30 +65,33 @@ class _AddLayerNorm(Function):
         dw = torch.empty(d, dtype=torch.float32, device=r.device)
         db = torch.empty(d, dtype=torch.float32, device=r.device)
         ws = torch.empty(max(lib.mfl_add_layernorm_workspace_bytes(rows, d), 4), dtype=torch.uint8, device=r.device)
-        rc = lib.mfl_add_layernorm_backward(dout.data_ptr(), r.data_ptr(), _TAGS[r.dtype], y.data_ptr(),
-                                            _TAGS[y.dtype], weight.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows,
-                                            d, dr.data_ptr(), dy.data_ptr(), dw.data_ptr(), db.data_ptr(),
-                                            ws.data_ptr(), _native.stream_handle(r.device))
+        rc = lib.mfl_add_layernorm_backward_ex(dout.data_ptr(), None, None, r.data_ptr(), _TAGS[r.dtype], y.data_ptr(),
+                                               _TAGS[y.dtype], weight.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                               rows, d, dr.data_ptr(), dy.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                                               None, ctx.p_drop, _ptr(seed), ws.data_ptr(),
+                                               _native.stream_handle(r.device))
         if rc != 0:
             raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
-        return dr, dy, dw, db, None
+        return dr, dy, dw, db, None, None, None
 
 
-def add_layer_norm(r, y, norm: nn.LayerNorm):
-    """``norm(r + y)``; fused on the GPU under autocast (see the module docstring)."""
+def add_layer_norm(r, y, norm: nn.LayerNorm, dropout=None):
+    """``norm(r + dropout(y))`` (``norm(r + y)`` without ``dropout``); fused on the GPU under autocast,
+    dropout included (see the module docstring)."""
     d = r.shape[-1]
     if (r.is_cuda and torch.is_autocast_enabled("cuda") and isinstance(norm, nn.LayerNorm)
             and norm.elementwise_affine and norm.bias is not None and tuple(norm.normalized_shape) == (d,)
             and norm.weight.dtype == torch.float32 and r.shape == y.shape and r.dtype in _TAGS
             and y.dtype in _TAGS and d % 256 == 0 and d <= 1024 and r.numel() > 0):
+        p_drop, seed = _drop_args(dropout, r.device)
         with torch.autocast("cuda", enabled=False):
-            return _AddLayerNorm.apply(r.contiguous(), y.contiguous(), norm.weight, norm.bias, norm.eps)
-    return norm(r + y)
+            return _AddLayerNorm.apply(r.contiguous(), y.contiguous(), norm.weight, norm.bias, norm.eps, p_drop, seed)
+    return norm(r + (dropout(y) if dropout is not None else y))
 
 
 class _AddLayerNormCarry(Function):
     @staticmethod
-    def forward(ctx, r, y, weight, bias, pos, eps):
+    def forward(ctx, r, y, weight, bias, pos, eps, p_drop, seed):
         from ... import _native
         lib = _native.load_library()
         ctx.set_materialize_grads(False)
@@ -87,24 +105,24 @@ class _AddLayerNormCarry(Function):
         rc = lib.mfl_add_layernorm_forward_ex(
             r.data_ptr(), _TAGS[r.dtype], y.data_ptr(), _TAGS[y.dtype], weight.data_ptr(), bias.data_ptr(), rows, d,
             float(eps), out.data_ptr(), mean.data_ptr(), rstd.data_ptr(), out16.data_ptr(),
-            pos.data_ptr() if pos is not None else None, q16.data_ptr() if q16 is not None else None,
-            _native.stream_handle(r.device))
+            _ptr(pos), _ptr(q16), p_drop, _ptr(seed), _native.stream_handle(r.device))
         if rc != 0:
             raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
         ctx.has_pos = pos is not None
         ctx.pos_needs_grad = pos is not None and pos.requires_grad
-        ctx.save_for_backward(r, y, weight, mean, rstd)
+        ctx.p_drop = p_drop
+        ctx.save_for_backward(r, y, weight, mean, rstd, seed)
         return out, out16, q16
 
     @staticmethod
     def backward(ctx, dout, dout16, dq16):
         from ... import _native
         lib = _native.load_library()
-        r, y, weight, mean, rstd = ctx.saved_tensors
+        r, y, weight, mean, rstd, seed = ctx.saved_tensors
         d = r.shape[-1]
         rows = r.numel() // d
         if dout is None and dout16 is None and dq16 is None:
-            return None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         dout = dout.to(torch.float32).contiguous() if dout is not None else None
         dout16 = dout16.to(torch.bfloat16).contiguous() if dout16 is not None else None
         dq16 = dq16.to(torch.bfloat16).contiguous() if dq16 is not None else None
@@ -117,17 +135,14 @@ class _AddLayerNormCarry(Function):
             dpos = (torch.empty(r.shape, dtype=torch.float32, device=r.device) if dq16 is not None
                     else torch.zeros(r.shape, dtype=torch.float32, device=r.device))
         ws = torch.empty(max(lib.mfl_add_layernorm_workspace_bytes(rows, d), 4), dtype=torch.uint8, device=r.device)
-
-        def ptr(t):
-            return t.data_ptr() if t is not None else None
         rc = lib.mfl_add_layernorm_backward_ex(
-            ptr(dout), ptr(dout16), ptr(dq16), r.data_ptr(), _TAGS[r.dtype], y.data_ptr(), _TAGS[y.dtype],
+            _ptr(dout), _ptr(dout16), _ptr(dq16), r.data_ptr(), _TAGS[r.dtype], y.data_ptr(), _TAGS[y.dtype],
             weight.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, d, dr.data_ptr(), dy.data_ptr(),
-            dw.data_ptr(), db.data_ptr(), ptr(dpos) if dq16 is not None else None, ws.data_ptr(),
-            _native.stream_handle(r.device))
+            dw.data_ptr(), db.data_ptr(), _ptr(dpos) if dq16 is not None else None, ctx.p_drop, _ptr(seed),
+            ws.data_ptr(), _native.stream_handle(r.device))
         if rc != 0:
             raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
-        return dr, dy, dw, db, dpos, None
+        return dr, dy, dw, db, dpos, None, None, None
 
 
 def carry_supported(r, norm) -> bool:
@@ -140,14 +155,15 @@ def carry_supported(r, norm) -> bool:
             and r.numel() > 0)
 
 
-def add_layer_norm_carry(r, y, norm: nn.LayerNorm, pos=None):
-    """``(out, out16, q16)`` with ``out = norm(r + y)`` (fp32 under autocast), ``out16`` its bf16
+def add_layer_norm_carry(r, y, norm: nn.LayerNorm, pos=None, dropout=None):
+    """``(out, out16, q16)`` with ``out = norm(r + dropout(y))`` (fp32 under autocast), ``out16`` its bf16
     copy and ``q16 = bf16(out + pos)`` (None without ``pos``).  Fused on the GPU under bf16
     autocast; elsewhere ``(out, out, out + pos)``, which every consumer treats exactly as before."""
     if (carry_supported(r, norm) and r.shape == y.shape and y.dtype in _TAGS
             and (pos is None or (pos.shape == r.shape and pos.dtype == torch.float32))):
+        p_drop, seed = _drop_args(dropout, r.device)
         with torch.autocast("cuda", enabled=False):
             return _AddLayerNormCarry.apply(r.contiguous(), y.contiguous(), norm.weight, norm.bias,
-                                            pos.contiguous() if pos is not None else None, norm.eps)
-    out = add_layer_norm(r, y, norm)
+                                            pos.contiguous() if pos is not None else None, norm.eps, p_drop, seed)
+    out = add_layer_norm(r, y, norm, dropout)
     return out, out, (out + pos if pos is not None else None)

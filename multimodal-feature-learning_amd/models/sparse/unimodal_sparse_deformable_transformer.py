@@ -188,14 +188,14 @@ class DeformableTransformerEncoderLayer(nn.Module):
 
     def forward_ffn(self, src):
         hidden = self.dropout2(self.activation(self.linear1(src)))
-        return add_layer_norm(src, self.dropout3(self.linear2(hidden)), self.norm2)
+        return add_layer_norm(src, self.linear2(hidden), self.norm2, dropout=self.dropout3)
 
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None, tgt=None):
         query = src if tgt is None else tgt
         attn, sampling_locations, attn_weights = self.self_attn(
             self.with_pos_embed(query, pos), reference_points, src, temporal_shapes, level_start_index, padding_mask,
             is_sparse=True)
-        out = add_layer_norm(query, self.dropout1(attn), self.norm1)
+        out = add_layer_norm(query, attn, self.norm1, dropout=self.dropout1)
         return self.forward_ffn(out), sampling_locations, attn_weights
 
 
@@ -289,17 +289,17 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward_ffn(self, tgt):
         hidden = self.dropout3(self.activation(self.linear1(tgt)))
-        return add_layer_norm(tgt, self.dropout4(self.linear2(hidden)), self.norm3)
+        return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None):
         qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
         sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
-        tgt = add_layer_norm(tgt, self.dropout2(sa), self.norm2)
+        tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         ca, sampling_locations, attn_weights = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points,
                                                                src, src_temporal_shapes, level_start_index,
                                                                src_padding_mask, is_sparse=True)
-        tgt = add_layer_norm(tgt, self.dropout1(ca), self.norm1)
+        tgt = add_layer_norm(tgt, ca, self.norm1, dropout=self.dropout1)
         return self.forward_ffn(tgt), sampling_locations, attn_weights
 
 
