@@ -1,0 +1,36 @@
+/*
+ * ffn_glue.h — C-ABI of the fused FFN activation dropout(relu(h)) of the deformable transformer
+ * layers (multimodal-feature-learning_amd/csrc/ffn_glue.hip, built into libmsda_hip.so).
+ *
+ * Replaces, under bf16 autocast, `self.dropout2(self.activation(self.linear1(src)))` of the
+ * reference's encoder FFN (models/deformable/unimodal_deformable_transformer.py:233-236) and the
+ * decoder's `dropout3(activation(linear1(tgt)))` (:360-362): ATen's relu, dropout (+ byte mask)
+ * and, in the backward, masked-scale and threshold_backward kernels.
+ *
+ * n bf16 elements, contiguous, n % 8 == 0, 16-byte aligned pointers.  seed: a device int64
+ * (null = no dropout, relu only); keep bits are a pure function of (seed, element index).
+ * The backward needs only the forward's output: dx = dy / (1 - p) where out > 0, else 0
+ * (`dropped` = whether the forward had a seed).  0 <= p_drop < 1.  Asynchronous on `stream`;
+ * 0 or non-zero with mfl_relu_dropout_last_error().
+ */
+#ifndef MFL_FFN_GLUE_H
+#define MFL_FFN_GLUE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int mfl_relu_dropout_forward(const void* x, int64_t n, float p_drop, const int64_t* seed, void* out, void* stream);
+
+int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float p_drop, int dropped, void* dx,
+                              void* stream);
+
+const char* mfl_relu_dropout_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MFL_FFN_GLUE_H */

@@ -43,6 +43,10 @@ EXPORTED_SYMBOLS = (
     "mfl_add_layernorm_forward_ex",
     "mfl_add_layernorm_backward_ex",
     "mfl_add_layernorm_last_error",
+    # include/ffn_glue.h
+    "mfl_relu_dropout_forward",
+    "mfl_relu_dropout_backward",
+    "mfl_relu_dropout_last_error",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -90,6 +94,12 @@ def _declare(lib):
     lib.mfl_add_layernorm_backward_ex.restype = i32
     lib.mfl_add_layernorm_backward_ex.argtypes = [vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, vp, vp, vp,
                                                   vp, f32, vp, vp, vp]
+    lib.mfl_relu_dropout_forward.restype = i32
+    lib.mfl_relu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]
+    lib.mfl_relu_dropout_backward.restype = i32
+    lib.mfl_relu_dropout_backward.argtypes = [vp, vp, i64, f32, i32, vp, vp]
+    lib.mfl_relu_dropout_last_error.restype = ctypes.c_char_p
+    lib.mfl_relu_dropout_last_error.argtypes = []
     lib.mfl_add_layernorm_last_error.restype = ctypes.c_char_p
     lib.mfl_add_layernorm_last_error.argtypes = []
     lib.flat_adamw_last_error.restype = ctypes.c_char_p

@@ -1,0 +1,146 @@
+// FFN activation of the deformable transformer layers: dropout(relu(linear1(x))) (reference
+// unimodal_deformable_transformer.py:233-236 forward_ffn, :360-362; the multimodal and sparse
+// layers repeat it).  Under bf16 autocast ATen runs it as a relu kernel, a dropout kernel that
+// also writes a byte mask, and in the backward a masked-scale kernel plus relu's
+// threshold_backward, each a full pass over the (tokens x d_ffn) hidden tensor.  Here:
+//   forward : out = relu(x) * keep * 1/(1-p), one read of x and one write of out; keep bits from a
+//             64-bit mix of (device seed, element index), as in add_layernorm.hip;
+//   backward: dx = dy * 1/(1-p) where out > 0, else 0 (out > 0 exactly when x > 0 and the element
+//             was kept), from the output linear2 keeps anyway: no mask, no RNG.
+// bf16 in and out, 8 elements (16 bytes) per lane, grid-stride over n / 8 vectors.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+
+#include "../../include/ffn_glue.h"
+
+namespace {
+
+thread_local char g_err[256];
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ uint32_t rne(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t e) {
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + e;
+  x ^= x >> 33;
+  x *= 0xff51afd7ed558ccdull;
+  x ^= x >> 33;
+  x *= 0xc4ceb9fe1a85ec53ull;
+  x ^= x >> 33;
+  return (uint32_t)x;
+}
+
+__device__ __forceinline__ float lo(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
+
+__global__ __launch_bounds__(kThreads) void relu_dropout_fwd(const uint4* __restrict__ x, long long nvec,
+                                                            const int64_t* __restrict__ seed_ptr, uint32_t thresh,
+                                                            float scale, uint4* __restrict__ out) {
+  const uint64_t seed = seed_ptr ? (uint64_t)seed_ptr[0] : 0;
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (long long)gridDim.x * kThreads) {
+    const uint4 v = x[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a = fmaxf(lo(w[j]), 0.f), b = fmaxf(hi(w[j]), 0.f);
+      if (seed_ptr) {
+        const uint64_t e = (uint64_t)i * 8 + 2 * j;
+        a = (drop_bits(seed, e) >> 8) >= thresh ? a * scale : 0.f;
+        b = (drop_bits(seed, e + 1) >> 8) >= thresh ? b * scale : 0.f;
+      }
+      o[j] = rne(a) | (rne(b) << 16);
+    }
+    out[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void relu_dropout_bwd(const uint4* __restrict__ dy, const uint4* __restrict__ out,
+                                                            long long nvec, float scale, uint4* __restrict__ dx) {
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (long long)gridDim.x * kThreads) {
+    const uint4 g = dy[i], y = out[i];
+    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, yw[4] = {y.x, y.y, y.z, y.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = lo(yw[j]) > 0.f ? lo(gw[j]) * scale : 0.f;
+      const float b = hi(yw[j]) > 0.f ? hi(gw[j]) * scale : 0.f;
+      o[j] = rne(a) | (rne(b) << 16);
+    }
+    dx[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+unsigned grid_for(long long nvec) {
+  const long long want = (nvec + kThreads - 1) / kThreads;
+  return (unsigned)(want < 256 * 32 ? (want > 0 ? want : 1) : 256 * 32);  // <= 32 blocks per CU, grid-stride
+}
+
+bool args_ok(const char* who, int64_t n, const void* a, const void* b, const void* c, float p) {
+  if (n < 0 || n % 8 != 0) {
+    snprintf(g_err, sizeof(g_err), "%s: n must be a non-negative multiple of 8", who);
+    return false;
+  }
+  if (!(p >= 0.f && p < 1.f)) {
+    snprintf(g_err, sizeof(g_err), "%s: dropout p must be in [0, 1)", who);
+    return false;
+  }
+  if (n > 0 && (!a || !b || !c)) {
+    snprintf(g_err, sizeof(g_err), "%s: null pointer", who);
+    return false;
+  }
+  if (((uintptr_t)a | (uintptr_t)b | (uintptr_t)c) & 15u) {
+    snprintf(g_err, sizeof(g_err), "%s: pointers must be 16-byte aligned", who);
+    return false;
+  }
+  return true;
+}
+
+int status(const char* what) {
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "ffn_glue: %s launch failed: %s", what, hipGetErrorString(e));
+    return 2;
+  }
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mfl_relu_dropout_forward(const void* x, int64_t n, float p_drop, const int64_t* seed, void* out, void* stream) {
+  g_err[0] = 0;
+  if (!args_ok("mfl_relu_dropout_forward", n, x, out, out, p_drop)) return 1;
+  if (n == 0) return 0;
+  const long long nvec = n / 8;
+  const uint32_t thresh = (uint32_t)fminf(p_drop * 16777216.f, 16777216.f);
+  const float scale = seed ? 1.f / (1.f - p_drop) : 1.f;
+  hipLaunchKernelGGL(relu_dropout_fwd, dim3(grid_for(nvec)), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint4*>(x), nvec, seed, thresh, scale, static_cast<uint4*>(out));
+  return status("forward");
+}
+
+int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float p_drop, int dropped, void* dx,
+                              void* stream) {
+  g_err[0] = 0;
+  if (!args_ok("mfl_relu_dropout_backward", n, dy, out, dx, p_drop)) return 1;
+  if (n == 0) return 0;
+  const long long nvec = n / 8;
+  const float scale = dropped ? 1.f / (1.f - p_drop) : 1.f;
+  hipLaunchKernelGGL(relu_dropout_bwd, dim3(grid_for(nvec)), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint4*>(dy), static_cast<const uint4*>(out), nvec, scale,
+                     static_cast<uint4*>(dx));
+  return status("backward");
+}
+
+const char* mfl_relu_dropout_last_error(void) { return g_err; }
+
+}  // extern "C"

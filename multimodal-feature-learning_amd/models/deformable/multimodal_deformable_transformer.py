@@ -17,6 +17,7 @@ from ..modules.attention import MSDeformAttn
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm
+from ..modules.ffn import relu_dropout
 from .unimodal_deformable_transformer import (_get_activation_fn, _get_clones, encoder_reference_points,
                                               level_metadata)
 
@@ -132,7 +133,7 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, src):
-        hidden = self.dropout2(self.activation(self.linear1(src)))
+        hidden = relu_dropout(self.linear1(src), self.activation, self.dropout2)
         return add_layer_norm(src, self.linear2(hidden), self.norm2, dropout=self.dropout3)
 
     def _self_block(self, src, pos, ref, shapes, starts, mask):
@@ -205,7 +206,7 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, tgt):
-        hidden = self.dropout3(self.activation(self.linear1(tgt)))
+        hidden = relu_dropout(self.linear1(tgt), self.activation, self.dropout3)
         return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
     def _cross_block(self, tgt, query_pos, ref, src, shapes, starts, mask):

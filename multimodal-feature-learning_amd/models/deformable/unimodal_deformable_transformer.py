@@ -20,6 +20,7 @@ from ..modules.attention import MSDeformAttn
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
+from ..modules.ffn import relu_dropout
 
 __all__ = [
     "DeformableTransformer", "DeformableTransformerEncoderLayer", "DeformableTransformerEncoder",
@@ -185,7 +186,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, src):
-        hidden = self.dropout2(self.activation(self.linear1(src)))
+        hidden = relu_dropout(self.linear1(src), self.activation, self.dropout2)
         return add_layer_norm(src, self.linear2(hidden), self.norm2, dropout=self.dropout3)
 
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None):
@@ -202,7 +203,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
         ``(src, value, query)`` (query = bf16(out + next_pos); None when next_pos is None)."""
         attn = self.self_attn(query, reference_points, value, temporal_shapes, level_start_index, padding_mask)
         src, src16, _ = add_layer_norm_carry(src, attn, self.norm1, dropout=self.dropout1)
-        hidden = self.dropout2(self.activation(self.linear1(src16)))
+        hidden = relu_dropout(self.linear1(src16), self.activation, self.dropout2)
         return add_layer_norm_carry(src, self.linear2(hidden), self.norm2, next_pos, self.dropout3)
 
 
@@ -264,7 +265,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, tgt):
-        hidden = self.dropout3(self.activation(self.linear1(tgt)))
+        hidden = relu_dropout(self.linear1(tgt), self.activation, self.dropout3)
         return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,

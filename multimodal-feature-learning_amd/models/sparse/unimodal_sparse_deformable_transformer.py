@@ -25,6 +25,7 @@ from ..deformable.unimodal_deformable_transformer import encoder_reference_point
 from ..modules.attention import MSDeformAttn
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm
+from ..modules.ffn import relu_dropout
 from ..modules.misc_modules import inverse_sigmoid
 
 __all__ = [
@@ -187,7 +188,7 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, src):
-        hidden = self.dropout2(self.activation(self.linear1(src)))
+        hidden = relu_dropout(self.linear1(src), self.activation, self.dropout2)
         return add_layer_norm(src, self.linear2(hidden), self.norm2, dropout=self.dropout3)
 
     def forward(self, src, pos, reference_points, temporal_shapes, level_start_index, padding_mask=None, tgt=None):
@@ -288,7 +289,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return tensor if pos is None else tensor + pos
 
     def forward_ffn(self, tgt):
-        hidden = self.dropout3(self.activation(self.linear1(tgt)))
+        hidden = relu_dropout(self.linear1(tgt), self.activation, self.dropout3)
         return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,

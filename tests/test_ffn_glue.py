@@ -1,0 +1,69 @@
+"""Fused FFN activation dropout(relu(h)) (models/modules/ffn.py, csrc/ffn_glue.hip): the reference's
+``self.dropout2(self.activation(self.linear1(src)))`` (unimodal_deformable_transformer.py:233-236,
+360-362).
+
+CPU / fp32 / eval: exactly ``dropout(relu(h))``.  GPU bf16: relu bit-exact without dropout; with
+dropout p the kept fraction of the positive elements is 1 - p and out / dx equal the ATen math run
+with the kernel's own mask (recovered from the output: out > 0 exactly where h > 0 and kept)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from conftest import PKG
+
+FF = PKG.models.modules.ffn
+
+
+def test_cpu_is_plain_dropout_relu():
+    torch.manual_seed(0)
+    drop = torch.nn.Dropout(0.1).eval()
+    h = torch.randn(4, 64, 2048)
+    torch.testing.assert_close(FF.relu_dropout(h, F.relu, drop), F.relu(h), rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_relu_only_bit_exact(dev):
+    torch.manual_seed(1)
+    drop = torch.nn.Dropout(0.1).eval()
+    h = torch.randn(8, 1920, 2048, device=dev).bfloat16().requires_grad_(True)
+    out = FF.relu_dropout(h, F.relu, drop)
+    dy = torch.randn_like(out)
+    out.backward(dy)
+    h2 = h.detach().clone().requires_grad_(True)
+    ref = F.relu(h2)
+    ref.backward(dy)
+    torch.testing.assert_close(out, ref, rtol=0, atol=0)
+    torch.testing.assert_close(h.grad, h2.grad, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [8, 4096 * 2048, 100 * 8 * 2048])
+def test_dropout_relu_matches_aten_math_with_its_mask(dev, n):
+    torch.manual_seed(n)
+    p = 0.1
+    drop = torch.nn.Dropout(p).train()
+    h = torch.randn(n, device=dev).bfloat16().requires_grad_(True)
+    out = FF.relu_dropout(h, F.relu, drop)
+    dy = torch.randn(n, device=dev).bfloat16()
+    out.backward(dy)
+    pos = h.detach() > 0
+    keep = out.detach() > 0
+    assert not bool((keep & ~pos).any())
+    if n > 1000:
+        rate = (keep.sum() / pos.sum()).item()
+        assert abs(rate - (1 - p)) < 0.005, rate
+    scale = 1.0 / (1.0 - p)
+    ref = (F.relu(h.detach().float()) * keep * scale).bfloat16()
+    torch.testing.assert_close(out.detach(), ref, rtol=2 ** -8, atol=0)
+    rdx = (dy.float() * keep * scale).bfloat16()
+    torch.testing.assert_close(h.grad, rdx, rtol=2 ** -8, atol=0)
+    assert bool((h.grad[~keep] == 0).all())
+
+
+@pytest.mark.gpu
+def test_fresh_mask_per_call(dev):
+    drop = torch.nn.Dropout(0.1).train()
+    h = torch.ones(1 << 20, device=dev).bfloat16()
+    a = FF.relu_dropout(h, F.relu, drop)
+    b = FF.relu_dropout(h, F.relu, drop)
+    assert (a != b).float().mean().item() > 0.1
