@@ -272,6 +272,15 @@ class DeformableTransformerDecoderLayer(nn.Module):
                 src_padding_mask=None, query_mask=None):
         qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
         sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
+        if carry_supported(tgt, self.norm2) and (query_pos is None or query_pos.shape == tgt.shape):
+            # bf16(tgt + query_pos) for the cross-attention query and bf16(tgt) for linear1 straight
+            # from the fused add + LayerNorms (no pos add, no casts, no gradient accumulation)
+            tgt, tgt16, q16 = add_layer_norm_carry(tgt, sa, self.norm2, query_pos, self.dropout2)
+            ca = self.cross_attn(q16 if q16 is not None else tgt16, reference_points, src, src_temporal_shapes,
+                                 level_start_index, src_padding_mask)
+            tgt, tgt16, _ = add_layer_norm_carry(tgt, ca, self.norm1, dropout=self.dropout1)
+            hidden = relu_dropout(self.linear1(tgt16), self.activation, self.dropout3)
+            return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
         tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         ca = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_temporal_shapes,
                              level_start_index, src_padding_mask)
@@ -295,6 +304,8 @@ class DeformableTransformerDecoder(nn.Module):
                 query_pos=None, src_padding_mask=None, query_padding_mask=None, disable_iterative_refine=False):
         output = tgt
         hs, refs = [], []
+        if query_pos is not None and not query_pos.is_contiguous():
+            query_pos = query_pos.contiguous()  # once, not per layer (the fused layers read it flat)
         for lid, layer in enumerate(self.layers):
             if reference_points.shape[-1] == 2:
                 scale = torch.stack([src_valid_ratios, src_valid_ratios], -1)[:, None]

@@ -227,3 +227,42 @@ def test_dropout_module_routes_through_kernel(dev):
         e = AN.add_layer_norm(r, y, norm)
     assert not torch.equal(a, b)
     torch.testing.assert_close(c, e, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_decoder_carry_matches_uncarried(dev, monkeypatch):
+    """Decoder layers with the cross-attention query bf16(tgt + query_pos) and the linear1 operand
+    bf16(tgt) from the fused add + LayerNorms, against the uncarried layers: forward bit-identical
+    (dropout 0), gradients (memory, tgt, query_pos, parameters) to bf16-ulp tolerance."""
+    UT = PKG.models.deformable.unimodal_deformable_transformer
+    torch.manual_seed(1)
+    B, Q, shapes, d = 2, 100, [128, 64, 32, 16], 512
+    layer = UT.DeformableTransformerDecoderLayer(d, 1024, 0.0, "relu", 4, 8, 4)
+    dec = UT.DeformableTransformerDecoder(layer, 2, return_intermediate=True).to(dev)
+    S = sum(shapes)
+    ts = torch.tensor(shapes, device=dev)
+    lsi = torch.cat([ts.new_zeros(1), ts.cumsum(0)[:-1]])
+    vr = torch.ones(B, 4, device=dev)
+    mem0 = torch.randn(B, S, d, device=dev)
+    tgt0 = torch.randn(B, Q, d, device=dev)
+    qpos0 = torch.randn(Q, d, device=dev)
+    ref = torch.rand(B, Q, 1, device=dev)
+    qmask = torch.ones(B, Q, dtype=torch.bool, device=dev)
+
+    def run():
+        dec.zero_grad(set_to_none=True)
+        mem, tgt = mem0.clone().requires_grad_(True), tgt0.clone().requires_grad_(True)
+        qpos = qpos0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            hs, _ = dec(tgt, ref, mem, ts, lsi, vr, query_pos=qpos.unsqueeze(0).expand(B, -1, -1),
+                        query_padding_mask=qmask)
+        (hs.float() * torch.linspace(-1, 1, d, device=dev)).sum().backward()
+        return hs.detach(), [mem.grad, tgt.grad, qpos.grad] + [p.grad.clone() for p in dec.parameters()]
+
+    h1, g1 = run()
+    monkeypatch.setattr(UT, "carry_supported", lambda *a: False)
+    h2, g2 = run()
+    torch.testing.assert_close(h1, h2, rtol=0, atol=0)
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -8 * b.abs().max().item())
+        assert (a - b).norm() <= 2 ** -8 * b.norm()
