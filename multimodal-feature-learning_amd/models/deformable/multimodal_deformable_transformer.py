@@ -16,7 +16,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..modules.attention import MSDeformAttn
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
-from ..modules.add_norm import add_layer_norm
+from ..modules.add_norm import add_layer_norm, add_layer_norm_carry
 from ..modules.ffn import relu_dropout
 from .unimodal_deformable_transformer import (_get_activation_fn, _get_clones, encoder_reference_points,
                                               level_metadata)
@@ -137,8 +137,12 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
         return add_layer_norm(src, self.linear2(hidden), self.norm2, dropout=self.dropout3)
 
     def _self_block(self, src, pos, ref, shapes, starts, mask):
+        """``norm1(src + dropout1(self_attn(src + pos, src)))`` as its bf16 copy (under bf16 autocast
+        on the GPU, from the fused add + LayerNorm; else the fp32 tensor itself): its only
+        consumers are the two cross-modal MSDA calls, as query of one and value of the other,
+        which would otherwise each cast it."""
         attn = self.self_attn(self.with_pos_embed(src, pos), ref, src, shapes, starts, mask)
-        return add_layer_norm(src, attn, self.norm1, dropout=self.dropout1)
+        return add_layer_norm_carry(src, attn, self.norm1, dropout=self.dropout1)[1]
 
     def forward(self, video_src, video_pos, video_reference_points, video_temporal_shapes, video_level_start_index,
                 video_padding_mask, audio_src, audio_pos, audio_reference_points, audio_temporal_shapes,

@@ -266,3 +266,47 @@ def test_decoder_carry_matches_uncarried(dev, monkeypatch):
     for a, b in zip(g1, g2):
         torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -8 * b.abs().max().item())
         assert (a - b).norm() <= 2 ** -8 * b.norm()
+
+
+@pytest.mark.gpu
+def test_multimodal_layer_carry_matches_uncarried(dev, monkeypatch):
+    """Multimodal encoder layer whose self blocks hand the cross-modal MSDA calls bf16(out) from the
+    fused add + LayerNorm, against the same layer with the fp32 output (autocast casts it per call):
+    forward bit-identical (dropout 0), gradients to bf16-ulp tolerance."""
+    MT = PKG.models.deformable.multimodal_deformable_transformer
+    torch.manual_seed(2)
+    B, d, vs, as_ = 2, 512, [128, 64, 32, 16], [50, 25, 13, 7]
+    layer = MT.MultimodalDeformableTransformerEncoderLayer(d, 1024, 0.0, "relu", 4, 8, 4).to(dev)
+
+    def meta(shapes):
+        ts = torch.tensor(shapes, device=dev)
+        return ts, torch.cat([ts.new_zeros(1), ts.cumsum(0)[:-1]])
+    vts, vlsi = meta(vs)
+    ats, alsi = meta(as_)
+    ones = torch.ones(B, 4, device=dev)
+    vref = MT.MultimodalDeformableTransformerEncoder.get_reference_points(vts, ones, dev)
+    aref = MT.MultimodalDeformableTransformerEncoder.get_reference_points(ats, ones, dev)
+    v0, a0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
+    vp0, ap0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
+
+    def run():
+        layer.zero_grad(set_to_none=True)
+        v, a = v0.clone().requires_grad_(True), a0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            ov, oa = layer(v, vp0, vref, vts, vlsi, None, a, ap0, aref, ats, alsi, None)
+        (ov.float().sum() + (oa.float() * 0.5).sum()).backward()
+        return (ov.detach(), oa.detach()), [v.grad, a.grad] + [p.grad.clone() for p in layer.parameters()]
+
+    o1, g1 = run()
+    AN_ = PKG.models.modules.add_norm
+
+    def uncarried(r, y, norm, pos=None, dropout=None):
+        out = AN_.add_layer_norm(r, y, norm, dropout)
+        return out, out, None
+    monkeypatch.setattr(MT, "add_layer_norm_carry", uncarried)
+    o2, g2 = run()
+    for a, b in zip(o1, o2):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -7 * b.abs().max().item())
+        assert (a - b).norm() <= 2 ** -8 * b.norm()
