@@ -16,7 +16,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..modules.attention import MSDeformAttn
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
-from ..modules.add_norm import add_layer_norm, add_layer_norm_carry
+from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 from ..modules.ffn import relu_dropout
 from .unimodal_deformable_transformer import (_get_activation_fn, _get_clones, encoder_reference_points,
                                               level_metadata)
@@ -136,6 +136,33 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
         hidden = relu_dropout(self.linear1(src), self.activation, self.dropout2)
         return add_layer_norm(src, self.linear2(hidden), self.norm2, dropout=self.dropout3)
 
+    def forward_carry(self, video, audio, video_next_pos, audio_next_pos, video_reference_points,
+                      video_temporal_shapes, video_level_start_index, video_padding_mask, audio_reference_points,
+                      audio_temporal_shapes, audio_level_start_index, audio_padding_mask):
+        """``forward`` with each stream as ``(src, value, query)``: the MSDA self-attention inputs
+        arrive as bf16 copies (``src``, ``src + pos``) from the previous layer's fused FFN add +
+        LayerNorm, and this layer's FFNs hand the next layer its copies (query = bf16(out +
+        next_pos); None when next_pos is None)."""
+        def self_block(stream, ref, shapes, starts, mask):
+            src, value, query = stream
+            attn = self.self_attn(query, ref, value, shapes, starts, mask)
+            return add_layer_norm_carry(src, attn, self.norm1, dropout=self.dropout1)[1]
+
+        def ffn(x, next_pos):
+            hidden = relu_dropout(self.linear1(x), self.activation, self.dropout2)
+            out, out16, q16 = add_layer_norm_carry(x, self.linear2(hidden), self.norm2, next_pos, self.dropout3)
+            return out, out16, (q16 if q16 is not None else out16)
+
+        v16 = self_block(video, video_reference_points, video_temporal_shapes, video_level_start_index,
+                         video_padding_mask)
+        a16 = self_block(audio, audio_reference_points, audio_temporal_shapes, audio_level_start_index,
+                         audio_padding_mask)
+        visual_attended_audio = self.self_attn(a16, audio_reference_points, v16, video_temporal_shapes,
+                                               video_level_start_index, video_padding_mask)
+        audio_attended_visual = self.self_attn(v16, video_reference_points, a16, audio_temporal_shapes,
+                                               audio_level_start_index, audio_padding_mask)
+        return ffn(audio_attended_visual, video_next_pos), ffn(visual_attended_audio, audio_next_pos)
+
     def _self_block(self, src, pos, ref, shapes, starts, mask):
         """``norm1(src + dropout1(self_attn(src + pos, src)))`` as its bf16 copy (under bf16 autocast
         on the GPU, from the fused add + LayerNorm; else the fp32 tensor itself): its only
@@ -177,6 +204,19 @@ class MultimodalDeformableTransformerEncoder(nn.Module):
         video_ref = self.get_reference_points(video_temporal_shapes, video_valid_ratios, device=video_src.device)
         audio_ref = self.get_reference_points(audio_temporal_shapes, audio_valid_ratios, device=audio_src.device)
         output = video_src, audio_src
+        if (self.layers and all(type(layer) is MultimodalDeformableTransformerEncoderLayer for layer in self.layers)
+                and carry_supported(video_src, self.layers[0].norm2) and carry_supported(audio_src, self.layers[0].norm2)
+                and all(p is None or p.dtype == torch.float32 for p in (video_pos, audio_pos))):
+            # bf16 MSDA operands carried from each layer's fused FFN add + LayerNorm to the next
+            wp = MultimodalDeformableTransformerEncoderLayer.with_pos_embed
+            v, a = (video_src, video_src, wp(video_src, video_pos)), (audio_src, audio_src, wp(audio_src, audio_pos))
+            for i, layer in enumerate(self.layers):
+                last = i + 1 == len(self.layers)
+                v, a = layer.forward_carry(v, a, None if last else video_pos, None if last else audio_pos,
+                                           video_ref, video_temporal_shapes, video_level_start_index,
+                                           video_padding_mask, audio_ref, audio_temporal_shapes,
+                                           audio_level_start_index, audio_padding_mask)
+            return v[0], a[0]
         for layer in self.layers:
             v, a = output
             output = layer(v, video_pos, video_ref, video_temporal_shapes, video_level_start_index, video_padding_mask,

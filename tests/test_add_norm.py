@@ -288,13 +288,15 @@ def test_multimodal_layer_carry_matches_uncarried(dev, monkeypatch):
     aref = MT.MultimodalDeformableTransformerEncoder.get_reference_points(ats, ones, dev)
     v0, a0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
     vp0, ap0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
+    wv, wa = torch.randn(d, device=dev), torch.randn(d, device=dev)
 
     def run():
         layer.zero_grad(set_to_none=True)
         v, a = v0.clone().requires_grad_(True), a0.clone().requires_grad_(True)
         with torch.autocast("cuda", dtype=torch.bfloat16):
             ov, oa = layer(v, vp0, vref, vts, vlsi, None, a, ap0, aref, ats, alsi, None)
-        (ov.float().sum() + (oa.float() * 0.5).sum()).backward()
+        # weighted: a plain sum of LayerNorm outputs has ~zero gradient (rounding noise only)
+        (ov.float() * wv).sum().add_((oa.float() * wa).sum()).backward()
         return (ov.detach(), oa.detach()), [v.grad, a.grad] + [p.grad.clone() for p in layer.parameters()]
 
     o1, g1 = run()
@@ -310,3 +312,48 @@ def test_multimodal_layer_carry_matches_uncarried(dev, monkeypatch):
     for a, b in zip(g1, g2):
         torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -7 * b.abs().max().item())
         assert (a - b).norm() <= 2 ** -8 * b.norm()
+
+
+@pytest.mark.gpu
+def test_multimodal_encoder_carry_matches_uncarried(dev, monkeypatch):
+    """Multimodal encoder stack carrying (src, bf16 src, bf16 src + pos) per stream between layers,
+    against the layer-by-layer stack: forward bit-identical (dropout 0).  Gradients (both inputs,
+    both positional embeddings, parameters) cross 3 layers of bf16 GEMMs and cross-modal MSDA, so
+    both bf16 runs are held to the fp32 run of the same stack: the carried one may not be further
+    from it than the uncarried one (x1.25), and the two agree to bf16-ulp tolerance elementwise."""
+    MT = PKG.models.deformable.multimodal_deformable_transformer
+    torch.manual_seed(3)
+    B, d, vs, as_ = 2, 512, [128, 64, 32, 16], [50, 25, 13, 7]
+    layer = MT.MultimodalDeformableTransformerEncoderLayer(d, 1024, 0.0, "relu", 4, 8, 4)
+    enc = MT.MultimodalDeformableTransformerEncoder(layer, 3).to(dev)
+
+    def meta(shapes):
+        ts = torch.tensor(shapes, device=dev)
+        return ts, torch.cat([ts.new_zeros(1), ts.cumsum(0)[:-1]])
+    vts, vlsi = meta(vs)
+    ats, alsi = meta(as_)
+    ones = torch.ones(B, 4, device=dev)
+    v0, a0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
+    vp0, ap0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
+    wv, wa = torch.randn(d, device=dev), torch.randn(d, device=dev)
+
+    def run(amp=True):
+        enc.zero_grad(set_to_none=True)
+        v, a = v0.clone().requires_grad_(True), a0.clone().requires_grad_(True)
+        vp, ap = vp0.clone().requires_grad_(True), ap0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            ov, oa = enc(v, vts, vlsi, ones, vp, None, a, ats, alsi, ones, ap, None)
+        # weighted: a plain sum of LayerNorm outputs has ~zero gradient (rounding noise only)
+        (ov.float() * wv).sum().add_((oa.float() * wa).sum()).backward()
+        return (ov.detach(), oa.detach()), [v.grad, a.grad, vp.grad, ap.grad] + [
+            p.grad.clone() for p in enc.parameters()]
+
+    o1, g1 = run()
+    monkeypatch.setattr(MT, "carry_supported", lambda *a: False)
+    o2, g2 = run()
+    _, g3 = run(amp=False)
+    for a, b in zip(o1, o2):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
+    for a, b, c in zip(g1, g2, g3):
+        torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -7 * b.abs().max().item())
+        assert (a - c).norm() <= 1.25 * (b - c).norm() + 1e-6 * c.norm()
