@@ -4,7 +4,7 @@
 // also writes a byte mask, and in the backward a masked-scale kernel plus relu's
 // threshold_backward, each a full pass over the (tokens x d_ffn) hidden tensor.  Here:
 //   forward : out = relu(x) * keep * 1/(1-p), one read of x and one write of out; keep bits from a
-//             64-bit mix of (device seed, element index), as in add_layernorm.hip;
+//             64-bit mix of (device seed, element index / 4), 16 bits per element;
 //   backward: dx = dy * 1/(1-p) where out > 0, else 0 (out > 0 exactly when x > 0 and the element
 //             was kept), from the output linear2 keeps anyway: no mask, no RNG.
 // bf16 in and out, 8 elements (16 bytes) per lane, grid-stride over n / 8 vectors.
@@ -27,14 +27,16 @@ __device__ __forceinline__ uint32_t rne(float f) {
   return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
 }
 
-__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t e) {
-  uint64_t x = seed * 0x9E3779B97F4A7C15ull + e;
+// 64 random bits per 4 consecutive elements (one 64-bit mix of (seed, e / 4)), 16 per element:
+// the mix's 64-bit multiplies, not HBM, bounded the forward with one mix per element
+__device__ __forceinline__ uint64_t drop_bits4(uint64_t seed, uint64_t quad) {
+  uint64_t x = seed * 0x9E3779B97F4A7C15ull + quad;
   x ^= x >> 33;
   x *= 0xff51afd7ed558ccdull;
   x ^= x >> 33;
   x *= 0xc4ceb9fe1a85ec53ull;
   x ^= x >> 33;
-  return (uint32_t)x;
+  return x;
 }
 
 __device__ __forceinline__ float lo(uint32_t w) { return __uint_as_float(w << 16); }
@@ -48,13 +50,18 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_fwd(const uint4* __rest
     const uint4 v = x[i];
     const uint32_t w[4] = {v.x, v.y, v.z, v.w};
     uint32_t o[4];
+    uint64_t bits[2] = {0ull, 0ull};
+    if (seed_ptr) {
+      bits[0] = drop_bits4(seed, (uint64_t)i * 2);
+      bits[1] = drop_bits4(seed, (uint64_t)i * 2 + 1);
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       float a = fmaxf(lo(w[j]), 0.f), b = fmaxf(hi(w[j]), 0.f);
-      if (seed_ptr) {
-        const uint64_t e = (uint64_t)i * 8 + 2 * j;
-        a = (drop_bits(seed, e) >> 8) >= thresh ? a * scale : 0.f;
-        b = (drop_bits(seed, e + 1) >> 8) >= thresh ? b * scale : 0.f;
+      if (seed_ptr) {  // elements 2j, 2j+1 of the vector: 16-bit draws (2j % 4), (2j % 4) + 1 of bits[j / 2]
+        const uint64_t q = bits[j >> 1] >> (32 * (j & 1));
+        a = (uint32_t)(q & 0xffffu) >= thresh ? a * scale : 0.f;
+        b = (uint32_t)((q >> 16) & 0xffffu) >= thresh ? b * scale : 0.f;
       }
       o[j] = rne(a) | (rne(b) << 16);
     }
@@ -121,7 +128,7 @@ int mfl_relu_dropout_forward(const void* x, int64_t n, float p_drop, const int64
   if (!args_ok("mfl_relu_dropout_forward", n, x, out, out, p_drop)) return 1;
   if (n == 0) return 0;
   const long long nvec = n / 8;
-  const uint32_t thresh = (uint32_t)fminf(p_drop * 16777216.f, 16777216.f);
+  const uint32_t thresh = (uint32_t)fminf(p_drop * 65536.f + 0.5f, 65536.f);  // keep iff 16-bit draw >= p * 2^16
   const float scale = seed ? 1.f / (1.f - p_drop) : 1.f;
   hipLaunchKernelGGL(relu_dropout_fwd, dim3(grid_for(nvec)), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
                      static_cast<const uint4*>(x), nvec, seed, thresh, scale, static_cast<uint4*>(out));
