@@ -57,7 +57,17 @@ class KernelTimer:
         _timer = None
         return False
 
+    # Eager steps are host-bound: an idle GPU would take the start event as soon as it is
+    # queued and then wait for the host to issue the launch (the ctypes call), which inflates
+    # the kernel time.  A short device spin queued first keeps the GPU busy until both the
+    # event and the launch are queued, so the events bracket the kernel alone.
+    SPIN_CYCLES = 200_000
+
     def _begin(self):
+        try:
+            torch.cuda._sleep(self.SPIN_CYCLES)
+        except (AttributeError, RuntimeError):
+            pass
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
         return ev
