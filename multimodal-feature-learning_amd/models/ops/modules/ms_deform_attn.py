@@ -100,6 +100,7 @@ class MSDeformAttn(nn.Module):
         # 1-D -> 2-D lift (H = 1, W = T_l; y = 0.5), reference ms_deform_attn.py:114-117
         loc = torch.stack((loc, 0.5 * loc.new_ones(loc.shape)), -1)
         shapes2d = torch.as_tensor([[1, t] for t in shapes], dtype=torch.long, device=query.device)
+        shapes2d._mfl_host = tuple(shapes)  # read by msda.host_levels instead of the device tensor
         return value, shapes2d, loc, aw
 
     def forward(self, query, reference_points, input_flatten, input_spatial_shapes, input_level_start_index,
@@ -112,7 +113,34 @@ class MSDeformAttn(nn.Module):
 
 class MSDeformAttnCap(MSDeformAttn):
     """reference ms_deform_attn_for_caption.py: returns the per-sample values
-    (``return_value=True`` of the 2-D border core) instead of the weighted sum."""
+    (``return_value=True`` of the 2-D border core) instead of the weighted sum.
+
+    Differs from ``MSDeformAttn`` as the reference does: the offset / weight projections read
+    2*d_model queries (:54-55) and the offset grid is centred over the points (:67)."""
+
+    def __init__(self, d_model=256, n_levels=4, n_heads=8, n_points=4):
+        nn.Module.__init__(self)
+        if d_model % n_heads != 0:
+            raise ValueError('d_model must be divisible by n_heads, but got {} and {}'.format(d_model, n_heads))
+        if not _is_power_of_2(d_model // n_heads):
+            warnings.warn("You'd better set d_model in MSDeformAttn to make the dimension of each attention "
+                          "head a power of 2 which is more efficient in our CUDA implementation.")
+        self.im2col_step = 64
+        self.d_model = d_model
+        self.n_levels = n_levels
+        self.n_heads = n_heads
+        self.n_points = n_points
+        self.sampling_offsets = Linear(2 * d_model, n_heads * n_levels * n_points)
+        self.attention_weights = Linear(2 * d_model, n_heads * n_levels * n_points)
+        self.value_proj = Linear(d_model, d_model)
+        self.output_proj = Linear(d_model, d_model)
+        self._reset_parameters()
+
+    def _reset_parameters(self):
+        super()._reset_parameters()
+        with torch.no_grad():
+            grid = self.sampling_offsets.bias.view(self.n_heads, self.n_levels, self.n_points)
+            grid.sub_(grid.mean(2, keepdim=True))
 
     def forward(self, query, reference_points, input_flatten, input_spatial_shapes, input_level_start_index,
                 input_padding_mask=None):

@@ -21,18 +21,23 @@ Follows:
   * padding "zeros" — the dormant CUDA extension on the 1-D (H=1) lift:
     models/ops/src/cuda/ms_deform_im2col_cuda.cuh:34-85 (im2col_bilinear), :238-300
     (forward, sample skipped unless -1 < w_im < W) and :88-160 (col2im_bilinear:
-    grad_w = W * aw * <grad_out, v_high - v_low>).  No reference run pins this mode
-    (CUDA-only, unbuildable here): parity for "zeros" is pinned by this restatement only.
+    grad_w = W * aw * <grad_out, v_high - v_low>).  The kernel itself is CUDA-only and
+    unbuildable here; the mode is pinned against the comparator of the reference's own kernel
+    test (models/ops/test.py:38-39, the 2-D core of ops/functions/ms_deform_attn_func.py:44-71)
+    run with grid_sample's padding set to the kernel's zeros (tests/golden/ops_api_f64.pt).
+  * msda_h1 — the extension API's (..., 2) [x, y] form on H = 1 maps (row weight of y folded
+    into the attention weight, cuh:34-160).
 
 Pinned: border mode against golden vectors produced by the real reference
-(tests/golden/make_golden.py imports /root/reference on CPU) — see tests/test_oracle.py.
+(tests/golden/make_golden.py imports /root/reference on CPU), zeros mode and the 2-D form
+against ops_api_f64 — see tests/test_oracle.py.
 
 All arithmetic happens in the dtype of ``value`` (float32 or float64) in the reference's
 operation order for the coordinates, so tap indices are bit-identical to ATen's.
 """
 import numpy as np
 
-__all__ = ["taps", "msda_forward", "msda_backward", "level_starts"]
+__all__ = ["taps", "msda_forward", "msda_backward", "level_starts", "row_weight_h1", "msda_h1"]
 
 
 def level_starts(shapes):
@@ -154,3 +159,36 @@ def msda_backward(value, shapes, loc, aw, grad_out, starts=None, padding="border
         np.add.at(gvl, (b, i1, m), c1)
         gv[:, starts[l]:starts[l] + T] += gvl
     return gv, gl, ga
+
+
+def row_weight_h1(y, padding):
+    """Weight of the single row of an H = 1 map and its y-derivative, for the 2-D extension API
+    ((L, 2) [H, W] shapes, (..., 2) [x, y] locations; models/ops/modules/ms_deform_attn.py:114-117).
+
+    zeros — cuh:34-85 / 88-160: h = y*H - 0.5, the sample lives iff -1 < h < H; h_low = floor(h);
+    row 0 is h_low (weight 1 - (h - h_low)) when h >= 0, else h_high (weight h - h_low); the y
+    gradient is H * (+-1) * aw * <grad, x-sample>.
+    border — grid_sample border on one row: y clamps to row 0, weight 1, zero y-gradient."""
+    y = np.asarray(y)
+    dt = y.dtype.type
+    if padding == "border":
+        return np.ones_like(y), np.zeros_like(y)
+    h = y - dt(0.5)
+    live = (h > dt(-1)) & (h < dt(1))
+    upper = h >= 0
+    rw = np.where(live, np.where(upper, dt(1) - h, h + dt(1)), dt(0)).astype(y.dtype)
+    drw = np.where(live, np.where(upper, dt(-1), dt(1)), dt(0)).astype(y.dtype)
+    return rw, drw
+
+
+def msda_h1(value, shapes, loc2, aw, grad_out, padding="zeros"):
+    """The extension API's 2-D form on H = 1 maps: (out, grad_value, grad_loc2 (...,2), grad_aw).
+    The row weight folds into the attention weight; the x part is msda_forward / msda_backward."""
+    loc2 = np.asarray(loc2)
+    x, y = loc2[..., 0], loc2[..., 1]
+    rw, drw = row_weight_h1(y, padding)
+    aw = np.asarray(aw)
+    out = msda_forward(value, shapes, x, aw * rw, padding=padding)
+    gv, gx, ga_eff = msda_backward(value, shapes, x, aw * rw, grad_out, padding=padding)
+    gy = aw * drw * ga_eff
+    return out, gv, np.stack([gx, gy], -1), ga_eff * rw

@@ -29,6 +29,13 @@ Fixtures:
   sparse_f64.pt              SparseDeformableTransformer (rho=0.3: mask predictor, top-k encoder
                              queries scattered back; 2 enc + 2 dec, d=64) fwd + grads, with the
                              decoder attention map of its own sampling locations.
+  ops_api_f64.pt             the extension-API 2-D form: ops/functions/ms_deform_attn_func.py:44-71 on
+                             (L,2) [H=1, W] shapes with (...,2) [x, y] locations, border as written and
+                             with zero padding (the extension kernel's; see _zeros_padding), y-grads;
+                             return_value stacks of that core and of attention.py:376-378.
+  ops_module_f64.pt          ops/modules MSDeformAttn (through the zero-padding kernel, as on a GPU) and
+                             MSDeformAttnCap (border, return_value), enc / dec, padding mask.
+  transformer_bf16.pt        transformer_f64's model and inputs under torch.autocast('cpu', bfloat16).
 
 usage: make_golden.py [case ...]   (default: every case; e.g. ``make_golden.py dam sparse``)
 """
@@ -332,6 +339,170 @@ def sparse_case(ref, seed=53):
                      "query_embedding": {k: p.grad.clone() for k, p in query_embedding.named_parameters()}})
 
 
+class _zeros_padding:
+    """Inside the reference's ops core (models/ops/functions/ms_deform_attn_func.py:61-62) force
+    ``F.grid_sample``'s padding to 'zeros': the padding of the extension kernel that the reference's
+    own test compares this core against (models/ops/test.py:38-39; ms_deform_im2col_cuda.cuh:34-85).
+    Only the module attribute ``F`` of the imported module object is swapped, for the duration."""
+
+    def __init__(self, ref):
+        self.mod = ref.ops_func
+
+    def __enter__(self):
+        real = torch.nn.functional
+
+        def grid_sample(*args, **kw):
+            kw["padding_mode"] = "zeros"
+            return real.grid_sample(*args, **kw)
+
+        self.saved = self.mod.F
+        self.mod.F = types.SimpleNamespace(grid_sample=grid_sample)
+        return self
+
+    def __exit__(self, *exc):
+        self.mod.F = self.saved
+        return False
+
+
+def _import_ops(ref):
+    import models.ops.functions.ms_deform_attn_func as ops_func  # noqa: E402 (extension import is try/except)
+    import models.ops.modules.ms_deform_attn as ops_mod  # noqa: E402
+    import models.ops.modules.ms_deform_attn_for_caption as ops_cap  # noqa: E402
+    ref.ops_func, ref.ops_mod, ref.ops_cap = ops_func, ops_mod, ops_cap
+    return ref
+
+
+def ops_api_case(ref, seed=61):
+    """The extension-API forms: the reference's 2-D core
+    (ops/functions/ms_deform_attn_func.py:44-71) on (L,2) [H=1, W=T] shapes with (...,2) [x, y]
+    locations — border as written, and zeros (the extension kernel's padding, see _zeros_padding) —
+    with all gradients including y; the ``return_value`` stacks of both cores (ops :67-68 and the
+    live attention.py:376-378) with the gradients of a weighted sum of the stack."""
+    _import_ops(ref)
+    gen = torch.Generator().manual_seed(seed)
+    shapes, B, M, D, Lq, P = [32, 16, 8, 4], 2, 4, 8, 20, 4
+    L, S = len(shapes), sum(shapes)
+    value = torch.randn((B, S, M, D), generator=gen, dtype=torch.float64)
+    x = _edge_points(_locations(gen, (B, Lq, M, L, P), torch.float64), shapes)
+    y = torch.rand((B, Lq, M, L, P), generator=gen, dtype=torch.float64) * 2.2 - 0.6  # row weight live in (-0.5, 1.5)
+    loc2 = torch.stack([x, y], -1)
+    aw = _attn(gen, (B, Lq, M, L, P), torch.float64)
+    gout = torch.randn((B, Lq, M * D), generator=gen, dtype=torch.float64)
+    shp2 = torch.tensor([[1, t] for t in shapes], dtype=torch.long)
+    out = dict(value=value, loc2=loc2, aw=aw, grad_out=gout, shapes2d=shp2)
+    for mode in ("border", "zeros"):
+        v, lc, a = (t.clone().requires_grad_(True) for t in (value, loc2, aw))
+        if mode == "zeros":
+            with _zeros_padding(ref):
+                o = ref.ops_func.ms_deform_attn_core_pytorch(v, shp2, lc, a)
+        else:
+            o = ref.ops_func.ms_deform_attn_core_pytorch(v, shp2, lc, a)
+        o.backward(gout)
+        out[mode] = dict(out=o.detach(), grad_value=v.grad, grad_loc=lc.grad, grad_aw=a.grad)
+    # return_value stacks: (B*M, D, Lq, L, P)
+    w_stack = torch.randn((B * M, D, Lq, L, P), generator=gen, dtype=torch.float64)
+    out["w_stack"] = w_stack
+    for name in ("ops_border", "ops_zeros", "live"):
+        v, lc, a = (t.clone().requires_grad_(True) for t in (value, loc2, aw))
+        if name == "live":
+            st = ref.attention.ms_deform_attn_core_pytorch(v, torch.tensor(shapes).unsqueeze(-1), lc[..., :1], a,
+                                                           return_value=True)
+        elif name == "ops_zeros":
+            with _zeros_padding(ref):
+                st = ref.ops_func.ms_deform_attn_core_pytorch(v, shp2, lc, a, return_value=True)
+        else:
+            st = ref.ops_func.ms_deform_attn_core_pytorch(v, shp2, lc, a, return_value=True)
+        (st * w_stack).sum().backward()
+        out["stack_" + name] = dict(stack=st.detach(), grad_value=v.grad, grad_loc=lc.grad)
+    return out
+
+
+def ops_module_case(ref, seed=67):
+    """The extension-backed modules: ops/modules/ms_deform_attn.py ``MSDeformAttn`` (1-D -> 2-D lift,
+    zero-init attention weights) as it runs on a GPU, i.e. through the zero-padding kernel
+    (:119-122; reproduced by _zeros_padding on the CPU core), and ``MSDeformAttnCap``
+    (ms_deform_attn_for_caption.py: 2*d_model queries, border core with return_value).
+    Attention-weight and offset weights are randomised so the softmax and locations are generic."""
+    _import_ops(ref)
+    torch.manual_seed(seed)
+    d_model, L, M, P, B = 32, 4, 4, 4, 2
+    shapes = [32, 16, 8, 4]
+    S = sum(shapes)
+    gen = torch.Generator().manual_seed(seed)
+    shp = torch.tensor(shapes, dtype=torch.long)
+    start = torch.cat((shp.new_zeros(1), shp.cumsum(0)[:-1]))
+    mask = torch.zeros(B, S, dtype=torch.bool)
+    for T, s0 in zip(shapes, start.tolist()):
+        mask[1, s0 + (3 * T) // 4:s0 + T] = True
+    res = {"shapes": shp}
+    for name, cls, qdim in (("attn", ref.ops_mod.MSDeformAttn, d_model), ("cap", ref.ops_cap.MSDeformAttnCap,
+                                                                          2 * d_model)):
+        m = cls(d_model, L, M, P).double()
+        with torch.no_grad():
+            for lin in (m.sampling_offsets, m.attention_weights):
+                lin.weight.copy_(torch.randn(lin.weight.shape, generator=gen, dtype=torch.float64) * 0.05)
+        entry = {"state_dict": _compact(m.state_dict())}
+        for case, Lq, refdim in (("enc", S, 1), ("dec", 12, 2)):
+            if refdim == 1:
+                refp = torch.rand((B, Lq, 1), generator=gen, dtype=torch.float64)[:, :, None].expand(B, Lq, L, 1)
+            else:
+                c = torch.rand((B, Lq, 1), generator=gen, dtype=torch.float64) * 0.8 + 0.1
+                w = torch.rand((B, Lq, 1), generator=gen, dtype=torch.float64) * 0.3 + 0.05
+                refp = torch.cat([c, w], -1)[:, :, None].expand(B, Lq, L, 2)
+            refp = refp.contiguous()
+            query = torch.randn((B, Lq, qdim), generator=gen, dtype=torch.float64).requires_grad_(True)
+            flat = torch.randn((B, S, d_model), generator=gen, dtype=torch.float64).requires_grad_(True)
+            m.zero_grad()
+            if name == "attn":
+                with _zeros_padding(ref):
+                    y = m(query, refp, flat, shp, start, mask)
+            else:
+                y = m(query, refp, flat, shp, start, mask)
+            gout = torch.randn(y.shape, generator=gen, dtype=torch.float64)
+            y.backward(gout)
+            entry[case] = dict(query=query.detach(), reference_points=refp, input_flatten=flat.detach(),
+                               grad_out=gout, output=y.detach(), grad_query=query.grad, grad_input_flatten=flat.grad,
+                               param_grads={k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None})
+        entry["padding_mask"] = mask
+        res[name] = entry
+    return res
+
+
+def transformer_bf16_case(ref):
+    """transformer_f64's model and inputs, run by the reference in fp32 under
+    ``torch.autocast('cpu', torch.bfloat16)``: the bench's precision regime executed by the
+    reference itself (grid_sample stays fp32 there: it is on autocast's promote list)."""
+    g = torch.load(os.path.join(HERE, "transformer_f64.pt"), weights_only=True)
+    d_model, heads = 64, 4
+    pos_embed = ref.embedding_layers.PositionEmbeddingVideoSine(d_model // 2, normalize=True)
+    base = ref.base_encoder.BaseEncoder(4, d_model, d_model)
+    tr = ref.uni.DeformableTransformer(d_model=d_model, num_head=heads, num_encoder_layers=2, num_decoder_layers=2,
+                                       dim_feedforward=128, dropout=0.0, return_intermediate_dec=True,
+                                       num_feature_levels=4, dec_n_points=4, enc_n_points=4)
+    qe = torch.nn.Embedding(g["state_dicts"]["query_embedding"]["weight"].shape[0], d_model * 2)
+    named = {"pos_embed": pos_embed, "base_encoder": base, "transformer": tr, "query_embedding": qe}
+    for n, m in named.items():
+        m.load_state_dict({k: v.float() if v.is_floating_point() else v for k, v in g["state_dicts"][n].items()})
+    video = g["video"].float().requires_grad_(True)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        srcs, masks, pos = base(video, g["mask"], g["durations"].float(), pos_embed)
+        src_flatten, shapes, starts, valid, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(srcs, masks, pos)
+        memory = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten)
+        B = video.shape[0]
+        qmask = torch.ones(B, qe.weight.shape[0], dtype=torch.bool)
+        _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qe.weight)
+        hs, inter = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten, qmask, False)
+    loss = (hs.float() * g["w_hs"].float()).sum() + (memory.float() * g["w_mem"].float()).sum()
+    loss.backward()
+    rel = lambda a, b: ((a.double() - b).norm() / b.norm()).item()  # noqa: E731
+    print("reference bf16-autocast vs its fp64 run: memory %.3e hs %.3e grad_video %.3e" % (
+        rel(memory.detach(), g["memory"]), rel(hs.detach(), g["hs"]), rel(video.grad, g["grad_video"])))
+    return dict(memory=memory.detach().float(), hs=hs.detach().float(), memory_dtype=str(memory.dtype),
+                grad_video=video.grad.clone(),
+                param_grads={n: {k: p.grad.clone() for k, p in m.named_parameters() if p.grad is not None}
+                             for n, m in named.items()})
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = import_reference()
@@ -345,6 +516,9 @@ def main():
         "multimodal_f64": lambda: multimodal_case(ref),
         "dam_f32": lambda: dam_case(ref),
         "sparse_f64": lambda: sparse_case(ref),
+        "ops_api_f64": lambda: ops_api_case(ref),
+        "ops_module_f64": lambda: ops_module_case(ref),
+        "transformer_bf16": lambda: transformer_bf16_case(ref),
     }
     wanted = sys.argv[1:] or list(cases)
     for name, fn in cases.items():

@@ -156,3 +156,12 @@ def test_multimodal_matches_reference(golden):
     for k, p in tr.named_parameters():
         if k in g["param_grads"]["transformer"]:
             _close(p.grad, g["param_grads"]["transformer"][k], rtol=1e-7, atol=1e-9)
+
+
+def test_cap_module_init_matches_reference_layout(golden):
+    """MSDeformAttnCap keeps the reference's 2*d_model query projections and centred offset grid."""
+    g = golden("ops_module_f64")
+    sd = g["cap"]["state_dict"]
+    m = M.ops.modules.MSDeformAttnCap(32, 4, 4, 4)
+    assert {k: tuple(v.shape) for k, v in m.state_dict().items()} == {k: tuple(v.shape) for k, v in sd.items()}
+    torch.testing.assert_close(m.sampling_offsets.bias, sd["sampling_offsets.bias"].float())

@@ -143,3 +143,20 @@ def test_oracle_gradient_matches_finite_differences(padding):
             fm = f(value, loc, aw)
             arr.flat[i] = saved
             np.testing.assert_allclose((fp - fm) / (2 * eps), grad.flat[i], rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("padding", ["zeros", "border"])
+def test_oracle_2d_form_matches_reference_ops_core(golden, padding):
+    """ZEROS and the (L,2) / (...,2) extension form pinned: the reference's 2-D core
+    (ops/functions/ms_deform_attn_func.py:44-71) on H = 1 maps, border as written and with the
+    extension kernel's zero padding (tests/golden/make_golden.py::ops_api_case), incl. the y-gradient."""
+    g = golden("ops_api_f64")
+    shapes = [int(w) for _, w in g["shapes2d"].tolist()]
+    r = g[padding]
+    out, gv, gl, ga = O.msda_h1(_np(g["value"]), shapes, _np(g["loc2"]), _np(g["aw"]), _np(g["grad_out"]), padding)
+    np.testing.assert_allclose(out, _np(r["out"]), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(gv, _np(r["grad_value"]), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(ga, _np(r["grad_aw"]), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(gl, _np(r["grad_loc"]), rtol=1e-11, atol=1e-10)
+    if padding == "zeros":
+        assert (_np(r["grad_loc"])[..., 1] != 0).any()  # the y-gradient is exercised
