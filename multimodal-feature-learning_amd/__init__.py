@@ -39,7 +39,12 @@ from .models.sparse import unimodal_sparse_deformable_transformer  # noqa: E402,
 from .models.ops.functions import ms_deform_attn_func  # noqa: E402,F401
 from .models.ops.modules import ms_deform_attn  # noqa: E402,F401
 from . import utils  # noqa: E402,F401
-from .utils import dam  # noqa: E402,F401
+from .utils import dam, box_ops, preds_postprocess  # noqa: E402,F401
+from .models import matcher, load_weights, dvc_common  # noqa: E402,F401
+from .models.modules import layers  # noqa: E402,F401
+from .models import unimodal_caption_decoder, multimodal_caption_decoder  # noqa: E402,F401
+from .models.deformable import unimodal_deformable_dvc, multimodal_deformable_dvc  # noqa: E402,F401
+from .models.sparse import unimodal_sparse_dvc  # noqa: E402,F401
 from . import dvc_core  # noqa: E402,F401
 from . import train_step  # noqa: E402,F401
 

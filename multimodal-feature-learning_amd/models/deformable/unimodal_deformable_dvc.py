@@ -1,0 +1,194 @@
+"""``UnimodalDeformableDVC``, reference models/deformable/unimodal_deformable_dvc.py:26-549, with the
+reference constructor, state_dict keys and ``forward(obj, is_training=True, faster_eval=False)``
+returning ``(out, captions, indices, indices_aux, mask)`` as engine.py:62 consumes it.
+
+The proposal path (BaseEncoder -> deformable encoder / decoder on the HIP MSDA kernel -> shared
+heads) is the bench workload; the caption path (matching, crop, caption decoder) follows.
+
+At HEAD the reference forward cannot run: its caption-decoder call passes the
+caption padding mask as ``memory_mask`` and the memory mask as ``tgt_padding_mask`` (:277-279 vs
+models/unimodal_caption_decoder.py:68), and without the differentiable mask ``pred_memory_mask`` is
+unbound (:264).  Restated intent, which is also what the working UnimodalSparseDVC does
+(models/sparse/unimodal_sparse_dvc.py:279-281): captions self-attend under the look-ahead and
+caption padding masks, and cross-attend to the matched segment's memory under its crop mask.
+That argument order is the only change: everything else computes what the reference's code does
+as written — including level l > 0 cropping level l-1's crop (``memory`` is rebound, :235) — and is
+pinned against the reference run with just that call fixed (tests/golden/deformable_dvc_f64.pt;
+the reference also needs ``use_differentiable_mask=True`` to run at all, :264).  Inference decodes
+with a KV cache: the same rows as the reference's full re-decode, one pass per word, last level only
+(the only level its token choice reads, :334-338)."""
+import math
+from math import ceil
+
+import torch
+from torch import nn
+
+from ..base_encoder import build_base_encoder
+from ..dvc_common import (append_end_token, context_mask, make_padding_mask, make_tgt_mask, segment_memory,
+                          special_tokens)
+from ..modules.embedding_layers import PositionEmbeddingVideoSine
+from ..modules.layers import FFN, ContextMaskModel
+from ..modules.linear import Linear
+from ..modules.misc_modules import predict_event_num
+from ..unimodal_caption_decoder import build_unimodal_caption_decoder
+from .unimodal_deformable_transformer import build_unimodal_deformable_transformer
+
+__all__ = ["UnimodalDeformableDVC"]
+
+
+class UnimodalDeformableDVC(nn.Module):
+    def __init__(self, input_modalities, num_queries, d_model, num_classes, aux_loss, matcher, threshold,
+                 max_eseq_length, vocab, seq_len, embedding_matrix, detr_args, caption_args,
+                 use_differentiable_mask=False):
+        super().__init__()
+        self.input_modalities = input_modalities
+        self.num_queries = num_queries
+        self.aux_loss = aux_loss
+        self.threshold = threshold
+        self.query_embedding = nn.Embedding(num_queries, d_model * 2)
+        self.class_embedding = Linear(d_model, num_classes + 1)
+        self.segment_embedding = FFN(in_dim=d_model, hidden_dim=d_model, out_dim=2, num_layers=3)
+        self.count_head = Linear(d_model, max_eseq_length + 1)
+        self.matcher = matcher
+        assert 'video' in input_modalities or 'audio' in input_modalities, \
+            f'input_modalities should contain one of "video" or "audio". You have {input_modalities}'
+        self.pos_embed = PositionEmbeddingVideoSine(d_model // 2, normalize=True)
+        self.base_encoder = build_base_encoder(detr_args)
+        prior_prob = 0.01
+        bias_value = -math.log((1 - prior_prob) / prior_prob)
+        self.class_embedding.bias.data = torch.ones(num_classes + 1) * bias_value
+        nn.init.constant_(self.segment_embedding.layers[-1].weight.data, 0)
+        nn.init.constant_(self.segment_embedding.layers[-1].bias.data, 0)
+        self.unimodal_deformable_transformer = build_unimodal_deformable_transformer(detr_args)
+        num_pred = detr_args.dec_layers
+        nn.init.constant_(self.segment_embedding.layers[-1].bias.data[2:], -2.0)
+        # heads shared by every decoder level (reference :72-74)
+        self.class_embedding = nn.ModuleList([self.class_embedding for _ in range(num_pred)])
+        self.count_head = nn.ModuleList([self.count_head for _ in range(num_pred)])
+        self.segment_embedding = nn.ModuleList([self.segment_embedding for _ in range(num_pred)])
+        self.num_feature_levels = detr_args.num_feature_levels
+        self.video_rescale_len = detr_args.video_rescale_len
+        self.num_tokens = ceil(((2 ** self.num_feature_levels - 1) / 2 ** (self.num_feature_levels - 1))
+                               * self.video_rescale_len)
+        self.use_differentiable_mask = use_differentiable_mask
+        if use_differentiable_mask:
+            self.context_mask_model = ContextMaskModel(in_dim=(2 + d_model), out_dim=self.num_tokens)
+        self.seq_len = seq_len
+        self.vocab = vocab
+        self.unimodal_caption_decoder = build_unimodal_caption_decoder(caption_args, len(vocab), seq_len,
+                                                                       embedding_matrix)
+
+    # --- proposal path ------------------------------------------------------------------------
+    def forward_proposals(self, video, video_mask, durations):
+        """BaseEncoder + deformable encoder / decoder + shared heads (reference :135-203).
+        -> (out, query_features (depth, B, Q, d), memory (B, S, d), heads stacked over depth)"""
+        tr = self.unimodal_deformable_transformer
+        B = video.shape[0]
+        srcs, masks, pos = self.base_encoder(video, video_mask, durations, self.pos_embed)
+        src_flatten, shapes, starts, valid, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(srcs, masks, pos)
+        memory = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten)
+        qw = self.query_embedding.weight
+        proposals_mask = torch.ones(B, qw.shape[0], device=qw.device).bool()
+        _, tgt, reference_points, qw = tr.prepare_decoder_input_query(B, qw)
+        query_features, _ = tr.forward_decoder(tgt, reference_points, memory, shapes, starts, valid, qw,
+                                               mask_flatten, proposals_mask, False)
+        classes, counts, segments = [], [], []
+        for lvl in range(query_features.shape[0]):
+            classes.append(self.class_embedding[lvl](query_features[lvl]).softmax(dim=-1))
+            segments.append(self.segment_embedding[lvl](query_features[lvl]).sigmoid())
+            counts.append(predict_event_num(self.count_head[lvl], query_features[lvl]))
+        heads = (torch.stack(classes), torch.stack(segments), torch.stack(counts))
+        out = {'pred_logits': heads[0][-1], 'pred_segments': heads[1][-1], 'pred_count': heads[2][-1]}
+        return out, query_features, memory, heads
+
+    def forward(self, obj, is_training=True, faster_eval=False):
+        video = obj['video_tensor']
+        video_mask = obj['video_mask']
+        durations = obj['video_length'][:, 1]
+        out, query_features, memory, (outputs_class, outputs_segment, outputs_count) = \
+            self.forward_proposals(video, video_mask, durations)
+        num_pred = query_features.shape[0]
+        out_aux = [{'pred_logits': outputs_class[l], 'pred_segments': outputs_segment[l],
+                    'pred_count': outputs_count[l]} for l in range(num_pred)]
+        # every level's matching in one device->host copy (reference: one .cpu() per level, :227)
+        level_indices = self.matcher.match_levels(out_aux, obj['video_target'])
+        video_durations = durations
+
+        outputs_captions, memory_list, memory_mask_list, pred_memory_mask_list = [], [], [], []
+        for lvl in range(num_pred):
+            indices = level_indices[lvl]
+            # as the reference (:235): ``memory`` is rebound to this level's crop, which the next level crops
+            idx, idx_dev, denorm, memory, key_mask = segment_memory(memory, out_aux[lvl], indices, video_durations,
+                                                                    self.num_feature_levels, self.video_rescale_len)
+            mem = memory
+            memory_mask = key_mask.unsqueeze(1).unsqueeze(1)  # (n, 1, 1, K)
+            pred_memory_mask = None
+            if self.use_differentiable_mask:
+                pred_logits, pred_bool = context_mask(self.context_mask_model, denorm, query_features[lvl][idx_dev],
+                                                      key_mask)
+                out['pred_memory_mask'] = pred_logits
+                pred_memory_mask = pred_bool.unsqueeze(1).unsqueeze(1)
+            memory_list.append(mem)
+            memory_mask_list.append(memory_mask)
+            pred_memory_mask_list.append(pred_memory_mask)
+            if is_training:
+                captions = obj['cap_tensor'][:, :-1]
+                padding_mask = obj['cap_mask'][:, :-1]
+                tgt_mask = make_tgt_mask(captions, padding_mask)
+                cross_mask = pred_memory_mask if self.use_differentiable_mask else memory_mask
+                output_caption = self.unimodal_caption_decoder(captions, mem, tgt_mask=tgt_mask, memory_mask=cross_mask,
+                                                               tgt_padding_mask=padding_mask)
+                outputs_captions.append(output_caption[-1])
+
+        mask_out = memory_mask_list[-1].squeeze().float() if self.use_differentiable_mask else None
+        if is_training:
+            outputs_caption = torch.stack(outputs_captions)
+            out['pred_captions'] = outputs_caption[-1]
+            outputs_caption_last_layer = torch.argmax(outputs_caption[-1], dim=2)
+            indices_aux = []
+            if self.aux_loss:
+                out['aux_outputs'] = self._set_aux_loss(outputs_class, outputs_segment, outputs_count, outputs_caption)
+                indices_aux = level_indices[:len(out['aux_outputs'])]  # same segments -> same assignment
+            return out, outputs_caption_last_layer, indices, indices_aux, mask_out
+
+        # inference: greedy decode of the last level (the reference's token choice reads only it, :334-338)
+        bos, eos, pad = special_tokens(self.vocab)
+        cross = pred_memory_mask_list if self.use_differentiable_mask else memory_mask_list
+        key_mask = cross[-1][:, 0, 0, :]
+        captions, last_input = self.unimodal_caption_decoder.greedy_decode(memory_list[-1], key_mask, bos, eos, pad,
+                                                                           self.seq_len - 1, faster_eval)
+        out['pred_captions'] = self._caption_probs(last_input, memory_list[-1], cross[-1])
+        captions_with_eos = append_end_token(captions, self.vocab, faster_eval)
+        indices_aux = []
+        if self.aux_loss:
+            # the reference's aux captions are the other levels' outputs at the first word (:367)
+            first = torch.full_like(captions, pad)
+            first[:, 0] = bos
+            aux_caps = [self._caption_probs(first, memory_list[l], cross[l]) for l in range(num_pred - 1)]
+            out['aux_outputs'] = self._set_aux_loss(outputs_class, outputs_segment, outputs_count, aux_caps + [None])
+            indices_aux = level_indices[:len(out['aux_outputs'])]
+        return out, captions_with_eos, indices, indices_aux, mask_out
+
+    @torch.no_grad()
+    def _caption_probs(self, captions, mem, cross_mask):
+        padding = make_padding_mask(captions, self.vocab)
+        return self.unimodal_caption_decoder(captions, mem, tgt_mask=make_tgt_mask(captions, padding),
+                                             memory_mask=cross_mask, tgt_padding_mask=padding)[-1]
+
+    def _set_aux_loss(self, outputs_class, outputs_segment, outputs_count, outputs_caption):
+        return [{'pred_logits': a, 'pred_segments': b, 'pred_count': c, 'pred_captions': d}
+                for a, b, c, d in zip(outputs_class[:-1], outputs_segment[:-1], outputs_count[:-1], outputs_caption[:-1])]
+
+    def make_tgt_mask(self, target, tgt_padding_mask):
+        return make_tgt_mask(target, tgt_padding_mask)
+
+    def make_padding_mask(self, target):
+        return make_padding_mask(target, self.vocab)
+
+    def get_segment_features(self, features, denormalized_segments, idx, video_durations):
+        return self.crop_segments(features, denormalized_segments, idx[0], video_durations)
+
+    def crop_segments(self, features, denormalized_segments, segment_batch_id, video_durations):
+        from ...utils.preds_postprocess import crop_segments
+        return crop_segments(features, denormalized_segments, segment_batch_id, video_durations,
+                             self.num_feature_levels, self.video_rescale_len)

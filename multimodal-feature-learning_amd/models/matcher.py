@@ -1,0 +1,69 @@
+"""Hungarian matching of predicted to target segments, reference models/matcher.py:14-101.
+
+Cost = cost_segment * L1(centre, length) + cost_giou * (-gIoU) on the device; the assignment is
+scipy's ``linear_sum_assignment`` on the host, as in the reference.  The reference makes one
+device->host copy per call (``.cpu()`` :86) plus two syncing asserts (utils/box_ops.py:59-60), once
+per decoder level; ``match_levels`` builds every level's cost matrix and the well-formedness flags
+on the device and moves them in ONE copy."""
+import torch
+from scipy.optimize import linear_sum_assignment
+from torch import nn
+
+from ..utils.box_ops import generalized_box_iou_unchecked, segment_cl_to_xy
+
+__all__ = ["HungarianMatcher", "build_matcher"]
+
+
+class HungarianMatcher(nn.Module):
+    def __init__(self, cost_class=1., cost_segment=1., cost_giou=1., cost_alpha=0.25, cost_gamma=2.0):
+        super().__init__()
+        self.cost_class = cost_class
+        self.cost_segment = cost_segment
+        self.cost_giou = cost_giou
+        self.cost_alpha = cost_alpha
+        self.cost_gamma = cost_gamma
+        assert cost_class != 0 or cost_segment != 0 or cost_giou != 0, "Costs cant be 0."
+
+    @torch.no_grad()
+    def forward(self, outputs, targets):
+        """outputs["pred_segments"] (B, Q, 2); targets: list of {"segments": (n_b, 2)} ->
+        [(pred_idx int64, tgt_idx int64)] per clip (reference :43-94)."""
+        return self.match_levels([outputs], targets)[0]
+
+    @torch.no_grad()
+    def match_levels(self, outputs_list, targets):
+        """``forward`` for several outputs (decoder levels) against the same targets."""
+        tgt_segments = torch.cat([v["segments"] for v in targets])
+        tgt_xy = segment_cl_to_xy(tgt_segments)
+        sizes = [len(v["segments"]) for v in targets]
+        costs, flags, shapes = [], [], []
+        for outputs in outputs_list:
+            B, Q = outputs["pred_segments"].shape[:2]
+            out_segments = outputs["pred_segments"].flatten(0, 1)
+            out_xy = segment_cl_to_xy(out_segments)
+            cost_segment = torch.cdist(out_segments, tgt_segments, p=1)
+            cost_giou = -generalized_box_iou_unchecked(out_xy, tgt_xy)
+            c = self.cost_segment * cost_segment + self.cost_giou * cost_giou
+            costs.append(c.reshape(-1).double())  # exact for fp32 costs; scipy solves in fp64
+            flags.append((out_xy[:, 1] >= out_xy[:, 0]).all().reshape(1))
+            shapes.append((B, Q))
+        flags.append((tgt_xy[:, 1] >= tgt_xy[:, 0]).all().reshape(1))
+        host = torch.cat(costs + [torch.cat(flags).double()]).cpu()  # the one device->host copy
+        ok = host[-len(flags):]
+        assert bool(ok[:-1].all()), "Segment start > Segment end (from output)"
+        assert bool(ok[-1]), "Segment start > Segment end (from target)"
+        result, off = [], 0
+        for B, Q in shapes:
+            n = B * Q * len(tgt_segments)
+            cost = host[off:off + n].view(B, Q, -1)
+            off += n
+            result.append([
+                (torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64))
+                for i, j in (linear_sum_assignment(c[b]) for b, c in enumerate(cost.split(sizes, -1)))])
+        return result
+
+
+def build_matcher(args):
+    """reference :97-101"""
+    return HungarianMatcher(cost_class=args.cost_class, cost_segment=args.cost_segment, cost_giou=args.cost_giou,
+                            cost_alpha=args.cost_alpha, cost_gamma=args.cost_gamma)

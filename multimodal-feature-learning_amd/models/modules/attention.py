@@ -12,6 +12,7 @@ models/deformable/unimodal_deformable_transformer.py:10 and friends):
   extension kernel (ms_deform_im2col_cuda.cuh:34-85).
 * ``MSDeformAttn``                  — reference attention.py:394-511.  Same constructor,
   parameter names / init and forward signature, including ``is_sparse``.
+* ``CrossAttention``                — reference attention.py:213-306 (caption decoder).
 
 There is no CPU path (see ``msda.py``).
 """
@@ -28,7 +29,8 @@ from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # referenc
 from ..ops.modules.ms_deform_attn import stack_sampled_values
 from .linear import Linear, linear_pair
 
-__all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn"]
+__all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
+           "masked_scores_softmax"]
 
 
 def _loc5(sampling_locations):
@@ -164,6 +166,70 @@ class MSDeformAttn(nn.Module):
         if is_sparse:
             return output, sampling_locations.unsqueeze(-1), attention_weights
         return output
+
+
+def masked_scores_softmax(scores, masked, scale, neg_fill=-1e20):
+    """softmax(scale * scores.masked_fill(masked, neg_fill)) over the last dim — the order of the
+    reference's CrossAttention (attention.py:288-294: fill with -1e20, then scale): a fully
+    masked row is uniform there, not NaN.  ``neg_fill=-inf`` gives nn.MultiheadAttention's."""
+    if masked is not None:
+        scores = scores.masked_fill(masked, neg_fill)
+    return (scores * scale).softmax(dim=-1)
+
+
+class CrossAttention(nn.Module):
+    """Multi-head attention of the caption decoder, reference attention.py:213-306: separate
+    ``q_linear`` / ``k_linear`` / ``v_linear`` (bias = qkv_bias), ``projection_layer``; masks are
+    boolean (True = masked) — ``attn_mask`` broadcast against (B, H, Lq, Lk), ``key_padding_mask``
+    (B, Lk) — filled with -1e20 before the 1/sqrt(hd) scale.
+
+    The weighted sum runs as one ``F.scaled_dot_product_attention`` (a fused attention kernel on
+    the GPU) with the masks folded into an additive bias of -1e20*scale: scores are O(1), so
+    ``s*scale + (-1e20*scale)`` rounds to exactly the reference's ``(-1e20)*scale`` and softmax
+    sees the same values, including uniform rows where everything is masked."""
+
+    def __init__(self, d_model, num_heads=12, qkv_bias=False, attention_dropout=0., projection_dropout=0.):
+        super().__init__()
+        self.d_model = d_model
+        self.num_heads = num_heads
+        self.head_dim = d_model // num_heads
+        assert d_model == self.head_dim * num_heads, "The model dimension must be divisible by the number of heads."
+        self.scale = self.head_dim ** -0.5
+        self.q_linear = Linear(d_model, d_model, bias=qkv_bias)
+        self.k_linear = Linear(d_model, d_model, bias=qkv_bias)
+        self.v_linear = Linear(d_model, d_model, bias=qkv_bias)
+        self.attention_dropout = nn.Dropout(attention_dropout)
+        self.projection_layer = Linear(d_model, d_model)
+
+    def _mask(self, attn_mask, key_padding_mask):
+        m = attn_mask
+        if key_padding_mask is not None:
+            kpm = key_padding_mask.unsqueeze(1).unsqueeze(1)
+            m = kpm if m is None else (m | kpm)
+        return m
+
+    def forward(self, q, k, v, attn_mask=None, key_padding_mask=None, need_weights=False):
+        assert k.shape == v.shape, (f"The keys and values inputted to the cross attention module should have the same "
+                                    f"shape. However, key has {k.shape} and value has {v.shape}.")
+        B, Lq, _ = q.shape
+        Lk = k.shape[1]
+        H, hd = self.num_heads, self.head_dim
+        q = self.q_linear(q).reshape(B, Lq, H, hd).transpose(1, 2)
+        k = self.k_linear(k).reshape(B, Lk, H, hd).transpose(1, 2)
+        v = self.v_linear(v).reshape(B, Lk, H, hd).transpose(1, 2)
+        masked = self._mask(attn_mask, key_padding_mask)
+        if need_weights:
+            att = self.attention_dropout(masked_scores_softmax(q @ k.transpose(-2, -1), masked, self.scale))
+            out = att @ v
+        else:
+            bias = None
+            if masked is not None:
+                bias = torch.zeros(masked.shape, dtype=q.dtype, device=q.device).masked_fill(masked, -1e20 * self.scale)
+            out = F.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=self.scale,
+                                                 dropout_p=self.attention_dropout.p if self.training else 0.0)
+            att = None
+        x = self.projection_layer(out.transpose(1, 2).flatten(2))
+        return x, att
 
 
 def _shape_tensor(input_spatial_shapes, shapes, device):

@@ -1,6 +1,7 @@
-"""Position embedding of the deformable path: the reference's ``PositionEmbeddingVideoSine``
-(models/modules/embedding_layers.py:185-227) and the ``FFN`` head MLP
-(models/modules/layers.py:871-906)."""
+"""Embeddings of the DVC path, reference models/modules/embedding_layers.py: the video position +
+duration embedding ``PositionEmbeddingVideoSine`` (:185-227), the caption decoder's
+``PositionalEncoding`` (:167-181) and ``VocabularyEmbedder`` (:231-261).  ``FFN`` (layers.py:871-906)
+is re-exported from ``layers`` for the importers of the first round."""
 import math
 
 import torch
@@ -8,8 +9,9 @@ from torch import nn
 
 from .misc_modules import NestedTensor
 from .linear import Linear
+from .layers import FFN  # noqa: F401  (re-export)
 
-__all__ = ["PositionEmbeddingVideoSine", "FFN"]
+__all__ = ["PositionEmbeddingVideoSine", "FFN", "PositionalEncoding", "VocabularyEmbedder"]
 
 
 class PositionEmbeddingVideoSine(nn.Module):
@@ -60,17 +62,51 @@ class PositionEmbeddingVideoSine(nn.Module):
         return self.duration_embed_layer(out)
 
 
-class FFN(nn.Module):
-    """n-layer MLP with ReLU between layers (reference layers.py:871-906)."""
+class PositionalEncoding(nn.Module):
+    """Sinusoidal token positions added to the caption embedding, then dropout (reference
+    embedding_layers.py:167-181; buffer ``pos_embedding`` (1, maxlen, d_model))."""
 
-    def __init__(self, in_dim, hidden_dim, out_dim, num_layers, dropout=0.):
+    def __init__(self, d_model, dropout, maxlen=5000):
         super().__init__()
-        self.num_layers = num_layers
-        h = [hidden_dim] * (num_layers - 1)
-        self.layers = nn.ModuleList(Linear(n, k) for n, k in zip([in_dim] + h, h + [out_dim]))
-        self.relu = nn.ReLU()
+        den = torch.exp(- torch.arange(0, d_model, 2) * math.log(10000) / d_model)
+        pos = torch.arange(0, maxlen).reshape(maxlen, 1)
+        pos_embedding = torch.zeros((maxlen, d_model))
+        pos_embedding[:, 0::2] = torch.sin(pos * den)
+        pos_embedding[:, 1::2] = torch.cos(pos * den)
+        self.dropout = nn.Dropout(dropout)
+        self.register_buffer('pos_embedding', pos_embedding.unsqueeze(0))
+
+    def forward(self, token_embedding, start=0):
+        """``start``: position of the first token (the incremental decode feeds single rows)."""
+        return self.dropout(token_embedding
+                            + self.pos_embedding[:, start:start + token_embedding.size(1), :].to(token_embedding.dtype))
+
+
+class VocabularyEmbedder(nn.Module):
+    """Token embedding times sqrt(d_model) (reference embedding_layers.py:231-261); GloVe-style
+    ``embedding_matrix`` loaded as the reference does (frozen unless emb_weights_req_grad; projected
+    by Linear + ReLU when its width differs from d_model)."""
+
+    def __init__(self, vocab_size, d_model):
+        super().__init__()
+        self.vocab_size = vocab_size
+        self.d_model = d_model
+        self.embedder = nn.Embedding(vocab_size, d_model)
 
     def forward(self, x):
-        for i, layer in enumerate(self.layers):
-            x = self.relu(layer(x)) if i < self.num_layers - 1 else layer(x)
-        return x
+        return self.embedder(x) * math.sqrt(self.d_model)
+
+    def init_word_embeddings(self, embedding_matrix, emb_weights_req_grad=True):
+        if embedding_matrix is None:
+            return
+        embedding_matrix = torch.as_tensor(embedding_matrix)
+        _, pretrained_embed_dim = embedding_matrix.shape
+        if self.d_model == pretrained_embed_dim:
+            self.embedder = self.embedder.from_pretrained(embedding_matrix)
+            self.embedder.weight.requires_grad = emb_weights_req_grad
+        else:
+            self.embedder = nn.Sequential(
+                nn.Embedding(self.vocab_size, pretrained_embed_dim).from_pretrained(embedding_matrix),
+                Linear(pretrained_embed_dim, self.d_model),
+                nn.ReLU())
+            self.embedder[0].weight.requires_grad = emb_weights_req_grad

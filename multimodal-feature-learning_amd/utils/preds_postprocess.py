@@ -1,0 +1,101 @@
+"""Post-decoder index math of the DVC wrappers, on the device:
+``get_src_permutation_idx`` and ``denormalize_segments`` (reference utils/preds_postprocess.py:16-80)
+and the memory crop of the wrappers' ``crop_segments``
+(models/deformable/unimodal_deformable_dvc.py:457-493).
+
+The reference runs these as Python loops over segments with one device->host read per element
+(``min(max(tensor, 0), d)``, ``torch.tensor([...])``) and builds the crop on the host followed by
+an upload (:476-493, ``.to(device)`` :237).  Here each is a handful of vectorised device ops with
+the same float32 operation order, so the token boundaries are bit-identical."""
+from math import floor
+
+import torch
+
+__all__ = ["get_src_permutation_idx", "denormalize_segments", "crop_segments", "level_token_ranges",
+           "captions_to_string", "pre_process"]
+
+
+def get_src_permutation_idx(indices):
+    """(batch_idx, src_idx) of the matched predictions, ordered by target index within each clip
+    (reference :16-29: ``src[argsort(tgt)]``)."""
+    batch_idx = torch.cat([torch.full_like(src, i) for i, (src, _) in enumerate(indices)])
+    src_idx = torch.cat([src[torch.sort(tgt)[1]].long() for (src, tgt) in indices])
+    return batch_idx, src_idx
+
+
+def _durations(video_durations, device):
+    if isinstance(video_durations, torch.Tensor):
+        return video_durations.to(device)
+    return torch.stack([torch.as_tensor(d) for d in video_durations]).to(device)
+
+
+def denormalize_segments(segments, video_durations, segment_batch_id):
+    """(centre, length) in [0, 1] -> (start, end) seconds, clamped to [0, duration] and ordered
+    (reference :54-80).  segments (n, 2) on any device; video_durations (B,) tensor or list of
+    0-dim tensors; segment_batch_id (n,).  Returns float32 (n, 2) on ``segments``' device."""
+    dev = segments.device
+    segments = segments.detach()  # the reference rebuilds them with torch.tensor(...): no gradient (:70-78)
+    d = _durations(video_durations, dev)[segment_batch_id.to(dev)]
+    c, l = segments[:, 0], segments[:, 1]
+    start = torch.minimum(torch.clamp(d / 2 * (2 * c - l), min=0), d)
+    end = torch.clamp(torch.minimum(d / 2 * (2 * c + l), d), min=0)
+    seg = torch.stack([start, end], 1).float()
+    swap = ~(seg[:, 0] < seg[:, 1])
+    return torch.where(swap[:, None], seg.flip(1), seg)
+
+
+def level_token_ranges(num_feature_levels, video_rescale_len):
+    """[(lower, upper)) token range of each pyramid level in the flattened memory (reference
+    crop_segments :481-484)."""
+    out = []
+    for n in range(num_feature_levels):
+        lower = floor(video_rescale_len * ((2 ** n - 1) / 2 ** (n - 1)))
+        upper = floor(video_rescale_len * ((2 ** (n + 1) - 1) / 2 ** n))
+        out.append((lower, upper))
+    return out
+
+
+def crop_segments(features, denormalized_segments, segment_batch_id, video_durations, num_feature_levels,
+                  video_rescale_len):
+    """Memory rows of each matched segment: per level, tokens [start, end) with
+    start / end = clamp(round(lower + diff * t / duration), lower, upper - 1) (reference :457-493);
+    other rows 0 and masked.  -> (features (n, K, d), padding mask (n, K) bool, True = masked)."""
+    n = denormalized_segments.shape[0]
+    K = features.shape[1]
+    dev = features.device
+    seg = denormalized_segments.to(dev, torch.float32)
+    bid = segment_batch_id.to(dev)
+    dur = _durations(video_durations, dev)[bid]  # its own dtype: the reference promotes seg / dur the same way
+    tok = torch.arange(K, device=dev)
+    keep = torch.zeros(n, K, dtype=torch.bool, device=dev)
+    for lower, upper in level_token_ranges(num_feature_levels, video_rescale_len):
+        diff = upper - lower
+        s = torch.clamp((lower + (diff * seg[:, 0] / dur)).round().long(), min=lower, max=upper - 1)
+        e = torch.clamp((lower + (diff * seg[:, 1] / dur)).round().long(), min=lower, max=upper - 1)
+        keep |= (tok[None, :] >= s[:, None]) & (tok[None, :] < e[:, None])
+    cropped = torch.where(keep[..., None], features[bid], features.new_zeros(()))
+    return cropped, ~keep
+
+
+def captions_to_string(captions, vocab):
+    """Token rows -> strings without <pad>/<bos>/<eos>/<unk> (reference :83-104)."""
+    unwanted = {vocab['<pad>'], vocab['<bos>'], vocab['<eos>'], vocab['<unk>']}
+    itos = vocab.get_itos()
+    rows = captions.tolist() if isinstance(captions, torch.Tensor) else captions
+    return pre_process([' '.join([itos[t] for t in row if t not in unwanted][1:-1]) for row in rows])
+
+
+def pre_process(captions):
+    """Drop punctuation tokens and immediate repeats (reference :138-152)."""
+    for i, caption in enumerate(captions):
+        tokens = caption.split()
+        if len(tokens) == 0:
+            captions[i] = ''
+            continue
+        res = [tokens[0]]
+        for t in tokens[1:]:
+            if t in ['.', ',', '/', "'"] or res[-1] == t:
+                continue
+            res.append(t)
+        captions[i] = ' '.join(res)
+    return captions

@@ -503,6 +503,232 @@ def transformer_bf16_case(ref):
                              for n, m in named.items()})
 
 
+SPARSE_DVC_VOCAB = ['<unk>', '<pad>', '<bos>', '<eos>'] + [f"w{i}" for i in range(26)]
+
+
+def sparse_dvc_args():
+    """Namespaces standing in for cfg.dvc / cfg.dvc.sparse_detr / cfg.dvc.caption (config_dvc_train.py)
+    at a small size; dropout 0 so forward and gradients are deterministic."""
+    ns = types.SimpleNamespace
+    d = 64
+    sparse = ns(feature_dim=d, d_model=d, hidden_dim=d, num_heads=4, num_feature_levels=4, dec_n_points=4,
+                enc_n_points=4, enc_layers=2, dec_layers=2, transformer_dropout_prob=0.0, transformer_ff_dim=128,
+                video_rescale_len=64, rho=0.3, use_enc_aux_loss=True, return_intermediate=True, eff_query_init=True,
+                eff_specific_head=True)
+    caption = ns(d_model=d, depth=2, num_heads=4, mlp_ratio=4, qkv_bias=True, positional_embedding_dropout=0.0,
+                 attention_dropout=0.0, projection_dropout=0.0, bridge_dropout=0.0, mlp_dropout_1=0.0, mlp_dropout_2=0.0,
+                 pre_norm=False, model_official=None, weight_init=True, weight_load=False, emb_weights_req_grad=True,
+                 return_intermediate=True)
+    matcher = ns(cost_class=1, cost_segment=5, cost_giou=2, cost_alpha=0.25, cost_gamma=2.0)
+    return dict(d_model=d, num_queries=10, num_classes=20, max_eseq_length=10, seq_len=12, sparse=sparse,
+                caption=caption, matcher=matcher)
+
+
+def sparse_dvc_batch(seed, d, T, dtype, vocab_size, seq_len):
+    """engine.py-shaped ``obj`` (dataset/anet_video.py:262-384 collate keys) with 2 clips."""
+    gen = torch.Generator().manual_seed(seed)
+    B = 2
+    video = torch.randn((B, T, d), generator=gen, dtype=torch.float64).to(dtype)
+    mask = torch.zeros(B, T, dtype=torch.bool)
+    mask[1, (3 * T) // 4:] = True
+    durations = torch.tensor([37.5, 121.25], dtype=torch.float32)
+    nseg = [3, 2]
+    targets, caps = [], []
+    for b in range(B):
+        c = torch.rand((nseg[b],), generator=gen, dtype=torch.float32) * 0.6 + 0.2
+        l = torch.rand((nseg[b],), generator=gen, dtype=torch.float32) * 0.3 + 0.05
+        targets.append({'segments': torch.stack([c, l], 1).to(dtype), 'labels': torch.zeros(nseg[b], dtype=torch.long),
+                        'masks': None, 'vid_id': f"v{b}"})
+    total = sum(nseg)
+    cap = torch.full((total, seq_len), 1, dtype=torch.long)
+    cap_mask = torch.ones((total, seq_len), dtype=torch.bool)
+    for i in range(total):
+        n = 4 + i % (seq_len - 5)
+        body = torch.randint(4, vocab_size, (n,), generator=gen)
+        row = torch.cat([torch.tensor([2]), body, torch.tensor([3])])
+        cap[i, :len(row)] = row
+        cap_mask[i, :len(row)] = False
+    length = torch.tensor([[float(T), durations[b].item(), float(nseg[b])] for b in range(B)], dtype=torch.float32)
+    return {'video_tensor': video, 'video_mask': mask, 'video_length': length, 'video_target': targets,
+            'cap_tensor': cap, 'cap_mask': cap_mask}
+
+
+def sparse_dvc_case(ref, seed=71):
+    """The reference's UnimodalSparseDVC (models/sparse/unimodal_sparse_dvc.py), the one DVC wrapper
+    that runs end to end at HEAD: training forward (heads, Hungarian matching, crop, teacher-forced
+    caption decoder) + backward of a weighted sum of its outputs, and the eval-mode greedy decode
+    (val_mode one_by_one, faster_eval False and True).  fp64."""
+    import models.matcher as ref_matcher  # noqa: E402
+    import models.sparse.unimodal_sparse_dvc as ref_sdvc  # noqa: E402
+    a = sparse_dvc_args()
+    vocab = {w: i for i, w in enumerate(SPARSE_DVC_VOCAB)}
+    torch.manual_seed(seed)
+    matcher = ref_matcher.build_matcher(a["matcher"])
+    model = ref_sdvc.UnimodalSparseDVC(['video'], a["num_queries"], a["d_model"], a["num_classes"], True, matcher,
+                                       0.5, a["max_eseq_length"], vocab, a["seq_len"], None, a["sparse"],
+                                       a["caption"], use_differentiable_mask=False).double()
+    # the duration embedding allocates with the default dtype (embedding_layers.py:222)
+    torch.set_default_dtype(torch.float64)
+    try:
+        _jitter_offsets(model, seed)
+        with torch.no_grad():  # move the zero-initialised segment heads off zero so matching is generic
+            g = torch.Generator().manual_seed(seed + 1)
+            for ffn in (model.segment_embedding_decoder, model.segment_embedding_encoder):
+                w = ffn.layers[-1].weight
+                w.copy_(torch.randn(w.shape, generator=g, dtype=torch.float64) * 0.2)
+        obj = sparse_dvc_batch(seed, a["d_model"], 64, torch.float64, len(vocab), a["seq_len"])
+        model.train()
+        out, caps, indices, indices_aux, _ = model(obj, is_training=True)
+        gen = torch.Generator().manual_seed(seed + 2)
+        keys = ("pred_segments", "pred_count", "pred_captions", "backbone_mask_prediction")
+        w = {k: torch.randn(out[k].shape, generator=gen, dtype=torch.float64) for k in keys}
+        loss = sum((out[k] * w[k]).sum() for k in keys)
+        loss = loss + sum((o["pred_segments"] * 0.5).sum() + (o["pred_count"] * 0.25).sum() for o in out["aux_outputs"])
+        loss = loss + sum((o["pred_segments"] * 0.3).sum() for o in out["aux_outputs_enc"])
+        loss.backward()
+        train = dict(out={k: out[k].detach() for k in keys}, captions=caps, weights=w, loss=loss.detach(),
+                     indices=[torch.stack(list(t)) for t in indices],
+                     indices_aux=[[torch.stack(list(t)) for t in lv] for lv in indices_aux],
+                     aux_segments=torch.stack([o["pred_segments"].detach() for o in out["aux_outputs"]]),
+                     aux_enc_segments=torch.stack([o["pred_segments"].detach() for o in out["aux_outputs_enc"]]),
+                     param_grads={k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None})
+        model.eval()
+        evals = {}
+        with torch.no_grad():
+            for fe in (False, True):
+                o, caps_e, ind, _, _ = model(obj, is_training=False, faster_eval=fe, val_mode="one_by_one")
+                evals["faster" if fe else "exact"] = dict(captions=caps_e, pred_captions=o["pred_captions"],
+                                                          indices=[torch.stack(list(t)) for t in ind])
+        sd = {k: v for k, v in model.state_dict().items() if not k.endswith("positional_encoding.pos_embedding")}
+        return dict(state_dict=_compact(sd), obj={k: v for k, v in obj.items()}, vocab=SPARSE_DVC_VOCAB, train=train,
+                    eval=evals)
+    finally:
+        torch.set_default_dtype(torch.float32)
+
+
+def deformable_dvc_case(ref, seed=73):
+    """The reference's UnimodalDeformableDVC (models/deformable/unimodal_deformable_dvc.py) run with
+    its one crashing call fixed: the caption decoder is called positionally as
+    (captions, memory, tgt_mask, padding_mask, memory_mask) (:277/:328) against the signature
+    (tgt, memory, tgt_mask, memory_mask, tgt_padding_mask) (unimodal_caption_decoder.py:68); the
+    instance's decoder ``forward`` is wrapped to swap those two arguments.  Everything else is the
+    reference code as written.  use_differentiable_mask=True: with False the forward reads an
+    unbound ``pred_memory_mask`` (:264).  Training forward + backward, and eval decode."""
+    import models.matcher as ref_matcher  # noqa: E402
+    import models.deformable.unimodal_deformable_dvc as ref_ddvc  # noqa: E402
+    a = sparse_dvc_args()
+    s = a["sparse"]
+    detr = types.SimpleNamespace(feature_dim=s.feature_dim, d_model=s.d_model, num_heads=s.num_heads,
+                                 num_feature_levels=4, dec_n_points=4, enc_n_points=4, enc_layers=2, dec_layers=2,
+                                 transformer_dropout_prob=0.0, transformer_ff_dim=128, video_rescale_len=64,
+                                 return_intermediate=True, hidden_dropout_prob=0.0, layer_norm_eps=1e-12)
+    vocab = {w: i for i, w in enumerate(SPARSE_DVC_VOCAB)}
+    torch.manual_seed(seed)
+    matcher = ref_matcher.build_matcher(a["matcher"])
+    model = ref_ddvc.UnimodalDeformableDVC(['video'], a["num_queries"], a["d_model"], a["num_classes"], True, matcher,
+                                           0.5, a["max_eseq_length"], vocab, a["seq_len"], None, detr, a["caption"],
+                                           use_differentiable_mask=True).double()
+    dec = model.unimodal_caption_decoder
+    real_forward = type(dec).forward
+    dec.forward = lambda tgt, memory, tgt_mask=None, arg4=None, arg5=None: real_forward(dec, tgt, memory, tgt_mask,
+                                                                                        arg5, arg4)
+    torch.set_default_dtype(torch.float64)
+    try:
+        _jitter_offsets(model, seed)
+        with torch.no_grad():
+            g = torch.Generator().manual_seed(seed + 1)
+            w = model.segment_embedding[0].layers[-1].weight
+            w.copy_(torch.randn(w.shape, generator=g, dtype=torch.float64) * 0.2)
+        obj = sparse_dvc_batch(seed, a["d_model"], 64, torch.float64, len(vocab), a["seq_len"])
+        model.train()
+        out, caps, indices, indices_aux, mask = model(obj, is_training=True)
+        gen = torch.Generator().manual_seed(seed + 2)
+        keys = ("pred_logits", "pred_segments", "pred_count", "pred_captions", "pred_memory_mask")
+        w = {k: torch.randn(out[k].shape, generator=gen, dtype=torch.float64) for k in keys}
+        loss = sum((out[k] * w[k]).sum() for k in keys)
+        loss = loss + sum((o["pred_captions"] * 0.5).sum() + (o["pred_segments"] * 0.5).sum() for o in out["aux_outputs"])
+        loss.backward()
+        train = dict(out={k: out[k].detach() for k in keys}, captions=caps, weights=w, loss=loss.detach(), mask=mask,
+                     indices=[torch.stack(list(t)) for t in indices],
+                     indices_aux=[[torch.stack(list(t)) for t in lv] for lv in indices_aux],
+                     aux_captions=torch.stack([o["pred_captions"].detach() for o in out["aux_outputs"]]),
+                     param_grads={k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None})
+        model.eval()
+        evals = {}
+        with torch.no_grad():
+            for fe in (False, True):
+                o, caps_e, ind, ind_aux, _ = model(obj, is_training=False, faster_eval=fe)
+                evals["faster" if fe else "exact"] = dict(
+                    captions=caps_e, pred_captions=o["pred_captions"], indices=[torch.stack(list(t)) for t in ind],
+                    aux_captions=torch.stack([x["pred_captions"] for x in o["aux_outputs"]]))
+        sd = {k: v for k, v in model.state_dict().items() if not k.endswith("positional_encoding.pos_embedding")}
+        return dict(state_dict=_compact(sd), obj=obj, vocab=SPARSE_DVC_VOCAB, train=train, eval=evals)
+    finally:
+        torch.set_default_dtype(torch.float32)
+
+
+def mm_caption_decoder_case(ref, seed=79):
+    """The reference's MultimodalCaptionDecoder (models/multimodal_caption_decoder.py) and its layer
+    (models/modules/layers.py:648-823), executed with the undefined names of HEAD bound to the
+    objects they evidently mean — nothing in the files is changed:
+      * module globals of multimodal_caption_decoder: ``CapMultimodalCaptionDecoderionDecoder`` (:29) ->
+        MultimodalCaptionDecoder, ``MultimodalCaptionDecoderrLayer`` (:42) -> a layer class taking the
+        decoder's ``dropout_1`` / ``dropout_2`` as the layer's ``mlp_dropout_1`` / ``mlp_dropout_2``;
+      * the layer's ``super(UnimodalCaptionDecoderLayer, self)`` (:667) resolves by making the layer
+        class also derive from UnimodalCaptionDecoderLayer (its MRO then reaches nn.Module);
+      * instance aliases ``activation`` -> ``activation_layer``, ``cross_attention`` ->
+        ``audio_cross_attention``, ``audio_projection_dropout_3`` -> ``projection_dropout_3`` (:760,819,823).
+    Post-norm (config pre_norm=False); the pre-norm path cannot run (LayerNorm(d) on a 2d concat, :757)."""
+    import models.modules.layers as ref_layers  # noqa: E402
+    import models.multimodal_caption_decoder as ref_mcd  # noqa: E402
+
+    class Layer(ref_layers.MultimodalCaptionDecoderLayer, ref_layers.UnimodalCaptionDecoderLayer):
+        def __init__(self, d_model, num_heads, mlp_ratio, qkv_bias, attention_dropout, projection_dropout,
+                     dropout_1, dropout_2, pre_norm):
+            ref_layers.MultimodalCaptionDecoderLayer.__init__(
+                self, d_model, num_heads, mlp_ratio=mlp_ratio, qkv_bias=qkv_bias, attention_dropout=attention_dropout,
+                projection_dropout=projection_dropout, mlp_dropout_1=dropout_1, mlp_dropout_2=dropout_2,
+                pre_norm=pre_norm)
+            # plain attributes (not registered submodules): the state_dict keeps the reference's names
+            object.__setattr__(self, "activation", self.activation_layer)
+            object.__setattr__(self, "cross_attention", self.audio_cross_attention)
+            object.__setattr__(self, "audio_projection_dropout_3", self.projection_dropout_3)
+
+        forward = ref_layers.MultimodalCaptionDecoderLayer.forward
+
+    ref_mcd.CapMultimodalCaptionDecoderionDecoder = ref_mcd.MultimodalCaptionDecoder
+    ref_mcd.MultimodalCaptionDecoderrLayer = Layer
+    torch.manual_seed(seed)
+    V, d, N, L, Kv, Ka = 30, 64, 3, 8, 20, 12
+    dec = ref_mcd.MultimodalCaptionDecoder(V, seq_len=L, d_model=d, depth=2, num_heads=4, mlp_ratio=4, qkv_bias=True,
+                                           pre_norm=False, return_intermediate=True).double()
+    gen = torch.Generator().manual_seed(seed)
+    with torch.no_grad():  # LayerNorm affine parameters off their (1, 0) init
+        for name, p in dec.named_parameters():
+            if "layer_norm" in name:
+                p.add_(torch.randn(p.shape, generator=gen, dtype=torch.float64) * 0.1)
+    tgt = torch.randint(4, V, (N, L), generator=gen)
+    tgt[:, 0] = 2
+    tgt[0, 6:] = 1
+    tgt[2, 4:] = 1
+    pad = tgt == 1
+    vm = torch.randn((N, Kv, d), generator=gen, dtype=torch.float64).requires_grad_(True)
+    am = torch.randn((N, Ka, d), generator=gen, dtype=torch.float64).requires_grad_(True)
+    vmask = torch.zeros(N, Kv, dtype=torch.bool)
+    vmask[1, 11:] = True
+    amask = torch.zeros(N, Ka, dtype=torch.bool)
+    amask[0, 5:] = True
+    look = torch.ones(L, L, dtype=torch.bool).triu(1)
+    out = dec(tgt=tgt, video_memory=vm, audio_memory=am, tgt_mask=look, video_memory_mask=None, audio_memory_mask=None,
+              tgt_padding_mask=pad, video_memory_padding_mask=vmask, audio_memory_padding_mask=amask)
+    w = torch.randn(out.shape, generator=gen, dtype=torch.float64)
+    (out * w).sum().backward()
+    sd = {k: v for k, v in dec.state_dict().items() if not k.endswith("positional_encoding.pos_embedding")}
+    return dict(state_dict=_compact(sd), tgt=tgt, video_memory=vm.detach(), audio_memory=am.detach(),
+                video_mask=vmask, audio_mask=amask, out=out.detach(), w=w, grad_video=vm.grad, grad_audio=am.grad,
+                param_grads={k: p.grad.clone() for k, p in dec.named_parameters() if p.grad is not None})
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = import_reference()
@@ -519,6 +745,9 @@ def main():
         "ops_api_f64": lambda: ops_api_case(ref),
         "ops_module_f64": lambda: ops_module_case(ref),
         "transformer_bf16": lambda: transformer_bf16_case(ref),
+        "sparse_dvc_f64": lambda: sparse_dvc_case(ref),
+        "deformable_dvc_f64": lambda: deformable_dvc_case(ref),
+        "mm_caption_decoder_f64": lambda: mm_caption_decoder_case(ref),
     }
     wanted = sys.argv[1:] or list(cases)
     for name, fn in cases.items():
