@@ -5,18 +5,20 @@ matching, per-modality crops and the MultimodalCaptionDecoder.  Constructor, sta
 ``forward(obj, is_training=True, faster_eval=False)`` -> ``(out, captions, indices, indices_aux,
 video_mask, audio_mask)`` as engine.py:71 consumes it.
 
-The reference cannot be built or run at HEAD; restated intent, each marked below:
+The reference cannot be built or run at HEAD.  What is restated, each marked at the code:
 * ``detr_args`` is used (:63,74,76,88) but the parameter is ``sparse_detr_args`` (:32): here the
   parameter is ``detr_args`` (what models/__init__.py:55-68 passes) and ``sparse_detr_args`` is
   accepted as an alias; ``max_eseq_length``, omitted by the builder, defaults to 10 (the config's).
-* the audio context-mask size uses the audio pyramid (:95 reads an undefined
-  ``video_num_tokens``); ``memory`` / ``memory_list`` (:284,348) are the video ones.
+* ``self.video_num_tokens`` (:95) is ``self.num_tokens``; ``memory`` (:284) is the video memory.
 * the caption-decoder calls use the keyword convention of the working sparse wrappers
-  (models/sparse/multimodal_sparse_dvc.py:299-305; the positional call at :320-322 shifts every
-  mask by one slot, and ``nn.MultiheadAttention`` rejects the (N,1,L,L) masks it builds).
-* each decoder level crops the encoder memories (the reference re-crops the previous crop) with its
-  own segments (the reference uses the last level's, :256); audio tokens are cropped on the audio
-  pyramid's level ranges (``audio_rescale_len``; the reference applies the video ranges)."""
+  (models/sparse/multimodal_sparse_dvc.py:299-305): the positional call (:320-322) shifts every mask
+  by one slot and ``nn.MultiheadAttention`` rejects the (N,1,L,L) masks it builds.
+* inference reads ``memory_list`` / ``memory_mask_list`` (:348-350), which do not exist: the video ones.
+Everything else is computed as written — each level denormalises the LAST level's segments at its
+own matching (:256), rebinds ``video_memory`` / ``audio_memory`` to its crop so the next level crops
+that (:259-260), and crops audio on the video token ranges (``crop_segments`` reads
+``video_rescale_len``, :530) — and the training forward is pinned against the reference run with
+exactly these names bound (tests/golden/mm_dvc_f64.pt)."""
 import math
 from math import ceil
 
@@ -75,7 +77,8 @@ class MultimodalDeformableDVC(nn.Module):
         self.audio_rescale_len = detr_args.audio_rescale_len
         self.num_tokens = ceil(((2 ** self.num_feature_levels - 1) / 2 ** (self.num_feature_levels - 1))
                                * self.video_rescale_len)
-        self.audio_num_tokens = self._pyramid_tokens(self.audio_rescale_len)
+        self.audio_num_tokens = ceil(((2 ** self.num_feature_levels - 1) / 2 ** (self.num_feature_levels - 1))
+                                     * self.audio_rescale_len)
         self.use_differentiable_mask = use_differentiable_mask
         if use_differentiable_mask:
             self.video_context_mask_model = ContextMaskModel(in_dim=(2 + d_model), out_dim=self.num_tokens)
@@ -84,15 +87,6 @@ class MultimodalDeformableDVC(nn.Module):
         self.vocab = vocab
         self.multimodal_caption_decoder = build_multimodal_caption_decoder(caption_args, len(vocab), seq_len,
                                                                            embedding_matrix)
-
-    def _pyramid_tokens(self, T):
-        """Flattened length of the BaseEncoder pyramid of a T-token input (stride-2, padding-1 levels)."""
-        total, t = 0, T
-        for lvl in range(self.num_feature_levels):
-            if lvl:
-                t = (t - 1) // 2 + 1
-            total += t
-        return total
 
     def forward_proposals(self, video, video_mask, audio, audio_mask, durations):
         tr = self.multimodal_deformable_transformer
@@ -134,23 +128,24 @@ class MultimodalDeformableDVC(nn.Module):
         vids, auds, outputs_captions = [], [], []
         for lvl in range(num_pred):
             indices = level_indices[lvl]
-            idx, idx_dev, denorm, v_mem, v_mask = segment_memory(video_memory, out_aux[lvl], indices, durations,
-                                                                 self.num_feature_levels, self.video_rescale_len)
-            a_mem, a_mask = crop_segments(audio_memory, denorm, idx_dev[0], durations, self.num_feature_levels,
-                                          self.audio_rescale_len)
+            # as written: the last level's segments at this level's matching (:256)
+            idx, idx_dev, denorm, video_memory, v_mask = segment_memory(video_memory, out, indices, durations,
+                                                                        self.num_feature_levels, self.video_rescale_len)
+            audio_memory, a_mask = crop_segments(audio_memory, denorm, idx_dev[0], durations, self.num_feature_levels,
+                                                 self.video_rescale_len)
             v_key, a_key = v_mask, a_mask
             if self.use_differentiable_mask:
                 qsel = query_features[-1][idx_dev]
                 v_pred, v_key = context_mask(self.video_context_mask_model, denorm, qsel, v_mask)
                 a_pred, a_key = context_mask(self.audio_context_mask_model, denorm, qsel, a_mask)
                 out['video_pred_memory_mask'], out['audio_pred_memory_mask'] = v_pred, a_pred
-            vids.append((v_mem, v_mask, v_key))
-            auds.append((a_mem, a_mask, a_key))
+            vids.append((video_memory, v_mask, v_key))
+            auds.append((audio_memory, a_mask, a_key))
             if is_training:
                 captions = obj['cap_tensor'][:, :-1]
                 padding_mask = obj['cap_mask'][:, :-1]
                 output_caption = self.multimodal_caption_decoder(
-                    tgt=captions, video_memory=v_mem, audio_memory=a_mem,
+                    tgt=captions, video_memory=video_memory, audio_memory=audio_memory,
                     tgt_mask=look_ahead_mask(captions.shape[1], captions.device), tgt_padding_mask=padding_mask,
                     video_memory_padding_mask=v_key, audio_memory_padding_mask=a_key)
                 outputs_captions.append(output_caption[-1])

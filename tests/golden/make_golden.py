@@ -36,6 +36,10 @@ Fixtures:
   ops_module_f64.pt          ops/modules MSDeformAttn (through the zero-padding kernel, as on a GPU) and
                              MSDeformAttnCap (border, return_value), enc / dec, padding mask.
   transformer_bf16.pt        transformer_f64's model and inputs under torch.autocast('cpu', bfloat16).
+  sparse_dvc_f64.pt          UnimodalSparseDVC end to end as written (train fwd + grads, greedy decode).
+  deformable_dvc_f64.pt      UnimodalDeformableDVC with its caption-decoder call's argument order fixed.
+  mm_caption_decoder_f64.pt  MultimodalCaptionDecoder with HEAD's undefined names bound (no file edits).
+  mm_dvc_f64.pt              MultimodalDeformableDVC training fwd + grads, undefined names bound likewise.
 
 usage: make_golden.py [case ...]   (default: every case; e.g. ``make_golden.py dam sparse``)
 """
@@ -729,6 +733,83 @@ def mm_caption_decoder_case(ref, seed=79):
                 param_grads={k: p.grad.clone() for k, p in dec.named_parameters() if p.grad is not None})
 
 
+def mm_dvc_args():
+    a = sparse_dvc_args()
+    s = a["sparse"]
+    detr = types.SimpleNamespace(feature_dim=s.feature_dim, d_model=s.d_model, num_heads=s.num_heads,
+                                 num_feature_levels=4, dec_n_points=4, enc_n_points=4, enc_layers=2, dec_layers=2,
+                                 transformer_dropout_prob=0.0, transformer_ff_dim=128, video_rescale_len=64,
+                                 audio_rescale_len=16, return_intermediate=True, rho=0.0, use_enc_aux_loss=False)
+    cap = types.SimpleNamespace(**vars(a["caption"]), dropout_1=0.0, dropout_2=0.0)
+    return a, detr, cap
+
+
+def mm_dvc_case(ref, seed=83):
+    """The reference's MultimodalDeformableDVC (models/deformable/multimodal_deformable_dvc.py) training
+    forward + backward, run with the names HEAD leaves undefined bound — nothing in the files changed:
+      * module global ``detr_args`` (used in __init__ :63,74,76,88) -> the model arguments;
+      * class attribute ``video_num_tokens`` (:95) -> num_tokens; module global ``memory`` (read only
+        for ``memory.shape[0]``, the matched-segment count, :284) -> a tensor of that length;
+      * the MultimodalCaptionDecoder bindings of mm_caption_decoder_case, and its positional call
+        (:320) mapped onto the keyword convention of models/sparse/multimodal_sparse_dvc.py:299-305
+        (look-ahead + caption key padding; memory masks as key padding), the only form
+        ``nn.MultiheadAttention`` accepts.
+    use_differentiable_mask=True: with False the forward reads an unbound mask (:303)."""
+    import models.matcher as ref_matcher  # noqa: E402
+    import models.deformable.multimodal_deformable_dvc as ref_mdvc  # noqa: E402
+    mm_caption_decoder_case(ref, seed)  # installs the caption-decoder bindings
+    a, detr, cap = mm_dvc_args()
+    vocab = {w: i for i, w in enumerate(SPARSE_DVC_VOCAB)}
+    obj = sparse_dvc_batch(seed, a["d_model"], 64, torch.float64, len(vocab), a["seq_len"])
+    gen = torch.Generator().manual_seed(seed + 5)
+    obj["audio_tensor"] = torch.randn((2, 16, a["d_model"]), generator=gen, dtype=torch.float64)
+    obj["audio_mask"] = torch.zeros(2, 16, dtype=torch.bool)
+    obj["audio_mask"][1, 13:] = True
+    n_segments = sum(len(t["segments"]) for t in obj["video_target"])
+    ref_mdvc.detr_args = detr
+    ref_mdvc.memory = torch.zeros(n_segments)
+    ref_mdvc.MultimodalDeformableDVC.video_num_tokens = 120
+    torch.manual_seed(seed)
+    matcher = ref_matcher.build_matcher(a["matcher"])
+    model = ref_mdvc.MultimodalDeformableDVC(['video', 'audio'], a["num_queries"], a["d_model"], a["num_classes"], True,
+                                             matcher, 0.5, a["max_eseq_length"], vocab, a["seq_len"], None, detr, cap,
+                                             use_differentiable_mask=True).double()
+    dec = model.multimodal_caption_decoder
+    real_forward = type(dec).forward
+    look = torch.ones(a["seq_len"] - 1, a["seq_len"] - 1, dtype=torch.bool).triu(1)
+
+    def positional_call(captions, video_memory, audio_memory, tgt_mask, padding_mask, vmask, amask):
+        return real_forward(dec, captions, video_memory, audio_memory, tgt_mask=look, tgt_padding_mask=padding_mask,
+                            video_memory_padding_mask=vmask[:, 0, 0, :], audio_memory_padding_mask=amask[:, 0, 0, :])
+
+    dec.forward = positional_call
+    torch.set_default_dtype(torch.float64)
+    try:
+        _jitter_offsets(model, seed)
+        with torch.no_grad():
+            g = torch.Generator().manual_seed(seed + 1)
+            w = model.segment_embedding[0].layers[-1].weight
+            w.copy_(torch.randn(w.shape, generator=g, dtype=torch.float64) * 0.2)
+        model.train()
+        out, caps, indices, indices_aux, vmask, amask = model(obj, is_training=True)
+        gen = torch.Generator().manual_seed(seed + 2)
+        keys = ("pred_logits", "pred_segments", "pred_count", "pred_captions", "video_pred_memory_mask",
+                "audio_pred_memory_mask")
+        w = {k: torch.randn(out[k].shape, generator=gen, dtype=torch.float64) for k in keys}
+        loss = sum((out[k] * w[k]).sum() for k in keys)
+        loss = loss + sum((o["pred_captions"] * 0.5).sum() + (o["pred_segments"] * 0.5).sum() for o in out["aux_outputs"])
+        loss.backward()
+        sd = {k: v for k, v in model.state_dict().items() if not k.endswith("positional_encoding.pos_embedding")}
+        return dict(state_dict=_compact(sd), obj=obj, vocab=SPARSE_DVC_VOCAB, out={k: out[k].detach() for k in keys},
+                    captions=caps, weights=w, loss=loss.detach(), video_mask=vmask, audio_mask=amask,
+                    indices=[torch.stack(list(t)) for t in indices],
+                    indices_aux=[[torch.stack(list(t)) for t in lv] for lv in indices_aux],
+                    aux_captions=torch.stack([o["pred_captions"].detach() for o in out["aux_outputs"]]),
+                    param_grads={k: p.grad.clone() for k, p in model.named_parameters() if p.grad is not None})
+    finally:
+        torch.set_default_dtype(torch.float32)
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = import_reference()
@@ -748,6 +829,7 @@ def main():
         "sparse_dvc_f64": lambda: sparse_dvc_case(ref),
         "deformable_dvc_f64": lambda: deformable_dvc_case(ref),
         "mm_caption_decoder_f64": lambda: mm_caption_decoder_case(ref),
+        "mm_dvc_f64": lambda: mm_dvc_case(ref),
     }
     wanted = sys.argv[1:] or list(cases)
     for name, fn in cases.items():

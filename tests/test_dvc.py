@@ -7,8 +7,8 @@ runs of the reference itself (tests/golden/make_golden.py):
   order) fixed, differentiable mask on (the reference cannot run with it off);
 * MultimodalCaptionDecoder — the reference's code with the undefined names of HEAD bound to what
   they evidently mean (make_golden.py::mm_caption_decoder_case);
-* MultimodalDeformableDVC — cannot be built at HEAD: runs, returns the engine.py:71 tuple, and its
-  KV-cached decode equals the full re-decode;
+* MultimodalDeformableDVC — the reference's training forward with HEAD's undefined names bound
+  (make_golden.py::mm_dvc_case); its inference (undefined there) runs and returns the engine.py:71 tuple;
 * the KV-cached greedy decode of both caption decoders equals the reference's full re-decode loop.
 
 CPU variants run the MSDA core as the oracle restatement (oracle.cpu_model); ``-m gpu`` variants run
@@ -96,6 +96,13 @@ def _run(model, obj, dev, **kw):
         torch.set_default_dtype(torch.float32)
 
 
+def _tol(dev):
+    """fp64 models, but the reference computes the sine position embedding in fp32
+    (embedding_layers.py:208): GPU vs CPU fp32 sin/cos differ by an ulp, so on the GPU the
+    outputs agree to ~1e-7 of fp32 resolution instead of 1e-9 (cf. test_gpu_module.py)."""
+    return 1e-9 if dev == "cpu" else 1e-6
+
+
 def _check_sparse_dvc(golden, dev):
     g = golden("sparse_dvc_f64")
     model = _load(build_sparse_dvc(dev), g["state_dict"])
@@ -108,19 +115,19 @@ def _check_sparse_dvc(golden, dev):
     for ours, ref in zip(indices_aux, t["indices_aux"]):
         _indices_equal(ours, ref)
     for k, v in t["out"].items():
-        _rel(out[k], v, 1e-9, k)
+        _rel(out[k], v, _tol(dev), k)
     assert torch.equal(caps.cpu(), t["captions"])
-    _rel(torch.stack([o["pred_segments"] for o in out["aux_outputs"]]), t["aux_segments"], 1e-9)
-    _rel(torch.stack([o["pred_segments"] for o in out["aux_outputs_enc"]]), t["aux_enc_segments"], 1e-9)
+    _rel(torch.stack([o["pred_segments"] for o in out["aux_outputs"]]), t["aux_segments"], _tol(dev))
+    _rel(torch.stack([o["pred_segments"] for o in out["aux_outputs_enc"]]), t["aux_enc_segments"], _tol(dev))
     w = {k: v.to(dev) for k, v in t["weights"].items()}
     loss = sum((out[k] * w[k]).sum() for k in w)
     loss = loss + sum((o["pred_segments"] * 0.5).sum() + (o["pred_count"] * 0.25).sum() for o in out["aux_outputs"])
     loss = loss + sum((o["pred_segments"] * 0.3).sum() for o in out["aux_outputs_enc"])
     _run_backward(loss, dev)
-    _rel(loss, t["loss"], 1e-10)
+    _rel(loss, t["loss"], _tol(dev) / 10)
     for k, p in model.named_parameters():
         if k in t["param_grads"]:
-            _rel(p.grad, t["param_grads"][k], 1e-8, k)
+            _rel(p.grad, t["param_grads"][k], 10 * _tol(dev), k)
         else:
             assert p.grad is None or p.grad.abs().max() == 0, k
     model.eval()
@@ -129,7 +136,7 @@ def _check_sparse_dvc(golden, dev):
             o, caps_e, ind, _, _ = _run(model, obj, dev, is_training=False, faster_eval=fe, val_mode="one_by_one")
             e = g["eval"][name]
             assert torch.equal(caps_e.cpu(), e["captions"]), name
-            _rel(o["pred_captions"], e["pred_captions"], 1e-9, name)
+            _rel(o["pred_captions"], e["pred_captions"], _tol(dev), name)
             _indices_equal(ind, e["indices"])
 
 
@@ -152,26 +159,26 @@ def _check_deformable_dvc(golden, dev):
     for ours, ref in zip(indices_aux, t["indices_aux"]):
         _indices_equal(ours, ref)
     for k, v in t["out"].items():
-        _rel(out[k], v, 1e-9, k)
+        _rel(out[k], v, _tol(dev), k)
     assert torch.equal(caps.cpu(), t["captions"])
     assert torch.equal(mask.cpu(), t["mask"])
-    _rel(torch.stack([o["pred_captions"] for o in out["aux_outputs"]]), t["aux_captions"], 1e-9)
+    _rel(torch.stack([o["pred_captions"] for o in out["aux_outputs"]]), t["aux_captions"], _tol(dev))
     w = {k: v.to(dev) for k, v in t["weights"].items()}
     loss = sum((out[k] * w[k]).sum() for k in w)
     loss = loss + sum((o["pred_captions"] * 0.5).sum() + (o["pred_segments"] * 0.5).sum() for o in out["aux_outputs"])
     _run_backward(loss, dev)
-    _rel(loss, t["loss"], 1e-10)
+    _rel(loss, t["loss"], _tol(dev) / 10)
     for k, p in model.named_parameters():
         if k in t["param_grads"]:
-            _rel(p.grad, t["param_grads"][k], 1e-8, k)
+            _rel(p.grad, t["param_grads"][k], 10 * _tol(dev), k)
     model.eval()
     with torch.no_grad():
         for name, fe in (("exact", False), ("faster", True)):
             o, caps_e, ind, ind_aux, _ = _run(model, obj, dev, is_training=False, faster_eval=fe)
             e = g["eval"][name]
             assert torch.equal(caps_e.cpu(), e["captions"]), name
-            _rel(o["pred_captions"], e["pred_captions"], 1e-9, name)
-            _rel(torch.stack([x["pred_captions"] for x in o["aux_outputs"]]), e["aux_captions"], 1e-9, name)
+            _rel(o["pred_captions"], e["pred_captions"], _tol(dev), name)
+            _rel(torch.stack([x["pred_captions"] for x in o["aux_outputs"]]), e["aux_captions"], _tol(dev), name)
             _indices_equal(ind, e["indices"])
 
 
@@ -286,39 +293,44 @@ def full_fn(kind, dec, mem, mem2, kmask, kmask2, look, pad):
                          video_memory_padding_mask=kmask, audio_memory_padding_mask=kmask2)[-1]
 
 
-def test_multimodal_dvc_runs_and_returns_engine_tuple():
-    a = MG.sparse_dvc_args()
-    s = a["sparse"]
-    detr = types.SimpleNamespace(feature_dim=s.feature_dim, d_model=s.d_model, num_heads=s.num_heads,
-                                 num_feature_levels=4, dec_n_points=4, enc_n_points=4, enc_layers=2, dec_layers=2,
-                                 transformer_dropout_prob=0.0, transformer_ff_dim=128, video_rescale_len=64,
-                                 audio_rescale_len=16, return_intermediate=True)
-    cap = types.SimpleNamespace(**vars(a["caption"]))
-    torch.manual_seed(3)
-    model = M.deformable.multimodal_deformable_dvc.MultimodalDeformableDVC(
+def build_mm_dvc(dev="cpu"):
+    a, detr, cap = MG.mm_dvc_args()
+    return M.deformable.multimodal_deformable_dvc.MultimodalDeformableDVC(
         ['video', 'audio'], a["num_queries"], a["d_model"], a["num_classes"], True,
-        M.matcher.build_matcher(a["matcher"]), 0.5, a["max_eseq_length"], _vocab(), a["seq_len"], None, detr,
-        cap).double()
-    obj = MG.sparse_dvc_batch(3, a["d_model"], 64, torch.float64, len(_vocab()), a["seq_len"])
-    gen = torch.Generator().manual_seed(4)
-    obj["audio_tensor"] = torch.randn(2, 16, a["d_model"], generator=gen, dtype=torch.float64)
-    obj["audio_mask"] = torch.zeros(2, 16, dtype=torch.bool)
+        M.matcher.build_matcher(a["matcher"]), 0.5, a["max_eseq_length"], _vocab(), a["seq_len"], None, detr, cap,
+        use_differentiable_mask=True).double().to(dev)
+
+
+def _check_mm_dvc(golden, dev):
+    g = golden("mm_dvc_f64")
+    model = _load(build_mm_dvc(dev), g["state_dict"])
+    obj = _obj_to(g["obj"], dev)
     model.train()
-    res = _run(model, obj, "cpu", is_training=True)
-    assert len(res) == 6
-    out, caps, indices, indices_aux, vm, am = res
-    assert out["pred_captions"].shape[:2] == (5, a["seq_len"] - 1) and caps.shape == (5, a["seq_len"] - 1)
-    assert len(indices) == 2 and len(indices_aux) == 1
-    torch.set_default_dtype(torch.float64)
-    try:
-        with oracle_core(PKG):
-            (out["pred_captions"].sum() + out["pred_segments"].sum()).backward()
-    finally:
-        torch.set_default_dtype(torch.float32)
+    out, caps, indices, indices_aux, vm, am = _run(model, obj, dev, is_training=True)
+    _indices_equal(indices, g["indices"])
+    for ours, ref in zip(indices_aux, g["indices_aux"]):
+        _indices_equal(ours, ref)
+    for k, v in g["out"].items():
+        _rel(out[k], v, _tol(dev), k)
+    assert torch.equal(caps.cpu(), g["captions"])
+    assert torch.equal(vm.cpu(), g["video_mask"]) and torch.equal(am.cpu(), g["audio_mask"])
+    _rel(torch.stack([o["pred_captions"] for o in out["aux_outputs"]]), g["aux_captions"], _tol(dev))
+    w = {k: v.to(dev) for k, v in g["weights"].items()}
+    loss = sum((out[k] * w[k]).sum() for k in w)
+    loss = loss + sum((o["pred_captions"] * 0.5).sum() + (o["pred_segments"] * 0.5).sum() for o in out["aux_outputs"])
+    _run_backward(loss, dev)
+    _rel(loss, g["loss"], _tol(dev) / 10)
+    for k, p in model.named_parameters():
+        if k in g["param_grads"]:
+            _rel(p.grad, g["param_grads"][k], 10 * _tol(dev), k)
     model.eval()
-    with torch.no_grad():
-        out, caps, indices, indices_aux, _, _ = _run(model, obj, "cpu", is_training=False)
-    assert caps.shape == (5, a["seq_len"]) and caps.dtype == torch.int32
+    with torch.no_grad():  # inference (the reference's reads undefined names here): runs, engine.py:71 tuple
+        res = _run(model, obj, dev, is_training=False)
+    assert len(res) == 6 and res[1].shape == (5, MG.sparse_dvc_args()["seq_len"]) and res[1].dtype == torch.int32
+
+
+def test_mm_dvc_matches_reference_cpu(golden):
+    _check_mm_dvc(golden, "cpu")
 
 
 # --- GPU (HIP MSDA) -----------------------------------------------------------------------------
@@ -336,3 +348,8 @@ def test_deformable_dvc_matches_reference_gpu(golden, dev):
 @pytest.mark.gpu
 def test_mm_caption_decoder_matches_reference_gpu(golden, dev):
     _check_mm_caption_decoder(golden, dev)
+
+
+@pytest.mark.gpu
+def test_mm_dvc_matches_reference_gpu(golden, dev):
+    _check_mm_dvc(golden, dev)
