@@ -196,12 +196,12 @@ def _check_mm_caption_decoder(golden, dev):
     out = dec(tgt=tgt, video_memory=vm, audio_memory=am, tgt_mask=look, tgt_padding_mask=tgt == 1,
               video_memory_padding_mask=g["video_mask"].to(dev), audio_memory_padding_mask=g["audio_mask"].to(dev))
     (out * g["w"].to(dev)).sum().backward()
-    _rel(out, g["out"], 1e-10)
-    _rel(vm.grad, g["grad_video"], 1e-9)
-    _rel(am.grad, g["grad_audio"], 1e-9)
+    _rel(out, g["out"], _tol(dev) / 10)
+    _rel(vm.grad, g["grad_video"], _tol(dev))
+    _rel(am.grad, g["grad_audio"], _tol(dev))
     for k, p in dec.named_parameters():
         if k in g["param_grads"]:
-            _rel(p.grad, g["param_grads"][k], 1e-9, k)
+            _rel(p.grad, g["param_grads"][k], _tol(dev), k)
 
 
 # --- CPU (oracle MSDA core) -----------------------------------------------------------------------
