@@ -727,7 +727,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_gvalue_kernel(
   const int T = lv.T[l];
   const int ncap = 2 * Lq * P;
 #ifdef MSDA_PHASE_TIMING  // debug build only: per-phase wall clock of two workgroups
-  unsigned long long tph[6];
+  unsigned long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   tph[0] = wall_clock64();
 #define MSDA_PH(i) do { __syncthreads(); tph[i] = wall_clock64(); } while (0)
 #else
@@ -1149,6 +1149,644 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
     printf("fused l=%d T=%d ncap=%d zero=%llu pass1=%llu scan=%llu place=%llu pull=%llu coords=%llu (x10ns)\n", l, T,
            ncap, tph[1] - tph[0], tph[2] - tph[1], tph[3] - tph[2], tph[4] - tph[3], tph[5] - tph[4],
            tph[6] - tph[5]);
+#endif
+#undef MSDA_PH
+}
+
+// ---------------------------------------------------------------------------------
+// Pair-pull fused backward (the default backward).
+// ---------------------------------------------------------------------------------
+// A sample's two taps always sit on consecutive rows i0, i0 + 1 of its level.  The per-tap
+// lists of msda_bwd_fused_kernel gather the sample's grad_out row once per tap; here a sample
+// is listed ONCE, under its base row r = i0 (r = -1 when only the upper tap is on the map, ZEROS
+// mode), and one gathered grad_out row g serves both taps:
+//   grad_value[r] = sum_{s in list r} c0_s g_s  +  sum_{s in list r-1} c1_s g_s,   c_k = aw w_k,
+// and the same g gives both dots d0 = <g, v_r>, d1 = <g, v_{r+1}>.  Half the gathers of the
+// per-tap kernel.  The lists are laid out by base row (list index r + 1) with, per entry, the key
+// q << 8 | p and (c0, c1) computed once at placement (12 B of LDS per sample); the pull overwrites
+// (c0, c1) with (d0, d1) and a per-entry epilogue turns them into grad_attn = w0 d0 + w1 d1 and
+// grad_loc = aw dy/dloc (d1 - d0).  Walking a list r, a slot (LPR lanes x 16 B) keeps two fp32 row
+// accumulators (rows r, r+1) and the two value rows; when list r is done row r is final.
+//
+// Work split.  One (or RS) workgroup(s) per (b, m, level); RS > 1 splits the level's list
+// positions at list boundaries, each workgroup re-reading the list just before its window (the
+// "pre-list", whose c1 halves complete its first row; nothing else of it is written).  Inside a
+// workgroup, by level:
+//   * row mode (sparse levels, N <= 4 (T + 1): decoder-like calls): every slot builds whole rows r
+//     from lists r-1 (c1) and r (c0), so an entry is gathered by both its rows, but rows are
+//     independent: no hand-over, no list walk;
+//   * striped mode (T + 1 < 2 x slots: short pyramids, a few rows with tens to thousands of taps
+//     each, as cross-modal calls onto the audio pyramid): every wave takes an even share of the
+//     positions and its slots stripe through each list together; a finished row is summed over
+//     the slots with lane shuffles, stored when all its taps lay in the wave's share, else kept as
+//     one of the wave's (at most 4) partial rows, which are summed in wave order at the end;
+//   * run mode (otherwise): every slot walks a run of whole lists, slot bounds snapped to list
+//     starts at even shares of the positions; the one row two slots share (c1 part of the earlier
+//     slot's last list | c0 part of the later slot's first list) is handed over through LDS after
+//     the pull, the later slot holding that row in registers meanwhile.
+// Rows with no listed tap on either side are written as zeros by a sweep.  No float atomics.
+// Deterministic mode (MSDA_HIP_DETERMINISTIC=1): lists sorted by key, so every sum has a fixed
+// order.  When 12 B per sample does not fit LDS (T = 4096: 30,720 samples a level, !STG) only the
+// keys are kept, loc / aw are loaded beside the gather, the taps recomputed in the pull and the
+// coordinate gradients stored from it (run mode only).
+struct PairLayout {
+  int off_cc, off_pos, off_xb, off_cur, off_pb, off_scr;
+};
+
+constexpr int kPairParts = 4;  // partial rows per wave (striped mode)
+
+template <typename scalar_t, int NSLOT, bool ZEROS, bool STG, int U>
+__global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
+    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, float* __restrict__ gloc,
+    float* __restrict__ gaw, const Levels lv, const int L, const int P, const int S, const int M,
+    const int D, const int Lq, const int RS, const unsigned striped_mask, const int sort_rows,
+    const PairLayout lay) {
+  static_assert(NSLOT > 0, "pair backward needs whole 16-byte chunks per lane");
+  constexpr int CPL = 16 / (int)sizeof(scalar_t);
+  constexpr int H = CPL / 2;
+  constexpr int LPR = 64 / NSLOT;
+  constexpr int NW = kGvThreads / 64;  // waves
+  constexpr int W = NW * NSLOT;        // slots per workgroup
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
+  const unsigned blk = xcd_block(blockIdx.x, gridDim.x);
+  const int part = (int)(blk % (unsigned)RS);
+  const unsigned lblk = blk / (unsigned)RS;
+  const int l = (int)(lblk % (unsigned)L);
+  const long long bm = lblk / (unsigned)L;
+  const int m = (int)(bm % M);
+  const long long b = bm / M;
+  const int T = lv.T[l];
+  const int NL = T + 1;  // lists by base row r = -1 .. T-1 at list index r + 1
+  const int nsamp = Lq * P;
+  const bool striped = STG && ((striped_mask >> l) & 1u) != 0u;
+  unsigned* ekey = reinterpret_cast<unsigned*>(smem_raw);
+  f32x2* ecc = reinterpret_cast<f32x2*>(smem_raw + lay.off_cc);  // (c0, c1), then (d0, d1)
+  int* pos_of = reinterpret_cast<int*>(smem_raw + lay.off_pos);   // STG: a sample's list position
+  float* xb = reinterpret_cast<float*>(smem_raw + lay.off_xb);    // hand-overs / wave partials
+  int* cur = reinterpret_cast<int*>(smem_raw + lay.off_cur);
+  int* pb = reinterpret_cast<int*>(smem_raw + lay.off_pb);
+  int* scratch = reinterpret_cast<int*>(smem_raw + lay.off_scr);
+#ifdef MSDA_PHASE_TIMING  // debug build only: per-phase wall clock of the (b=0, m=0) workgroups
+  unsigned long long tph[6];
+  tph[0] = wall_clock64();
+#define MSDA_PH(i) do { __syncthreads(); tph[i] = wall_clock64(); } while (0)
+#else
+#define MSDA_PH(i) do { } while (0)
+#endif
+
+  for (int i = threadIdx.x; i < NL; i += kGvThreads) cur[i] = 0;
+  __syncthreads();
+
+  const int LP = L * P;
+  const long long qs = (long long)M * LP;
+  const float* __restrict__ locb = loc + (b * Lq * M + m) * LP + l * P;
+  const float* __restrict__ awb = aw + (b * Lq * M + m) * LP + l * P;
+  float* __restrict__ gab = gaw == nullptr ? nullptr : gaw + (b * Lq * M + m) * LP + l * P;
+  float* __restrict__ glb = gloc == nullptr ? nullptr : gloc + (b * Lq * M + m) * LP + l * P;
+  const bool coords = gab != nullptr || glb != nullptr;
+  // list index of a sample (base row + 1); -1 when neither tap is on the map (ZEROS)
+  auto list_index = [&](const Taps<float>& t) -> int {
+    if constexpr (ZEROS) return t.ok0 ? t.i0 + 1 : (t.ok1 ? 0 : -1);
+    else return t.i0 + 1;
+  };
+
+  // 1. samples per list; the first kGvCache samples of every thread keep loc in registers
+  float cl[kGvCache];
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) {
+      const int q = s / P, p = s - q * P;
+      cl[k] = locb[q * qs + p];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) {
+      const int li = list_index(make_taps<float, ZEROS>(cl[k], T));
+      if (li >= 0) atomicAdd(&cur[li], 1);
+    }
+  }
+  for (int s = threadIdx.x + kGvCache * kGvThreads; s < nsamp; s += kGvThreads) {
+    const int q = s / P, p = s - q * P;
+    const int li = list_index(make_taps<float, ZEROS>(locb[q * qs + p], T));
+    if (li >= 0) atomicAdd(&cur[li], 1);
+  }
+  __syncthreads();
+  MSDA_PH(1);
+
+  // 2. exclusive scan over the lists: thread i owns lists [i*chunk, (i+1)*chunk)
+  const int chunk = (NL + kGvThreads - 1) / kGvThreads;
+  const int clo = min((int)threadIdx.x * chunk, NL), chi = min(clo + chunk, NL);
+  int N = 0;  // listed samples of the level
+  {
+    int mine = 0;
+    for (int i = clo; i < chi; ++i) mine += cur[i];
+    int run = block_exclusive_scan(mine, scratch, &N);
+    for (int i = clo; i < chi; ++i) {
+      const int c = cur[i];
+      cur[i] = run;
+      run += c;
+    }
+  }
+  __syncthreads();
+  // this workgroup's window of positions: snapped to list starts at even shares (cur = starts now)
+  auto snap = [&](long long t) -> int {  // first list start >= t (N if none)
+    if (t <= 0) return 0;
+    if (t >= N || cur[NL - 1] < t) return N;
+    int lo = 0, hi = NL - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cur[mid] >= t) hi = mid; else lo = mid + 1;
+    }
+    return cur[lo];
+  };
+  const int wlo = part == 0 ? 0 : snap((long long)N * part / RS);
+  const int whi = part == RS - 1 ? N : snap((long long)N * (part + 1) / RS);
+  if (RS > 1) __syncthreads();  // every thread has read the starts before placement moves them
+
+  // 3. place key and (c0, c1) in list order (cur[li] ends at the end of list li); STG: the
+  // sample's position, for the coordinate epilogue
+  auto place = [&](int s, float lc) {
+    const Taps<float> t = make_taps<float, ZEROS>(lc, T);
+    const int li = list_index(t);
+    const int q = s / P, p = s - q * P;
+    if (li >= 0) {
+      const int pos = atomicAdd(&cur[li], 1);
+      ekey[pos] = ((unsigned)q << 8) | (unsigned)p;
+      if constexpr (STG) {
+        const float a = awb[q * qs + p];
+        ecc[pos] = f32x2{t.ok0 ? a * t.w0 : 0.f, t.ok1 ? a * t.w1 : 0.f};
+        pos_of[s] = pos;
+      }
+    } else if (part == 0) {  // no tap on the map: zero coordinate gradients
+      const long long o = q * qs + p;
+      if (gab != nullptr) gab[o] = 0.f;
+      if (glb != nullptr) glb[o] = 0.f;
+    }
+  };
+#pragma unroll
+  for (int k = 0; k < kGvCache; ++k) {
+    const int s = threadIdx.x + k * kGvThreads;
+    if (s < nsamp) place(s, cl[k]);
+  }
+  for (int s = threadIdx.x + kGvCache * kGvThreads; s < nsamp; s += kGvThreads) {
+    const int q = s / P, p = s - q * P;
+    place(s, locb[q * qs + p]);
+  }
+  __syncthreads();
+  if (sort_rows) {  // deterministic mode: every list in key order (insertion sort)
+    for (int i = clo; i < chi; ++i) {
+      const int e1 = cur[i], e0 = (i == 0 ? 0 : cur[i - 1]);
+      for (int x = e0 + 1; x < e1; ++x) {
+        const unsigned key = ekey[x];
+        f32x2 kc = f32x2{0.f, 0.f};
+        if constexpr (STG) kc = ecc[x];
+        int y = x - 1;
+        while (y >= e0 && ekey[y] > key) {
+          ekey[y + 1] = ekey[y];
+          if constexpr (STG) ecc[y + 1] = ecc[y];
+          --y;
+        }
+        ekey[y + 1] = key;
+        if constexpr (STG) ecc[y + 1] = kc;
+      }
+    }
+    __syncthreads();
+    if (STG)  // the sorted positions
+      for (int e = (int)threadIdx.x; e < N; e += kGvThreads) {
+        const unsigned key = ekey[e];
+        pos_of[(int)(key >> 8) * P + (int)(key & 0xffu)] = e;
+      }
+    __syncthreads();
+  }
+  MSDA_PH(2);
+
+  // 4. the window's rows and pre-list, then slots (run mode); cur[li] = end of list li now
+  auto en = [&](int r) -> int { return cur[r + 1]; };          // end of list r   (r >= -1)
+  auto st = [&](int r) -> int { return r >= 0 ? cur[r] : 0; };  // start of list r
+  auto snap_e = [&](long long t) -> int {  // first list start >= t (N if none)
+    if (t <= 0) return 0;
+    if (t >= N || st(T - 1) < t) return N;
+    int lo = 0, hi = T - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (st(mid) >= t) hi = mid; else lo = mid + 1;
+    }
+    return st(lo);
+  };
+  auto row_of = [&](int pos) -> int {  // base row of the list holding position pos < N
+    int lo = -1, hi = T - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;  // arithmetic shift: floor, also for lo = -1
+      if (en(mid) > pos) hi = mid; else lo = mid + 1;
+    }
+    return lo;
+  };
+  int rlo = 0, rhi = 0, pre = wlo;  // rows [rlo, rhi) are this workgroup's to write from the pull
+  if (wlo < whi) {
+    const int bf = row_of(wlo), bl = row_of(whi - 1);
+    rlo = bf;
+    rhi = bl + 1 >= T ? T : (st(bl + 1) == en(bl + 1) ? bl + 2 : bl + 1);
+    if (part > 0 && st(bf - 1) < en(bf - 1)) pre = st(bf - 1);
+  }
+  // row mode (sparse levels: decoder-like calls, a few samples a row): every slot builds whole
+  // rows r from the entries of lists r-1 (c1) and r (c0) — each entry gathered by both of its rows,
+  // but rows need no hand-over and every slot runs independently
+  const bool rowmode = STG && (long long)N <= 4LL * NL;
+  if (!striped && !rowmode && (int)threadIdx.x <= W) {
+    const int j = threadIdx.x;
+    pb[j] = j == 0 ? pre : (j == W ? whi : snap_e(wlo + (long long)(whi - wlo) * j / W));
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int slot = lane / LPR;
+  const int c_l = lane - slot * LPR;
+  const int rs = M * D;  // row stride; offsets inside one clip fit 32 bits
+  // wave-uniform bases + 32-bit lane offsets
+  const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D;
+  const long long vofs = ((b * S + lv.start[l]) * M + m) * (long long)D;
+  const scalar_t* __restrict__ vl = value + vofs;
+  scalar_t* __restrict__ gvl = gval + vofs;
+  const int co = c_l * CPL;
+
+  // rows with no listed tap on either side (lists r-1 and r empty) are zero
+  {
+    const int zlo = (int)((long long)T * part / RS), zhi = (int)((long long)T * (part + 1) / RS);
+#ifndef MSDA_PAIR_NO_ZERO  // A/B timing builds only
+    for (int x = zlo + wave * NSLOT + slot; x < zhi; x += W)
+      if (st(x - 1) == en(x)) *reinterpret_cast<uint4*>(gvl + (x * rs + co)) = make_uint4(0u, 0u, 0u, 0u);
+#endif
+  }
+
+  // 5. pull
+  auto vload = [&](int x) -> uint4 {  // value row x (zeros off the level)
+    if (!coords || x < 0 || x >= T) return make_uint4(0u, 0u, 0u, 0u);
+    return load16_if_nt(true, vl + (x * rs + co));
+  };
+  auto store_row = [&](int x, const f32x2 (&a)[H]) {
+    float o[CPL];
+#pragma unroll
+    for (int e = 0; e < H; ++e) {
+      o[2 * e] = a[e].x;
+      o[2 * e + 1] = a[e].y;
+    }
+#ifndef MSDA_PAIR_NO_STORE  // A/B timing builds only
+    store_vec_nt<scalar_t, CPL>(gvl + (x * rs + co), o);
+#endif
+  };
+  f32x2 a0[H], a1[H];
+#pragma unroll
+  for (int e = 0; e < H; ++e) a0[e] = a1[e] = f32x2{0.f, 0.f};
+  uint4 v0, v1;
+  // one batch: the slot's entries ebase + u * STR below lim, all of list rb (rows rb, rb + 1)
+  auto batch = [&](int ebase, int STR, int lim) {
+    uint4 g[U];
+    f32x2 cc[U];
+    float lcv[U], acv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = ebase + u * STR;
+      const bool have = e < lim;
+      const unsigned key = ekey[have ? e : 0];
+      g[u] = *reinterpret_cast<const uint4*>(gb + (__umul24(key >> 8, (unsigned)rs) + co));
+      if constexpr (STG) {
+        cc[u] = ecc[have ? e : 0];
+        if (!have) cc[u] = f32x2{0.f, 0.f};
+      } else {
+        const long long o = (long long)(key >> 8) * qs + (key & 0xffu);
+        lcv[u] = locb[o];
+        acv[u] = have ? awb[o] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = ebase + u * STR;
+      const bool have = e < lim;
+      Taps<float> t{};
+      if constexpr (!STG) {
+        t = make_taps<float, ZEROS>(lcv[u], T);
+        cc[u] = f32x2{t.ok0 ? acv[u] * t.w0 : 0.f, t.ok1 ? acv[u] * t.w1 : 0.f};
+      }
+      f32x2 x[H];
+      cvt16x2<scalar_t, CPL>(g[u], x);
+      const f32x2 k0{cc[u].x, cc[u].x}, k1{cc[u].y, cc[u].y};
+#pragma unroll
+      for (int e2 = 0; e2 < H; ++e2) {
+        a0[e2] = pk_fma(x[e2], k0, a0[e2]);
+        a1[e2] = pk_fma(x[e2], k1, a1[e2]);
+      }
+      if (coords) {
+        const float d0 = group_sum<LPR>(dot16<scalar_t>(g[u], v0));
+        const float d1 = group_sum<LPR>(dot16<scalar_t>(g[u], v1));
+        if (have && c_l == 0) {
+          if constexpr (STG) {
+            ecc[e] = f32x2{d0, d1};
+          } else if (e >= wlo) {  // pre-list samples belong to the previous workgroup
+            const unsigned key = ekey[e];
+            const long long o = (long long)(key >> 8) * qs + (key & 0xffu);
+            if (gab != nullptr) gab[o] = d0 * t.w0 + d1 * t.w1;
+            if (glb != nullptr) glb[o] = ((d1 - d0) * acv[u]) * t.gmul;
+          }
+        }
+      }
+    }
+  };
+
+  if (rowmode) {
+    const int j = wave * NSLOT + slot;
+    float* ed = reinterpret_cast<float*>(ecc);  // entry e: [2e] = c0 -> d0, [2e + 1] = c1 -> d1
+    const int rend = min(rhi, T - 1);  // row rhi: the dots of the window's last list only
+    for (int rr = max(rlo, 0); rr <= rend; rr += W) {
+      const int r = rr + j;
+      const bool rv = r <= rend;
+      int pos = rv ? st(r - 1) : 0;
+      const int mid = rv ? en(r - 1) : 0, hi = rv ? en(r) : 0;
+      v0 = vload(rv ? r : -1);
+#pragma unroll
+      for (int e = 0; e < H; ++e) a0[e] = f32x2{0.f, 0.f};
+      while (__ballot(pos < hi) != 0ull) {
+        const int lim = min(pos + U, hi);
+        uint4 g[U];
+        float k[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = pos + u;
+          const bool have = e < lim;
+          const unsigned key = ekey[have ? e : 0];
+          g[u] = *reinterpret_cast<const uint4*>(gb + (__umul24(key >> 8, (unsigned)rs) + co));
+          k[u] = have ? ed[2 * e + (e < mid ? 1 : 0)] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int e = pos + u;
+          f32x2 x[H];
+          cvt16x2<scalar_t, CPL>(g[u], x);
+          const f32x2 kk{k[u], k[u]};
+#pragma unroll
+          for (int e2 = 0; e2 < H; ++e2) a0[e2] = pk_fma(x[e2], kk, a0[e2]);
+          if (coords) {
+            const float d = group_sum<LPR>(dot16<scalar_t>(g[u], v0));
+            if (e < lim && c_l == 0) ed[2 * e + (e < mid ? 1 : 0)] = d;
+          }
+        }
+        pos = max(pos, lim);
+      }
+      if (rv && r < rhi) store_row(r, a0);
+    }
+    MSDA_PH(3);
+  } else if (!striped) {
+    const int j = wave * NSLOT + slot;
+    const int lo = pb[j], hi = pb[j + 1];
+    int rb = lo < hi ? row_of(lo) : 0;
+    // the slot's first row also takes the c1 part of list rb-1 from the slot before
+    const int hold_row = (j > 0 && lo < hi && rb >= 0 && st(rb - 1) < en(rb - 1)) ? rb : -2;
+    f32x2 hold[H];
+#pragma unroll
+    for (int e = 0; e < H; ++e) hold[e] = f32x2{0.f, 0.f};
+    auto flush = [&](int x, const f32x2 (&a)[H]) {
+      if (x < rlo || x >= rhi || x < 0) return;  // another workgroup's row
+      if (x == hold_row) {
+#pragma unroll
+        for (int e = 0; e < H; ++e) hold[e] = a[e];
+      } else {
+        store_row(x, a);
+      }
+    };
+    int eo = lo < hi ? en(rb) : 0;  // end of list rb
+    v0 = vload(rb);
+    v1 = vload(rb + 1);
+    int pos = lo;
+    while (__ballot(pos < hi) != 0ull) {
+      const bool act = pos < hi;
+      const int lim = act ? min(pos + U, eo) : pos;
+      batch(pos, 1, lim);
+      pos = lim;
+      if (act && pos < hi && pos == eo) {  // list rb done: row rb is final
+        int nb = rb + 1;
+        while (en(nb) == pos) ++nb;  // next list with entries
+        flush(rb, a0);
+        if (nb == rb + 1) {
+#pragma unroll
+          for (int e = 0; e < H; ++e) {
+            a0[e] = a1[e];
+            a1[e] = f32x2{0.f, 0.f};
+          }
+          v0 = v1;
+          v1 = vload(nb + 1);
+        } else {  // list rb+1 empty: row rb+1 holds only list rb's c1 part
+          flush(rb + 1, a1);
+#pragma unroll
+          for (int e = 0; e < H; ++e) a0[e] = a1[e] = f32x2{0.f, 0.f};
+          v0 = vload(nb);
+          v1 = vload(nb + 1);
+        }
+        rb = nb;
+        eo = en(nb);
+      }
+    }
+    bool send = false;
+    if (lo < hi) {
+      flush(rb, a0);
+      const int x = rb + 1;
+      if (x < T) {
+        if (st(x) < en(x)) send = x < rhi;  // list x goes on in the next slot: hand its row over
+        else flush(x, a1);
+      }
+    }
+    MSDA_PH(3);
+    // hand-overs: a slot's c1 part goes to the next slot with entries; inside the wave by lane
+    // shuffles (empty slots pass on what they got), across waves through LDS
+    const bool busy = lo < hi;
+    f32x2 fwd[H], inc[H];
+#pragma unroll
+    for (int e = 0; e < H; ++e) fwd[e] = send ? a1[e] : f32x2{0.f, 0.f};
+    auto up = [&](const f32x2 (&x)[H], f32x2 (&y)[H]) {
+#pragma unroll
+      for (int e = 0; e < H; ++e) {
+        y[e].x = __shfl_up(x[e].x, LPR);
+        y[e].y = __shfl_up(x[e].y, LPR);
+      }
+    };
+    for (int step = 0; step < NSLOT - 1; ++step) {
+      up(fwd, inc);
+      if (!busy && slot > 0)
+#pragma unroll
+        for (int e = 0; e < H; ++e) fwd[e] = inc[e];
+    }
+    up(fwd, inc);
+    const unsigned long long busy_lanes = __ballot(busy && c_l == 0);
+    int* wflag = reinterpret_cast<int*>(xb + NW * D);
+    if (slot == NSLOT - 1) {  // the wave's carry-out: the c1 part of its last slot with entries
+      float* cb = xb + (wave * D + co);
+#pragma unroll
+      for (int e = 0; e < H; ++e) {
+        cb[2 * e] = fwd[e].x;
+        cb[2 * e + 1] = fwd[e].y;
+      }
+      if (c_l == 0) wflag[wave] = busy_lanes != 0ull;
+    }
+    __syncthreads();
+    if (hold_row >= 0) {
+      const unsigned long long below = busy_lanes & ((1ull << (slot * LPR)) - 1ull);
+      if (below != 0ull) {  // a slot of this wave sent it
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+          hold[e].x += inc[e].x;
+          hold[e].y += inc[e].y;
+        }
+      } else if (wave > 0) {  // the last slot with entries of the nearest earlier wave that has any
+        int w = wave - 1;
+        while (w > 0 && wflag[w] == 0) --w;
+        const float* cb = xb + (w * D + co);
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+          hold[e].x += cb[2 * e];
+          hold[e].y += cb[2 * e + 1];
+        }
+      }
+      store_row(hold_row, hold);
+    }
+  } else {
+    // striped: wave w owns positions [qlo, qhi); its slots take every NSLOT-th entry of a list
+    const int qlo = wave == 0 ? pre : wlo + (int)((long long)(whi - wlo) * wave / NW);
+    const int qhi = wlo + (int)((long long)(whi - wlo) * (wave + 1) / NW);
+    int* ptag = reinterpret_cast<int*>(xb + NW * kPairParts * D);  // [NW][kPairParts] rows, -1 = unused
+    int npart = 0;
+    auto flush = [&](int x, f32x2 (&a)[H]) {  // wave-uniform
+      if (x < rlo || x >= rhi || x < 0) return;
+      const int c_lo = st(x - 1), c_hi = en(x);
+      if (c_lo >= c_hi) return;  // a zero row (the sweep wrote it)
+      for (int o = LPR; o < 64; o <<= 1) {
+#pragma unroll
+        for (int e = 0; e < H; ++e) {
+          a[e].x += __shfl_xor(a[e].x, o);
+          a[e].y += __shfl_xor(a[e].y, o);
+        }
+      }
+      if (c_lo >= qlo && c_hi <= qhi) {  // every tap of the row is in this wave's share
+        if (slot == 0) store_row(x, a);
+      } else {
+        if (slot == 0) {
+          float* pr = xb + ((wave * kPairParts + npart) * D + co);
+#pragma unroll
+          for (int e = 0; e < H; ++e) {
+            pr[2 * e] = a[e].x;
+            pr[2 * e + 1] = a[e].y;
+          }
+          if (c_l == 0) ptag[wave * kPairParts + npart] = x;
+        }
+        ++npart;
+      }
+    };
+    if (lane < kPairParts) ptag[wave * kPairParts + lane] = -1;
+    if (qlo < qhi) {
+      int rb = row_of(qlo);
+      int eo = en(rb);
+      v0 = vload(rb);
+      v1 = vload(rb + 1);
+      int pos = qlo;
+      while (pos < qhi) {
+        const int lim = min(min(pos + NSLOT * U, eo), qhi);
+        batch(pos + slot, NSLOT, lim);
+        pos = lim;
+        if (pos < qhi && pos == eo) {
+          int nb = rb + 1;
+          while (en(nb) == pos) ++nb;
+          flush(rb, a0);
+          if (nb == rb + 1) {
+#pragma unroll
+            for (int e = 0; e < H; ++e) {
+              a0[e] = a1[e];
+              a1[e] = f32x2{0.f, 0.f};
+            }
+            v0 = v1;
+            v1 = vload(nb + 1);
+          } else {
+            flush(rb + 1, a1);
+#pragma unroll
+            for (int e = 0; e < H; ++e) a0[e] = a1[e] = f32x2{0.f, 0.f};
+            v0 = vload(nb);
+            v1 = vload(nb + 1);
+          }
+          rb = nb;
+          eo = en(nb);
+        }
+      }
+      flush(rb, a0);
+      flush(rb + 1, a1);
+    }
+    MSDA_PH(3);
+    __syncthreads();
+    // partial rows: the first wave holding row x sums the partials of x over the waves in order
+    {
+      const int j = wave * NSLOT + slot;
+      if (j < NW * kPairParts) {
+        const int w = j / kPairParts;
+        const int x = ptag[j];
+        bool first = x >= 0;  // no earlier wave holds row x (waves with empty shares hold none)
+        for (int k = 0; first && k < w * kPairParts; ++k) first = ptag[k] != x;
+        if (first) {
+          float o[CPL];
+          const float* p0 = xb + (j * D + co);
+#pragma unroll
+          for (int e = 0; e < CPL; ++e) o[e] = p0[e];
+          for (int k = (w + 1) * kPairParts; k < NW * kPairParts; ++k) {
+            if (ptag[k] != x) continue;
+            const float* p2 = xb + (k * D + co);
+#pragma unroll
+            for (int e = 0; e < CPL; ++e) o[e] += p2[e];
+          }
+          store_vec_nt<scalar_t, CPL>(gvl + (x * rs + co), o);
+        }
+      }
+    }
+  }
+
+  // 6. coordinate gradients from the dots, in sample order (coalesced loc / aw / output): a
+  // sample of this workgroup's window finds its list position parked in its output slot
+  if constexpr (STG) {
+    if (coords) {
+      __syncthreads();  // every dot written
+      MSDA_PH(5);
+      const int li_lo = wlo < whi ? row_of(wlo) + 1 : 1, li_hi = wlo < whi ? row_of(whi - 1) + 1 : 0;
+      for (int s0 = threadIdx.x; s0 < nsamp; s0 += kGvThreads * kGvCache) {
+        float lcv[kGvCache], acv[kGvCache];
+#pragma unroll
+        for (int k = 0; k < kGvCache; ++k) {  // unconditional loads (clamped index): all in flight
+          const int s = min(s0 + k * kGvThreads, nsamp - 1);
+          const int q = s / P, p = s - q * P;
+          const long long o = q * qs + p;
+          lcv[k] = locb[o];
+          acv[k] = awb[o];
+        }
+#pragma unroll
+        for (int k = 0; k < kGvCache; ++k) {
+          const int s = s0 + k * kGvThreads;
+          if (s < nsamp) {
+            const Taps<float> t = make_taps<float, ZEROS>(lcv[k], T);
+            const int li = list_index(t);
+            if (li >= li_lo && li <= li_hi) {
+              const int q = s / P, p = s - q * P;
+              const long long o = q * qs + p;
+              const f32x2 d = ecc[pos_of[s]];
+              if (gab != nullptr) gab[o] = d.x * t.w0 + d.y * t.w1;
+              if (glb != nullptr) glb[o] = ((d.y - d.x) * acv[k]) * t.gmul;
+            }
+          }
+        }
+      }
+    }
+  }
+#ifdef MSDA_PHASE_TIMING
+  MSDA_PH(4);
+  if (threadIdx.x == 0 && bm == 0 && part == 0)
+    printf("pair l=%d T=%d N=%d striped=%d row=%d hist=%llu scan+place=%llu pull=%llu handover=%llu coords=%llu (x10ns)\n",
+           l, T, N, (int)striped, (int)rowmode, tph[1] - tph[0], tph[2] - tph[1], tph[3] - tph[2], tph[5] - tph[3],
+           tph[4] - tph[5]);
 #endif
 #undef MSDA_PH
 }
@@ -1781,12 +2419,166 @@ int run_backward_fused(const Problem& pr, int ns, const void* value, const void*
   return launch_status("backward fused");
 }
 
+// ---- pair-pull backward: path choice and LDS plan ----
+// MSDA_HIP_BWD_PATH: unset = pair kernel where it applies; "fused1" = per-tap fused kernel,
+// "unfused" = gvalue + coordinate kernels, "split" = sort + pull + coordinates (A/B builds).
+int bwd_env_path() {
+  static const int path = [] {
+    const char* e = getenv("MSDA_HIP_BWD_PATH");
+    if (e == nullptr || e[0] == 0) return 0;
+    if (strcmp(e, "fused1") == 0) return 1;
+    if (strcmp(e, "unfused") == 0) return 2;
+    if (strcmp(e, "split") == 0) return 3;
+    return 0;
+  }();
+  return path;
+}
+
+int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return (e != nullptr && e[0] != 0) ? atoi(e) : dflt;
+}
+
+constexpr size_t kPairLdsMax = 160 * 1024;
+
+struct PairPlan {
+  PairLayout lay;
+  size_t lds;
+  unsigned striped_mask;
+  bool stg;
+};
+
+size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// LDS bytes of the pair kernel: keys | (c0, c1), sample positions (STG) | wave carry-outs or wave
+// partials | T+1 list cursors | W+1 slot bounds | scan scratch.
+size_t pair_layout(long long N, long long D, int ns, long long maxT, bool stg, bool any_striped,
+                   PairLayout* lay) {
+  const size_t W = (size_t)(kGvThreads / 64) * ns;
+  const size_t keys = a16((size_t)N * 4);
+  const size_t hand = (size_t)(kGvThreads / 64) * (D * 4 + 4);  // per-wave carry-out + flag
+  const size_t parts = any_striped ? (size_t)(kGvThreads / 64) * kPairParts * (D * 4 + 4) : 0;
+  lay->off_cc = (int)keys;
+  lay->off_pos = (int)(keys + (stg ? a16((size_t)N * 8) : 0));
+  lay->off_xb = lay->off_pos + (int)(stg ? a16((size_t)N * 4) : 0);
+  const size_t end = (size_t)lay->off_xb + a16(std::max(hand, parts));
+  lay->off_cur = (int)a16(end);
+  lay->off_pb = lay->off_cur + (int)a16((size_t)(maxT + 2) * 4);
+  lay->off_scr = lay->off_pb + (int)a16((W + 1) * 4);
+  return (size_t)lay->off_scr + 32 * 4;
+}
+
+// Slots per wave of the pair kernel (16-byte chunks: D/CPL lanes per row), or 0.
+int pair_slots(int value_dtype, long long D) {
+  if (value_dtype == MSDA_DTYPE_F64) return 0;
+  const long long cpl = value_dtype == MSDA_DTYPE_F32 ? 4 : 8;
+  if (D % cpl != 0) return 0;
+  const long long lpr = D / cpl;
+  return lpr == 8 ? 8 : lpr == 16 ? 4 : lpr == 32 ? 2 : lpr == 64 ? 1 : 0;
+}
+
+// The plan for a call (levels known) or, with T == nullptr, the bound used by the workspace
+// query (every level taken as S rows long, no striped level): if the bound fits, the call does.
+// Striped levels: fewer lists than twice the slots (T + 1 < 2 W), at least 4 slots a wave (the partial-row
+// merge uses one slot per partial), STG only.  MSDA_HIP_STRIPED_ROWS caps T (A/B builds; read per
+// call so tests can switch it).
+bool pair_plan(int value_dtype, long long Lq, long long P, long long D, long long L, const int* T,
+               long long S, PairPlan* pp) {
+  if (bwd_env_path() != 0) return false;
+  const int ns = pair_slots(value_dtype, D);
+  if (ns == 0 || P > 256 || Lq >= (1LL << 24) || Lq * P >= (1LL << 30)) return false;
+  const long long N = Lq * P;
+  const long long W = (kGvThreads / 64) * ns;
+  const int striped_rows = env_int("MSDA_HIP_STRIPED_ROWS", 1 << 30);
+  long long maxT = 1;
+  unsigned mask = 0;
+  if (T == nullptr) {
+    maxT = S;
+  } else {
+    for (int l = 0; l < L; ++l) {
+      maxT = std::max(maxT, (long long)T[l]);
+      if (ns >= 4 && T[l] + 1 < 2 * W && T[l] <= striped_rows) mask |= 1u << l;
+    }
+  }
+  for (int stg = 1; stg >= 0; --stg) {
+    PairLayout lay;
+    const size_t lds = pair_layout(N, D, ns, maxT, stg != 0, stg != 0 && mask != 0, &lay);
+    if (lds <= kPairLdsMax) {
+      pp->lay = lay;
+      pp->lds = lds;
+      pp->striped_mask = stg ? mask : 0u;
+      pp->stg = stg != 0;
+      return true;
+    }
+  }
+  return false;
+}
+
+template <typename scalar_t>
+int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, const void* loc,
+                      const void* aw, const void* gout, void* gval, void* gloc, void* gaw, int pad,
+                      hipStream_t st) {
+  static const int det = env_int("MSDA_HIP_DETERMINISTIC", 0);
+  const int ns = pair_slots(std::is_same<scalar_t, float>::value ? MSDA_DTYPE_F32 : MSDA_DTYPE_BF16, pr.D);
+  const long long wgs = pr.B * pr.M * pr.L;
+  // workgroups per (b, m, level): enough to fill the chip's 256 CUs (MSDA_HIP_PAIR_RS overrides)
+  int rs = env_int("MSDA_HIP_PAIR_RS", 0);
+  if (rs <= 0) rs = wgs >= 256 ? 1 : (int)std::min<long long>(8, (256 + wgs - 1) / wgs);
+  const unsigned blocks = (unsigned)(wgs * rs);
+  const bool z = pad == MSDA_PAD_ZEROS;
+  auto* v = static_cast<const scalar_t*>(value);
+  auto* lc = static_cast<const float*>(loc);
+  auto* a = static_cast<const float*>(aw);
+  auto* g = static_cast<const scalar_t*>(gout);
+  auto* gv = static_cast<scalar_t*>(gval);
+  auto* gl = static_cast<float*>(gloc);
+  auto* ga = static_cast<float*>(gaw);
+  int rc;
+#define MSDA_PA_(NSL, Z, STGV, UU)                                                                  \
+  do {                                                                                          \
+    if ((rc = allow_lds(msda_bwd_pair_kernel<scalar_t, NSL, Z, STGV, UU>, pp.lds))) return rc;   \
+    hipLaunchKernelGGL((msda_bwd_pair_kernel<scalar_t, NSL, Z, STGV, UU>), dim3(blocks),         \
+                       dim3(kGvThreads), pp.lds, st, v, lc, a, g, gv, gl, ga, pr.lv, (int)pr.L,   \
+                       (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, rs, pp.striped_mask, \
+                       det, pp.lay);                                                            \
+  } while (0)
+#ifndef MSDA_PAIR_U
+#define MSDA_PAIR_U 8  // gathers in flight per slot
+#endif
+#define MSDA_PA(NSL, Z)                                                                           \
+  do {                                                                                          \
+    if (!pp.stg) MSDA_PA_(NSL, Z, false, MSDA_PAIR_U);                                          \
+    else MSDA_PA_(NSL, Z, true, MSDA_PAIR_U);                                                   \
+  } while (0)
+#define MSDA_PA_NS(Z)                                                                             \
+  switch (ns) {                                                                                 \
+    case 8: MSDA_PA(8, Z); break;                                                               \
+    case 4: MSDA_PA(4, Z); break;                                                               \
+    case 2: MSDA_PA(2, Z); break;                                                               \
+    default: MSDA_PA(1, Z); break;                                                              \
+  }
+  if (z) { MSDA_PA_NS(true) } else { MSDA_PA_NS(false) }
+#undef MSDA_PA_NS
+#undef MSDA_PA
+#undef MSDA_PA_
+  return launch_status("backward pair");
+}
+
 template <typename scalar_t, typename coord_t>
 int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
                  const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
                  int value_dtype, int pad, hipStream_t st) {
   if constexpr (std::is_same<coord_t, float>::value) {
     const int ns = pr.B * pr.M * pr.S > 0 ? fused_bwd_rows<scalar_t, coord_t>(pr, value_dtype, gval) : 0;
+    // sparse calls (every level at most 4 samples a row: decoder-like) stay on the per-tap fused
+    // kernel: few taps a row, so the pair kernel's halved gathers do not pay for its list walk
+    int minT = 1 << 30;
+    for (int l = 0; l < pr.L; ++l) minT = min(minT, pr.lv.T[l]);
+    const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1);
+    PairPlan pp;
+    if (gval != nullptr && pr.B * pr.M * pr.S > 0 && !(sparse && ns > 0) &&
+        pair_plan(value_dtype, pr.Lq, pr.P, pr.D, pr.L, pr.lv.T, pr.S, &pp))
+      return run_backward_pair<scalar_t>(pr, pp, value, loc, aw, gout, gval, gloc, gaw, pad, st);
     if (ns > 0)
       return run_backward_fused<scalar_t>(pr, ns, value, loc, aw, gout, gval, gloc, gaw, pad, st);
   }
@@ -2399,6 +3191,10 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
                                          int64_t num_levels, int64_t num_point) {
   (void)channels;
   if (batch <= 0 || spatial_size <= 0 || num_heads <= 0) return 0;
+  PairPlan pp;
+  if (value_dtype != MSDA_DTYPE_F64 &&
+      pair_plan(value_dtype, num_query, num_point, channels, num_levels, nullptr, spatial_size, &pp))
+    return 0;
   if (use_fused_gvalue(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point))
     return 0;
   return bwd_layout(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point).total;

@@ -34,18 +34,18 @@ def test_library_exports_every_declared_symbol():
 def test_abi_version_and_workspace():
     lib = PKG._native.load_library()
     assert lib.msda_hip_abi_version() == PKG._native.ABI_VERSION
-    # split path (sort + pull, few (b, m, level) workgroups): row table + per-row tap lists
     B, S, M, D, Lq, L, P = 2, 1920, 8, 64, 1920, 4, 4
-    f32 = lib.msda_hip_backward_workspace_bytes(0, B, S, M, D, Lq, L, P)
+    # pair-pull backward (16-byte chunks per lane, lists in LDS, any batch size): no workspace,
+    # also at T = 4096 (S = 7680: keys only in LDS)
+    for dt in (0, 2, 3):
+        assert lib.msda_hip_backward_workspace_bytes(dt, B, S, M, D, Lq, L, P) == 0
+    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) == 0
+    # split path (sort + pull): fp64, or heads not made of 16-byte chunks with few workgroups —
+    # row table + per-row tap lists
     f64 = lib.msda_hip_backward_workspace_bytes(1, B, S, M, D, Lq, L, P)
+    assert f64 >= B * M * S * 8 + B * M * L * 2 * Lq * P * 16
+    f32 = lib.msda_hip_backward_workspace_bytes(0, B, S, M, 30, Lq, L, P)
     assert f32 >= B * M * S * 8 + B * M * L * 2 * Lq * P * 8
-    assert f64 > f32
-    assert lib.msda_hip_backward_workspace_bytes(2, B, S, M, D, Lq, L, P) == f32  # bf16 keeps fp32 coords
-    # fused path (entry lists live in LDS, >= 256 (b, m, level) workgroups): no workspace,
-    # except fp64 (16-byte entries do not fit) and lists beyond the LDS budget
-    assert lib.msda_hip_backward_workspace_bytes(2, 8, S, M, D, Lq, L, P) == 0
-    assert lib.msda_hip_backward_workspace_bytes(1, 8, S, M, D, Lq, L, P) > 0
-    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) > 0
     assert lib.msda_hip_backward_workspace_bytes(0, 0, S, M, D, Lq, L, P) == 0
 
 

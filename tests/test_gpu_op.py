@@ -81,6 +81,7 @@ CASES = [
     ([16, 8, 4, 2],         8, 8, 30,   20, 2),    # odd channel count: lane-per-channel pull
     ([8, 4, 2, 1],          8, 8, 16,   200, 4),   # 800 taps on one row
     ([64, 32, 16, 8],       8, 8, 16,   4000, 2),  # 16000 entries: near the LDS budget
+    ([50, 25, 13, 7],       4, 8, 64,   1920, 4),  # video queries over the audio pyramid: ~1100 taps a row
 ]
 
 
@@ -215,3 +216,79 @@ def test_full_size_properties(dev, shapes, B):
     torch.testing.assert_close(oab, o1 + 0.5 * oa, rtol=1e-4, atol=1e-4)
     r_out = O.msda_forward(_np(v1[:1]), shapes, _np(loc[:1]), _np(aw[:1]))
     np.testing.assert_allclose(o1[:1].cpu().numpy(), r_out, rtol=2e-5, atol=2e-5)
+    # the whole backward of one clip against the oracle (clips are independent)
+    gv, gl, ga = msda.msda_backward(c(v1), shapes, starts, c(loc), c(aw), c(gout))
+    r_gv, r_gl, r_ga = O.msda_backward(_np(v1[:1]), shapes, _np(loc[:1]), _np(aw[:1]), _np(gout[:1]))
+    np.testing.assert_allclose(ga[:1].cpu().numpy(), r_ga, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(gv[:1].cpu().numpy(), r_gv, rtol=2e-4, atol=2e-4)
+    np.testing.assert_allclose(gl[:1].cpu().numpy(), r_gl, rtol=2e-4, atol=2e-5 * max(shapes))
+
+
+def clustered_locations(B, Lq, M, shapes, P, seed):
+    """Half the samples scattered, half piled onto a few positions per level: long lists on a few
+    rows (split between slots in table mode, walked by one slot in run mode) beside short ones."""
+    gen = torch.Generator().manual_seed(seed)
+    L = len(shapes)
+    loc = torch.rand(B, Lq, M, L, P, generator=gen)
+    hot = torch.tensor([0.1, 0.5, 0.73, 0.999]).view(1, 1, 1, 1, 4)
+    pick = torch.randint(0, 4, (B, Lq, M, L, P), generator=gen)
+    piled = hot.expand(B, Lq, M, L, 4).gather(-1, pick) + torch.randn(B, Lq, M, L, P, generator=gen) * 1e-3
+    mask = torch.rand(B, Lq, M, L, P, generator=gen) < 0.5
+    return torch.where(mask, piled, loc).clamp(-0.1, 1.1)
+
+
+@pytest.mark.parametrize("rs", ["", "1", "3", "8"])
+@pytest.mark.parametrize("striped_rows", ["0", ""])
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("shapes", [[256, 128, 64, 32], [1024, 512, 64, 32]])
+def test_pair_backward_work_splits_match_oracle(dev, monkeypatch, rs, striped_rows, padding, shapes):
+    """The pair-pull backward under each of its work splits: workgroups per (b, m, level)
+    (MSDA_HIP_PAIR_RS; "" = the default choice), run vs striped mode per level
+    (MSDA_HIP_STRIPED_ROWS: 0 = run mode everywhere, "" = striped where T + 1 < 2 x slots) and
+    row mode (levels with at most 4 samples a row: T = 1024, 512 in the second pyramid)."""
+    monkeypatch.setenv("MSDA_HIP_PAIR_RS", rs)
+    monkeypatch.setenv("MSDA_HIP_STRIPED_ROWS", striped_rows)
+    B, M, D, Lq, P = 2, 8, 64, 300, 4
+    value, _, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.float32, seed=21)
+    loc = clustered_locations(B, Lq, M, shapes, P, seed=22)
+    out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout, padding)
+    r_gv, r_gl, r_ga = O.msda_backward(_np(value), shapes, _np(loc), _np(aw), _np(gout), padding=padding)
+    np.testing.assert_allclose(_np(ga), r_ga, rtol=2e-5, atol=2e-5)
+    np.testing.assert_allclose(_np(gv), r_gv, rtol=2e-4, atol=2e-4)
+    np.testing.assert_allclose(_np(gl), r_gl, rtol=2e-4, atol=2e-5 * max(shapes))
+
+
+def test_deterministic_backward_is_bitwise_reproducible(dev, tmp_path):
+    """MSDA_HIP_DETERMINISTIC=1 (read once per process, so in a child process): lists sorted,
+    run mode only — two calls give bitwise equal gradients, equal to the default path within
+    fp32 summation-order error."""
+    import subprocess
+    import sys
+    import os
+    code = f"""
+import sys, torch
+sys.path.insert(0, {repr(str(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))})
+sys.path.insert(0, {repr(os.path.dirname(os.path.abspath(__file__)))})
+from test_gpu_op import rand_case, clustered_locations
+from conftest import PKG
+from oracle import msda_oracle as O
+shapes = [256, 128, 64, 32]
+value, _, aw, gout = rand_case(shapes, 2, 8, 64, 300, 4, torch.bfloat16, seed=31)
+loc = clustered_locations(2, 300, 8, shapes, 4, seed=32)
+args = [t.cuda() for t in (value, loc, aw, gout)]
+starts = O.level_starts(shapes)
+r1 = PKG.msda.msda_backward(args[0], shapes, starts, args[1], args[2], args[3])
+r2 = PKG.msda.msda_backward(args[0], shapes, starts, args[1], args[2], args[3])
+torch.save([t.cpu() for t in r1] + [t.cpu() for t in r2], sys.argv[1])
+"""
+    outs = {}
+    for det in ("1", "0"):
+        f = tmp_path / f"det{det}.pt"
+        env = dict(os.environ, MSDA_HIP_DETERMINISTIC=det)
+        subprocess.run([sys.executable, "-c", code, str(f)], check=True, env=env, timeout=300)
+        outs[det] = torch.load(f, weights_only=True)
+    d = outs["1"]
+    for a, b in zip(d[:3], d[3:]):
+        assert torch.equal(a, b)
+    for a, b in zip(d[:3], outs["0"][:3]):
+        torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)

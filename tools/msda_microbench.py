@@ -29,6 +29,8 @@ def make(regime, B, Lq, shapes, M, P, dtype, dev, seed=0):
     value = torch.randn(B, S, M, 64, generator=g).to(dev, dtype)
     if Lq == S:  # encoder: the reference points of every token (valid ratio 1)
         ref = torch.cat([(torch.arange(t, dtype=torch.float32) + 0.5) / t for t in shapes])
+    elif Lq == 1920:  # cross-modal: the video tokens' reference points over the audio pyramid
+        ref = torch.cat([(torch.arange(t, dtype=torch.float32) + 0.5) / t for t in (1024, 512, 256, 128)])
     else:
         ref = torch.rand(Lq, generator=g)
     ref = ref.view(1, Lq, 1, 1, 1).expand(B, Lq, M, L, P)
@@ -71,15 +73,19 @@ def main():
     ap.add_argument("--kernels", default="fwd,bwd_loc_aw,bwd_value,bwd_all,prologue_fwd,prologue_bwd")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    shapes = [1024, 512, 256, 128]
-    starts = [0, 1024, 1536, 1792]
-    S, M, L, P, D = sum(shapes), 8, 4, 4, 64
+    M, L, P, D = 8, 4, 4, 64
+    # (name, level shapes, Lq): configs[1] encoder / decoder calls, configs[3]'s T=4096 encoder
+    # call, configs[2]'s video queries over the audio pyramid (T_a = 50)
+    calls = [("enc", [1024, 512, 256, 128], 1920), ("dec", [1024, 512, 256, 128], 100),
+             ("enc4096", [4096, 2048, 1024, 512], 7680), ("xmod", [50, 25, 13, 7], 1920)]
     for dname in args.dtypes.split(","):
         dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[dname]
         vb = 2 if dtype == torch.bfloat16 else 4
-        for Lq, shape_name in ((S, "enc"), (100, "dec")):
+        for shape_name, shapes, Lq in calls:
             if shape_name not in args.shapes.split(","):
                 continue
+            S = sum(shapes)
+            starts = [sum(shapes[:i]) for i in range(L)]
             for regime in args.regimes.split(","):
                 value, loc, aw, gout = make(regime, args.B, Lq, shapes, M, P, dtype, dev)
                 fwd_b = msda.algorithmic_bytes("fwd", args.B, S, M, D, Lq, L, P, vb)
