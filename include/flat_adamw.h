@@ -25,10 +25,13 @@ extern "C" {
 size_t flat_adamw_workspace_bytes(void);
 
 /* One optimizer step over n parameters (16-byte aligned fp32 buffers; bf16_shadow may be NULL).
- * max_norm <= 0 disables clipping.  Returns 0, or non-zero with flat_adamw_last_error(). */
+ * max_norm <= 0 disables clipping.  lr_wd: NULL, or a device array {lr, weight_decay} read by the
+ * kernels in place of the lr / weight_decay arguments, so that a captured HIP graph follows a
+ * learning-rate schedule (reference main.py:99 StepLR) instead of replaying the capture's values.
+ * Returns 0, or non-zero with flat_adamw_last_error(). */
 int flat_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, uint16_t* bf16_shadow,
                     int64_t n, float* step, void* workspace, float lr, float beta1, float beta2, float eps,
-                    float weight_decay, float max_norm, void* stream);
+                    float weight_decay, float max_norm, const float* lr_wd, void* stream);
 
 /* Column sums in fp32 of a row-major (K, N) matrix x (dtype tag as msda_hip.h: 0 fp32, 2 bf16,
  * 3 fp16; N*elt a multiple of 16 bytes, x 16-byte aligned): the bias gradient of the autocast

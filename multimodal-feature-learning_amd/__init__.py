@@ -23,7 +23,21 @@ import sys as _sys
 # step replayed after eager work that allocates device memory produced corrupted gradients
 # (tools/step_diag.py --graph 1; exact again with the capture off).  Replays
 # with nothing allocating between them were exact either way.
-_os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+_PACKET_CAPTURE_VAR = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
+import torch as _torch  # noqa: E402  (importing torch does not initialise HIP)
+# HIP already up when the package was imported: the variable counts only if it was set by then
+_HIP_UP_AT_IMPORT = _torch.cuda.is_initialized()
+_PACKET_CAPTURE_AT_IMPORT = _os.environ.get(_PACKET_CAPTURE_VAR)
+_os.environ.setdefault(_PACKET_CAPTURE_VAR, "0")
+
+
+def graph_packet_capture_off():
+    """True when the HIP runtime of this process runs with the graph packet capture off: the
+    variable is "0" now, and it was already "0" when HIP initialised (the package set it, HIP
+    initialising after the import; or the environment had it before HIP came up)."""
+    if _os.environ.get(_PACKET_CAPTURE_VAR) != "0":
+        return False
+    return (not _HIP_UP_AT_IMPORT) or _PACKET_CAPTURE_AT_IMPORT == "0"
 
 __version__ = "0.1.0"
 

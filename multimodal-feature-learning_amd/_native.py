@@ -77,7 +77,7 @@ def _declare(lib):
     lib.flat_adamw_workspace_bytes.restype = ctypes.c_size_t
     lib.flat_adamw_workspace_bytes.argtypes = []
     lib.flat_adamw_step.restype = i32
-    lib.flat_adamw_step.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, f32, f32, f32, f32, f32, f32, vp]
+    lib.flat_adamw_step.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, f32, f32, f32, f32, f32, f32, vp, vp]
     lib.mfl_colsum_workspace_bytes.restype = ctypes.c_size_t
     lib.mfl_colsum_workspace_bytes.argtypes = [i64, i64]
     lib.mfl_colsum.restype = i32

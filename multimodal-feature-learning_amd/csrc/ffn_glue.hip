@@ -39,6 +39,7 @@ __device__ __forceinline__ uint64_t drop_bits4(uint64_t seed, uint64_t quad) {
   return x;
 }
 
+__device__ __forceinline__ float relu_nan(float x) { return x > 0.f ? x : (x != x ? x : 0.f); }
 __device__ __forceinline__ float lo(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi(uint32_t w) { return __uint_as_float(w & 0xffff0000u); }
 
@@ -57,11 +58,13 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_fwd(const uint4* __rest
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      float a = fmaxf(lo(w[j]), 0.f), b = fmaxf(hi(w[j]), 0.f);
+      // relu as ATen's: NaN stays NaN (fmaxf would turn it into 0 and hide a diverging FFN)
+      float a = relu_nan(lo(w[j])), b = relu_nan(hi(w[j]));
       if (seed_ptr) {  // elements 2j, 2j+1 of the vector: 16-bit draws (2j % 4), (2j % 4) + 1 of bits[j / 2]
         const uint64_t q = bits[j >> 1] >> (32 * (j & 1));
-        a = (uint32_t)(q & 0xffffu) >= thresh ? a * scale : 0.f;
-        b = (uint32_t)((q >> 16) & 0xffffu) >= thresh ? b * scale : 0.f;
+        // dropped: x * 0 as ATen's x * mask (a NaN stays NaN)
+        a *= (uint32_t)(q & 0xffffu) >= thresh ? scale : 0.f;
+        b *= (uint32_t)((q >> 16) & 0xffffu) >= thresh ? scale : 0.f;
       }
       o[j] = rne(a) | (rne(b) << 16);
     }
@@ -77,8 +80,9 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_bwd(const uint4* __rest
     uint32_t o[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const float a = lo(yw[j]) > 0.f ? lo(gw[j]) * scale : 0.f;
-      const float b = hi(yw[j]) > 0.f ? hi(gw[j]) * scale : 0.f;
+      // ATen's threshold_backward: zero where out <= 0 (a NaN output passes its gradient)
+      const float a = !(lo(yw[j]) <= 0.f) ? lo(gw[j]) * scale : 0.f;
+      const float b = !(hi(yw[j]) <= 0.f) ? hi(gw[j]) * scale : 0.f;
       o[j] = rne(a) | (rne(b) << 16);
     }
     dx[i] = make_uint4(o[0], o[1], o[2], o[3]);

@@ -35,7 +35,8 @@ struct State {  // device-resident, FLAT_ADAMW_STATE_BYTES
   double step;      // step count after this update
   double step_size; // lr / bc1
   double bc2_sqrt;  // sqrt(1 - b2^step)
-  double pad[3];
+  double decay;     // 1 - lr * weight_decay
+  double pad[2];
 };
 
 __global__ __launch_bounds__(kThreads) void flat_sq_partials(const float* __restrict__ g, long long n,
@@ -66,7 +67,8 @@ __global__ __launch_bounds__(kThreads) void flat_sq_partials(const float* __rest
 
 __global__ __launch_bounds__(kThreads) void flat_adamw_prepare(const double* __restrict__ partials, int nparts,
                                                               State* __restrict__ st, float* __restrict__ step_io,
-                                                              double max_norm, double beta1, double beta2, double lr) {
+                                                              double max_norm, double beta1, double beta2, double lr,
+                                                              double wd, const float* __restrict__ lr_wd) {
   double d = 0;
   for (int i = threadIdx.x; i < nparts; i += kThreads) d += partials[i];
   for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
@@ -84,8 +86,13 @@ __global__ __launch_bounds__(kThreads) void flat_adamw_prepare(const double* __r
     const double step = (double)step_io[0] + 1.0;
     step_io[0] = (float)step;
     st->step = step;
-    st->step_size = lr / (1.0 - pow(beta1, step));
+    // lr / weight_decay from device memory when given: a graph replays the values of the step,
+    // not those of the capture (a StepLR schedule changes them between replays)
+    const float lr_f = lr_wd != nullptr ? lr_wd[0] : (float)lr;
+    const float wd_f = lr_wd != nullptr ? lr_wd[1] : (float)wd;
+    st->step_size = (double)lr_f / (1.0 - pow(beta1, step));
     st->bc2_sqrt = sqrt(1.0 - pow(beta2, step));
+    st->decay = (double)(1.f - lr_f * wd_f);  // fp32 as torch's p.mul_(1 - lr * wd)
   }
 }
 
@@ -109,12 +116,12 @@ __device__ __forceinline__ uint16_t to_bf16(float x) {
 __global__ __launch_bounds__(kThreads) void flat_adamw_update(float* __restrict__ p, const float* __restrict__ g,
                                                              float* __restrict__ m, float* __restrict__ v,
                                                              uint16_t* __restrict__ shadow, long long n,
-                                                             const State* __restrict__ st, float lr, float wd,
-                                                             float b1, float b2, float eps) {
+                                                             const State* __restrict__ st, float b1, float b2,
+                                                             float eps) {
   const float c = (float)st->coef;
   const float step_size = (float)st->step_size;
   const float bc2 = (float)st->bc2_sqrt;
-  const float decay = 1.f - lr * wd;
+  const float decay = (float)st->decay;
   const long long n4 = n / 4;
   for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n4; i += (long long)gridDim.x * kThreads) {
     float4 pp = reinterpret_cast<float4*>(p)[i];
@@ -256,7 +263,7 @@ size_t flat_adamw_workspace_bytes(void) { return sizeof(State) + kPartials * siz
 
 int flat_adamw_step(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, uint16_t* bf16_shadow,
                     int64_t n, float* step, void* workspace, float lr, float beta1, float beta2, float eps,
-                    float weight_decay, float max_norm, void* stream) {
+                    float weight_decay, float max_norm, const float* lr_wd, void* stream) {
   g_err[0] = 0;
   if (n < 0 || (n > 0 && (params == nullptr || grads == nullptr || exp_avg == nullptr || exp_avg_sq == nullptr)) ||
       step == nullptr || workspace == nullptr) {
@@ -281,11 +288,11 @@ int flat_adamw_step(float* params, const float* grads, float* exp_avg, float* ex
   hipLaunchKernelGGL(flat_sq_partials, dim3(nparts), dim3(kThreads), 0, st, grads, (long long)n, partials);
   if ((rc = status("norm"))) return rc;
   hipLaunchKernelGGL(flat_adamw_prepare, dim3(1), dim3(kThreads), 0, st, partials, nparts, state, step,
-                     (double)max_norm, (double)beta1, (double)beta2, (double)lr);
+                     (double)max_norm, (double)beta1, (double)beta2, (double)lr, (double)weight_decay, lr_wd);
   if ((rc = status("prepare"))) return rc;
   const unsigned blocks = (unsigned)std::min<long long>(8192, std::max<long long>(1, (n4 + kThreads - 1) / kThreads));
   hipLaunchKernelGGL(flat_adamw_update, dim3(blocks), dim3(kThreads), 0, st, params, grads, exp_avg, exp_avg_sq,
-                     bf16_shadow, (long long)n, state, lr, weight_decay, beta1, beta2, eps);
+                     bf16_shadow, (long long)n, state, beta1, beta2, eps);
   return status("update");
 }
 

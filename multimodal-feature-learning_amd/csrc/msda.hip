@@ -1195,13 +1195,24 @@ struct PairLayout {
 
 constexpr int kPairParts = 4;  // partial rows per wave (striped mode)
 
-template <typename scalar_t, int NSLOT, bool ZEROS, bool STG, int U>
+// The loads of one pull batch of a slot: UB gathered grad_out fragments and their entries'
+// (c0, c1) (STG) or loc / aw (!STG).
+template <int UB>
+struct PairBatch {
+  uint4 g[UB];
+  f32x2 cc[UB];
+  float lc[UB], ac[UB];
+};
+
+// STG: 1 = (c0, c1) and sample positions staged in LDS; 2 = staged in a global workspace slice
+// of the workgroup (when they do not fit LDS beside the keys); 0 = keys only.
+template <typename scalar_t, int NSLOT, bool ZEROS, int STG, int U>
 __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
     const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, float* __restrict__ gloc,
     float* __restrict__ gaw, const Levels lv, const int L, const int P, const int S, const int M,
     const int D, const int Lq, const int RS, const unsigned striped_mask, const int sort_rows,
-    const PairLayout lay) {
+    const PairLayout lay, unsigned char* __restrict__ gstage) {
   static_assert(NSLOT > 0, "pair backward needs whole 16-byte chunks per lane");
   constexpr int CPL = 16 / (int)sizeof(scalar_t);
   constexpr int H = CPL / 2;
@@ -1219,10 +1230,21 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
   const int T = lv.T[l];
   const int NL = T + 1;  // lists by base row r = -1 .. T-1 at list index r + 1
   const int nsamp = Lq * P;
-  const bool striped = STG && ((striped_mask >> l) & 1u) != 0u;
+  const bool striped = STG == 1 && ((striped_mask >> l) & 1u) != 0u;
   unsigned* ekey = reinterpret_cast<unsigned*>(smem_raw);
-  f32x2* ecc = reinterpret_cast<f32x2*>(smem_raw + lay.off_cc);  // (c0, c1), then (d0, d1)
-  int* pos_of = reinterpret_cast<int*>(smem_raw + lay.off_pos);   // STG: a sample's list position
+  // STG == 2: this workgroup's slice of the workspace, [(c0, c1) x Lq*P | position x Lq*P]
+  unsigned char* gsl = STG == 2 ? gstage + (size_t)blk * ((size_t)Lq * P * 12) : nullptr;
+  f32x2* ecc = STG == 2 ? reinterpret_cast<f32x2*>(gsl)
+                        : reinterpret_cast<f32x2*>(smem_raw + lay.off_cc);  // (c0, c1), then (d0, d1)
+  int* pos_of = STG == 2 ? reinterpret_cast<int*>(gsl + (size_t)Lq * P * 8)
+                         : reinterpret_cast<int*>(smem_raw + lay.off_pos);  // a sample's list position
+  // STG == 2: global stores of other waves become visible to this CU's loads only after they
+  // completed (a barrier does not wait for them) and L1 holds no stale copy (agent acquire)
+  auto gstage_sync = [&]() {
+    if constexpr (STG == 2) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if constexpr (STG == 2) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  };
   float* xb = reinterpret_cast<float*>(smem_raw + lay.off_xb);    // hand-overs / wave partials
   int* cur = reinterpret_cast<int*>(smem_raw + lay.off_cur);
   int* pb = reinterpret_cast<int*>(smem_raw + lay.off_pb);
@@ -1336,7 +1358,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
     const int q = s / P, p = s - q * P;
     place(s, locb[q * qs + p]);
   }
-  __syncthreads();
+  gstage_sync();
   if (sort_rows) {  // deterministic mode: every list in key order (insertion sort)
     for (int i = clo; i < chi; ++i) {
       const int e1 = cur[i], e0 = (i == 0 ? 0 : cur[i - 1]);
@@ -1354,13 +1376,13 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
         if constexpr (STG) ecc[y + 1] = kc;
       }
     }
-    __syncthreads();
+    gstage_sync();
     if (STG)  // the sorted positions
       for (int e = (int)threadIdx.x; e < N; e += kGvThreads) {
         const unsigned key = ekey[e];
         pos_of[(int)(key >> 8) * P + (int)(key & 0xffu)] = e;
       }
-    __syncthreads();
+    gstage_sync();
   }
   MSDA_PH(2);
 
@@ -1395,7 +1417,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
   // row mode (sparse levels: decoder-like calls, a few samples a row): every slot builds whole
   // rows r from the entries of lists r-1 (c1) and r (c0) — each entry gathered by both of its rows,
   // but rows need no hand-over and every slot runs independently
-  const bool rowmode = STG && (long long)N <= 4LL * NL;
+  const bool rowmode = STG == 1 && (long long)N <= 4LL * NL;
   if (!striped && !rowmode && (int)threadIdx.x <= W) {
     const int j = threadIdx.x;
     pb[j] = j == 0 ? pre : (j == W ? whi : snap_e(wlo + (long long)(whi - wlo) * j / W));
@@ -1442,46 +1464,49 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
 #pragma unroll
   for (int e = 0; e < H; ++e) a0[e] = a1[e] = f32x2{0.f, 0.f};
   uint4 v0, v1;
-  // one batch: the slot's entries ebase + u * STR below lim, all of list rb (rows rb, rb + 1)
-  auto batch = [&](int ebase, int STR, int lim) {
-    uint4 g[U];
-    f32x2 cc[U];
-    float lcv[U], acv[U];
+  // one batch: the slot's entries ebase + u * STR below lim, all of list rb (rows rb, rb + 1);
+  // issue() starts its loads, consume() adds it into a0 / a1 and writes its dots
+  auto issue = [&](auto& bt, int ebase, int STR, int lim) {
+    constexpr int UB = sizeof(bt.g) / sizeof(bt.g[0]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < UB; ++u) {
       const int e = ebase + u * STR;
       const bool have = e < lim;
       const unsigned key = ekey[have ? e : 0];
-      g[u] = *reinterpret_cast<const uint4*>(gb + (__umul24(key >> 8, (unsigned)rs) + co));
+      bt.g[u] = *reinterpret_cast<const uint4*>(gb + (__umul24(key >> 8, (unsigned)rs) + co));
       if constexpr (STG) {
-        cc[u] = ecc[have ? e : 0];
-        if (!have) cc[u] = f32x2{0.f, 0.f};
+        bt.cc[u] = ecc[have ? e : 0];
+        if (!have) bt.cc[u] = f32x2{0.f, 0.f};
       } else {
         const long long o = (long long)(key >> 8) * qs + (key & 0xffu);
-        lcv[u] = locb[o];
-        acv[u] = have ? awb[o] : 0.f;
+        bt.lc[u] = locb[o];
+        bt.ac[u] = have ? awb[o] : 0.f;
       }
     }
+  };
+  auto consume = [&](auto& bt, int ebase, int STR, int lim) {
+    constexpr int UB = sizeof(bt.g) / sizeof(bt.g[0]);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 0; u < UB; ++u) {
       const int e = ebase + u * STR;
       const bool have = e < lim;
       Taps<float> t{};
+      f32x2 cu = bt.cc[u];
       if constexpr (!STG) {
-        t = make_taps<float, ZEROS>(lcv[u], T);
-        cc[u] = f32x2{t.ok0 ? acv[u] * t.w0 : 0.f, t.ok1 ? acv[u] * t.w1 : 0.f};
+        t = make_taps<float, ZEROS>(bt.lc[u], T);
+        cu = f32x2{t.ok0 ? bt.ac[u] * t.w0 : 0.f, t.ok1 ? bt.ac[u] * t.w1 : 0.f};
       }
       f32x2 x[H];
-      cvt16x2<scalar_t, CPL>(g[u], x);
-      const f32x2 k0{cc[u].x, cc[u].x}, k1{cc[u].y, cc[u].y};
+      cvt16x2<scalar_t, CPL>(bt.g[u], x);
+      const f32x2 k0{cu.x, cu.x}, k1{cu.y, cu.y};
 #pragma unroll
       for (int e2 = 0; e2 < H; ++e2) {
         a0[e2] = pk_fma(x[e2], k0, a0[e2]);
         a1[e2] = pk_fma(x[e2], k1, a1[e2]);
       }
       if (coords) {
-        const float d0 = group_sum<LPR>(dot16<scalar_t>(g[u], v0));
-        const float d1 = group_sum<LPR>(dot16<scalar_t>(g[u], v1));
+        const float d0 = group_sum<LPR>(dot16<scalar_t>(bt.g[u], v0));
+        const float d1 = group_sum<LPR>(dot16<scalar_t>(bt.g[u], v1));
         if (have && c_l == 0) {
           if constexpr (STG) {
             ecc[e] = f32x2{d0, d1};
@@ -1489,11 +1514,16 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
             const unsigned key = ekey[e];
             const long long o = (long long)(key >> 8) * qs + (key & 0xffu);
             if (gab != nullptr) gab[o] = d0 * t.w0 + d1 * t.w1;
-            if (glb != nullptr) glb[o] = ((d1 - d0) * acv[u]) * t.gmul;
+            if (glb != nullptr) glb[o] = ((d1 - d0) * bt.ac[u]) * t.gmul;
           }
         }
       }
     }
+  };
+  auto batch = [&](int ebase, int STR, int lim) {
+    PairBatch<U> bt;
+    issue(bt, ebase, STR, lim);
+    consume(bt, ebase, STR, lim);
   };
 
   if (rowmode) {
@@ -1556,6 +1586,8 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
         store_row(x, a);
       }
     };
+    // (a software-pipelined variant — next batch's loads issued before this one is consumed, row
+    // stores after them — measured slower: pull 42 vs 37 us at the encoder shape, U = 4 + 4)
     int eo = lo < hi ? en(rb) : 0;  // end of list rb
     v0 = vload(rb);
     v1 = vload(rb + 1);
@@ -1750,7 +1782,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
   // sample of this workgroup's window finds its list position parked in its output slot
   if constexpr (STG) {
     if (coords) {
-      __syncthreads();  // every dot written
+      gstage_sync();  // every dot written
       MSDA_PH(5);
       const int li_lo = wlo < whi ? row_of(wlo) + 1 : 1, li_hi = wlo < whi ? row_of(whi - 1) + 1 : 0;
       for (int s0 = threadIdx.x; s0 < nsamp; s0 += kGvThreads * kGvCache) {
@@ -2445,8 +2477,18 @@ struct PairPlan {
   PairLayout lay;
   size_t lds;
   unsigned striped_mask;
-  bool stg;
+  int stg;          // staging of the entries' (c0, c1) / positions: 1 LDS, 2 workspace, 0 none
+  int rs;           // workgroups per (b, m, level)
+  size_t ws_bytes;  // workspace of stg 2
 };
+
+// workgroups per (b, m, level): enough to fill the chip's 256 CUs (MSDA_HIP_PAIR_RS overrides;
+// read per call so tests can switch it)
+int pair_rs(long long wgs) {
+  const int rs = env_int("MSDA_HIP_PAIR_RS", 0);
+  if (rs > 0) return rs;
+  return wgs >= 256 ? 1 : (int)std::min<long long>(8, (256 + std::max<long long>(wgs, 1) - 1) / std::max<long long>(wgs, 1));
+}
 
 size_t a16(size_t x) { return (x + 15) & ~(size_t)15; }
 
@@ -2482,8 +2524,10 @@ int pair_slots(int value_dtype, long long D) {
 // Striped levels: fewer lists than twice the slots (T + 1 < 2 W), at least 4 slots a wave (the partial-row
 // merge uses one slot per partial), STG only.  MSDA_HIP_STRIPED_ROWS caps T (A/B builds; read per
 // call so tests can switch it).
-bool pair_plan(int value_dtype, long long Lq, long long P, long long D, long long L, const int* T,
-               long long S, PairPlan* pp) {
+// stg 2 (workspace staging) only when allow_ws: the query's bound sets it, and a launch with a
+// workspace (the query asked for one) may take it.
+bool pair_plan(int value_dtype, long long B, long long M, long long Lq, long long P, long long D, long long L,
+               const int* T, long long S, bool allow_ws, PairPlan* pp) {
   if (bwd_env_path() != 0) return false;
   const int ns = pair_slots(value_dtype, D);
   if (ns == 0 || P > 256 || Lq >= (1LL << 24) || Lq * P >= (1LL << 30)) return false;
@@ -2500,14 +2544,17 @@ bool pair_plan(int value_dtype, long long Lq, long long P, long long D, long lon
       if (ns >= 4 && T[l] + 1 < 2 * W && T[l] <= striped_rows) mask |= 1u << l;
     }
   }
-  for (int stg = 1; stg >= 0; --stg) {
+  pp->rs = pair_rs(B * M * L);
+  for (int stg : {1, 2}) {  // (stg 0 — keys only, coordinates from the pull — is not launched)
+    if (stg == 2 && !allow_ws) continue;
     PairLayout lay;
-    const size_t lds = pair_layout(N, D, ns, maxT, stg != 0, stg != 0 && mask != 0, &lay);
+    const size_t lds = pair_layout(N, D, ns, maxT, stg == 1, stg == 1 && mask != 0, &lay);
     if (lds <= kPairLdsMax) {
       pp->lay = lay;
       pp->lds = lds;
-      pp->striped_mask = stg ? mask : 0u;
-      pp->stg = stg != 0;
+      pp->striped_mask = stg == 1 ? mask : 0u;
+      pp->stg = stg;
+      pp->ws_bytes = stg == 2 ? (size_t)(B * M * L * pp->rs) * (size_t)N * 12 : 0;
       return true;
     }
   }
@@ -2516,15 +2563,14 @@ bool pair_plan(int value_dtype, long long Lq, long long P, long long D, long lon
 
 template <typename scalar_t>
 int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, const void* loc,
-                      const void* aw, const void* gout, void* gval, void* gloc, void* gaw, int pad,
-                      hipStream_t st) {
+                      const void* aw, const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
+                      int pad, hipStream_t st) {
   static const int det = env_int("MSDA_HIP_DETERMINISTIC", 0);
   const int ns = pair_slots(std::is_same<scalar_t, float>::value ? MSDA_DTYPE_F32 : MSDA_DTYPE_BF16, pr.D);
   const long long wgs = pr.B * pr.M * pr.L;
-  // workgroups per (b, m, level): enough to fill the chip's 256 CUs (MSDA_HIP_PAIR_RS overrides)
-  int rs = env_int("MSDA_HIP_PAIR_RS", 0);
-  if (rs <= 0) rs = wgs >= 256 ? 1 : (int)std::min<long long>(8, (256 + wgs - 1) / wgs);
+  const int rs = pp.rs;
   const unsigned blocks = (unsigned)(wgs * rs);
+  auto* gsg = static_cast<unsigned char*>(workspace);
   const bool z = pad == MSDA_PAD_ZEROS;
   auto* v = static_cast<const scalar_t*>(value);
   auto* lc = static_cast<const float*>(loc);
@@ -2540,15 +2586,15 @@ int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, 
     hipLaunchKernelGGL((msda_bwd_pair_kernel<scalar_t, NSL, Z, STGV, UU>), dim3(blocks),         \
                        dim3(kGvThreads), pp.lds, st, v, lc, a, g, gv, gl, ga, pr.lv, (int)pr.L,   \
                        (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq, rs, pp.striped_mask, \
-                       det, pp.lay);                                                            \
+                       det, pp.lay, gsg);                                                       \
   } while (0)
 #ifndef MSDA_PAIR_U
 #define MSDA_PAIR_U 8  // gathers in flight per slot
 #endif
 #define MSDA_PA(NSL, Z)                                                                           \
   do {                                                                                          \
-    if (!pp.stg) MSDA_PA_(NSL, Z, false, MSDA_PAIR_U);                                          \
-    else MSDA_PA_(NSL, Z, true, MSDA_PAIR_U);                                                   \
+    if (pp.stg == 1) MSDA_PA_(NSL, Z, 1, MSDA_PAIR_U);                                          \
+    else MSDA_PA_(NSL, Z, 2, MSDA_PAIR_U);                                                      \
   } while (0)
 #define MSDA_PA_NS(Z)                                                                             \
   switch (ns) {                                                                                 \
@@ -2570,15 +2616,16 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
                  int value_dtype, int pad, hipStream_t st) {
   if constexpr (std::is_same<coord_t, float>::value) {
     const int ns = pr.B * pr.M * pr.S > 0 ? fused_bwd_rows<scalar_t, coord_t>(pr, value_dtype, gval) : 0;
-    // sparse calls (every level at most 4 samples a row: decoder-like) stay on the per-tap fused
-    // kernel: few taps a row, so the pair kernel's halved gathers do not pay for its list walk
+    // sparse or tiny calls (every level at most 4 samples a row: decoder-like; or at most 512
+    // samples a level: the audio self / decoder calls of configs[2]) stay on the per-tap fused
+    // kernel: its shorter phase chain wins where the pair kernel's halved gathers are few
     int minT = 1 << 30;
     for (int l = 0; l < pr.L; ++l) minT = min(minT, pr.lv.T[l]);
-    const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1);
+    const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1) || pr.Lq * pr.P <= 512;
     PairPlan pp;
     if (gval != nullptr && pr.B * pr.M * pr.S > 0 && !(sparse && ns > 0) &&
-        pair_plan(value_dtype, pr.Lq, pr.P, pr.D, pr.L, pr.lv.T, pr.S, &pp))
-      return run_backward_pair<scalar_t>(pr, pp, value, loc, aw, gout, gval, gloc, gaw, pad, st);
+        pair_plan(value_dtype, pr.B, pr.M, pr.Lq, pr.P, pr.D, pr.L, pr.lv.T, pr.S, workspace != nullptr, &pp))
+      return run_backward_pair<scalar_t>(pr, pp, value, loc, aw, gout, gval, gloc, gaw, workspace, pad, st);
     if (ns > 0)
       return run_backward_fused<scalar_t>(pr, ns, value, loc, aw, gout, gval, gloc, gaw, pad, st);
   }
@@ -3192,9 +3239,9 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
   (void)channels;
   if (batch <= 0 || spatial_size <= 0 || num_heads <= 0) return 0;
   PairPlan pp;
-  if (value_dtype != MSDA_DTYPE_F64 &&
-      pair_plan(value_dtype, num_query, num_point, channels, num_levels, nullptr, spatial_size, &pp))
-    return 0;
+  if (value_dtype != MSDA_DTYPE_F64 && pair_plan(value_dtype, batch, num_heads, num_query, num_point, channels,
+                                                  num_levels, nullptr, spatial_size, true, &pp))
+    return pp.ws_bytes;
   if (use_fused_gvalue(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point))
     return 0;
   return bwd_layout(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point).total;

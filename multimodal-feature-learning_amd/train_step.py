@@ -19,9 +19,14 @@ the MI355X the way the hardware wants it:
   and replayed — the ~1500 kernels of a step are launched by two ``hipGraphLaunch`` calls
   instead of ~1500 Python-driven launches (the eager step is launch-bound: its GPU is idle
   for about a quarter of the step, profiles/);
-* between the two graphs the flat buffer is all-reduced with ONE RCCL call over xGMI
-  (a single large collective instead of DDP's 25 MB buckets; 7 point-to-point xGMI links
-  per GPU favour few large transfers).  The all-reduce is the only data-path collective:
+* with several ranks the flat gradient is all-reduced in a few large buckets (contiguous ranges
+  of the flat buffer in reverse parameter order, ``bucket_mb`` each: 7 point-to-point xGMI
+  links per GPU favour few large transfers over DDP's 25 MB) overlapped with the backward: a
+  parameter's post-accumulate-grad hook hands its gradient to the bucket, and a bucket whose
+  gradients are all final is copied into the flat buffer and all-reduced on a side stream while
+  autograd computes the earlier layers (the reference's DDP overlap, main.py:85).  Under graphs
+  the bucket collectives are captured with the backward (``capture_collectives``; otherwise one
+  all-reduce runs between the two graphs).  The all-reduce is the only data-path collective:
   every MSDA call reads only its own clip, so the path shards by clip.
 
 ``graph=False`` runs the same three phases eagerly (CPU tests, world_size-2 gloo).
@@ -37,7 +42,7 @@ __all__ = ["FlatGradTrainer"]
 class FlatGradTrainer:
     def __init__(self, model, loss_fn, lr=1e-4, weight_decay=1e-4, max_norm=0.1, use_bf16=True, graph=True,
                  process_group=None, fused_optimizer=None, betas=(0.9, 0.999), eps=1e-8, handover=True,
-                 shadow=True):
+                 shadow=True, bucket_mb=32.0, overlap=True, capture_collectives=None):
         self.model = model
         self.loss_fn = loss_fn
         self.max_norm = max_norm
@@ -77,8 +82,12 @@ class FlatGradTrainer:
                         continue
                     self._linears.append((mod, index[id(mod.weight)], b))
             self._refresh_shadow()
-        self.lr, self.weight_decay, self.betas, self.eps = lr, weight_decay, betas, eps
+        self.betas, self.eps = betas, eps
         self.fused = (dev.type == "cuda") if fused_optimizer is None else bool(fused_optimizer)
+        # lr / weight_decay live in device memory read by the update kernels, so a replayed graph
+        # uses the current values (setting trainer.lr between replays is a schedule step)
+        self._lr_wd = torch.tensor([lr, weight_decay], dtype=torch.float32, device=dev)
+        self._lr, self._wd = float(lr), float(weight_decay)
         if self.fused:
             from . import _native
             self._lib = _native.load_library()
@@ -88,11 +97,112 @@ class FlatGradTrainer:
             self._opt_ws = torch.empty(self._lib.flat_adamw_workspace_bytes(), dtype=torch.uint8, device=dev)
             self.opt = None
         else:
-            self.opt = torch.optim.AdamW(self.params, lr=lr, betas=betas, eps=eps, weight_decay=weight_decay,
+            # a tensor lr under graphs: the captured step reads it (schedules fill it in place)
+            lr0 = torch.tensor(float(lr), device=dev) if graph else lr
+            self.opt = torch.optim.AdamW(self.params, lr=lr0, betas=betas, eps=eps, weight_decay=weight_decay,
                                          capturable=graph, foreach=True)
         self._g_fb = None
         self._g_up = None
         self._loss = None
+        # gradient buckets: contiguous flat ranges, reverse parameter order (the backward's order)
+        self.buckets = self._make_buckets(int(bucket_mb * 2 ** 20 / 4))
+        # overlap="force": the bucket collectives also at world size 1 (a one-rank RCCL smoke)
+        self.overlap = handover and (overlap == "force" or (bool(overlap) and self.world > 1))
+        backend = dist.get_backend(process_group) if self.world > 1 else None
+        self.capture_collectives = (backend == "nccl") if capture_collectives is None else bool(capture_collectives)
+        self._comm_stream = None
+        self._pending = None
+        self._overlap_now = self.overlap  # eager steps; capture() decides for the graph
+        self._fb_reduces = False          # the captured fwd+bwd graph all-reduces the buckets
+        self._bucket_of = {}
+        for bi, (_, _, idx) in enumerate(self.buckets):
+            for i in idx:
+                self._bucket_of[i] = bi
+        if self.overlap:
+            for i, p in enumerate(self.params):
+                p.register_post_accumulate_grad_hook(self._make_hook(i))
+
+    # --- gradient buckets ----------------------------------------------------------------
+    def _make_buckets(self, cap_elems):
+        """[(start, end, [param index, ...]), ...]: consecutive parameters from the last one
+        backwards, each bucket a contiguous range of the flat buffer of at most cap_elems elements
+        (or one parameter larger than that)."""
+        offs, off = [], 0
+        for p in self.params:
+            offs.append(off)
+            off += p.numel()
+        buckets, cur, cur_n = [], [], 0
+        for i in reversed(range(len(self.params))):
+            n = self.params[i].numel()
+            if cur and cur_n + n > cap_elems:
+                buckets.append(cur)
+                cur, cur_n = [], 0
+            cur.append(i)
+            cur_n += n
+        if cur:
+            buckets.append(cur)
+        out = []
+        for idx in buckets:
+            lo, hi = min(idx), max(idx)
+            out.append((offs[lo], offs[hi] + self.params[hi].numel(), sorted(idx)))
+        return out
+
+    def _make_hook(self, i):
+        def hook(p):
+            if self._pending is None:  # backward outside _forward_backward (user code): nothing to do
+                return
+            b = self._bucket_of[i]
+            self._pending[b] -= 1
+            if self._pending[b] == 0:
+                self._flush_bucket(b)
+        return hook
+
+    def _flush_bucket(self, b):
+        start, end, idx = self.buckets[b]
+        got = [(self.grad_views[i], self.params[i].grad) for i in idx if self.params[i].grad is not None]
+        missing = [self.grad_views[i] for i in idx if self.params[i].grad is None]
+        if got:
+            torch._foreach_copy_([v for v, _ in got], [g for _, g in got])
+        if missing:
+            torch._foreach_zero_(missing)
+        self._done[b] = True
+        if self._overlap_now:
+            cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+            if cur is not None:
+                if self._comm_stream is None:
+                    self._comm_stream = torch.cuda.Stream(self.device)
+                self._comm_stream.wait_stream(cur)
+                with torch.cuda.stream(self._comm_stream):
+                    dist.all_reduce(self.flat_grad[start:end], group=self.pg)
+            else:
+                self._works.append(dist.all_reduce(self.flat_grad[start:end], group=self.pg, async_op=True))
+
+    @property
+    def lr(self):
+        return self._lr
+
+    @lr.setter
+    def lr(self, value):
+        self._lr = float(value)
+        self._lr_wd[0] = self._lr  # in place: the captured update graph reads it
+        if self.opt is not None:
+            for group in self.opt.param_groups:
+                if torch.is_tensor(group["lr"]):
+                    group["lr"].fill_(self._lr)
+                else:
+                    group["lr"] = self._lr
+
+    @property
+    def weight_decay(self):
+        return self._wd
+
+    @weight_decay.setter
+    def weight_decay(self, value):
+        self._wd = float(value)
+        self._lr_wd[1] = self._wd
+        if self.opt is not None:
+            for group in self.opt.param_groups:
+                group["weight_decay"] = self._wd
 
     # --- the three phases ------------------------------------------------------------
     def _views(self, flat):
@@ -131,18 +241,28 @@ class FlatGradTrainer:
                             cache_enabled=cache_casts):
             out = self.model(*batch)
             loss = self.loss_fn(out)
-        loss.backward()
-        got = [(v, p.grad) for p, v in zip(self.params, self.grad_views) if p.grad is not None]
-        missing = [v for p, v in zip(self.params, self.grad_views) if p.grad is None]
-        if got:
-            torch._foreach_copy_([v for v, _ in got], [g for _, g in got])
-        if missing:
-            torch._foreach_zero_(missing)
+        self._pending = [len(idx) for _, _, idx in self.buckets]
+        self._done = [False] * len(self.buckets)
+        self._works = []
+        try:
+            loss.backward()  # overlap: full buckets are copied and all-reduced from the hooks
+        finally:
+            pending, self._pending = self._pending, None
+        for b in range(len(self.buckets)):  # buckets with parameters that got no gradient
+            if not self._done[b]:
+                self._flush_bucket(b)
+        if self._overlap_now:
+            if self._comm_stream is not None:
+                torch.cuda.current_stream(self.device).wait_stream(self._comm_stream)
+            for w in self._works:
+                w.wait()
+            self._works = []
+            self.flat_grad.div_(self.world)
         self._attach_grads()
         return loss.detach()
 
     def _allreduce(self):
-        if self.world > 1:
+        if self.world > 1 and not self._overlap_now:
             dist.all_reduce(self.flat_grad, group=self.pg)  # SUM: gloo has no AVG
             self.flat_grad.div_(self.world)
 
@@ -156,8 +276,8 @@ class FlatGradTrainer:
         shadow = self.flat_bf16.data_ptr() if self.flat_bf16 is not None else None
         rc = self._lib.flat_adamw_step(
             self.flat_param.data_ptr(), self.flat_grad.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
-            shadow, self.flat_param.numel(), self.opt_step.data_ptr(), self._opt_ws.data_ptr(), self.lr,
-            self.betas[0], self.betas[1], self.eps, self.weight_decay, self.max_norm,
+            shadow, self.flat_param.numel(), self.opt_step.data_ptr(), self._opt_ws.data_ptr(), self._lr,
+            self.betas[0], self.betas[1], self.eps, self._wd, self.max_norm, self._lr_wd.data_ptr(),
             _native.stream_handle(self.device))
         if rc != 0:
             raise RuntimeError("flat_adamw_step failed: " + self._lib.flat_adamw_last_error().decode())
@@ -176,6 +296,14 @@ class FlatGradTrainer:
         ``batch`` tensors are the graph's static inputs: refill them in place to change data."""
         if not self.graph:
             return
+        import importlib
+        pkg = importlib.import_module(__name__.rsplit(".", 1)[0])
+        if not pkg.graph_packet_capture_off():
+            raise RuntimeError(
+                "FlatGradTrainer.capture: the HIP runtime's graph packet capture is on "
+                "(DEBUG_CLR_GRAPH_PACKET_CAPTURE must be '0' before HIP initialises: import the package "
+                "before any device call, or export the variable); with it on, replays after allocating "
+                "eager work produced corrupted gradients (DESIGN.md §6)")
         side = torch.cuda.Stream(self.device)
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
@@ -184,8 +312,12 @@ class FlatGradTrainer:
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
         self._g_fb = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_fb):
-            self._loss = self._forward_backward(batch, cache_casts=False)
+        self._overlap_now = self.overlap and self.capture_collectives
+        try:
+            with torch.cuda.graph(self._g_fb):
+                self._loss = self._forward_backward(batch, cache_casts=False)
+        finally:
+            self._fb_reduces, self._overlap_now = self._overlap_now, self.overlap
         self._g_up = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_up, pool=self._g_fb.pool()):
             self._update()
@@ -199,6 +331,9 @@ class FlatGradTrainer:
         if self._g_fb is None:
             raise RuntimeError("FlatGradTrainer.capture(batch) must run before step()")
         self._g_fb.replay()
-        self._allreduce()
+        if not self._fb_reduces:
+            self._overlap_now = False
+            self._allreduce()  # one all-reduce between the two graphs
+            self._overlap_now = self.overlap
         self._g_up.replay()
         return self._loss

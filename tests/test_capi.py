@@ -35,11 +35,12 @@ def test_abi_version_and_workspace():
     lib = PKG._native.load_library()
     assert lib.msda_hip_abi_version() == PKG._native.ABI_VERSION
     B, S, M, D, Lq, L, P = 2, 1920, 8, 64, 1920, 4, 4
-    # pair-pull backward (16-byte chunks per lane, lists in LDS, any batch size): no workspace,
-    # also at T = 4096 (S = 7680: keys only in LDS)
+    # pair-pull backward (16-byte chunks per lane, lists in LDS, any batch size): no workspace;
+    # at T = 4096 (S = 7680) the keys alone fill LDS and each (b, m, level) workgroup stages its
+    # entries' (c0, c1) and positions (12 B a sample) in the workspace
     for dt in (0, 2, 3):
         assert lib.msda_hip_backward_workspace_bytes(dt, B, S, M, D, Lq, L, P) == 0
-    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) == 0
+    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * 4 * Lq * P * 12
     # split path (sort + pull): fp64, or heads not made of 16-byte chunks with few workgroups —
     # row table + per-row tap lists
     f64 = lib.msda_hip_backward_workspace_bytes(1, B, S, M, D, Lq, L, P)

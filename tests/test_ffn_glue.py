@@ -67,3 +67,17 @@ def test_fresh_mask_per_call(dev):
     a = FF.relu_dropout(h, F.relu, drop)
     b = FF.relu_dropout(h, F.relu, drop)
     assert (a != b).float().mean().item() > 0.1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("train", [False, True])
+def test_nan_propagates_as_aten(dev, train):
+    """ATen's relu keeps NaN (and x * mask keeps it through dropout): a diverging FFN shows up as
+    NaN instead of being zeroed by the fused kernel."""
+    drop = torch.nn.Dropout(0.5).train(train)
+    h = torch.randn(4096, device=dev)
+    h[::7] = float("nan")
+    h = h.bfloat16()
+    out = FF.relu_dropout(h, F.relu, drop)
+    assert bool(torch.isnan(out[::7]).all())
+    assert not bool(torch.isnan(out[1::7]).any())

@@ -77,9 +77,10 @@ def _rank_main(rank, world, port, out_path):
         model = pkg.dvc_core.DeformableDVCCore(**SMALL)
         video, mask, dur = pkg.dvc_core.synthetic_clips(2, T=32, feature_dim=64, padded=True, seed=3)
         shard = (video[rank:rank + 1], mask[rank:rank + 1], dur[rank:rank + 1])
+        # small buckets: several all-reduces overlapped with the backward
         tr = pkg.train_step.FlatGradTrainer(model, pkg.dvc_core.workload_loss, lr=1e-3, weight_decay=1e-4,
-                                            max_norm=0.1, use_bf16=False, graph=False)
-        assert tr.world == world
+                                            max_norm=0.1, use_bf16=False, graph=False, bucket_mb=0.05)
+        assert tr.world == world and tr.overlap and len(tr.buckets) > 3
         with oracle_core(pkg):
             tr._forward_backward(shard)
             tr._allreduce()
@@ -222,3 +223,135 @@ def test_fused_flat_adamw_matches_torch_adamw():
     t.eager_step(batch)
     torch.cuda.synchronize()
     assert torch.equal(t.flat_bf16, t.flat_param.to(torch.bfloat16))
+
+
+def test_capture_refuses_when_graph_packet_capture_is_on():
+    """capture() raises unless the HIP runtime's graph packet capture is off; checked
+    before any device work, so it runs on the CPU (fresh process: the variable is read at import)."""
+    import subprocess
+    import sys
+    code = (
+        "import sys, importlib; sys.path.insert(0, %r)\n"
+        "pkg = importlib.import_module('multimodal-feature-learning_amd')\n"
+        "assert not pkg.graph_packet_capture_off()\n"
+        "import torch\n"
+        "torch.manual_seed(0)\n"
+        "m = pkg.dvc_core.DeformableDVCCore(d_model=64, num_queries=6, feature_dim=64, enc_layers=1, dec_layers=1,"
+        " ff_dim=128, dropout=0.0)\n"
+        "tr = pkg.train_step.FlatGradTrainer(m, pkg.dvc_core.workload_loss, use_bf16=False, graph=True)\n"
+        "try:\n"
+        "    tr.capture(None)\n"
+        "except RuntimeError as e:\n"
+        "    assert 'DEBUG_CLR_GRAPH_PACKET_CAPTURE' in str(e)\n"
+        "    print('refused')\n"
+    ) % ROOT
+    env = dict(os.environ, DEBUG_CLR_GRAPH_PACKET_CAPTURE="1")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "refused" in r.stdout, r.stderr
+
+
+@pytest.mark.gpu
+def test_learning_rate_change_reaches_the_replayed_update(dev):
+    """lr lives in device memory read by the update kernels: a schedule step between replays
+    (reference main.py:99 StepLR) changes what the captured update graph does."""
+    batch = _batch(2, dev)
+    model = _model(dev)
+    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, lr=1e-3, weight_decay=1e-2,
+                                        max_norm=0.1, use_bf16=True, graph=True)
+    tr.capture(batch, warmup=1)
+    tr._g_fb.replay()
+    tr.lr = 0.0  # no step and no decay (1 - lr * wd = 1)
+    before = tr.flat_param.clone()
+    tr._g_up.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(tr.flat_param, before)
+    tr.lr = 1e-3
+    tr._g_up.replay()
+    torch.cuda.synchronize()
+    assert not torch.equal(tr.flat_param, before)
+
+
+@pytest.mark.gpu
+def test_dropout_masks_are_fresh_on_every_replay(dev):
+    """The fused dropout kernels draw their keep bits from a device seed made by torch.randint
+    inside the captured graph: two replays on the same weights and inputs give different
+    gradients (a seed frozen at capture would replay the same masks every step)."""
+    torch.manual_seed(0)
+    model = PKG.dvc_core.DeformableDVCCore(**dict(SMALL, dropout=0.1)).to(dev)
+    batch = _batch(2, dev)
+    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, lr=1e-3, use_bf16=True, graph=True)
+    tr.capture(batch, warmup=1)
+    tr._g_fb.replay()
+    g1 = tr.flat_grad.clone()
+    tr._g_fb.replay()
+    g2 = tr.flat_grad.clone()
+    torch.cuda.synchronize()
+    assert torch.isfinite(g1).all() and torch.isfinite(g2).all()
+    assert not torch.equal(g1, g2)
+
+
+@pytest.mark.parametrize("bucket_mb", [0.001, 0.05, 32.0])
+def test_buckets_cover_every_parameter_once_in_reverse_order(bucket_mb):
+    """The all-reduce buckets: contiguous ranges of the flat buffer that tile it exactly, every
+    parameter in exactly one bucket, the last parameters (the backward's first gradients) first."""
+    model = _model()
+    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, use_bf16=False, graph=False,
+                                        bucket_mb=bucket_mb)
+    seen = sorted(i for _, _, idx in tr.buckets for i in idx)
+    assert seen == list(range(len(tr.params)))
+    ends = [(s, e) for s, e, _ in tr.buckets]
+    assert ends[0][1] == tr.flat_grad.numel() and ends[-1][0] == 0
+    for (s0, _), (_, e1) in zip(ends, ends[1:]):
+        assert e1 == s0  # reverse order, no gap, no overlap
+    cap = int(bucket_mb * 2 ** 20 / 4)
+    for s_, e, idx in tr.buckets:
+        assert e - s_ == sum(tr.params[i].numel() for i in idx)
+        assert e - s_ <= cap or len(idx) == 1
+
+
+def _nccl_rank_main(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import importlib
+    pkg = importlib.import_module("multimodal-feature-learning_amd")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    try:
+        torch.manual_seed(0)
+        base = pkg.dvc_core.DeformableDVCCore(**SMALL)
+        batch = pkg.dvc_core.synthetic_clips(2, T=32, feature_dim=64, padded=True, seed=3, device=dev)
+        res = {}
+        for name, kw in (("plain", dict(overlap=False)), ("overlap", dict(overlap="force", bucket_mb=0.05))):
+            tr = pkg.train_step.FlatGradTrainer(copy.deepcopy(base).to(dev), pkg.dvc_core.workload_loss, lr=1e-3,
+                                                use_bf16=False, graph=False, **kw)
+            tr._forward_backward(batch)
+            tr._allreduce()
+            res[name] = tr.flat_grad.cpu()
+        # graph mode: the bucket all-reduces captured with the backward
+        tr = pkg.train_step.FlatGradTrainer(copy.deepcopy(base).to(dev), pkg.dvc_core.workload_loss, lr=1e-3,
+                                            use_bf16=False, graph=True, overlap="force", bucket_mb=0.05)
+        assert tr.capture_collectives
+        tr.capture(batch, warmup=1)
+        tr._g_fb.replay()
+        torch.cuda.synchronize()
+        res["graph"] = tr.flat_grad.cpu()
+        res["graph_reduces"] = tr._fb_reduces
+        torch.save(res, out_path)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_one_rank_bucketed_allreduce_smoke(dev):
+    """The RCCL code path on one GPU: an nccl (= RCCL) process group of world size 1, the bucket
+    all-reduces overlapped with the backward (forced at one rank) eagerly and captured in the
+    fwd+bwd graph, against the trainer without collectives (one rank: the all-reduce is identity)."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "nccl.pt")
+        mp.start_processes(_nccl_rank_main, args=(1, _free_port(), out), nprocs=1, join=True, start_method="spawn")
+        r = torch.load(out, weights_only=True)
+    torch.testing.assert_close(r["overlap"], r["plain"], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(r["graph"], r["plain"], rtol=1e-4, atol=1e-5)
+    assert r["graph_reduces"]
