@@ -1195,15 +1195,6 @@ struct PairLayout {
 
 constexpr int kPairParts = 4;  // partial rows per wave (striped mode)
 
-// The loads of one pull batch of a slot: UB gathered grad_out fragments and their entries'
-// (c0, c1) (STG) or loc / aw (!STG).
-template <int UB>
-struct PairBatch {
-  uint4 g[UB];
-  f32x2 cc[UB];
-  float lc[UB], ac[UB];
-};
-
 // STG: 1 = (c0, c1) and sample positions staged in LDS; 2 = staged in a global workspace slice
 // of the workgroup (when they do not fit LDS beside the keys); 0 = keys only.
 template <typename scalar_t, int NSLOT, bool ZEROS, int STG, int U>
@@ -1232,12 +1223,18 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
   const int nsamp = Lq * P;
   const bool striped = STG == 1 && ((striped_mask >> l) & 1u) != 0u;
   unsigned* ekey = reinterpret_cast<unsigned*>(smem_raw);
-  // STG == 2: this workgroup's slice of the workspace, [(c0, c1) x Lq*P | position x Lq*P]
+  // an entry's (c0, c1), then (d0, d1); a sample's list position.  STG == 2: in this workgroup's
+  // slice of the workspace, [(c0, c1) x Lq*P | position x Lq*P].  Accessors (not one pointer
+  // chosen by a condition) so that every access keeps its address space: ds_* for LDS.
   unsigned char* gsl = STG == 2 ? gstage + (size_t)blk * ((size_t)Lq * P * 12) : nullptr;
-  f32x2* ecc = STG == 2 ? reinterpret_cast<f32x2*>(gsl)
-                        : reinterpret_cast<f32x2*>(smem_raw + lay.off_cc);  // (c0, c1), then (d0, d1)
-  int* pos_of = STG == 2 ? reinterpret_cast<int*>(gsl + (size_t)Lq * P * 8)
-                         : reinterpret_cast<int*>(smem_raw + lay.off_pos);  // a sample's list position
+  auto ECC = [&](int i) -> f32x2& {
+    if constexpr (STG == 2) return reinterpret_cast<f32x2*>(gsl)[i];
+    else return reinterpret_cast<f32x2*>(smem_raw + lay.off_cc)[i];
+  };
+  auto POS = [&](int i) -> int& {
+    if constexpr (STG == 2) return reinterpret_cast<int*>(gsl + (size_t)Lq * P * 8)[i];
+    else return reinterpret_cast<int*>(smem_raw + lay.off_pos)[i];
+  };
   // STG == 2: global stores of other waves become visible to this CU's loads only after they
   // completed (a barrier does not wait for them) and L1 holds no stale copy (agent acquire)
   auto gstage_sync = [&]() {
@@ -1340,8 +1337,8 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
       ekey[pos] = ((unsigned)q << 8) | (unsigned)p;
       if constexpr (STG) {
         const float a = awb[q * qs + p];
-        ecc[pos] = f32x2{t.ok0 ? a * t.w0 : 0.f, t.ok1 ? a * t.w1 : 0.f};
-        pos_of[s] = pos;
+        ECC(pos) = f32x2{t.ok0 ? a * t.w0 : 0.f, t.ok1 ? a * t.w1 : 0.f};
+        POS(s) = pos;
       }
     } else if (part == 0) {  // no tap on the map: zero coordinate gradients
       const long long o = q * qs + p;
@@ -1365,22 +1362,22 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
       for (int x = e0 + 1; x < e1; ++x) {
         const unsigned key = ekey[x];
         f32x2 kc = f32x2{0.f, 0.f};
-        if constexpr (STG) kc = ecc[x];
+        if constexpr (STG) kc = ECC(x);
         int y = x - 1;
         while (y >= e0 && ekey[y] > key) {
           ekey[y + 1] = ekey[y];
-          if constexpr (STG) ecc[y + 1] = ecc[y];
+          if constexpr (STG) ECC(y + 1) = ECC(y);
           --y;
         }
         ekey[y + 1] = key;
-        if constexpr (STG) ecc[y + 1] = kc;
+        if constexpr (STG) ECC(y + 1) = kc;
       }
     }
     gstage_sync();
     if (STG)  // the sorted positions
       for (int e = (int)threadIdx.x; e < N; e += kGvThreads) {
         const unsigned key = ekey[e];
-        pos_of[(int)(key >> 8) * P + (int)(key & 0xffu)] = e;
+        POS((int)(key >> 8) * P + (int)(key & 0xffu)) = e;
       }
     gstage_sync();
   }
@@ -1450,6 +1447,13 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
     return load16_if_nt(true, vl + (x * rs + co));
   };
   auto store_row = [&](int x, const f32x2 (&a)[H]) {
+#ifdef MSDA_PAIR_CHECK
+    if (x < 0 || x >= T) {
+      printf("pair check: store row %d of T=%d l=%d part=%d striped=%d row=%d\n", x, T, l, part, (int)striped,
+             (int)rowmode);
+      return;
+    }
+#endif
     float o[CPL];
 #pragma unroll
     for (int e = 0; e < H; ++e) {
@@ -1464,71 +1468,70 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
 #pragma unroll
   for (int e = 0; e < H; ++e) a0[e] = a1[e] = f32x2{0.f, 0.f};
   uint4 v0, v1;
-  // one batch: the slot's entries ebase + u * STR below lim, all of list rb (rows rb, rb + 1);
-  // issue() starts its loads, consume() adds it into a0 / a1 and writes its dots
-  auto issue = [&](auto& bt, int ebase, int STR, int lim) {
-    constexpr int UB = sizeof(bt.g) / sizeof(bt.g[0]);
+  // one batch: the slot's entries ebase + u * STR below lim, all of list rb (rows rb, rb + 1)
+  auto batch = [&](int ebase, int STR, int lim) {
+    uint4 g[U];
+    f32x2 cc[U];
+    float lcv[U], acv[U];
 #pragma unroll
-    for (int u = 0; u < UB; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int e = ebase + u * STR;
       const bool have = e < lim;
-      const unsigned key = ekey[have ? e : 0];
-      bt.g[u] = *reinterpret_cast<const uint4*>(gb + (__umul24(key >> 8, (unsigned)rs) + co));
+      unsigned key = ekey[have ? e : 0];
+#ifdef MSDA_PAIR_CHECK  // debug builds: report (instead of gathering through) an impossible key
+      if ((int)(key >> 8) >= Lq || (int)(key & 0xffu) >= P || (have && (e < 0 || e >= N))) {
+        printf("pair check: l=%d part=%d b=%lld m=%d e=%d lim=%d N=%d key=%u Lq=%d striped=%d row=%d\n", l, part,
+               b, m, e, lim, N, key, Lq, (int)striped, (int)rowmode);
+        key = 0;
+      }
+#endif
+      g[u] = *reinterpret_cast<const uint4*>(gb + (__umul24(key >> 8, (unsigned)rs) + co));
       if constexpr (STG) {
-        bt.cc[u] = ecc[have ? e : 0];
-        if (!have) bt.cc[u] = f32x2{0.f, 0.f};
+        cc[u] = have ? ECC(e) : f32x2{0.f, 0.f};
       } else {
         const long long o = (long long)(key >> 8) * qs + (key & 0xffu);
-        bt.lc[u] = locb[o];
-        bt.ac[u] = have ? awb[o] : 0.f;
+        lcv[u] = locb[o];
+        acv[u] = have ? awb[o] : 0.f;
       }
     }
-  };
-  auto consume = [&](auto& bt, int ebase, int STR, int lim) {
-    constexpr int UB = sizeof(bt.g) / sizeof(bt.g[0]);
 #pragma unroll
-    for (int u = 0; u < UB; ++u) {
+    for (int u = 0; u < U; ++u) {
       const int e = ebase + u * STR;
       const bool have = e < lim;
       Taps<float> t{};
-      f32x2 cu = bt.cc[u];
       if constexpr (!STG) {
-        t = make_taps<float, ZEROS>(bt.lc[u], T);
-        cu = f32x2{t.ok0 ? bt.ac[u] * t.w0 : 0.f, t.ok1 ? bt.ac[u] * t.w1 : 0.f};
+        t = make_taps<float, ZEROS>(lcv[u], T);
+        cc[u] = f32x2{t.ok0 ? acv[u] * t.w0 : 0.f, t.ok1 ? acv[u] * t.w1 : 0.f};
       }
       f32x2 x[H];
-      cvt16x2<scalar_t, CPL>(bt.g[u], x);
-      const f32x2 k0{cu.x, cu.x}, k1{cu.y, cu.y};
+      cvt16x2<scalar_t, CPL>(g[u], x);
+      const f32x2 k0{cc[u].x, cc[u].x}, k1{cc[u].y, cc[u].y};
 #pragma unroll
       for (int e2 = 0; e2 < H; ++e2) {
         a0[e2] = pk_fma(x[e2], k0, a0[e2]);
         a1[e2] = pk_fma(x[e2], k1, a1[e2]);
       }
       if (coords) {
-        const float d0 = group_sum<LPR>(dot16<scalar_t>(bt.g[u], v0));
-        const float d1 = group_sum<LPR>(dot16<scalar_t>(bt.g[u], v1));
+        const float d0 = group_sum<LPR>(dot16<scalar_t>(g[u], v0));
+        const float d1 = group_sum<LPR>(dot16<scalar_t>(g[u], v1));
         if (have && c_l == 0) {
           if constexpr (STG) {
-            ecc[e] = f32x2{d0, d1};
+            ECC(e) = f32x2{d0, d1};
           } else if (e >= wlo) {  // pre-list samples belong to the previous workgroup
             const unsigned key = ekey[e];
             const long long o = (long long)(key >> 8) * qs + (key & 0xffu);
             if (gab != nullptr) gab[o] = d0 * t.w0 + d1 * t.w1;
-            if (glb != nullptr) glb[o] = ((d1 - d0) * bt.ac[u]) * t.gmul;
+            if (glb != nullptr) glb[o] = ((d1 - d0) * acv[u]) * t.gmul;
           }
         }
       }
     }
   };
-  auto batch = [&](int ebase, int STR, int lim) {
-    PairBatch<U> bt;
-    issue(bt, ebase, STR, lim);
-    consume(bt, ebase, STR, lim);
-  };
 
   if (rowmode) {
     const int j = wave * NSLOT + slot;
-    float* ed = reinterpret_cast<float*>(ecc);  // entry e: [2e] = c0 -> d0, [2e + 1] = c1 -> d1
+    // entry e: [2e] = c0 -> d0, [2e + 1] = c1 -> d1 (row mode: STG == 1 only, LDS)
+    float* ed = reinterpret_cast<float*>(smem_raw + lay.off_cc);
     const int rend = min(rhi, T - 1);  // row rhi: the dots of the window's last list only
     for (int rr = max(rlo, 0); rr <= rend; rr += W) {
       const int r = rr + j;
@@ -1587,7 +1590,8 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
       }
     };
     // (a software-pipelined variant — next batch's loads issued before this one is consumed, row
-    // stores after them — measured slower: pull 42 vs 37 us at the encoder shape, U = 4 + 4)
+    // stores after them — measured slower: pull 42 vs 37 us at the encoder shape, U = 4 + 4;
+    // its batch buffers, passed between lambdas, also went to scratch)
     int eo = lo < hi ? en(rb) : 0;  // end of list rb
     v0 = vload(rb);
     v1 = vload(rb + 1);
@@ -1772,6 +1776,9 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
 #pragma unroll
             for (int e = 0; e < CPL; ++e) o[e] += p2[e];
           }
+#ifdef MSDA_PAIR_CHECK
+          if (x >= T) printf("pair check: merged row %d of T=%d l=%d\n", x, T, l); else
+#endif
           store_vec_nt<scalar_t, CPL>(gvl + (x * rs + co), o);
         }
       }
@@ -1804,7 +1811,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
             if (li >= li_lo && li <= li_hi) {
               const int q = s / P, p = s - q * P;
               const long long o = q * qs + p;
-              const f32x2 d = ecc[pos_of[s]];
+              const f32x2 d = ECC(POS(s));
               if (gab != nullptr) gab[o] = d.x * t.w0 + d.y * t.w1;
               if (glb != nullptr) glb[o] = ((d.y - d.x) * acv[k]) * t.gmul;
             }

@@ -108,7 +108,7 @@ class FlatGradTrainer:
         self.buckets = self._make_buckets(int(bucket_mb * 2 ** 20 / 4))
         # overlap="force": the bucket collectives also at world size 1 (a one-rank RCCL smoke)
         self.overlap = handover and (overlap == "force" or (bool(overlap) and self.world > 1))
-        backend = dist.get_backend(process_group) if self.world > 1 else None
+        backend = dist.get_backend(process_group) if dist.is_available() and dist.is_initialized() else None
         self.capture_collectives = (backend == "nccl") if capture_collectives is None else bool(capture_collectives)
         self._comm_stream = None
         self._pending = None
