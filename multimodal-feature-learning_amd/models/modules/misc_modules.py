@@ -4,8 +4,7 @@ from typing import Optional
 import torch
 from torch import Tensor
 
-__all__ = ["inverse_sigmoid", "predict_event_num", "predict_event_num_with_depth", "NestedTensor",
-           "decide_two_stage"]
+__all__ = ["inverse_sigmoid", "predict_event_num", "predict_event_num_with_depth", "NestedTensor"]
 
 
 def inverse_sigmoid(x, eps=1e-5):
@@ -46,25 +45,3 @@ class NestedTensor(object):
 
     def __repr__(self):
         return str(self.tensors)
-
-
-def decide_two_stage(transformer_input_type, gt_boxes, gt_boxes_mask, criterion):
-    """reference misc_modules.py:88-107"""
-    if transformer_input_type == 'gt_proposals':
-        two_stage = True
-        proposals = gt_boxes
-        proposals_mask = gt_boxes_mask
-        criterion.matcher.cost_caption = 0
-        for q_k in ['loss_length', 'loss_ce', 'loss_bbox', 'loss_giou']:
-            for key in criterion.weight_dict.keys():
-                if q_k in key:
-                    criterion.weight_dict[key] = 0
-        disable_iterative_refine = True
-    elif transformer_input_type == 'queries':
-        two_stage = False
-        proposals = None
-        proposals_mask = None
-        disable_iterative_refine = False
-    else:
-        raise ValueError('Wrong value of transformer_input_type, got {}'.format(transformer_input_type))
-    return two_stage, disable_iterative_refine, proposals, proposals_mask

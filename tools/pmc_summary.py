@@ -50,8 +50,17 @@ def main(root):
 # pyramid, bf16; tools/pmc_msda.sh runs the encoder shape only, so one grid per kernel)
 CALL_KERNELS = {
     "msda_fwd_S1920_Lq1920": ("msda_fwd16_kernel",),
-    "msda_bwd_S1920_Lq1920": ("msda_bwd_fused_kernel",),
+    "msda_bwd_S1920_Lq1920": ("msda_bwd_pair_kernel",),
 }
+
+
+def source_sha16():
+    """sha256 (16 hex) of csrc/msda.hip: bench.py takes the traffic only while the kernels that
+    produced it are the ones it runs."""
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    src = os.path.join(root, "multimodal-feature-learning_amd", "csrc", "msda.hip")
+    return hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
 
 
 def traffic_per_call(out):
@@ -64,6 +73,7 @@ def traffic_per_call(out):
                 parts[kname] = rec["traffic_bytes"]
         if len(parts) == len(kernels):
             res[call] = round(sum(parts.values()))
+    res["msda_hip_sha16"] = source_sha16()
     return res
 
 
