@@ -73,6 +73,9 @@ def parse():
     p.add_argument("--cpu-clips", type=int, default=3)
     p.add_argument("--graph", type=int, default=1, help="1: replay the step as HIP graphs (train_step.py)")
     p.add_argument("--timer-steps", type=int, default=2, help="eager steps timed per MSDA launch (roofline)")
+    p.add_argument("--gemm-solutions", default=os.path.join(ROOT, "profiles", "tunableop_gfx950.csv"),
+                   help="TunableOp results (hipBLASLt / rocBLAS solution per GEMM shape, tools/tune_gemms.py), "
+                        "read with tuning off; 'none' = the libraries' default heuristics")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                    help="per-launch HBM bytes from rocprofv3 PMC passes (profiles/), if present")
     return p.parse_args()
@@ -179,6 +182,21 @@ def roofline(summary, traffic):
                          for (k, (s, q)), v in summary.items()}}
 
 
+def use_gemm_solutions(path):
+    """Select the GEMM solutions recorded by tools/tune_gemms.py (PyTorch TunableOp over hipBLASLt
+    and rocBLAS): lookups only, no tuning inside the run; shapes not in the file keep the default."""
+    if not path or path == "none" or not os.path.exists(path):
+        return "library default heuristics"
+    tun = torch.cuda.tunable
+    tun.enable(True)
+    tun.tuning_enable(False)
+    tun.record_untuned_enable(False)
+    if not tun.read_file(path):
+        tun.enable(False)
+        return "library default heuristics (TunableOp file rejected)"
+    return "TunableOp selection " + os.path.relpath(path, ROOT)
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -189,6 +207,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     device = torch.device("cuda", local_rank)
     PKG._native.load_library()  # fail loudly before anything else if the HIP library is missing
+    gemm_sel = use_gemm_solutions(args.gemm_solutions)
 
     model = build_model(args, device)
     if world > 1:  # identical initial weights on every rank (the reference's DDP broadcast)
@@ -249,7 +268,7 @@ def main():
             "config": {"workload": WORKLOADS[args.config], "model": MODELS[args.config],
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch, "seq_len": args.T,
                        "d_model": 512, "levels": 4, "queries": args.queries, "parallelism": f"dp{world}",
-                       "execution": "hip_graph" if args.graph else "eager"},
+                       "execution": "hip_graph" if args.graph else "eager", "gemm_solutions": gemm_sel},
             "roofline": roofline(summary, traffic),
             "cpu_baseline": None,
         }

@@ -27,6 +27,15 @@ int mfl_relu_dropout_forward(const void* x, int64_t n, float p_drop, const int64
 int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float p_drop, int dropped, void* dx,
                               void* stream);
 
+/*
+ * x.view(rows, row_bytes).masked_fill_(mask[:, None], 0) in place: `value.masked_fill(
+ * input_padding_mask[..., None], 0)` of MSDeformAttn.forward (reference
+ * models/modules/attention.py:462-463) and its backward (the same on the value gradient).
+ * mask: rows bytes (torch.bool), non-zero = padding.  row_bytes % 16 == 0, x 16-byte aligned.
+ * Only padding rows are written.  Errors via mfl_relu_dropout_last_error().
+ */
+int mfl_zero_masked_rows(void* x, int64_t rows, int64_t row_bytes, const uint8_t* mask, void* stream);
+
 const char* mfl_relu_dropout_last_error(void);
 
 #ifdef __cplusplus

@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "mfl_relu_dropout_forward",
     "mfl_relu_dropout_backward",
     "mfl_relu_dropout_last_error",
+    "mfl_zero_masked_rows",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -98,6 +99,8 @@ def _declare(lib):
     lib.mfl_relu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]
     lib.mfl_relu_dropout_backward.restype = i32
     lib.mfl_relu_dropout_backward.argtypes = [vp, vp, i64, f32, i32, vp, vp]
+    lib.mfl_zero_masked_rows.restype = i32
+    lib.mfl_zero_masked_rows.argtypes = [vp, i64, i64, vp, vp]
     lib.mfl_relu_dropout_last_error.restype = ctypes.c_char_p
     lib.mfl_relu_dropout_last_error.argtypes = []
     lib.mfl_add_layernorm_last_error.restype = ctypes.c_char_p

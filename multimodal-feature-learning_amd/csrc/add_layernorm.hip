@@ -11,6 +11,8 @@
 // chunk): the row stays in registers between the statistics and the output.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdint>
 #include <cstdio>
 
@@ -90,6 +92,15 @@ __device__ __forceinline__ uint32_t drop_thresh(float p) {  // keep iff 24-bit d
   return (uint32_t)fminf(p * 16777216.f, 16777216.f);
 }
 
+// z = r + y: with both operands bf16 the reference's autocast add is a bf16 op (its result is
+// rounded to bf16 before the fp32 LayerNorm); otherwise the add is fp32.
+template <typename RT, typename YT>
+__device__ __forceinline__ float add_z(float a, float b) {
+  const float z = a + b;
+  if (sizeof(RT) == 2 && sizeof(YT) == 2) return __uint_as_float(Vec4<uint16_t>::rne(z) << 16);
+  return z;
+}
+
 template <typename RT, typename YT, int CH>
 __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__ r, const YT* __restrict__ y,
                                                          const float* __restrict__ gamma,
@@ -118,7 +129,7 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      z[c][k] = a[k] + b[k];
+      z[c][k] = add_z<RT, YT>(a[k], b[k]);
       s += z[c][k];
     }
   }
@@ -207,7 +218,7 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
       Vec4<float>::load(gamma + col, ga);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        xh[c][k] = (a[k] + b[k] - mean) * rstd;
+        xh[c][k] = (add_z<RT, YT>(a[k], b[k]) - mean) * rstd;
         g[c][k] = go[k] * ga[k];
         s1 += g[c][k];
         s2 += g[c][k] * xh[c][k];
@@ -328,6 +339,21 @@ int bwd(const float* dout, const void* r, const void* y, const float* gamma, con
 }
 #undef MFL_ALN_BWD
 
+// Zero fill as a kernel, not hipMemsetAsync: under the HIP runtime's graph packet capture a
+// captured memset node did not take effect on replays that followed eager work
+// (tools/packet_capture_unit.py), so nothing this library launches is a memset.
+__global__ void zero_f32_kernel(float* __restrict__ p, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] = 0.f;
+}
+
+hipError_t zero_f32(float* p, long long n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(zero_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, n);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -387,8 +413,7 @@ int mfl_add_layernorm_backward_ex(const float* dout, const uint16_t* dout16, con
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (rows == 0) {
-    if (hipMemsetAsync(dgamma, 0, (size_t)d * 4, st) != hipSuccess ||
-        hipMemsetAsync(dbeta, 0, (size_t)d * 4, st) != hipSuccess)
+    if (zero_f32(dgamma, d, st) != hipSuccess || zero_f32(dbeta, d, st) != hipSuccess)
       return 2;
     return 0;
   }

@@ -255,6 +255,21 @@ int status(const char* what) {
   return 0;
 }
 
+// Zero fill as a kernel, not hipMemsetAsync: under the HIP runtime's graph packet capture a
+// captured memset node did not take effect on replays that followed eager work
+// (tools/packet_capture_unit.py), so nothing this library launches is a memset.
+__global__ void zero_f32_kernel(float* __restrict__ p, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] = 0.f;
+}
+
+hipError_t zero_f32(float* p, long long n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(zero_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, n);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -312,7 +327,7 @@ int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void*
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (K == 0) {
-    return hipMemsetAsync(out, 0, (size_t)N * 4, st) == hipSuccess ? 0 : 2;
+    return zero_f32(out, N, st) == hipSuccess ? 0 : 2;
   }
   const long long chunks = std::min<long long>(256, std::max<long long>(1, (K + 63) / 64));
   const int rows_per_chunk = (int)((K + chunks - 1) / chunks);

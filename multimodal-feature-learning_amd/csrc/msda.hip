@@ -3157,6 +3157,21 @@ __global__ __launch_bounds__(kDamThreads) void msda_dam_kernel(
   }
 }
 
+// Zero fill as a kernel, not hipMemsetAsync: under the HIP runtime's graph packet capture a
+// captured memset node did not take effect on replays that followed eager work
+// (tools/packet_capture_unit.py), so nothing this library launches is a memset.
+__global__ void zero_f32_kernel(float* __restrict__ p, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] = 0.f;
+}
+
+hipError_t zero_f32(float* p, long long n, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(zero_f32_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, n);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 extern "C" {
@@ -3191,8 +3206,8 @@ int msda_hip_dam_flat_grid(const void* sampling_loc, const void* attn_weight, co
     hipLaunchKernelGGL((msda_dam_kernel<true>), dim3((unsigned)nrows), dim3(kDamThreads), lds, st, lc, a, out,
                        pr.lv, (int)pr.L, (int)pr.P, (int)pr.M, (int)pr.Lq, (int)S);
   } else {
-    if (hipMemsetAsync(out, 0, (size_t)nrows * S * 4, st) != hipSuccess) {
-      set_error("msda_hip_dam_flat_grid: memset failed");
+    if (zero_f32(out, nrows * S, st) != hipSuccess) {
+      set_error("msda_hip_dam_flat_grid: zero fill failed");
       return MSDA_ERR_LAUNCH;
     }
     hipLaunchKernelGGL((msda_dam_kernel<false>), dim3((unsigned)nrows), dim3(kDamThreads), 0, st, lc, a, out, pr.lv,

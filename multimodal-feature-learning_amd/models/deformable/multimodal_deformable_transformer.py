@@ -13,7 +13,7 @@ import torch
 from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
-from ..modules.attention import MSDeformAttn
+from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
@@ -260,8 +260,7 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
     def forward(self, tgt, query_pos, reference_points_input_video, reference_points_input_audio, query_mask,
                 video_src, video_temporal_shapes, video_level_start_index, video_src_padding_mask, audio_src,
                 audio_temporal_shapes, audio_level_start_index, audio_src_padding_mask):
-        qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
-        sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
+        sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask)
         tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         tgt_video = self._cross_block(tgt, query_pos, reference_points_input_video, video_src, video_temporal_shapes,
                                       video_level_start_index, video_src_padding_mask)

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
-from ..modules.attention import MSDeformAttn
+from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
@@ -270,8 +270,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None):
-        qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
-        sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
+        sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask)
         if carry_supported(tgt, self.norm2) and (query_pos is None or query_pos.shape == tgt.shape):
             # bf16(tgt + query_pos) for the cross-attention query and bf16(tgt) for linear1 straight
             # from the fused add + LayerNorms (no pos add, no casts, no gradient accumulation)

@@ -5,9 +5,10 @@ Reference pattern: ``src = self.norm1(src + self.dropout1(src2))`` and the FFN's
 362-373; the multimodal and sparse layers repeat it).  Under bf16 autocast that is an fp32 add
 of the residual stream and the 16-bit branch, an fp32 LayerNorm, and in the backward
 LayerNorm's input and gamma/beta kernels plus a cast of the branch gradient back to 16 bits.
-``add_layer_norm`` runs it as csrc/add_layernorm.hip (include/add_layernorm.h): the same fp32
-arithmetic (z = r + y in fp32, fp32 statistics), with the branch gradient written directly in
-its own dtype.  Outside autocast, on the CPU, or for shapes the kernel does not take
+``add_layer_norm`` runs it as csrc/add_layernorm.hip (include/add_layernorm.h): the same
+arithmetic (z = r + y in fp32 — rounded to bf16 when both operands are bf16, as autocast's bf16
+add is, e.g. the multimodal FFN — and fp32 statistics), with the branch gradient written
+directly in its own dtype.  Outside autocast, on the CPU, or for shapes the kernel does not take
 (d % 256 != 0, d > 1024, other dtypes) it is exactly ``norm(r + y)``.
 """
 import torch

@@ -30,7 +30,7 @@ from ..ops.modules.ms_deform_attn import stack_sampled_values
 from .linear import Linear, linear_pair
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
-           "masked_scores_softmax"]
+           "masked_scores_softmax", "mask_padding_rows", "mha_self_attention"]
 
 
 def _loc5(sampling_locations):
@@ -129,7 +129,7 @@ class MSDeformAttn(nn.Module):
 
         value = self.value_proj(input_flatten)
         if input_padding_mask is not None:
-            value = value.masked_fill(input_padding_mask[..., None], float(0))
+            value = mask_padding_rows(value, input_padding_mask)
         value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
 
         # one input cast and one fused backward for the two query projections
@@ -166,6 +166,75 @@ class MSDeformAttn(nn.Module):
         if is_sparse:
             return output, sampling_locations.unsqueeze(-1), attention_weights
         return output
+
+
+class _ZeroPaddingRows(torch.autograd.Function):
+    """In-place ``value.masked_fill_(mask[..., None], 0)`` through ``mfl_zero_masked_rows``: only
+    padding rows are written (an all-valid batch reads the mask and nothing else); the backward
+    zeroes the same rows of the incoming gradient, which only the MSDA backward produced."""
+
+    @staticmethod
+    def forward(ctx, value, mask):
+        _zero_rows(value, mask)
+        ctx.mark_dirty(value)
+        ctx.save_for_backward(mask)
+        return value
+
+    @staticmethod
+    def backward(ctx, grad):
+        (mask,) = ctx.saved_tensors
+        grad = grad.contiguous()
+        _zero_rows(grad, mask)
+        return grad, None
+
+
+def _zero_rows(x, mask):
+    from ... import _native
+    lib = _native.load_library()
+    rows = mask.numel()
+    rc = lib.mfl_zero_masked_rows(x.data_ptr(), rows, x.numel() * x.element_size() // max(rows, 1),
+                                  mask.data_ptr(), _native.stream_handle(x.device))
+    if rc != 0:
+        raise RuntimeError("mfl_zero_masked_rows failed: " + lib.mfl_relu_dropout_last_error().decode())
+
+
+def mask_padding_rows(value, mask):
+    """``value.masked_fill(mask[..., None], 0)`` for value (N, Len_in, C) and a bool mask (N, Len_in)
+    (reference attention.py:462-463).  On the GPU, for a contiguous value whose rows are a multiple
+    of 16 bytes, the fill is done in place on the value projection's fresh output (the projection
+    keeps its input, not its output, for the backward)."""
+    if (value.is_cuda and value.is_contiguous() and mask.dtype == torch.bool and mask.is_contiguous()
+            and mask.device == value.device and mask.shape == value.shape[:-1]
+            and (value.shape[-1] * value.element_size()) % 16 == 0 and value.data_ptr() % 16 == 0
+            and value.numel() > 0):
+        return _ZeroPaddingRows.apply(value, mask)
+    return value.masked_fill(mask[..., None], float(0))
+
+
+def mha_self_attention(mha, tgt, query_pos, query_mask):
+    """The decoder's query self-attention, batch first:
+    ``mha((tgt + pos)^T, (tgt + pos)^T, tgt^T, key_padding_mask=~query_mask)[0]^T`` (reference
+    unimodal_deformable_transformer.py:352-353 and the multimodal / sparse decoders) with the
+    module's own parameters (``in_proj_weight`` / ``in_proj_bias`` / ``out_proj``, so state_dicts
+    are unchanged).  The reference discards the attention weights it asks for, so the product runs
+    as one ``F.scaled_dot_product_attention`` (dropout on the attention probabilities as the
+    module's) instead of bmm / softmax / dropout / bmm and the sequence-first transposes.
+    tgt, query_pos (B, L, E); query_mask (B, L) bool, True = a real query."""
+    if (mha.batch_first or not mha._qkv_same_embed_dim or mha.bias_k is not None or mha.add_zero_attn
+            or mha.in_proj_bias is None or (query_pos is not None and query_pos.shape != tgt.shape)):
+        qk = (tgt if query_pos is None else tgt + query_pos).transpose(0, 1)
+        return mha(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
+    B, L, E = tgt.shape
+    H = mha.num_heads
+    hd = E // H
+    w, b = mha.in_proj_weight, mha.in_proj_bias
+    qk = F.linear(tgt if query_pos is None else tgt + query_pos, w[:2 * E], b[:2 * E])
+    v = F.linear(tgt, w[2 * E:], b[2 * E:])
+    q, k = qk.view(B, L, 2, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
+    v = v.view(B, L, H, hd).transpose(1, 2)
+    out = F.scaled_dot_product_attention(q, k, v, attn_mask=query_mask[:, None, None, :],
+                                         dropout_p=mha.dropout if mha.training else 0.0)
+    return F.linear(out.transpose(1, 2).reshape(B, L, E), mha.out_proj.weight, mha.out_proj.bias)
 
 
 def masked_scores_softmax(scores, masked, scale, neg_fill=-1e20):

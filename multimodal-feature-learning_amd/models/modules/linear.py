@@ -83,7 +83,9 @@ class _AutocastLinear(torch.autograd.Function):
         ctx.save_for_backward(x2, wc)
         ctx.has_bias = bias is not None
         ctx.x_shape = x.shape
-        return y.view(*x.shape[:-1], wc.shape[0])
+        # not an autograd view of the 2-D GEMM output (as F.linear's 3-D result): callers may
+        # modify it in place (MSDeformAttn zeroes the padding rows of value_proj's output)
+        return torch.ops.aten._unsafe_view(y, (*x.shape[:-1], wc.shape[0]))
 
     @staticmethod
     def backward(ctx, gy):

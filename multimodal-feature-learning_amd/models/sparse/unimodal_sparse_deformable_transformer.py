@@ -22,7 +22,7 @@ from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from ..deformable.unimodal_deformable_transformer import encoder_reference_points, level_metadata
-from ..modules.attention import MSDeformAttn
+from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm
 from ..modules.ffn import relu_dropout
@@ -294,8 +294,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None):
-        qk = self.with_pos_embed(tgt, query_pos).transpose(0, 1)
-        sa = self.self_attn(qk, qk, tgt.transpose(0, 1), key_padding_mask=~query_mask)[0].transpose(0, 1)
+        sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask)
         tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         ca, sampling_locations, attn_weights = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points,
                                                                src, src_temporal_shapes, level_start_index,

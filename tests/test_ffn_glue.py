@@ -81,3 +81,37 @@ def test_nan_propagates_as_aten(dev, train):
     out = FF.relu_dropout(h, F.relu, drop)
     assert bool(torch.isnan(out[::7]).all())
     assert not bool(torch.isnan(out[1::7]).any())
+
+
+@pytest.mark.gpu
+def test_graph_replays_draw_fresh_masks(dev):
+    """The dropout seed is drawn on the device inside the captured region, so every replay of a
+    graph draws new keep bits (a seed frozen at capture would reuse one mask for every step):
+    the FFN relu_dropout and the fused add + LayerNorm's residual dropout, replayed twice."""
+    AN = PKG.models.modules.add_norm
+    torch.manual_seed(3)
+    drop = torch.nn.Dropout(0.1).train()
+    norm = torch.nn.LayerNorm(512).to(dev)
+    h = torch.randn(256, 2048, device=dev).abs().bfloat16() + 0.5  # relu keeps every element
+    r = torch.randn(256, 512, device=dev)
+    y = torch.randn(256, 512, device=dev).bfloat16()
+    side = torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(side), torch.autocast("cuda", dtype=torch.bfloat16):
+        FF.relu_dropout(h, F.relu, drop)
+        AN.add_layer_norm(r, y, norm, drop)
+    torch.cuda.current_stream().wait_stream(side)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g), torch.autocast("cuda", dtype=torch.bfloat16):
+        out_f = FF.relu_dropout(h, F.relu, drop)
+        out_n = AN.add_layer_norm(r, y, norm, drop)
+    masks, norms = [], []
+    for _ in range(2):
+        g.replay()
+        torch.cuda.synchronize()
+        masks.append(out_f != 0)
+        norms.append(out_n.clone())
+    for m in masks:
+        assert abs(m.float().mean().item() - 0.9) < 0.01
+    assert (masks[0] != masks[1]).float().mean().item() > 0.1  # independent masks differ in ~18 %
+    assert not torch.equal(norms[0], norms[1])

@@ -165,3 +165,27 @@ def test_cap_module_init_matches_reference_layout(golden):
     m = M.ops.modules.MSDeformAttnCap(32, 4, 4, 4)
     assert {k: tuple(v.shape) for k, v in m.state_dict().items()} == {k: tuple(v.shape) for k, v in sd.items()}
     torch.testing.assert_close(m.sampling_offsets.bias, sd["sampling_offsets.bias"].float())
+
+
+def test_mha_self_attention_matches_module():
+    """Decoder query self-attention as one SDPA over the module's parameters (attention.py
+    mha_self_attention) equals nn.MultiheadAttention's sequence-first call (reference
+    unimodal_deformable_transformer.py:352-353), fp64, with padded queries; gradients too."""
+    import torch
+    from conftest import PKG
+    att = PKG.models.modules.attention
+    torch.manual_seed(0)
+    mha = torch.nn.MultiheadAttention(64, 8, dropout=0.1).double().eval()
+    tgt = torch.randn(3, 10, 64, dtype=torch.float64, requires_grad=True)
+    pos = torch.randn(3, 10, 64, dtype=torch.float64)
+    qmask = torch.ones(3, 10, dtype=torch.bool)
+    qmask[1, 7:] = False
+    out = att.mha_self_attention(mha, tgt, pos, qmask)
+    qk = (tgt + pos).transpose(0, 1)
+    ref = mha(qk, qk, tgt.transpose(0, 1), key_padding_mask=~qmask)[0].transpose(0, 1)
+    torch.testing.assert_close(out, ref, rtol=1e-12, atol=1e-12)
+    g = torch.randn_like(out)
+    ga = torch.autograd.grad(out, [tgt] + list(mha.parameters()), g)
+    gb = torch.autograd.grad(ref, [tgt] + list(mha.parameters()), g)
+    for a, b in zip(ga, gb):
+        torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-10)

@@ -5,7 +5,9 @@ Each case captures a tiny graph around ONE node kind between two kernels, replay
 allocating eager work (new tensors, a D2D clone, a reduction, a GEMM), replays again and checks
 the result against the eager value.  Node kinds: a same-dtype D2D copy (hipMemcpyAsync, the
 runtime's copyBuffer blit kernel), a hipMemsetAsync (the library's K=0 column-sum path), a
-side-stream fork/join (event record / wait), and a plain kernel chain as the control.
+side-stream fork/join (event record / wait), a multi-block ATen sum, the library's K = 0 column
+sum (a hipMemsetAsync until round 2, now a zero-fill kernel), and a plain kernel chain as the
+control.
 Run once with DEBUG_CLR_GRAPH_PACKET_CAPTURE=1 and once with 0 (PROBE_PACKET_CAPTURE).
 Diagnostic only."""
 import importlib
@@ -70,15 +72,6 @@ def k_chain(b):
     b["out"].add_(1.0)
 
 
-def k_memset(b):
-    lib = PKG._native.load_library()
-    b["tmp"].copy_(b["x"] * 2.0)
-    rc = lib.mfl_colsum(b["tmp"].data_ptr(), 0, 0, 256, b["col"].data_ptr(), b["tmp"].data_ptr(),
-                        PKG._native.stream_handle(dev))  # K = 0: hipMemsetAsync of the output
-    assert rc == 0
-    b["out"].copy_(b["tmp"] + b["col"].sum())
-
-
 _side = None
 
 
@@ -95,7 +88,31 @@ def k_fork(b):
     b["out"].copy_(b["tmp"] + b["col"].sum())
 
 
+def k_sum(b):  # a multi-block ATen reduction (its semaphores are zeroed with a memset)
+    b["tmp"].copy_(b["x"] * 2.0)
+    b["out"].copy_(b["tmp"] + b["tmp"].sum())
+
+
+def k_colsum0(b):  # the library's K = 0 column sum, now a zero-fill kernel
+    lib = PKG._native.load_library()
+    b["tmp"].copy_(b["x"] * 2.0)
+    assert lib.mfl_colsum(b["tmp"].data_ptr(), 0, 0, 256, b["col"].data_ptr(), b["tmp"].data_ptr(),
+                          PKG._native.stream_handle(dev)) == 0
+    b["out"].copy_(b["tmp"] + b["col"].sum())
+
+
+def k_memset_raw(b):  # hipMemsetAsync itself, through the HIP runtime
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    b["tmp"].copy_(b["x"] * 2.0)
+    b["col"].fill_(5.0)
+    assert hip.hipMemsetAsync(ctypes.c_void_p(b["col"].data_ptr()), 0, ctypes.c_size_t(1024),
+                              ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    b["out"].copy_(b["tmp"] + b["col"].sum())
+
+
 bad = 0
-for name, fn in (("kernel chain", k_chain), ("D2D memcpy", k_copy), ("memset", k_memset), ("fork/join", k_fork)):
+for name, fn in (("kernel chain", k_chain), ("D2D memcpy", k_copy), ("hipMemsetAsync", k_memset_raw),
+                 ("colsum K=0", k_colsum0), ("torch sum", k_sum), ("fork/join", k_fork)):
     bad += run_case(name, fn)
 print("packet capture", os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"], "bad cases:", bad)
