@@ -36,6 +36,11 @@ int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float 
  */
 int mfl_zero_masked_rows(void* x, int64_t rows, int64_t row_bytes, const uint8_t* mask, void* stream);
 
+/* The same on nbatch consecutive (rows x row_bytes) matrices sharing one mask of rows bytes: the
+ * decoder's value projections of all layers, computed as one batch (models/modules/value_proj.py). */
+int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t row_bytes, const uint8_t* mask,
+                                 void* stream);
+
 const char* mfl_relu_dropout_last_error(void);
 
 #ifdef __cplusplus

@@ -40,7 +40,12 @@ int flat_adamw_step(float* params, const float* grads, float* exp_avg, float* ex
 size_t mfl_colsum_workspace_bytes(int64_t K, int64_t N);
 int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void* workspace, void* stream);
 
-/* Text of the last error of flat_adamw_step / mfl_colsum on the calling thread. */
+/* out[i] = sum over k < s of part[k * n + i] (fp32, chunk order): the split-K partial products of
+ * the autocast Linear's weight gradient summed into the fp32 gradient.  n % 4 == 0, 16-byte
+ * aligned pointers. */
+int mfl_sum_slabs(const float* part, int64_t s, int64_t n, float* out, void* stream);
+
+/* Text of the last error of flat_adamw_step / mfl_colsum / mfl_sum_slabs on the calling thread. */
 const char* flat_adamw_last_error(void);
 
 #ifdef __cplusplus

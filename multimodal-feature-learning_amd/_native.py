@@ -36,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "flat_adamw_last_error",
     "mfl_colsum_workspace_bytes",
     "mfl_colsum",
+    "mfl_sum_slabs",
     # include/add_layernorm.h
     "mfl_add_layernorm_workspace_bytes",
     "mfl_add_layernorm_forward",
@@ -48,6 +49,7 @@ EXPORTED_SYMBOLS = (
     "mfl_relu_dropout_backward",
     "mfl_relu_dropout_last_error",
     "mfl_zero_masked_rows",
+    "mfl_zero_masked_rows_batched",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -81,6 +83,8 @@ def _declare(lib):
     lib.flat_adamw_step.argtypes = [vp, vp, vp, vp, vp, i64, vp, vp, f32, f32, f32, f32, f32, f32, vp, vp]
     lib.mfl_colsum_workspace_bytes.restype = ctypes.c_size_t
     lib.mfl_colsum_workspace_bytes.argtypes = [i64, i64]
+    lib.mfl_sum_slabs.restype = i32
+    lib.mfl_sum_slabs.argtypes = [vp, i64, i64, vp, vp]
     lib.mfl_colsum.restype = i32
     lib.mfl_colsum.argtypes = [vp, i32, i64, i64, vp, vp, vp]
     lib.mfl_add_layernorm_workspace_bytes.restype = ctypes.c_size_t
@@ -101,6 +105,8 @@ def _declare(lib):
     lib.mfl_relu_dropout_backward.argtypes = [vp, vp, i64, f32, i32, vp, vp]
     lib.mfl_zero_masked_rows.restype = i32
     lib.mfl_zero_masked_rows.argtypes = [vp, i64, i64, vp, vp]
+    lib.mfl_zero_masked_rows_batched.restype = i32
+    lib.mfl_zero_masked_rows_batched.argtypes = [vp, i64, i64, i64, vp, vp]
     lib.mfl_relu_dropout_last_error.restype = ctypes.c_char_p
     lib.mfl_relu_dropout_last_error.argtypes = []
     lib.mfl_add_layernorm_last_error.restype = ctypes.c_char_p

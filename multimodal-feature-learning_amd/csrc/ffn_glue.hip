@@ -92,11 +92,13 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_bwd(const uint4* __rest
 // value.masked_fill(padding_mask[..., None], 0) of MSDeformAttn (reference attention.py:462-463) in
 // place, and the same on its gradient: one wave per row reads the row's mask byte and stores zeros
 // only when the row is padding, so an all-valid batch costs the mask read, not a pass over value.
+// Row i of x uses mask[i % mask_rows] (a batch of matrices sharing one token mask).
 __global__ __launch_bounds__(kThreads) void zero_masked_rows_kernel(uint4* __restrict__ x, long long rows,
                                                                    int vec_per_row,
-                                                                   const uint8_t* __restrict__ mask) {
+                                                                   const uint8_t* __restrict__ mask,
+                                                                   long long mask_rows) {
   const long long row = (long long)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (row >= rows || mask[row] == 0) return;  // wave-uniform
+  if (row >= rows || mask[row % mask_rows] == 0) return;  // wave-uniform
   uint4* p = x + row * vec_per_row;
   for (int i = threadIdx.x & 63; i < vec_per_row; i += 64) p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
@@ -164,22 +166,28 @@ int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float 
   return status("backward");
 }
 
-int mfl_zero_masked_rows(void* x, int64_t rows, int64_t row_bytes, const uint8_t* mask, void* stream) {
+int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t row_bytes, const uint8_t* mask,
+                                 void* stream) {
   g_err[0] = 0;
-  if (rows < 0 || row_bytes <= 0 || row_bytes % 16 != 0 || row_bytes / 16 > (1 << 30)) {
+  if (nbatch < 0 || rows < 0 || row_bytes <= 0 || row_bytes % 16 != 0 || row_bytes / 16 > (1 << 30)) {
     snprintf(g_err, sizeof(g_err), "mfl_zero_masked_rows: rows >= 0 and row_bytes a positive multiple of 16 needed");
     return 1;
   }
-  if (rows == 0) return 0;
+  if (rows == 0 || nbatch == 0) return 0;
   if (!x || !mask || ((uintptr_t)x & 15u)) {
     snprintf(g_err, sizeof(g_err), "mfl_zero_masked_rows: null pointer or x not 16-byte aligned");
     return 1;
   }
-  const long long blocks = (rows + kThreads / 64 - 1) / (kThreads / 64);
+  const long long total = nbatch * rows;
+  const long long blocks = (total + kThreads / 64 - 1) / (kThreads / 64);
   hipLaunchKernelGGL(zero_masked_rows_kernel, dim3((unsigned)blocks), dim3(kThreads), 0,
-                     static_cast<hipStream_t>(stream), static_cast<uint4*>(x), (long long)rows, (int)(row_bytes / 16),
-                     mask);
+                     static_cast<hipStream_t>(stream), static_cast<uint4*>(x), total, (int)(row_bytes / 16), mask,
+                     (long long)rows);
   return status("zero masked rows");
+}
+
+int mfl_zero_masked_rows(void* x, int64_t rows, int64_t row_bytes, const uint8_t* mask, void* stream) {
+  return mfl_zero_masked_rows_batched(x, 1, rows, row_bytes, mask, stream);
 }
 
 const char* mfl_relu_dropout_last_error(void) { return g_err; }

@@ -68,15 +68,29 @@ class DeformableDVCCore(nn.Module):
         _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qw)
         hs, inter = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten, query_mask,
                                        False)
-        classes, segments, counts = [], [], []
-        for lvl in range(hs.shape[0]):
-            classes.append(self.class_embedding[lvl](hs[lvl]).softmax(dim=-1))
-            segments.append(self.segment_embedding[lvl](hs[lvl]).sigmoid())
-            counts.append(predict_event_num(self.count_head[lvl], hs[lvl]))
-        cls, seg, cnt = torch.stack(classes), torch.stack(segments), torch.stack(counts)
+        cls, seg, cnt = _level_heads(self, hs)
         return {"pred_logits": cls[-1], "pred_segments": seg[-1], "pred_count": cnt[-1],
                 "all_logits": cls, "all_segments": seg, "all_counts": cnt,
                 "hs": hs, "inter_references": inter, "memory": memory}
+
+
+def _level_heads(core, hs):
+    """Class / segment / count heads on every decoder level of hs (depth, B, Q, d), stacked over
+    levels (reference unimodal_deformable_dvc.py:197-203, heads applied per level).  The reference
+    builds the per-level heads as ONE shared module (:72-74), so here each head runs once over the
+    stacked levels (row-wise layers: the same numbers, a sixth of the launches, and no per-level
+    select whose backward writes a full-size zero gradient per level); distinct per-level heads
+    run level by level."""
+    heads = (core.class_embedding, core.segment_embedding, core.count_head)
+    if all(all(m is h[0] for m in h) for h in heads):
+        return (core.class_embedding[0](hs).softmax(dim=-1), core.segment_embedding[0](hs).sigmoid(),
+                predict_event_num_with_depth(core.count_head[0], hs))
+    classes, segments, counts = [], [], []
+    for lvl, h in enumerate(hs.unbind(0)):
+        classes.append(core.class_embedding[lvl](h).softmax(dim=-1))
+        segments.append(core.segment_embedding[lvl](h).sigmoid())
+        counts.append(predict_event_num(core.count_head[lvl], h))
+    return torch.stack(classes), torch.stack(segments), torch.stack(counts)
 
 
 def synthetic_clips(batch, T=1024, feature_dim=512, padded=False, seed=0, device="cpu", dtype=torch.float32):
@@ -147,13 +161,9 @@ class MultimodalDVCCore(nn.Module):
         _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qw)
         hs, inter = tr.forward_decoder(tgt, refp, qpos, query_mask, mem_v, v[1], v[2], v[3], v[5], mem_a, a[1], a[2],
                                        a[3], a[5], False)
-        classes, segments, counts = [], [], []
-        for lvl in range(hs.shape[0]):
-            classes.append(self.class_embedding[lvl](hs[lvl]).softmax(dim=-1))
-            segments.append(self.segment_embedding[lvl](hs[lvl]).sigmoid())
-            counts.append(predict_event_num(self.count_head[lvl], hs[lvl]))
-        return {"all_logits": torch.stack(classes), "all_segments": torch.stack(segments),
-                "all_counts": torch.stack(counts), "hs": hs, "memory_video": mem_v, "memory_audio": mem_a}
+        cls, seg, cnt = _level_heads(self, hs)
+        return {"all_logits": cls, "all_segments": seg, "all_counts": cnt, "hs": hs, "memory_video": mem_v,
+                "memory_audio": mem_a}
 
 
 def multimodal_workload_loss(out):

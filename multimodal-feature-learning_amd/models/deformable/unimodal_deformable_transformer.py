@@ -21,6 +21,7 @@ from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 from ..modules.ffn import relu_dropout
+from ..modules.value_proj import layer_values, layer_values_supported
 
 __all__ = [
     "DeformableTransformer", "DeformableTransformerEncoderLayer", "DeformableTransformerEncoder",
@@ -233,6 +234,7 @@ class DeformableTransformerEncoder(nn.Module):
                                                         temporal_shapes, level_start_index, padding_mask)
                 if query is None:
                     query = value
+            out._mfl_bf16 = value  # the last layer's bf16(out): the decoder's value projections read it
             return out
         for layer in self.layers:
             out = layer(out, pos, reference_points, temporal_shapes, level_start_index, padding_mask)
@@ -269,20 +271,21 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
-                src_padding_mask=None, query_mask=None):
+                src_padding_mask=None, query_mask=None, value=None):
+        """``value``: this layer's cross-attention value, when the decoder computed it (value_proj.py)."""
         sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask)
         if carry_supported(tgt, self.norm2) and (query_pos is None or query_pos.shape == tgt.shape):
             # bf16(tgt + query_pos) for the cross-attention query and bf16(tgt) for linear1 straight
             # from the fused add + LayerNorms (no pos add, no casts, no gradient accumulation)
             tgt, tgt16, q16 = add_layer_norm_carry(tgt, sa, self.norm2, query_pos, self.dropout2)
             ca = self.cross_attn(q16 if q16 is not None else tgt16, reference_points, src, src_temporal_shapes,
-                                 level_start_index, src_padding_mask)
+                                 level_start_index, src_padding_mask, value=value)
             tgt, tgt16, _ = add_layer_norm_carry(tgt, ca, self.norm1, dropout=self.dropout1)
             hidden = relu_dropout(self.linear1(tgt16), self.activation, self.dropout3)
             return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
         tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         ca = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_temporal_shapes,
-                             level_start_index, src_padding_mask)
+                             level_start_index, src_padding_mask, value=value)
         tgt = add_layer_norm(tgt, ca, self.norm1, dropout=self.dropout1)
         return self.forward_ffn(tgt)
 
@@ -305,6 +308,12 @@ class DeformableTransformerDecoder(nn.Module):
         hs, refs = [], []
         if query_pos is not None and not query_pos.is_contiguous():
             query_pos = query_pos.contiguous()  # once, not per layer (the fused layers read it flat)
+        values = None
+        attns = [getattr(layer, "cross_attn", None) for layer in self.layers]
+        if (all(type(layer) is DeformableTransformerDecoderLayer for layer in self.layers)
+                and layer_values_supported(attns, src, src_padding_mask)):
+            # every layer projects the same memory: one batched GEMM each way (value_proj.py)
+            values = layer_values(attns, src, src_padding_mask)
         for lid, layer in enumerate(self.layers):
             if reference_points.shape[-1] == 2:
                 scale = torch.stack([src_valid_ratios, src_valid_ratios], -1)[:, None]
@@ -312,8 +321,12 @@ class DeformableTransformerDecoder(nn.Module):
             else:
                 assert reference_points.shape[-1] == 1
                 reference_points_input = reference_points[:, :, None] * src_valid_ratios[:, None, :, None]
-            output = layer(output, query_pos, reference_points_input, src, src_temporal_shapes,
-                           src_level_start_index, src_padding_mask, query_padding_mask)
+            if values is not None:
+                output = layer(output, query_pos, reference_points_input, src, src_temporal_shapes,
+                               src_level_start_index, src_padding_mask, query_padding_mask, value=values[lid])
+            else:
+                output = layer(output, query_pos, reference_points_input, src, src_temporal_shapes,
+                               src_level_start_index, src_padding_mask, query_padding_mask)
             if not disable_iterative_refine and self.bbox_head is not None:
                 delta = self.bbox_head[lid](output)
                 if reference_points.shape[-1] == 2:

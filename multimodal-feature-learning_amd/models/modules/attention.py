@@ -112,7 +112,7 @@ class MSDeformAttn(nn.Module):
         constant_(self.output_proj.bias.data, 0.)
 
     def forward(self, query, reference_points, input_flatten, input_spatial_shapes,
-                input_level_start_index, input_padding_mask=None, is_sparse=False):
+                input_level_start_index, input_padding_mask=None, is_sparse=False, value=None):
         """
         :param query                   (N, Len_q, C)
         :param reference_points        (N, Len_q, n_levels, 1) in [0, 1], or (N, Len_q, n_levels, 2) (centre, length)
@@ -120,6 +120,9 @@ class MSDeformAttn(nn.Module):
         :param input_spatial_shapes    (n_levels,) [T_0, ..., T_{L-1}]
         :param input_level_start_index (n_levels,)
         :param input_padding_mask      (N, sum_l T_l) bool, True = padding
+        :param value                   optional (N, sum_l T_l, C): this module's projected, padding-masked
+                                       value, already computed (the decoder computes every layer's at once,
+                                       models/modules/value_proj.py); input_flatten is then not projected
         :return output (N, Len_q, C)  [, sampling_locations (N,Len_q,M,L,P,1), attention_weights (N,Len_q,M,L,P)]
         """
         N, Len_q, _ = query.shape
@@ -127,9 +130,10 @@ class MSDeformAttn(nn.Module):
         shapes, starts = _msda.host_levels(input_spatial_shapes, input_level_start_index)
         assert sum(shapes) == Len_in  # attention.py:458, without the device sync
 
-        value = self.value_proj(input_flatten)
-        if input_padding_mask is not None:
-            value = mask_padding_rows(value, input_padding_mask)
+        if value is None:
+            value = self.value_proj(input_flatten)
+            if input_padding_mask is not None:
+                value = mask_padding_rows(value, input_padding_mask)
         value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
 
         # one input cast and one fused backward for the two query projections

@@ -53,6 +53,21 @@ def _bias_grad(g2):
     return out
 
 
+def _sum_slabs(part):
+    """part.sum(0) of the fp32 split-K partials (s, n_out, n_in) through mfl_sum_slabs (one pass,
+    chunk order)."""
+    n = part[0].numel()
+    if n % 4 or not part.is_contiguous():
+        return part.sum(0)
+    from ... import _native
+    lib = _native.load_library()
+    out = torch.empty(part.shape[1:], dtype=torch.float32, device=part.device)
+    rc = lib.mfl_sum_slabs(part.data_ptr(), part.shape[0], n, out.data_ptr(), _native.stream_handle(part.device))
+    if rc != 0:
+        raise RuntimeError("mfl_sum_slabs failed: " + lib.flat_adamw_last_error().decode())
+    return out
+
+
 def _weight_grad(g2, x2):
     """fp32 dW = dY^T X of 16-bit dY (K, N) and X (K, C): K split into chunks, one strided-batched
     GEMM with fp32 partial outputs, then their sum."""
@@ -62,7 +77,7 @@ def _weight_grad(g2, x2):
         part = torch.empty(s, n_out, n_in, device=g2.device, dtype=torch.float32)
         torch.baddbmm(part, g2.view(s, k // s, n_out).transpose(1, 2), x2.view(s, k // s, n_in),
                       beta=0, out_dtype=torch.float32, out=part)
-        return part.sum(0)
+        return _sum_slabs(part)
     return torch.mm(g2.t(), x2, out_dtype=torch.float32)
 
 

@@ -61,3 +61,51 @@ def test_module_with_padding_mask_uses_kernel(dev, monkeypatch):
     monkeypatch.setattr(ATT, "mask_padding_rows", lambda v, m: v.masked_fill(m[..., None], 0.0))
     out2 = attn(src, ref, src, ts, lsi, mask)
     torch.testing.assert_close(out, out2, rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("carried,padded", [(False, False), (True, True), (False, True)])
+def test_layer_values_match_per_layer_projections(dev, carried, padded):
+    """The decoder's value projections of all layers as one batched GEMM each way
+    (models/modules/value_proj.py) against each layer's own ``value_proj(src).masked_fill(...)``
+    (reference attention.py:461-463) under bf16 autocast: values to bf16 rounding of the same
+    fp32-accumulated product, gradients of src / weights / biases to bf16-GEMM tolerance."""
+    VP = PKG.models.modules.value_proj
+    torch.manual_seed(3)
+    n, B, S, C = 4, 2, 1920, 512
+    attns = [ATT.MSDeformAttn(C, 4, 8, 4).to(dev) for _ in range(n)]
+    for a in attns:
+        torch.nn.init.normal_(a.value_proj.bias, std=0.5)
+    src0 = torch.randn(B, S, C, device=dev)
+    mask = (torch.rand(B, S, device=dev) < 0.2) if padded else None
+    gs = [torch.randn(B, S, C, device=dev).bfloat16() for _ in range(n)]
+
+    def run(batched):
+        for a in attns:
+            a.zero_grad(set_to_none=True)
+        src = src0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            x = src
+            if carried:
+                x16 = src.bfloat16()
+                x = src * 1
+                x._mfl_bf16 = x16
+            if batched:
+                assert VP.layer_values_supported(attns, x, mask)
+                vals = VP.layer_values(attns, x, mask)
+            else:
+                vals = [a.value_proj(x) for a in attns]
+                if mask is not None:
+                    vals = [v.masked_fill(mask[..., None], 0.0) for v in vals]
+        sum((v.float() * g.float()).sum() for v, g in zip(vals, gs)).backward()
+        return vals, [src.grad] + [p.grad for a in attns for p in (a.value_proj.weight, a.value_proj.bias)]
+
+    v1, g1 = run(True)
+    v0, g0 = run(False)
+    for a, b in zip(v1, v0):
+        assert a.dtype == torch.bfloat16
+        torch.testing.assert_close(a.float(), b.float(), rtol=2 ** -7, atol=2 ** -7)
+        if mask is not None:
+            assert (a[mask] == 0).all()
+    for a, b in zip(g1, g0):
+        torch.testing.assert_close(a.float(), b.float(), rtol=2 ** -6, atol=2 ** -6 * b.abs().max().item())
