@@ -15,7 +15,7 @@ import torch
 from torch import nn
 from torch.autograd import Function
 
-__all__ = ["add_layer_norm", "add_layer_norm_carry"]
+__all__ = ["add_layer_norm", "add_layer_norm_carry", "seed_pool"]
 
 _TAGS = {torch.float32: 0, torch.bfloat16: 2}
 
@@ -24,11 +24,47 @@ def _ptr(t):
     return t.data_ptr() if t is not None else None
 
 
+class _SeedPool:
+    """Dropout seeds for one step drawn in blocks: inside ``seed_pool(device)`` (the training step
+    opens it around its forward) the fused kernels' seeds are consecutive elements of device
+    tensors of ``block`` seeds, each drawn by ONE kernel, instead of one random kernel per dropout
+    site (42 a step in the bench's 6 + 6 layers).  The pool starts empty on entry, so every
+    seed used inside a captured graph is drawn inside it (fresh on every replay)."""
+    active = None
+
+    def __init__(self, device, block=64):
+        self.device, self.block, self.buf, self.i = device, block, None, 0
+
+    def take(self):
+        if self.buf is None or self.i >= self.block:
+            self.buf = torch.randint(0, 2 ** 62, (self.block,), device=self.device, dtype=torch.int64)
+            self.i = 0
+        self.i += 1
+        return self.buf[self.i - 1:self.i]
+
+
+class seed_pool:  # noqa: N801  (a context manager, used like a function)
+    def __init__(self, device, block=64):
+        self.pool = _SeedPool(torch.device(device), block)
+
+    def __enter__(self):
+        self.prev, _SeedPool.active = _SeedPool.active, self.pool
+        return self.pool
+
+    def __exit__(self, *exc):
+        _SeedPool.active = self.prev
+        return False
+
+
 def _drop_args(dropout, device):
     """(p, seed tensor) of an active nn.Dropout, else (0.0, None).  The seed is drawn on the device
-    from torch's generator (graph-capture safe: a fresh value on every replay) and kept for the
-    backward, which regenerates the keep bits from it."""
+    from torch's generator (graph-capture safe: a fresh value on every replay; from the step's
+    seed pool when one is open) and kept for the backward, which regenerates the keep bits
+    from it."""
     if isinstance(dropout, nn.Dropout) and dropout.training and dropout.p > 0:
+        pool = _SeedPool.active
+        if pool is not None and pool.device == device:
+            return float(dropout.p), pool.take()
         return float(dropout.p), torch.randint(0, 2 ** 62, (1,), device=device, dtype=torch.int64)
     return 0.0, None
 

@@ -34,6 +34,7 @@ the MI355X the way the hardware wants it:
 import torch
 import torch.distributed as dist
 
+from .models.modules.add_norm import seed_pool
 from .models.modules.linear import Linear
 
 __all__ = ["FlatGradTrainer"]
@@ -238,7 +239,7 @@ class FlatGradTrainer:
         for p in self.params:  # autograd then hands over fresh gradients (no accumulate kernels)
             p.grad = None
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_bf16,
-                            cache_enabled=cache_casts):
+                            cache_enabled=cache_casts), seed_pool(self.device):
             out = self.model(*batch)
             loss = self.loss_fn(out)
         self._pending = [len(idx) for _, _, idx in self.buckets]
