@@ -27,7 +27,7 @@ from torch.nn.init import constant_, xavier_uniform_
 from ... import msda as _msda
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
-from .linear import Linear, linear_pair
+from .linear import Linear, _AutocastLinear, _bias_grad, _weight_grad, linear_pair
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
            "masked_scores_softmax", "mask_padding_rows", "mha_self_attention"]
@@ -232,13 +232,65 @@ def mha_self_attention(mha, tgt, query_pos, query_mask):
     H = mha.num_heads
     hd = E // H
     w, b = mha.in_proj_weight, mha.in_proj_bias
-    qk = F.linear(tgt if query_pos is None else tgt + query_pos, w[:2 * E], b[:2 * E])
+    x_qk = tgt if query_pos is None else tgt + query_pos
+    if (tgt.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and w.dtype == torch.float32 and mha.out_proj.bias is not None):
+        # the projections as the autocast Linear's: bf16 weights from the trainer's shadow, fp32
+        # weight / bias gradients straight from the GEMMs (no per-use casts, no slice-gradient adds)
+        sh = getattr(mha, "_mfl_shadow", None)
+        ok = sh is not None and sh[4] == w._version and sh[5] == mha.out_proj.weight._version
+        with torch.autocast("cuda", enabled=False):
+            qk, v = _InProjection.apply(x_qk.to(torch.bfloat16), tgt.to(torch.bfloat16), w, b,
+                                        sh[0] if ok else None, sh[1] if ok else None)
+            q, k = qk.view(B, L, 2, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
+            v = v.view(B, L, H, hd).transpose(1, 2)
+            out = F.scaled_dot_product_attention(q, k, v, attn_mask=query_mask[:, None, None, :],
+                                                 dropout_p=mha.dropout if mha.training else 0.0)
+            return _AutocastLinear.apply(out.transpose(1, 2).reshape(B, L, E), mha.out_proj.weight,
+                                         mha.out_proj.bias, sh[2] if ok else None, sh[3] if ok else None)
+    qk = F.linear(x_qk, w[:2 * E], b[:2 * E])
     v = F.linear(tgt, w[2 * E:], b[2 * E:])
     q, k = qk.view(B, L, 2, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
     v = v.view(B, L, H, hd).transpose(1, 2)
     out = F.scaled_dot_product_attention(q, k, v, attn_mask=query_mask[:, None, None, :],
                                          dropout_p=mha.dropout if mha.training else 0.0)
     return F.linear(out.transpose(1, 2).reshape(B, L, E), mha.out_proj.weight, mha.out_proj.bias)
+
+
+class _InProjection(torch.autograd.Function):
+    """(x_qk W_qk^T + b_qk, x_v W_v^T + b_v) with W = in_proj_weight (3E, E) split [q; k | v]: two
+    bf16 GEMMs forward; backward two dgrad GEMMs and ONE fp32 (3E, E) weight gradient / (3E,)
+    bias gradient (no slice gradients to add)."""
+
+    @staticmethod
+    def forward(ctx, x_qk, x_v, w, b, wc, bc):
+        dt = x_qk.dtype
+        wc = w.to(dt) if wc is None else wc
+        bc = b.to(dt) if bc is None else bc
+        e = w.shape[1]
+        a2, v2 = x_qk.reshape(-1, e), x_v.reshape(-1, e)
+        qk = torch.addmm(bc[:2 * e], a2, wc[:2 * e].t())
+        v = torch.addmm(bc[2 * e:], v2, wc[2 * e:].t())
+        ctx.save_for_backward(a2, v2, wc)
+        ctx.shape = x_qk.shape
+        lead = x_qk.shape[:-1]
+        return (torch.ops.aten._unsafe_view(qk, (*lead, 2 * e)), torch.ops.aten._unsafe_view(v, (*lead, e)))
+
+    @staticmethod
+    def backward(ctx, gqk, gv):
+        a2, v2, wc = ctx.saved_tensors
+        e = wc.shape[1]
+        gqk = gqk.reshape(-1, 2 * e).to(wc.dtype)
+        gv = gv.reshape(-1, e).to(wc.dtype)
+        nig = ctx.needs_input_grad
+        dqk = torch.mm(gqk, wc[:2 * e]).view(ctx.shape) if nig[0] else None
+        dv = torch.mm(gv, wc[2 * e:]).view(ctx.shape) if nig[1] else None
+        dw = db = None
+        if nig[2]:
+            dw = torch.cat((_weight_grad(gqk, a2), _weight_grad(gv, v2)), 0)
+        if nig[3]:
+            db = torch.cat((_bias_grad(gqk), _bias_grad(gv)), 0)
+        return dqk, dv, dw, db, None, None
 
 
 def masked_scores_softmax(scores, masked, scale, neg_fill=-1e20):

@@ -72,6 +72,7 @@ class FlatGradTrainer:
         # bf16 weight shadow for the autocast Linear layers (one cast per step, _refresh_shadow)
         self.flat_bf16 = None
         self._linears = []
+        self._mhas = []
         self.handover = handover
         if use_bf16 and dev.type == "cuda" and shadow:
             self.flat_bf16 = self.flat_param.to(torch.bfloat16)
@@ -82,6 +83,13 @@ class FlatGradTrainer:
                     if mod.bias is not None and b is None:
                         continue
                     self._linears.append((mod, index[id(mod.weight)], b))
+                elif (isinstance(mod, torch.nn.MultiheadAttention) and mod.in_proj_weight is not None
+                      and id(mod.in_proj_weight) in index and mod.in_proj_bias is not None
+                      and id(mod.in_proj_bias) in index and id(mod.out_proj.weight) in index
+                      and mod.out_proj.bias is not None and id(mod.out_proj.bias) in index):
+                    # the decoder's query self-attention (attention.py::mha_self_attention) reads these
+                    self._mhas.append((mod, index[id(mod.in_proj_weight)], index[id(mod.in_proj_bias)],
+                                       index[id(mod.out_proj.weight)], index[id(mod.out_proj.bias)]))
             self._refresh_shadow()
         self.betas, self.eps = betas, eps
         self.fused = (dev.type == "cuda") if fused_optimizer is None else bool(fused_optimizer)
@@ -115,6 +123,11 @@ class FlatGradTrainer:
         self._pending = None
         self._overlap_now = self.overlap  # eager steps; capture() decides for the graph
         self._fb_reduces = False          # the captured fwd+bwd graph all-reduces the buckets
+        # parameters that never receive a gradient (found on the first step) are left untouched, as
+        # torch AdamW leaves a parameter whose grad is None (reference DDP find_unused_parameters)
+        self._got = [False] * len(self.params)
+        self._unused = None
+        self._frozen = None
         self._bucket_of = {}
         for bi, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
@@ -160,6 +173,9 @@ class FlatGradTrainer:
 
     def _flush_bucket(self, b):
         start, end, idx = self.buckets[b]
+        for i in idx:
+            if self.params[i].grad is not None:
+                self._got[i] = True
         got = [(self.grad_views[i], self.params[i].grad) for i in idx if self.params[i].grad is not None]
         missing = [self.grad_views[i] for i in idx if self.params[i].grad is None]
         if got:
@@ -227,6 +243,8 @@ class FlatGradTrainer:
             self.flat_bf16.copy_(self.flat_param)
         for mod, w, b in self._linears:
             mod.set_bf16_shadow(w, b)
+        for mod, w, b, ow, ob in self._mhas:
+            mod._mfl_shadow = (w, b, ow, ob, mod.in_proj_weight._version, mod.out_proj.weight._version)
 
     def _forward_backward(self, batch, cache_casts=True):
         if not self.handover:  # accumulate into the zeroed flat buffer (one add kernel per parameter)
@@ -260,7 +278,34 @@ class FlatGradTrainer:
             self._works = []
             self.flat_grad.div_(self.world)
         self._attach_grads()
+        if self._unused is None and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
+            self._find_unused()
+        if self._unused and self.opt is not None:
+            for i in self._unused:  # torch AdamW skips a parameter whose grad is None
+                self.params[i].grad = None
         return loss.detach()
+
+    def _find_unused(self):
+        """After the first backward: the parameters no rank gave a gradient.  The fused update then
+        restores their values, moments and bf16 shadow after every step (a few small copies,
+        captured with the update graph), so weight decay never touches them."""
+        got = torch.tensor([1 if g else 0 for g in self._got], dtype=torch.int32, device=self.device)
+        if self.world > 1:
+            dist.all_reduce(got, op=dist.ReduceOp.MAX, group=self.pg)
+        self._unused = [i for i, g in enumerate(got.tolist()) if g == 0]
+        if not self._unused or self.opt is not None:
+            return
+        views = []
+        flats = [self.flat_param, self.exp_avg, self.exp_avg_sq] + ([self.flat_bf16] if self.flat_bf16 is not None
+                                                                     else [])
+        offs, off = [], 0
+        for p in self.params:
+            offs.append(off)
+            off += p.numel()
+        for i in self._unused:
+            n = self.params[i].numel()
+            views.extend(f[offs[i]:offs[i] + n] for f in flats)
+        self._frozen = (views, [v.clone() for v in views])
 
     def _allreduce(self):
         if self.world > 1 and not self._overlap_now:
@@ -282,6 +327,8 @@ class FlatGradTrainer:
             _native.stream_handle(self.device))
         if rc != 0:
             raise RuntimeError("flat_adamw_step failed: " + self._lib.flat_adamw_last_error().decode())
+        if self._frozen is not None:  # parameters without gradients: values, moments, shadow unchanged
+            torch._foreach_copy_(self._frozen[0], self._frozen[1])
         self._refresh_shadow(copy=False)
 
     # --- public -------------------------------------------------------------------------

@@ -109,3 +109,33 @@ def test_layer_values_match_per_layer_projections(dev, carried, padded):
             assert (a[mask] == 0).all()
     for a, b in zip(g1, g0):
         torch.testing.assert_close(a.float(), b.float(), rtol=2 ** -6, atol=2 ** -6 * b.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_mha_self_attention_autocast_matches_module(dev):
+    """The decoder's query self-attention under bf16 autocast (SDPA + the autocast-Linear
+    projections, attention.py::mha_self_attention) against nn.MultiheadAttention's own call
+    (reference unimodal_deformable_transformer.py:352-353) under the same autocast: output and
+    gradients of the input, in_proj and out_proj to bf16 tolerance."""
+    torch.manual_seed(4)
+    mha = torch.nn.MultiheadAttention(512, 8, dropout=0.0).to(dev)
+    tgt0 = torch.randn(8, 100, 512, device=dev)
+    pos = torch.randn(8, 100, 512, device=dev)
+    qmask = torch.ones(8, 100, dtype=torch.bool, device=dev)
+    qmask[3, 90:] = False
+    g = torch.randn(8, 100, 512, device=dev)
+
+    def run(mine):
+        mha.zero_grad(set_to_none=True)
+        tgt = tgt0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            if mine:
+                out = ATT.mha_self_attention(mha, tgt, pos, qmask)
+            else:
+                qk = (tgt + pos).transpose(0, 1)
+                out = mha(qk, qk, tgt.transpose(0, 1), key_padding_mask=~qmask)[0].transpose(0, 1)
+        (out.float() * g).sum().backward()
+        return [out.float(), tgt.grad] + [p.grad.float() for p in mha.parameters()]
+
+    for a, b in zip(run(True), run(False)):
+        torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())

@@ -358,3 +358,47 @@ def test_rccl_one_rank_bucketed_allreduce_smoke(dev):
     torch.testing.assert_close(r["overlap"], r["plain"], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(r["graph"], r["graph_eager"], rtol=1e-4, atol=1e-5)
     assert r["graph_reduces"]
+
+
+def test_parameters_without_gradients_are_left_untouched():
+    """MultimodalDVCCore has parameters the forward never uses (pos_trans / pos_trans_norm, as the
+    reference's multimodal transformer): the reference's AdamW skips them (grad None, DDP
+    find_unused_parameters); the trainer leaves their values alone as well — no weight decay."""
+    from oracle.cpu_model import oracle_core
+    torch.manual_seed(0)
+    model = PKG.dvc_core.MultimodalDVCCore(**{k: v for k, v in SMALL.items() if k != "num_classes"})
+    v = PKG.dvc_core.synthetic_clips(1, T=32, feature_dim=64, seed=1)
+    a = PKG.dvc_core.synthetic_clips(1, T=16, feature_dim=64, seed=2)
+    before = _params(model)
+    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.multimodal_workload_loss, lr=1e-2, weight_decay=0.5,
+                                        use_bf16=False, graph=False)
+    with oracle_core(PKG):
+        for _ in range(2):
+            tr.eager_step((v[0], v[1], a[0], a[1], v[2]))
+    after = _params(model)
+    unused = [k for k in before if "pos_trans" in k]
+    assert unused and len(tr._unused) == len(unused)
+    for k in unused:
+        torch.testing.assert_close(after[k], before[k], rtol=0, atol=0, msg=k)
+    assert any(not torch.equal(after[k], before[k]) for k in before if k not in unused)
+
+
+@pytest.mark.gpu
+def test_fused_update_leaves_unused_parameters_untouched(dev):
+    torch.manual_seed(0)
+    model = PKG.dvc_core.MultimodalDVCCore(**{k: v for k, v in SMALL.items() if k != "num_classes"}).to(dev)
+    v = PKG.dvc_core.synthetic_clips(2, T=32, feature_dim=64, seed=1, device=dev)
+    a = PKG.dvc_core.synthetic_clips(2, T=16, feature_dim=64, seed=2, device=dev)
+    before = _params(model)
+    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.multimodal_workload_loss, lr=1e-2, weight_decay=0.5,
+                                        use_bf16=True, graph=True)
+    batch = (v[0], v[1], a[0], a[1], v[2])
+    tr.capture(batch, warmup=2)
+    for _ in range(2):
+        tr.step(batch)
+    torch.cuda.synchronize()
+    after = _params(model)
+    unused = [k for k in before if "pos_trans" in k]
+    assert unused
+    for k in unused:
+        torch.testing.assert_close(after[k], before[k], rtol=0, atol=0, msg=k)
