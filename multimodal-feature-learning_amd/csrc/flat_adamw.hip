@@ -216,6 +216,41 @@ __global__ __launch_bounds__(kColRows * kColLanes) void colsum_partial(const T* 
   }
 }
 
+// Short K (the decoder's 800-token Linear layers): one pass, no partials.  A block owns a strip of
+// kColLanes * V columns and all K rows: kColRows * 4 row lanes stride through the rows, then the
+// row lanes are summed in LDS in a fixed order (deterministic).
+constexpr int kSmallRowLanes = 32;
+template <typename T>
+__global__ __launch_bounds__(kSmallRowLanes * 8) void colsum_small(const T* __restrict__ x, long long K, int N,
+                                                                   float* __restrict__ out) {
+  constexpr int V = 16 / sizeof(T);
+  constexpr int CL = 8;  // 16-byte column lanes per block
+  __shared__ float red[kSmallRowLanes][CL * V];
+  const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
+  const int c0 = (blockIdx.x * CL + cl) * V;
+  float acc[V];
+#pragma unroll
+  for (int i = 0; i < V; ++i) acc[i] = 0.f;
+  if (c0 < N) {
+    for (long long r = rl; r < K; r += kSmallRowLanes) {
+      float f[V];
+      cvt16<T>(*reinterpret_cast<const uint4*>(x + r * N + c0), f);
+#pragma unroll
+      for (int i = 0; i < V; ++i) acc[i] += f[i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < V; ++i) red[rl][cl * V + i] = acc[i];
+  __syncthreads();
+  for (int c = threadIdx.x; c < CL * V; c += kSmallRowLanes * 8) {
+    float t = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < kSmallRowLanes; ++r) t += red[r][c];
+    const int col = blockIdx.x * CL * V + c;
+    if (col < N) out[col] = t;
+  }
+}
+
 // out[c] = sum over chunks of part[k][c]: 16 chunk groups x 64 columns per 1024-thread block,
 // each thread a strided quarter-unrolled run over its chunks, then an LDS reduction over the
 // groups (fixed order: deterministic).
@@ -345,9 +380,22 @@ int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void*
   if (K == 0) {
     return zero_f32(out, N, st) == hipSuccess ? 0 : 2;
   }
+  const int V = 16 / elt;
+  if (K <= 4096) {  // one pass: at most 128 rows per row lane
+    const dim3 g1((unsigned)((N / V + 7) / 8));
+    if (dtype == 0)
+      hipLaunchKernelGGL(colsum_small<float>, g1, dim3(kSmallRowLanes * 8), 0, st, static_cast<const float*>(x),
+                         (long long)K, (int)N, out);
+    else if (dtype == 2)
+      hipLaunchKernelGGL(colsum_small<uint16_t>, g1, dim3(kSmallRowLanes * 8), 0, st,
+                         static_cast<const uint16_t*>(x), (long long)K, (int)N, out);
+    else
+      hipLaunchKernelGGL(colsum_small<_Float16>, g1, dim3(kSmallRowLanes * 8), 0, st,
+                         static_cast<const _Float16*>(x), (long long)K, (int)N, out);
+    return status("colsum small");
+  }
   const long long chunks = std::min<long long>(256, std::max<long long>(1, (K + 63) / 64));
   const int rows_per_chunk = (int)((K + chunks - 1) / chunks);
-  const int V = 16 / elt;
   const dim3 grid((unsigned)((N / V + kColLanes - 1) / kColLanes), (unsigned)chunks);
   auto* part = static_cast<float*>(workspace);
   if (dtype == 0)

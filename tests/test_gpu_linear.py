@@ -92,9 +92,12 @@ def test_bf16_shadow_is_bitwise_the_cast_and_expires(dev):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K,N,dtype", [(15360, 512, torch.bfloat16), (800, 128, torch.bfloat16),
-                                       (15360, 2048, torch.float16), (37, 8, torch.bfloat16), (0, 64, torch.bfloat16)])
+                                       (15360, 2048, torch.float16), (37, 8, torch.bfloat16), (0, 64, torch.bfloat16),
+                                       (4096, 1536, torch.bfloat16), (4097, 512, torch.bfloat16),
+                                       (801, 3072, torch.float16)])
 def test_bias_grad_column_sum(dev, K, N, dtype):
-    """mfl_colsum (the Linear's bias gradient): fp32 column sums of a 16-bit (K, N) matrix vs fp64."""
+    """mfl_colsum (the Linear's bias gradient): fp32 column sums of a 16-bit (K, N) matrix vs fp64
+    (K <= 4096: the one-pass kernel; longer K: partials + final)."""
     g = torch.randn(K, N, device=dev).to(dtype)
     out = linear_mod._bias_grad(g)
     ref = g.double().sum(0)
