@@ -1794,6 +1794,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
       const int li_lo = wlo < whi ? row_of(wlo) + 1 : 1, li_hi = wlo < whi ? row_of(whi - 1) + 1 : 0;
       for (int s0 = threadIdx.x; s0 < nsamp; s0 += kGvThreads * kGvCache) {
         float lcv[kGvCache], acv[kGvCache];
+        int psv[kGvCache];
 #pragma unroll
         for (int k = 0; k < kGvCache; ++k) {  // unconditional loads (clamped index): all in flight
           const int s = min(s0 + k * kGvThreads, nsamp - 1);
@@ -1801,6 +1802,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
           const long long o = q * qs + p;
           lcv[k] = locb[o];
           acv[k] = awb[o];
+          psv[k] = POS(s);  // beside loc / aw: the dot gather below then waits on one load, not two
         }
 #pragma unroll
         for (int k = 0; k < kGvCache; ++k) {
@@ -1811,7 +1813,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
             if (li >= li_lo && li <= li_hi) {
               const int q = s / P, p = s - q * P;
               const long long o = q * qs + p;
-              const f32x2 d = ECC(POS(s));
+              const f32x2 d = ECC(psv[k]);
               if (gab != nullptr) gab[o] = d.x * t.w0 + d.y * t.w1;
               if (glb != nullptr) glb[o] = ((d.y - d.x) * acv[k]) * t.gmul;
             }
