@@ -24,6 +24,11 @@ thread_local char g_err[256];
 
 constexpr int kWaves = 4;     // rows in flight per block (one per wave)
 constexpr int kBwdRows = 16;  // rows per backward block (kWaves waves x 4 rows): gamma/beta partials
+// Short calls (the decoder's 800 query rows) take one row per wave instead: 16-row blocks gave them
+// 50 workgroups, each wave walking 4 dependent rows (14 us per call); 4-row blocks give 200.
+constexpr int kBwdRowsShort = 4;
+constexpr long long kBwdShortMax = 4096;
+inline int bwd_rows_per_block(long long rows) { return rows <= kBwdShortMax ? kBwdRowsShort : kBwdRows; }
 
 template <typename T> struct Vec4;
 template <> struct Vec4<float> {
@@ -167,7 +172,7 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__
   }
 }
 
-template <typename RT, typename YT, int CH>
+template <typename RT, typename YT, int CH, int RPB>
 __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
     const float* __restrict__ dout, const RT* __restrict__ r, const YT* __restrict__ y,
     const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
@@ -181,8 +186,8 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
   for (int c = 0; c < CH; ++c)
 #pragma unroll
     for (int k = 0; k < 4; ++k) dg[c][k] = db[c][k] = 0.f;
-  for (int i = 0; i < kBwdRows / kWaves; ++i) {
-    const long long row = (long long)blockIdx.x * kBwdRows + i * kWaves + wave;
+  for (int i = 0; i < RPB / kWaves; ++i) {
+    const long long row = (long long)blockIdx.x * RPB + i * kWaves + wave;
     if (row >= rows) break;  // wave-uniform
     const long long base = row * d;
     const float mean = mean_in[row], rstd = rstd_in[row];
@@ -320,15 +325,20 @@ int fwd(const void* r, const void* y, const float* gamma, const float* beta, int
 }
 #undef MFL_ALN_FWD
 
-#define MFL_ALN_BWD(CHN)                                                                                   \
-  hipLaunchKernelGGL((add_ln_bwd<RT, YT, CHN>), dim3(blocks), dim3(kWaves * 64), 0, st, dout, rp, yp, gamma, \
+#define MFL_ALN_BWD_R(CHN, R)                                                                              \
+  hipLaunchKernelGGL((add_ln_bwd<RT, YT, CHN, R>), dim3(blocks), dim3(kWaves * 64), 0, st, dout, rp, yp, gamma, \
                      mean, rstd, (long long)rows, (int)d, drp, dyp, part, dout16, dq16, dpos, drop)
+#define MFL_ALN_BWD(CHN)                                                                                   \
+  do {                                                                                                     \
+    if (rpb == kBwdRowsShort) MFL_ALN_BWD_R(CHN, kBwdRowsShort); else MFL_ALN_BWD_R(CHN, kBwdRows);        \
+  } while (0)
 
 template <typename RT, typename YT>
 int bwd(const float* dout, const void* r, const void* y, const float* gamma, const float* mean, const float* rstd,
         int64_t rows, int64_t d, void* dr, void* dy, float* dgamma, float* dbeta, void* workspace,
         const uint16_t* dout16, const uint16_t* dq16, float* dpos, Drop drop, hipStream_t st) {
-  const unsigned blocks = (unsigned)((rows + kBwdRows - 1) / kBwdRows);
+  const int rpb = bwd_rows_per_block(rows);
+  const unsigned blocks = (unsigned)((rows + rpb - 1) / rpb);
   auto* rp = static_cast<const RT*>(r);
   auto* yp = static_cast<const YT*>(y);
   auto* drp = static_cast<RT*>(dr);
@@ -348,6 +358,7 @@ int bwd(const float* dout, const void* r, const void* y, const float* gamma, con
   return status("backward params");
 }
 #undef MFL_ALN_BWD
+#undef MFL_ALN_BWD_R
 
 // Zero fill as a kernel, not hipMemsetAsync: under the HIP runtime's graph packet capture a
 // captured memset node did not take effect on replays that followed eager work
@@ -370,7 +381,8 @@ extern "C" {
 
 size_t mfl_add_layernorm_workspace_bytes(int64_t rows, int64_t d) {
   if (rows <= 0 || d <= 0) return 0;
-  return (size_t)((rows + kBwdRows - 1) / kBwdRows) * 2 * (size_t)d * sizeof(float);
+  const int rpb = bwd_rows_per_block(rows);
+  return (size_t)((rows + rpb - 1) / rpb) * 2 * (size_t)d * sizeof(float);
 }
 
 int mfl_add_layernorm_forward_ex(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,

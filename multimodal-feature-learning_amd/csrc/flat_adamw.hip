@@ -216,23 +216,27 @@ __global__ __launch_bounds__(kColRows * kColLanes) void colsum_partial(const T* 
   }
 }
 
-// Short K (the decoder's 800-token Linear layers): one pass, no partials.  A block owns a strip of
-// kColLanes * V columns and all K rows: kColRows * 4 row lanes stride through the rows, then the
-// row lanes are summed in LDS in a fixed order (deterministic).
-constexpr int kSmallRowLanes = 32;
+// Short K (the decoder's 800-token Linear layers): one pass, no partials.  A 256-thread block owns
+// a strip of 2 x 16-byte column lanes and all K rows (128 row lanes stride through them); the row
+// lanes are then summed in LDS in two fixed-order stages (deterministic).  Narrow strips give
+// N / 16 workgroups for bf16 (32 at N = 512): wide ones left this latency-bound on 8 CUs.
+constexpr int kSmallCL = 2;     // 16-byte column lanes per block
+constexpr int kSmallRL = 128;   // row lanes per block
 template <typename T>
-__global__ __launch_bounds__(kSmallRowLanes * 8) void colsum_small(const T* __restrict__ x, long long K, int N,
+__global__ __launch_bounds__(kSmallCL * kSmallRL) void colsum_small(const T* __restrict__ x, long long K, int N,
                                                                    float* __restrict__ out) {
   constexpr int V = 16 / sizeof(T);
-  constexpr int CL = 8;  // 16-byte column lanes per block
-  __shared__ float red[kSmallRowLanes][CL * V];
-  const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
-  const int c0 = (blockIdx.x * CL + cl) * V;
+  constexpr int C = kSmallCL * V;                 // columns per block
+  constexpr int G = kSmallCL * kSmallRL / C;      // row groups of stage 2
+  __shared__ float red[kSmallRL][C];
+  __shared__ float red2[G][C];
+  const int cl = threadIdx.x % kSmallCL, rl = threadIdx.x / kSmallCL;
+  const int c0 = (blockIdx.x * kSmallCL + cl) * V;
   float acc[V];
 #pragma unroll
   for (int i = 0; i < V; ++i) acc[i] = 0.f;
   if (c0 < N) {
-    for (long long r = rl; r < K; r += kSmallRowLanes) {
+    for (long long r = rl; r < K; r += kSmallRL) {
       float f[V];
       cvt16<T>(*reinterpret_cast<const uint4*>(x + r * N + c0), f);
 #pragma unroll
@@ -242,11 +246,19 @@ __global__ __launch_bounds__(kSmallRowLanes * 8) void colsum_small(const T* __re
 #pragma unroll
   for (int i = 0; i < V; ++i) red[rl][cl * V + i] = acc[i];
   __syncthreads();
-  for (int c = threadIdx.x; c < CL * V; c += kSmallRowLanes * 8) {
+  {
+    const int c = threadIdx.x % C, g = threadIdx.x / C;
     float t = 0.f;
-#pragma unroll 8
-    for (int r = 0; r < kSmallRowLanes; ++r) t += red[r][c];
-    const int col = blockIdx.x * CL * V + c;
+#pragma unroll
+    for (int r = 0; r < kSmallRL / G; ++r) t += red[g * (kSmallRL / G) + r][c];
+    red2[g][c] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < C) {
+    float t = 0.f;
+#pragma unroll
+    for (int g = 0; g < G; ++g) t += red2[g][threadIdx.x];
+    const int col = blockIdx.x * C + threadIdx.x;
     if (col < N) out[col] = t;
   }
 }
@@ -382,15 +394,15 @@ int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void*
   }
   const int V = 16 / elt;
   if (K <= 4096) {  // one pass: at most 128 rows per row lane
-    const dim3 g1((unsigned)((N / V + 7) / 8));
+    const dim3 g1((unsigned)((N / V + kSmallCL - 1) / kSmallCL));
     if (dtype == 0)
-      hipLaunchKernelGGL(colsum_small<float>, g1, dim3(kSmallRowLanes * 8), 0, st, static_cast<const float*>(x),
+      hipLaunchKernelGGL(colsum_small<float>, g1, dim3(kSmallCL * kSmallRL), 0, st, static_cast<const float*>(x),
                          (long long)K, (int)N, out);
     else if (dtype == 2)
-      hipLaunchKernelGGL(colsum_small<uint16_t>, g1, dim3(kSmallRowLanes * 8), 0, st,
+      hipLaunchKernelGGL(colsum_small<uint16_t>, g1, dim3(kSmallCL * kSmallRL), 0, st,
                          static_cast<const uint16_t*>(x), (long long)K, (int)N, out);
     else
-      hipLaunchKernelGGL(colsum_small<_Float16>, g1, dim3(kSmallRowLanes * 8), 0, st,
+      hipLaunchKernelGGL(colsum_small<_Float16>, g1, dim3(kSmallCL * kSmallRL), 0, st,
                          static_cast<const _Float16*>(x), (long long)K, (int)N, out);
     return status("colsum small");
   }

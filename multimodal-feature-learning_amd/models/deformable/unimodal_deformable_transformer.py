@@ -273,7 +273,15 @@ class DeformableTransformerDecoderLayer(nn.Module):
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
                 src_padding_mask=None, query_mask=None, value=None):
         """``value``: this layer's cross-attention value, when the decoder computed it (value_proj.py)."""
-        sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask)
+        return self.forward_carry(tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
+                                  src_padding_mask, query_mask, value)[0]
+
+    def forward_carry(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
+                      src_padding_mask=None, query_mask=None, value=None, carried=None):
+        """``forward`` returning ``(out, out16, q16)``: under bf16 autocast on the GPU the last fused add +
+        LayerNorm also writes bf16(out) and bf16(out + query_pos), the next layer's self-attention
+        inputs (``carried``); (out, None, None) otherwise."""
+        sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask, carried)
         if carry_supported(tgt, self.norm2) and (query_pos is None or query_pos.shape == tgt.shape):
             # bf16(tgt + query_pos) for the cross-attention query and bf16(tgt) for linear1 straight
             # from the fused add + LayerNorms (no pos add, no casts, no gradient accumulation)
@@ -282,12 +290,13 @@ class DeformableTransformerDecoderLayer(nn.Module):
                                  level_start_index, src_padding_mask, value=value)
             tgt, tgt16, _ = add_layer_norm_carry(tgt, ca, self.norm1, dropout=self.dropout1)
             hidden = relu_dropout(self.linear1(tgt16), self.activation, self.dropout3)
-            return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
+            out, out16, q16 = add_layer_norm_carry(tgt, self.linear2(hidden), self.norm3, query_pos, self.dropout4)
+            return out, out16, q16
         tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         ca = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_temporal_shapes,
                              level_start_index, src_padding_mask, value=value)
         tgt = add_layer_norm(tgt, ca, self.norm1, dropout=self.dropout1)
-        return self.forward_ffn(tgt)
+        return self.forward_ffn(tgt), None, None
 
 
 class DeformableTransformerDecoder(nn.Module):
@@ -314,6 +323,7 @@ class DeformableTransformerDecoder(nn.Module):
                 and layer_values_supported(attns, src, src_padding_mask)):
             # every layer projects the same memory: one batched GEMM each way (value_proj.py)
             values = layer_values(attns, src, src_padding_mask)
+        carried = None
         for lid, layer in enumerate(self.layers):
             if reference_points.shape[-1] == 2:
                 scale = torch.stack([src_valid_ratios, src_valid_ratios], -1)[:, None]
@@ -321,7 +331,13 @@ class DeformableTransformerDecoder(nn.Module):
             else:
                 assert reference_points.shape[-1] == 1
                 reference_points_input = reference_points[:, :, None] * src_valid_ratios[:, None, :, None]
-            if values is not None:
+            if type(layer) is DeformableTransformerDecoderLayer:
+                # bf16 self-attention inputs carried from the previous layer's last add + LayerNorm
+                output, out16, q16 = layer.forward_carry(
+                    output, query_pos, reference_points_input, src, src_temporal_shapes, src_level_start_index,
+                    src_padding_mask, query_padding_mask, values[lid] if values is not None else None, carried)
+                carried = (out16, q16)
+            elif values is not None:
                 output = layer(output, query_pos, reference_points_input, src, src_temporal_shapes,
                                src_level_start_index, src_padding_mask, query_padding_mask, value=values[lid])
             else:

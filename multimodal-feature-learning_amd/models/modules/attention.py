@@ -215,7 +215,7 @@ def mask_padding_rows(value, mask):
     return value.masked_fill(mask[..., None], float(0))
 
 
-def mha_self_attention(mha, tgt, query_pos, query_mask):
+def mha_self_attention(mha, tgt, query_pos, query_mask, carried=None):
     """The decoder's query self-attention, batch first:
     ``mha((tgt + pos)^T, (tgt + pos)^T, tgt^T, key_padding_mask=~query_mask)[0]^T`` (reference
     unimodal_deformable_transformer.py:352-353 and the multimodal / sparse decoders) with the
@@ -223,7 +223,9 @@ def mha_self_attention(mha, tgt, query_pos, query_mask):
     are unchanged).  The reference discards the attention weights it asks for, so the product runs
     as one ``F.scaled_dot_product_attention`` (dropout on the attention probabilities as the
     module's) instead of bmm / softmax / dropout / bmm and the sequence-first transposes.
-    tgt, query_pos (B, L, E); query_mask (B, L) bool, True = a real query."""
+    tgt, query_pos (B, L, E); query_mask (B, L) bool, True = a real query.  ``carried``: optional
+    ``(bf16(tgt), bf16(tgt + query_pos))`` written by the previous layer's fused add + LayerNorm (the
+    same values this function would cast; their gradients flow back into that kernel)."""
     if (mha.batch_first or not mha._qkv_same_embed_dim or mha.bias_k is not None or mha.add_zero_attn
             or mha.in_proj_bias is None or (query_pos is not None and query_pos.shape != tgt.shape)):
         qk = (tgt if query_pos is None else tgt + query_pos).transpose(0, 1)
@@ -239,9 +241,13 @@ def mha_self_attention(mha, tgt, query_pos, query_mask):
         # weight / bias gradients straight from the GEMMs (no per-use casts, no slice-gradient adds)
         sh = getattr(mha, "_mfl_shadow", None)
         ok = sh is not None and sh[4] == w._version and sh[5] == mha.out_proj.weight._version
+        if (carried is not None and carried[0] is not None and carried[1] is not None
+                and carried[0].dtype == carried[1].dtype == torch.bfloat16):
+            v16, qk16 = carried
+        else:
+            qk16, v16 = x_qk.to(torch.bfloat16), tgt.to(torch.bfloat16)
         with torch.autocast("cuda", enabled=False):
-            qk, v = _InProjection.apply(x_qk.to(torch.bfloat16), tgt.to(torch.bfloat16), w, b,
-                                        sh[0] if ok else None, sh[1] if ok else None)
+            qk, v = _InProjection.apply(qk16, v16, w, b, sh[0] if ok else None, sh[1] if ok else None)
             q, k = qk.view(B, L, 2, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
             v = v.view(B, L, H, hd).transpose(1, 2)
             out = F.scaled_dot_product_attention(q, k, v, attn_mask=query_mask[:, None, None, :],

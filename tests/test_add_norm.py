@@ -14,6 +14,7 @@ import torch
 from conftest import PKG
 
 AN = PKG.models.modules.add_norm
+ATT = PKG.models.modules.attention
 
 
 def test_cpu_is_plain_layer_norm():
@@ -383,3 +384,43 @@ def test_multimodal_encoder_carry_matches_uncarried(dev, monkeypatch):
     for a, b, c in zip(g1, g2, g3):
         torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -7 * b.abs().max().item())
         assert (a - c).norm() <= 1.25 * (b - c).norm() + 1e-6 * c.norm()
+
+
+@pytest.mark.gpu
+def test_decoder_self_attention_carry_matches_uncarried(dev, monkeypatch):
+    """Decoder stack whose layers hand the next layer's self-attention its bf16 inputs
+    (bf16(out), bf16(out + query_pos)) from the last fused add + LayerNorm, against the same stack
+    casting them in each layer: forward bit-identical (dropout 0), gradients to fp32-sum order."""
+    UT = PKG.models.deformable.unimodal_deformable_transformer
+    torch.manual_seed(6)
+    layer = UT.DeformableTransformerDecoderLayer(512, 1024, 0.0, "relu", 4, 8, 4)
+    dec = UT.DeformableTransformerDecoder(layer, 3, return_intermediate=True).to(dev)
+    shapes = [256, 128, 64, 32]
+    ts = torch.tensor(shapes, device=dev)
+    lsi = torch.cat([ts.new_zeros(1), ts.cumsum(0)[:-1]])
+    B, Q = 2, 100
+    src = torch.randn(B, sum(shapes), 512, device=dev)
+    tgt0 = torch.randn(B, Q, 512, device=dev)
+    qpos = torch.randn(B, Q, 512, device=dev, requires_grad=True)
+    ref = torch.rand(B, Q, 1, device=dev)
+    vr = torch.ones(B, 4, device=dev)
+    qmask = torch.ones(B, Q, dtype=torch.bool, device=dev)
+    w = torch.randn(512, device=dev)
+
+    def run():
+        dec.zero_grad(set_to_none=True)
+        qpos.grad = None
+        tgt = tgt0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            hs, _ = dec(tgt, ref, src, ts, lsi, vr, qpos, None, qmask)
+        (hs.float() * w).sum().backward()
+        return hs.detach(), [tgt.grad, qpos.grad] + [p.grad.clone() for p in dec.parameters() if p.grad is not None]
+
+    h1, g1 = run()
+    real = ATT.mha_self_attention
+    monkeypatch.setattr(UT, "mha_self_attention", lambda m, t, p, q, carried=None: real(m, t, p, q))
+    h2, g2 = run()
+    torch.testing.assert_close(h1, h2, rtol=0, atol=0)
+    assert len(g1) == len(g2)
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3 * b.abs().max().item())
