@@ -76,6 +76,9 @@ def parse():
     p.add_argument("--gemm-solutions", default=os.path.join(ROOT, "profiles", "tunableop_gfx950.csv"),
                    help="TunableOp results (hipBLASLt / rocBLAS solution per GEMM shape, tools/tune_gemms.py), "
                         "read with tuning off; 'none' = the libraries' default heuristics")
+    p.add_argument("--conv-find", type=int, default=0,
+                   help="1: MIOpen searches the BaseEncoder Conv1d solvers once per shape in the warm-up "
+                        "(torch.backends.cudnn.benchmark; measured no gain: 712.5 vs 712.4 clips/s); 0: its immediate-mode heuristic")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"),
                    help="per-launch HBM bytes from rocprofv3 PMC passes (profiles/), if present")
     return p.parse_args()
@@ -208,6 +211,7 @@ def main():
     device = torch.device("cuda", local_rank)
     PKG._native.load_library()  # fail loudly before anything else if the HIP library is missing
     gemm_sel = use_gemm_solutions(args.gemm_solutions)
+    torch.backends.cudnn.benchmark = bool(args.conv_find)
 
     model = build_model(args, device)
     if world > 1:  # identical initial weights on every rank (the reference's DDP broadcast)
@@ -268,7 +272,8 @@ def main():
             "config": {"workload": WORKLOADS[args.config], "model": MODELS[args.config],
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch, "seq_len": args.T,
                        "d_model": 512, "levels": 4, "queries": args.queries, "parallelism": f"dp{world}",
-                       "execution": "hip_graph" if args.graph else "eager", "gemm_solutions": gemm_sel},
+                       "execution": "hip_graph" if args.graph else "eager", "gemm_solutions": gemm_sel,
+                       "conv_solver": "MIOpen find (cudnn.benchmark)" if args.conv_find else "MIOpen immediate"},
             "roofline": roofline(summary, traffic),
             "cpu_baseline": None,
         }
