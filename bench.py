@@ -47,7 +47,7 @@ WORKLOADS = {
     "multimodal": "configs[2]: multimodal video T=1024 + audio T=50 deformable fusion (4 MSDA calls per encoder "
                   "layer, 2 per decoder layer), d=512, 100 queries, 6 + 6 layers + heads, AdamW step",
     "sparse": "Sparse-DETR DVC (models/sparse, rho=0.3) T=1024 d=512, 100 queries, 6 + 6 layers, segment / count "
-              "heads + mask-prediction loss through the DAM kernel, AdamW step, eager",
+              "heads + mask-prediction loss through the DAM kernel, AdamW step (static top-k width: graph-captured)",
 }
 MODELS = {"video": "DeformableDVCCore (UnimodalDeformableDVC proposal path)",
           "multimodal": "MultimodalDVCCore (MultimodalDeformableDVC proposal path)",
@@ -65,8 +65,8 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--config", default="video", choices=["video", "multimodal", "sparse"],
                    help="video: configs[1], the headline line.  multimodal: configs[2] (video + audio T_a=50, "
-                        "SURVEY 8(d)); sparse: the Sparse-DETR DVC (rho=0.3, eager: its top-k sizes are host "
-                        "values).  Only 'video' is the BASELINE metric's workload.")
+                        "SURVEY 8(d)); sparse: the Sparse-DETR DVC (rho=0.3; top-k width from the shapes, so it is "
+                        "graph-captured too).  Only 'video' is the BASELINE metric's workload.")
     p.add_argument("--audio-T", type=int, default=50, help="audio length (reference audio_rescale_len)")
     p.add_argument("--dropout", type=float, default=0.1)
     p.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU reference path (rank 0, N=1)")
@@ -218,8 +218,6 @@ def main():
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, src=0)
     use_bf16 = args.dtype == "bf16"
-    if args.config == "sparse":
-        args.graph = 0  # host-side top-k sizes (reference :212, criterion.py:271): not capturable
     trainer = PKG.train_step.FlatGradTrainer(model, loss_fn(args), lr=1e-4, weight_decay=1e-4,
                                              max_norm=0.1, use_bf16=use_bf16, graph=bool(args.graph))
     batch = build_batch(args, rank, device)

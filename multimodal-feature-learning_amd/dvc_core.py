@@ -195,6 +195,8 @@ class SparseDVCCore(nn.Module):
             d_model=d_model, num_head=num_heads, num_encoder_layers=enc_layers, num_decoder_layers=dec_layers,
             dim_feedforward=ff_dim, dropout=dropout, activation="relu", return_intermediate_dec=True,
             num_feature_levels=num_feature_levels, dec_n_points=dec_n_points, enc_n_points=enc_n_points, rho=rho)
+        # top-k widths from the shapes, not from a device read: the step is graph-capturable
+        self.unimodal_sparse_transformer.static_topk = True
 
     def forward(self, video, video_mask, durations):
         tr = self.unimodal_sparse_transformer
@@ -215,6 +217,7 @@ class SparseDVCCore(nn.Module):
         # (depth, B, Q, 1) broadcast over both segment terms, as ``outputs_segment[..., :2] += reference`` (:203)
         segments = (segments + inverse_sigmoid(reference)).sigmoid()
         return {"all_segments": segments, "all_counts": counts, "hs": hs, "memory": memory,
+                "sparse_topk": topk.shape[1] if topk is not None else None,
                 "backbone_mask_prediction": mask_pred, "sparse_token_nums": sparse_token_nums,
                 "sampling_locations_dec": sl_dec, "attn_weights_dec": aw_dec, "temporal_shapes": shapes,
                 "level_start_index": starts, "mask_flatten": mask_flatten}
@@ -228,7 +231,8 @@ def sparse_workload_loss(out):
                                 out["sampling_locations_dec"].detach(), out["attn_weights_dec"].detach()).sum(dim=(1, 2))
     dam = dam.masked_fill(out["mask_flatten"], dam.min() - 1)
     nums = out["sparse_token_nums"]
-    topk = torch.topk(dam, int(nums.max()))[1]
+    k = out.get("sparse_topk") or int(nums.max())  # the encoder's static width: no host read
+    topk = torch.topk(dam, k)[1]
     keep = torch.arange(topk.shape[1], device=topk.device)[None, :] < nums[:, None]
     pred = out["backbone_mask_prediction"]
     target = torch.zeros_like(pred).scatter_(1, topk, keep.to(pred.dtype))

@@ -49,6 +49,11 @@ class SparseDeformableTransformer(nn.Module):
         self.eff_query_init = eff_query_init
         self.eff_specific_head = eff_specific_head
         self.rho = rho
+        # True: the top-k width is the host-known bound min(S, int(S * rho) + 1) of every clip's
+        # sparse_token_nums instead of their maximum (a device -> host read, :212); the per-clip
+        # ``keep`` masks select the same tokens, so outputs are unchanged, and the step can be
+        # captured in a HIP graph.  Equal widths when no clip is padded.
+        self.static_topk = False
         self.two_stage = False
         self.use_enc_aux_loss = use_enc_aux_loss
         self.sparse_enc_head = 1 if self.two_stage and self.rho else 0
@@ -130,7 +135,11 @@ class SparseDeformableTransformer(nn.Module):
             self.valid_token_nums = valid_token_nums
         if self.rho:
             sparse_token_nums = (valid_token_nums * self.rho).int() + 1
-            backbone_topk = min(int(max(sparse_token_nums)), backbone_output_memory.shape[1])  # host sync, as :212
+            S_tok = backbone_output_memory.shape[1]
+            if self.static_topk:
+                backbone_topk = min(int(S_tok * self.rho) + 1, S_tok)
+            else:
+                backbone_topk = min(int(max(sparse_token_nums)), S_tok)  # host sync, as :212
             self.sparse_token_nums = sparse_token_nums
             backbone_mask_prediction = self.enc_mask_predictor(backbone_output_memory).squeeze(-1)
             backbone_mask_prediction = backbone_mask_prediction.masked_fill(mask_flatten,

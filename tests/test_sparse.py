@@ -83,3 +83,44 @@ def test_sparse_transformer_matches_reference_gpu(golden, dev):
     dam = PKG.utils.dam.attn_map_to_flat_grid(r["shapes"], r["starts"], r["sl_dec"].detach(), r["aw_dec"].detach())
     ref = g["dam_flat_grid"]
     torch.testing.assert_close(dam.cpu(), ref, rtol=1e-5, atol=1e-5 * ref.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_static_topk_width_matches_data_dependent_width(dev):
+    """SparseDVCCore's top-k width from the shapes (min(S, int(S*rho)+1), no device read) selects
+    the same encoder tokens per clip as the reference's max(sparse_token_nums) width (:212) — the
+    per-clip keep masks cut both to each clip's count — on padded clips: identical outputs."""
+    import copy
+    torch.manual_seed(0)
+    core = PKG.dvc_core.SparseDVCCore(d_model=64, num_queries=6, feature_dim=64, enc_layers=2, dec_layers=2,
+                                      ff_dim=128, dropout=0.0).to(dev).double()
+    ref_core = copy.deepcopy(core)
+    ref_core.unimodal_sparse_transformer.static_topk = False
+    video, mask, dur = PKG.dvc_core.synthetic_clips(3, T=64, feature_dim=64, padded=True, seed=5, device=dev,
+                                                    dtype=torch.float64)
+    a, b = core(video, mask, dur), ref_core(video, mask, dur)
+    assert a["sparse_topk"] >= b["sparse_topk"]
+    for k in ("hs", "memory", "all_segments", "all_counts"):
+        torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, msg=k)
+    torch.testing.assert_close(PKG.dvc_core.sparse_workload_loss(a), PKG.dvc_core.sparse_workload_loss(b),
+                               rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_sparse_step_is_graph_captured(dev):
+    """With the static top-k width the Sparse-DETR training step has no host read and is replayed
+    as HIP graphs; replays track the eager step."""
+    import copy
+    torch.manual_seed(0)
+    base = PKG.dvc_core.SparseDVCCore(d_model=64, num_queries=6, feature_dim=64, enc_layers=1, dec_layers=1,
+                                      ff_dim=128, dropout=0.0)
+    batch = PKG.dvc_core.synthetic_clips(2, T=64, feature_dim=64, padded=False, seed=3, device=dev)
+    mk = lambda g: PKG.train_step.FlatGradTrainer(copy.deepcopy(base).to(dev), PKG.dvc_core.sparse_workload_loss,  # noqa
+                                                  lr=1e-4, use_bf16=True, graph=g)
+    tg, te = mk(True), mk(False)
+    tg.capture(batch, warmup=2)
+    for _ in range(2):
+        te.step(batch)
+    for _ in range(3):
+        lg, le = tg.step(batch).item(), te.step(batch).item()
+        assert abs(lg - le) <= 1e-2 * abs(le) + 1e-2
