@@ -229,7 +229,7 @@ def sparse_workload_loss(out):
     heads, its top sparse_token_nums tokens as the target of the mask predictor."""
     dam = attn_map_to_flat_grid(out["temporal_shapes"], out["level_start_index"],
                                 out["sampling_locations_dec"].detach(), out["attn_weights_dec"].detach()).sum(dim=(1, 2))
-    dam = dam.masked_fill(out["mask_flatten"], dam.min() - 1)
+    dam = torch.where(out["mask_flatten"], dam.min() - 1, dam)  # masked_fill with a tensor value syncs
     nums = out["sparse_token_nums"]
     k = out.get("sparse_topk") or int(nums.max())  # the encoder's static width: no host read
     topk = torch.topk(dam, k)[1]

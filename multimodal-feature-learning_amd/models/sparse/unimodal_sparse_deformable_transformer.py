@@ -142,8 +142,9 @@ class SparseDeformableTransformer(nn.Module):
                 backbone_topk = min(int(max(sparse_token_nums)), S_tok)  # host sync, as :212
             self.sparse_token_nums = sparse_token_nums
             backbone_mask_prediction = self.enc_mask_predictor(backbone_output_memory).squeeze(-1)
-            backbone_mask_prediction = backbone_mask_prediction.masked_fill(mask_flatten,
-                                                                            backbone_mask_prediction.min())
+            # masked_fill(mask, tensor.min()) reads the 0-dim value on the host; where() keeps it on the device
+            backbone_mask_prediction = torch.where(mask_flatten, backbone_mask_prediction.min(),
+                                                   backbone_mask_prediction)
             backbone_topk_proposals = torch.topk(backbone_mask_prediction, backbone_topk, dim=1)[1]
         else:
             backbone_topk_proposals = backbone_mask_prediction = sparse_token_nums = None

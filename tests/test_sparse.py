@@ -89,21 +89,21 @@ def test_sparse_transformer_matches_reference_gpu(golden, dev):
 def test_static_topk_width_matches_data_dependent_width(dev):
     """SparseDVCCore's top-k width from the shapes (min(S, int(S*rho)+1), no device read) selects
     the same encoder tokens per clip as the reference's max(sparse_token_nums) width (:212) — the
-    per-clip keep masks cut both to each clip's count — on padded clips: identical outputs."""
+    per-clip keep masks cut both to each clip's count — on padded clips: identical outputs (every MSDA
+    query is computed independently, so the extra masked-out queries change nothing)."""
     import copy
     torch.manual_seed(0)
     core = PKG.dvc_core.SparseDVCCore(d_model=64, num_queries=6, feature_dim=64, enc_layers=2, dec_layers=2,
-                                      ff_dim=128, dropout=0.0).to(dev).double()
+                                      ff_dim=128, dropout=0.0).to(dev)
     ref_core = copy.deepcopy(core)
     ref_core.unimodal_sparse_transformer.static_topk = False
-    video, mask, dur = PKG.dvc_core.synthetic_clips(3, T=64, feature_dim=64, padded=True, seed=5, device=dev,
-                                                    dtype=torch.float64)
+    video, mask, dur = PKG.dvc_core.synthetic_clips(3, T=64, feature_dim=64, padded=True, seed=5, device=dev)
     a, b = core(video, mask, dur), ref_core(video, mask, dur)
     assert a["sparse_topk"] >= b["sparse_topk"]
     for k in ("hs", "memory", "all_segments", "all_counts"):
         torch.testing.assert_close(a[k], b[k], rtol=0, atol=0, msg=k)
     torch.testing.assert_close(PKG.dvc_core.sparse_workload_loss(a), PKG.dvc_core.sparse_workload_loss(b),
-                               rtol=1e-12, atol=1e-12)
+                               rtol=1e-6, atol=1e-6)
 
 
 @pytest.mark.gpu
