@@ -18,6 +18,7 @@ from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 from ..modules.ffn import relu_dropout
+from ..modules.value_proj import layer_values, layer_values_supported
 from .unimodal_deformable_transformer import (_get_activation_fn, _get_clones, encoder_reference_points,
                                               level_metadata)
 
@@ -216,6 +217,7 @@ class MultimodalDeformableTransformerEncoder(nn.Module):
                                            video_ref, video_temporal_shapes, video_level_start_index,
                                            video_padding_mask, audio_ref, audio_temporal_shapes,
                                            audio_level_start_index, audio_padding_mask)
+            v[0]._mfl_bf16, a[0]._mfl_bf16 = v[1], a[1]  # bf16(out): the decoder's value projections read them
             return v[0], a[0]
         for layer in self.layers:
             v, a = output
@@ -253,19 +255,22 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
         hidden = relu_dropout(self.linear1(tgt), self.activation, self.dropout3)
         return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
-    def _cross_block(self, tgt, query_pos, ref, src, shapes, starts, mask):
-        attn = self.cross_attn(self.with_pos_embed(tgt, query_pos), ref, src, shapes, starts, mask)
+    def _cross_block(self, tgt, query_pos, ref, src, shapes, starts, mask, value=None):
+        attn = self.cross_attn(self.with_pos_embed(tgt, query_pos), ref, src, shapes, starts, mask, value=value)
         return add_layer_norm(tgt, attn, self.norm1, dropout=self.dropout1)
 
     def forward(self, tgt, query_pos, reference_points_input_video, reference_points_input_audio, query_mask,
                 video_src, video_temporal_shapes, video_level_start_index, video_src_padding_mask, audio_src,
-                audio_temporal_shapes, audio_level_start_index, audio_src_padding_mask):
+                audio_temporal_shapes, audio_level_start_index, audio_src_padding_mask, video_value=None,
+                audio_value=None):
+        """``video_value`` / ``audio_value``: this layer's cross-attention values of the two memories,
+        when the decoder computed every layer's at once (models/modules/value_proj.py)."""
         sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask)
         tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         tgt_video = self._cross_block(tgt, query_pos, reference_points_input_video, video_src, video_temporal_shapes,
-                                      video_level_start_index, video_src_padding_mask)
+                                      video_level_start_index, video_src_padding_mask, video_value)
         tgt_audio = self._cross_block(tgt, query_pos, reference_points_input_audio, audio_src, audio_temporal_shapes,
-                                      audio_level_start_index, audio_src_padding_mask)
+                                      audio_level_start_index, audio_src_padding_mask, audio_value)
         bridged = self.linear3(self.norm4(torch.cat([tgt_video, tgt_audio], dim=-1)))
         tgt = self.activation(self.dropout5(bridged))
         return self.forward_ffn(tgt)
@@ -293,12 +298,21 @@ class MultimodalDeformableTransformerDecoder(nn.Module):
                 audio_level_start_index, audio_valid_ratios, audio_padding_mask, disable_iterative_refine=False):
         output = tgt
         hs, refs = [], []
+        vvals = avals = None
+        attns = [getattr(layer, "cross_attn", None) for layer in self.layers]
+        if (all(type(layer) is MultimodalDeformableTransformerDecoderLayer for layer in self.layers)
+                and layer_values_supported(attns, video_src, video_padding_mask)
+                and layer_values_supported(attns, audio_src, audio_padding_mask)):
+            # every layer projects the same two memories: one batched GEMM each way per memory
+            vvals = layer_values(attns, video_src, video_padding_mask)
+            avals = layer_values(attns, audio_src, audio_padding_mask)
         for lid, layer in enumerate(self.layers):
             ref_v = self._per_level(reference_points, video_valid_ratios)
             ref_a = self._per_level(reference_points, audio_valid_ratios)
+            extra = {} if vvals is None else {"video_value": vvals[lid], "audio_value": avals[lid]}
             output = layer(output, query_pos, ref_v, ref_a, query_padding_mask, video_src, video_temporal_shapes,
                            video_level_start_index, video_padding_mask, audio_src, audio_temporal_shapes,
-                           audio_level_start_index, audio_padding_mask)
+                           audio_level_start_index, audio_padding_mask, **extra)
             if not disable_iterative_refine and self.bbox_head is not None:
                 delta = self.bbox_head[lid](output)
                 if reference_points.shape[-1] == 2:
