@@ -359,15 +359,18 @@ class FlatGradTrainer:
                 self.eager_step(batch)
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+        # capture_error_mode "thread_local": the RCCL process group's watchdog thread polls the
+        # events of the warm-up collectives (hipEventQuery) while this thread captures; under the
+        # default global mode that poll is refused and the watchdog aborts the process
         self._g_fb = torch.cuda.CUDAGraph()
         self._overlap_now = self.overlap and self.capture_collectives
         try:
-            with torch.cuda.graph(self._g_fb):
+            with torch.cuda.graph(self._g_fb, capture_error_mode="thread_local"):
                 self._loss = self._forward_backward(batch, cache_casts=False)
         finally:
             self._fb_reduces, self._overlap_now = self._overlap_now, self.overlap
         self._g_up = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_up, pool=self._g_fb.pool()):
+        with torch.cuda.graph(self._g_up, pool=self._g_fb.pool(), capture_error_mode="thread_local"):
             self._update()
         torch.cuda.synchronize(self.device)
 
