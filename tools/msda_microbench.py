@@ -77,7 +77,8 @@ def main():
     # (name, level shapes, Lq): configs[1] encoder / decoder calls, configs[3]'s T=4096 encoder
     # call, configs[2]'s video queries over the audio pyramid (T_a = 50)
     calls = [("enc", [1024, 512, 256, 128], 1920), ("dec", [1024, 512, 256, 128], 100),
-             ("enc4096", [4096, 2048, 1024, 512], 7680), ("xmod", [50, 25, 13, 7], 1920)]
+             ("enc4096", [4096, 2048, 1024, 512], 7680), ("xmod", [50, 25, 13, 7], 1920),
+             ("sparse", [1024, 512, 256, 128], 577)]
     for dname in args.dtypes.split(","):
         dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[dname]
         vb = 2 if dtype == torch.bfloat16 else 4
