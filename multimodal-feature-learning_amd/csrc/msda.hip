@@ -1473,8 +1473,16 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
     uint4 g[U];
     f32x2 cc[U];
     float lcv[U], acv[U];
+    // steps u that no slot of the wave has an entry for (a list or a share ending inside the
+    // batch) are skipped, gather and arithmetic: the pull is VALU-bound (one step is ~40 wave64
+    // VALU instructions), and a cut batch computed all U steps before
+    int nu = U;
+#pragma unroll
+    for (int u = 1; u < U; ++u)
+      if (nu == U && __ballot(ebase + u * STR < lim) == 0ull) nu = u;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      if (u >= nu) break;
       const int e = ebase + u * STR;
       const bool have = e < lim;
       unsigned key = ekey[have ? e : 0];
@@ -1496,6 +1504,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_pair_kernel(
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
+      if (u >= nu) break;
       const int e = ebase + u * STR;
       const bool have = e < lim;
       Taps<float> t{};
