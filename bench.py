@@ -3,7 +3,7 @@
 (BaseEncoder + 6 enc + 6 dec deformable transformer + heads, T=1024, d=512, L=4 levels,
 100 queries) — BASELINE.json ``metric`` / ``configs[1]`` — on N MI355X, one process per GPU.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python bench.py [--gpus N] [--steps K] [--warmup W]     (N > 1: spawns the N ranks itself)
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
@@ -200,8 +200,42 @@ def use_gemm_solutions(path):
     return "TunableOp selection " + os.path.relpath(path, ROOT)
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_plan(gpus, env, argv):
+    """How this invocation runs its ranks (the reference launches one DDP process per GPU,
+    main.py:85 under utils/misc.py:436-458's env:// rendezvous):
+      None   — run here: a launcher already started this rank (WORLD_SIZE set, equal to --gpus)
+               or --gpus 1;
+      [cmd]  — --gpus N > 1 and no launcher: spawn ``torch.distributed.run --nproc-per-node N``
+               over 127.0.0.1 with the same arguments, as a child process (nothing here has
+               touched the GPU yet), and exit with its status.
+    Raises SystemExit(2) when WORLD_SIZE disagrees with --gpus: the line's n_gpus must be --gpus."""
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    world_env = env.get("WORLD_SIZE")
+    if world_env is not None:
+        if int(world_env) != gpus:
+            print(f"bench.py: --gpus {gpus} but WORLD_SIZE={world_env} (launcher started {world_env} ranks)",
+                  file=sys.stderr, flush=True)
+            raise SystemExit(2)
+        return None
+    if gpus == 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+
+
 def main():
     args = parse()
+    cmd = launch_plan(args.gpus, os.environ, sys.argv[1:])
+    if cmd is not None:  # rank 0 of the child job prints the JSON line on the shared stdout
+        sys.exit(subprocess.run(cmd).returncode)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -42,6 +42,7 @@ def graph_packet_capture_off():
 __version__ = "0.1.0"
 
 from . import _native  # noqa: E402
+from . import _trace  # noqa: E402,F401
 from . import msda  # noqa: E402
 from . import MultiScaleDeformableAttention  # noqa: E402
 from . import models  # noqa: E402

@@ -2284,6 +2284,10 @@ int run_backward_impl(const Problem& pr, const void* value, const void* loc, con
   }
 
   // 1. sort: one workgroup per (b, m, level)
+  if (workspace == nullptr) {  // the workspace query promised this call none: refuse, never fault
+    set_error("msda_hip_backward: the sort / pull path needs a workspace of %zu bytes (none given)", wl.total);
+    return MSDA_ERR_ARG;
+  }
   {
     static const int deterministic = [] {
       const char* e = getenv("MSDA_HIP_DETERMINISTIC");
@@ -2562,11 +2566,15 @@ bool pair_plan(int value_dtype, long long B, long long M, long long Lq, long lon
       if (ns >= 4 && T[l] + 1 < 2 * W && T[l] <= striped_rows) mask |= 1u << l;
     }
   }
+  // the query's bound reserves the striped levels' wave-partial rows whenever a level could be
+  // striped (ns >= 4): the call's plan then never needs more LDS than the bound, so a call whose
+  // bound fitted stg 1 (no workspace handed over) fits stg 1 too
+  const bool any_striped = T == nullptr ? ns >= 4 : mask != 0;
   pp->rs = pair_rs(B * M * L);
   for (int stg : {1, 2}) {  // (stg 0 — keys only, coordinates from the pull — is not launched)
     if (stg == 2 && !allow_ws) continue;
     PairLayout lay;
-    const size_t lds = pair_layout(N, D, ns, maxT, stg == 1, stg == 1 && mask != 0, &lay);
+    const size_t lds = pair_layout(N, D, ns, maxT, stg == 1, stg == 1 && any_striped, &lay);
     if (lds <= kPairLdsMax) {
       pp->lay = lay;
       pp->lds = lds;

@@ -72,7 +72,8 @@ def _drop_args(dropout, device):
 class _AddLayerNorm(Function):
     @staticmethod
     def forward(ctx, r, y, weight, bias, eps, p_drop, seed):
-        from ... import _native
+        from ... import _native, _trace
+        _trace.hit("add_ln")
         lib = _native.load_library()
         d = r.shape[-1]
         rows = r.numel() // d
@@ -129,7 +130,8 @@ def add_layer_norm(r, y, norm: nn.LayerNorm, dropout=None):
 class _AddLayerNormCarry(Function):
     @staticmethod
     def forward(ctx, r, y, weight, bias, pos, eps, p_drop, seed):
-        from ... import _native
+        from ... import _native, _trace
+        _trace.hit("add_ln_carry")
         lib = _native.load_library()
         ctx.set_materialize_grads(False)
         d = r.shape[-1]

@@ -172,13 +172,25 @@ class MSDeformAttn(nn.Module):
         return output
 
 
+def private_grad(grad):
+    """Whether ``grad`` (or the tensor it views) is a gradient the MSDA backward just allocated and
+    nothing else references (msda.MSDAFunction tags it): a second consumer of the value gives a
+    fresh sum instead, so only then may the gradient be written in place."""
+    base = grad if grad._base is None else grad._base
+    return base._base is None and getattr(base, "_mfl_private", False) and grad.is_contiguous()
+
+
 class _ZeroPaddingRows(torch.autograd.Function):
     """In-place ``value.masked_fill_(mask[..., None], 0)`` through ``mfl_zero_masked_rows``: only
     padding rows are written (an all-valid batch reads the mask and nothing else); the backward
-    zeroes the same rows of the incoming gradient, which only the MSDA backward produced."""
+    zeroes the same rows of the incoming gradient in place when the MSDA backward produced it and
+    nothing else holds it (``private_grad``), else out of place (``masked_fill``).  A hook on the
+    masked value that keeps the gradient it is given sees the zeroed rows (not supported)."""
 
     @staticmethod
     def forward(ctx, value, mask):
+        from ... import _trace
+        _trace.hit("zero_rows")
         _zero_rows(value, mask)
         ctx.mark_dirty(value)
         ctx.save_for_backward(mask)
@@ -187,7 +199,8 @@ class _ZeroPaddingRows(torch.autograd.Function):
     @staticmethod
     def backward(ctx, grad):
         (mask,) = ctx.saved_tensors
-        grad = grad.contiguous()
+        if not private_grad(grad):
+            return grad.masked_fill(mask[..., None], 0), None
         _zero_rows(grad, mask)
         return grad, None
 
@@ -270,6 +283,8 @@ class _InProjection(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x_qk, x_v, w, b, wc, bc):
+        from ... import _trace
+        _trace.hit("sdpa_self_attn_shadow" if wc is not None else "sdpa_self_attn_cast")
         dt = x_qk.dtype
         wc = w.to(dt) if wc is None else wc
         bc = b.to(dt) if bc is None else bc

@@ -23,7 +23,8 @@ __all__ = ["relu_dropout"]
 class _ReluDropout(Function):
     @staticmethod
     def forward(ctx, h, p_drop, seed):
-        from ... import _native
+        from ... import _native, _trace
+        _trace.hit("relu_dropout")
         lib = _native.load_library()
         out = torch.empty_like(h)
         rc = lib.mfl_relu_dropout_forward(h.data_ptr(), h.numel(), p_drop, _ptr(seed), out.data_ptr(),

@@ -87,6 +87,8 @@ class _AutocastLinear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, weight, bias, wc, bc):
+        from ... import _trace
+        _trace.hit("linear_shadow" if wc is not None else "linear_cast")
         dt = x.dtype
         if wc is None:
             wc = weight.to(dt)
@@ -123,6 +125,8 @@ class _AutocastLinearPair(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wa, ba, wb, bb, wca, bca, wcb, bcb):
+        from ... import _trace
+        _trace.hit("linear_pair_shadow" if wca is not None and wcb is not None else "linear_pair_cast")
         dt = x.dtype
         wca = wa.to(dt) if wca is None else wca
         wcb = wb.to(dt) if wcb is None else wcb

@@ -39,7 +39,9 @@ def _zero_rows(y, nbatch, rows, mask):
 class _LayerValues(Function):
     @staticmethod
     def forward(ctx, x, mask, n, *params):
+        from ... import _trace
         w, b, wc, bc = params[:n], params[n:2 * n], params[2 * n:3 * n], params[3 * n:4 * n]
+        _trace.hit("layer_values_shadow" if all(t is not None for t in wc) else "layer_values")
         dt = torch.bfloat16
         lead = x.shape[:-1]
         c = x.shape[-1]

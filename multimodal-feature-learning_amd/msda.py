@@ -233,6 +233,8 @@ class MSDAFunction(Function):
 
     @staticmethod
     def forward(ctx, value, loc, aw, shapes, starts, padding_mode):
+        from . import _trace
+        _trace.hit("msda_" + str(value.dtype).replace("torch.", ""))
         ctx.meta = (shapes, starts, padding_mode)
         ctx.save_for_backward(value, loc, aw)
         return msda_forward(value, shapes, starts, loc, aw, padding_mode)
@@ -245,6 +247,8 @@ class MSDAFunction(Function):
         nv, nl, na = ctx.needs_input_grad[:3]
         gv, gl, ga = msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode,
                                    need_value=nv, need_loc=nl, need_aw=na)
+        if gv is not None:
+            gv._mfl_private = True  # fresh, referenced by nothing else: consumers may write it in place
         return gv, gl, ga, None, None, None
 
 
@@ -325,6 +329,8 @@ def prologue_backward(grad_loc, grad_aw, aw, offsets, ref, shapes, need_off=True
 class MSDAPrologueFunction(Function):
     @staticmethod
     def forward(ctx, offsets, logits, ref, shapes):
+        from . import _trace
+        _trace.hit("msda_prologue")
         loc, aw = prologue_forward(offsets, logits, ref, shapes)
         ctx.shapes = shapes
         ctx.save_for_backward(aw, offsets, ref)

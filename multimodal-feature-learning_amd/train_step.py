@@ -123,11 +123,15 @@ class FlatGradTrainer:
         self._pending = None
         self._overlap_now = self.overlap  # eager steps; capture() decides for the graph
         self._fb_reduces = False          # the captured fwd+bwd graph all-reduces the buckets
-        # parameters that never receive a gradient (found on the first step) are left untouched, as
-        # torch AdamW leaves a parameter whose grad is None (reference DDP find_unused_parameters)
+        # parameters that no rank gave a gradient are left untouched, as torch AdamW leaves a
+        # parameter whose grad is None (reference DDP find_unused_parameters=True, main.py:85):
+        # found again after every eager step; the captured graphs keep the set of their capture
+        # (a replay runs the captured kernels, so which parameters get gradients cannot change)
         self._got = [False] * len(self.params)
         self._unused = None
-        self._frozen = None
+        self._frozen = None       # (views of their values / moments / shadow, scratch copies)
+        self._frozen_keep = []    # earlier scratch sets, alive while a captured graph may read them
+        self._late = False
         self._bucket_of = {}
         for bi, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
@@ -165,11 +169,26 @@ class FlatGradTrainer:
         def hook(p):
             if self._pending is None:  # backward outside _forward_backward (user code): nothing to do
                 return
+            self._got[i] = True
             b = self._bucket_of[i]
+            if i in self._known_unused or b < self._next_flush:
+                # a parameter found unused got a gradient (its bucket may be reduced already):
+                # after the backward the whole buffer is reduced again (_forward_backward)
+                self._late = True
+                return
             self._pending[b] -= 1
             if self._pending[b] == 0:
-                self._flush_bucket(b)
+                self._ready[b] = True
+                self._flush_ready()
         return hook
+
+    def _flush_ready(self):
+        """Reduce the complete buckets in index order: every rank issues the same collectives in
+        the same order and sizes, whatever order its backward completes them in (DDP's bucket
+        order; a bucket waiting on a late parameter holds back the ones after it)."""
+        while self._next_flush < len(self.buckets) and self._ready[self._next_flush]:
+            self._flush_bucket(self._next_flush)
+            self._next_flush += 1
 
     def _flush_bucket(self, b):
         start, end, idx = self.buckets[b]
@@ -182,7 +201,6 @@ class FlatGradTrainer:
             torch._foreach_copy_([v for v, _ in got], [g for _, g in got])
         if missing:
             torch._foreach_zero_(missing)
-        self._done[b] = True
         if self._overlap_now:
             cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
             if cur is not None:
@@ -215,6 +233,11 @@ class FlatGradTrainer:
 
     @weight_decay.setter
     def weight_decay(self, value):
+        if self.opt is not None and self._g_up is not None and float(value) != self._wd:
+            # torch AdamW reads weight_decay as a Python float: the captured update graph has the
+            # capture's value baked in (the fused update reads it from device memory instead)
+            raise RuntimeError("FlatGradTrainer: weight_decay cannot change after capture() with the torch AdamW "
+                               "update (fused_optimizer=False); capture again or use the fused update")
         self._wd = float(value)
         self._lr_wd[1] = self._wd
         if self.opt is not None:
@@ -260,40 +283,66 @@ class FlatGradTrainer:
                             cache_enabled=cache_casts), seed_pool(self.device):
             out = self.model(*batch)
             loss = self.loss_fn(out)
-        self._pending = [len(idx) for _, _, idx in self.buckets]
-        self._done = [False] * len(self.buckets)
+        capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
+        # parameters found unused (by every rank, last step) do not hold their buckets back
+        self._known_unused = frozenset(self._unused or ())
+        self._got = [False] * len(self.params)
+        self._pending = [sum(1 for i in idx if i not in self._known_unused) for _, _, idx in self.buckets]
+        self._ready = [n == 0 for n in self._pending]
+        self._next_flush = 0
+        self._late = False
         self._works = []
         try:
-            loss.backward()  # overlap: full buckets are copied and all-reduced from the hooks
+            self._flush_ready()
+            loss.backward()  # overlap: complete buckets are copied and all-reduced from the hooks, in order
         finally:
-            pending, self._pending = self._pending, None
-        for b in range(len(self.buckets)):  # buckets with parameters that got no gradient
-            if not self._done[b]:
-                self._flush_bucket(b)
+            self._pending = None
+        self._ready = [True] * len(self.buckets)  # buckets with parameters that got no gradient
+        self._flush_ready()
         if self._overlap_now:
             if self._comm_stream is not None:
                 torch.cuda.current_stream(self.device).wait_stream(self._comm_stream)
             for w in self._works:
                 w.wait()
             self._works = []
+        if not capturing:
+            self._find_unused()  # also reduces again if any rank had a late gradient
+        if self._overlap_now:
             self.flat_grad.div_(self.world)
         self._attach_grads()
-        if self._unused is None and not (self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()):
-            self._find_unused()
         if self._unused and self.opt is not None:
             for i in self._unused:  # torch AdamW skips a parameter whose grad is None
                 self.params[i].grad = None
         return loss.detach()
 
     def _find_unused(self):
-        """After the first backward: the parameters no rank gave a gradient.  The fused update then
-        restores their values, moments and bf16 shadow after every step (a few small copies,
-        captured with the update graph), so weight decay never touches them."""
-        got = torch.tensor([1 if g else 0 for g in self._got], dtype=torch.int32, device=self.device)
+        """After an eager backward: the parameters no rank gave a gradient (one small MAX all-reduce
+        of the per-parameter flags at world size > 1, which also carries the late-gradient flag).
+        The fused update leaves their values, moments and bf16 shadow as they were before it (saved
+        and restored around the update kernels, captured with the update graph), so weight decay
+        never touches them.  A step on which some rank gave a gradient to a parameter found unused
+        before (its bucket was reduced without it) reduces the whole gradient buffer once more."""
+        flags = [1 if g else 0 for g in self._got] + [1 if self._late else 0]
         if self.world > 1:
-            dist.all_reduce(got, op=dist.ReduceOp.MAX, group=self.pg)
-        self._unused = [i for i, g in enumerate(got.tolist()) if g == 0]
-        if not self._unused or self.opt is not None:
+            t = torch.tensor(flags, dtype=torch.int32, device=self.device)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
+            flags = t.tolist()
+        if flags[-1] and self._overlap_now:
+            # the local gradients are still attached to the parameters: reduce them all again
+            for v, p in zip(self.grad_views, self.params):
+                if p.grad is not None:
+                    v.copy_(p.grad)
+                else:
+                    v.zero_()
+            dist.all_reduce(self.flat_grad, group=self.pg)
+        unused = [i for i, g in enumerate(flags[:-1]) if g == 0]
+        if unused == self._unused:
+            return
+        self._unused = unused
+        if self._frozen is not None:
+            self._frozen_keep.append(self._frozen)
+        self._frozen = None
+        if not unused or self.opt is not None:
             return
         views = []
         flats = [self.flat_param, self.exp_avg, self.exp_avg_sq] + ([self.flat_bf16] if self.flat_bf16 is not None
@@ -302,10 +351,10 @@ class FlatGradTrainer:
         for p in self.params:
             offs.append(off)
             off += p.numel()
-        for i in self._unused:
+        for i in unused:
             n = self.params[i].numel()
             views.extend(f[offs[i]:offs[i] + n] for f in flats)
-        self._frozen = (views, [v.clone() for v in views])
+        self._frozen = (views, [torch.empty_like(v) for v in views])
 
     def _allreduce(self):
         if self.world > 1 and not self._overlap_now:
@@ -320,6 +369,8 @@ class FlatGradTrainer:
             return
         from . import _native
         shadow = self.flat_bf16.data_ptr() if self.flat_bf16 is not None else None
+        if self._frozen is not None:  # parameters without gradients: saved before, restored after
+            torch._foreach_copy_(self._frozen[1], self._frozen[0])
         rc = self._lib.flat_adamw_step(
             self.flat_param.data_ptr(), self.flat_grad.data_ptr(), self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
             shadow, self.flat_param.numel(), self.opt_step.data_ptr(), self._opt_ws.data_ptr(), self._lr,
@@ -327,7 +378,7 @@ class FlatGradTrainer:
             _native.stream_handle(self.device))
         if rc != 0:
             raise RuntimeError("flat_adamw_step failed: " + self._lib.flat_adamw_last_error().decode())
-        if self._frozen is not None:  # parameters without gradients: values, moments, shadow unchanged
+        if self._frozen is not None:  # values, moments and shadow as before the update
             torch._foreach_copy_(self._frozen[0], self._frozen[1])
         self._refresh_shadow(copy=False)
 
@@ -344,6 +395,8 @@ class FlatGradTrainer:
         ``batch`` tensors are the graph's static inputs: refill them in place to change data."""
         if not self.graph:
             return
+        if warmup < 1:  # the eager warm-up finds the unused parameters the graphs keep (_find_unused)
+            raise ValueError("FlatGradTrainer.capture: warmup must be >= 1")
         import importlib
         pkg = importlib.import_module(__name__.rsplit(".", 1)[0])
         if not pkg.graph_packet_capture_off():

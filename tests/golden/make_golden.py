@@ -40,6 +40,15 @@ Fixtures:
   deformable_dvc_f64.pt      UnimodalDeformableDVC with its caption-decoder call's argument order fixed.
   mm_caption_decoder_f64.pt  MultimodalCaptionDecoder with HEAD's undefined names bound (no file edits).
   mm_dvc_f64.pt              MultimodalDeformableDVC training fwd + grads, undefined names bound likewise.
+  transformer_bf16_d256.pt   BaseEncoder + DeformableTransformer (2 enc + 2 dec) at d=256, 8 heads, ff 1024,
+                             T=64, B=2 (one padded clip), dropout 0: the reference's fp64 run and its run
+                             under torch.autocast('cpu', bfloat16) — d % 256 == 0, so the GPU test runs the
+                             bench's fused composition on it.  Parameters regenerated from their names
+                             (regen_parameters, no state_dict stored); gradients stored on fixed index
+                             samples (grad_sample_index) plus their full norms.
+  caption_bf16.pt            UnimodalCaptionDecoder at d=512, 8 heads, depth 2, vocab 10000, seq_len 20:
+                             teacher-forced forward + caption log-likelihood gradients and the reference's
+                             greedy re-decode loop (unimodal_deformable_dvc.py:304-354), fp64 and bf16 autocast.
 
 usage: make_golden.py [case ...]   (default: every case; e.g. ``make_golden.py dam sparse``)
 """
@@ -129,6 +138,84 @@ def _edge_points(loc, shapes):
                 flat[i] = v
         loc[:, 0, :, l] = flat.view(loc[:, 0, :, l].shape)
     return loc
+
+
+def _name_seed(name, seed):
+    import zlib
+    return (zlib.crc32(name.encode()) ^ (seed * 2654435761)) & 0x7FFFFFFF
+
+
+KEEP_INIT = ("sampling_offsets.bias",)  # the reference's deterministic offset grid (attention.py:427-435)
+
+
+def regen_parameters(module, seed, scale=None):
+    """Overwrite every parameter of ``module`` with values that depend only on its state_dict name
+    and ``seed`` (construction-order free), so a fixture stores no weights: the GPU test rebuilds
+    the same values on the mirrored modules, whose parameter names are the reference's.
+    LayerNorm / GroupNorm weights 1 + U(-0.1, 0.1); other vectors U(-0.05, 0.05); matrices and
+    convolutions xavier-uniform bounds; embeddings and ``level_embed`` N(0, 1);
+    ``sampling_offsets.weight`` N(0, 0.05) (generic sample positions, as _jitter_offsets);
+    ``scale`` multiplies named parameters afterwards.  Returns {name: sum of |p|} (checked by the test)."""
+    kinds = {}
+    for mname, mod in module.named_modules():
+        for pname, _ in mod.named_parameters(recurse=False):
+            full = f"{mname}.{pname}" if mname else pname
+            if isinstance(mod, (torch.nn.LayerNorm, torch.nn.GroupNorm)):
+                kinds[full] = "norm_" + pname
+            elif isinstance(mod, torch.nn.Embedding) or pname == "level_embed":
+                kinds[full] = "embedding"
+            else:
+                kinds[full] = "other"
+    sums = {}
+    with torch.no_grad():
+        for name, p in sorted(module.named_parameters()):
+            if name.endswith(KEEP_INIT):
+                sums[name] = p.double().abs().sum().item()
+                continue
+            g = torch.Generator().manual_seed(_name_seed(name, seed))
+            u = torch.rand(p.shape, generator=g, dtype=torch.float64) * 2 - 1
+            kind = kinds[name]
+            if kind == "embedding":
+                v = torch.randn(p.shape, generator=g, dtype=torch.float64)
+            elif kind == "norm_weight":
+                v = 1 + 0.1 * u
+            elif name.endswith("sampling_offsets.weight"):
+                v = torch.randn(p.shape, generator=g, dtype=torch.float64) * 0.05
+            elif p.dim() >= 2:
+                rf = 1
+                for k in p.shape[2:]:
+                    rf *= k
+                v = u * (6.0 / (p.shape[0] * rf + p.shape[1] * rf)) ** 0.5
+            else:
+                v = 0.05 * u
+            if scale and name in scale:
+                v = v * scale[name]
+            p.copy_(v.to(p.dtype))
+            sums[name] = p.double().abs().sum().item()
+    return sums
+
+
+def grad_sample_index(name, n, k=2048):
+    """Fixed sample of a flattened gradient's positions (all of them when n <= k)."""
+    if n <= k:
+        return torch.arange(n)
+    g = torch.Generator().manual_seed(_name_seed(name, 7))
+    return torch.randperm(n, generator=g)[:k].sort().values
+
+
+def sampled_grads(named):
+    """{module: {param: (sample of the flat gradient (fp32), full norm (fp64))}}"""
+    out = {}
+    for mname, m in named.items():
+        d = {}
+        for k, p in m.named_parameters():
+            if p.grad is None:
+                continue
+            flat = p.grad.reshape(-1)
+            d[k] = dict(sample=flat[grad_sample_index(mname + "." + k, flat.numel())].float(),
+                        norm=torch.tensor(flat.double().norm().item(), dtype=torch.float64))
+        out[mname] = d
+    return out
 
 
 def op_case(ref, dtype, shapes, B, M, D, Lq, P, seed, edge=True):
@@ -507,6 +594,200 @@ def transformer_bf16_case(ref):
                              for n, m in named.items()})
 
 
+D256 = dict(d_model=256, heads=8, ff=1024, Q=20, B=2, T=64, seed=97)
+
+
+def d256_inputs():
+    """Inputs of transformer_bf16_d256 (regenerable: the GPU test calls this too)."""
+    c = D256
+    gen = torch.Generator().manual_seed(c["seed"])
+    video = torch.randn((c["B"], c["T"], c["d_model"]), generator=gen, dtype=torch.float64).float()
+    mask = torch.zeros(c["B"], c["T"], dtype=torch.bool)
+    mask[1, 48:] = True
+    durations = torch.tensor([37.5, 120.25], dtype=torch.float32)
+    return video, mask, durations, gen
+
+
+def transformer_bf16_d256_case(ref):
+    """The bench's composition at a shape where its fused paths engage (d % 256 == 0, >= 2 decoder
+    layers): PositionEmbeddingVideoSine + BaseEncoder + DeformableTransformer (2 + 2 layers, 8 heads,
+    ff 1024, dropout 0) on T=64, B=2 with one padded clip, run by the reference in fp64 (the truth)
+    and in fp32 under torch.autocast('cpu', bfloat16) (the reference's own bf16 run: grid_sample
+    stays fp32 there, autocast promotes it).  Parameters from regen_parameters; loss
+    (hs * w_hs).sum() + (memory * w_mem).sum()."""
+    c = D256
+    d, heads, Q = c["d_model"], c["heads"], c["Q"]
+    named = torch.nn.ModuleDict(dict(
+        pos_embed=ref.embedding_layers.PositionEmbeddingVideoSine(d // 2, normalize=True),
+        base_encoder=ref.base_encoder.BaseEncoder(4, d, d),
+        transformer=ref.uni.DeformableTransformer(d_model=d, num_head=heads, num_encoder_layers=2,
+                                                  num_decoder_layers=2, dim_feedforward=c["ff"], dropout=0.0,
+                                                  return_intermediate_dec=True, num_feature_levels=4,
+                                                  dec_n_points=4, enc_n_points=4),
+        query_embedding=torch.nn.Embedding(Q, 2 * d)))
+    sums = regen_parameters(named, c["seed"])
+    video, mask, durations, gen = d256_inputs()
+    w_hs = torch.randn((2, c["B"], Q, d), generator=gen, dtype=torch.float64).float()
+    w_mem = torch.randn((c["B"], 120, d), generator=gen, dtype=torch.float64).float()
+
+    def run(mods, dtype, autocast):
+        v = video.to(dtype).requires_grad_(True)
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            srcs, masks, pos = mods["base_encoder"](v, mask, durations.to(dtype), mods["pos_embed"])
+            tr = mods["transformer"]
+            src_flatten, shapes, starts, valid, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(srcs, masks, pos)
+            memory = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten)
+            qmask = torch.ones(c["B"], Q, dtype=torch.bool)
+            _, tgt, refp, qpos = tr.prepare_decoder_input_query(c["B"], mods["query_embedding"].weight)
+            hs, _ = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten, qmask, False)
+        loss = (hs.to(dtype) * w_hs.to(dtype)).sum() + (memory.to(dtype) * w_mem.to(dtype)).sum()
+        loss.backward()
+        return dict(memory=memory.detach().float(), hs=hs.detach().float(), grad_video=v.grad.float(),
+                    grads=sampled_grads(dict(mods.items())))
+
+    import copy
+    m64 = copy.deepcopy(named).double()
+    torch.set_default_dtype(torch.float64)  # the duration embedding allocates with the default dtype
+    try:
+        truth = run(m64, torch.float64, False)
+    finally:
+        torch.set_default_dtype(torch.float32)
+    bf16 = run(named, torch.float32, True)
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    print("d256: reference bf16 vs fp64: memory %.3e hs %.3e grad_video %.3e" % (
+        rel(bf16["memory"], truth["memory"]), rel(bf16["hs"], truth["hs"]),
+        rel(bf16["grad_video"], truth["grad_video"])))
+    return dict(config={k: torch.tensor(v) for k, v in c.items()}, param_abs_sums=sums, w_hs=w_hs, w_mem=w_mem,
+                truth=truth, bf16=bf16)
+
+
+CAPTION = dict(vocab=10000, seq_len=20, d_model=512, depth=2, heads=8, N=6, K=40, seed=101, head_scale=8.0,
+               bos=2, eos=3, pad=1)
+
+
+def caption_inputs():
+    """Captions, memories and masks of caption_bf16 (regenerable: the GPU test calls this too)."""
+    c = CAPTION
+    gen = torch.Generator().manual_seed(c["seed"])
+    L = c["seq_len"] - 1
+    tgt = torch.randint(4, c["vocab"], (c["N"], L), generator=gen)
+    tgt[:, 0] = c["bos"]
+    for n, end in enumerate([19, 12, 7, 19, 15, 10]):
+        if end < L:
+            tgt[n, end] = c["eos"]
+            tgt[n, end + 1:] = c["pad"]
+    memory = torch.randn((c["N"], c["K"], c["d_model"]), generator=gen, dtype=torch.float64).float()
+    kmask = torch.zeros(c["N"], c["K"], dtype=torch.bool)
+    kmask[1, 30:] = True
+    kmask[4, 11:] = True
+    return tgt, memory, kmask
+
+
+def caption_masks(captions, pad):
+    """make_padding_mask / make_tgt_mask of the reference DVC (unimodal_deformable_dvc.py:384-431)."""
+    padding = captions == pad
+    L = captions.shape[1]
+    look = 1 - torch.tril(torch.ones((L, L), device=captions.device))
+    return padding, torch.maximum(padding.unsqueeze(1).unsqueeze(1), look).bool()
+
+
+def decode_gap(full64, caps, pad, eos, faster_eval):
+    """How far a decoded caption path is from greedy under an fp64 model: the largest
+    log p(argmax) - log p(chosen) over the words the loop chose, each step evaluated on the
+    loop's own input at that step (words >= w still <pad>).  0 for the fp64 greedy path."""
+    worst = 0.0
+    n, L = caps.shape
+    done = torch.zeros(n, dtype=torch.bool, device=caps.device)
+    with torch.no_grad():
+        for w in range(1, L):
+            inp = caps.clone()
+            inp[:, w:] = pad
+            pmask, tmask = caption_masks(inp, pad)
+            lp = torch.log(full64(inp, pmask, tmask)[:, w].double() + 1e-300)
+            chosen = caps[:, w].long()
+            g = lp.max(-1).values - lp.gather(-1, chosen[:, None])[:, 0]
+            live = torch.ones(n, dtype=torch.bool, device=caps.device) if faster_eval else ~done
+            if live.any():
+                worst = max(worst, g[live].max().item())
+            if not faster_eval:
+                done = done | (live & (chosen == eos))
+    return worst
+
+
+def caption_bf16_case(ref):
+    """The reference's UnimodalCaptionDecoder (models/unimodal_caption_decoder.py:19-107) at config
+    scale (d=512, 8 heads, vocab 10000, seq_len 20; depth 2, post-norm, dropout 0), parameters from
+    regen_parameters (head weights x8: confident argmax, so greedy decodes have no near-ties):
+    teacher-forced forward with the DVC's masks and -sum log p(target) gradients; the reference's
+    greedy re-decode loop (unimodal_deformable_dvc.py:304-354, exact and faster_eval) — each in
+    fp64 and under torch.autocast('cpu', bfloat16).  The caption decoder is called with the
+    argument order its signature declares (tgt_mask, memory_mask, tgt_padding_mask)."""
+    import models.unimodal_caption_decoder as ref_ucd  # noqa: E402
+    c = CAPTION
+    torch.manual_seed(c["seed"])
+    dec = ref_ucd.UnimodalCaptionDecoder(c["vocab"], seq_len=c["seq_len"], d_model=c["d_model"], depth=c["depth"],
+                                         num_heads=c["heads"], mlp_ratio=4, qkv_bias=True, pre_norm=False,
+                                         return_intermediate=True)
+    sums = regen_parameters(dec, c["seed"], scale={"head.weight": c["head_scale"]})
+    tgt, memory, kmask = caption_inputs()
+    padding, tgt_mask = caption_masks(tgt, c["pad"])
+    gen = torch.Generator().manual_seed(c["seed"] + 1)
+    vsub = torch.randperm(c["vocab"], generator=gen)[:256].sort().values
+    nxt = torch.cat([tgt[:, 1:], torch.full((c["N"], 1), c["eos"])], 1)  # the word each position predicts
+    live = nxt != c["pad"]
+
+    def forward(m, dtype, autocast):
+        mem = memory.to(dtype).requires_grad_(True)
+        m.zero_grad()
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            out = m(tgt, mem, tgt_mask=tgt_mask, memory_mask=kmask[:, None, None, :], tgt_padding_mask=padding)
+        out = out.to(dtype)
+        p_t = out.gather(-1, nxt[None, :, :, None].expand(out.shape[0], -1, -1, 1))[..., 0]
+        loss = -(torch.log(p_t + 1e-9) * live).sum()
+        loss.backward()
+        return dict(argmax=out.argmax(-1), p_target=p_t.detach().float(), probs_sub=out[..., vsub].detach().float(),
+                    grad_memory=mem.grad.float(), grads=sampled_grads({"decoder": m}))
+
+    def decode(m, dtype, autocast, faster_eval):
+        mem = memory.to(dtype)
+        caps = torch.ones([c["N"], c["seq_len"] - 1], dtype=torch.int32)
+        caps[:, 0] = c["bos"]
+        done = []
+        with torch.no_grad(), torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            for w in range(1, c["seq_len"] - 1):
+                pmask, tmask = caption_masks(caps, c["pad"])
+                out = m(caps, mem, tgt_mask=tmask, memory_mask=kmask[:, None, None, :], tgt_padding_mask=pmask)
+                top = torch.argmax(out[-1], dim=2)
+                if faster_eval:
+                    caps[:, w] = top[:, w]
+                else:
+                    for i in range(c["N"]):
+                        if i not in done:
+                            caps[i, w] = top[i, w]
+                            if top[i, w] == c["eos"]:
+                                done.append(i)
+        return caps
+
+    import copy
+    d64 = copy.deepcopy(dec).double()
+    res = dict(config={k: torch.tensor(v) for k, v in c.items()}, param_abs_sums=sums, vocab_sample=vsub,
+               truth=forward(d64, torch.float64, False), bf16=forward(dec, torch.float32, True))
+    for fe in (False, True):
+        key = "faster" if fe else "exact"
+        truth, b16 = decode(d64, torch.float64, False, fe), decode(dec, torch.float32, True, fe)
+        gap = decode_gap(lambda cp, pm, tm: d64(cp, memory.double(), tgt_mask=tm,
+                                                memory_mask=kmask[:, None, None, :], tgt_padding_mask=pm)[-1],
+                         b16, c["pad"], c["eos"], fe)
+        res["decode_" + key] = dict(truth=truth, bf16=b16, bf16_gap=torch.tensor(gap, dtype=torch.float64))
+        print("caption decode %s: reference bf16 == fp64: %s; bf16 path's worst fp64 log-prob gap %.4f" % (
+            key, bool(torch.equal(truth, b16)), gap))
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    print("caption: reference bf16 vs fp64: p_target %.3e grad_memory %.3e" % (
+        rel(res["bf16"]["p_target"], res["truth"]["p_target"]),
+        rel(res["bf16"]["grad_memory"], res["truth"]["grad_memory"])))
+    return res
+
+
 SPARSE_DVC_VOCAB = ['<unk>', '<pad>', '<bos>', '<eos>'] + [f"w{i}" for i in range(26)]
 
 
@@ -830,6 +1111,8 @@ def main():
         "deformable_dvc_f64": lambda: deformable_dvc_case(ref),
         "mm_caption_decoder_f64": lambda: mm_caption_decoder_case(ref),
         "mm_dvc_f64": lambda: mm_dvc_case(ref),
+        "transformer_bf16_d256": lambda: transformer_bf16_d256_case(ref),
+        "caption_bf16": lambda: caption_bf16_case(ref),
     }
     wanted = sys.argv[1:] or list(cases)
     for name, fn in cases.items():

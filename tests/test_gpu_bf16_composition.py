@@ -1,0 +1,194 @@
+"""The benchmarked bf16 composition against the reference's own bf16 runs (``-m gpu``).
+
+transformer_bf16_d256: BaseEncoder + DeformableTransformer at d=256 (8 heads, 2 + 2 layers, ff 1024,
+T=64, B=2 with one padded clip, dropout 0), run here exactly as bench.py runs the step — inside
+FlatGradTrainer (bf16 shadow weights) under bf16 autocast — and asserted to take the fused paths the
+bench takes: fused add + LayerNorm (and its bf16 carry), fused relu-dropout, the decoder's batched
+value projections, SDPA query self-attention, shadow-weight Linear layers, the MSDA prologue,
+padding-row zeroing and the bf16 MSDA kernels (reference: unimodal_deformable_transformer.py:228-249,
+342-373 under torch.autocast).  Every output and gradient must be as close to the reference's fp64
+run as the reference's own bf16 run is (error <= 1.5 x the reference's + 2e-3, relative L2), and
+close to that bf16 run itself.
+
+caption_bf16: UnimodalCaptionDecoder at config scale (d=512, vocab 10000, seq_len 20) under bf16
+autocast against the reference's bf16 run: teacher-forced outputs and gradients with the same bound;
+the KV-cached greedy decode's path must be as near greedy under the fp64 model as the reference's bf16
+re-decode path is, and in fp64 it must reproduce the reference's fp64 captions exactly
+(unimodal_caption_decoder.py:68-107, unimodal_deformable_dvc.py:304-354).
+
+Parameters are regenerated from their names (make_golden.regen_parameters; the stored sums of |p|
+check that both sides built the same values)."""
+import importlib.util
+import os
+
+import pytest
+import torch
+from torch import nn
+
+from conftest import PKG, ROOT
+
+pytestmark = pytest.mark.gpu
+M = PKG.models
+_spec = importlib.util.spec_from_file_location("_mg", os.path.join(ROOT, "tests", "golden", "make_golden.py"))
+MG = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(MG)
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+def check(name, ours, truth, ref16, slack=2e-3, report=None):
+    """ours vs the fp64 truth no worse than 1.5x the reference's bf16 run (+ slack), and near that run."""
+    e_ours, e_ref = rel(ours, truth), rel(ref16, truth)
+    if report is not None:
+        report.append((name, e_ours, e_ref))
+    assert e_ours <= 1.5 * e_ref + slack, (name, e_ours, e_ref)
+    assert rel(ours, ref16) <= 2.5 * e_ref + slack, (name, rel(ours, ref16), e_ref)
+
+
+def _check_param_sums(module, seed, want, scale=None):
+    got = MG.regen_parameters(module, seed, scale=scale)
+    assert set(got) == set(want), sorted(set(got) ^ set(want))
+    for k in got:
+        assert abs(got[k] - want[k]) <= 1e-9 * max(1.0, abs(want[k])), k
+
+
+class _Stack(nn.Module):
+    def __init__(self, mods):
+        super().__init__()
+        self.mods = mods
+
+    def forward(self, video, mask, durations):
+        m = self.mods
+        tr = m["transformer"]
+        srcs, masks, pos = m["base_encoder"](video, mask, durations, m["pos_embed"])
+        src_flatten, shapes, starts, valid, lvl_pos, mask_flatten = tr.prepare_encoder_inputs(srcs, masks, pos)
+        memory = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten)
+        B = video.shape[0]
+        qw = m["query_embedding"].weight
+        qmask = torch.ones(B, qw.shape[0], dtype=torch.bool, device=video.device)
+        _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qw)
+        hs, _ = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten, qmask, False)
+        return memory, hs
+
+
+EXPECTED_PATHS = ("add_ln", "add_ln_carry", "relu_dropout", "layer_values_shadow", "sdpa_self_attn_shadow",
+                  "linear_shadow", "linear_pair_shadow", "msda_prologue", "zero_rows", "msda_bfloat16")
+
+
+def test_d256_bench_composition_matches_reference_bf16(golden, dev):
+    g = golden("transformer_bf16_d256")
+    c = {k: int(v) for k, v in g["config"].items()}
+    d, Q = c["d_model"], c["Q"]
+    mods = nn.ModuleDict(dict(
+        pos_embed=M.modules.embedding_layers.PositionEmbeddingVideoSine(d // 2, normalize=True),
+        base_encoder=M.base_encoder.BaseEncoder(4, d, d),
+        transformer=M.deformable.unimodal_deformable_transformer.DeformableTransformer(
+            d_model=d, num_head=c["heads"], num_encoder_layers=2, num_decoder_layers=2, dim_feedforward=c["ff"],
+            dropout=0.0, return_intermediate_dec=True, num_feature_levels=4, dec_n_points=4, enc_n_points=4),
+        query_embedding=nn.Embedding(Q, 2 * d)))
+    _check_param_sums(mods, c["seed"], g["param_abs_sums"])
+    stack = _Stack(mods).to(dev)
+    video, mask, durations, _ = MG.d256_inputs()
+    video = video.to(dev).requires_grad_(True)
+    w_hs, w_mem = g["w_hs"].to(dev), g["w_mem"].to(dev)
+    outs = {}
+
+    def loss_fn(out):
+        outs["memory"], outs["hs"] = out
+        return (out[1].float() * w_hs).sum() + (out[0].float() * w_mem).sum()
+
+    # the bench's step: flat fp32 master weights with a bf16 shadow, bf16 autocast (train_step.py)
+    trainer = PKG.train_step.FlatGradTrainer(stack, loss_fn, use_bf16=True, graph=False)
+    PKG._trace.clear()
+    trainer._forward_backward((video, mask.to(dev), durations.to(dev)))
+    torch.cuda.synchronize()
+    hits = dict(PKG._trace.hits)
+    for path in EXPECTED_PATHS:
+        assert hits.get(path, 0) > 0, (path, hits)
+    assert not any(k.endswith("_cast") for k in hits), hits  # every Linear read the trainer's shadow
+
+    truth, ref16 = g["truth"], g["bf16"]
+    report = []
+    check("memory", outs["memory"].float(), truth["memory"], ref16["memory"], report=report)
+    check("hs", outs["hs"].float(), truth["hs"], ref16["hs"], report=report)
+    check("grad_video", video.grad, truth["grad_video"], ref16["grad_video"], report=report)
+    named = dict(mods.items())
+    n = 0
+    for mname, grads in truth["grads"].items():
+        params = dict(named[mname].named_parameters())
+        for k, t in grads.items():
+            p = params[k]
+            flat = p.grad.reshape(-1)
+            s = flat[MG.grad_sample_index(mname + "." + k, flat.numel()).to(dev)]
+            check(f"{mname}.{k}", s, t["sample"], ref16["grads"][mname][k]["sample"], slack=5e-3, report=report)
+            e_ours = abs(flat.double().norm().item() / t["norm"].item() - 1)
+            e_ref = abs(ref16["grads"][mname][k]["norm"].item() / t["norm"].item() - 1)
+            assert e_ours <= 1.5 * e_ref + 5e-3, (mname, k, "norm", e_ours, e_ref)
+            n += 1
+    assert n >= 60
+    worst = sorted(report, key=lambda r: r[1] - 1.5 * r[2])[-5:]
+    print("closest to the bound (name, ours vs fp64, reference bf16 vs fp64):", worst)
+
+
+def _caption_decoder(c, dev):
+    dec = M.unimodal_caption_decoder.UnimodalCaptionDecoder(
+        c["vocab"], seq_len=c["seq_len"], d_model=c["d_model"], depth=c["depth"], num_heads=c["heads"], mlp_ratio=4,
+        qkv_bias=True, pre_norm=False, return_intermediate=True)
+    return dec
+
+
+def test_caption_decoder_bf16_matches_reference_bf16(golden, dev):
+    g = golden("caption_bf16")
+    c = {k: (float(v) if k == "head_scale" else int(v)) for k, v in g["config"].items()}
+    dec = _caption_decoder(c, dev)
+    _check_param_sums(dec, c["seed"], g["param_abs_sums"], scale={"head.weight": c["head_scale"]})
+    dec = dec.to(dev)
+    tgt, memory, kmask = (t.to(dev) for t in MG.caption_inputs())
+    padding, tgt_mask = MG.caption_masks(tgt, c["pad"])
+    nxt = torch.cat([tgt[:, 1:], torch.full((c["N"], 1), c["eos"], device=dev)], 1)
+    live = nxt != c["pad"]
+    vsub = g["vocab_sample"].to(dev)
+
+    mem = memory.clone().requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = dec(tgt, mem, tgt_mask=tgt_mask, memory_mask=kmask[:, None, None, :], tgt_padding_mask=padding)
+    out = out.float()
+    p_t = out.gather(-1, nxt[None, :, :, None].expand(out.shape[0], -1, -1, 1))[..., 0]
+    (-(torch.log(p_t + 1e-9) * live).sum()).backward()
+    truth, ref16 = g["truth"], g["bf16"]
+    report = []
+    check("p_target", p_t, truth["p_target"], ref16["p_target"], report=report)
+    check("probs_sub", out[..., vsub], truth["probs_sub"], ref16["probs_sub"], report=report)
+    check("grad_memory", mem.grad, truth["grad_memory"], ref16["grad_memory"], report=report)
+    agree_ours = (out.argmax(-1).cpu() == truth["argmax"]).float().mean().item()
+    agree_ref = (ref16["argmax"] == truth["argmax"]).float().mean().item()
+    assert agree_ours >= agree_ref - 0.02, (agree_ours, agree_ref)
+    params = dict(dec.named_parameters())
+    for k, t in truth["grads"]["decoder"].items():
+        flat = params[k].grad.reshape(-1)
+        s = flat[MG.grad_sample_index("decoder." + k, flat.numel()).to(dev)]
+        check(k, s, t["sample"], ref16["grads"]["decoder"][k]["sample"], slack=5e-3, report=report)
+    print("caption bf16 (name, ours vs fp64, reference bf16 vs fp64):", report[:3])
+
+    # greedy decode: the KV-cached loop under bf16 autocast, judged by how far its path is from
+    # greedy under the fp64 model (the mirror in fp64, pinned against the reference below)
+    d64 = _caption_decoder(c, dev).double()
+    d64.load_state_dict(dec.state_dict())
+    mem64 = memory.double()
+    full64 = lambda cp, pm, tm: d64(cp, mem64, tgt_mask=tm, memory_mask=kmask[:, None, None, :],  # noqa: E731
+                                    tgt_padding_mask=pm)[-1]
+    L = c["seq_len"] - 1
+    for fe in (False, True):
+        key = "decode_faster" if fe else "decode_exact"
+        with torch.no_grad():
+            caps64, _ = d64.greedy_decode(mem64, kmask, c["bos"], c["eos"], c["pad"], L, fe)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                caps16, _ = dec.greedy_decode(memory, kmask, c["bos"], c["eos"], c["pad"], L, fe)
+        assert torch.equal(caps64.cpu(), g[key]["truth"]), key  # fp64: the reference's captions exactly
+        gap = MG.decode_gap(full64, caps16, c["pad"], c["eos"], fe)
+        ref_gap = g[key]["bf16_gap"].item()
+        print(f"{key}: bf16 path gap {gap:.4f} (reference bf16 {ref_gap:.4f})")
+        assert gap <= 1.5 * ref_gap + 0.05, (key, gap, ref_gap)

@@ -36,8 +36,42 @@ def test_zero_rows_matches_masked_fill(dev, dt, kind):
     v = x * 1  # a fresh non-leaf tensor, as the value projection's output
     out = ATT.mask_padding_rows(v, mask)
     torch.testing.assert_close(out, ref, rtol=0, atol=0)
+    g0 = g.clone()
     out.backward(g)
     torch.testing.assert_close(x.grad, g.masked_fill(mask[..., None], 0.0), rtol=0, atol=0)
+    assert torch.equal(g, g0)  # a gradient the caller holds is not written in place
+
+
+@pytest.mark.gpu
+def test_zero_rows_backward_in_place_only_on_private_msda_gradient(dev, monkeypatch):
+    """The backward zeroes in place only the gradient the MSDA backward allocated (tagged); a
+    second consumer of the masked value makes autograd hand over a fresh sum instead, which is
+    zeroed out of place — both give masked_fill's gradient."""
+    torch.manual_seed(3)
+    shapes, B, M, D, Lq, P = [32, 16, 8, 4], 2, 4, 16, 12, 4
+    S = sum(shapes)
+    mask = torch.rand(B, S, device=dev) < 0.3
+    loc = torch.rand(B, Lq, M, 4, P, device=dev)
+    aw = torch.rand(B, Lq, M, 4, P, device=dev)
+    gout = torch.randn(B, Lq, M * D, device=dev)
+    starts = [0, 32, 48, 56]
+    inplace = []
+    real = ATT._zero_rows
+    monkeypatch.setattr(ATT, "_zero_rows", lambda x, m: inplace.append(x.data_ptr()) or real(x, m))
+    for second in (False, True):
+        x = torch.randn(B, S, M * D, device=dev, requires_grad=True)
+        inplace.clear()
+        v = ATT.mask_padding_rows(x * 1, mask)
+        out = PKG.msda.msda_apply(v.view(B, S, M, D), shapes, starts, loc, aw)
+        loss = (out * gout).sum() + ((v * 3).sum() if second else 0)
+        loss.backward()
+        xr = x.detach().clone().requires_grad_(True)
+        vr = (xr * 1).masked_fill(mask[..., None], 0.0)
+        outr = PKG.msda.msda_apply(vr.view(B, S, M, D), shapes, starts, loc, aw)
+        ((outr * gout).sum() + ((vr * 3).sum() if second else 0)).backward()
+        torch.testing.assert_close(x.grad, xr.grad, rtol=0, atol=0)
+        # forward zeroing, plus the backward's in place only for the MSDA backward's own gradient
+        assert len(inplace) == (1 if second else 2)
 
 
 @pytest.mark.gpu

@@ -224,6 +224,67 @@ def test_full_size_properties(dev, shapes, B):
     np.testing.assert_allclose(gl[:1].cpu().numpy(), r_gl, rtol=2e-4, atol=2e-5 * max(shapes))
 
 
+def test_bf16_T4096_bench_instantiation_matches_oracle(dev):
+    """The configs[3] per-rank call exactly as the T=4096 bench runs it: bf16 values, B=8, T=4096
+    (S = Lq = 7680), M=8, D=64, P=4 — the pair backward with 8 slots a wave, one workgroup per
+    (b, m, level) and (c0, c1) / positions staged in the workspace (they do not fit LDS beside
+    the keys).  Clips 0 and 7 against the oracle on the same bf16-rounded inputs in fp32
+    (reference semantics attention.py:331-383)."""
+    shapes, B, M, D, P = [4096, 2048, 1024, 512], 8, 8, 64, 4
+    Lq = sum(shapes)
+    lib = PKG._native.load_library()
+    ws = lib.msda_hip_backward_workspace_bytes(PKG._native.DTYPE_TAGS[torch.bfloat16], B, Lq, M, D, Lq, 4, P)
+    assert ws >= B * M * 4 * Lq * P * 12  # the workspace-staged pair path (12 B per sample)
+    value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=41, lo=0.0, hi=1.0)
+    out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout)
+    assert gv.dtype == torch.bfloat16
+    eps = 2 ** -8
+    for b in (0, B - 1):
+        v32, g32 = value[b:b + 1].float(), gout[b:b + 1].float()
+        r_out = O.msda_forward(_np(v32), shapes, _np(loc[b:b + 1]), _np(aw[b:b + 1]))
+        r_gv, r_gl, r_ga = O.msda_backward(_np(v32), shapes, _np(loc[b:b + 1]), _np(aw[b:b + 1]), _np(g32))
+        np.testing.assert_allclose(_np(out[b:b + 1]), r_out, rtol=eps, atol=eps * np.abs(r_out).max())
+        np.testing.assert_allclose(_np(gv[b:b + 1]), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
+        np.testing.assert_allclose(_np(ga[b:b + 1]), r_ga, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(_np(gl[b:b + 1]), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_striped_levels_near_lds_budget_take_workspace(dev, dtype):
+    """Short (striped) levels with ~9.7K samples each and few (b, m, level) workgroups: the plan
+    needs the striped levels' wave-partial rows beside keys / (c0, c1) / positions, which does not
+    fit LDS, so the call takes the workspace-staged plan — the workspace query must ask for it
+    (the query once left the partial rows out, returned 0 bytes, and the call then ran
+    the sort / pull path without its workspace)."""
+    shapes, B, M, D, Lq, P = [100, 50, 25, 13], 1, 8, 64, 2425, 4
+    lib = PKG._native.load_library()
+    ws = lib.msda_hip_backward_workspace_bytes(PKG._native.DTYPE_TAGS[dtype], B, sum(shapes), M, D, Lq, 4, P)
+    assert ws > 0
+    value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, dtype, seed=43)
+    out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout)
+    v32, g32 = value.float(), gout.float()
+    r_gv, r_gl, r_ga = O.msda_backward(_np(v32), shapes, _np(loc), _np(aw), _np(g32))
+    eps = 2 ** -8 if dtype == torch.bfloat16 else 2e-5
+    np.testing.assert_allclose(_np(gv), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
+    np.testing.assert_allclose(_np(ga), r_ga, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gl), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))
+
+
+def test_backward_without_required_workspace_is_refused(dev):
+    """A call that needs a workspace and gets none returns an error (no device fault)."""
+    shapes, B, M, D, Lq, P = [100, 50, 25, 13], 1, 8, 64, 2425, 4
+    value, loc, aw, gout = (t.cuda() for t in rand_case(shapes, B, M, D, Lq, P, torch.float32, seed=44))
+    lib = PKG._native.load_library()
+    gv = torch.empty_like(value)
+    rc = lib.msda_hip_backward(value.data_ptr(), PKG._native.DTYPE_TAGS[torch.float32],
+                               PKG._native.host_i64_array(shapes), PKG._native.host_i64_array(O.level_starts(shapes)),
+                               4, loc.data_ptr(), aw.data_ptr(), gout.data_ptr(), gv.data_ptr(), None, None, None,
+                               B, sum(shapes), M, D, Lq, P, 0, PKG._native.stream_handle(value.device))
+    torch.cuda.synchronize()
+    assert rc != 0
+    assert b"workspace" in lib.msda_hip_last_error()
+
+
 def clustered_locations(B, Lq, M, shapes, P, seed):
     """Half the samples scattered, half piled onto a few positions per level: long lists on a few
     rows (split between slots in table mode, walked by one slot in run mode) beside short ones."""

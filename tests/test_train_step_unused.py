@@ -1,0 +1,128 @@
+"""FlatGradTrainer with parameters whose use changes from step to step (CPU; gloo world 2):
+the reference runs DDP with find_unused_parameters=True (main.py:85) and torch AdamW skips a
+parameter on exactly the steps where its grad is None.  The trainer finds the unused set after
+every eager step, reduces its buckets in a fixed order whatever order each rank's backward
+completes them in, and reduces again on a step where a parameter found unused gets a gradient."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+from torch import nn
+
+from conftest import PKG, ROOT
+
+
+class Branchy(nn.Module):
+    def __init__(self):
+        super().__init__()
+        torch.manual_seed(0)
+        self.a = nn.Linear(8, 8)
+        self.b = nn.Linear(8, 8)
+        self.c = nn.Linear(8, 1)
+
+    def forward(self, x, use_b):
+        h = torch.tanh(self.a(x))
+        if use_b:
+            h = h + self.b(x)
+        return self.c(h)
+
+
+def loss_fn(out):
+    return out.square().sum()
+
+
+def _x(seed):
+    return torch.randn(4, 8, generator=torch.Generator().manual_seed(seed))
+
+
+def _trainer(model, **kw):
+    return PKG.train_step.FlatGradTrainer(model, loss_fn, lr=1e-2, weight_decay=0.5, use_bf16=False, graph=False,
+                                          **kw)
+
+
+def test_unused_set_follows_each_step():
+    model = Branchy()
+    tr = _trainer(model)
+    b0 = model.b.weight.detach().clone()
+    tr.eager_step((_x(1), False))
+    assert sorted(tr._unused) == [2, 3]  # b.weight, b.bias
+    assert torch.equal(model.b.weight, b0)
+    tr.eager_step((_x(2), True))  # b used now: updated (the first version froze it for good)
+    assert tr._unused == []
+    b1 = model.b.weight.detach().clone()
+    assert not torch.equal(b1, b0)
+    with torch.no_grad():  # an external write (e.g. a checkpoint load) is kept, not reverted
+        model.b.weight.fill_(0.25)
+    tr.eager_step((_x(3), False))
+    assert torch.all(model.b.weight == 0.25)
+
+
+def test_capture_refuses_zero_warmup():
+    tr = PKG.train_step.FlatGradTrainer(Branchy(), loss_fn, use_bf16=False, graph=True)
+    with pytest.raises(ValueError, match="warmup"):
+        tr.capture((_x(1), True), warmup=0)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+# per step: which ranks use the b branch
+PLAN = [(True, False), (False, False), (True, False), (False, True)]
+
+
+def _rank_main(rank, world, port, out_path):
+    import sys
+    sys.path.insert(0, ROOT)
+    import importlib
+    pkg = importlib.import_module("multimodal-feature-learning_amd")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        model = Branchy()
+        # one bucket per parameter: b's buckets complete in a different order (or not at all) per rank
+        tr = pkg.train_step.FlatGradTrainer(model, loss_fn, lr=1e-2, weight_decay=0.5, use_bf16=False,
+                                            graph=False, bucket_mb=1e-6)
+        assert tr.overlap and len(tr.buckets) == len(tr.params)
+        res = []
+        for step, use in enumerate(PLAN):
+            before = tr.flat_param.clone()
+            tr._forward_backward((_x(10 * step + rank), use[rank]))
+            res.append(dict(params=before, grad=tr.flat_grad.clone(), unused=list(tr._unused), late=tr._late))
+            tr._update()
+        torch.save(res, f"{out_path}.{rank}")
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_ranks_with_different_unused_parameters():
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res")
+        mp.start_processes(_rank_main, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+        r = [torch.load(f"{out}.{k}", weights_only=True) for k in range(2)]
+    # reference: each rank's batch on the step's parameters, the gradients averaged
+    for step, use in enumerate(PLAN):
+        assert torch.equal(r[0][step]["params"], r[1][step]["params"])
+        grads = []
+        for rank in range(2):
+            m = Branchy()
+            off = 0
+            with torch.no_grad():
+                for p in m.parameters():
+                    p.copy_(r[0][step]["params"][off:off + p.numel()].view_as(p))
+                    off += p.numel()
+            loss_fn(m(_x(10 * step + rank), use[rank])).backward()
+            grads.append(torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
+                                    for p in m.parameters()]))
+        want = (grads[0] + grads[1]) / 2
+        for rank in range(2):
+            torch.testing.assert_close(r[rank][step]["grad"], want, rtol=1e-6, atol=1e-7)
+        assert r[0][step]["unused"] == r[1][step]["unused"] == ([] if any(use) else [2, 3])
+        # step 2: b was found unused after step 1 and rank 0 uses it again -> reduced once more
+        assert r[0][step]["late"] == (step == 2)
