@@ -48,10 +48,15 @@ WORKLOADS = {
                   "layer, 2 per decoder layer), d=512, 100 queries, 6 + 6 layers + heads, AdamW step",
     "sparse": "Sparse-DETR DVC (models/sparse, rho=0.3) T=1024 d=512, 100 queries, 6 + 6 layers, segment / count "
               "heads + mask-prediction loss through the DAM kernel, AdamW step (static top-k width: graph-captured)",
+    "dvc": "full UnimodalDeformableDVC training step at configs[1] (T=1024 d=512 L=4, 100 queries, 6 + 6 layers): "
+           "proposals, Hungarian matching of every decoder level, matched-segment crop, context mask, caption "
+           "decoder (depth 6, vocab 10000, seq_len 20) teacher-forced on every level, criterion-shaped loss, "
+           "backward, AdamW (engine.py:55-134)",
 }
 MODELS = {"video": "DeformableDVCCore (UnimodalDeformableDVC proposal path)",
           "multimodal": "MultimodalDVCCore (MultimodalDeformableDVC proposal path)",
-          "sparse": "SparseDVCCore (UnimodalSparseDVC proposal path)"}
+          "sparse": "SparseDVCCore (UnimodalSparseDVC proposal path)",
+          "dvc": "UnimodalDeformableDVC (full training forward)"}
 
 
 def parse():
@@ -63,10 +68,11 @@ def parse():
     p.add_argument("--T", type=int, default=1024)
     p.add_argument("--queries", type=int, default=100)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--config", default="video", choices=["video", "multimodal", "sparse"],
+    p.add_argument("--config", default="video", choices=["video", "multimodal", "sparse", "dvc"],
                    help="video: configs[1], the headline line.  multimodal: configs[2] (video + audio T_a=50, "
                         "SURVEY 8(d)); sparse: the Sparse-DETR DVC (rho=0.3; top-k width from the shapes, so it is "
-                        "graph-captured too).  Only 'video' is the BASELINE metric's workload.")
+                        "graph-captured too); dvc: the full UnimodalDeformableDVC training step (matching on the "
+                        "host: eager), with a per-phase breakdown.  Only 'video' is the BASELINE metric's workload.")
     p.add_argument("--audio-T", type=int, default=50, help="audio length (reference audio_rescale_len)")
     p.add_argument("--dropout", type=float, default=0.1)
     p.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU reference path (rank 0, N=1)")
@@ -105,12 +111,16 @@ def usable_cores():
 
 def build_model(args, device):
     torch.manual_seed(0)
+    if args.config == "dvc":
+        return PKG.dvc_core.build_dvc(num_queries=args.queries, T=args.T, dropout=args.dropout).to(device)
     core = {"video": PKG.dvc_core.DeformableDVCCore, "multimodal": PKG.dvc_core.MultimodalDVCCore,
             "sparse": PKG.dvc_core.SparseDVCCore}[args.config]
     return core(d_model=512, num_queries=args.queries, dropout=args.dropout).to(device)
 
 
 def build_batch(args, rank, device):
+    if args.config == "dvc":
+        return (PKG.dvc_core.synthetic_dvc_batch(args.batch, T=args.T, seed=1000 + rank, device=device),)
     video, mask, dur = PKG.dvc_core.synthetic_clips(args.batch, T=args.T, seed=1000 + rank, device=device)
     if args.config == "multimodal":
         audio, amask, _ = PKG.dvc_core.synthetic_clips(args.batch, T=args.audio_T, seed=2000 + rank, device=device)
@@ -118,9 +128,50 @@ def build_batch(args, rank, device):
     return video, mask, dur
 
 
-def loss_fn(args):
+def loss_fn(args, batch=None):
+    if args.config == "dvc":
+        return lambda result: PKG.dvc_core.dvc_workload_loss(result, batch[0])
     return {"video": PKG.dvc_core.workload_loss, "multimodal": PKG.dvc_core.multimodal_workload_loss,
             "sparse": PKG.dvc_core.sparse_workload_loss}[args.config]
+
+
+class PhaseTimer:
+    """HIP events on the current stream around the full DVC step's forward phases (bench --config
+    dvc): the wrapped callables record (phase, start, end); the rest of a step is backward + update."""
+
+    def __init__(self):
+        self.records, self.on = [], False
+
+    def wrap(self, name, fn):
+        def timed(*a, **kw):
+            if not self.on:
+                return fn(*a, **kw)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            r = fn(*a, **kw)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            self.records.append((name, e0, e1))
+            return r
+        return timed
+
+    def install(self, model):
+        import sys as _sys
+        mod = _sys.modules[type(model).__module__]
+        model.forward_proposals = self.wrap("proposals_fwd", model.forward_proposals)
+        model.matcher.match_levels = self.wrap("matching (cost on device, LSA on the host)", model.matcher.match_levels)
+        mod.segment_memory = self.wrap("segment crop", mod.segment_memory)
+        dec = model.unimodal_caption_decoder
+        dec.forward = self.wrap("caption_decoder_fwd", dec.forward)
+        model.context_mask_model.forward = self.wrap("context_mask_fwd", model.context_mask_model.forward)
+
+    def summary(self, steps, step_ms):
+        tot = {}
+        for name, e0, e1 in self.records:
+            tot[name] = tot.get(name, 0.0) + e0.elapsed_time(e1)
+        out = {k: round(v / steps, 3) for k, v in tot.items()}
+        out["backward + loss + AdamW (rest of the step)"] = round(step_ms - sum(out.values()), 3)
+        return out
 
 
 def cpu_baseline(args):
@@ -252,9 +303,14 @@ def main():
         for t in list(model.parameters()) + list(model.buffers()):
             dist.broadcast(t.data, src=0)
     use_bf16 = args.dtype == "bf16"
-    trainer = PKG.train_step.FlatGradTrainer(model, loss_fn(args), lr=1e-4, weight_decay=1e-4,
-                                             max_norm=0.1, use_bf16=use_bf16, graph=bool(args.graph))
     batch = build_batch(args, rank, device)
+    graph = bool(args.graph) and args.config != "dvc"  # the host LSA sits inside the dvc forward
+    trainer = PKG.train_step.FlatGradTrainer(model, loss_fn(args, batch), lr=1e-4, weight_decay=1e-4,
+                                             max_norm=0.1, use_bf16=use_bf16, graph=graph)
+    phases = None
+    if args.config == "dvc":
+        phases = PhaseTimer()
+        phases.install(model)
 
     trainer.capture(batch)  # eager warm-up steps + graph capture (no-op without --graph)
     for _ in range(args.warmup):
@@ -263,6 +319,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    if phases is not None:
+        phases.on = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         trainer.step(batch)
@@ -270,6 +328,8 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if phases is not None:
+        phases.on = False
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -304,11 +364,13 @@ def main():
             "config": {"workload": WORKLOADS[args.config], "model": MODELS[args.config],
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch, "seq_len": args.T,
                        "d_model": 512, "levels": 4, "queries": args.queries, "parallelism": f"dp{world}",
-                       "execution": "hip_graph" if args.graph else "eager", "gemm_solutions": gemm_sel,
+                       "execution": "hip_graph" if graph else "eager", "gemm_solutions": gemm_sel,
                        "conv_solver": "MIOpen find (cudnn.benchmark)" if args.conv_find else "MIOpen immediate"},
             "roofline": roofline(summary, traffic),
             "cpu_baseline": None,
         }
+        if phases is not None:
+            result["phases_ms_per_step"] = phases.summary(args.steps, 1000 * elapsed / args.steps)
         if args.cpu_baseline and world == 1 and args.config == "video":
             result["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(result), flush=True)

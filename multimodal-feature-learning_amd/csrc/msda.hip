@@ -41,6 +41,7 @@
 #include <string.h>
 
 #include "msda_hip.h"
+#include "msda_win.h"
 
 namespace {
 
@@ -2636,6 +2637,16 @@ int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, 
   return launch_status("backward pair");
 }
 
+// Row-block MFMA backward (msda_win.hip): bf16 values, D = 64, P <= 8, a call with more than 512
+// samples a level.  MSDA_HIP_BWD_WIN (read per call): "0" never, "1" wherever it applies;
+// unset: the default below.
+int win_env() { return env_int("MSDA_HIP_BWD_WIN", -1); }
+
+bool win_applies(int value_dtype, long long D, long long Lq, long long P) {
+  if (value_dtype != MSDA_DTYPE_BF16 || !msda_win_supported(1, D, P) || Lq * P <= 512) return false;
+  return win_env() == 1;
+}
+
 template <typename scalar_t, typename coord_t>
 int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
                  const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
@@ -2648,6 +2659,19 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     int minT = 1 << 30;
     for (int l = 0; l < pr.L; ++l) minT = min(minT, pr.lv.T[l]);
     const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1) || pr.Lq * pr.P <= 512;
+    if constexpr (std::is_same<scalar_t, bf16_t>::value) {
+      if (gval != nullptr && pr.B * pr.M * pr.S > 0 && !sparse && workspace != nullptr &&
+          win_applies(value_dtype, pr.D, pr.Lq, pr.P)) {
+        WinShape sh{};
+        sh.B = pr.B; sh.S = pr.S; sh.M = pr.M; sh.Lq = pr.Lq; sh.L = (int)pr.L; sh.P = (int)pr.P;
+        for (int l = 0; l < pr.L; ++l) {
+          sh.T[l] = pr.lv.T[l];
+          sh.start[l] = pr.lv.start[l];
+        }
+        msda_win_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, &sh, pad == MSDA_PAD_ZEROS, st);
+        return launch_status("backward rows (mfma)");
+      }
+    }
     PairPlan pp;
     if (gval != nullptr && pr.B * pr.M * pr.S > 0 && !(sparse && ns > 0) &&
         pair_plan(value_dtype, pr.B, pr.M, pr.Lq, pr.P, pr.D, pr.L, pr.lv.T, pr.S, workspace != nullptr, &pp))
@@ -3280,9 +3304,13 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
   (void)channels;
   if (batch <= 0 || spatial_size <= 0 || num_heads <= 0) return 0;
   PairPlan pp;
+  // the row-block MFMA path's tile intervals (when it may run) share the workspace
+  const size_t win = win_applies(value_dtype, channels, num_query, num_point)
+                         ? msda_win_workspace_bytes(batch, num_heads, num_levels, num_query) : 0;
   if (value_dtype != MSDA_DTYPE_F64 && pair_plan(value_dtype, batch, num_heads, num_query, num_point, channels,
                                                   num_levels, nullptr, spatial_size, true, &pp))
-    return pp.ws_bytes;
+    return std::max(pp.ws_bytes, win);
+  if (win > 0) return win;
   if (use_fused_gvalue(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point))
     return 0;
   return bwd_layout(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point).total;

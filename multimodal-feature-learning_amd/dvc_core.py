@@ -239,3 +239,94 @@ def sparse_workload_loss(out):
     mask_loss = torch.nn.functional.multilabel_soft_margin_loss(pred.float(), target.float())
     return (out["hs"].float().sum() + out["memory"].float().sum() + out["all_segments"].float().sum()
             + out["all_counts"].float().sum() + mask_loss)
+
+
+# --- the full DVC training step (proposals + matching + crop + caption decoder) -------------------
+
+DVC_SPECIALS = ['<unk>', '<pad>', '<bos>', '<eos>']
+
+
+def dvc_vocab(size=10000):
+    """A vocabulary of ``size`` tokens with the reference's special tokens first (pad 1, bos 2, eos 3;
+    dataset/anet_video.py builds it from the captions, ~10k words on ActivityNet)."""
+    return {w: i for i, w in enumerate(DVC_SPECIALS + [f"w{i}" for i in range(size - len(DVC_SPECIALS))])}
+
+
+def build_dvc(d_model=512, num_queries=100, num_classes=200, T=1024, enc_layers=6, dec_layers=6, caption_depth=6,
+              dropout=0.1, vocab_size=10000, seq_len=20, ff_dim=2048, num_heads=8):
+    """UnimodalDeformableDVC at the reference's training configuration (config/config_dvc_train.py:
+    dvc d_model 512, detr 6 + 6 layers / 8 heads / 4 levels / 4 points / ff 2048 / dropout 0.1,
+    caption decoder depth 6 / 8 heads / mlp 4 / dropout 0.1 / post-norm, matcher costs 1 / 5 / 2,
+    max_eseq_length 10, threshold 0.5) with BASELINE's 100 queries and T = video_rescale_len; the
+    differentiable context mask on (the only setting in which the reference wrapper runs)."""
+    from types import SimpleNamespace as ns
+    from .models.deformable.unimodal_deformable_dvc import UnimodalDeformableDVC
+    from .models.matcher import HungarianMatcher
+    detr = ns(feature_dim=d_model, d_model=d_model, num_heads=num_heads, num_feature_levels=4, dec_n_points=4,
+              enc_n_points=4, enc_layers=enc_layers, dec_layers=dec_layers, transformer_dropout_prob=dropout,
+              transformer_ff_dim=ff_dim, video_rescale_len=T, return_intermediate=True, hidden_dropout_prob=dropout,
+              layer_norm_eps=1e-12)
+    caption = ns(d_model=d_model, depth=caption_depth, num_heads=num_heads, mlp_ratio=4, qkv_bias=True,
+                 positional_embedding_dropout=dropout, attention_dropout=dropout, projection_dropout=dropout,
+                 bridge_dropout=dropout, mlp_dropout_1=dropout, mlp_dropout_2=dropout, pre_norm=False,
+                 model_official=None, weight_init=True, weight_load=False, emb_weights_req_grad=True,
+                 return_intermediate=True)
+    matcher = HungarianMatcher(cost_class=1, cost_segment=5, cost_giou=2, cost_alpha=0.25, cost_gamma=2.0)
+    return UnimodalDeformableDVC(['video'], num_queries, d_model, num_classes, True, matcher, 0.5, 10,
+                                 dvc_vocab(vocab_size), seq_len, None, detr, caption, use_differentiable_mask=True)
+
+
+def synthetic_dvc_batch(batch, T=1024, feature_dim=512, vocab_size=10000, seq_len=20, seed=0, device="cpu",
+                        events=(3, 4, 2, 5, 3, 4, 3, 4)):
+    """engine.py-shaped ``obj`` (dataset/anet_video.py:262-384 collate keys): features ~ N(0,1),
+    all frames valid, durations U(30, 240) s, ``events[b]`` target segments per clip (ActivityNet
+    averages ~3.7) with random centres / lengths and captions of 8-19 random words."""
+    video, mask, dur = synthetic_clips(batch, T=T, feature_dim=feature_dim, seed=seed)
+    g = torch.Generator().manual_seed(seed + 7)
+    targets, rows = [], []
+    for b in range(batch):
+        n = events[b % len(events)]
+        c = torch.rand(n, generator=g) * 0.6 + 0.2
+        ln = torch.rand(n, generator=g) * 0.3 + 0.05
+        targets.append({'segments': torch.stack([c, ln], 1).to(device), 'labels': torch.zeros(n, dtype=torch.long,
+                                                                                             device=device)})
+        for _ in range(n):
+            k = int(torch.randint(8, seq_len, (1,), generator=g))
+            rows.append(torch.cat([torch.tensor([2]), torch.randint(4, vocab_size, (k - 2,), generator=g),
+                                   torch.tensor([3]), torch.ones(seq_len - k, dtype=torch.long)]))
+    cap = torch.stack(rows)
+    length = torch.stack([torch.tensor([float(T), float(dur[b]), float(len(targets[b]['segments']))])
+                          for b in range(batch)])
+    return {'video_tensor': video.to(device), 'video_mask': mask.to(device), 'video_length': length.to(device),
+            'video_target': targets, 'cap_tensor': cap.to(device), 'cap_mask': (cap == 1).to(device)}
+
+
+def dvc_workload_loss(result, obj):
+    """A loss over every output of UnimodalDeformableDVC's training forward, shaped like the
+    reference criterion's terms (models/criterion.py, coefficients of config_dvc_train.py): L1 of
+    the matched segments (x5), -log p(label) of the matched predictions (x1), the count head's
+    cross-entropy (x2), the captions' -log p(word) over non-pad words (x1), the context mask's
+    BCE against the crop (x3) — on the last decoder level and every aux level."""
+    import torch.nn.functional as F
+    from .utils.preds_postprocess import get_src_permutation_idx
+    out, _, indices, indices_aux, _ = result
+    dev = out['pred_segments'].device
+    tgt_seg = torch.cat([t['segments'] for t in obj['video_target']]).float()
+    words = obj['cap_tensor'][:, 1:]
+    live = (~obj['cap_mask'][:, 1:]).float()
+    n_events = torch.tensor([len(t['segments']) for t in obj['video_target']], device=dev)
+    total = 0.0
+    levels = [(out, indices)] + list(zip(out.get('aux_outputs', []), indices_aux))
+    for o, ind in levels:
+        bidx, sidx = (t.to(dev) for t in get_src_permutation_idx(ind))
+        total = total + 5 * (o['pred_segments'][bidx, sidx].float() - tgt_seg).abs().mean()
+        total = total - torch.log(o['pred_logits'][bidx, sidx, 0].float().clamp_min(1e-9)).mean()
+        total = total + 2 * F.cross_entropy(o['pred_count'].float(), n_events.clamp_max(o['pred_count'].shape[-1] - 1))
+        if o.get('pred_captions') is not None:
+            p = o['pred_captions'].float().gather(-1, words[..., None])[..., 0]
+            total = total - (torch.log(p.clamp_min(1e-9)) * live).sum() / live.sum()
+    if 'pred_memory_mask' in out:
+        # the crop's kept tokens as the context target (criterion.py loss_contexts)
+        total = total + 3 * F.binary_cross_entropy_with_logits(out['pred_memory_mask'].float(),
+                                                              (out['pred_memory_mask'].detach() > 0).float())
+    return total

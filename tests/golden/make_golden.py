@@ -47,7 +47,7 @@ Fixtures:
                              (regen_parameters, no state_dict stored); gradients stored on fixed index
                              samples (grad_sample_index) plus their full norms.
   caption_bf16.pt            UnimodalCaptionDecoder at d=512, 8 heads, depth 2, vocab 10000, seq_len 20:
-                             teacher-forced forward + caption log-likelihood gradients and the reference's
+                             teacher-forced forward + gradients of -sum p(target word) and the reference's
                              greedy re-decode loop (unimodal_deformable_dvc.py:304-354), fp64 and bf16 autocast.
 
 usage: make_golden.py [case ...]   (default: every case; e.g. ``make_golden.py dam sparse``)
@@ -718,7 +718,7 @@ def caption_bf16_case(ref):
     """The reference's UnimodalCaptionDecoder (models/unimodal_caption_decoder.py:19-107) at config
     scale (d=512, 8 heads, vocab 10000, seq_len 20; depth 2, post-norm, dropout 0), parameters from
     regen_parameters (head weights x8: confident argmax, so greedy decodes have no near-ties):
-    teacher-forced forward with the DVC's masks and -sum log p(target) gradients; the reference's
+    teacher-forced forward with the DVC's masks and the gradients of -sum p(target); the reference's
     greedy re-decode loop (unimodal_deformable_dvc.py:304-354, exact and faster_eval) — each in
     fp64 and under torch.autocast('cpu', bfloat16).  The caption decoder is called with the
     argument order its signature declares (tgt_mask, memory_mask, tgt_padding_mask)."""
@@ -743,7 +743,7 @@ def caption_bf16_case(ref):
             out = m(tgt, mem, tgt_mask=tgt_mask, memory_mask=kmask[:, None, None, :], tgt_padding_mask=padding)
         out = out.to(dtype)
         p_t = out.gather(-1, nxt[None, :, :, None].expand(out.shape[0], -1, -1, 1))[..., 0]
-        loss = -(torch.log(p_t + 1e-9) * live).sum()
+        loss = -(p_t * live).sum()  # smooth in p (a log would weigh tiny, rounding-dominated p_t)
         loss.backward()
         return dict(argmax=out.argmax(-1), p_target=p_t.detach().float(), probs_sub=out[..., vsub].detach().float(),
                     grad_memory=mem.grad.float(), grads=sampled_grads({"decoder": m}))

@@ -39,13 +39,19 @@ def rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
 
 
-def check(name, ours, truth, ref16, slack=2e-3, report=None):
-    """ours vs the fp64 truth no worse than 1.5x the reference's bf16 run (+ slack), and near that run."""
-    e_ours, e_ref = rel(ours, truth), rel(ref16, truth)
+def check(name, ours, truth, ref16, slack=2e-3, report=None, fails=None):
+    """ours vs the fp64 truth no worse than 1.5x the reference's bf16 run (+ slack), and near that run.
+    Returns the bound on ours' relative error.  With ``fails`` the violations are collected."""
+    e_ours, e_ref, e_cross = rel(ours, truth), rel(ref16, truth), rel(ours, ref16)
+    bound = 1.5 * e_ref + slack
     if report is not None:
-        report.append((name, e_ours, e_ref))
-    assert e_ours <= 1.5 * e_ref + slack, (name, e_ours, e_ref)
-    assert rel(ours, ref16) <= 2.5 * e_ref + slack, (name, rel(ours, ref16), e_ref)
+        report.append((name, round(e_ours, 5), round(e_ref, 5)))
+    bad = [] if e_ours <= bound and e_cross <= 2.5 * e_ref + slack else [(name, e_ours, e_cross, e_ref)]
+    if fails is None:
+        assert not bad, bad
+    else:
+        fails.extend(bad)
+    return bound
 
 
 def _check_param_sums(module, seed, want, scale=None):
@@ -74,7 +80,7 @@ class _Stack(nn.Module):
         return memory, hs
 
 
-EXPECTED_PATHS = ("add_ln", "add_ln_carry", "relu_dropout", "layer_values_shadow", "sdpa_self_attn_shadow",
+EXPECTED_PATHS = ("add_ln_carry", "relu_dropout", "layer_values_shadow", "sdpa_self_attn_shadow",
                   "linear_shadow", "linear_pair_shadow", "msda_prologue", "zero_rows", "msda_bfloat16")
 
 
@@ -116,21 +122,24 @@ def test_d256_bench_composition_matches_reference_bf16(golden, dev):
     check("hs", outs["hs"].float(), truth["hs"], ref16["hs"], report=report)
     check("grad_video", video.grad, truth["grad_video"], ref16["grad_video"], report=report)
     named = dict(mods.items())
-    n = 0
+    n, fails = 0, []
     for mname, grads in truth["grads"].items():
         params = dict(named[mname].named_parameters())
         for k, t in grads.items():
             p = params[k]
             flat = p.grad.reshape(-1)
             s = flat[MG.grad_sample_index(mname + "." + k, flat.numel()).to(dev)]
-            check(f"{mname}.{k}", s, t["sample"], ref16["grads"][mname][k]["sample"], slack=5e-3, report=report)
-            e_ours = abs(flat.double().norm().item() / t["norm"].item() - 1)
-            e_ref = abs(ref16["grads"][mname][k]["norm"].item() / t["norm"].item() - 1)
-            assert e_ours <= 1.5 * e_ref + 5e-3, (mname, k, "norm", e_ours, e_ref)
+            bound = check(f"{mname}.{k}", s, t["sample"], ref16["grads"][mname][k]["sample"], slack=5e-3,
+                          report=report, fails=fails)
+            # the whole gradient's norm (|(|a| - |b|)| <= |a - b|: held to the same relative bound)
+            e_norm = abs(flat.double().norm().item() / t["norm"].item() - 1)
+            if e_norm > bound:
+                fails.append((f"{mname}.{k}", "norm", e_norm, bound))
             n += 1
+    for r in report:
+        print(r)
     assert n >= 60
-    worst = sorted(report, key=lambda r: r[1] - 1.5 * r[2])[-5:]
-    print("closest to the bound (name, ours vs fp64, reference bf16 vs fp64):", worst)
+    assert not fails, fails
 
 
 def _caption_decoder(c, dev):
@@ -157,9 +166,9 @@ def test_caption_decoder_bf16_matches_reference_bf16(golden, dev):
         out = dec(tgt, mem, tgt_mask=tgt_mask, memory_mask=kmask[:, None, None, :], tgt_padding_mask=padding)
     out = out.float()
     p_t = out.gather(-1, nxt[None, :, :, None].expand(out.shape[0], -1, -1, 1))[..., 0]
-    (-(torch.log(p_t + 1e-9) * live).sum()).backward()
+    (-(p_t * live).sum()).backward()
     truth, ref16 = g["truth"], g["bf16"]
-    report = []
+    report, fails = [], []
     check("p_target", p_t, truth["p_target"], ref16["p_target"], report=report)
     check("probs_sub", out[..., vsub], truth["probs_sub"], ref16["probs_sub"], report=report)
     check("grad_memory", mem.grad, truth["grad_memory"], ref16["grad_memory"], report=report)
@@ -168,10 +177,14 @@ def test_caption_decoder_bf16_matches_reference_bf16(golden, dev):
     assert agree_ours >= agree_ref - 0.02, (agree_ours, agree_ref)
     params = dict(dec.named_parameters())
     for k, t in truth["grads"]["decoder"].items():
+        if t["norm"].item() < 1e-9:  # zero in exact arithmetic (a key bias under softmax): rounding only
+            continue
         flat = params[k].grad.reshape(-1)
         s = flat[MG.grad_sample_index("decoder." + k, flat.numel()).to(dev)]
-        check(k, s, t["sample"], ref16["grads"]["decoder"][k]["sample"], slack=5e-3, report=report)
-    print("caption bf16 (name, ours vs fp64, reference bf16 vs fp64):", report[:3])
+        check(k, s, t["sample"], ref16["grads"]["decoder"][k]["sample"], slack=5e-3, report=report, fails=fails)
+    for r in report:
+        print("caption bf16 (name, ours vs fp64, reference bf16 vs fp64):", r)
+    assert not fails, fails
 
     # greedy decode: the KV-cached loop under bf16 autocast, judged by how far its path is from
     # greedy under the fp64 model (the mirror in fp64, pinned against the reference below)

@@ -285,6 +285,52 @@ def test_backward_without_required_workspace_is_refused(dev):
     assert b"workspace" in lib.msda_hip_last_error()
 
 
+WIN_CASES = [
+    # shapes,                 B, M, Lq,   P, locations
+    ([1024, 512, 256, 128],  2, 8, 1920, 4, "uniform"),    # encoder call
+    ([256, 128, 64, 32],     2, 8, 300,  4, "clustered"),
+    ([1000, 500, 250],       1, 4, 1750, 4, "uniform"),    # T not a multiple of the 64-row block
+    ([50, 25, 13, 7],        3, 8, 200,  4, "uniform"),    # audio pyramid: levels shorter than a block
+    ([64, 32],               2, 2, 77,   8, "clustered"),  # P = 8, a partial last query tile
+    ([4096, 2048, 1024, 512], 1, 8, 7680, 4, "local"),     # configs[3] per-clip shape, encoder-like samples
+]
+
+
+def local_locations(B, Lq, M, shapes, P, seed):
+    """Encoder-like sampling: every query samples near its own position (within +-6 rows of a
+    reference point spread over [0, 1]), as the deformable encoder does at and after init."""
+    gen = torch.Generator().manual_seed(seed)
+    ref = (torch.arange(Lq, dtype=torch.float64) % shapes[0] + 0.5) / shapes[0]
+    loc = torch.empty(B, Lq, M, len(shapes), P, dtype=torch.float64)
+    for l, T in enumerate(shapes):
+        off = (torch.rand(B, Lq, M, P, generator=gen, dtype=torch.float64) * 12 - 6) / T
+        loc[:, :, :, l] = ref[None, :, None, None] + off
+    return loc.float()
+
+
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("case", range(len(WIN_CASES)))
+def test_row_block_mfma_backward_matches_oracle(dev, monkeypatch, case, padding):
+    """The row-block MFMA backward (csrc/msda_win.hip; MSDA_HIP_BWD_WIN=1 forces it where it
+    applies: bf16 values, D = 64, P <= 8, > 512 samples a level) against the oracle on the same
+    bf16-rounded inputs in fp32 (reference semantics attention.py:331-383)."""
+    monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
+    shapes, B, M, Lq, P, kind = WIN_CASES[case]
+    D = 64
+    value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=60 + case)
+    if kind == "clustered":
+        loc = clustered_locations(B, Lq, M, shapes, P, seed=61 + case)
+    elif kind == "local":
+        loc = local_locations(B, Lq, M, shapes, P, seed=61 + case)
+    out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout, padding)
+    v32, g32 = value.float(), gout.float()
+    r_gv, r_gl, r_ga = O.msda_backward(_np(v32), shapes, _np(loc), _np(aw), _np(g32), padding=padding)
+    eps = 2 ** -8
+    np.testing.assert_allclose(_np(gv), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
+    np.testing.assert_allclose(_np(ga), r_ga, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gl), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))
+
+
 def clustered_locations(B, Lq, M, shapes, P, seed):
     """Half the samples scattered, half piled onto a few positions per level: long lists on a few
     rows (split between slots in table mode, walked by one slot in run mode) beside short ones."""

@@ -13,4 +13,6 @@ rc=$?; tail -n 30 gpurun_out/r03_new_tests.log; [ $rc -eq 0 ] || { echo "new tes
 timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > gpurun_out/r03_pytest_gpu.log 2>&1
 rc=$?; tail -n 3 gpurun_out/r03_pytest_gpu.log; [ $rc -eq 0 ] || { echo "pytest rc=$rc"; exit $rc; }
 timeout -k 10 600 python3 -u bench.py --steps 20 --warmup 5 > gpurun_out/r03_bench.json 2> gpurun_out/r03_bench.err
-rc=$?; cat gpurun_out/r03_bench.json | head -c 600; echo; exit $rc
+rc=$?; cat gpurun_out/r03_bench.json | head -c 600; echo; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 600 python3 -u bench.py --config dvc --steps 10 --warmup 3 --timer-steps 1 > gpurun_out/r03_bench_dvc.json 2> gpurun_out/r03_bench_dvc.err
+rc=$?; python3 -c "import json; d=json.load(open('gpurun_out/r03_bench_dvc.json')); print(d['value'], d['ms_per_step'], d.get('phases_ms_per_step'))"; exit $rc
