@@ -2643,7 +2643,7 @@ int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, 
 int win_env() { return env_int("MSDA_HIP_BWD_WIN", -1); }
 
 bool win_applies(int value_dtype, long long D, long long Lq, long long P) {
-  if (value_dtype != MSDA_DTYPE_BF16 || !msda_win_supported(1, D, P) || Lq * P <= 512) return false;
+  if (value_dtype != MSDA_DTYPE_BF16 || !msda_win_supported(1, D, P, Lq) || Lq * P <= 512) return false;
   return win_env() == 1;
 }
 

@@ -39,18 +39,18 @@
 namespace {
 
 constexpr int kQT = 32;       // queries per tile
-constexpr int kRB = 64;       // value rows per workgroup (4 waves x 16)
 constexpr int kThreads = 256;
-constexpr int kDotRows = 80;  // rows r0 .. r0+79 in the dot products (r0+64 is the last needed)
 constexpr int kGS = 144;      // LDS row stride (bytes) of grad_out / value rows: 16-B aligned, spreads banks
-constexpr int kDS = kDotRows + 1;  // floats per dot row (padded)
 constexpr int kMaxSamp = 256;      // samples per tile (32 x P, P <= 8)
 constexpr int kNone = 1 << 29;     // base of an absent sample
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
-typedef __attribute__((ext_vector_type(4))) short s16x4;
-typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+// (the v4i16 form of the transposed read with per-element bit casts into a bf16x8 was compiled
+// into a splat of element 0 — tools/probes/mfma_tr_probe.hip; the v4bf16 form + shufflevector is exact)
 
 __device__ __forceinline__ unsigned xcd_block(unsigned orig, unsigned nwg) {
   const unsigned xcd = orig % 8u, q = nwg / 8u, r = nwg % 8u;
@@ -157,23 +157,33 @@ __device__ __forceinline__ short bf16_bits(float x) {  // round to nearest even 
 }
 __device__ __forceinline__ float bf16_val(short h) { return __uint_as_float(((uint32_t)(uint16_t)h) << 16); }
 
-template <bool ZEROS, bool COORDS>
-__global__ __launch_bounds__(kThreads) void win_bwd_kernel(
+// One wave per 16-row block of one (b, m, level): barrier-free (every LDS exchange is inside the
+// wave, ordered by the wave's own LDS queue), so many blocks per CU overlap their latencies, and
+// a coarse level's block meets about as many query tiles as a fine level's (16 rows each).
+// The next visit's coordinates and grad_out rows are loaded into registers while the current
+// visit computes.
+constexpr int kRW = 16;          // rows per block (one wave)
+constexpr int kVRows = kRW + 1;  // value rows r0 .. r0+16 in the dot products
+constexpr int kDSW = kVRows;     // dots kept per query: rows r0 .. r0+16
+
+// Orders one wave's LDS writes before its later LDS reads: the wave's LDS operations execute in
+// issue order, so this only has to stop the compiler from moving LDS accesses across it (no
+// wait on the global loads in flight).
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
+
+template <bool ZEROS, bool COORDS, int P>
+__global__ __launch_bounds__(64) void win_bwd_kernel(
     const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     const uint16_t* __restrict__ gout, uint16_t* __restrict__ gval, float* __restrict__ gloc,
     float* __restrict__ gaw, const int2* __restrict__ tiles, const WinShape sh) {
-  __shared__ __attribute__((aligned(16))) unsigned char s_g[kQT * kGS];        // grad_out rows of the tile
-  __shared__ __attribute__((aligned(16))) unsigned char s_v[kDotRows * kGS];   // the block's value rows
-  __shared__ float s_d[kQT * kDS];                                             // dots [q][row - r0]
-  __shared__ int s_base[kMaxSamp + 1];
-  __shared__ float s_c0[kMaxSamp + 1], s_c1[kMaxSamp + 1];
-  __shared__ unsigned short s_list[4][kMaxSamp + kQT];                         // per-wave compacted samples
-  __shared__ unsigned short s_visit[kThreads];
-  __shared__ int s_nvisit[kThreads / 64];
+  constexpr int NS = kQT * P;                  // samples per tile
+  constexpr int SPL = NS >= 64 ? NS / 64 : 1;  // samples per lane
+  __shared__ __attribute__((aligned(16))) unsigned char s_g[kQT * kGS];     // grad_out rows of the tile
+  __shared__ __attribute__((aligned(16))) unsigned char s_v[kVRows * kGS];  // the block's value rows
+  __shared__ float s_d[kQT * kDSW];                                         // dots [q][row - r0]
+  __shared__ int4 s_rec[NS + kQT];  // compacted samples {base - r0, c0 | c1 hi, c0 | c1 lo, query}, padded
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  // workgroup -> (b, m, level, block): (b, m) major, so a clip-head's workgroups share one XCD's L2
+  const int lane = threadIdx.x, g = lane >> 4, li = lane & 15;
   const unsigned id = xcd_block(blockIdx.x, gridDim.x);
   const unsigned bm = id / (unsigned)sh.nblk;
   unsigned rem = id % (unsigned)sh.nblk;
@@ -182,172 +192,207 @@ __global__ __launch_bounds__(kThreads) void win_bwd_kernel(
   const int k = (int)rem - sh.blk0[l];
   const int m = (int)(bm % (unsigned)sh.M);
   const long long b = bm / (unsigned)sh.M;
-  const int T = sh.T[l], P = sh.P, LP = sh.L * sh.P, nsamp = kQT * P;
-  const int r0 = k * kRB, rw0 = r0 + 16 * wave;
-  const int rs = sh.M * 64;  // value / grad_out row stride (elements)
+  const int T = sh.T[l], LP = sh.L * P;
+  const int r0 = k * kRW;
+  const int rs = sh.M * 64;                           // grad_out / value row stride (elements)
+  const int qstride = sh.M * LP;                      // coordinate stride of one query
   const uint16_t* __restrict__ vl = value + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
   const uint16_t* __restrict__ gb = gout + (b * sh.Lq * sh.M + m) * 64;
-  const long long cbase = (b * sh.Lq * sh.M + m) * (long long)LP + l * P;  // + q * M * LP + p
+  const long long cbase = (b * sh.Lq * sh.M + m) * (long long)LP + l * P;
+  // per-lane constant parts of the addresses
+  int soff[SPL];
+#pragma unroll
+  for (int j = 0; j < SPL; ++j) {
+    const int s = lane + 64 * j;
+    soff[j] = (s / P) * qstride + s % P;
+  }
+  const int grow = lane >> 3, gch = lane & 7;  // grad_out piece (row grow + 8 i, 16-byte chunk gch)
 
-  // the block's value rows r0 .. r0+79 (zeros outside the level), staged once
-  for (int c = tid; c < kDotRows * 8; c += kThreads) {
+  // the block's value rows r0 .. r0+16 (zeros outside the level)
+  for (int c = lane; c < kVRows * 8; c += 64) {
     const int row = c >> 3, ch = c & 7, x = r0 + row;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (x < T) v = *reinterpret_cast<const uint4*>(vl + (long long)x * rs + ch * 8);
     *reinterpret_cast<uint4*>(s_v + row * kGS + ch * 16) = v;
   }
-  if (tid == 0) {  // the padding sample of the compacted lists: no tap anywhere
-    s_base[kMaxSamp] = kNone;
-    s_c0[kMaxSamp] = 0.f;
-    s_c1[kMaxSamp] = 0.f;
-  }
+  // the query tiles whose row interval meets [r0, r0 + 15]: 64 tiles per ballot mask, walked
+  // bit by bit (wave-uniform); the next visit is known one visit ahead for the prefetch
+  const int2* __restrict__ tl = tiles + ((long long)bm * sh.L + l) * sh.ntile;
+  auto chunk_mask = [&](int t0) -> unsigned long long {
+    const int t = min(t0 + lane, sh.ntile - 1);
+    const int2 iv = tl[t];
+    return __ballot(t0 + lane < sh.ntile && iv.x <= r0 + kRW - 1 && iv.y >= r0);
+  };
+  int cur_t0 = 0;
+  unsigned long long mask = chunk_mask(0);
+  auto next_tile = [&]() -> int {  // pops the next visit (-1 when done)
+    while (mask == 0ull) {
+      cur_t0 += 64;
+      if (cur_t0 >= sh.ntile) return -1;
+      mask = chunk_mask(cur_t0);
+    }
+    const int t = cur_t0 + __builtin_ctzll(mask);
+    mask &= mask - 1ull;
+    return t;
+  };
 
   f32x4 acc[4];
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int2* __restrict__ tl = tiles + ((long long)bm * sh.L + l) * sh.ntile;
-  for (int t0 = 0; t0 < sh.ntile; t0 += kThreads) {
-    // the tiles of this chunk whose row interval meets [r0, r0 + 63]
-    {
-      const int t = t0 + tid;
-      bool hit = false;
-      if (t < sh.ntile) {
-        const int2 iv = tl[t];
-        hit = iv.x <= r0 + kRB - 1 && iv.y >= r0;
+  // a visit's inputs in registers: SPL samples and 4 grad_out pieces per lane
+  float rl[SPL], ra[SPL];
+  uint4 rg[4];
+  auto fetch = [&](int tile) {
+    const int q0 = tile * kQT;
+    const float* __restrict__ lt = loc + cbase + (long long)q0 * qstride;
+    const float* __restrict__ at = aw + cbase + (long long)q0 * qstride;
+    const uint16_t* __restrict__ gt = gb + (long long)q0 * rs;
+    if (q0 + kQT <= sh.Lq) {  // a whole tile (wave-uniform)
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) {
+        const bool in = NS >= 64 || lane < NS;
+        rl[j] = in ? lt[soff[j]] : 0.f;
+        ra[j] = in ? at[soff[j]] : 0.f;
       }
-      const unsigned long long bal = __ballot(hit);
-      if (lane == 0) s_nvisit[wave] = __popcll(bal);
-      __syncthreads();
-      int before = 0;
-      for (int w = 0; w < wave; ++w) before += s_nvisit[w];
-      if (hit) s_visit[before + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)(t - t0);
-      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rg[i] = *reinterpret_cast<const uint4*>(gt + (grow + 8 * i) * rs + gch * 8);
+    } else {
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) {
+        const int s = lane + 64 * j;
+        const bool in = (NS >= 64 || lane < NS) && q0 + s / P < sh.Lq;
+        rl[j] = in ? lt[soff[j]] : 0.f;
+        ra[j] = in ? at[soff[j]] : 0.f;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        rg[i] = q0 + grow + 8 * i < sh.Lq ? *reinterpret_cast<const uint4*>(gt + (grow + 8 * i) * rs + gch * 8)
+                                         : make_uint4(0u, 0u, 0u, 0u);
     }
-    const int nvisit = s_nvisit[0] + s_nvisit[1] + s_nvisit[2] + s_nvisit[3];
+  };
+  int tile = next_tile();
+  if (tile >= 0) fetch(tile);
 
-    for (int vi = 0; vi < nvisit; ++vi) {
-      const int tile = t0 + s_visit[vi];
-      const int q0 = tile * kQT;
-      // 1. the tile's samples (one per thread) and its grad_out rows (one 16-B piece per thread)
-      Taps tp;
-      float a = 0.f;
-      int q = 0, p = 0;
-      bool have = false;
-      if (tid < nsamp) {
-        q = q0 + tid / P;
-        p = tid % P;
-        have = q < sh.Lq;
-        if (have) {
-          const long long o = cbase + (long long)q * sh.M * LP + p;
-          a = aw[o];
-          tp = make_taps<ZEROS>(loc[o], T);
-        }
-        s_base[tid] = have && tp.live ? tp.base : kNone;
-        s_c0[tid] = have && tp.ok0 ? a * tp.w0 : 0.f;
-        s_c1[tid] = have && tp.ok1 ? a * tp.w1 : 0.f;
+  while (tile >= 0) {
+    const int q0 = tile * kQT;
+    // 1. the visit's taps (kept in registers) and grad_out rows (into LDS); the samples with a tap
+    // in the block's 16 rows compacted into records
+    Taps tp[SPL];
+    float a[SPL];
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < SPL; ++j) {
+      const int s = lane + 64 * j;
+      const bool in = (NS >= 64 || lane < NS) && q0 + s / P < sh.Lq;
+      tp[j] = make_taps<ZEROS>(rl[j], T);
+      tp[j].live = tp[j].live && in;
+      a[j] = ra[j];
+      const int dr = tp[j].base - r0;
+      const bool sel = tp[j].live && dr >= -1 && dr <= kRW - 1;
+      const unsigned long long bal = __ballot(sel);
+      if (sel) {  // record: row offset, bf16 hi parts (c0 | c1 << 16), lo parts, query row of the tile
+        const float c0 = tp[j].ok0 ? a[j] * tp[j].w0 : 0.f;
+        const float c1 = tp[j].ok1 ? a[j] * tp[j].w1 : 0.f;
+        const uint32_t h0 = (uint16_t)bf16_bits(c0), h1 = (uint16_t)bf16_bits(c1);
+        const uint32_t l0 = (uint16_t)bf16_bits(c0 - bf16_val((short)h0));
+        const uint32_t l1 = (uint16_t)bf16_bits(c1 - bf16_val((short)h1));
+        s_rec[n + __popcll(bal & ((1ull << lane) - 1ull))] = make_int4(dr, (int)(h0 | (h1 << 16)),
+                                                                       (int)(l0 | (l1 << 16)), s / P);
       }
-      {
-        const int row = tid >> 3, ch = tid & 7;
-        uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (q0 + row < sh.Lq) v = *reinterpret_cast<const uint4*>(gb + (long long)(q0 + row) * rs + ch * 8);
-        *reinterpret_cast<uint4*>(s_g + row * kGS + ch * 16) = v;
-      }
-      __syncthreads();
+      n += __popcll(bal);
+    }
+    const int nk = (n + 31) >> 5;
+    if (lane < nk * 32 - n) s_rec[n + lane] = make_int4(kNone, 0, 0, 0);  // pad to whole MFMA steps
+#pragma unroll
+    for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(s_g + (grow + 8 * i) * kGS + gch * 16) = rg[i];
+    wave_lds_fence();
+    const int next = next_tile();
+    if (next >= 0) fetch(next);  // in flight during the compute below
 
-      // 2a. grad_value of the wave's 16 rows: the samples with a tap in them, 32 per MFMA step
-      if (rw0 < T) {
-        int n = 0;
-        for (int s0 = 0; s0 < nsamp; s0 += 64) {
-          const int s = s0 + lane;
-          const int bs = s < nsamp ? s_base[s] : kNone;
-          const bool sel = bs >= rw0 - 1 && bs <= rw0 + 15;
-          const unsigned long long bal = __ballot(sel);
-          if (sel) s_list[wave][n + __popcll(bal & ((1ull << lane) - 1ull))] = (unsigned short)s;
-          n += __popcll(bal);
+    // 2a. grad_value of the 16 rows += C . G, 32 compacted samples per MFMA step
+    for (int ks = 0; ks < nk; ++ks) {
+      const int4* rec = &s_rec[ks * 32 + 8 * g];
+      u32x4 hw, lw;  // this lane's row (li) of C: per sample c0 on its base row, c1 on the next
+#pragma unroll
+      for (int j2 = 0; j2 < 4; ++j2) {
+        uint32_t hp = 0u, lp = 0u;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int4 r = rec[2 * j2 + e];
+          const int sh16 = r.x == li ? 0 : 16;  // which half (c0 or c1), if any, lands on row li
+          const bool any = r.x == li || r.x + 1 == li;
+          hp |= any ? (((uint32_t)r.y >> sh16) & 0xffffu) << (16 * e) : 0u;
+          lp |= any ? (((uint32_t)r.z >> sh16) & 0xffffu) << (16 * e) : 0u;
         }
-        if (n > 0) {
-          const int nk = (n + 31) >> 5;
-          if (lane < nk * 32 - n) s_list[wave][n + lane] = (unsigned short)kMaxSamp;  // pad to whole steps
-          for (int ks = 0; ks < nk; ++ks) {
-            const unsigned short* lst = &s_list[wave][ks * 32 + 8 * g];
-            bf16x8 ahi, alo;
+        hw[j2] = hp;
+        lw[j2] = lp;
+      }
+      const bf16x8 ahi = __builtin_bit_cast(bf16x8, hw), alo = __builtin_bit_cast(bf16x8, lw);
+      // rows of the transposed reads: lane 4q'+pp of the group names record 8g + 4h + q'
+      const int qq = li >> 2, pp = li & 3;
+      const int rowa = rec[qq].w, rowb = rec[4 + qq].w;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const int s = lst[j];
-              const int dr = s_base[s] - rw0;
-              const float c = (dr == li ? s_c0[s] : 0.f) + (dr + 1 == li ? s_c1[s] : 0.f);
-              const short h = bf16_bits(c);
-              ahi[j] = __builtin_bit_cast(__bf16, h);
-              alo[j] = __builtin_bit_cast(__bf16, bf16_bits(c - bf16_val(h)));
-            }
-            // rows of the transposed reads: lane 4q'+pp of the group names sample 8g + 4h + q'
-            const int qq = (li >> 2), pp = li & 3;
-            const int sa = lst[qq], sb = lst[4 + qq];
-            const int ra = sa < kMaxSamp ? sa / P : 0, rb = sb < kMaxSamp ? sb / P : 0;
+      for (int cb = 0; cb < 4; ++cb) {
+        const int col = (cb * 16 + 4 * pp) * 2;
+        const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(s_g + rowa * kGS + col));
+        const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(s_g + rowb * kGS + col));
+        const bf16x8 bv = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, acc[cb], 0, 0, 0);
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, acc[cb], 0, 0, 0);
+      }
+    }
+    // 2b. dots of the tile's 32 queries with rows r0 .. r0+16 (2 query halves x 2 row blocks; of
+    // the second block only row r0+16 is kept, its other columns read row r0+16 again)
+    if (COORDS) {
 #pragma unroll
-            for (int cb = 0; cb < 4; ++cb) {
-              const int col = (cb * 16 + 4 * pp) * 2;
-              const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(s_g + ra * kGS + col));
-              const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(s_g + rb * kGS + col));
-              bf16x8 bv;
+      for (int tt = 0; tt < 4; ++tt) {
+        const int qh = tt >> 1, cb = tt & 1;
+        const int vrow = cb == 0 ? li : kRW;
+        f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-              for (int j = 0; j < 4; ++j) {
-                bv[j] = __builtin_bit_cast(__bf16, x0[j]);
-                bv[4 + j] = __builtin_bit_cast(__bf16, x1[j]);
-              }
-              acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, acc[cb], 0, 0, 0);
-              acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, acc[cb], 0, 0, 0);
-            }
-          }
+        for (int ks = 0; ks < 2; ++ks) {
+          const int off = (ks * 32 + 8 * g) * 2;
+          const bf16x8 av = *reinterpret_cast<const bf16x8*>(s_g + (qh * 16 + li) * kGS + off);
+          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(s_v + vrow * kGS + off);
+          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, d, 0, 0, 0);
+        }
+        if (cb == 0 || li == 0) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) s_d[(qh * 16 + 4 * g + j) * kDSW + cb * 16 + li] = d[j];
         }
       }
-      // 2b. dots of the tile's 32 queries with rows r0 .. r0+79: 2 query halves x 5 row blocks
-      if (COORDS) {
-        for (int tt = wave; tt < 10; tt += 4) {
-          const int qh = tt / 5, cb = tt % 5;
-          f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            const int off = (ks * 32 + 8 * g) * 2;
-            const bf16x8 av = *reinterpret_cast<const bf16x8*>(s_g + (qh * 16 + li) * kGS + off);
-            const bf16x8 bv = *reinterpret_cast<const bf16x8*>(s_v + (cb * 16 + li) * kGS + off);
-            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, d, 0, 0, 0);
-          }
-#pragma unroll
-          for (int j = 0; j < 4; ++j) s_d[(qh * 16 + 4 * g + j) * kDS + cb * 16 + li] = d[j];
-        }
-      }
-      __syncthreads();
-
+      wave_lds_fence();
       // 3. coordinate gradients of the samples this block owns (base row in it; the level's first
       // block also owns the samples with no tap on the map)
-      if (COORDS && tid < nsamp && have) {
-        const bool own = tp.live ? (tp.base >= r0 && tp.base < r0 + kRB) || (tp.base < 0 && k == 0) : k == 0;
-        if (own) {
-          const int qi = tid / P;
-          const float d0 = tp.ok0 ? s_d[qi * kDS + tp.base - r0] : 0.f;
-          const float d1 = tp.ok1 ? s_d[qi * kDS + tp.base + 1 - r0] : 0.f;
-          const long long o = cbase + (long long)q * sh.M * LP + p;
-          if (gaw != nullptr) gaw[o] = d0 * tp.w0 + d1 * tp.w1;
-          if (gloc != nullptr) gloc[o] = ((d1 - d0) * a) * tp.gmul;
+      const long long tb = cbase + (long long)q0 * qstride;
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) {
+        const int s = lane + 64 * j;
+        const bool in = (NS >= 64 || lane < NS) && q0 + s / P < sh.Lq;
+        const Taps& t = tp[j];
+        const bool own = t.live ? (t.base >= r0 && t.base < r0 + kRW) || (t.base < 0 && k == 0) : k == 0;
+        if (in && own) {
+          const int qi = s / P;
+          const float d0 = t.ok0 ? s_d[qi * kDSW + t.base - r0] : 0.f;
+          const float d1 = t.ok1 ? s_d[qi * kDSW + t.base + 1 - r0] : 0.f;
+          if (gaw != nullptr) gaw[tb + soff[j]] = d0 * t.w0 + d1 * t.w1;
+          if (gloc != nullptr) gloc[tb + soff[j]] = ((d1 - d0) * a[j]) * t.gmul;
         }
       }
-      __syncthreads();  // the next visit overwrites the tile's LDS
     }
-    __syncthreads();  // every wave has read this chunk's visit count before the next chunk writes it
+    wave_lds_fence();  // this visit's LDS reads before the next visit's writes
+    tile = next;
   }
 
-  // grad_value rows rw0 + 4g + j, channels 16 cb + li (every row of the block, zeros included)
-  if (rw0 < T) {
-    uint16_t* __restrict__ gvl = gval + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
+  // grad_value rows r0 + 4g + j, channels 16 cb + li (every row of the block, zeros included)
+  uint16_t* __restrict__ gvl = gval + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int x = rw0 + 4 * g + j;
-      if (x < T) {
+  for (int j = 0; j < 4; ++j) {
+    const int x = r0 + 4 * g + j;
+    if (x < T) {
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) gvl[(long long)x * rs + cb * 16 + li] = (uint16_t)bf16_bits(acc[cb][j]);
-      }
+      for (int cb = 0; cb < 4; ++cb) gvl[(long long)x * rs + cb * 16 + li] = (uint16_t)bf16_bits(acc[cb][j]);
     }
   }
 }
@@ -359,8 +404,8 @@ size_t msda_win_workspace_bytes(long long B, long long M, long long L, long long
   return (size_t)(B * M * L * ntile) * sizeof(int2);
 }
 
-int msda_win_supported(int value_dtype_is_bf16, long long D, long long P) {
-  return value_dtype_is_bf16 && D == 64 && P >= 1 && P <= kMaxSamp / kQT;
+int msda_win_supported(int value_dtype_is_bf16, long long D, long long P, long long Lq) {
+  return value_dtype_is_bf16 && D == 64 && (P == 1 || P == 2 || P == 4 || P == 8) && Lq < (1LL << 24);
 }
 
 int msda_win_backward(const void* value, const void* loc, const void* aw, const void* gout, void* gval,
@@ -370,7 +415,7 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   int nb = 0;
   for (int l = 0; l < sh.L; ++l) {
     sh.blk0[l] = nb;
-    nb += (sh.T[l] + kRB - 1) / kRB;
+    nb += (sh.T[l] + kRW - 1) / kRW;
   }
   sh.blk0[sh.L] = nb;
   sh.nblk = nb;
@@ -395,13 +440,23 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   auto* gv = static_cast<uint16_t*>(gval);
   auto* gl = static_cast<float*>(gloc);
   auto* ga = static_cast<float*>(gaw);
-#define WIN_LAUNCH(Z, C) \
-  hipLaunchKernelGGL((win_bwd_kernel<Z, C>), dim3(grid), dim3(kThreads), 0, st, v, lc, a, g, gv, gl, ga, tiles, sh)
+#define WIN_LAUNCH(Z, C, N) \
+  hipLaunchKernelGGL((win_bwd_kernel<Z, C, N>), dim3(grid), dim3(64), 0, st, v, lc, a, g, gv, gl, ga, tiles, sh)
+#define WIN_SPL(Z, C)                                                   \
+  do {                                                                  \
+    switch (sh.P) {                                                     \
+      case 1: WIN_LAUNCH(Z, C, 1); break;                               \
+      case 2: WIN_LAUNCH(Z, C, 2); break;                               \
+      case 4: WIN_LAUNCH(Z, C, 4); break;                               \
+      default: WIN_LAUNCH(Z, C, 8); break;                              \
+    }                                                                   \
+  } while (0)
   if (zeros) {
-    if (coords) WIN_LAUNCH(true, true); else WIN_LAUNCH(true, false);
+    if (coords) WIN_SPL(true, true); else WIN_SPL(true, false);
   } else {
-    if (coords) WIN_LAUNCH(false, true); else WIN_LAUNCH(false, false);
+    if (coords) WIN_SPL(false, true); else WIN_SPL(false, false);
   }
+#undef WIN_SPL
 #undef WIN_LAUNCH
   return 0;  // launch errors: the caller's hipGetLastError
 }

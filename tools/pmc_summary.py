@@ -15,7 +15,7 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"(msda_\w+?)<(.*?)>\(", name)
+    m = re.search(r"((?:msda|win)_\w+?)<(.*?)>\(", name)
     return None if not m else f"{m.group(1)}<{m.group(2).replace('(anonymous namespace)::', '')}>"
 
 
