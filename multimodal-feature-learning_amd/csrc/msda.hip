@@ -2642,8 +2642,8 @@ int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, 
 // unset: the default below.
 int win_env() { return env_int("MSDA_HIP_BWD_WIN", -1); }
 
-bool win_applies(int value_dtype, long long D, long long Lq, long long P) {
-  if (value_dtype != MSDA_DTYPE_BF16 || !msda_win_supported(1, D, P, Lq) || Lq * P <= 512) return false;
+bool win_applies(int value_dtype, long long D, long long Lq, long long P, long long M, long long L) {
+  if (value_dtype != MSDA_DTYPE_BF16 || !msda_win_supported(1, D, P, Lq, M * L * P) || Lq * P <= 512) return false;
   return win_env() == 1;
 }
 
@@ -2661,7 +2661,7 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1) || pr.Lq * pr.P <= 512;
     if constexpr (std::is_same<scalar_t, bf16_t>::value) {
       if (gval != nullptr && pr.B * pr.M * pr.S > 0 && !sparse && workspace != nullptr &&
-          win_applies(value_dtype, pr.D, pr.Lq, pr.P)) {
+          win_applies(value_dtype, pr.D, pr.Lq, pr.P, pr.M, pr.L)) {
         WinShape sh{};
         sh.B = pr.B; sh.S = pr.S; sh.M = pr.M; sh.Lq = pr.Lq; sh.L = (int)pr.L; sh.P = (int)pr.P;
         for (int l = 0; l < pr.L; ++l) {
@@ -3305,7 +3305,7 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
   if (batch <= 0 || spatial_size <= 0 || num_heads <= 0) return 0;
   PairPlan pp;
   // the row-block MFMA path's tile intervals (when it may run) share the workspace
-  const size_t win = win_applies(value_dtype, channels, num_query, num_point)
+  const size_t win = win_applies(value_dtype, channels, num_query, num_point, num_heads, num_levels)
                          ? msda_win_workspace_bytes(batch, num_heads, num_levels, num_query) : 0;
   if (value_dtype != MSDA_DTYPE_F64 && pair_plan(value_dtype, batch, num_heads, num_query, num_point, channels,
                                                   num_levels, nullptr, spatial_size, true, &pp))

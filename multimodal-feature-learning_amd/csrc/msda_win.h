@@ -15,7 +15,8 @@ struct WinShape {
 
 __attribute__((visibility("hidden"))) size_t msda_win_workspace_bytes(long long B, long long M, long long L,
                                                                      long long Lq);
-__attribute__((visibility("hidden"))) int msda_win_supported(int value_dtype_is_bf16, long long D, long long P, long long Lq);
+__attribute__((visibility("hidden"))) int msda_win_supported(int value_dtype_is_bf16, long long D, long long P, long long Lq,
+                                                                  long long row_floats);
 __attribute__((visibility("hidden"))) int msda_win_backward(const void* value, const void* loc, const void* aw,
                                                             const void* gout, void* gval, void* gloc, void* gaw,
                                                             void* workspace, const WinShape* shape, int zeros,

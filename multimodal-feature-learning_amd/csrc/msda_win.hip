@@ -110,18 +110,11 @@ __device__ __forceinline__ int2 sample_rows(const Taps& t) {
   return make_int2(t.base < 0 ? 0 : t.base, t.base + 1);
 }
 
-__device__ __forceinline__ int wave_min(int x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o));
-  return x;
-}
-__device__ __forceinline__ int wave_max(int x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x = max(x, __shfl_xor(x, o));
-  return x;
-}
-
-// One wave per (b, m, level, tile): the interval of rows its samples touch or own.
+// The row interval every (b, m, level, query tile) touches or owns.  One wave per (b, tile): a
+// query's coordinates of all heads and levels are one contiguous row of M * L * P floats, so the
+// wave reads the tile's 32 rows coalesced (lane i holds float i + 64 j of each row) and reduces
+// each (m, level)'s P consecutive floats over P lanes at the end.
+constexpr int kRowRegs = 8;  // M * L * P <= 512 floats per query row
 template <bool ZEROS>
 __global__ __launch_bounds__(kThreads) void win_tiles_kernel(const float* __restrict__ loc, int2* __restrict__ tiles,
                                                              const WinShape sh, const long long n_waves) {
@@ -129,26 +122,44 @@ __global__ __launch_bounds__(kThreads) void win_tiles_kernel(const float* __rest
   if (wv >= n_waves) return;  // wave-uniform
   const int lane = threadIdx.x & 63;
   const int tile = (int)(wv % sh.ntile);
-  const long long bml = wv / sh.ntile;
-  const int l = (int)(bml % sh.L);
-  const long long bm = bml / sh.L;
-  const int m = (int)(bm % sh.M);
-  const long long b = bm / sh.M;
-  const int T = sh.T[l];
-  const int P = sh.P, LP = sh.L * sh.P;
-  int lo = kNone, hi = -kNone;
-  for (int s = lane; s < kQT * P; s += 64) {
-    const int q = tile * kQT + s / P;
-    if (q < sh.Lq) {
-      const Taps t = make_taps<ZEROS>(loc[((b * sh.Lq + q) * sh.M + m) * LP + l * P + s % P], T);
-      const int2 r = sample_rows<ZEROS>(t);
-      lo = min(lo, r.x);
-      hi = max(hi, r.y);
-    }
+  const long long b = wv / sh.ntile;
+  const int P = sh.P, n = (int)sh.M * sh.L * P;
+  const int q0 = tile * kQT, nq = (int)min((long long)kQT, sh.Lq - q0);
+  const float* __restrict__ rows = loc + (b * sh.Lq + q0) * (long long)n;
+  int lo[kRowRegs], hi[kRowRegs], T[kRowRegs];
+#pragma unroll
+  for (int j = 0; j < kRowRegs; ++j) {
+    lo[j] = kNone;
+    hi[j] = -kNone;
+    T[j] = sh.T[((lane + 64 * j) / P) % sh.L];
   }
-  lo = wave_min(lo);
-  hi = wave_max(hi);
-  if (lane == 0) tiles[wv] = make_int2(lo, hi);
+  for (int q = 0; q < nq; q += 4) {
+    float x[4][kRowRegs];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < kRowRegs; ++j)
+        x[u][j] = (q + u < nq && lane + 64 * j < n) ? rows[(long long)(q + u) * n + lane + 64 * j] : 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < kRowRegs; ++j) {
+        if (q + u < nq && lane + 64 * j < n) {
+          const int2 r = sample_rows<ZEROS>(make_taps<ZEROS>(x[u][j], T[j]));
+          lo[j] = min(lo[j], r.x);
+          hi[j] = max(hi[j], r.y);
+        }
+      }
+  }
+#pragma unroll
+  for (int j = 0; j < kRowRegs; ++j) {
+    for (int o = 1; o < P; o <<= 1) {
+      lo[j] = min(lo[j], __shfl_xor(lo[j], o));
+      hi[j] = max(hi[j], __shfl_xor(hi[j], o));
+    }
+    const int i = lane + 64 * j;
+    if (i < n && i % P == 0) tiles[(b * sh.M * sh.L + i / P) * sh.ntile + tile] = make_int2(lo[j], hi[j]);
+  }
 }
 
 __device__ __forceinline__ short bf16_bits(float x) {  // round to nearest even (finite inputs)
@@ -172,7 +183,7 @@ constexpr int kDSW = kVRows;     // dots kept per query: rows r0 .. r0+16
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
 
 template <bool ZEROS, bool COORDS, int P>
-__global__ __launch_bounds__(64) void win_bwd_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void win_bwd_kernel(
     const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     const uint16_t* __restrict__ gout, uint16_t* __restrict__ gval, float* __restrict__ gloc,
     float* __restrict__ gaw, const int2* __restrict__ tiles, const WinShape sh) {
@@ -180,8 +191,12 @@ __global__ __launch_bounds__(64) void win_bwd_kernel(
   constexpr int SPL = NS >= 64 ? NS / 64 : 1;  // samples per lane
   __shared__ __attribute__((aligned(16))) unsigned char s_g[kQT * kGS];     // grad_out rows of the tile
   __shared__ __attribute__((aligned(16))) unsigned char s_v[kVRows * kGS];  // the block's value rows
-  __shared__ float s_d[kQT * kDSW];                                         // dots [q][row - r0]
-  __shared__ int4 s_rec[NS + kQT];  // compacted samples {base - r0, c0 | c1 hi, c0 | c1 lo, query}, padded
+  // C of one MFMA step ([row][hi 32 | lo 32], step 2a), then the dots ([q][row - r0], 2b / 3): in
+  // turn, in the wave's LDS order
+  constexpr int kCBytes = kRW * kGS > kQT * kDSW * 4 ? kRW * kGS : kQT * kDSW * 4;
+  __shared__ __attribute__((aligned(16))) unsigned char s_c[kCBytes];
+  float* const s_d = reinterpret_cast<float*>(s_c);
+  __shared__ int s_q[NS + kQT];  // query row (in the tile) of each compacted sample, padded
 
   const int lane = threadIdx.x, g = lane >> 4, li = lane & 15;
   const unsigned id = xcd_block(blockIdx.x, gridDim.x);
@@ -277,9 +292,11 @@ __global__ __launch_bounds__(64) void win_bwd_kernel(
   while (tile >= 0) {
     const int q0 = tile * kQT;
     // 1. the visit's taps (kept in registers) and grad_out rows (into LDS); the samples with a tap
-    // in the block's 16 rows compacted into records
+    // in the block's 16 rows are compacted (ballot): position kp, coefficients split into bf16 hi / lo
     Taps tp[SPL];
     float a[SPL];
+    int kp[SPL], dr[SPL];
+    uint32_t ch[SPL], cl[SPL];  // c0 | c1 << 16, hi and lo parts
     int n = 0;
 #pragma unroll
     for (int j = 0; j < SPL; ++j) {
@@ -288,50 +305,57 @@ __global__ __launch_bounds__(64) void win_bwd_kernel(
       tp[j] = make_taps<ZEROS>(rl[j], T);
       tp[j].live = tp[j].live && in;
       a[j] = ra[j];
-      const int dr = tp[j].base - r0;
-      const bool sel = tp[j].live && dr >= -1 && dr <= kRW - 1;
+      dr[j] = tp[j].base - r0;
+      const bool sel = tp[j].live && dr[j] >= -1 && dr[j] <= kRW - 1;
       const unsigned long long bal = __ballot(sel);
-      if (sel) {  // record: row offset, bf16 hi parts (c0 | c1 << 16), lo parts, query row of the tile
-        const float c0 = tp[j].ok0 ? a[j] * tp[j].w0 : 0.f;
-        const float c1 = tp[j].ok1 ? a[j] * tp[j].w1 : 0.f;
-        const uint32_t h0 = (uint16_t)bf16_bits(c0), h1 = (uint16_t)bf16_bits(c1);
-        const uint32_t l0 = (uint16_t)bf16_bits(c0 - bf16_val((short)h0));
-        const uint32_t l1 = (uint16_t)bf16_bits(c1 - bf16_val((short)h1));
-        s_rec[n + __popcll(bal & ((1ull << lane) - 1ull))] = make_int4(dr, (int)(h0 | (h1 << 16)),
-                                                                       (int)(l0 | (l1 << 16)), s / P);
-      }
+      kp[j] = sel ? n + __popcll(bal & ((1ull << lane) - 1ull)) : -1;
+      const float c0 = tp[j].ok0 ? a[j] * tp[j].w0 : 0.f;
+      const float c1 = tp[j].ok1 ? a[j] * tp[j].w1 : 0.f;
+      const uint32_t h0 = (uint16_t)bf16_bits(c0), h1 = (uint16_t)bf16_bits(c1);
+      ch[j] = h0 | (h1 << 16);
+      cl[j] = (uint32_t)(uint16_t)bf16_bits(c0 - bf16_val((short)h0)) |
+              ((uint32_t)(uint16_t)bf16_bits(c1 - bf16_val((short)h1)) << 16);
+      if (sel) s_q[kp[j]] = s / P;
       n += __popcll(bal);
     }
     const int nk = (n + 31) >> 5;
-    if (lane < nk * 32 - n) s_rec[n + lane] = make_int4(kNone, 0, 0, 0);  // pad to whole MFMA steps
+    if (lane < nk * 32 - n) s_q[n + lane] = 0;  // padding columns: C is zero there
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(s_g + (grow + 8 * i) * kGS + gch * 16) = rg[i];
     wave_lds_fence();
     const int next = next_tile();
     if (next >= 0) fetch(next);  // in flight during the compute below
 
-    // 2a. grad_value of the 16 rows += C . G, 32 compacted samples per MFMA step
+    // 2a. grad_value of the 16 rows += C . G, 32 compacted samples per MFMA step: C built in LDS
+    // (zeroed, then each sample writes c0 on its base row and c1 on the next, where in the block)
     for (int ks = 0; ks < nk; ++ks) {
-      const int4* rec = &s_rec[ks * 32 + 8 * g];
-      u32x4 hw, lw;  // this lane's row (li) of C: per sample c0 on its base row, c1 on the next
-#pragma unroll
-      for (int j2 = 0; j2 < 4; ++j2) {
-        uint32_t hp = 0u, lp = 0u;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int4 r = rec[2 * j2 + e];
-          const int sh16 = r.x == li ? 0 : 16;  // which half (c0 or c1), if any, lands on row li
-          const bool any = r.x == li || r.x + 1 == li;
-          hp |= any ? (((uint32_t)r.y >> sh16) & 0xffffu) << (16 * e) : 0u;
-          lp |= any ? (((uint32_t)r.z >> sh16) & 0xffffu) << (16 * e) : 0u;
-        }
-        hw[j2] = hp;
-        lw[j2] = lp;
+      {
+        uint4* z = reinterpret_cast<uint4*>(s_c + (lane >> 2) * kGS + (lane & 3) * 32);
+        z[0] = make_uint4(0u, 0u, 0u, 0u);
+        z[1] = make_uint4(0u, 0u, 0u, 0u);
       }
-      const bf16x8 ahi = __builtin_bit_cast(bf16x8, hw), alo = __builtin_bit_cast(bf16x8, lw);
-      // rows of the transposed reads: lane 4q'+pp of the group names record 8g + 4h + q'
+      wave_lds_fence();
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) {
+        const int col = kp[j] - 32 * ks;
+        if (col >= 0 && col < 32) {
+          uint16_t* r = reinterpret_cast<uint16_t*>(s_c + dr[j] * kGS) + col;  // row dr (may be -1: not written)
+          if (dr[j] >= 0) {
+            r[0] = (uint16_t)ch[j];
+            r[32] = (uint16_t)cl[j];
+          }
+          if (dr[j] + 1 < kRW) {
+            r[kGS / 2] = (uint16_t)(ch[j] >> 16);
+            r[kGS / 2 + 32] = (uint16_t)(cl[j] >> 16);
+          }
+        }
+      }
+      wave_lds_fence();
+      const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(s_c + li * kGS + 16 * g);
+      const bf16x8 alo = *reinterpret_cast<const bf16x8*>(s_c + li * kGS + 64 + 16 * g);
+      // rows of the transposed reads: lane 4q'+pp of the group names compacted sample 8g + 4h + q'
       const int qq = li >> 2, pp = li & 3;
-      const int rowa = rec[qq].w, rowb = rec[4 + qq].w;
+      const int rowa = s_q[ks * 32 + 8 * g + qq], rowb = s_q[ks * 32 + 8 * g + 4 + qq];
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
         const int col = (cb * 16 + 4 * pp) * 2;
@@ -341,6 +365,7 @@ __global__ __launch_bounds__(64) void win_bwd_kernel(
         acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, acc[cb], 0, 0, 0);
         acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, acc[cb], 0, 0, 0);
       }
+      wave_lds_fence();  // this step's C reads before the next step's zeroing
     }
     // 2b. dots of the tile's 32 queries with rows r0 .. r0+16 (2 query halves x 2 row blocks; of
     // the second block only row r0+16 is kept, its other columns read row r0+16 again)
@@ -404,8 +429,10 @@ size_t msda_win_workspace_bytes(long long B, long long M, long long L, long long
   return (size_t)(B * M * L * ntile) * sizeof(int2);
 }
 
-int msda_win_supported(int value_dtype_is_bf16, long long D, long long P, long long Lq) {
-  return value_dtype_is_bf16 && D == 64 && (P == 1 || P == 2 || P == 4 || P == 8) && Lq < (1LL << 24);
+int msda_win_supported(int value_dtype_is_bf16, long long D, long long P, long long Lq, long long row_floats) {
+  // row_floats = M * L * P: one query's coordinates, read by the prepass in kRowRegs x 64 lanes
+  return value_dtype_is_bf16 && D == 64 && (P == 1 || P == 2 || P == 4 || P == 8) && Lq < (1LL << 24) &&
+         row_floats <= 64 * kRowRegs;
 }
 
 int msda_win_backward(const void* value, const void* loc, const void* aw, const void* gout, void* gval,
@@ -421,7 +448,7 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   sh.nblk = nb;
   if (sh.B * sh.M == 0 || nb == 0) return 0;
   auto* tiles = static_cast<int2*>(workspace);
-  const long long n_waves = sh.B * sh.M * sh.L * sh.ntile;
+  const long long n_waves = sh.B * sh.ntile;
   if (n_waves > 0) {
     const unsigned blocks = (unsigned)((n_waves + 3) / 4);
     if (zeros)

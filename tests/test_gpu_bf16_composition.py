@@ -188,7 +188,7 @@ def test_caption_decoder_bf16_matches_reference_bf16(golden, dev):
 
     # greedy decode: the KV-cached loop under bf16 autocast, judged by how far its path is from
     # greedy under the fp64 model (the mirror in fp64, pinned against the reference below)
-    d64 = _caption_decoder(c, dev).double()
+    d64 = _caption_decoder(c, dev).to(dev).double()
     d64.load_state_dict(dec.state_dict())
     mem64 = memory.double()
     full64 = lambda cp, pm, tm: d64(cp, mem64, tgt_mask=tm, memory_mask=kmask[:, None, None, :],  # noqa: E731
