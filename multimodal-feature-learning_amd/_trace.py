@@ -9,8 +9,8 @@ import collections
 hits = collections.Counter()
 
 
-def hit(name):
-    hits[name] += 1
+def hit(name, n=1):
+    hits[name] += n
 
 
 def clear():

@@ -2639,12 +2639,17 @@ int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, 
 
 // Row-block MFMA backward (msda_win.hip): bf16 values, D = 64, P <= 8, a call with more than 512
 // samples a level.  MSDA_HIP_BWD_WIN (read per call): "0" never, "1" wherever it applies;
-// unset: the default below.
+// unset: where a level's samples do not fit the pair kernel's LDS lists (16 B a sample: key,
+// (c0, c1), position), i.e. where the pair kernel would stage them through a workspace — the
+// configs[3] per-rank call (T = 4096: 262-294 us against 420-510, tools/win_ab.py); at the
+// encoder shape (T = 1024) the pair kernel is faster (69-82 us against 89-98).
 int win_env() { return env_int("MSDA_HIP_BWD_WIN", -1); }
 
 bool win_applies(int value_dtype, long long D, long long Lq, long long P, long long M, long long L) {
   if (value_dtype != MSDA_DTYPE_BF16 || !msda_win_supported(1, D, P, Lq, M * L * P) || Lq * P <= 512) return false;
-  return win_env() == 1;
+  const int e = win_env();
+  if (e >= 0) return e == 1;
+  return (size_t)(Lq * P) * 16 > kPairLdsMax;
 }
 
 template <typename scalar_t, typename coord_t>
@@ -2660,7 +2665,8 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     for (int l = 0; l < pr.L; ++l) minT = min(minT, pr.lv.T[l]);
     const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1) || pr.Lq * pr.P <= 512;
     if constexpr (std::is_same<scalar_t, bf16_t>::value) {
-      if (gval != nullptr && pr.B * pr.M * pr.S > 0 && !sparse && workspace != nullptr &&
+      // (gval may be null: the row-block kernel then writes the coordinate gradients only)
+      if (pr.B * pr.M * pr.S > 0 && !sparse && workspace != nullptr &&
           win_applies(value_dtype, pr.D, pr.Lq, pr.P, pr.M, pr.L)) {
         WinShape sh{};
         sh.B = pr.B; sh.S = pr.S; sh.M = pr.M; sh.Lq = pr.Lq; sh.L = (int)pr.L; sh.P = (int)pr.P;
@@ -3307,10 +3313,10 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
   // the row-block MFMA path's tile intervals (when it may run) share the workspace
   const size_t win = win_applies(value_dtype, channels, num_query, num_point, num_heads, num_levels)
                          ? msda_win_workspace_bytes(batch, num_heads, num_levels, num_query) : 0;
+  if (win > 0) return win;  // the call takes the row-block path (same decision, run_backward)
   if (value_dtype != MSDA_DTYPE_F64 && pair_plan(value_dtype, batch, num_heads, num_query, num_point, channels,
                                                   num_levels, nullptr, spatial_size, true, &pp))
-    return std::max(pp.ws_bytes, win);
-  if (win > 0) return win;
+    return pp.ws_bytes;
   if (use_fused_gvalue(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point))
     return 0;
   return bwd_layout(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point).total;

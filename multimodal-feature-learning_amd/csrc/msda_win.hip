@@ -175,7 +175,7 @@ __device__ __forceinline__ float bf16_val(short h) { return __uint_as_float(((ui
 // visit computes.
 constexpr int kRW = 16;          // rows per block (one wave)
 constexpr int kVRows = kRW + 1;  // value rows r0 .. r0+16 in the dot products
-constexpr int kDSW = kVRows;     // dots kept per query: rows r0 .. r0+16
+constexpr int kDQS = kQT + 4;    // dots row stride (floats): [row - r0][q], rows r0 .. r0+16, 16-B rows
 
 // Orders one wave's LDS writes before its later LDS reads: the wave's LDS operations execute in
 // issue order, so this only has to stop the compiler from moving LDS accesses across it (no
@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
   __shared__ __attribute__((aligned(16))) unsigned char s_v[kVRows * kGS];  // the block's value rows
   // C of one MFMA step ([row][hi 32 | lo 32], step 2a), then the dots ([q][row - r0], 2b / 3): in
   // turn, in the wave's LDS order
-  constexpr int kCBytes = kRW * kGS > kQT * kDSW * 4 ? kRW * kGS : kQT * kDSW * 4;
+  constexpr int kCBytes = kRW * kGS > kVRows * kDQS * 4 ? kRW * kGS : kVRows * kDQS * 4;
   __shared__ __attribute__((aligned(16))) unsigned char s_c[kCBytes];
   float* const s_d = reinterpret_cast<float*>(s_c);
   __shared__ int s_q[NS + kQT];  // query row (in the tile) of each compacted sample, padded
@@ -311,10 +311,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
       kp[j] = sel ? n + __popcll(bal & ((1ull << lane) - 1ull)) : -1;
       const float c0 = tp[j].ok0 ? a[j] * tp[j].w0 : 0.f;
       const float c1 = tp[j].ok1 ? a[j] * tp[j].w1 : 0.f;
-      const uint32_t h0 = (uint16_t)bf16_bits(c0), h1 = (uint16_t)bf16_bits(c1);
-      ch[j] = h0 | (h1 << 16);
-      cl[j] = (uint32_t)(uint16_t)bf16_bits(c0 - bf16_val((short)h0)) |
-              ((uint32_t)(uint16_t)bf16_bits(c1 - bf16_val((short)h1)) << 16);
+      // c = hi + lo: hi the truncated bf16 (exact remainder c - hi), lo that remainder rounded to
+      // bf16 — |c - hi - lo| <= 2^-16 |c|, far below the bf16 rounding of grad_value
+      const uint32_t u0 = __float_as_uint(c0) & 0xffff0000u, u1 = __float_as_uint(c1) & 0xffff0000u;
+      ch[j] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);  // hi halves: c0 low, c1 high
+      cl[j] = (uint32_t)(uint16_t)bf16_bits(c0 - __uint_as_float(u0)) |
+              ((uint32_t)(uint16_t)bf16_bits(c1 - __uint_as_float(u1)) << 16);
       if (sel) s_q[kp[j]] = s / P;
       n += __popcll(bal);
     }
@@ -382,10 +384,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
           const bf16x8 bv = *reinterpret_cast<const bf16x8*>(s_v + vrow * kGS + off);
           d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, d, 0, 0, 0);
         }
-        if (cb == 0 || li == 0) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) s_d[(qh * 16 + 4 * g + j) * kDSW + cb * 16 + li] = d[j];
-        }
+        // lane (g, li) holds queries qh*16 + 4g .. +3 of row li (cb 0) / row 16 (cb 1): one 16-B store
+        if (cb == 0 || li == 0)
+          *reinterpret_cast<f32x4*>(s_d + (cb * 16 + li) * kDQS + qh * 16 + 4 * g) = d;
       }
       wave_lds_fence();
       // 3. coordinate gradients of the samples this block owns (base row in it; the level's first
@@ -399,8 +400,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
         const bool own = t.live ? (t.base >= r0 && t.base < r0 + kRW) || (t.base < 0 && k == 0) : k == 0;
         if (in && own) {
           const int qi = s / P;
-          const float d0 = t.ok0 ? s_d[qi * kDSW + t.base - r0] : 0.f;
-          const float d1 = t.ok1 ? s_d[qi * kDSW + t.base + 1 - r0] : 0.f;
+          const float d0 = t.ok0 ? s_d[(t.base - r0) * kDQS + qi] : 0.f;
+          const float d1 = t.ok1 ? s_d[(t.base + 1 - r0) * kDQS + qi] : 0.f;
           if (gaw != nullptr) gaw[tb + soff[j]] = d0 * t.w0 + d1 * t.w1;
           if (gloc != nullptr) gloc[tb + soff[j]] = ((d1 - d0) * a[j]) * t.gmul;
         }
@@ -411,6 +412,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
   }
 
   // grad_value rows r0 + 4g + j, channels 16 cb + li (every row of the block, zeros included)
+  if (gval == nullptr) return;
   uint16_t* __restrict__ gvl = gval + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {

@@ -18,7 +18,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
-from ..modules.linear import Linear
+from ..modules.linear import Linear, flush_point
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 from ..modules.ffn import relu_dropout
 from ..modules.value_proj import layer_values, layer_values_supported
@@ -313,7 +313,10 @@ class DeformableTransformerDecoder(nn.Module):
 
     def forward(self, tgt, reference_points, src, src_temporal_shapes, src_level_start_index, src_valid_ratios,
                 query_pos=None, src_padding_mask=None, query_padding_mask=None, disable_iterative_refine=False):
-        output = tgt
+        # the decoder's batched weight gradients are computed once the query's gradient is (the
+        # first layer's backward done), so a data-parallel step reduces them while the encoder's
+        # backward runs (linear.py); not on src: its carried bf16 copy must stay attached
+        output = flush_point(tgt)
         hs, refs = [], []
         if query_pos is not None and not query_pos.is_contiguous():
             query_pos = query_pos.contiguous()  # once, not per layer (the fused layers read it flat)

@@ -27,7 +27,7 @@ from torch.nn.init import constant_, xavier_uniform_
 from ... import msda as _msda
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
-from .linear import Linear, _AutocastLinear, _bias_grad, _weight_grad, linear_pair
+from .linear import Linear, _AutocastLinear, _bias_grad, _defer, _weight_grad, linear_pair
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
            "masked_scores_softmax", "mask_padding_rows", "mha_self_attention"]
@@ -294,6 +294,7 @@ class _InProjection(torch.autograd.Function):
         v = torch.addmm(bc[2 * e:], v2, wc[2 * e:].t())
         ctx.save_for_backward(a2, v2, wc)
         ctx.shape = x_qk.shape
+        ctx.params = (w, b)
         lead = x_qk.shape[:-1]
         return (torch.ops.aten._unsafe_view(qk, (*lead, 2 * e)), torch.ops.aten._unsafe_view(v, (*lead, e)))
 
@@ -306,6 +307,9 @@ class _InProjection(torch.autograd.Function):
         nig = ctx.needs_input_grad
         dqk = torch.mm(gqk, wc[:2 * e]).view(ctx.shape) if nig[0] else None
         dv = torch.mm(gv, wc[2 * e:]).view(ctx.shape) if nig[1] else None
+        w, b = ctx.params  # weight / bias gradients batched with the other short-K layers' (linear.py)
+        if nig[2] and nig[3] and _defer((gqk, a2, w, 0, b), (gv, v2, w, 2 * e, b)):
+            return dqk, dv, None, None, None, None
         dw = db = None
         if nig[2]:
             dw = torch.cat((_weight_grad(gqk, a2), _weight_grad(gv, v2)), 0)

@@ -17,12 +17,119 @@ FFNs of ``unimodal_deformable_transformer.py:174-177``).  Only the autocast back
 
 Outside autocast on a GPU (fp32 / fp64 parity runs) and on the CPU it is exactly
 ``F.linear``.
+
+Deferred weight gradients.  Inside ``deferred_weight_grads(deliver)`` (the training step's
+backward, train_step.py) a short-K layer (at most ``DEFER_MAX_ROWS`` input rows: the decoder's
+800 query rows, the caption decoder's words) does not compute dW and db in its backward: it
+queues (dY, X) and returns no weight gradient; ``flush()`` then computes every queued product
+of one shape as ONE strided-batched GEMM (fp32 output) and every bias gradient of one shape as
+one reduction, and hands each parameter its gradient through ``deliver(param, grad)``.  The
+decoder's 48 weight-gradient GEMMs of a step (800-row, 10-15 us each at 25-140 TF/s: each is
+too small to fill 256 CUs) become five batched GEMMs.  dX stays in the backward (the chain
+needs it).  ``flush_point(t)`` marks a tensor whose gradient completes a group of layers (the
+decoder's memory): the queue is flushed there inside the backward, so a data-parallel step
+all-reduces those gradients while the encoder's backward runs.
 """
+import contextlib
+
 import torch
 import torch.nn.functional as F
 from torch import nn
 
-__all__ = ["Linear", "split_k_chunks", "linear_pair"]
+__all__ = ["Linear", "split_k_chunks", "linear_pair", "deferred_weight_grads", "flush_point"]
+
+DEFER_MAX_ROWS = 4096  # GEMM K (input rows) up to which weight gradients are queued and batched
+
+
+class _WgradQueue:
+    """Queued weight / bias gradient products of one backward (see the module docstring)."""
+
+    def __init__(self, deliver):
+        self.deliver = deliver
+        self.entries = []  # (dY (K, N), X (K, C), weight param, row offset, bias param or None)
+
+    def push(self, g2, x2, weight, row, bias):
+        self.entries.append((g2, x2, weight, row, bias))
+
+    @torch.no_grad()
+    def flush(self):
+        entries, self.entries = self.entries, []
+        if not entries:
+            return
+        groups = {}
+        for e in entries:
+            g2, x2 = e[0], e[1]
+            groups.setdefault((g2.shape[0], g2.shape[1], x2.shape[1], g2.dtype), []).append(e)
+        from ... import _trace
+        _trace.hit("wgrad_batched", len(entries))
+        parts = {}  # param -> [(row offset, fp32 grad rows)]
+        for (_, n_out, _, _), es in groups.items():
+            gs = es[0][0][None] if len(es) == 1 else torch.stack([e[0] for e in es])
+            xs = es[0][1][None] if len(es) == 1 else torch.stack([e[1] for e in es])
+            if gs.is_cuda:  # fp32 accumulate and output
+                dw = torch.bmm(gs.transpose(1, 2), xs, out_dtype=torch.float32)
+            else:  # (CPU unit tests of the queue: no 16-bit-in / fp32-out GEMM there)
+                dw = torch.bmm(gs.transpose(1, 2).float(), xs.float())
+            with_bias = [k for k, e in enumerate(es) if e[4] is not None]
+            db = gs.sum(1, dtype=torch.float32) if with_bias else None
+            for k, (_, _, w, row, b) in enumerate(es):
+                parts.setdefault(w, []).append((row, dw[k]))
+                if b is not None:
+                    parts.setdefault(b, []).append((row, db[k]))
+        for prm, ps in parts.items():
+            if len(ps) == 1 and ps[0][0] == 0 and ps[0][1].shape == prm.shape:
+                grad = ps[0][1]
+            else:  # a weight split over several products (in_proj q / k | v) or used several times
+                grad = torch.zeros(prm.shape, dtype=torch.float32, device=prm.device)
+                for row, g in ps:
+                    grad[row:row + g.shape[0]] += g
+            self.deliver(prm, grad)
+
+
+_queue = None
+
+
+@contextlib.contextmanager
+def deferred_weight_grads(deliver):
+    """Queue the short-K layers' weight / bias gradients of the backward run inside; the caller
+    calls ``flush()`` on the yielded queue after the backward (flush points flush earlier)."""
+    global _queue
+    prev, _queue = _queue, _WgradQueue(deliver)
+    try:
+        yield _queue
+    finally:
+        _queue = prev
+
+
+def _defer(*entries):
+    """Queue the (dY, X, weight, row offset, bias) products of one backward when a queue is active
+    and every K is short — all of them or none; True if queued."""
+    q = _queue
+    if q is None or any(e[0].shape[0] > DEFER_MAX_ROWS or e[2].dtype != torch.float32 for e in entries):
+        return False
+    for e in entries:
+        q.push(*e)
+    return True
+
+
+class _FlushPoint(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        return x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        if _queue is not None:
+            _queue.flush()
+        return g
+
+
+def flush_point(t):
+    """Identity; in a deferred backward the queued weight gradients are computed once t's gradient
+    is (see the module docstring)."""
+    if _queue is None and not torch.is_grad_enabled():
+        return t
+    return _FlushPoint.apply(t) if t.requires_grad else t
 
 
 def split_k_chunks(k, min_chunk=1024, max_split=8):
@@ -100,6 +207,7 @@ class _AutocastLinear(torch.autograd.Function):
         ctx.save_for_backward(x2, wc)
         ctx.has_bias = bias is not None
         ctx.x_shape = x.shape
+        ctx.weight, ctx.bias = weight, bias  # the parameters a deferred gradient is delivered to
         # not an autograd view of the 2-D GEMM output (as F.linear's 3-D result): callers may
         # modify it in place (MSDeformAttn zeroes the padding rows of value_proj's output)
         return torch.ops.aten._unsafe_view(y, (*x.shape[:-1], wc.shape[0]))
@@ -109,11 +217,14 @@ class _AutocastLinear(torch.autograd.Function):
         x2, wc = ctx.saved_tensors
         g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype)
         gx = gw = gb = None
-        if ctx.needs_input_grad[0]:
+        nig = ctx.needs_input_grad
+        if nig[0]:
             gx = torch.mm(g2, wc).view(ctx.x_shape)
-        if ctx.needs_input_grad[1]:
+        if nig[1] and (not ctx.has_bias or nig[2]) and _defer((g2, x2, ctx.weight, 0, ctx.bias if ctx.has_bias else None)):
+            return gx, None, None, None, None
+        if nig[1]:
             gw = _weight_grad(g2, x2)
-        if ctx.has_bias and ctx.needs_input_grad[2]:
+        if ctx.has_bias and nig[2]:
             gb = _bias_grad(g2)
         return gx, gw, gb, None, None
 
@@ -135,6 +246,7 @@ class _AutocastLinearPair(torch.autograd.Function):
         yb = torch.addmm(bb.to(dt) if bcb is None else bcb, x2, wcb.t())
         ctx.save_for_backward(x2, wca, wcb)
         ctx.x_shape = x.shape
+        ctx.params = (wa, ba, wb, bb)
         lead = x.shape[:-1]
         return ya.view(*lead, wca.shape[0]), yb.view(*lead, wcb.shape[0])
 
@@ -148,6 +260,9 @@ class _AutocastLinearPair(torch.autograd.Function):
         g2 = torch.cat((ga, gb_), 1)
         nig = ctx.needs_input_grad
         gx = torch.mm(g2, torch.cat((wca, wcb), 0)).view(ctx.x_shape) if nig[0] else None
+        wa, ba, wb, bb = ctx.params
+        if all(nig[1:5]) and _defer((ga, x2, wa, 0, ba), (gb_, x2, wb, 0, bb)):
+            return gx, None, None, None, None, None, None, None, None
         gwa = gwb = gba = gbb = None
         if nig[1] or nig[3]:
             gw = _weight_grad(g2, x2)

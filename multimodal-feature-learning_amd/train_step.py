@@ -35,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from .models.modules.add_norm import seed_pool
-from .models.modules.linear import Linear
+from .models.modules.linear import Linear, deferred_weight_grads
 
 __all__ = ["FlatGradTrainer"]
 
@@ -136,9 +136,12 @@ class FlatGradTrainer:
         for bi, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
                 self._bucket_of[i] = bi
+        self._index = {id(p): i for i, p in enumerate(self.params)}
+        self._hooks = {}
         if self.overlap:
             for i, p in enumerate(self.params):
-                p.register_post_accumulate_grad_hook(self._make_hook(i))
+                self._hooks[i] = self._make_hook(i)
+                p.register_post_accumulate_grad_hook(self._hooks[i])
 
     # --- gradient buckets ----------------------------------------------------------------
     def _make_buckets(self, cap_elems):
@@ -168,6 +171,11 @@ class FlatGradTrainer:
     def _make_hook(self, i):
         def hook(p):
             if self._pending is None:  # backward outside _forward_backward (user code): nothing to do
+                return
+            if self._got[i]:
+                # a second gradient for i this step (a deferred weight gradient delivered beside an
+                # autograd one): its bucket may be reduced already, so reduce everything again
+                self._late = True
                 return
             self._got[i] = True
             b = self._bucket_of[i]
@@ -293,8 +301,12 @@ class FlatGradTrainer:
         self._late = False
         self._works = []
         try:
-            self._flush_ready()
-            loss.backward()  # overlap: complete buckets are copied and all-reduced from the hooks, in order
+            # the short-K layers' weight gradients are batched (models/modules/linear.py) and
+            # handed over by _deliver, at the model's flush points or after the backward
+            with deferred_weight_grads(self._deliver) as queue:
+                self._flush_ready()
+                loss.backward()  # overlap: complete buckets are copied and all-reduced from the hooks, in order
+                queue.flush()
         finally:
             self._pending = None
         self._ready = [True] * len(self.buckets)  # buckets with parameters that got no gradient
@@ -314,6 +326,17 @@ class FlatGradTrainer:
             for i in self._unused:  # torch AdamW skips a parameter whose grad is None
                 self.params[i].grad = None
         return loss.detach()
+
+    def _deliver(self, p, grad):
+        """A batched weight / bias gradient for parameter p: set (or added to) p.grad, then the
+        parameter's post-accumulate step (bucket hand-over) as autograd's hook would run it."""
+        if p.grad is None:
+            p.grad = grad
+        else:
+            p.grad.add_(grad)
+        i = self._index.get(id(p))
+        if i is not None and i in self._hooks:
+            self._hooks[i](p)
 
     def _find_unused(self):
         """After an eager backward: the parameters no rank gave a gradient (one small MAX all-reduce

@@ -36,11 +36,13 @@ def test_abi_version_and_workspace():
     assert lib.msda_hip_abi_version() == PKG._native.ABI_VERSION
     B, S, M, D, Lq, L, P = 2, 1920, 8, 64, 1920, 4, 4
     # pair-pull backward (16-byte chunks per lane, lists in LDS, any batch size): no workspace;
-    # at T = 4096 (S = 7680) the keys alone fill LDS and each (b, m, level) workgroup stages its
-    # entries' (c0, c1) and positions (12 B a sample) in the workspace
+    # at T = 4096 (S = 7680) the keys alone fill LDS: fp16 stages each (b, m, level) workgroup's
+    # entries' (c0, c1) and positions (12 B a sample) in the workspace, bf16 takes the row-block
+    # MFMA backward (one int2 row interval per (b, m, level, 32-query tile))
     for dt in (0, 2, 3):
         assert lib.msda_hip_backward_workspace_bytes(dt, B, S, M, D, Lq, L, P) == 0
-    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * 4 * Lq * P * 12
+    assert lib.msda_hip_backward_workspace_bytes(3, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * 4 * Lq * P * 12
+    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * (4 * Lq // 32) * 8
     # split path (sort + pull): fp64, or heads not made of 16-byte chunks with few workgroups —
     # row table + per-row tap lists
     f64 = lib.msda_hip_backward_workspace_bytes(1, B, S, M, D, Lq, L, P)

@@ -135,3 +135,58 @@ def test_linear_pair_matches_two_linears(dev, tokens, shadow):
         assert p.grad.dtype == torch.float32
         torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-5 * q.grad.abs().max().item())
     torch.testing.assert_close(x1.grad, x2.grad, rtol=2e-2, atol=2e-2 * x2.grad.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_trainer_batched_weight_grads_match_per_layer(dev, graph, monkeypatch):
+    """FlatGradTrainer's backward with the short-K weight gradients queued and batched
+    (linear.py deferred_weight_grads: the decoder's 2 x 20 query rows) gives the gradients of the
+    per-layer GEMMs; eager and graph-captured."""
+    def run(defer_rows):
+        monkeypatch.setattr(PKG.models.modules.linear, "DEFER_MAX_ROWS", defer_rows)
+        torch.manual_seed(0)
+        model = PKG.dvc_core.DeformableDVCCore(d_model=256, num_queries=20, enc_layers=2, dec_layers=2,
+                                               ff_dim=512, dropout=0.0).to(dev)
+        batch = PKG.dvc_core.synthetic_clips(2, T=64, feature_dim=512, device=dev)
+        gen = torch.Generator(device=dev).manual_seed(5)
+        wts = {}
+
+        def loss_fn(out):  # random output weights: workload_loss's sums of LayerNorm outputs have
+            # (near-)zero exact gradients, i.e. gradients made of rounding noise
+            total = 0.0
+            for k in ("hs", "memory", "all_segments", "all_counts", "all_logits"):
+                o = out[k].float()
+                if k not in wts:
+                    wts[k] = torch.randn(o.shape, generator=gen, device=dev)
+                total = total + (o * wts[k]).sum()
+            return total
+
+        tr = PKG.train_step.FlatGradTrainer(model, loss_fn, graph=graph)
+        PKG._trace.clear()
+        if graph:
+            tr.capture(batch, warmup=1)
+            tr._g_fb.replay()
+        else:
+            tr._forward_backward(batch)
+        torch.cuda.synchronize()
+        return tr.flat_grad.clone(), dict(PKG._trace.hits), [p.numel() for p in tr.params]
+
+    monkeypatch.setenv("MSDA_HIP_DETERMINISTIC", "1")
+    ref, hits_ref, sizes = run(0)
+    ref2, _, _ = run(0)  # the run-to-run spread of the step (reductions in arrival order elsewhere)
+    got, hits, _ = run(4096)
+    assert hits_ref.get("wgrad_batched", 0) == 0
+    assert hits.get("wgrad_batched", 0) >= 2 * 8  # 8 products per decoder layer (eager: one step)
+    off, bad = 0, []
+    for i, n in enumerate(sizes):
+        a, b, c = (t[off:off + n].double() for t in (got, ref, ref2))
+        scale = b.norm().item() + 1e-12
+        noise = (c - b).norm().item() / scale
+        err = (a - b).norm().item() / scale
+        # (a few-element bias gradient is a sum of thousands of signed terms: its relative error
+        # is that of a cancelling sum, bounded loosely)
+        if err > 2 * noise + (2e-3 if n >= 64 else 0.1):
+            bad.append((i, n, err, noise))
+        off += n
+    assert not bad, bad

@@ -224,17 +224,26 @@ def test_full_size_properties(dev, shapes, B):
     np.testing.assert_allclose(gl[:1].cpu().numpy(), r_gl, rtol=2e-4, atol=2e-5 * max(shapes))
 
 
-def test_bf16_T4096_bench_instantiation_matches_oracle(dev):
+@pytest.mark.parametrize("path", ["rows", "pair"])
+def test_bf16_T4096_bench_instantiation_matches_oracle(dev, path, monkeypatch):
     """The configs[3] per-rank call exactly as the T=4096 bench runs it: bf16 values, B=8, T=4096
-    (S = Lq = 7680), M=8, D=64, P=4 — the pair backward with 8 slots a wave, one workgroup per
-    (b, m, level) and (c0, c1) / positions staged in the workspace (they do not fit LDS beside
-    the keys).  Clips 0 and 7 against the oracle on the same bf16-rounded inputs in fp32
+    (S = Lq = 7680), M=8, D=64, P=4 — by default the row-block MFMA backward (csrc/msda_win.hip:
+    a level's 30,720 samples do not fit the pair kernel's LDS lists); "pair": the pair backward
+    with 8 slots a wave, one workgroup per (b, m, level) and (c0, c1) / positions staged in the
+    workspace.  Clips 0 and 7 against the oracle on the same bf16-rounded inputs in fp32
     (reference semantics attention.py:331-383)."""
+    if path == "pair":
+        monkeypatch.setenv("MSDA_HIP_BWD_WIN", "0")
+    else:
+        monkeypatch.delenv("MSDA_HIP_BWD_WIN", raising=False)
     shapes, B, M, D, P = [4096, 2048, 1024, 512], 8, 8, 64, 4
     Lq = sum(shapes)
     lib = PKG._native.load_library()
     ws = lib.msda_hip_backward_workspace_bytes(PKG._native.DTYPE_TAGS[torch.bfloat16], B, Lq, M, D, Lq, 4, P)
-    assert ws >= B * M * 4 * Lq * P * 12  # the workspace-staged pair path (12 B per sample)
+    if path == "pair":
+        assert ws >= B * M * 4 * Lq * P * 12  # the workspace-staged pair path (12 B per sample)
+    else:
+        assert ws == B * M * 4 * ((Lq + 31) // 32) * 8  # the row-block path's tile intervals only
     value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=41, lo=0.0, hi=1.0)
     out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout)
     assert gv.dtype == torch.bfloat16

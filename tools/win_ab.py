@@ -33,18 +33,20 @@ def run(win, args, iters=20):
 
 def main():
     dev = torch.device("cuda", 0)
-    for T in (1024, 4096):
-        shapes = [T, T // 2, T // 4, T // 8]
+    cases = [("enc", [1024, 512, 256, 128], 1920), ("enc", [4096, 2048, 1024, 512], 7680),
+             ("video->audio", [50, 25, 13, 7], 1920)]  # configs[2]: video queries on the audio pyramid
+    for name, shapes, Lq in cases:
+        T = shapes[0]
         S = sum(shapes)
-        starts = [0, T, T + T // 2, T + T // 2 + T // 4]
+        starts = [sum(shapes[:i]) for i in range(len(shapes))]
         for regime in ("init", "trained"):
-            value, loc, aw, gout = make(regime, 8, S, shapes, 8, 4, torch.bfloat16, dev)
+            value, loc, aw, gout = make(regime, 8, Lq, shapes, 8, 4, torch.bfloat16, dev)
             args = (value, shapes, starts, loc, aw, gout)
             t_pair, r_pair = run("0", args)
             t_win, r_win = run("1", args)
             err = [((a.float() - b.float()).norm() / b.float().norm()).item() for a, b in zip(r_win, r_pair)]
-            nbytes = msda.algorithmic_bytes("bwd", 8, S, 8, 64, S, 4, 4, 2)
-            print(json.dumps({"T": T, "regime": regime, "pair_us": round(t_pair, 2), "win_us": round(t_win, 2),
+            nbytes = msda.algorithmic_bytes("bwd", 8, S, 8, 64, Lq, 4, 4, 2)
+            print(json.dumps({"call": name, "T": T, "Lq": Lq, "regime": regime, "pair_us": round(t_pair, 2), "win_us": round(t_win, 2),
                               "win_frac": round(nbytes / (t_win * 1e-6) / 8e12, 4),
                               "rel_diff_gv_gl_ga": [round(e, 6) for e in err]}), flush=True)
 
