@@ -2638,18 +2638,31 @@ int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, 
 }
 
 // Row-block MFMA backward (msda_win.hip): bf16 values, D = 64, P <= 8, a call with more than 512
-// samples a level.  MSDA_HIP_BWD_WIN (read per call): "0" never, "1" wherever it applies;
-// unset: where a level's samples do not fit the pair kernel's LDS lists (16 B a sample: key,
-// (c0, c1), position), i.e. where the pair kernel would stage them through a workspace — the
-// configs[3] per-rank call (T = 4096: 262-294 us against 420-510, tools/win_ab.py); at the
-// encoder shape (T = 1024) the pair kernel is faster (69-82 us against 89-98).
+// samples a level.  MSDA_HIP_BWD_WIN (read per call): "0" never, "1" wherever it applies; unset:
+//  * where a level's samples do not fit the pair kernel's LDS lists (16 B a sample: key, (c0, c1),
+//    position), i.e. where the pair kernel would stage them through a workspace — the configs[3]
+//    per-rank call (T = 4096: 237-263 us against 421-511, tools/win_ab.py);
+//  * self-attention-like calls — queries covering the value pyramid (2 Lq >= S) and every level at
+//    least 64 rows: the encoder (T = 1024: 68-77 us against 69-82).  Cross-modal calls onto a short
+//    pyramid (video queries on the 95-row audio pyramid: every query tile meets every row block)
+//    keep the pair kernel (66 us against 127).
 int win_env() { return env_int("MSDA_HIP_BWD_WIN", -1); }
 
-bool win_applies(int value_dtype, long long D, long long Lq, long long P, long long M, long long L) {
-  if (value_dtype != MSDA_DTYPE_BF16 || !msda_win_supported(1, D, P, Lq, M * L * P) || Lq * P <= 512) return false;
-  const int e = win_env();
-  if (e >= 0) return e == 1;
-  return (size_t)(Lq * P) * 16 > kPairLdsMax;
+bool win_supported_call(int value_dtype, long long D, long long Lq, long long P, long long M, long long L) {
+  return value_dtype == MSDA_DTYPE_BF16 && msda_win_supported(1, D, P, Lq, M * L * P) && Lq * P > 512 &&
+         win_env() != 0 && bwd_env_path() == 0;  // (a forced MSDA_HIP_BWD_PATH keeps its path)
+}
+
+bool win_overflow(long long Lq, long long P) { return (size_t)(Lq * P) * 16 > kPairLdsMax; }
+
+// the decision for a call (levels known)
+bool win_applies(int value_dtype, long long D, long long Lq, long long P, long long M, long long L, const int* T,
+                 long long S) {
+  if (!win_supported_call(value_dtype, D, Lq, P, M, L)) return false;
+  if (win_env() == 1 || win_overflow(Lq, P)) return true;
+  int minT = 1 << 30;
+  for (int l = 0; l < L; ++l) minT = min(minT, T[l]);
+  return minT >= 64 && 2 * Lq >= S;
 }
 
 template <typename scalar_t, typename coord_t>
@@ -2667,7 +2680,7 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     if constexpr (std::is_same<scalar_t, bf16_t>::value) {
       // (gval may be null: the row-block kernel then writes the coordinate gradients only)
       if (pr.B * pr.M * pr.S > 0 && !sparse && workspace != nullptr &&
-          win_applies(value_dtype, pr.D, pr.Lq, pr.P, pr.M, pr.L)) {
+          win_applies(value_dtype, pr.D, pr.Lq, pr.P, pr.M, pr.L, pr.lv.T, pr.S)) {
         WinShape sh{};
         sh.B = pr.B; sh.S = pr.S; sh.M = pr.M; sh.Lq = pr.Lq; sh.L = (int)pr.L; sh.P = (int)pr.P;
         for (int l = 0; l < pr.L; ++l) {
@@ -3310,13 +3323,15 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
   (void)channels;
   if (batch <= 0 || spatial_size <= 0 || num_heads <= 0) return 0;
   PairPlan pp;
-  // the row-block MFMA path's tile intervals (when it may run) share the workspace
-  const size_t win = win_applies(value_dtype, channels, num_query, num_point, num_heads, num_levels)
-                         ? msda_win_workspace_bytes(batch, num_heads, num_levels, num_query) : 0;
-  if (win > 0) return win;  // the call takes the row-block path (same decision, run_backward)
+  // the row-block MFMA path's tile intervals (when it may run: the levels are not known here)
+  const bool may_win = win_supported_call(value_dtype, channels, num_query, num_point, num_heads, num_levels);
+  const size_t win = may_win ? msda_win_workspace_bytes(batch, num_heads, num_levels, num_query) : 0;
+  if (may_win && (win_env() == 1 || win_overflow(num_query, num_point)))
+    return win;  // the call takes the row-block path whatever its levels (run_backward)
   if (value_dtype != MSDA_DTYPE_F64 && pair_plan(value_dtype, batch, num_heads, num_query, num_point, channels,
                                                   num_levels, nullptr, spatial_size, true, &pp))
-    return pp.ws_bytes;
+    return std::max(pp.ws_bytes, win);
+  if (win > 0) return win;
   if (use_fused_gvalue(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point))
     return 0;
   return bwd_layout(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point).total;

@@ -52,11 +52,6 @@ typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
 // (the v4i16 form of the transposed read with per-element bit casts into a bf16x8 was compiled
 // into a splat of element 0 — tools/probes/mfma_tr_probe.hip; the v4bf16 form + shufflevector is exact)
 
-__device__ __forceinline__ unsigned xcd_block(unsigned orig, unsigned nwg) {
-  const unsigned xcd = orig % 8u, q = nwg / 8u, r = nwg % 8u;
-  return (xcd < r ? xcd * (q + 1u) : r * (q + 1u) + (xcd - r) * q) + orig / 8u;
-}
-
 struct Taps {
   int base;      // floor of the sample position (-1 .. T-1); taps base, base + 1
   float w0, w1;  // 0 for a tap outside the map
@@ -110,55 +105,60 @@ __device__ __forceinline__ int2 sample_rows(const Taps& t) {
   return make_int2(t.base < 0 ? 0 : t.base, t.base + 1);
 }
 
-// The row interval every (b, m, level, query tile) touches or owns.  One wave per (b, tile): a
-// query's coordinates of all heads and levels are one contiguous row of M * L * P floats, so the
-// wave reads the tile's 32 rows coalesced (lane i holds float i + 64 j of each row) and reduces
-// each (m, level)'s P consecutive floats over P lanes at the end.
+// The row interval every (b, m, level, query tile) touches or owns.  One 256-thread workgroup per
+// (b, tile): a query's coordinates of all heads and levels are one contiguous row of M * L * P
+// floats, so each wave reads 8 of the tile's 32 rows coalesced (lane i: floats i + 64 j), every
+// load issued before the first is used; each (m, level)'s P consecutive floats are reduced over P
+// lanes, then the four waves' intervals through LDS.
 constexpr int kRowRegs = 8;  // M * L * P <= 512 floats per query row
-template <bool ZEROS>
+constexpr int kTileWaves = kThreads / 64;
+constexpr int kQPW = kQT / kTileWaves;  // queries per wave
+template <bool ZEROS, int NJ>
 __global__ __launch_bounds__(kThreads) void win_tiles_kernel(const float* __restrict__ loc, int2* __restrict__ tiles,
-                                                             const WinShape sh, const long long n_waves) {
-  const long long wv = (long long)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (wv >= n_waves) return;  // wave-uniform
-  const int lane = threadIdx.x & 63;
-  const int tile = (int)(wv % sh.ntile);
-  const long long b = wv / sh.ntile;
+                                                             const WinShape sh) {
+  __shared__ int2 s_iv[kTileWaves][64 * NJ];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int tile = (int)(blockIdx.x % (unsigned)sh.ntile);
+  const long long b = blockIdx.x / (unsigned)sh.ntile;
   const int P = sh.P, n = (int)sh.M * sh.L * P;
-  const int q0 = tile * kQT, nq = (int)min((long long)kQT, sh.Lq - q0);
+  const int q0 = tile * kQT + w * kQPW;
+  const int nq = (int)max(0LL, min((long long)kQPW, sh.Lq - q0));
   const float* __restrict__ rows = loc + (b * sh.Lq + q0) * (long long)n;
-  int lo[kRowRegs], hi[kRowRegs], T[kRowRegs];
+  float x[kQPW][NJ];
 #pragma unroll
-  for (int j = 0; j < kRowRegs; ++j) {
-    lo[j] = kNone;
-    hi[j] = -kNone;
-    T[j] = sh.T[((lane + 64 * j) / P) % sh.L];
-  }
-  for (int q = 0; q < nq; q += 4) {
-    float x[4][kRowRegs];
+  for (int u = 0; u < kQPW; ++u)
 #pragma unroll
-    for (int u = 0; u < 4; ++u)
+    for (int j = 0; j < NJ; ++j)
+      x[u][j] = (u < nq && lane + 64 * j < n) ? rows[(long long)u * n + lane + 64 * j] : 0.f;
 #pragma unroll
-      for (int j = 0; j < kRowRegs; ++j)
-        x[u][j] = (q + u < nq && lane + 64 * j < n) ? rows[(long long)(q + u) * n + lane + 64 * j] : 0.f;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-#pragma unroll
-      for (int j = 0; j < kRowRegs; ++j) {
-        if (q + u < nq && lane + 64 * j < n) {
-          const int2 r = sample_rows<ZEROS>(make_taps<ZEROS>(x[u][j], T[j]));
-          lo[j] = min(lo[j], r.x);
-          hi[j] = max(hi[j], r.y);
-        }
-      }
-  }
-#pragma unroll
-  for (int j = 0; j < kRowRegs; ++j) {
-    for (int o = 1; o < P; o <<= 1) {
-      lo[j] = min(lo[j], __shfl_xor(lo[j], o));
-      hi[j] = max(hi[j], __shfl_xor(hi[j], o));
-    }
+  for (int j = 0; j < NJ; ++j) {
     const int i = lane + 64 * j;
-    if (i < n && i % P == 0) tiles[(b * sh.M * sh.L + i / P) * sh.ntile + tile] = make_int2(lo[j], hi[j]);
+    const int T = sh.T[(i / P) % sh.L];
+    int lo = kNone, hi = -kNone;
+#pragma unroll
+    for (int u = 0; u < kQPW; ++u) {
+      if (u < nq && i < n) {
+        const int2 r = sample_rows<ZEROS>(make_taps<ZEROS>(x[u][j], T));
+        lo = min(lo, r.x);
+        hi = max(hi, r.y);
+      }
+    }
+    for (int o = 1; o < P; o <<= 1) {
+      lo = min(lo, __shfl_xor(lo, o));
+      hi = max(hi, __shfl_xor(hi, o));
+    }
+    s_iv[w][i] = make_int2(lo, hi);
+  }
+  __syncthreads();
+  for (int g = threadIdx.x; g * P < n; g += kThreads) {  // one (m, level) per thread
+    int2 iv = s_iv[0][g * P];
+#pragma unroll
+    for (int v = 1; v < kTileWaves; ++v) {
+      const int2 o = s_iv[v][g * P];
+      iv.x = min(iv.x, o.x);
+      iv.y = max(iv.y, o.y);
+    }
+    tiles[(b * sh.M * sh.L + g) * sh.ntile + tile] = iv;
   }
 }
 
@@ -199,12 +199,27 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
   __shared__ int s_q[NS + kQT];  // query row (in the tile) of each compacted sample, padded
 
   const int lane = threadIdx.x, g = lane >> 4, li = lane & 15;
-  const unsigned id = xcd_block(blockIdx.x, gridDim.x);
-  const unsigned bm = id / (unsigned)sh.nblk;
-  unsigned rem = id % (unsigned)sh.nblk;
-  int l = 0;
-  while (l + 1 < sh.L && rem >= (unsigned)sh.blk0[l + 1]) ++l;
-  const int k = (int)rem - sh.blk0[l];
+  // dispatch order: the coarsest level's blocks first (a level-3 block meets ~12 query tiles, a
+  // level-0 block ~5: longest first shortens the tail), each level split into 8 contiguous chunks,
+  // chunk x on XCD x (block p runs on XCD p % 8), so neighbouring blocks share that XCD's L2
+  const unsigned x8 = blockIdx.x % 8u;
+  unsigned slot = blockIdx.x / 8u;
+  int l = sh.L - 1;
+  long long j = -1;
+  for (; l >= 0; --l) {
+    const long long nl = (long long)sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]);
+    const unsigned cl = (unsigned)((nl + 7) / 8);
+    if (slot < cl) {
+      j = (long long)x8 * cl + slot;
+      if (j >= nl) return;  // padding of the level's last chunk (wave-uniform, before any LDS use)
+      break;
+    }
+    slot -= cl;
+  }
+  if (l < 0) return;
+  const int nbl = sh.blk0[l + 1] - sh.blk0[l];
+  const unsigned bm = (unsigned)(j / nbl);
+  const int k = (int)(j % nbl);
   const int m = (int)(bm % (unsigned)sh.M);
   const long long b = bm / (unsigned)sh.M;
   const int T = sh.T[l], LP = sh.L * P;
@@ -450,17 +465,24 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   sh.nblk = nb;
   if (sh.B * sh.M == 0 || nb == 0) return 0;
   auto* tiles = static_cast<int2*>(workspace);
-  const long long n_waves = sh.B * sh.ntile;
-  if (n_waves > 0) {
-    const unsigned blocks = (unsigned)((n_waves + 3) / 4);
-    if (zeros)
-      hipLaunchKernelGGL(win_tiles_kernel<true>, dim3(blocks), dim3(kThreads), 0, st,
-                         static_cast<const float*>(loc), tiles, sh, n_waves);
-    else
-      hipLaunchKernelGGL(win_tiles_kernel<false>, dim3(blocks), dim3(kThreads), 0, st,
-                         static_cast<const float*>(loc), tiles, sh, n_waves);
+  const unsigned tile_wgs = (unsigned)(sh.B * sh.ntile);
+  const int nj = (int)((sh.M * sh.L * sh.P + 63) / 64);
+  auto* lc0 = static_cast<const float*>(loc);
+#define WIN_TILES(Z, NJ) hipLaunchKernelGGL((win_tiles_kernel<Z, NJ>), dim3(tile_wgs), dim3(kThreads), 0, st, lc0, tiles, sh)
+#define WIN_TILES_NJ(Z)                                              \
+  do {                                                               \
+    if (nj <= 1) WIN_TILES(Z, 1);                                    \
+    else if (nj <= 2) WIN_TILES(Z, 2);                               \
+    else if (nj <= 4) WIN_TILES(Z, 4);                               \
+    else WIN_TILES(Z, 8);                                            \
+  } while (0)
+  if (tile_wgs > 0) {
+    if (zeros) WIN_TILES_NJ(true); else WIN_TILES_NJ(false);
   }
-  const unsigned grid = (unsigned)(sh.B * sh.M * nb);
+#undef WIN_TILES_NJ
+#undef WIN_TILES
+  unsigned grid = 0;  // 8 x per-level chunks (see win_bwd_kernel's dispatch order)
+  for (int l = 0; l < sh.L; ++l) grid += 8u * (unsigned)((sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + 7) / 8);
   const bool coords = gloc != nullptr || gaw != nullptr;
   auto* v = static_cast<const uint16_t*>(value);
   auto* lc = static_cast<const float*>(loc);

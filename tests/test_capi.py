@@ -39,8 +39,10 @@ def test_abi_version_and_workspace():
     # at T = 4096 (S = 7680) the keys alone fill LDS: fp16 stages each (b, m, level) workgroup's
     # entries' (c0, c1) and positions (12 B a sample) in the workspace, bf16 takes the row-block
     # MFMA backward (one int2 row interval per (b, m, level, 32-query tile))
-    for dt in (0, 2, 3):
+    for dt in (0, 3):
         assert lib.msda_hip_backward_workspace_bytes(dt, B, S, M, D, Lq, L, P) == 0
+    # bf16 may take the row-block MFMA backward (the encoder's calls): its tile intervals
+    assert lib.msda_hip_backward_workspace_bytes(2, B, S, M, D, Lq, L, P) == B * M * L * (Lq // 32) * 8
     assert lib.msda_hip_backward_workspace_bytes(3, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * 4 * Lq * P * 12
     assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * (4 * Lq // 32) * 8
     # split path (sort + pull): fp64, or heads not made of 16-byte chunks with few workgroups —
