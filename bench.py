@@ -59,6 +59,16 @@ MODELS = {"video": "DeformableDVCCore (UnimodalDeformableDVC proposal path)",
           "dvc": "UnimodalDeformableDVC (full training forward)"}
 
 
+def workload_label(args):
+    """configs[1] names T=1024; --T 4096 --config video is configs[3]'s per-rank shape (batch 64 over
+    8 GPUs = 8 clips per rank at T=4096); other lengths are named as what they are."""
+    if args.config == "video" and args.T != 1024:
+        head = ("configs[3] per-rank shape: " if args.T == 4096 and args.batch == 8 else f"configs[1] at T={args.T}: ")
+        return head + (f"models/deformable video-only, 4-level pyramid T={args.T} d=512, 100 queries; "
+                       "BaseEncoder + 6 enc + 6 dec + heads, AdamW step")
+    return WORKLOADS[args.config]
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -203,9 +213,12 @@ def cpu_baseline(args):
 
 
 def msda_source_sha16():
+    """The MSDA kernel sources' hash (as tools/pmc_summary.py records it with the PMC bytes)."""
     import hashlib
-    src = os.path.join(ROOT, "multimodal-feature-learning_amd", "csrc", "msda.hip")
-    return hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+    h = hashlib.sha256()
+    for f in ("msda.hip", "msda_win.hip"):
+        h.update(open(os.path.join(ROOT, "multimodal-feature-learning_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def roofline(summary, traffic):
@@ -218,8 +231,9 @@ def roofline(summary, traffic):
     tr = traffic.get(name) if traffic else None
     gathered = d["gather_bytes_per_launch"]
     return {"bound": "hbm", "kernel": name,
-            "timing": "HIP events around each MSDA C-ABI call on its launch stream (one kernel: "
-                      "msda_fwd16_kernel / msda_bwd_pair_kernel), eager steps after the timed region",
+            "timing": "HIP events around each MSDA C-ABI call on its launch stream (forward: msda_fwd16_kernel; "
+                      "encoder backward: win_tiles_kernel + win_bwd_kernel, the row-block MFMA backward), "
+                      "eager steps after the timed region",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": tr,
             "algorithmic_bytes_per_launch": d["bytes_per_launch"], "avg_launch_ms": round(d["avg_ms"], 5),
@@ -361,7 +375,7 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "bf16" if use_bf16 else "fp32",
             "data": "synthetic (ActivityNet-shaped features N(0,1), random-init weights)",
-            "config": {"workload": WORKLOADS[args.config], "model": MODELS[args.config],
+            "config": {"workload": workload_label(args), "model": MODELS[args.config],
                        "global_batch": world * args.batch, "per_gpu_batch": args.batch, "seq_len": args.T,
                        "d_model": 512, "levels": 4, "queries": args.queries, "parallelism": f"dp{world}",
                        "execution": "hip_graph" if graph else "eager", "gemm_solutions": gemm_sel,

@@ -183,8 +183,8 @@ def test_gradcheck_fp64(dev, channels):
         assert torch.autograd.gradcheck(f, inputs, eps=1e-6, atol=1e-5, rtol=1e-4)
 
 
-@pytest.mark.parametrize("shapes,B", [([1024, 512, 256, 128], 8),     # configs[1] encoder call (fused backward)
-                                      ([4096, 2048, 1024, 512], 2)])  # configs[3]: S = 7680 (sort + pull)
+@pytest.mark.parametrize("shapes,B", [([1024, 512, 256, 128], 8),     # configs[1] encoder call (fp32: pair backward)
+                                      ([4096, 2048, 1024, 512], 2)])  # configs[3]: S = 7680 (fp32: workspace-staged pair)
 def test_full_size_properties(dev, shapes, B):
     """At full encoder-call sizes (the bench's B=8, T=1024; and T=4096, S=7680) where the oracle
     is too slow to run whole: linearity in value and in aw, the adjoint identity

@@ -50,17 +50,19 @@ def main(root):
 # pyramid, bf16; tools/pmc_msda.sh runs the encoder shape only, so one grid per kernel)
 CALL_KERNELS = {
     "msda_fwd_S1920_Lq1920": ("msda_fwd16_kernel",),
-    "msda_bwd_S1920_Lq1920": ("msda_bwd_pair_kernel",),
+    "msda_bwd_S1920_Lq1920": ("win_tiles_kernel", "win_bwd_kernel"),  # row-block MFMA backward (msda_win.hip)
 }
 
 
 def source_sha16():
-    """sha256 (16 hex) of csrc/msda.hip: bench.py takes the traffic only while the kernels that
-    produced it are the ones it runs."""
+    """sha256 (16 hex) of csrc/msda.hip + csrc/msda_win.hip: bench.py takes the traffic only while
+    the kernels that produced it are the ones it runs."""
     import hashlib
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    src = os.path.join(root, "multimodal-feature-learning_amd", "csrc", "msda.hip")
-    return hashlib.sha256(open(src, "rb").read()).hexdigest()[:16]
+    h = hashlib.sha256()
+    for f in ("msda.hip", "msda_win.hip"):
+        h.update(open(os.path.join(root, "multimodal-feature-learning_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
 
 
 def traffic_per_call(out):
