@@ -138,8 +138,10 @@ def build_batch(args, rank, device):
     return video, mask, dur
 
 
-def loss_fn(args, batch=None):
+def loss_fn(args, batch=None, model=None):
     if args.config == "dvc":
+        if args.graph:  # the step around its host matching as two HIP graphs (train_step.py, staged losses)
+            return PKG.dvc_core.StagedDVCLoss(batch[0], model)
         return lambda result: PKG.dvc_core.dvc_workload_loss(result, batch[0])
     return {"video": PKG.dvc_core.workload_loss, "multimodal": PKG.dvc_core.multimodal_workload_loss,
             "sparse": PKG.dvc_core.sparse_workload_loss}[args.config]
@@ -169,7 +171,9 @@ class PhaseTimer:
         import sys as _sys
         mod = _sys.modules[type(model).__module__]
         model.forward_proposals = self.wrap("proposals_fwd", model.forward_proposals)
-        model.matcher.match_levels = self.wrap("matching (cost on device, LSA on the host)", model.matcher.match_levels)
+        model.matcher.level_costs = self.wrap("matching costs (device)", model.matcher.level_costs)
+        model.matcher.solve_levels = self.wrap("matching (device->host copy, LSA on the host)",
+                                               model.matcher.solve_levels)
         mod.segment_memory = self.wrap("segment crop", mod.segment_memory)
         dec = model.unimodal_caption_decoder
         dec.forward = self.wrap("caption_decoder_fwd", dec.forward)
@@ -318,11 +322,11 @@ def main():
             dist.broadcast(t.data, src=0)
     use_bf16 = args.dtype == "bf16"
     batch = build_batch(args, rank, device)
-    graph = bool(args.graph) and args.config != "dvc"  # the host LSA sits inside the dvc forward
-    trainer = PKG.train_step.FlatGradTrainer(model, loss_fn(args, batch), lr=1e-4, weight_decay=1e-4,
+    graph = bool(args.graph)  # dvc: two graphs around the host matching (StagedDVCLoss)
+    trainer = PKG.train_step.FlatGradTrainer(model, loss_fn(args, batch, model), lr=1e-4, weight_decay=1e-4,
                                              max_norm=0.1, use_bf16=use_bf16, graph=graph)
     phases = None
-    if args.config == "dvc":
+    if args.config == "dvc" and not graph:
         phases = PhaseTimer()
         phases.install(model)
 
@@ -335,6 +339,8 @@ def main():
     torch.cuda.synchronize()
     if phases is not None:
         phases.on = True
+    if args.config == "dvc" and graph:
+        trainer.phase_events = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
         trainer.step(batch)
@@ -344,6 +350,13 @@ def main():
     elapsed = time.perf_counter() - t0
     if phases is not None:
         phases.on = False
+    graph_phases = None
+    if trainer.phase_events:
+        graph_phases = {}
+        for name, e0, e1 in trainer.phase_events:
+            graph_phases[name] = graph_phases.get(name, 0.0) + e0.elapsed_time(e1) / args.steps
+        graph_phases = {k: round(v, 3) for k, v in graph_phases.items()}
+        trainer.phase_events = None
     if world > 1:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -385,6 +398,8 @@ def main():
         }
         if phases is not None:
             result["phases_ms_per_step"] = phases.summary(args.steps, 1000 * elapsed / args.steps)
+        if graph_phases is not None:
+            result["phases_ms_per_step"] = graph_phases
         if args.cpu_baseline and world == 1 and args.config == "video":
             result["cpu_baseline"] = cpu_baseline(args)
         print(json.dumps(result), flush=True)

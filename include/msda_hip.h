@@ -100,6 +100,37 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
                       int64_t spatial_size, int64_t num_heads, int64_t channels,
                       int64_t num_query, int64_t num_point, int padding_mode, void* stream);
 
+/* Forward that also hands the backward its row intervals (ABI v5; an extension: the reference's
+ * extension has no forward-to-backward state beyond the saved inputs).  For calls whose backward
+ * takes the row-block MFMA path (bf16 values, channels == 64, encoder-like calls: the queries
+ * cover the pyramid; csrc/msda.hip win_takes) the backward first computes, for every
+ * (batch, head, level, tile of 32 queries), the value rows the tile's samples touch: a pass over
+ * all of sampling_loc.  The forward already reads sampling_loc, so it can write them instead.
+ *   msda_hip_forward_tiles_bytes  size of that interval buffer for a call, 0 when the call's
+ *                                 backward does not take the row-block path (then use the
+ *                                 plain entry points)
+ *   msda_hip_forward_tiles        msda_hip_forward + fills `tiles` (that many bytes)
+ *   msda_hip_backward_tiles       msda_hip_backward on the same inputs with the filled `tiles`
+ *                                 (the row-block path needs no other workspace; `workspace` is
+ *                                 then only read if the call takes another path, e.g. under
+ *                                 MSDA_HIP_BWD_WIN=0, and must be sized as for msda_hip_backward
+ *                                 whenever msda_hip_backward_workspace_bytes differs from the
+ *                                 tiles size) */
+size_t msda_hip_forward_tiles_bytes(int value_dtype, const int64_t* spatial_shapes, int64_t num_levels,
+                                    int64_t batch, int64_t spatial_size, int64_t num_heads, int64_t channels,
+                                    int64_t num_query, int64_t num_point);
+int msda_hip_forward_tiles(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                           const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                           const void* attn_weight, void* output, void* tiles, int64_t batch, int64_t spatial_size,
+                           int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
+                           int padding_mode, void* stream);
+int msda_hip_backward_tiles(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                            const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                            const void* attn_weight, const void* grad_output, void* grad_value,
+                            void* grad_loc, void* grad_attn, void* workspace, const void* tiles, int64_t batch,
+                            int64_t spatial_size, int64_t num_heads, int64_t channels,
+                            int64_t num_query, int64_t num_point, int padding_mode, void* stream);
+
 /* MSDA prologue.  Replaces the elementwise chain of MSDeformAttn.forward
  * between its two query projections and the core (reference models/modules/attention.py:468-483):
  *   attn_weight  = softmax(attn_logits over num_levels*num_point)                 (coord dtype)
@@ -125,6 +156,23 @@ int msda_hip_prologue_backward(const void* grad_loc, const void* grad_attn, cons
                                int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
                                int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
                                void* grad_offsets, void* grad_logits, void* grad_ref, void* stream);
+
+/* The same with the (batch, num_query) rows of sampling_offsets / attn_logits (and of
+ * grad_offsets / grad_logits) `in_stride` elements apart (>= num_heads*num_levels*num_point;
+ * ABI v6): both query projections can then be ONE GEMM writing [offsets | logits] rows of
+ * 2*num_heads*num_levels*num_point, read in place, and the backward writes both gradients into
+ * one such buffer, the input of one dgrad GEMM (models/modules/attention.py, _QueryPrologue). */
+int msda_hip_prologue_forward_ex(const void* sampling_offsets, const void* attn_logits, int dtype,
+                                 const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
+                                 int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,
+                                 int64_t num_point, int64_t in_stride, void* sampling_loc, void* attn_weight,
+                                 void* stream);
+int msda_hip_prologue_backward_ex(const void* grad_loc, const void* grad_attn, const void* attn_weight,
+                                  const void* sampling_offsets, int dtype, const void* reference_points,
+                                  int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
+                                  int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
+                                  int64_t in_stride, void* grad_offsets, void* grad_logits, void* grad_ref,
+                                  void* stream);
 
 /* Sparse-DETR decoder attention map.  Replaces attn_map_to_flat_grid
  * (reference utils/dam.py:20-73): per (row, head), the attention weight of every sample is

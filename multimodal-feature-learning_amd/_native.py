@@ -20,15 +20,20 @@ LIB_PATH = os.environ.get("MSDA_HIP_LIB", LIB_PATH)
 DTYPE_TAGS = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2, torch.float16: 3}
 PAD_TAGS = {"border": 0, "zeros": 1}
 MAX_LEVELS = 16
-ABI_VERSION = 4
+ABI_VERSION = 6
 
 # every symbol include/msda_hip.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "msda_hip_forward",
     "msda_hip_backward",
     "msda_hip_backward_workspace_bytes",
+    "msda_hip_forward_tiles_bytes",
+    "msda_hip_forward_tiles",
+    "msda_hip_backward_tiles",
     "msda_hip_prologue_forward",
     "msda_hip_prologue_backward",
+    "msda_hip_prologue_forward_ex",
+    "msda_hip_prologue_backward_ex",
     "msda_hip_dam_flat_grid",
     # include/flat_adamw.h (training-step runtime, same library)
     "flat_adamw_workspace_bytes",
@@ -67,10 +72,23 @@ def _declare(lib):
     lib.msda_hip_backward.restype = i32
     lib.msda_hip_backward.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp, vp, vp, vp,
                                       i64, i64, i64, i64, i64, i64, i32, vp]
+    lib.msda_hip_forward_tiles_bytes.restype = ctypes.c_size_t
+    lib.msda_hip_forward_tiles_bytes.argtypes = [i32, p64, i64, i64, i64, i64, i64, i64, i64]
+    lib.msda_hip_forward_tiles.restype = i32
+    lib.msda_hip_forward_tiles.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp,
+                                           i64, i64, i64, i64, i64, i64, i32, vp]
+    lib.msda_hip_backward_tiles.restype = i32
+    lib.msda_hip_backward_tiles.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                            i64, i64, i64, i64, i64, i64, i32, vp]
     lib.msda_hip_backward_workspace_bytes.restype = ctypes.c_size_t
     lib.msda_hip_backward_workspace_bytes.argtypes = [i32, i64, i64, i64, i64, i64, i64, i64]
     lib.msda_hip_prologue_forward.restype = i32
     lib.msda_hip_prologue_forward.argtypes = [vp, vp, i32, vp, i32, p64, i64, i64, i64, i64, i64, vp, vp, vp]
+    lib.msda_hip_prologue_forward_ex.restype = i32
+    lib.msda_hip_prologue_forward_ex.argtypes = [vp, vp, i32, vp, i32, p64, i64, i64, i64, i64, i64, i64, vp, vp, vp]
+    lib.msda_hip_prologue_backward_ex.restype = i32
+    lib.msda_hip_prologue_backward_ex.argtypes = [vp, vp, vp, vp, i32, vp, i32, p64, i64, i64, i64, i64, i64, i64,
+                                                  vp, vp, vp, vp]
     lib.msda_hip_prologue_backward.restype = i32
     lib.msda_hip_prologue_backward.argtypes = [vp, vp, vp, vp, i32, vp, i32, p64, i64, i64, i64, i64, i64,
                                                vp, vp, vp, vp]

@@ -359,25 +359,13 @@ __device__ __forceinline__ void load_coords16(const float* __restrict__ p, int L
   }
 }
 
-template <typename scalar_t, int VEC, int G, bool ZEROS>
-__global__ __launch_bounds__(256) void msda_fwd16_kernel(
-    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
-    scalar_t* __restrict__ out, const Levels lv, const int L, const int P, const int S, const int M,
-    const int D, const int Lq, const long long n_items) {
+// One (b, q, m) item's output chunk: the body of msda_fwd16_kernel (vb: the item's head and
+// lane offset in its clip's value rows; rs: the row stride, tap offsets inside a clip fit 32 bits)
+template <typename scalar_t, int VEC, bool ZEROS>
+__device__ __forceinline__ void fwd16_item(const scalar_t* __restrict__ vb, const float (&lr)[kLPMax],
+                                           const float (&ar)[kLPMax], const Levels& lv, int P, int LP, int rs,
+                                           scalar_t* __restrict__ op) {
   using acc_t = float;
-  const long long tid = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-  const long long item = tid / G;
-  if (item >= n_items) return;
-  const int lg = (int)(tid % G);
-  const int m = (int)(item % M);
-  const long long b = item / M / Lq;
-  const long long rowstride = (long long)M * D;
-  const int LP = L * P;
-  float lr[kLPMax], ar[kLPMax];
-  load_coords16(loc + item * LP, LP, lr);
-  load_coords16(aw + item * LP, LP, ar);
-  const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D + lg * VEC;
-  const int rs = M * D;  // row stride; tap offsets inside one clip fit 32 bits
   f32x2 acc2[VEC / 2];
 #pragma unroll
   for (int e = 0; e < VEC / 2; ++e) acc2[e] = f32x2{0.f, 0.f};
@@ -413,7 +401,97 @@ __global__ __launch_bounds__(256) void msda_fwd16_kernel(
     acc[2 * e] = acc2[e].x;
     acc[2 * e + 1] = acc2[e].y;
   }
-  store_vec<scalar_t, VEC>(out + item * D + lg * VEC, acc);
+  store_vec<scalar_t, VEC>(op, acc);
+}
+
+template <typename scalar_t, int VEC, int G, bool ZEROS>
+__global__ __launch_bounds__(256) void msda_fwd16_kernel(
+    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    scalar_t* __restrict__ out, const Levels lv, const int L, const int P, const int S, const int M,
+    const int D, const int Lq, const long long n_items) {
+  const long long tid = (long long)xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  const long long item = tid / G;
+  if (item >= n_items) return;
+  const int lg = (int)(tid % G);
+  const int m = (int)(item % M);
+  const long long b = item / M / Lq;
+  const int LP = L * P;
+  float lr[kLPMax], ar[kLPMax];
+  load_coords16(loc + item * LP, LP, lr);
+  load_coords16(aw + item * LP, LP, ar);
+  fwd16_item<scalar_t, VEC, ZEROS>(value + (b * S * M + m) * (long long)D + lg * VEC, lr, ar, lv, P, LP, M * D,
+                                   out + item * D + lg * VEC);
+}
+
+// msda_fwd16_kernel for D = 64 16-bit values (G = 8 lanes an item) that also writes the
+// row-block backward's tile intervals (msda_win.hip): for every (b, m, level, query tile of 32)
+// the rows [lo, hi] its samples touch or own (win_sample_rows, msda_win.h).  One 256-thread
+// workgroup per (b, m, tile): its 32 items are the tile's queries of one head, so the intervals
+// are reduced in the workgroup (xor shuffles over the 8 items of a wave, then LDS over the 4
+// waves) and written once, no atomics — the backward then skips its interval prepass (a kernel
+// that re-read all of loc: 11 us at the bench's encoder call).  Items in (b, m, q) order: each
+// still reads its 64-B loc / aw rows and writes its 128-B output row whole.
+template <typename scalar_t, bool ZEROS, int P>
+__global__ __launch_bounds__(256) void msda_fwd16_tiles_kernel(
+    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    scalar_t* __restrict__ out, int2* __restrict__ tiles, const Levels lv, const int L, const int S, const int M,
+    const int Lq, const int ntile) {
+  constexpr int VEC = 8, D = 64, NL = kLPMax / P;
+  __shared__ int2 s_iv[4][NL];
+  const unsigned wg = xcd_block(blockIdx.x, gridDim.x);
+  const unsigned bm = wg / (unsigned)ntile;
+  const int tile = (int)(wg % (unsigned)ntile);
+  const int m = (int)(bm % (unsigned)M);
+  const long long b = bm / (unsigned)M;
+  const int i = threadIdx.x >> 3, lg = threadIdx.x & 7;
+  const int q = tile * kWinQT + i;
+  const int LP = L * P;
+  int lo[NL], hi[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    lo[l] = kWinNone;
+    hi[l] = -kWinNone;
+  }
+  if (q < Lq) {
+    const long long item = (b * Lq + q) * M + m;
+    float lr[kLPMax], ar[kLPMax];
+    load_coords16(loc + item * LP, LP, lr);
+    load_coords16(aw + item * LP, LP, ar);
+    fwd16_item<scalar_t, VEC, ZEROS>(value + (b * S * M + m) * (long long)D + lg * VEC, lr, ar, lv, P, LP, M * D,
+                                     out + item * D + lg * VEC);
+#pragma unroll
+    for (int j = 0; j < kLPMax; ++j) {
+      if (j < LP) {
+        const int2 r = win_sample_rows(lr[j], lv.T[j / P], ZEROS);
+        lo[j / P] = min(lo[j / P], r.x);
+        hi[j / P] = max(hi[j / P], r.y);
+      }
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      lo[l] = min(lo[l], __shfl_xor(lo[l], o));
+      hi[l] = max(hi[l], __shfl_xor(hi[l], o));
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int l = 0; l < NL; ++l) s_iv[w][l] = make_int2(lo[l], hi[l]);
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < L) {
+    int2 iv = s_iv[0][threadIdx.x];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) {
+      const int2 o = s_iv[v][threadIdx.x];
+      iv.x = min(iv.x, o.x);
+      iv.y = max(iv.y, o.y);
+    }
+    tiles[((long long)bm * L + threadIdx.x) * ntile + tile] = iv;
+  }
 }
 
 // ---------------------------------------------------------------------------------
@@ -2063,7 +2141,7 @@ int fast16_group(const Problem& pr) {
 
 template <typename scalar_t, typename coord_t, int VEC>
 int run_forward(const Problem& pr, const void* value, const void* loc, const void* aw, void* out,
-                int pad, hipStream_t st) {
+                int pad, hipStream_t st, void* tiles = nullptr) {
   const long long n_items = pr.B * pr.Lq * pr.M;
   if (n_items == 0) return MSDA_OK;
   const int gshift = group_shift_for(pr.D / VEC);
@@ -2075,6 +2153,29 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
   auto* o = static_cast<scalar_t*>(out);
   if constexpr (!std::is_same<coord_t, double>::value && VEC * sizeof(scalar_t) == 16) {
     const int G = fast16_group<scalar_t>(pr);
+    if constexpr (sizeof(scalar_t) == 2) {
+    if (tiles != nullptr) {  // the caller checked forward_tiles_ok: 16-bit values, D = 64 (G = 8)
+      const int ntile = (int)((pr.Lq + kWinQT - 1) / kWinQT);
+      const unsigned tblocks = (unsigned)(pr.B * pr.M * ntile);
+      auto* tl = static_cast<int2*>(tiles);
+#define MSDA_FT(Z, PP)                                                                              \
+  hipLaunchKernelGGL((msda_fwd16_tiles_kernel<scalar_t, Z, PP>), dim3(tblocks), dim3(256), 0, st, v, lc, a, o, \
+                     tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile)
+#define MSDA_FT_P(Z)                                                                                \
+  switch (pr.P) {                                                                                 \
+    case 1: MSDA_FT(Z, 1); break;                                                                 \
+    case 2: MSDA_FT(Z, 2); break;                                                                 \
+    case 4: MSDA_FT(Z, 4); break;                                                                 \
+    default: MSDA_FT(Z, 8); break;                                                                \
+  }
+      if (tblocks > 0) {
+        if (pad == MSDA_PAD_ZEROS) { MSDA_FT_P(true) } else { MSDA_FT_P(false) }
+      }
+#undef MSDA_FT_P
+#undef MSDA_FT
+      return launch_status("forward (tiles)");
+    }
+    }
     if (G > 0) {
       const unsigned fblocks = (unsigned)((n_items * G + 255) / 256);
 #define MSDA_F16(GG, Z)                                                                            \
@@ -2665,10 +2766,28 @@ bool win_applies(int value_dtype, long long D, long long Lq, long long P, long l
   return minT >= 64 && 2 * Lq >= S;
 }
 
+// The backward of this call takes the row-block MFMA path (msda_win.hip) when handed a workspace
+// or the forward's tile intervals (run_backward below)
+bool win_takes(const Problem& pr, int value_dtype) {
+  if (pr.B * pr.M * pr.S <= 0) return false;
+  int minT = 1 << 30;
+  for (int l = 0; l < pr.L; ++l) minT = min(minT, pr.lv.T[l]);
+  const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1) || pr.Lq * pr.P <= 512;
+  return !sparse && win_applies(value_dtype, pr.D, pr.Lq, pr.P, pr.M, pr.L, pr.lv.T, pr.S);
+}
+
+// The forward can write those intervals: the win_takes calls the tiles forward kernel covers
+// (16-bit values with D = 64: 8 lanes an item, 32 items a workgroup; P of the win kernel)
+bool forward_tiles_ok(const Problem& pr, int value_dtype) {
+  if (value_dtype != MSDA_DTYPE_BF16 || pr.D != 64 || pr.L * pr.P > kLPMax || (pr.L * pr.P) % 4 != 0) return false;
+  if (!(pr.P == 1 || pr.P == 2 || pr.P == 4 || pr.P == 8)) return false;
+  return win_takes(pr, value_dtype);
+}
+
 template <typename scalar_t, typename coord_t>
 int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
                  const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
-                 int value_dtype, int pad, hipStream_t st) {
+                 int value_dtype, int pad, hipStream_t st, const void* tiles = nullptr) {
   if constexpr (std::is_same<coord_t, float>::value) {
     const int ns = pr.B * pr.M * pr.S > 0 ? fused_bwd_rows<scalar_t, coord_t>(pr, value_dtype, gval) : 0;
     // sparse or tiny calls (every level at most 4 samples a row: decoder-like; or at most 512
@@ -2679,15 +2798,14 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1) || pr.Lq * pr.P <= 512;
     if constexpr (std::is_same<scalar_t, bf16_t>::value) {
       // (gval may be null: the row-block kernel then writes the coordinate gradients only)
-      if (pr.B * pr.M * pr.S > 0 && !sparse && workspace != nullptr &&
-          win_applies(value_dtype, pr.D, pr.Lq, pr.P, pr.M, pr.L, pr.lv.T, pr.S)) {
+      if ((workspace != nullptr || tiles != nullptr) && win_takes(pr, value_dtype)) {
         WinShape sh{};
         sh.B = pr.B; sh.S = pr.S; sh.M = pr.M; sh.Lq = pr.Lq; sh.L = (int)pr.L; sh.P = (int)pr.P;
         for (int l = 0; l < pr.L; ++l) {
           sh.T[l] = pr.lv.T[l];
           sh.start[l] = pr.lv.start[l];
         }
-        msda_win_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, &sh, pad == MSDA_PAD_ZEROS, st);
+        msda_win_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, tiles, &sh, pad == MSDA_PAD_ZEROS, st);
         return launch_status("backward rows (mfma)");
       }
     }
@@ -2811,7 +2929,7 @@ __global__ __launch_bounds__(1024) void msda_prologue_fwd_kernel(
     const scalar_t* __restrict__ off, const scalar_t* __restrict__ logits,
     const coord_t* __restrict__ ref, const int ref_dim, coord_t* __restrict__ loc,
     coord_t* __restrict__ aw, const Levels lv, const int L, const int P, const int M,
-    const long long n_queries, const int G, const int sQS, const int sLP, const int sP) {
+    const long long n_queries, const int G, const int sQS, const int sLP, const int sP, const long long is) {
 #pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   coord_t* sx = reinterpret_cast<coord_t*>(smem_raw);
@@ -2824,9 +2942,10 @@ __global__ __launch_bounds__(1024) void msda_prologue_fwd_kernel(
   const long long bq = active ? bq_raw : 0;  // clamped: every load below is unconditional
   const int r = ix.r, j = ix.j, l = ix.l;
   const long long e = bq * QS + r;
+  const long long ei = bq * is + r;  // offsets / logits rows: `is` elements apart
   // all global loads of the thread issued together: one round trip
-  const coord_t x = (coord_t)to_acc(logits[e]);
-  const coord_t v = (coord_t)to_acc(off[e]);
+  const coord_t x = (coord_t)to_acc(logits[ei]);
+  const coord_t v = (coord_t)to_acc(off[ei]);
   const coord_t r0 = ref[(bq * L + l) * ref_dim];
   const coord_t r1 = ref[(bq * L + l) * ref_dim + (ref_dim - 1)];
   const coord_t T = (coord_t)level_T(lv, l, L);
@@ -2848,7 +2967,7 @@ __global__ __launch_bounds__(1024) void msda_prologue_bwd_kernel(
     const coord_t* __restrict__ aw, const scalar_t* __restrict__ off, const coord_t* __restrict__ ref,
     const int ref_dim, scalar_t* __restrict__ grad_off, scalar_t* __restrict__ grad_logits,
     coord_t* __restrict__ grad_ref, const Levels lv, const int L, const int P, const int M,
-    const long long n_queries, const int G, const int sQS, const int sLP, const int sP) {
+    const long long n_queries, const int G, const int sQS, const int sLP, const int sP, const long long is) {
 #pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   coord_t* s0 = reinterpret_cast<coord_t*>(smem_raw);  // g*y, then grad_loc
@@ -2861,28 +2980,29 @@ __global__ __launch_bounds__(1024) void msda_prologue_bwd_kernel(
   const long long bq = active ? bq_raw : 0;  // clamped: loads below are unconditional
   const int r = ix.r, j = ix.j, l = ix.l;
   const long long e = bq * QS + r;
+  const long long ei = bq * is + r;  // offsets / logits (and their gradients) rows: `is` elements apart
   const bool pow2 = (LP & (LP - 1)) == 0;
   const bool loc_side = grad_off != nullptr || grad_ref != nullptr;
   const bool box = ref_dim == 2;
   const coord_t T = (coord_t)level_T(lv, l, L);
   const coord_t gl = loc_side ? (active ? grad_loc[e] : (coord_t)0) : (coord_t)0;
   const coord_t r1 = box ? ref[(bq * L + l) * 2 + 1] : (coord_t)0;
-  const coord_t ov = box ? (coord_t)to_acc(off[e]) : (coord_t)0;
+  const coord_t ov = box ? (coord_t)to_acc(off[ei]) : (coord_t)0;
   if (grad_logits != nullptr) {  // uniform
     const coord_t g = active ? grad_aw[e] : (coord_t)0;
     const coord_t y = active ? aw[e] : (coord_t)0;
     const coord_t dot = item_reduce<coord_t, false>(g * y, LP, pow2, s0, t, t - j);
-    if (active) from_acc((typename AccOf<scalar_t>::type)(y * (g - dot)), &grad_logits[e]);
+    if (active) from_acc((typename AccOf<scalar_t>::type)(y * (g - dot)), &grad_logits[ei]);
   }
   if (!loc_side) return;
   coord_t gu = 0;  // box form: d loc / d ref1 contribution
   if (!box) {
     if (grad_off != nullptr && active)
-      from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gl) / T), &grad_off[e]);
+      from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gl) / T), &grad_off[ei]);
   } else if (active) {
     const coord_t gh = gl * (coord_t)0.5;
     if (grad_off != nullptr)
-      from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gh * r1) / (coord_t)P), &grad_off[e]);
+      from_acc((typename AccOf<scalar_t>::type)(round_to<scalar_t>(gh * r1) / (coord_t)P), &grad_off[ei]);
     gu = gh * round_to<scalar_t>(ov / (coord_t)P);
   }
   if (grad_ref == nullptr) return;  // uniform
@@ -2934,15 +3054,16 @@ template <typename scalar_t, int M, int P>
 __global__ __launch_bounds__(256) void msda_prologue16_fwd_kernel(
     const scalar_t* __restrict__ off, const scalar_t* __restrict__ logits, const float* __restrict__ ref,
     const int ref_dim, float* __restrict__ loc, float* __restrict__ aw, const Levels lv,
-    const long long n_items) {
+    const long long n_items, const long long is) {
 #pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
   constexpr int L = 16 / P;
   const long long item = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (item >= n_items) return;
   const long long bq = item / M;
+  const long long ii = bq * is + (item % M) * 16;  // offsets / logits rows: `is` elements apart
   float x[16], v[16];
-  load16s<scalar_t>(logits + item * 16, x);
-  load16s<scalar_t>(off + item * 16, v);
+  load16s<scalar_t>(logits + ii, x);
+  load16s<scalar_t>(off + ii, v);
   float mx = x[0];
 #pragma unroll
   for (int j = 1; j < 16; ++j) mx = x[j] > mx ? x[j] : mx;
@@ -2974,7 +3095,7 @@ __global__ __launch_bounds__(256) void msda_prologue16_bwd_kernel(
     const float* __restrict__ grad_loc, const float* __restrict__ grad_aw, const float* __restrict__ aw,
     const scalar_t* __restrict__ off, const float* __restrict__ ref, const int ref_dim,
     scalar_t* __restrict__ grad_off, scalar_t* __restrict__ grad_logits, float* __restrict__ grad_ref,
-    const Levels lv, const long long n_items) {
+    const Levels lv, const long long n_items, const long long is) {
 #pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
   constexpr int L = 16 / P;
   const long long item_raw = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2982,6 +3103,7 @@ __global__ __launch_bounds__(256) void msda_prologue16_bwd_kernel(
   const long long item = active ? item_raw : 0;
   const long long bq = item / M;
   const int m = (int)(item % M);
+  const long long ii = bq * is + m * 16;  // offsets / logits (and their gradients): rows `is` elements apart
   if (grad_logits != nullptr) {
     float g[16], y[16];
     load16s<float>(grad_aw + item * 16, g);
@@ -2991,13 +3113,13 @@ __global__ __launch_bounds__(256) void msda_prologue16_bwd_kernel(
     for (int j = 0; j < 16; ++j) dot += g[j] * y[j];
 #pragma unroll
     for (int j = 0; j < 16; ++j) g[j] = y[j] * (g[j] - dot);
-    if (active) store16s<scalar_t>(grad_logits + item * 16, g);
+    if (active) store16s<scalar_t>(grad_logits + ii, g);
   }
   if (grad_off == nullptr && grad_ref == nullptr) return;
   float gl[16], o[16];
   load16s<float>(grad_loc + item * 16, gl);
   const bool box = ref_dim == 2;
-  if (box) load16s<scalar_t>(off + item * 16, o);
+  if (box) load16s<scalar_t>(off + ii, o);
   const float* __restrict__ rb = ref + bq * L * ref_dim;
   float go[16], s1[16];
 #pragma unroll
@@ -3012,7 +3134,7 @@ __global__ __launch_bounds__(256) void msda_prologue16_bwd_kernel(
       s1[j] = gh * round_to<scalar_t>(o[j] / (float)P);
     }
   }
-  if (grad_off != nullptr && active) store16s<scalar_t>(grad_off + item * 16, go);
+  if (grad_off != nullptr && active) store16s<scalar_t>(grad_off + ii, go);
   if (grad_ref != nullptr) {
 #pragma unroll
     for (int l = 0; l < L; ++l) {
@@ -3035,7 +3157,7 @@ __global__ __launch_bounds__(256) void msda_prologue16_bwd_kernel(
 template <typename scalar_t, typename coord_t>
 int run_prologue(bool fwd, const Problem& pr, int ref_dim, const void* off, const void* logits,
                  const void* ref, void* loc, void* aw, const void* grad_loc, const void* grad_aw,
-                 void* grad_off, void* grad_logits, void* grad_ref, hipStream_t st) {
+                 void* grad_off, void* grad_logits, void* grad_ref, long long is, hipStream_t st) {
   const long long n_queries = pr.B * pr.Lq;
   if (n_queries == 0) return MSDA_OK;
   if constexpr (!std::is_same<coord_t, double>::value) {
@@ -3054,12 +3176,12 @@ int run_prologue(bool fwd, const Problem& pr, int ref_dim, const void* off, cons
     if (fwd)                                                                                     \
       hipLaunchKernelGGL((msda_prologue16_fwd_kernel<scalar_t, MM, PP>), dim3(blocks), dim3(256), 0, st, o, \
                          static_cast<const scalar_t*>(logits), rf, ref_dim, static_cast<float*>(loc), \
-                         static_cast<float*>(aw), pr.lv, n_items);                               \
+                         static_cast<float*>(aw), pr.lv, n_items, is);                           \
     else                                                                                         \
       hipLaunchKernelGGL((msda_prologue16_bwd_kernel<scalar_t, MM, PP>), dim3(blocks), dim3(256), 0, st, \
                          static_cast<const float*>(grad_loc), static_cast<const float*>(grad_aw), \
                          static_cast<const float*>(aw), o, rf, ref_dim, static_cast<scalar_t*>(grad_off), \
-                         static_cast<scalar_t*>(grad_logits), static_cast<float*>(grad_ref), pr.lv, n_items); \
+                         static_cast<scalar_t*>(grad_logits), static_cast<float*>(grad_ref), pr.lv, n_items, is); \
   } while (0)
 #define MSDA_P16(MM)                                                                               \
   do {                                                                                           \
@@ -3101,13 +3223,13 @@ int run_prologue(bool fwd, const Problem& pr, int ref_dim, const void* off, cons
       hipLaunchKernelGGL((msda_prologue_fwd_kernel<scalar_t, coord_t, PW>), dim3(blocks), dim3(threads), lds, \
                          st, o, static_cast<const scalar_t*>(logits), r, ref_dim, static_cast<coord_t*>(loc), \
                          static_cast<coord_t*>(aw), pr.lv, (int)pr.L, (int)pr.P, (int)pr.M, n_queries, G, \
-                         sQS, sLP, sP);                                                              \
+                         sQS, sLP, sP, is);                                                          \
     else                                                                                            \
       hipLaunchKernelGGL((msda_prologue_bwd_kernel<scalar_t, coord_t, PW>), dim3(blocks), dim3(threads), lds, \
                          st, static_cast<const coord_t*>(grad_loc), static_cast<const coord_t*>(grad_aw), \
                          static_cast<const coord_t*>(aw), o, r, ref_dim, static_cast<scalar_t*>(grad_off), \
                          static_cast<scalar_t*>(grad_logits), static_cast<coord_t*>(grad_ref), pr.lv,   \
-                         (int)pr.L, (int)pr.P, (int)pr.M, n_queries, G, sQS, sLP, sP);              \
+                         (int)pr.L, (int)pr.P, (int)pr.M, n_queries, G, sQS, sLP, sP, is);          \
   } while (0)
   if (pow2) MSDA_PRO(true);
   else MSDA_PRO(false);
@@ -3138,20 +3260,20 @@ int check_prologue(const int64_t* shapes, int64_t L, int64_t B, int64_t Lq, int6
 int dispatch_prologue(bool fwd, int dtype, const Problem& pr, int ref_dim, const void* off,
                       const void* logits, const void* ref, void* loc, void* aw, const void* grad_loc,
                       const void* grad_aw, void* grad_off, void* grad_logits, void* grad_ref,
-                      hipStream_t st) {
+                      long long is, hipStream_t st) {
   switch (dtype) {
     case MSDA_DTYPE_F32:
       return run_prologue<float, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw, grad_off,
-                                        grad_logits, grad_ref, st);
+                                        grad_logits, grad_ref, is, st);
     case MSDA_DTYPE_F64:
       return run_prologue<double, double>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
-                                          grad_off, grad_logits, grad_ref, st);
+                                          grad_off, grad_logits, grad_ref, is, st);
     case MSDA_DTYPE_BF16:
       return run_prologue<bf16_t, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
-                                         grad_off, grad_logits, grad_ref, st);
+                                         grad_off, grad_logits, grad_ref, is, st);
     case MSDA_DTYPE_F16:
       return run_prologue<f16_t, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
-                                        grad_off, grad_logits, grad_ref, st);
+                                        grad_off, grad_logits, grad_ref, is, st);
     default:
       set_error("msda prologue: unknown dtype %d", dtype);
       return MSDA_ERR_ARG;
@@ -3238,7 +3360,7 @@ hipError_t zero_f32(float* p, long long n, hipStream_t st) {
 
 extern "C" {
 
-int msda_hip_abi_version(void) { return 4; }
+int msda_hip_abi_version(void) { return 6; }
 
 const char* msda_hip_last_error(void) { return g_last_error; }
 
@@ -3278,33 +3400,52 @@ int msda_hip_dam_flat_grid(const void* sampling_loc, const void* attn_weight, co
   return launch_status("dam flat grid");
 }
 
-int msda_hip_prologue_forward(const void* sampling_offsets, const void* attn_logits, int dtype,
-                              const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
-                              int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,
-                              int64_t num_point, void* sampling_loc, void* attn_weight, void* stream) {
+int msda_hip_prologue_forward_ex(const void* sampling_offsets, const void* attn_logits, int dtype,
+                                 const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
+                                 int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,
+                                 int64_t num_point, int64_t in_stride, void* sampling_loc, void* attn_weight,
+                                 void* stream) {
   g_last_error[0] = 0;
   Problem pr;
   int rc = check_prologue(spatial_shapes, num_levels, batch, num_query, num_heads, num_point, ref_dim, &pr);
   if (rc) return rc;
+  if (in_stride < num_heads * num_levels * num_point) {
+    set_error("msda_hip_prologue_forward: in_stride %lld < num_heads * num_levels * num_point", (long long)in_stride);
+    return MSDA_ERR_ARG;
+  }
   if (batch * num_query > 0 && (sampling_offsets == nullptr || attn_logits == nullptr ||
                                 reference_points == nullptr || sampling_loc == nullptr || attn_weight == nullptr)) {
     set_error("msda_hip_prologue_forward: null pointer");
     return MSDA_ERR_ARG;
   }
   return dispatch_prologue(true, dtype, pr, ref_dim, sampling_offsets, attn_logits, reference_points,
-                           sampling_loc, attn_weight, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           sampling_loc, attn_weight, nullptr, nullptr, nullptr, nullptr, nullptr, in_stride,
                            static_cast<hipStream_t>(stream));
 }
 
-int msda_hip_prologue_backward(const void* grad_loc, const void* grad_attn, const void* attn_weight,
-                               const void* sampling_offsets, int dtype, const void* reference_points,
-                               int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
-                               int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
-                               void* grad_offsets, void* grad_logits, void* grad_ref, void* stream) {
+int msda_hip_prologue_forward(const void* sampling_offsets, const void* attn_logits, int dtype,
+                              const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
+                              int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,
+                              int64_t num_point, void* sampling_loc, void* attn_weight, void* stream) {
+  return msda_hip_prologue_forward_ex(sampling_offsets, attn_logits, dtype, reference_points, ref_dim, spatial_shapes,
+                                      num_levels, batch, num_query, num_heads, num_point,
+                                      num_heads * num_levels * num_point, sampling_loc, attn_weight, stream);
+}
+
+int msda_hip_prologue_backward_ex(const void* grad_loc, const void* grad_attn, const void* attn_weight,
+                                  const void* sampling_offsets, int dtype, const void* reference_points,
+                                  int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
+                                  int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
+                                  int64_t in_stride, void* grad_offsets, void* grad_logits, void* grad_ref,
+                                  void* stream) {
   g_last_error[0] = 0;
   Problem pr;
   int rc = check_prologue(spatial_shapes, num_levels, batch, num_query, num_heads, num_point, ref_dim, &pr);
   if (rc) return rc;
+  if (in_stride < num_heads * num_levels * num_point) {
+    set_error("msda_hip_prologue_backward: in_stride %lld < num_heads * num_levels * num_point", (long long)in_stride);
+    return MSDA_ERR_ARG;
+  }
   const bool need_loc_side = grad_offsets != nullptr || grad_ref != nullptr;
   if (batch * num_query > 0 &&
       ((need_loc_side && grad_loc == nullptr) || (grad_logits != nullptr && (grad_attn == nullptr || attn_weight == nullptr)) ||
@@ -3314,7 +3455,18 @@ int msda_hip_prologue_backward(const void* grad_loc, const void* grad_attn, cons
   }
   return dispatch_prologue(false, dtype, pr, ref_dim, sampling_offsets, nullptr, reference_points, nullptr,
                            const_cast<void*>(attn_weight), grad_loc, grad_attn, grad_offsets, grad_logits,
-                           grad_ref, static_cast<hipStream_t>(stream));
+                           grad_ref, in_stride, static_cast<hipStream_t>(stream));
+}
+
+int msda_hip_prologue_backward(const void* grad_loc, const void* grad_attn, const void* attn_weight,
+                               const void* sampling_offsets, int dtype, const void* reference_points,
+                               int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
+                               int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
+                               void* grad_offsets, void* grad_logits, void* grad_ref, void* stream) {
+  return msda_hip_prologue_backward_ex(grad_loc, grad_attn, attn_weight, sampling_offsets, dtype, reference_points,
+                                       ref_dim, spatial_shapes, num_levels, batch, num_query, num_heads, num_point,
+                                       num_heads * num_levels * num_point, grad_offsets, grad_logits, grad_ref,
+                                       stream);
 }
 
 size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t spatial_size,
@@ -3337,11 +3489,11 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
   return bwd_layout(value_dtype, batch, spatial_size, num_heads, num_query, num_levels, num_point).total;
 }
 
-int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_shapes,
-                     const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
-                     const void* attn_weight, void* output, int64_t batch, int64_t spatial_size,
-                     int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
-                     int padding_mode, void* stream) {
+static int forward_entry(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                         const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                         const void* attn_weight, void* output, void* tiles, int64_t batch, int64_t spatial_size,
+                         int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
+                         int padding_mode, void* stream) {
   g_last_error[0] = 0;
   Problem pr;
   int rc = check_problem(spatial_shapes, level_start, num_levels, batch, spatial_size, num_heads,
@@ -3362,6 +3514,14 @@ int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_
     return MSDA_ERR_ARG;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (tiles != nullptr) {
+    if (!forward_tiles_ok(pr, value_dtype)) {
+      set_error("msda_hip_forward_tiles: the call's backward does not take the row-block path "
+                "(msda_hip_forward_tiles_bytes is 0)");
+      return MSDA_ERR_ARG;
+    }
+    return run_forward<bf16_t, float, 8>(pr, value, sampling_loc, attn_weight, output, padding_mode, st, tiles);
+  }
   const int vec = pick_vec(value_dtype, pr.D);
   switch (value_dtype) {
     case MSDA_DTYPE_F32:
@@ -3382,12 +3542,52 @@ int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_
   }
 }
 
-int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial_shapes,
-                      const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
-                      const void* attn_weight, const void* grad_output, void* grad_value,
-                      void* grad_loc, void* grad_attn, void* workspace, int64_t batch,
-                      int64_t spatial_size, int64_t num_heads, int64_t channels,
-                      int64_t num_query, int64_t num_point, int padding_mode, void* stream) {
+int msda_hip_forward(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                     const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                     const void* attn_weight, void* output, int64_t batch, int64_t spatial_size,
+                     int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
+                     int padding_mode, void* stream) {
+  return forward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
+                       output, nullptr, batch, spatial_size, num_heads, channels, num_query, num_point,
+                       padding_mode, stream);
+}
+
+size_t msda_hip_forward_tiles_bytes(int value_dtype, const int64_t* spatial_shapes, int64_t num_levels,
+                                    int64_t batch, int64_t spatial_size, int64_t num_heads, int64_t channels,
+                                    int64_t num_query, int64_t num_point) {
+  if (spatial_shapes == nullptr || num_levels < 1 || num_levels > MSDA_MAX_LEVELS) return 0;
+  Problem pr{};
+  pr.B = batch; pr.S = spatial_size; pr.M = num_heads; pr.D = channels; pr.Lq = num_query;
+  pr.L = num_levels; pr.P = num_point;
+  for (int l = 0; l < num_levels; ++l) {
+    if (spatial_shapes[l] < 1 || spatial_shapes[l] > (1 << 24)) return 0;
+    pr.lv.T[l] = (int)spatial_shapes[l];
+  }
+  if (batch <= 0 || num_query <= 0 || !forward_tiles_ok(pr, value_dtype)) return 0;
+  return msda_win_workspace_bytes(batch, num_heads, num_levels, num_query);
+}
+
+int msda_hip_forward_tiles(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                           const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                           const void* attn_weight, void* output, void* tiles, int64_t batch, int64_t spatial_size,
+                           int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
+                           int padding_mode, void* stream) {
+  if (tiles == nullptr) {
+    g_last_error[0] = 0;
+    set_error("msda_hip_forward_tiles: null tiles");
+    return MSDA_ERR_ARG;
+  }
+  return forward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
+                       output, tiles, batch, spatial_size, num_heads, channels, num_query, num_point,
+                       padding_mode, stream);
+}
+
+static int backward_entry(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                          const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                          const void* attn_weight, const void* grad_output, void* grad_value,
+                          void* grad_loc, void* grad_attn, void* workspace, const void* tiles, int64_t batch,
+                          int64_t spatial_size, int64_t num_heads, int64_t channels,
+                          int64_t num_query, int64_t num_point, int padding_mode, void* stream) {
   g_last_error[0] = 0;
   Problem pr;
   int rc = check_problem(spatial_shapes, level_start, num_levels, batch, spatial_size, num_heads,
@@ -3431,8 +3631,15 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
   }
   const size_t need = msda_hip_backward_workspace_bytes(value_dtype, batch, spatial_size, num_heads,
                                                         channels, num_query, num_levels, num_point);
-  if (need > 0 && workspace == nullptr) {
+  // (the forward's tile intervals are all the row-block path needs)
+  const bool tiles_do = tiles != nullptr && forward_tiles_ok(pr, value_dtype);
+  if (need > 0 && workspace == nullptr &&
+      !(tiles_do && need == msda_win_workspace_bytes(batch, num_heads, num_levels, num_query))) {
     set_error("msda_hip_backward: workspace of %zu bytes required", need);
+    return MSDA_ERR_ARG;
+  }
+  if (tiles != nullptr && !tiles_do) {
+    set_error("msda_hip_backward_tiles: the call does not take the row-block path (no tiles forward)");
     return MSDA_ERR_ARG;
   }
   if (grad_value == nullptr && grad_loc == nullptr && grad_attn == nullptr) return MSDA_OK;
@@ -3446,11 +3653,38 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
                                           grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
     case MSDA_DTYPE_BF16:
       return run_backward<bf16_t, float>(pr, value, sampling_loc, attn_weight, grad_output, grad_value,
-                                         grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
+                                         grad_loc, grad_attn, workspace, value_dtype, padding_mode, st, tiles);
     default:
       return run_backward<f16_t, float>(pr, value, sampling_loc, attn_weight, grad_output, grad_value,
                                         grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
   }
+}
+
+int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                      const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                      const void* attn_weight, const void* grad_output, void* grad_value,
+                      void* grad_loc, void* grad_attn, void* workspace, int64_t batch,
+                      int64_t spatial_size, int64_t num_heads, int64_t channels,
+                      int64_t num_query, int64_t num_point, int padding_mode, void* stream) {
+  return backward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
+                        grad_output, grad_value, grad_loc, grad_attn, workspace, nullptr, batch, spatial_size,
+                        num_heads, channels, num_query, num_point, padding_mode, stream);
+}
+
+int msda_hip_backward_tiles(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                            const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                            const void* attn_weight, const void* grad_output, void* grad_value,
+                            void* grad_loc, void* grad_attn, void* workspace, const void* tiles, int64_t batch,
+                            int64_t spatial_size, int64_t num_heads, int64_t channels,
+                            int64_t num_query, int64_t num_point, int padding_mode, void* stream) {
+  if (tiles == nullptr) {
+    g_last_error[0] = 0;
+    set_error("msda_hip_backward_tiles: null tiles");
+    return MSDA_ERR_ARG;
+  }
+  return backward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
+                        grad_output, grad_value, grad_loc, grad_attn, workspace, tiles, batch, spatial_size,
+                        num_heads, channels, num_query, num_point, padding_mode, stream);
 }
 
 }  // extern "C"

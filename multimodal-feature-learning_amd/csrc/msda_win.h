@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 
+constexpr int kWinMaxChunks = 64;  // position chunks of the dispatch order
+constexpr int kWinMaxSeq = 512;    // row blocks of one (b, m) in the position-chunk order
+
 struct WinShape {
   long long B, S, M, Lq;
   int L, P;
@@ -11,7 +14,37 @@ struct WinShape {
   int blk0[17];  // first row block of each level (set by msda_win_backward)
   int nblk;      // row blocks over all levels (set by msda_win_backward)
   int ntile;     // query tiles (set by msda_win_backward)
+  // dispatch order (set by msda_win_backward; nchunk == 0: coarsest level first): position
+  // chunks c of every level, chunk c = level l's blocks [cs_l(c), cs_l(c+1)); the blocks of one
+  // (b, m) in chunk order are seq[cs[c] .. cs[c+1]) as (level << 12 | block)
+  int nchunk, ppx;
+  unsigned short cs[kWinMaxChunks + 1];
+  unsigned short seq[kWinMaxSeq];
 };
+
+constexpr int kWinQT = 32;          // queries per tile of the row-block backward
+constexpr int kWinNone = 1 << 29;   // an empty interval is (kWinNone, -kWinNone)
+
+// The rows [lo, hi] a sample at normalised location `loc` on a T-row level touches or owns in
+// the row-block backward: its taps base and base + 1 (base = floor of the sample position, as
+// msda_win.hip's make_taps computes it); a zero-padding sample with no tap on the map is owned
+// by row 0.  Shared by the backward's interval prepass and the forward that writes the same
+// intervals (msda.hip, msda_fwd16_tiles_kernel), so both see the same rows bit for bit.
+__device__ __forceinline__ int2 win_sample_rows(float loc, int T, bool zeros) {
+#pragma clang fp contract(off)
+  if (zeros) {
+    const float x = loc * (float)T - 0.5f;
+    if (!((x > -1.f) && (x < (float)T))) return make_int2(0, 0);
+    const int lo = (int)floorf(x);
+    return make_int2(lo < 0 ? 0 : lo, lo + 1);
+  }
+  const float g = loc * 2.f - 1.f;
+  const float y = fmaf(g + 1.f, (float)T * 0.5f, -0.5f);
+  const float ymax = (float)(T - 1);
+  const float yc = y > 0.f ? (y < ymax ? y : ymax) : 0.f;
+  const int base = (int)floorf(yc);
+  return make_int2(base, base + 1);
+}
 
 __attribute__((visibility("hidden"))) size_t msda_win_workspace_bytes(long long B, long long M, long long L,
                                                                      long long Lq);
@@ -19,5 +52,5 @@ __attribute__((visibility("hidden"))) int msda_win_supported(int value_dtype_is_
                                                                   long long row_floats);
 __attribute__((visibility("hidden"))) int msda_win_backward(const void* value, const void* loc, const void* aw,
                                                             const void* gout, void* gval, void* gloc, void* gaw,
-                                                            void* workspace, const WinShape* shape, int zeros,
-                                                            hipStream_t st);
+                                                            void* workspace, const void* tiles_ready,
+                                                            const WinShape* shape, int zeros, hipStream_t st);

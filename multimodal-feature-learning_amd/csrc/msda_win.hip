@@ -33,16 +33,17 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "msda_win.h"
 
 namespace {
 
-constexpr int kQT = 32;       // queries per tile
+constexpr int kQT = kWinQT;    // queries per tile
 constexpr int kThreads = 256;
 constexpr int kGS = 144;      // LDS row stride (bytes) of grad_out / value rows: 16-B aligned, spreads banks
 constexpr int kMaxSamp = 256;      // samples per tile (32 x P, P <= 8)
-constexpr int kNone = 1 << 29;     // base of an absent sample
+constexpr int kNone = kWinNone;    // an empty interval is (kNone, -kNone)
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
@@ -97,13 +98,6 @@ __device__ __forceinline__ Taps make_taps(float loc, int T) {
   return t;
 }
 
-// rows a sample writes or owns: [lo, hi] (base / base + 1 for a live sample; row 0 otherwise:
-// samples with no tap on the map are owned by the level's first block, which writes their zeros)
-template <bool ZEROS>
-__device__ __forceinline__ int2 sample_rows(const Taps& t) {
-  if (!t.live) return make_int2(0, 0);
-  return make_int2(t.base < 0 ? 0 : t.base, t.base + 1);
-}
 
 // The row interval every (b, m, level, query tile) touches or owns.  One 256-thread workgroup per
 // (b, tile): a query's coordinates of all heads and levels are one contiguous row of M * L * P
@@ -138,7 +132,7 @@ __global__ __launch_bounds__(kThreads) void win_tiles_kernel(const float* __rest
 #pragma unroll
     for (int u = 0; u < kQPW; ++u) {
       if (u < nq && i < n) {
-        const int2 r = sample_rows<ZEROS>(make_taps<ZEROS>(x[u][j], T));
+        const int2 r = win_sample_rows(x[u][j], T, ZEROS);  // msda_win.h: the rows make_taps gives
         lo = min(lo, r.x);
         hi = max(hi, r.y);
       }
@@ -182,44 +176,73 @@ constexpr int kDQS = kQT + 4;    // dots row stride (floats): [row - r0][q], row
 // wait on the global loads in flight).
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
 
-template <bool ZEROS, bool COORDS, int P>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void win_bwd_kernel(
+// W waves per row block (one workgroup of 64 W threads): the block's query-tile visits are dealt
+// round-robin over the waves (each with its own LDS), and the waves' grad_value partial sums are
+// added through LDS at the end — for calls with few row blocks (short pyramids: video queries on
+// the audio pyramid), where one wave per block leaves the chip mostly idle.
+template <bool ZEROS, bool COORDS, int P, int W>
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void win_bwd_kernel(
     const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     const uint16_t* __restrict__ gout, uint16_t* __restrict__ gval, float* __restrict__ gloc,
     float* __restrict__ gaw, const int2* __restrict__ tiles, const WinShape sh) {
   constexpr int NS = kQT * P;                  // samples per tile
   constexpr int SPL = NS >= 64 ? NS / 64 : 1;  // samples per lane
-  __shared__ __attribute__((aligned(16))) unsigned char s_g[kQT * kGS];     // grad_out rows of the tile
-  __shared__ __attribute__((aligned(16))) unsigned char s_v[kVRows * kGS];  // the block's value rows
+  __shared__ __attribute__((aligned(16))) unsigned char s_g_w[W][kQT * kGS];     // grad_out rows of the tile
+  __shared__ __attribute__((aligned(16))) unsigned char s_v_w[W][kVRows * kGS];  // the block's value rows
   // C of one MFMA step ([row][hi 32 | lo 32], step 2a), then the dots ([q][row - r0], 2b / 3): in
   // turn, in the wave's LDS order
   constexpr int kCBytes = kRW * kGS > kVRows * kDQS * 4 ? kRW * kGS : kVRows * kDQS * 4;
-  __shared__ __attribute__((aligned(16))) unsigned char s_c[kCBytes];
+  __shared__ __attribute__((aligned(16))) unsigned char s_c_w[W][kCBytes];
+  __shared__ int s_q_w[W][NS + kQT];  // query row (in the tile) of each compacted sample, padded
+  const int wid = W > 1 ? (int)(threadIdx.x >> 6) : 0;
+  unsigned char* const s_g = s_g_w[wid];
+  unsigned char* const s_v = s_v_w[wid];
+  unsigned char* const s_c = s_c_w[wid];
   float* const s_d = reinterpret_cast<float*>(s_c);
-  __shared__ int s_q[NS + kQT];  // query row (in the tile) of each compacted sample, padded
+  int* const s_q = s_q_w[wid];
 
-  const int lane = threadIdx.x, g = lane >> 4, li = lane & 15;
-  // dispatch order: the coarsest level's blocks first (a level-3 block meets ~12 query tiles, a
-  // level-0 block ~5: longest first shortens the tail), each level split into 8 contiguous chunks,
-  // chunk x on XCD x (block p runs on XCD p % 8), so neighbouring blocks share that XCD's L2
-  const unsigned x8 = blockIdx.x % 8u;
+  const int lane = (int)(threadIdx.x & 63), g = lane >> 4, li = lane & 15;
+  const unsigned x8 = blockIdx.x % 8u;  // block p runs on XCD p % 8 (round-robin dispatch)
   unsigned slot = blockIdx.x / 8u;
-  int l = sh.L - 1;
-  long long j = -1;
-  for (; l >= 0; --l) {
-    const long long nl = (long long)sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]);
-    const unsigned cl = (unsigned)((nl + 7) / 8);
-    if (slot < cl) {
-      j = (long long)x8 * cl + slot;
-      if (j >= nl) return;  // padding of the level's last chunk (wave-uniform, before any LDS use)
-      break;
+  int l = sh.L - 1, k;
+  unsigned bm;
+  if (sh.nchunk > 0) {
+    // position-chunk order: XCD x takes (b, m) pairs [x ppx, (x+1) ppx) and walks the level
+    // pyramid by position — chunk c of every level for each of its pairs, coarse level first,
+    // then chunk c + 1.  The blocks that write one query's coordinate gradients (its (m, level)
+    // pieces: 16 B each, one 64-B line per (q, m)) and read its loc / aw lines then run together
+    // on one XCD, so those lines are merged / reused in its L2 instead of written back and
+    // fetched once per level (row-block traffic: tools/pmc_win.sh)
+    int c = 0;
+    while (c + 1 < sh.nchunk && slot >= (unsigned)sh.ppx * sh.cs[c + 1]) ++c;
+    const unsigned nc = sh.cs[c + 1] - sh.cs[c];
+    const unsigned off = slot - (unsigned)sh.ppx * sh.cs[c];
+    const unsigned pair = x8 * (unsigned)sh.ppx + off / nc;
+    if (off / nc >= (unsigned)sh.ppx || pair >= (unsigned)(sh.B * sh.M)) return;  // grid padding (wave-uniform)
+    const unsigned e = sh.seq[sh.cs[c] + off % nc];
+    l = (int)(e >> 12);
+    k = (int)(e & 4095u);
+    bm = pair;
+  } else {
+    // the coarsest level's blocks first (a level-3 block meets ~12 query tiles, a level-0 block
+    // ~5: longest first shortens the tail), each level split into 8 contiguous chunks, chunk x
+    // on XCD x, so neighbouring blocks share that XCD's L2
+    long long j = -1;
+    for (; l >= 0; --l) {
+      const long long nl = (long long)sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]);
+      const unsigned cl = (unsigned)((nl + 7) / 8);
+      if (slot < cl) {
+        j = (long long)x8 * cl + slot;
+        if (j >= nl) return;  // padding of the level's last chunk (wave-uniform, before any LDS use)
+        break;
+      }
+      slot -= cl;
     }
-    slot -= cl;
+    if (l < 0) return;
+    const int nbl = sh.blk0[l + 1] - sh.blk0[l];
+    bm = (unsigned)(j / nbl);
+    k = (int)(j % nbl);
   }
-  if (l < 0) return;
-  const int nbl = sh.blk0[l + 1] - sh.blk0[l];
-  const unsigned bm = (unsigned)(j / nbl);
-  const int k = (int)(j % nbl);
   const int m = (int)(bm % (unsigned)sh.M);
   const long long b = bm / (unsigned)sh.M;
   const int T = sh.T[l], LP = sh.L * P;
@@ -255,7 +278,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
   };
   int cur_t0 = 0;
   unsigned long long mask = chunk_mask(0);
-  auto next_tile = [&]() -> int {  // pops the next visit (-1 when done)
+  auto pop_tile = [&]() -> int {  // pops the block's next visit (-1 when done)
     while (mask == 0ull) {
       cur_t0 += 64;
       if (cur_t0 >= sh.ntile) return -1;
@@ -264,6 +287,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
     const int t = cur_t0 + __builtin_ctzll(mask);
     mask &= mask - 1ull;
     return t;
+  };
+  bool first_pop = true;
+  auto next_tile = [&]() -> int {  // this wave's next visit: visits wid, wid + W, wid + 2W, ...
+    const int skip = first_pop ? wid : W - 1;
+    first_pop = false;
+    for (int i = 0; i < skip; ++i)
+      if (pop_tile() < 0) return -1;
+    return pop_tile();
   };
 
   f32x4 acc[4];
@@ -428,6 +459,24 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
 
   // grad_value rows r0 + 4g + j, channels 16 cb + li (every row of the block, zeros included)
   if (gval == nullptr) return;
+  if constexpr (W > 1) {  // the waves' partial sums through LDS (each wave's grad_out tile space)
+    __syncthreads();
+    float* red = reinterpret_cast<float*>(s_g);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) red[(4 * g + j) * 64 + cb * 16 + li] = acc[cb][j];
+    __syncthreads();
+    if (wid != 0) return;
+#pragma unroll
+    for (int v = 1; v < W; ++v) {
+      const float* o = reinterpret_cast<const float*>(s_g_w[v]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) acc[cb][j] += o[(4 * g + j) * 64 + cb * 16 + li];
+    }
+  }
   uint16_t* __restrict__ gvl = gval + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -452,8 +501,33 @@ int msda_win_supported(int value_dtype_is_bf16, long long D, long long P, long l
          row_floats <= 64 * kRowRegs;
 }
 
+// The position-chunk dispatch order of win_bwd_kernel: chunks of the level with the fewest
+// blocks (one of its blocks each), every level's blocks split evenly over them.  Returns false
+// (coarsest-level-first order) when the table does not fit WinShape.
+static bool win_chunk_order(WinShape& sh) {
+  sh.nchunk = 0;
+  int C = 1 << 30;
+  for (int l = 0; l < sh.L; ++l) C = min(C, sh.blk0[l + 1] - sh.blk0[l]);
+  if (C < 1 || C > kWinMaxChunks || sh.nblk > kWinMaxSeq) return false;
+  int n = 0;
+  for (int c = 0; c < C; ++c) {
+    sh.cs[c] = (unsigned short)n;
+    for (int l = sh.L - 1; l >= 0; --l) {
+      const int nb = sh.blk0[l + 1] - sh.blk0[l];
+      if (nb > 4096) return false;
+      for (int k = (int)((long long)c * nb / C); k < (int)((long long)(c + 1) * nb / C); ++k)
+        sh.seq[n++] = (unsigned short)(l << 12 | k);
+    }
+  }
+  sh.cs[C] = (unsigned short)n;
+  sh.nchunk = C;
+  sh.ppx = (int)((sh.B * sh.M + 7) / 8);
+  return n == sh.nblk;
+}
+
 int msda_win_backward(const void* value, const void* loc, const void* aw, const void* gout, void* gval,
-                      void* gloc, void* gaw, void* workspace, const WinShape* shape, int zeros, hipStream_t st) {
+                      void* gloc, void* gaw, void* workspace, const void* tiles_ready, const WinShape* shape,
+                      int zeros, hipStream_t st) {
   WinShape sh = *shape;
   sh.ntile = (int)((sh.Lq + kQT - 1) / kQT);
   int nb = 0;
@@ -464,8 +538,11 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   sh.blk0[sh.L] = nb;
   sh.nblk = nb;
   if (sh.B * sh.M == 0 || nb == 0) return 0;
-  auto* tiles = static_cast<int2*>(workspace);
-  const unsigned tile_wgs = (unsigned)(sh.B * sh.ntile);
+  const bool chunked = win_chunk_order(sh) && !(getenv("MSDA_HIP_WIN_ORDER") && atoi(getenv("MSDA_HIP_WIN_ORDER")) == 0);
+  if (!chunked) sh.nchunk = 0;
+  // tile intervals: written by the forward (msda_fwd16_tiles_kernel) or by the prepass below
+  auto* tiles = static_cast<int2*>(tiles_ready != nullptr ? const_cast<void*>(tiles_ready) : workspace);
+  const unsigned tile_wgs = tiles_ready != nullptr ? 0u : (unsigned)(sh.B * sh.ntile);
   const int nj = (int)((sh.M * sh.L * sh.P + 63) / 64);
   auto* lc0 = static_cast<const float*>(loc);
 #define WIN_TILES(Z, NJ) hipLaunchKernelGGL((win_tiles_kernel<Z, NJ>), dim3(tile_wgs), dim3(kThreads), 0, st, lc0, tiles, sh)
@@ -481,8 +558,11 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   }
 #undef WIN_TILES_NJ
 #undef WIN_TILES
-  unsigned grid = 0;  // 8 x per-level chunks (see win_bwd_kernel's dispatch order)
-  for (int l = 0; l < sh.L; ++l) grid += 8u * (unsigned)((sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + 7) / 8);
+  unsigned grid = 0;  // 8 x per-XCD slots (see win_bwd_kernel's dispatch order)
+  if (sh.nchunk > 0)
+    grid = 8u * (unsigned)sh.ppx * (unsigned)sh.nblk;
+  else
+    for (int l = 0; l < sh.L; ++l) grid += 8u * (unsigned)((sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + 7) / 8);
   const bool coords = gloc != nullptr || gaw != nullptr;
   auto* v = static_cast<const uint16_t*>(value);
   auto* lc = static_cast<const float*>(loc);
@@ -491,8 +571,22 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   auto* gv = static_cast<uint16_t*>(gval);
   auto* gl = static_cast<float*>(gloc);
   auto* ga = static_cast<float*>(gaw);
-#define WIN_LAUNCH(Z, C, N) \
-  hipLaunchKernelGGL((win_bwd_kernel<Z, C, N>), dim3(grid), dim3(64), 0, st, v, lc, a, g, gv, gl, ga, tiles, sh)
+  // waves per row block: enough waves for the chip when the blocks are few (MSDA_HIP_WIN_SPLIT
+  // forces 1 / 4 / 8)
+  const long long nblocks = sh.B * sh.M * (long long)sh.nblk;
+  int W = nblocks <= 1024 ? 8 : nblocks <= 4096 ? 4 : 1;
+  if (const char* e = getenv("MSDA_HIP_WIN_SPLIT")) {
+    const int f = atoi(e);
+    if (f == 1 || f == 4 || f == 8) W = f;
+  }
+#define WIN_LAUNCH_W(Z, C, N, WW) \
+  hipLaunchKernelGGL((win_bwd_kernel<Z, C, N, WW>), dim3(grid), dim3(64 * WW), 0, st, v, lc, a, g, gv, gl, ga, tiles, sh)
+#define WIN_LAUNCH(Z, C, N)                                             \
+  do {                                                                  \
+    if (W == 8) WIN_LAUNCH_W(Z, C, N, 8);                               \
+    else if (W == 4) WIN_LAUNCH_W(Z, C, N, 4);                          \
+    else WIN_LAUNCH_W(Z, C, N, 1);                                      \
+  } while (0)
 #define WIN_SPL(Z, C)                                                   \
   do {                                                                  \
     switch (sh.P) {                                                     \
@@ -509,5 +603,6 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   }
 #undef WIN_SPL
 #undef WIN_LAUNCH
+#undef WIN_LAUNCH_W
   return 0;  // launch errors: the caller's hipGetLastError
 }

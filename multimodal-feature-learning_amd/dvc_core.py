@@ -24,7 +24,7 @@ from .utils.dam import attn_map_to_flat_grid
 from .models.modules.linear import Linear
 
 __all__ = ["DeformableDVCCore", "MultimodalDVCCore", "SparseDVCCore", "synthetic_clips", "workload_loss",
-           "multimodal_workload_loss", "sparse_workload_loss"]
+           "multimodal_workload_loss", "sparse_workload_loss", "StagedDVCLoss"]
 
 
 class DeformableDVCCore(nn.Module):
@@ -330,3 +330,83 @@ def dvc_workload_loss(result, obj):
         total = total + 3 * F.binary_cross_entropy_with_logits(out['pred_memory_mask'].float(),
                                                               (out['pred_memory_mask'].detach() > 0).float())
     return total
+
+
+class StagedDVCLoss:
+    """``dvc_workload_loss`` over ``UnimodalDeformableDVC``'s training forward, split around its
+    host step (the Hungarian assignment, reference engine.py:62 -> models/matcher.py:86) so that
+    ``FlatGradTrainer`` captures the step as two HIP graphs (train_step.py, staged losses):
+
+    * ``stage_a``: the proposals and every decoder level's matching costs (device);
+    * ``host``: scipy's assignment of the copied costs and the matched (batch, prediction) index
+      pairs of each level, written into pinned buffers; ``upload`` copies them (stream-ordered)
+      into static device buffers;
+    * ``stage_b``: the crop, context mask and caption decoder of every level from those buffers,
+      and the loss — with the batch's targets kept as device constants, so nothing in it reads
+      the host.
+
+    The number of matches is the batch's number of target segments (one per target), so every
+    shape is fixed by the batch: a replay only changes which predictions are matched."""
+
+    def __init__(self, obj, model):
+        dev = obj['video_tensor'].device
+        num_levels = len(model.class_embedding)
+        self._matcher = model.matcher
+        self.obj = obj
+        tgts = obj['video_target']
+        self.tgt_seg = torch.cat([t['segments'] for t in tgts]).float()
+        self.words = obj['cap_tensor'][:, 1:]
+        self.live = (~obj['cap_mask'][:, 1:]).float()
+        self.live_sum = self.live.sum()
+        self.n_events = torch.tensor([len(t['segments']) for t in tgts], device=dev)
+        n = int(self.tgt_seg.shape[0])
+        self.idx_host = torch.empty((num_levels, 2, n), dtype=torch.int64)
+        if dev.type == "cuda":
+            self.idx_host = self.idx_host.pin_memory()
+        self.idx_dev = torch.zeros((num_levels, 2, n), dtype=torch.int64, device=dev)
+        self.level_indices = None
+
+    # --- the staged-loss protocol of FlatGradTrainer ---------------------------------------
+    def stage_a(self, model, batch):
+        return model.forward_stage_proposals(batch[0])
+
+    @staticmethod
+    def request(state):
+        return state['costs']
+
+    def host(self, state, cpu):
+        from .utils.preds_postprocess import get_src_permutation_idx
+        self.level_indices = self._matcher.solve_levels(cpu, state['cost_meta'])
+        for lvl, ind in enumerate(self.level_indices):
+            b, s = get_src_permutation_idx(ind)
+            self.idx_host[lvl, 0].copy_(b)
+            self.idx_host[lvl, 1].copy_(s)
+
+    def upload(self):
+        self.idx_dev.copy_(self.idx_host, non_blocking=True)
+
+    def stage_b(self, model, batch, state):
+        levels = [(self.idx_dev[l, 0], self.idx_dev[l, 1]) for l in range(self.idx_dev.shape[0])]
+        result = model.forward_stage_captions(batch[0], state, self.level_indices, levels, is_training=True)
+        return self.loss(result, levels)
+
+    def loss(self, result, levels):
+        """``dvc_workload_loss`` with the matched indices from ``levels`` (device) and the targets
+        as device constants: the same terms in the same order."""
+        import torch.nn.functional as F
+        out = result[0]
+        total = 0.0
+        outs = [out] + list(out.get('aux_outputs', []))
+        lv = [levels[-1]] + levels[:len(outs) - 1]
+        for o, (bidx, sidx) in zip(outs, lv):
+            total = total + 5 * (o['pred_segments'][bidx, sidx].float() - self.tgt_seg).abs().mean()
+            total = total - torch.log(o['pred_logits'][bidx, sidx, 0].float().clamp_min(1e-9)).mean()
+            total = total + 2 * F.cross_entropy(o['pred_count'].float(),
+                                                self.n_events.clamp_max(o['pred_count'].shape[-1] - 1))
+            if o.get('pred_captions') is not None:
+                p = o['pred_captions'].float().gather(-1, self.words[..., None])[..., 0]
+                total = total - (torch.log(p.clamp_min(1e-9)) * self.live).sum() / self.live_sum
+        if 'pred_memory_mask' in out:
+            total = total + 3 * F.binary_cross_entropy_with_logits(out['pred_memory_mask'].float(),
+                                                                  (out['pred_memory_mask'].detach() > 0).float())
+        return total

@@ -102,6 +102,15 @@ class UnimodalDeformableDVC(nn.Module):
         return out, query_features, memory, heads
 
     def forward(self, obj, is_training=True, faster_eval=False):
+        st = self.forward_stage_proposals(obj)
+        # every level's matching in one device->host copy (reference: one .cpu() per level, :227)
+        level_indices = self.matcher.solve_levels(st['costs'].cpu(), st['cost_meta'])
+        return self.forward_stage_captions(obj, st, level_indices, None, is_training, faster_eval)
+
+    def forward_stage_proposals(self, obj):
+        """The device work before the Hungarian matching: proposals and every level's cost
+        matrix (``HungarianMatcher.level_costs``).  A graph-captured training step replays this
+        stage, copies ``costs`` to the host for the assignment, then replays the caption stage."""
         video = obj['video_tensor']
         video_mask = obj['video_mask']
         durations = obj['video_length'][:, 1]
@@ -110,16 +119,29 @@ class UnimodalDeformableDVC(nn.Module):
         num_pred = query_features.shape[0]
         out_aux = [{'pred_logits': outputs_class[l], 'pred_segments': outputs_segment[l],
                     'pred_count': outputs_count[l]} for l in range(num_pred)]
-        # every level's matching in one device->host copy (reference: one .cpu() per level, :227)
-        level_indices = self.matcher.match_levels(out_aux, obj['video_target'])
-        video_durations = durations
+        costs, meta = self.matcher.level_costs(out_aux, obj['video_target'])
+        return {'out': out, 'query_features': query_features, 'memory': memory, 'durations': durations,
+                'heads': (outputs_class, outputs_segment, outputs_count), 'out_aux': out_aux, 'costs': costs,
+                'cost_meta': meta}
+
+    def forward_stage_captions(self, obj, st, level_indices, level_idx_dev=None, is_training=True,
+                               faster_eval=False):
+        """Everything after the matching (reference :227-372).  ``level_idx_dev``: per decoder level
+        the (batch, prediction) indices of the matched segments already on the device (static
+        buffers of a captured step), else derived from ``level_indices``."""
+        out, query_features, memory = st['out'], st['query_features'], st['memory']
+        outputs_class, outputs_segment, outputs_count = st['heads']
+        out_aux = st['out_aux']
+        num_pred = query_features.shape[0]
+        video_durations = st['durations']
+        indices = level_indices[-1]
 
         outputs_captions, memory_list, memory_mask_list, pred_memory_mask_list = [], [], [], []
         for lvl in range(num_pred):
-            indices = level_indices[lvl]
             # as the reference (:235): ``memory`` is rebound to this level's crop, which the next level crops
-            idx, idx_dev, denorm, memory, key_mask = segment_memory(memory, out_aux[lvl], indices, video_durations,
-                                                                    self.num_feature_levels, self.video_rescale_len)
+            idx, idx_dev, denorm, memory, key_mask = segment_memory(
+                memory, out_aux[lvl], level_indices[lvl], video_durations, self.num_feature_levels,
+                self.video_rescale_len, idx_dev=None if level_idx_dev is None else level_idx_dev[lvl])
             mem = memory
             memory_mask = key_mask.unsqueeze(1).unsqueeze(1)  # (n, 1, 1, K)
             pred_memory_mask = None
@@ -136,8 +158,9 @@ class UnimodalDeformableDVC(nn.Module):
                 padding_mask = obj['cap_mask'][:, :-1]
                 tgt_mask = make_tgt_mask(captions, padding_mask)
                 cross_mask = pred_memory_mask if self.use_differentiable_mask else memory_mask
+                # only the last caption layer's word probabilities are read (:281): the head runs on it alone
                 output_caption = self.unimodal_caption_decoder(captions, mem, tgt_mask=tgt_mask, memory_mask=cross_mask,
-                                                               tgt_padding_mask=padding_mask)
+                                                               tgt_padding_mask=padding_mask, last_only=True)
                 outputs_captions.append(output_caption[-1])
 
         mask_out = memory_mask_list[-1].squeeze().float() if self.use_differentiable_mask else None

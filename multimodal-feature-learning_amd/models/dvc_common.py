@@ -30,12 +30,17 @@ def make_padding_mask(target, vocab):
     return target == vocab['<pad>']
 
 
-def segment_memory(memory, out_aux, indices, video_durations, num_feature_levels, rescale_len):
-    """Matched segments of one decoder level -> (idx, denormalised (n, 2), cropped memory (n, K, d),
-    key mask (n, K)) (reference unimodal_deformable_dvc.py:229-240, 434-493)."""
-    idx = get_src_permutation_idx(indices)
-    dev = out_aux['pred_segments'].device
-    idx_dev = (idx[0].to(dev), idx[1].to(dev))
+def segment_memory(memory, out_aux, indices, video_durations, num_feature_levels, rescale_len, idx_dev=None):
+    """Matched segments of one decoder level -> (idx, idx on the device, denormalised (n, 2),
+    cropped memory (n, K, d), key mask (n, K)) (reference unimodal_deformable_dvc.py:229-240,
+    434-493).  ``idx_dev``: the level's (batch, prediction) index pair already on the device (a
+    graph-captured step uploads it from the host matching; ``idx`` is then ``indices``)."""
+    if idx_dev is not None:
+        idx = indices
+    else:
+        idx = get_src_permutation_idx(indices)
+        dev = out_aux['pred_segments'].device
+        idx_dev = (idx[0].to(dev), idx[1].to(dev))
     denorm = denormalize_segments(out_aux['pred_segments'][idx_dev], video_durations, idx_dev[0])
     mem, key_mask = crop_segments(memory, denorm, idx_dev[0], video_durations, num_feature_levels, rescale_len)
     return idx, idx_dev, denorm, mem, key_mask

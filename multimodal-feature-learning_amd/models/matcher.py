@@ -33,6 +33,14 @@ class HungarianMatcher(nn.Module):
     @torch.no_grad()
     def match_levels(self, outputs_list, targets):
         """``forward`` for several outputs (decoder levels) against the same targets."""
+        costs, meta = self.level_costs(outputs_list, targets)
+        return self.solve_levels(costs.cpu(), meta)  # the one device->host copy
+
+    @torch.no_grad()
+    def level_costs(self, outputs_list, targets):
+        """The device half of ``match_levels``: every level's cost matrix and the well-formedness
+        flags packed in one fp64 device tensor (a graph-captured step copies it to the host),
+        plus the host metadata ``solve_levels`` needs."""
         tgt_segments = torch.cat([v["segments"] for v in targets])
         tgt_xy = segment_cl_to_xy(tgt_segments)
         sizes = [len(v["segments"]) for v in targets]
@@ -48,13 +56,19 @@ class HungarianMatcher(nn.Module):
             flags.append((out_xy[:, 1] >= out_xy[:, 0]).all().reshape(1))
             shapes.append((B, Q))
         flags.append((tgt_xy[:, 1] >= tgt_xy[:, 0]).all().reshape(1))
-        host = torch.cat(costs + [torch.cat(flags).double()]).cpu()  # the one device->host copy
-        ok = host[-len(flags):]
+        return torch.cat(costs + [torch.cat(flags).double()]), (shapes, sizes, len(tgt_segments), len(flags))
+
+    @staticmethod
+    def solve_levels(host, meta):
+        """The host half: the reference's syncing asserts (utils/box_ops.py:59-60) and scipy's
+        linear_sum_assignment per clip and level (reference :86-94)."""
+        shapes, sizes, n_tgt, n_flags = meta
+        ok = host[-n_flags:]
         assert bool(ok[:-1].all()), "Segment start > Segment end (from output)"
         assert bool(ok[-1]), "Segment start > Segment end (from target)"
         result, off = [], 0
         for B, Q in shapes:
-            n = B * Q * len(tgt_segments)
+            n = B * Q * n_tgt
             cost = host[off:off + n].view(B, Q, -1)
             off += n
             result.append([

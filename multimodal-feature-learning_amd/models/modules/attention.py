@@ -22,6 +22,7 @@ import warnings
 import torch
 import torch.nn.functional as F
 from torch import nn
+from torch.autograd.function import once_differentiable
 from torch.nn.init import constant_, xavier_uniform_
 
 from ... import msda as _msda
@@ -66,6 +67,62 @@ def _is_power_of_2(n):
     return (n & (n - 1) == 0) and n != 0
 
 
+def _rows_view(a, b):
+    """[a; b] (rows of a, then rows of b) as a view when b's storage follows a's (the trainer lays
+    paired parameters out that way, ``MSDeformAttn.flat_groups``), else a copy."""
+    if (a.is_contiguous() and b.is_contiguous() and a.dtype == b.dtype and a.shape[1:] == b.shape[1:]
+            and a.untyped_storage().data_ptr() == b.untyped_storage().data_ptr()
+            and b.storage_offset() == a.storage_offset() + a.numel()):
+        return a.new_empty(0).set_(a.untyped_storage(), a.storage_offset(), (a.shape[0] + b.shape[0],) + a.shape[1:])
+    return torch.cat((a, b), 0)
+
+
+class _QueryPrologue(torch.autograd.Function):
+    """``sampling_offsets`` and ``attention_weights`` of MSDeformAttn (attention.py:468-470) as ONE
+    GEMM into rows of [offsets | logits], and the prologue (softmax + locations, :471-483) reading
+    those rows in place (``msda_hip_prologue_forward_ex``).  Backward: the prologue backward writes
+    both gradients into one buffer of the same rows, which is the input of ONE dgrad GEMM against
+    [W_off; W_aw] and of the weight-gradient product (queued with the short-K layers' when the
+    query rows are few).  Against the two-projection form (linear_pair + MSDAPrologueFunction): one
+    GEMM instead of two each way and no concatenation of the two gradients.  The arithmetic is the
+    same: each output column is its own dot product over the input, in the GEMM's dtype."""
+
+    @staticmethod
+    def forward(ctx, x, wa, ba, wb, bb, wca, bca, wcb, bcb, ref, shapes, dims):
+        from ... import _trace
+        _trace.hit("query_prologue")
+        B, Lq, M, L, P = dims
+        wc, bc = _rows_view(wca, wcb), _rows_view(bca, bcb)
+        x2 = x.reshape(-1, x.shape[-1])
+        y = torch.addmm(bc, x2, wc.t())
+        loc, aw = _msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes)
+        ctx.save_for_backward(x2, wc, y, aw, ref)
+        ctx.shapes, ctx.x_shape = shapes, x.shape
+        ctx.params = (wa, ba, wb, bb)
+        return loc, aw
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_loc, grad_aw):
+        x2, wc, y, aw, ref = ctx.saved_tensors
+        nig = ctx.needs_input_grad
+        g2, g_ref = _msda.prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, ctx.shapes, need_ref=nig[9])
+        gx = torch.mm(g2, wc).view(ctx.x_shape) if nig[0] else None
+        wa, ba, wb, bb = ctx.params
+        na = wa.shape[0]
+        rest = (None, None, None, None, g_ref, None, None)
+        if all(nig[1:5]) and _defer((g2[:, :na], x2, wa, 0, ba), (g2[:, na:], x2, wb, 0, bb)):
+            return (gx, None, None, None, None) + rest
+        gwa = gwb = gba = gbb = None
+        if nig[1] or nig[3]:
+            gw = _weight_grad(g2, x2)
+            gwa, gwb = gw[:na], gw[na:]
+        if nig[2] or nig[4]:
+            gbias = _bias_grad(g2)
+            gba, gbb = gbias[:na], gbias[na:]
+        return (gx, gwa, gba, gwb, gbb) + rest
+
+
 class MSDeformAttn(nn.Module):
     """Multi-scale temporal deformable attention, reference attention.py:394-511.
 
@@ -93,6 +150,12 @@ class MSDeformAttn(nn.Module):
         self.value_proj = Linear(d_model, d_model)
         self.output_proj = Linear(d_model, d_model)
         self._reset_parameters()
+
+    def flat_groups(self):
+        """Parameters a flat-buffer trainer should lay out back to back (train_step.py): the two
+        query projections' weights and biases, so that [W_off; W_aw] is a view (_QueryPrologue)."""
+        return [(self.sampling_offsets.weight, self.attention_weights.weight),
+                (self.sampling_offsets.bias, self.attention_weights.bias)]
 
     def _reset_parameters(self):
         constant_(self.sampling_offsets.weight.data, 0.)
@@ -135,6 +198,28 @@ class MSDeformAttn(nn.Module):
             if input_padding_mask is not None:
                 value = mask_padding_rows(value, input_padding_mask)
         value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
+
+        a, b = self.sampling_offsets, self.attention_weights
+        dt = a._autocast_dtype(query) if isinstance(a, Linear) else None
+        if (dt == torch.bfloat16 and isinstance(b, Linear) and a.bias is not None and b.bias is not None
+                and reference_points.shape[-1] in (1, 2)
+                and _msda.prologue_supported(self.n_heads, self.n_levels, self.n_points)):
+            # both query projections as one GEMM read in place by the prologue kernel, one
+            # backward GEMM each way (_QueryPrologue)
+            wca, bca = a._low(dt)
+            wcb, bcb = b._low(dt)
+            if wca is None or wcb is None:
+                wca, bca, wcb, bcb = a.weight.to(dt), a.bias.to(dt), b.weight.to(dt), b.bias.to(dt)
+            with torch.autocast("cuda", enabled=False):
+                sampling_locations, attention_weights = _QueryPrologue.apply(
+                    query.to(dt), a.weight, a.bias, b.weight, b.bias, wca, bca, wcb, bcb,
+                    reference_points.float().contiguous(), tuple(int(t) for t in shapes),
+                    (N, Len_q, self.n_heads, self.n_levels, self.n_points))
+            output = ms_deform_attn_core_pytorch(value, shapes, sampling_locations, attention_weights)
+            output = self.output_proj(output)
+            if is_sparse:
+                return output, sampling_locations.unsqueeze(-1), attention_weights
+            return output
 
         # one input cast and one fused backward for the two query projections
         sampling_offsets, attention_weights = linear_pair(query, self.sampling_offsets, self.attention_weights)

@@ -75,14 +75,17 @@ class UnimodalCaptionDecoder(nn.Module):
         self.head = Linear(d_model, vocab_size)
         self.init_weights(embedding_matrix, emb_weights_req_grad)
 
-    def forward(self, tgt, memory, tgt_mask=None, memory_mask=None, tgt_padding_mask=None, memory_padding_mask=None):
+    def forward(self, tgt, memory, tgt_mask=None, memory_mask=None, tgt_padding_mask=None, memory_padding_mask=None,
+                last_only=False):
+        """``last_only``: the head and softmax on the last layer only, (1, N, L, vocab) — the row
+        ``[-1]`` of the full result, for callers that read nothing else (the DVC training forward)."""
         tgt = self.positional_encoding(self.target_embedding(tgt))
         intermediate = []
         for layer in self.decoder:
             tgt = layer(tgt, memory, tgt_mask, memory_mask, tgt_padding_mask, memory_padding_mask)
-            if self.return_intermediate:
+            if self.return_intermediate and not last_only:
                 intermediate.append(tgt)
-        tgt = torch.stack(intermediate) if self.return_intermediate else tgt.unsqueeze(0)
+        tgt = torch.stack(intermediate) if self.return_intermediate and not last_only else tgt.unsqueeze(0)
         return self.head(tgt).softmax(dim=-1)
 
     def init_weights(self, embedding_matrix, emb_weights_req_grad):

@@ -170,31 +170,44 @@ def _check_inputs(value, loc, aw, shapes, starts):
         raise ValueError(f"levels {shapes} starting at {starts} exceed spatial size {S}")
 
 
-def msda_forward(value, shapes, starts, loc, aw, padding_mode="border"):
-    """out (B, Lq, M*D) = MSDA(value (B,S,M,D), loc/aw (B,Lq,M,L,P)) on the HIP kernel."""
+def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_tiles=False):
+    """out (B, Lq, M*D) = MSDA(value (B,S,M,D), loc/aw (B,Lq,M,L,P)) on the HIP kernel.
+
+    ``want_tiles``: also return the backward's row intervals when the call's backward takes the
+    row-block path (``msda_hip_forward_tiles``; None otherwise): ``(out, tiles)``."""
     _check_inputs(value, loc, aw, shapes, starts)
     lib = _native.load_library()
     B, S, M, D = value.shape
     Lq, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
     out = torch.empty((B, Lq, M * D), dtype=value.dtype, device=value.device)
+    tiles = None
+    if want_tiles:
+        nb = lib.msda_hip_forward_tiles_bytes(_native.DTYPE_TAGS[value.dtype], _native.host_i64_array(shapes), L,
+                                              B, S, M, D, Lq, P)
+        if nb:
+            tiles = torch.empty(nb, dtype=torch.uint8, device=value.device)
     timer = _timer
     if timer is not None:
         ev0 = timer._begin()
-    rc = lib.msda_hip_forward(
-        value.data_ptr(), _native.DTYPE_TAGS[value.dtype],
-        _native.host_i64_array(shapes), _native.host_i64_array(starts), L,
-        loc.data_ptr(), aw.data_ptr(), out.data_ptr(),
-        B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
+    args = (value.data_ptr(), _native.DTYPE_TAGS[value.dtype],
+            _native.host_i64_array(shapes), _native.host_i64_array(starts), L,
+            loc.data_ptr(), aw.data_ptr(), out.data_ptr())
+    tail = (B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
+    if tiles is None:
+        rc = lib.msda_hip_forward(*args, *tail)
+    else:
+        rc = lib.msda_hip_forward_tiles(*args, tiles.data_ptr(), *tail)
     _native.check(rc, "msda_hip_forward")
     if timer is not None:
         timer._end("fwd", (S, Lq), algorithmic_bytes("fwd", B, S, M, D, Lq, L, P, value.element_size()), ev0,
                    gathered_bytes(B, M, D, Lq, L, P, value.element_size()))
-    return out
+    return (out, tiles) if want_tiles else out
 
 
 def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="border",
-                  need_value=True, need_loc=True, need_aw=True):
-    """(grad_value, grad_loc, grad_aw) of msda_forward; unneeded ones come back None."""
+                  need_value=True, need_loc=True, need_aw=True, tiles=None):
+    """(grad_value, grad_loc, grad_aw) of msda_forward; unneeded ones come back None.
+    ``tiles``: the row intervals ``msda_forward(..., want_tiles=True)`` returned for these inputs."""
     _check_inputs(value, loc, aw, shapes, starts)
     grad_output = grad_output.to(value.dtype).contiguous()
     B, S, M, D = value.shape
@@ -207,18 +220,23 @@ def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="bor
     ga = torch.empty_like(aw) if need_aw else None
     ws = None
     nbytes = lib.msda_hip_backward_workspace_bytes(_native.DTYPE_TAGS[value.dtype], B, S, M, D, Lq, L, P)
-    if nbytes:  # through the caching allocator: no hipMalloc on the hot path, graph-capturable
+    if nbytes and (tiles is None or nbytes != tiles.numel()):
+        # through the caching allocator: no hipMalloc on the hot path, graph-capturable (the
+        # row-block path needs nothing beyond the forward's tiles)
         ws = torch.empty(nbytes, dtype=torch.uint8, device=value.device)
     ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
     timer = _timer
     if timer is not None:
         ev0 = timer._begin()
-    rc = lib.msda_hip_backward(
-        value.data_ptr(), _native.DTYPE_TAGS[value.dtype],
-        _native.host_i64_array(shapes), _native.host_i64_array(starts), L,
-        loc.data_ptr(), aw.data_ptr(), grad_output.data_ptr(),
-        ptr(gv), ptr(gl), ptr(ga), ptr(ws),
-        B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
+    args = (value.data_ptr(), _native.DTYPE_TAGS[value.dtype],
+            _native.host_i64_array(shapes), _native.host_i64_array(starts), L,
+            loc.data_ptr(), aw.data_ptr(), grad_output.data_ptr(),
+            ptr(gv), ptr(gl), ptr(ga), ptr(ws))
+    tail = (B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
+    if tiles is None:
+        rc = lib.msda_hip_backward(*args, *tail)
+    else:
+        rc = lib.msda_hip_backward_tiles(*args, tiles.data_ptr(), *tail)
     _native.check(rc, "msda_hip_backward")
     if timer is not None:
         timer._end("bwd", (S, Lq), algorithmic_bytes("bwd", B, S, M, D, Lq, L, P, value.element_size()), ev0,
@@ -237,7 +255,10 @@ class MSDAFunction(Function):
         _trace.hit("msda_" + str(value.dtype).replace("torch.", ""))
         ctx.meta = (shapes, starts, padding_mode)
         ctx.save_for_backward(value, loc, aw)
-        return msda_forward(value, shapes, starts, loc, aw, padding_mode)
+        # the row intervals of the row-block backward come with the forward (it reads loc anyway)
+        out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode,
+                                      want_tiles=any(ctx.needs_input_grad[:3]))
+        return out
 
     @staticmethod
     @once_differentiable
@@ -246,7 +267,8 @@ class MSDAFunction(Function):
         shapes, starts, padding_mode = ctx.meta
         nv, nl, na = ctx.needs_input_grad[:3]
         gv, gl, ga = msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode,
-                                   need_value=nv, need_loc=nl, need_aw=na)
+                                   need_value=nv, need_loc=nl, need_aw=na, tiles=ctx.tiles)
+        ctx.tiles = None
         if gv is not None:
             gv._mfl_private = True  # fresh, referenced by nothing else: consumers may write it in place
         return gv, gl, ga, None, None, None
@@ -324,6 +346,48 @@ def prologue_backward(grad_loc, grad_aw, aw, offsets, ref, shapes, need_off=True
         B, Lq, M, P, ptr(g_off), ptr(g_log), ptr(g_ref), _native.stream_handle(offsets.device))
     _native.check(rc, "msda_hip_prologue_backward")
     return g_off, g_log, g_ref
+
+
+def prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes):
+    """``prologue_forward`` on the output of ONE query-projection GEMM: y (B*Lq, 2*M*L*P), each
+    row [sampling offsets | attention logits] (``msda_hip_prologue_forward_ex``, read in place)."""
+    n = M * L * P
+    if y.dim() != 2 or tuple(y.shape) != (B * Lq, 2 * n) or not y.is_contiguous() or not y.is_cuda:
+        raise ValueError(f"MSDA prologue rows: y must be a contiguous device (B*Lq, 2*M*L*P) tensor, got "
+                         f"{tuple(y.shape)}")
+    cd = torch.float64 if y.dtype == torch.float64 else torch.float32
+    if ref.dtype != cd or tuple(ref.shape[:3]) != (B, Lq, L) or not ref.is_contiguous():
+        raise ValueError(f"MSDA prologue rows: reference_points {tuple(ref.shape)} {ref.dtype}")
+    lib = _native.load_library()
+    loc = torch.empty((B, Lq, M, L, P), dtype=cd, device=y.device)
+    aw = torch.empty_like(loc)
+    base = y.data_ptr()
+    rc = lib.msda_hip_prologue_forward_ex(
+        base, base + n * y.element_size(), _native.DTYPE_TAGS[y.dtype], ref.data_ptr(), ref.shape[3],
+        _native.host_i64_array(shapes), L, B, Lq, M, P, 2 * n, loc.data_ptr(), aw.data_ptr(),
+        _native.stream_handle(y.device))
+    _native.check(rc, "msda_hip_prologue_forward_ex")
+    return loc, aw
+
+
+def prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, shapes, need_ref=True):
+    """``prologue_backward`` into ONE (B*Lq, 2*M*L*P) buffer of [grad offsets | grad logits] rows
+    (the dgrad GEMM's input) -> (g2, grad_ref or None)."""
+    B, Lq, M, L, P = aw.shape
+    n = M * L * P
+    cd = aw.dtype
+    lib = _native.load_library()
+    grad_loc = torch.zeros_like(aw) if grad_loc is None else grad_loc.to(cd).contiguous()
+    grad_aw = torch.zeros_like(aw) if grad_aw is None else grad_aw.to(cd).contiguous()
+    g2 = torch.empty_like(y)
+    g_ref = torch.empty_like(ref) if need_ref else None
+    base, ybase = g2.data_ptr(), y.data_ptr()
+    rc = lib.msda_hip_prologue_backward_ex(
+        grad_loc.data_ptr(), grad_aw.data_ptr(), aw.data_ptr(), ybase, _native.DTYPE_TAGS[y.dtype], ref.data_ptr(),
+        ref.shape[3], _native.host_i64_array(shapes), L, B, Lq, M, P, 2 * n, base, base + n * g2.element_size(),
+        None if g_ref is None else g_ref.data_ptr(), _native.stream_handle(y.device))
+    _native.check(rc, "msda_hip_prologue_backward_ex")
+    return g2, g_ref
 
 
 class MSDAPrologueFunction(Function):

@@ -40,6 +40,44 @@ from .models.modules.linear import Linear, deferred_weight_grads
 __all__ = ["FlatGradTrainer"]
 
 
+def _flat_order(model, params):
+    """``params`` in model order, except that the groups modules ask to be adjacent
+    (``flat_groups()``, e.g. MSDeformAttn's two query projections) are laid out back to back where
+    the group's first member stands: their views into the flat buffers (fp32 values / gradients,
+    bf16 shadow) are then consecutive, and a fused kernel reads them as one tensor."""
+    follow = {}
+    for mod in model.modules():
+        groups = getattr(mod, "flat_groups", None)
+        if callable(groups):
+            for g in groups():
+                if all(p.requires_grad for p in g) and all(id(p) not in follow for p in g):
+                    follow[id(g[0])] = list(g)
+                    for p in g[1:]:
+                        follow[id(p)] = None
+    out, seen = [], set()
+    for p in params:
+        if id(p) in seen:
+            continue
+        grp = follow.get(id(p), [p]) if id(p) in follow else [p]
+        if grp is None:  # placed with its group's first member
+            continue
+        for q in grp:
+            if id(q) not in seen:
+                seen.add(id(q))
+                out.append(q)
+    for p in params:  # a member whose group leader is absent (frozen) keeps its place at the end
+        if id(p) not in seen:
+            seen.add(id(p))
+            out.append(p)
+    return out
+
+
+def _record(events):
+    e = torch.cuda.Event(enable_timing=True)
+    e.record()
+    return e
+
+
 class FlatGradTrainer:
     def __init__(self, model, loss_fn, lr=1e-4, weight_decay=1e-4, max_norm=0.1, use_bf16=True, graph=True,
                  process_group=None, fused_optimizer=None, betas=(0.9, 0.999), eps=1e-8, handover=True,
@@ -51,7 +89,7 @@ class FlatGradTrainer:
         self.graph = graph
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_available() and dist.is_initialized() else 1
-        self.params = [p for p in model.parameters() if p.requires_grad]
+        self.params = _flat_order(model, [p for p in model.parameters() if p.requires_grad])
         dev = self.params[0].device
         self.device = dev
         for p in self.params:
@@ -110,6 +148,17 @@ class FlatGradTrainer:
             lr0 = torch.tensor(float(lr), device=dev) if graph else lr
             self.opt = torch.optim.AdamW(self.params, lr=lr0, betas=betas, eps=eps, weight_decay=weight_decay,
                                          capturable=graph, foreach=True)
+        # a loss with a host step inside the forward (the DVC step's Hungarian matching): an object
+        # with stage_a(model, batch) -> state, request(state) -> device tensor for the host,
+        # host(state, cpu_tensor), upload() (stream-ordered H2D copies into its static device
+        # buffers) and stage_b(model, batch, state) -> loss.  Captured as two graphs around the
+        # host step (capture()).
+        self.staged = all(hasattr(loss_fn, a) for a in ("stage_a", "request", "host", "upload", "stage_b"))
+        self._g_a = None
+        self._stage_state = None
+        self._request_like = None
+        self._request_host = None
+        self.phase_events = None  # a list: step() appends (name, start, end) HIP events per phase
         self._g_fb = None
         self._g_up = None
         self._loss = None
@@ -277,7 +326,9 @@ class FlatGradTrainer:
         for mod, w, b, ow, ob in self._mhas:
             mod._mfl_shadow = (w, b, ow, ob, mod.in_proj_weight._version, mod.out_proj.weight._version)
 
-    def _forward_backward(self, batch, cache_casts=True):
+    def _forward_backward(self, batch, cache_casts=True, stage_state=None):
+        if not self.handover and self.staged:
+            raise ValueError("FlatGradTrainer: a staged loss needs handover=True")
         if not self.handover:  # accumulate into the zeroed flat buffer (one add kernel per parameter)
             self.flat_grad.zero_()
             with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_bf16,
@@ -289,8 +340,17 @@ class FlatGradTrainer:
             p.grad = None
         with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_bf16,
                             cache_enabled=cache_casts), seed_pool(self.device):
-            out = self.model(*batch)
-            loss = self.loss_fn(out)
+            if not self.staged:
+                out = self.model(*batch)
+                loss = self.loss_fn(out)
+            else:  # a host step inside the forward (staged loss, see capture())
+                if stage_state is None:
+                    stage_state = self.loss_fn.stage_a(self.model, batch)
+                    req = self.loss_fn.request(stage_state)
+                    self._request_like = (tuple(req.shape), req.dtype)
+                    self.loss_fn.host(stage_state, req.cpu())  # the step's host synchronisation
+                    self.loss_fn.upload()
+                loss = self.loss_fn.stage_b(self.model, batch, stage_state)
         capturing = self.device.type == "cuda" and torch.cuda.is_current_stream_capturing()
         # parameters found unused (by every rank, last step) do not hold their buckets back
         self._known_unused = frozenset(self._unused or ())
@@ -438,11 +498,25 @@ class FlatGradTrainer:
         # capture_error_mode "thread_local": the RCCL process group's watchdog thread polls the
         # events of the warm-up collectives (hipEventQuery) while this thread captures; under the
         # default global mode that poll is refused and the watchdog aborts the process
+        pool = None
+        if self.staged:
+            # graph A: the forward up to the host step and the copy of its request into pinned
+            # host memory; graph B (same memory pool) runs the rest of the forward and the whole
+            # backward, through graph A's autograd nodes, whose saved tensors A refreshes in place
+            shape, dtype = self._request_like  # from the eager warm-up
+            self._request_host = torch.empty(shape, dtype=dtype, device="cpu").pin_memory()
+            self._g_a = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self._g_a, capture_error_mode="thread_local"):
+                with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_bf16,
+                                    cache_enabled=False), seed_pool(self.device):
+                    self._stage_state = self.loss_fn.stage_a(self.model, batch)
+                self._request_host.copy_(self.loss_fn.request(self._stage_state), non_blocking=True)
+            pool = self._g_a.pool()
         self._g_fb = torch.cuda.CUDAGraph()
         self._overlap_now = self.overlap and self.capture_collectives
         try:
-            with torch.cuda.graph(self._g_fb, capture_error_mode="thread_local"):
-                self._loss = self._forward_backward(batch, cache_casts=False)
+            with torch.cuda.graph(self._g_fb, pool=pool, capture_error_mode="thread_local"):
+                self._loss = self._forward_backward(batch, cache_casts=False, stage_state=self._stage_state)
         finally:
             self._fb_reduces, self._overlap_now = self._overlap_now, self.overlap
         self._g_up = torch.cuda.CUDAGraph()
@@ -457,10 +531,28 @@ class FlatGradTrainer:
             return self.eager_step(batch)
         if self._g_fb is None:
             raise RuntimeError("FlatGradTrainer.capture(batch) must run before step()")
+        ev = self.phase_events
+        mark = (lambda: None) if ev is None else (lambda: _record(ev))
+        t0 = mark()
+        if self.staged:
+            self._g_a.replay()
+            t1 = mark()
+            torch.cuda.current_stream(self.device).synchronize()  # the request is in pinned memory
+            self.loss_fn.host(self._stage_state, self._request_host)
+            self.loss_fn.upload()
+            t2 = mark()
+            if ev is not None:
+                ev.append(("graph A: forward to the host step", t0, t1))
+                ev.append(("host step (device->host wait, host work, upload)", t1, t2))
+            t0 = t2
         self._g_fb.replay()
+        t1 = mark()
         if not self._fb_reduces:
             self._overlap_now = False
             self._allreduce()  # one all-reduce between the two graphs
             self._overlap_now = self.overlap
         self._g_up.replay()
+        if ev is not None:
+            ev.append(("graph B: rest of forward + backward" if self.staged else "forward + backward", t0, t1))
+            ev.append(("all-reduce + clip + AdamW", t1, mark()))
         return self._loss

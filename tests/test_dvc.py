@@ -353,3 +353,20 @@ def test_mm_caption_decoder_matches_reference_gpu(golden, dev):
 @pytest.mark.gpu
 def test_mm_dvc_matches_reference_gpu(golden, dev):
     _check_mm_dvc(golden, dev)
+
+
+def test_staged_dvc_loss_equals_eager_loss_cpu():
+    """StagedDVCLoss (the two-graph DVC step's stages, run eagerly by the trainer) computes
+    dvc_workload_loss of the plain forward: fp32 on the CPU with the oracle MSDA core, dropout off."""
+    torch.manual_seed(0)
+    model = PKG.dvc_core.build_dvc(d_model=64, num_queries=10, T=32, enc_layers=1, dec_layers=2, caption_depth=1,
+                                   dropout=0.0, vocab_size=100, ff_dim=128)
+    obj = PKG.dvc_core.synthetic_dvc_batch(3, T=32, feature_dim=64, vocab_size=100, seed=3)
+    with oracle_core(PKG):
+        loss_e = PKG.dvc_core.dvc_workload_loss(model(obj, is_training=True), obj)
+        sl = PKG.dvc_core.StagedDVCLoss(obj, model)
+        tr = PKG.train_step.FlatGradTrainer(model, sl, lr=1e-3, use_bf16=False, graph=False)
+        assert tr.staged
+        loss_s = tr._forward_backward((obj,))
+    torch.testing.assert_close(loss_s, loss_e.detach(), rtol=1e-6, atol=1e-6)
+    assert torch.isfinite(tr.flat_grad).all() and tr.flat_grad.abs().sum() > 0

@@ -81,7 +81,7 @@ class _Stack(nn.Module):
 
 
 EXPECTED_PATHS = ("add_ln_carry", "relu_dropout", "layer_values_shadow", "sdpa_self_attn_shadow",
-                  "linear_shadow", "linear_pair_shadow", "msda_prologue", "zero_rows", "msda_bfloat16")
+                  "linear_shadow", "query_prologue", "zero_rows", "msda_bfloat16")
 
 
 def test_d256_bench_composition_matches_reference_bf16(golden, dev):

@@ -1,0 +1,75 @@
+"""The full DVC training step as two HIP graphs around its host matching (train_step.py, staged
+losses; dvc_core.StagedDVCLoss): the staged forward computes the eager forward's loss, and
+graph-replayed steps follow eager steps of the same model (reference engine.py:55-134 with
+models/deformable/unimodal_deformable_dvc.py:103-300)."""
+import copy
+
+import pytest
+import torch
+
+from conftest import PKG
+
+pytestmark = pytest.mark.gpu
+
+
+def _small(dev, dtype=torch.float32):
+    torch.manual_seed(0)
+    model = PKG.dvc_core.build_dvc(d_model=256, num_queries=20, T=128, enc_layers=2, dec_layers=2, caption_depth=2,
+                                   dropout=0.0, vocab_size=500, ff_dim=512).to(dev, dtype)
+    obj = PKG.dvc_core.synthetic_dvc_batch(4, T=128, feature_dim=256, vocab_size=500, seed=5, device=dev)
+    obj['video_tensor'] = obj['video_tensor'].to(dtype)
+    obj['video_length'] = obj['video_length'].to(dtype)
+    for t in obj['video_target']:
+        t['segments'] = t['segments'].to(dtype)
+    return model, obj
+
+
+def test_staged_forward_equals_eager_forward(dev):
+    """stage_a -> host matching -> upload -> stage_b gives the loss of forward() +
+    dvc_workload_loss on the same weights (fp32, dropout off): the same kernels on the same
+    matched indices, which reach stage_b through the static device buffers."""
+    model, obj = _small(dev)
+    model.train()
+    loss_e = PKG.dvc_core.dvc_workload_loss(model(obj, is_training=True), obj)
+    sl = PKG.dvc_core.StagedDVCLoss(obj, model)
+    st = sl.stage_a(model, (obj,))
+    sl.host(st, sl.request(st).cpu())
+    sl.upload()
+    loss_s = sl.stage_b(model, (obj,), st)
+    torch.cuda.synchronize()
+    torch.testing.assert_close(loss_s, loss_e, rtol=1e-6, atol=1e-6)
+    # the uploaded indices are the eager matching's, level by level
+    levels = model.matcher.match_levels(st['out_aux'], obj['video_target'])
+    for lvl, ind in enumerate(levels):
+        b, s = PKG.utils.preds_postprocess.get_src_permutation_idx(ind)
+        assert torch.equal(sl.idx_dev[lvl, 0].cpu(), b) and torch.equal(sl.idx_dev[lvl, 1].cpu(), s)
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_staged_graph_steps_track_eager_steps(dev, bf16):
+    """Three graph-replayed DVC steps (graph A: proposals + matching costs; host: assignment and
+    index upload; graph B: crop, context mask, caption decoder, loss, backward; then clip +
+    AdamW) follow three eager steps from the same weights: losses and gradient norms agree, and
+    every replay re-runs the matching on the replayed costs."""
+    model, obj = _small(dev)
+    batch = (obj,)
+    te = PKG.train_step.FlatGradTrainer(copy.deepcopy(model), lambda r: PKG.dvc_core.dvc_workload_loss(r, obj),
+                                        lr=1e-4, weight_decay=1e-4, max_norm=0.1, use_bf16=bf16, graph=False)
+    mg = copy.deepcopy(model)
+    tg = PKG.train_step.FlatGradTrainer(mg, PKG.dvc_core.StagedDVCLoss(obj, mg), lr=1e-4, weight_decay=1e-4,
+                                        max_norm=0.1, use_bf16=bf16, graph=True)
+    assert tg.staged
+    tg.capture(batch, warmup=2)
+    for _ in range(2):  # capture() ran two eager warm-up steps: same starting point
+        te.step(batch)
+    calls = []
+    host = tg.loss_fn.host
+    tg.loss_fn.host = lambda st, cpu: (calls.append(cpu.clone()), host(st, cpu))[1]
+    for i in range(3):
+        lg = tg.step(batch).item()
+        le = te.step(batch).item()
+        gg, ge = tg.flat_grad.norm().item(), te.flat_grad.norm().item()
+        tol = 1e-2 if bf16 else 1e-4
+        assert abs(lg - le) <= tol * abs(le), (i, lg, le)
+        assert abs(gg - ge) <= 10 * tol * ge, (i, gg, ge)
+    assert len(calls) == 3 and not torch.equal(calls[0], calls[2])  # fresh costs on every replay

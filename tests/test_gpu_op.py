@@ -302,6 +302,7 @@ WIN_CASES = [
     ([50, 25, 13, 7],        3, 8, 200,  4, "uniform"),    # audio pyramid: levels shorter than a block
     ([64, 32],               2, 2, 77,   8, "clustered"),  # P = 8, a partial last query tile
     ([4096, 2048, 1024, 512], 1, 8, 7680, 4, "local"),     # configs[3] per-clip shape, encoder-like samples
+    ([50, 25, 13, 7],        2, 8, 1920, 4, "uniform"),    # configs[2]: video queries on the audio pyramid
 ]
 
 
@@ -317,13 +318,20 @@ def local_locations(B, Lq, M, shapes, P, seed):
     return loc.float()
 
 
+@pytest.mark.parametrize("split", ["", "1", "8"])
 @pytest.mark.parametrize("padding", ["border", "zeros"])
 @pytest.mark.parametrize("case", range(len(WIN_CASES)))
-def test_row_block_mfma_backward_matches_oracle(dev, monkeypatch, case, padding):
+def test_row_block_mfma_backward_matches_oracle(dev, monkeypatch, case, padding, split):
     """The row-block MFMA backward (csrc/msda_win.hip; MSDA_HIP_BWD_WIN=1 forces it where it
     applies: bf16 values, D = 64, P <= 8, > 512 samples a level) against the oracle on the same
-    bf16-rounded inputs in fp32 (reference semantics attention.py:331-383)."""
+    bf16-rounded inputs in fp32 (reference semantics attention.py:331-383), with the default and
+    forced waves per row block (MSDA_HIP_WIN_SPLIT: visits dealt over 1 or 8 waves, partial sums
+    added through LDS)."""
     monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
+    if split:
+        monkeypatch.setenv("MSDA_HIP_WIN_SPLIT", split)
+    else:
+        monkeypatch.delenv("MSDA_HIP_WIN_SPLIT", raising=False)
     shapes, B, M, Lq, P, kind = WIN_CASES[case]
     D = 64
     value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=60 + case)
@@ -338,6 +346,67 @@ def test_row_block_mfma_backward_matches_oracle(dev, monkeypatch, case, padding)
     np.testing.assert_allclose(_np(gv), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
     np.testing.assert_allclose(_np(ga), r_ga, rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(_np(gl), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))
+
+
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("case", range(len(WIN_CASES)))
+def test_forward_tiles_equal_backward_prepass(dev, monkeypatch, case, padding):
+    """The tiles forward (msda_hip_forward_tiles: (b, m, q)-ordered items, the row-block
+    backward's tile intervals reduced in the workgroup) gives the plain forward's output bit for
+    bit, and the backward fed those intervals (msda_hip_backward_tiles) gives the gradients of
+    the backward that computes them in its own prepass bit for bit — both see the same rows
+    (msda_win.h win_sample_rows), so every row block visits the same tiles in the same order."""
+    monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
+    shapes, B, M, Lq, P, kind = WIN_CASES[case]
+    D = 64
+    value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=70 + case)
+    if kind == "clustered":
+        loc = clustered_locations(B, Lq, M, shapes, P, seed=71 + case)
+    elif kind == "local":
+        loc = local_locations(B, Lq, M, shapes, P, seed=71 + case)
+    starts = O.level_starts(shapes)
+    v, lc, a, g = (t.cuda() for t in (value, loc, aw, gout))
+    out = msda.msda_forward(v, shapes, starts, lc, a, padding)
+    out_t, tiles = msda.msda_forward(v, shapes, starts, lc, a, padding, want_tiles=True)
+    assert tiles is not None and tiles.numel() == B * M * len(shapes) * ((Lq + 31) // 32) * 8
+    assert torch.equal(out, out_t)
+    ref = msda.msda_backward(v, shapes, starts, lc, a, g, padding)
+    got = msda.msda_backward(v, shapes, starts, lc, a, g, padding, tiles=tiles)
+    for r, x in zip(ref, got):
+        assert torch.equal(r, x)
+    # intervals: every (b, m, level, tile) interval holds each of its samples' base rows (up to
+    # one row of slack: this float64 restatement may floor differently at exact row boundaries)
+    iv = tiles.view(torch.int32).view(B, M, len(shapes), -1, 2).cpu()
+    x = loc.double()
+    for l, T in enumerate(shapes):
+        if padding == "border":
+            y = ((x[..., l, :] * 2 - 1 + 1) * (T * 0.5) - 0.5).clamp(0, T - 1).floor()
+            lo_r = y
+        else:
+            y = x[..., l, :] * T - 0.5
+            live = (y > -1) & (y < T)
+            lo_r = torch.where(live, y.floor().clamp(min=0), torch.zeros_like(y))
+        q_tile = torch.arange(Lq) // 32
+        for t in (0, (Lq - 1) // 32):
+            sel = q_tile == t
+            rows = lo_r[:, sel].permute(0, 2, 1, 3).reshape(B, M, -1)  # (B, M, samples)
+            assert (iv[:, :, l, t, 0] <= rows.min(-1).values.long() + 1).all()
+            assert (iv[:, :, l, t, 1] >= rows.max(-1).values.long()).all()
+
+
+def test_row_block_dispatch_orders_agree(dev, monkeypatch):
+    """The position-chunk dispatch order (default) and the coarsest-level-first order
+    (MSDA_HIP_WIN_ORDER=0) compute every row block the same way: bitwise equal gradients."""
+    monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
+    shapes, B, M, Lq, P = [1024, 512, 256, 128], 3, 8, 1920, 4   # B * M = 24: pairs over 8 XCDs, 3 each
+    value, loc, aw, gout = rand_case(shapes, B, M, 64, Lq, P, torch.bfloat16, seed=80)
+    loc = local_locations(B, Lq, M, shapes, P, seed=81)
+    runs = []
+    for order in ("0", "1"):
+        monkeypatch.setenv("MSDA_HIP_WIN_ORDER", order)
+        runs.append(run_hip(value, shapes, loc, aw, gout))
+    for a, b in zip(runs[0][1:], runs[1][1:]):
+        assert torch.equal(a, b)
 
 
 def clustered_locations(B, Lq, M, shapes, P, seed):

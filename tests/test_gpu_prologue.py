@@ -123,3 +123,48 @@ def test_module_uses_fused_prologue_and_matches_composite(dev):
         a.zero_grad()
     for u, v in zip(*outs):
         torch.testing.assert_close(u, v, rtol=1e-10, atol=1e-10)
+
+
+@pytest.mark.parametrize("Lq,ref_dim", [(1920, 1), (100, 2), (37, 1)])
+def test_query_prologue_matches_two_projection_form(dev, Lq, ref_dim):
+    """_QueryPrologue (both query projections as one GEMM into [offsets | logits] rows, the strided
+    prologue kernels reading / writing those rows; msda_hip_prologue_*_ex) against the
+    two-projection form (linear_pair + the prologue on separate tensors), bf16 autocast with the
+    trainer's shadow layout (the two weights back to back): locations, weights and every
+    gradient agree to bf16 rounding of the projections."""
+    from torch import nn
+    att = PKG.models.modules.attention
+    torch.manual_seed(3)
+    m = att.MSDeformAttn(256, 4, 8, 4).to(dev)
+    nn.init.normal_(m.sampling_offsets.weight, std=0.02)
+    B, L, M, P = 2, 4, 8, 4
+    shapes = [64, 32, 16, 8]
+    x = torch.randn(B, Lq, 256, device=dev).requires_grad_(True)
+    ref = torch.rand(B, Lq, L, ref_dim, device=dev).requires_grad_(True)
+    a, b = m.sampling_offsets, m.attention_weights
+    wc = torch.cat((a.weight, b.weight)).to(torch.bfloat16)
+    bc = torch.cat((a.bias, b.bias)).to(torch.bfloat16)
+    wca, wcb, bca, bcb = wc[:128], wc[128:], bc[:128], bc[128:]  # adjacent views, as the trainer's shadow
+    gl = torch.randn(B, Lq, M, L, P, device=dev)
+    ga = torch.randn(B, Lq, M, L, P, device=dev)
+
+    def grads(loc, aw):
+        params = [x, ref, a.weight, a.bias, b.weight, b.bias]
+        return torch.autograd.grad((loc * gl).sum() + (aw * ga).sum(), params)
+
+    PKG._trace.clear()
+    loc1, aw1 = att._QueryPrologue.apply(x.to(torch.bfloat16), a.weight, a.bias, b.weight, b.bias, wca, bca, wcb, bcb,
+                                         ref, tuple(shapes), (B, Lq, M, L, P))
+    assert PKG._trace.hits.get("query_prologue") == 1
+    g1 = grads(loc1, aw1)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        for mod, w, bb in ((a, wca, bca), (b, wcb, bcb)):
+            mod.set_bf16_shadow(w, bb)
+        off, lg = PKG.models.modules.linear.linear_pair(x, a, b)
+    loc2, aw2 = msda.msda_prologue_apply(off.view(B, Lq, M, L, P), lg.view(B, Lq, M, L * P), ref, shapes)
+    g2 = grads(loc2, aw2)
+    torch.testing.assert_close(aw1, aw2, rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(loc1, loc2, rtol=2e-2, atol=2e-3)
+    for n, u, v in zip(("x", "ref", "w_off", "b_off", "w_aw", "b_aw"), g1, g2):
+        err = (u.float() - v.float()).norm() / v.float().norm().clamp_min(1e-12)
+        assert err < 2e-2, (n, err.item())

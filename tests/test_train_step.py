@@ -402,3 +402,19 @@ def test_fused_update_leaves_unused_parameters_untouched(dev):
     assert unused
     for k in unused:
         torch.testing.assert_close(after[k], before[k], rtol=0, atol=0, msg=k)
+
+
+def test_flat_order_lays_query_projection_pairs_back_to_back():
+    """FlatGradTrainer's flat layout puts each MSDeformAttn's sampling_offsets / attention_weights
+    weights (and biases) next to each other (MSDeformAttn.flat_groups), keeping every parameter
+    once: the fused query projection then reads [W_off; W_aw] as one view of the bf16 shadow."""
+    model = _model()
+    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, use_bf16=False, graph=False)
+    assert sorted(map(id, tr.params)) == sorted(id(p) for p in model.parameters() if p.requires_grad)
+    pos = {id(p): i for i, p in enumerate(tr.params)}
+    att = [m for m in model.modules() if isinstance(m, PKG.models.modules.attention.MSDeformAttn)]
+    assert att
+    for m in att:
+        for a, b in m.flat_groups():
+            assert pos[id(b)] == pos[id(a)] + 1
+            assert b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()
