@@ -30,6 +30,7 @@ from ..modules.embedding_layers import PositionEmbeddingVideoSine
 from ..modules.layers import FFN, ContextMaskModel
 from ..modules.linear import Linear
 from ..modules.misc_modules import predict_event_num
+from ...utils.preds_postprocess import SegmentMemory
 from ..unimodal_caption_decoder import build_unimodal_caption_decoder
 from .unimodal_deformable_transformer import build_unimodal_deformable_transformer
 
@@ -135,6 +136,10 @@ class UnimodalDeformableDVC(nn.Module):
         num_pred = query_features.shape[0]
         video_durations = st['durations']
         indices = level_indices[-1]
+        if is_training:
+            # the levels' crops as views of the encoder memory: the caption decoder projects the
+            # clips' rows once a step (utils/preds_postprocess.py, SegmentMemory)
+            memory = SegmentMemory.of(memory)
 
         outputs_captions, memory_list, memory_mask_list, pred_memory_mask_list = [], [], [], []
         for lvl in range(num_pred):

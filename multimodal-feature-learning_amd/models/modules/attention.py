@@ -26,6 +26,7 @@ from torch.autograd.function import once_differentiable
 from torch.nn.init import constant_, xavier_uniform_
 
 from ... import msda as _msda
+from ...utils.preds_postprocess import SegmentMemory
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
 from .linear import Linear, _AutocastLinear, _bias_grad, _defer, _weight_grad, linear_pair
@@ -450,8 +451,12 @@ class CrossAttention(nn.Module):
         Lk = k.shape[1]
         H, hd = self.num_heads, self.head_dim
         q = self.q_linear(q).reshape(B, Lq, H, hd).transpose(1, 2)
-        k = self.k_linear(k).reshape(B, Lk, H, hd).transpose(1, 2)
-        v = self.v_linear(v).reshape(B, Lk, H, hd).transpose(1, 2)
+        if isinstance(k, SegmentMemory):  # the DVC's cropped memory: projections of the clips' rows, gathered
+            k = k.project(self.k_linear).reshape(B, Lk, H, hd).transpose(1, 2)
+            v = v.project(self.v_linear).reshape(B, Lk, H, hd).transpose(1, 2)
+        else:
+            k = self.k_linear(k).reshape(B, Lk, H, hd).transpose(1, 2)
+            v = self.v_linear(v).reshape(B, Lk, H, hd).transpose(1, 2)
         masked = self._mask(attn_mask, key_padding_mask)
         if need_weights:
             att = self.attention_dropout(masked_scores_softmax(q @ k.transpose(-2, -1), masked, self.scale))

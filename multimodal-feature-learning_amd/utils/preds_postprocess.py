@@ -11,7 +11,7 @@ from math import floor
 
 import torch
 
-__all__ = ["get_src_permutation_idx", "denormalize_segments", "crop_segments", "level_token_ranges",
+__all__ = ["get_src_permutation_idx", "denormalize_segments", "crop_segments", "SegmentMemory", "level_token_ranges",
            "captions_to_string", "pre_process"]
 
 
@@ -73,8 +73,60 @@ def crop_segments(features, denormalized_segments, segment_batch_id, video_durat
         s = torch.clamp((lower + (diff * seg[:, 0] / dur)).round().long(), min=lower, max=upper - 1)
         e = torch.clamp((lower + (diff * seg[:, 1] / dur)).round().long(), min=lower, max=upper - 1)
         keep |= (tok[None, :] >= s[:, None]) & (tok[None, :] < e[:, None])
+    if isinstance(features, SegmentMemory):
+        return features.select(bid, keep), ~keep
     cropped = torch.where(keep[..., None], features[bid], features.new_zeros(()))
     return cropped, ~keep
+
+
+class SegmentMemory:
+    """The cropped memory of the matched segments, (n, K, d), without materialising it: row s is
+    ``source[index[s]]`` where ``keep[s]`` and 0 elsewhere (crop_segments).  A crop of a crop (the
+    reference's level l > 0 crops level l-1's crop, unimodal_deformable_dvc.py:235) is again one:
+    ``select`` composes the index and ANDs the keep masks, so every level's memory refers to the
+    one (B, K, d) encoder memory.
+
+    What it saves is the caption decoder's cross-attention projections (models/modules/attention.py
+    CrossAttention): k_linear / v_linear of a cropped row are those of its source row where kept and
+    the bias where zeroed (0 . W + b), so ``project`` runs each projection over the B clips' K rows
+    ONCE per step — shared by every segment and every decoder level, since they all read the same
+    caption decoder — and gathers per segment, instead of a GEMM over the n K rows of every level.
+    The projected rows are the same values the materialised crop gives (each output row is its
+    own product); ``materialize`` returns the crop itself."""
+
+    def __init__(self, source, index, keep, cache=None):
+        self.source, self.index, self.keep = source, index, keep
+        self.cache = {} if cache is None else cache
+        self.shape = (int(index.shape[0]),) + tuple(source.shape[1:])
+        self.dtype, self.device = source.dtype, source.device
+
+    @classmethod
+    def of(cls, memory):
+        """The uncropped memory (B, K, d) as the source of the crops."""
+        B, K = memory.shape[0], memory.shape[1]
+        return cls(memory, torch.arange(B, device=memory.device),
+                   torch.ones(B, K, dtype=torch.bool, device=memory.device))
+
+    def __getitem__(self, rows):
+        if not isinstance(rows, torch.Tensor) or rows.dim() != 1:
+            raise TypeError("SegmentMemory: only 1-D index tensors select segments")
+        return SegmentMemory(self.source, self.index[rows], self.keep[rows], self.cache)
+
+    def select(self, rows, keep):
+        """Rows ``rows`` of this memory with everything outside ``keep`` (n, K) zeroed."""
+        return SegmentMemory(self.source, self.index[rows], self.keep[rows] & keep, self.cache)
+
+    def materialize(self):
+        return torch.where(self.keep[..., None], self.source[self.index], self.source.new_zeros(()))
+
+    def project(self, linear):
+        """``linear(self.materialize())`` from one projection of the source per step."""
+        P = self.cache.get(linear)
+        if P is None:
+            P = linear(self.source)
+            self.cache[linear] = P
+        bias = linear.bias.to(P.dtype) if linear.bias is not None else P.new_zeros(())
+        return torch.where(self.keep[..., None], P.index_select(0, self.index), bias)
 
 
 def captions_to_string(captions, vocab):
