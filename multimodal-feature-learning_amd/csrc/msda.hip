@@ -2744,9 +2744,9 @@ int run_backward_pair(const Problem& pr, const PairPlan& pp, const void* value, 
 //    position), i.e. where the pair kernel would stage them through a workspace — the configs[3]
 //    per-rank call (T = 4096: 237-263 us against 421-511, tools/win_ab.py);
 //  * self-attention-like calls — queries covering the value pyramid (2 Lq >= S) and every level at
-//    least 64 rows: the encoder (T = 1024: 68-77 us against 69-82).  Cross-modal calls onto a short
-//    pyramid (video queries on the 95-row audio pyramid: every query tile meets every row block)
-//    keep the pair kernel (66 us against 127).
+//    least 64 rows: the encoder (T = 1024: 68-77 us against 69-82);
+//  * queries far outnumbering the rows (Lq >= 4 S): the cross-modal call onto the audio pyramid,
+//    where every query tile meets every row block — with several waves a block (msda_win.hip).
 int win_env() { return env_int("MSDA_HIP_BWD_WIN", -1); }
 
 bool win_supported_call(int value_dtype, long long D, long long Lq, long long P, long long M, long long L) {
@@ -2763,7 +2763,9 @@ bool win_applies(int value_dtype, long long D, long long Lq, long long P, long l
   if (win_env() == 1 || win_overflow(Lq, P)) return true;
   int minT = 1 << 30;
   for (int l = 0; l < L; ++l) minT = min(minT, T[l]);
-  return minT >= 64 && 2 * Lq >= S;
+  // encoder-like calls, or queries far outnumbering the rows (configs[2]'s video queries on the
+  // 95-row audio pyramid: 8 waves a row block, 51.6 us against the pair kernel's 63.3)
+  return (minT >= 64 && 2 * Lq >= S) || Lq >= 4 * S;
 }
 
 // The backward of this call takes the row-block MFMA path (msda_win.hip) when handed a workspace

@@ -538,7 +538,13 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   sh.blk0[sh.L] = nb;
   sh.nblk = nb;
   if (sh.B * sh.M == 0 || nb == 0) return 0;
-  const bool chunked = win_chunk_order(sh) && !(getenv("MSDA_HIP_WIN_ORDER") && atoi(getenv("MSDA_HIP_WIN_ORDER")) == 0);
+  // position-chunk order where the blocks are many (T = 4096: 3,840 an XCD; 245 -> 219 us at the
+  // configs[3] call), coarsest-level-first where they are few and the longest blocks set the tail
+  // (T = 1024: 960 an XCD; 55 against 64 us, tools/win_tiles_ab.py).  MSDA_HIP_WIN_ORDER: 0 / 1 forces.
+  const char* oe = getenv("MSDA_HIP_WIN_ORDER");
+  const int order_env = oe ? atoi(oe) : -1;
+  const bool chunked = win_chunk_order(sh) &&
+                       (order_env == 1 || (order_env != 0 && (long long)sh.ppx * sh.nblk >= 2048));
   if (!chunked) sh.nchunk = 0;
   // tile intervals: written by the forward (msda_fwd16_tiles_kernel) or by the prepass below
   auto* tiles = static_cast<int2*>(tiles_ready != nullptr ? const_cast<void*>(tiles_ready) : workspace);

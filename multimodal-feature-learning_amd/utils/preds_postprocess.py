@@ -125,8 +125,36 @@ class SegmentMemory:
         if P is None:
             P = linear(self.source)
             self.cache[linear] = P
-        bias = linear.bias.to(P.dtype) if linear.bias is not None else P.new_zeros(())
-        return torch.where(self.keep[..., None], P.index_select(0, self.index), bias)
+        bias = linear.bias.to(P.dtype) if linear.bias is not None else P.new_zeros(P.shape[-1])
+        return _GatherKeep.apply(P, bias, self.index, self.keep)
+
+
+class _GatherKeep(torch.autograd.Function):
+    """``where(keep[..., None], P[index], bias)``.  The backward sums each source row's gradient
+    over the segments that read it, and the bias's over the positions that read it, in fp32 and
+    rounds once — autograd's index_select backward would accumulate 16-bit P's gradient in 16 bits
+    (segments of one clip adding into the same rows)."""
+
+    @staticmethod
+    def forward(ctx, P, bias, index, keep):
+        ctx.save_for_backward(index, keep)
+        ctx.p_shape, ctx.dtypes = P.shape, (P.dtype, bias.dtype)
+        return torch.where(keep[..., None], P.index_select(0, index), bias)
+
+    @staticmethod
+    def backward(ctx, g):
+        index, keep = ctx.saved_tensors
+        k = keep[..., None]
+        acc = torch.promote_types(g.dtype, torch.float32)  # fp32, or fp64 for fp64 memories
+        g32 = g.to(acc)
+        gP = gb = None
+        if ctx.needs_input_grad[0]:
+            gP = torch.zeros(ctx.p_shape, dtype=acc, device=g.device)
+            gP.index_add_(0, index, torch.where(k, g32, 0.0))
+            gP = gP.to(ctx.dtypes[0])
+        if ctx.needs_input_grad[1]:
+            gb = torch.where(k, 0.0, g32).sum((0, 1)).to(ctx.dtypes[1])
+        return gP, gb, None, None
 
 
 def captions_to_string(captions, vocab):

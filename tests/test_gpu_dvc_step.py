@@ -45,19 +45,18 @@ def test_staged_forward_equals_eager_forward(dev):
         assert torch.equal(sl.idx_dev[lvl, 0].cpu(), b) and torch.equal(sl.idx_dev[lvl, 1].cpu(), s)
 
 
-@pytest.mark.parametrize("bf16", [False, True])
-def test_staged_graph_steps_track_eager_steps(dev, bf16):
+def test_staged_graph_steps_track_eager_steps(dev):
     """Three graph-replayed DVC steps (graph A: proposals + matching costs; host: assignment and
     index upload; graph B: crop, context mask, caption decoder, loss, backward; then clip +
-    AdamW) follow three eager steps from the same weights: losses and gradient norms agree, and
-    every replay re-runs the matching on the replayed costs."""
+    AdamW) follow three eager steps from the same weights (fp32: the same kernels, so the same
+    values), and every replay re-runs the matching on the replayed costs."""
     model, obj = _small(dev)
     batch = (obj,)
     te = PKG.train_step.FlatGradTrainer(copy.deepcopy(model), lambda r: PKG.dvc_core.dvc_workload_loss(r, obj),
-                                        lr=1e-4, weight_decay=1e-4, max_norm=0.1, use_bf16=bf16, graph=False)
+                                        lr=1e-4, weight_decay=1e-4, max_norm=0.1, use_bf16=False, graph=False)
     mg = copy.deepcopy(model)
     tg = PKG.train_step.FlatGradTrainer(mg, PKG.dvc_core.StagedDVCLoss(obj, mg), lr=1e-4, weight_decay=1e-4,
-                                        max_norm=0.1, use_bf16=bf16, graph=True)
+                                        max_norm=0.1, use_bf16=False, graph=True)
     assert tg.staged
     tg.capture(batch, warmup=2)
     for _ in range(2):  # capture() ran two eager warm-up steps: same starting point
@@ -69,7 +68,28 @@ def test_staged_graph_steps_track_eager_steps(dev, bf16):
         lg = tg.step(batch).item()
         le = te.step(batch).item()
         gg, ge = tg.flat_grad.norm().item(), te.flat_grad.norm().item()
-        tol = 1e-2 if bf16 else 1e-4
-        assert abs(lg - le) <= tol * abs(le), (i, lg, le)
-        assert abs(gg - ge) <= 10 * tol * ge, (i, gg, ge)
+        assert abs(lg - le) <= 1e-4 * abs(le), (i, lg, le)
+        assert abs(gg - ge) <= 1e-3 * ge, (i, gg, ge)
     assert len(calls) == 3 and not torch.equal(calls[0], calls[2])  # fresh costs on every replay
+
+
+def test_staged_graph_replay_matches_eager_bf16(dev):
+    """Under bf16 autocast (the bench's regime): one replay of graph A + host matching + graph B
+    gives the eager staged step's loss and gradient on the same weights, to the run-to-run spread
+    of the bf16 backward (fp32 index-add atomics in the segment-memory gather: ~1e-2 of the
+    gradient norm; the loss to 1e-3)."""
+    model, obj = _small(dev)
+    tg = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.StagedDVCLoss(obj, model), lr=1e-4, use_bf16=True,
+                                        graph=True)
+    tg.capture((obj,), warmup=1)
+    tg._g_a.replay()
+    torch.cuda.synchronize()
+    tg.loss_fn.host(tg._stage_state, tg._request_host)
+    tg.loss_fn.upload()
+    tg._g_fb.replay()
+    torch.cuda.synchronize()
+    lg, fg = tg._loss.item(), tg.flat_grad.clone()
+    le = tg._forward_backward((obj,)).item()
+    fe = tg.flat_grad.clone()
+    assert abs(lg - le) <= 1e-3 * abs(le), (lg, le)
+    assert (fg - fe).norm() <= 5e-2 * fe.norm(), ((fg - fe).norm().item(), fe.norm().item())

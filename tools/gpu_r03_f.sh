@@ -15,4 +15,6 @@ timeout -k 10 500 python3 -u -m pytest -x -v --timeout 300 --timeout-method thre
   tests/test_gpu_dvc_step.py tests/test_dvc.py -m gpu > gpurun_out/r03f_dvc_tests.log 2>&1
 rc=$?; tail -n 12 gpurun_out/r03f_dvc_tests.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 300 python3 -u bench.py --config dvc --steps 10 --warmup 3 --cpu-baseline 0 --timer-steps 1 > gpurun_out/r03f_bench_dvc.json 2> gpurun_out/r03f_bench_dvc.err
-rc=$?; python3 -c "import json; d=json.load(open('gpurun_out/r03f_bench_dvc.json')); print(d['value'], d['ms_per_step'], d.get('phases_ms_per_step'))"; tail -n 3 gpurun_out/r03f_bench_dvc.err; exit $rc
+rc=$?; python3 -c "import json; d=json.load(open('gpurun_out/r03f_bench_dvc.json')); print(d['value'], d['ms_per_step'], d.get('phases_ms_per_step'))"; tail -n 3 gpurun_out/r03f_bench_dvc.err; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_dvc -o run --output-format csv -- python3 bench.py --config dvc --steps 3 --warmup 2 --cpu-baseline 0 --timer-steps 0 > gpurun_out/r03f_prof_dvc.log 2>&1
+rc=$?; echo "prof dvc rc=$rc"; exit $rc
