@@ -36,7 +36,8 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-__all__ = ["Linear", "split_k_chunks", "linear_pair", "deferred_weight_grads", "flush_point"]
+__all__ = ["Linear", "split_k_chunks", "linear_pair", "deferred_weight_grads", "flush_point",
+           "flat_grad_destinations"]
 
 DEFER_MAX_ROWS = 4096  # GEMM K (input rows) up to which weight gradients are queued and batched
 
@@ -148,15 +149,49 @@ def split_k_chunks(k, min_chunk=1024, max_split=8):
     return 1
 
 
-def _bias_grad(g2):
+_dest = None  # flat_grad_destinations: {"views": {id(param): flat view}, "claimed": set()}
+
+
+@contextlib.contextmanager
+def flat_grad_destinations(views):
+    """Inside (the trainer's backward): the first gradient produced for a parameter in ``views``
+    ({id(param): its fp32 view of the flat gradient buffer}) is written straight into that view,
+    which autograd then hands to the parameter as its .grad — instead of a fresh tensor copied
+    into the flat buffer afterwards (one 171 MB copy pass per step at the bench shape)."""
+    global _dest
+    prev, _dest = _dest, {"views": views, "claimed": set()}
+    try:
+        yield
+    finally:
+        _dest = prev
+
+
+def _claim(param):
+    """The flat view ``param``'s gradient may be written into, or None: once per backward and
+    only while the parameter has no gradient yet (a later producer's result is added by autograd,
+    into that view or a copy of it)."""
+    d = _dest
+    if d is None or param is None or param.grad is not None:
+        return None
+    v = d["views"].get(id(param))
+    if v is None or id(param) in d["claimed"]:
+        return None
+    d["claimed"].add(id(param))
+    return v.view_as(v)  # a fresh view object: autograd adopts it as .grad instead of cloning
+
+
+def _bias_grad(g2, out=None):
     """fp32 column sum of dY (K, N) through mfl_colsum (one streaming pass, fixed order);
-    torch's column reduction where the kernel's layout conditions do not hold."""
+    torch's column reduction where the kernel's layout conditions do not hold.  ``out``: an fp32
+    (N,) destination (a flat-buffer view)."""
     if g2.dtype not in (torch.bfloat16, torch.float16) or (g2.shape[1] * 2) % 16 or not g2.is_contiguous():
-        return g2.sum(0, dtype=torch.float32)
+        r = g2.sum(0, dtype=torch.float32)
+        return r if out is None else out.copy_(r)
     from ... import _native
     lib = _native.load_library()
     K, N = g2.shape
-    out = torch.empty(N, dtype=torch.float32, device=g2.device)
+    if out is None:
+        out = torch.empty(N, dtype=torch.float32, device=g2.device)
     ws = torch.empty(lib.mfl_colsum_workspace_bytes(K, N), dtype=torch.uint8, device=g2.device)
     rc = lib.mfl_colsum(g2.data_ptr(), _native.DTYPE_TAGS[g2.dtype], K, N, out.data_ptr(), ws.data_ptr(),
                         _native.stream_handle(g2.device))
@@ -165,24 +200,25 @@ def _bias_grad(g2):
     return out
 
 
-def _sum_slabs(part):
+def _sum_slabs(part, out=None):
     """part.sum(0) of the fp32 split-K partials (s, n_out, n_in) through mfl_sum_slabs (one pass,
-    chunk order)."""
+    chunk order), into ``out`` if given."""
     n = part[0].numel()
     if n % 4 or not part.is_contiguous():
-        return part.sum(0)
+        return part.sum(0) if out is None else torch.sum(part, 0, out=out)
     from ... import _native
     lib = _native.load_library()
-    out = torch.empty(part.shape[1:], dtype=torch.float32, device=part.device)
+    if out is None:
+        out = torch.empty(part.shape[1:], dtype=torch.float32, device=part.device)
     rc = lib.mfl_sum_slabs(part.data_ptr(), part.shape[0], n, out.data_ptr(), _native.stream_handle(part.device))
     if rc != 0:
         raise RuntimeError("mfl_sum_slabs failed: " + lib.flat_adamw_last_error().decode())
     return out
 
 
-def _weight_grad(g2, x2):
+def _weight_grad(g2, x2, out=None):
     """fp32 dW = dY^T X of 16-bit dY (K, N) and X (K, C): K split into chunks, one strided-batched
-    GEMM with fp32 partial outputs, then their sum."""
+    GEMM with fp32 partial outputs, then their sum (into ``out`` if given)."""
     k, n_out, n_in = x2.shape[0], g2.shape[1], x2.shape[1]
     s = split_k_chunks(k)
     if s > 1:
@@ -190,8 +226,9 @@ def _weight_grad(g2, x2):
         # extra 8-32 MB pass per call, ~0.3 ms per step, tools/op_census.py)
         part = torch.bmm(g2.view(s, k // s, n_out).transpose(1, 2), x2.view(s, k // s, n_in),
                          out_dtype=torch.float32)
-        return _sum_slabs(part)
-    return torch.mm(g2.t(), x2, out_dtype=torch.float32)
+        return _sum_slabs(part, out)
+    r = torch.mm(g2.t(), x2, out_dtype=torch.float32)
+    return r if out is None else out.copy_(r)
 
 
 class _AutocastLinear(torch.autograd.Function):
@@ -229,9 +266,9 @@ class _AutocastLinear(torch.autograd.Function):
         if nig[1] and (not ctx.has_bias or nig[2]) and _defer((g2, x2, ctx.weight, 0, ctx.bias if ctx.has_bias else None)):
             return gx, None, None, None, None
         if nig[1]:
-            gw = _weight_grad(g2, x2)
+            gw = _weight_grad(g2, x2, _claim(ctx.weight))
         if ctx.has_bias and nig[2]:
-            gb = _bias_grad(g2)
+            gb = _bias_grad(g2, _claim(ctx.bias))
         return gx, gw, gb, None, None
 
 

@@ -256,8 +256,10 @@ class MSDAFunction(Function):
         ctx.meta = (shapes, starts, padding_mode)
         ctx.save_for_backward(value, loc, aw)
         # the row intervals of the row-block backward come with the forward (it reads loc anyway)
-        out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode,
-                                      want_tiles=any(ctx.needs_input_grad[:3]))
+        if any(ctx.needs_input_grad[:3]):
+            out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode, want_tiles=True)
+        else:
+            out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode), None
         return out
 
     @staticmethod

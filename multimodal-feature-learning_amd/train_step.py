@@ -35,7 +35,7 @@ import torch
 import torch.distributed as dist
 
 from .models.modules.add_norm import seed_pool
-from .models.modules.linear import Linear, deferred_weight_grads
+from .models.modules.linear import Linear, deferred_weight_grads, flat_grad_destinations
 
 __all__ = ["FlatGradTrainer"]
 
@@ -107,6 +107,8 @@ class FlatGradTrainer:
             self.grad_views.append(self.flat_grad[off:off + k].view_as(p))
             off += k
         self._attach_grads()
+        # the flat views the large weight-gradient GEMMs write into directly (linear.py, _claim)
+        self._grad_dest = {id(p): v for p, v in zip(self.params, self.grad_views)}
         # bf16 weight shadow for the autocast Linear layers (one cast per step, _refresh_shadow)
         self.flat_bf16 = None
         self._linears = []
@@ -252,7 +254,8 @@ class FlatGradTrainer:
         for i in idx:
             if self.params[i].grad is not None:
                 self._got[i] = True
-        got = [(self.grad_views[i], self.params[i].grad) for i in idx if self.params[i].grad is not None]
+        got = [(self.grad_views[i], self.params[i].grad) for i in idx if self.params[i].grad is not None
+               and self.params[i].grad.data_ptr() != self.grad_views[i].data_ptr()]  # (written in place)
         missing = [self.grad_views[i] for i in idx if self.params[i].grad is None]
         if got:
             torch._foreach_copy_([v for v, _ in got], [g for _, g in got])
@@ -363,7 +366,7 @@ class FlatGradTrainer:
         try:
             # the short-K layers' weight gradients are batched (models/modules/linear.py) and
             # handed over by _deliver, at the model's flush points or after the backward
-            with deferred_weight_grads(self._deliver) as queue:
+            with deferred_weight_grads(self._deliver) as queue, flat_grad_destinations(self._grad_dest):
                 self._flush_ready()
                 loss.backward()  # overlap: complete buckets are copied and all-reduced from the hooks, in order
                 queue.flush()

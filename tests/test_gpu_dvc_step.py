@@ -74,22 +74,32 @@ def test_staged_graph_steps_track_eager_steps(dev):
 
 
 def test_staged_graph_replay_matches_eager_bf16(dev):
-    """Under bf16 autocast (the bench's regime): one replay of graph A + host matching + graph B
-    gives the eager staged step's loss and gradient on the same weights, to the run-to-run spread
-    of the bf16 backward (fp32 index-add atomics in the segment-memory gather: ~1e-2 of the
-    gradient norm; the loss to 1e-3)."""
+    """Under bf16 autocast (the bench's regime): replays of graph A + host matching + graph B give
+    the eager staged step's loss and gradient on the same weights, to within the eager step's own
+    run-to-run spread: the bf16 backward is not bitwise reproducible (fp32 atomics in the index
+    gathers' backward, rounded into bf16 activations gradients downstream; two eager steps on the
+    same weights differ by ~8 % of the gradient norm at this tiny random model, tools/dvc_graph_diag2.py),
+    so replay-vs-eager is held to twice the eager-vs-eager difference; the loss to 1e-3."""
     model, obj = _small(dev)
     tg = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.StagedDVCLoss(obj, model), lr=1e-4, use_bf16=True,
                                         graph=True)
     tg.capture((obj,), warmup=1)
-    tg._g_a.replay()
-    torch.cuda.synchronize()
-    tg.loss_fn.host(tg._stage_state, tg._request_host)
-    tg.loss_fn.upload()
-    tg._g_fb.replay()
-    torch.cuda.synchronize()
-    lg, fg = tg._loss.item(), tg.flat_grad.clone()
-    le = tg._forward_backward((obj,)).item()
-    fe = tg.flat_grad.clone()
+
+    def replay():
+        tg._g_a.replay()
+        torch.cuda.synchronize()
+        tg.loss_fn.host(tg._stage_state, tg._request_host)
+        tg.loss_fn.upload()
+        tg._g_fb.replay()
+        torch.cuda.synchronize()
+        return tg._loss.item(), tg.flat_grad.clone()
+
+    def eager():
+        loss = tg._forward_backward((obj,)).item()
+        torch.cuda.synchronize()
+        return loss, tg.flat_grad.clone()
+
+    (lg, fg), (le, fe), (le2, fe2) = replay(), eager(), eager()
     assert abs(lg - le) <= 1e-3 * abs(le), (lg, le)
-    assert (fg - fe).norm() <= 5e-2 * fe.norm(), ((fg - fe).norm().item(), fe.norm().item())
+    spread = (fe2 - fe).norm() / fe.norm()
+    assert (fg - fe).norm() / fe.norm() <= 2 * spread + 1e-2, ((fg - fe).norm().item(), spread.item())
