@@ -95,17 +95,20 @@ class FlatGradTrainer:
         for p in self.params:
             if p.dtype != torch.float32:
                 raise TypeError("FlatGradTrainer keeps fp32 master parameters; got " + str(p.dtype))
-        n = sum(p.numel() for p in self.params)
-        self.flat_param = torch.empty(n, dtype=torch.float32, device=dev)
+        # every parameter starts on a 16-byte boundary (the 16-byte vector kernels that write weight
+        # gradients straight into their views, linear.py _claim); the pad elements stay zero
+        self._offs, n = [], 0
+        for p in self.params:
+            self._offs.append(n)
+            n += (p.numel() + 3) // 4 * 4
+        self.flat_param = torch.zeros(n, dtype=torch.float32, device=dev)
         self.flat_grad = torch.zeros(n, dtype=torch.float32, device=dev)
         self.grad_views = []
-        off = 0
-        for p in self.params:
+        for p, off in zip(self.params, self._offs):
             k = p.numel()
             self.flat_param[off:off + k].copy_(p.detach().reshape(-1))
             p.data = self.flat_param[off:off + k].view_as(p)
             self.grad_views.append(self.flat_grad[off:off + k].view_as(p))
-            off += k
         self._attach_grads()
         # the flat views the large weight-gradient GEMMs write into directly (linear.py, _claim)
         self._grad_dest = {id(p): v for p, v in zip(self.params, self.grad_views)}
@@ -199,13 +202,10 @@ class FlatGradTrainer:
         """[(start, end, [param index, ...]), ...]: consecutive parameters from the last one
         backwards, each bucket a contiguous range of the flat buffer of at most cap_elems elements
         (or one parameter larger than that)."""
-        offs, off = [], 0
-        for p in self.params:
-            offs.append(off)
-            off += p.numel()
+        offs = self._offs
         buckets, cur, cur_n = [], [], 0
         for i in reversed(range(len(self.params))):
-            n = self.params[i].numel()
+            n = (self.params[i].numel() + 3) // 4 * 4  # its span in the flat buffer (16-B aligned)
             if cur and cur_n + n > cap_elems:
                 buckets.append(cur)
                 cur, cur_n = [], 0
@@ -216,7 +216,8 @@ class FlatGradTrainer:
         out = []
         for idx in buckets:
             lo, hi = min(idx), max(idx)
-            out.append((offs[lo], offs[hi] + self.params[hi].numel(), sorted(idx)))
+            end = offs[hi + 1] if hi + 1 < len(offs) else self.flat_grad.numel()  # (with the 16-B pad)
+            out.append((offs[lo], end, sorted(idx)))
         return out
 
     def _make_hook(self, i):
@@ -306,11 +307,7 @@ class FlatGradTrainer:
 
     # --- the three phases ------------------------------------------------------------
     def _views(self, flat):
-        out, off = [], 0
-        for p in self.params:
-            out.append(flat[off:off + p.numel()].view_as(p))
-            off += p.numel()
-        return out
+        return [flat[off:off + p.numel()].view_as(p) for p, off in zip(self.params, self._offs)]
 
     def _attach_grads(self):
         for p, g in zip(self.params, self.grad_views):
@@ -433,10 +430,7 @@ class FlatGradTrainer:
         views = []
         flats = [self.flat_param, self.exp_avg, self.exp_avg_sq] + ([self.flat_bf16] if self.flat_bf16 is not None
                                                                      else [])
-        offs, off = [], 0
-        for p in self.params:
-            offs.append(off)
-            off += p.numel()
+        offs = self._offs
         for i in unused:
             n = self.params[i].numel()
             views.extend(f[offs[i]:offs[i] + n] for f in flats)

@@ -177,7 +177,7 @@ def test_trainer_batched_weight_grads_match_per_layer(dev, graph, monkeypatch):
         else:
             tr._forward_backward((x,))
         torch.cuda.synchronize()
-        return tr.flat_grad.clone(), dict(PKG._trace.hits), [p.numel() for p in tr.params]
+        return torch.cat([v.reshape(-1) for v in tr.grad_views]), dict(PKG._trace.hits), [p.numel() for p in tr.params]
 
     ref, hits_ref, sizes = run(0)
     got, hits, _ = run(4096)
@@ -217,7 +217,7 @@ def test_dvc_core_step_with_batched_weight_grads(dev, monkeypatch):
         PKG._trace.clear()
         tr._forward_backward(batch)
         torch.cuda.synchronize()
-        return tr.flat_grad.clone(), dict(PKG._trace.hits), [p.numel() for p in tr.params]
+        return torch.cat([v.reshape(-1) for v in tr.grad_views]), dict(PKG._trace.hits), [p.numel() for p in tr.params]
 
     ref, _, sizes = run(0)
     ref2, _, _ = run(0)

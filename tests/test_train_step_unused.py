@@ -92,9 +92,11 @@ def _rank_main(rank, world, port, out_path):
         assert tr.overlap and len(tr.buckets) == len(tr.params)
         res = []
         for step, use in enumerate(PLAN):
-            before = tr.flat_param.clone()
+            # (per-parameter views: the flat buffers pad each parameter to 16 bytes)
+            before = torch.cat([p.detach().reshape(-1) for p in tr.params]).clone()
             tr._forward_backward((_x(10 * step + rank), use[rank]))
-            res.append(dict(params=before, grad=tr.flat_grad.clone(), unused=list(tr._unused), late=tr._late))
+            res.append(dict(params=before, grad=torch.cat([v.reshape(-1) for v in tr.grad_views]).clone(),
+                            unused=list(tr._unused), late=tr._late))
             tr._update()
         torch.save(res, f"{out_path}.{rank}")
     finally:
