@@ -55,6 +55,9 @@ EXPORTED_SYMBOLS = (
     "mfl_relu_dropout_last_error",
     "mfl_zero_masked_rows",
     "mfl_zero_masked_rows_batched",
+    # include/gemm_small.h
+    "mfl_gemm_nt_bf16",
+    "mfl_gemm_last_error",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -117,6 +120,9 @@ def _declare(lib):
     lib.mfl_add_layernorm_backward_ex.restype = i32
     lib.mfl_add_layernorm_backward_ex.argtypes = [vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, vp, vp, vp,
                                                   vp, f32, vp, vp, vp]
+    lib.mfl_gemm_nt_bf16.restype = i32
+    lib.mfl_gemm_nt_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
+    lib.mfl_gemm_last_error.restype = ctypes.c_char_p
     lib.mfl_relu_dropout_forward.restype = i32
     lib.mfl_relu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]
     lib.mfl_relu_dropout_backward.restype = i32

@@ -29,7 +29,7 @@ from ... import msda as _msda
 from ...utils.preds_postprocess import SegmentMemory
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
-from .linear import Linear, _AutocastLinear, _bias_grad, _defer, _weight_grad, linear_pair
+from .linear import Linear, _AutocastLinear, _addmm, _bias_grad, _defer, _weight_grad, linear_pair
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
            "masked_scores_softmax", "mask_padding_rows", "mha_self_attention"]
@@ -95,7 +95,7 @@ class _QueryPrologue(torch.autograd.Function):
         B, Lq, M, L, P = dims
         wc, bc = _rows_view(wca, wcb), _rows_view(bca, bcb)
         x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(bc, x2, wc.t())
+        y = _addmm(bc, x2, wc)
         loc, aw = _msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes)
         ctx.save_for_backward(x2, wc, y, aw, ref)
         ctx.shapes, ctx.x_shape = shapes, x.shape
@@ -376,8 +376,8 @@ class _InProjection(torch.autograd.Function):
         bc = b.to(dt) if bc is None else bc
         e = w.shape[1]
         a2, v2 = x_qk.reshape(-1, e), x_v.reshape(-1, e)
-        qk = torch.addmm(bc[:2 * e], a2, wc[:2 * e].t())
-        v = torch.addmm(bc[2 * e:], v2, wc[2 * e:].t())
+        qk = _addmm(bc[:2 * e], a2, wc[:2 * e])
+        v = _addmm(bc[2 * e:], v2, wc[2 * e:])
         ctx.save_for_backward(a2, v2, wc)
         ctx.shape = x_qk.shape
         ctx.params = (w, b)

@@ -37,7 +37,7 @@ import torch.nn.functional as F
 from torch import nn
 
 __all__ = ["Linear", "split_k_chunks", "linear_pair", "deferred_weight_grads", "flush_point",
-           "flat_grad_destinations"]
+           "flat_grad_destinations", "small_addmm"]
 
 DEFER_MAX_ROWS = 4096  # GEMM K (input rows) up to which weight gradients are queued and batched
 
@@ -136,6 +136,47 @@ def flush_point(t):
     if _queue is None and not torch.is_grad_enabled():
         return t
     return _FlushPoint.apply(t) if t.requires_grad else t
+
+
+SMALL_GEMM_MAX_ROWS = 1024  # GEMM rows (tokens) up to which small_addmm runs the HIP kernel
+
+
+def small_addmm(bias, x2, w):
+    """``bias + x2 @ w.T`` (bias may be None) for bf16 x2 (M, K) with M <= SMALL_GEMM_MAX_ROWS and
+    w (N, K), on the short-M HIP GEMM (include/gemm_small.h: a workgroup a 32 x 32 tile, its waves
+    splitting K): the decoder's 800-token Linear layers take 9-15 us in the library GEMM, latency
+    bound.  None where it does not apply (the caller keeps torch.addmm).  MFL_SMALL_GEMM=0 turns it
+    off."""
+    M, K = x2.shape
+    N = w.shape[0]
+    if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 0 < M <= SMALL_GEMM_MAX_ROWS
+            and N % 32 == 0 and K % 32 == 0 and x2.stride(1) == 1 and w.stride(1) == 1
+            and x2.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and x2.stride(0) >= K and w.stride(0) >= K
+            and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N))
+            and x2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
+        return None
+    import os
+    if os.environ.get("MFL_SMALL_GEMM", "1") == "0":
+        return None
+    from ... import _native, _trace
+    lib = _native.load_library()
+    out = torch.empty(M, N, dtype=torch.bfloat16, device=x2.device)
+    rc = lib.mfl_gemm_nt_bf16(x2.data_ptr(), w.data_ptr(), None if bias is None else bias.data_ptr(), out.data_ptr(),
+                              M, N, K, x2.stride(0), w.stride(0), N, _native.stream_handle(x2.device))
+    if rc == 2:  # MFL_GEMM_UNSUPPORTED
+        return None
+    if rc != 0:
+        raise RuntimeError("mfl_gemm_nt_bf16 failed: " + lib.mfl_gemm_last_error().decode())
+    _trace.hit("small_gemm")
+    return out
+
+
+def _addmm(bias, x2, w):
+    """``bias + x2 @ w.T`` (``x2 @ w.T`` without bias): the short-M HIP GEMM where it applies."""
+    y = small_addmm(bias, x2, w)
+    if y is not None:
+        return y
+    return torch.mm(x2, w.t()) if bias is None else torch.addmm(bias, x2, w.t())
 
 
 def split_k_chunks(k, min_chunk=1024, max_split=8):
@@ -243,10 +284,7 @@ class _AutocastLinear(torch.autograd.Function):
         if wc is None:
             wc = weight.to(dt)
         x2 = x.reshape(-1, x.shape[-1])
-        if bias is not None:
-            y = torch.addmm(bias.to(dt) if bc is None else bc, x2, wc.t())
-        else:
-            y = torch.mm(x2, wc.t())
+        y = _addmm((bias.to(dt) if bc is None else bc) if bias is not None else None, x2, wc)
         ctx.save_for_backward(x2, wc)
         ctx.has_bias = bias is not None
         ctx.x_shape = x.shape
@@ -285,8 +323,8 @@ class _AutocastLinearPair(torch.autograd.Function):
         wca = wa.to(dt) if wca is None else wca
         wcb = wb.to(dt) if wcb is None else wcb
         x2 = x.reshape(-1, x.shape[-1])
-        ya = torch.addmm(ba.to(dt) if bca is None else bca, x2, wca.t())
-        yb = torch.addmm(bb.to(dt) if bcb is None else bcb, x2, wcb.t())
+        ya = _addmm(ba.to(dt) if bca is None else bca, x2, wca)
+        yb = _addmm(bb.to(dt) if bcb is None else bcb, x2, wcb)
         ctx.save_for_backward(x2, wca, wcb)
         ctx.x_shape = x.shape
         ctx.params = (wa, ba, wb, bb)

@@ -233,3 +233,34 @@ def test_dvc_core_step_with_batched_weight_grads(dev, monkeypatch):
             bad.append((i, n, err, noise))
         off += n
     assert not bad, bad
+
+
+@pytest.mark.parametrize("M,N,K,bias", [(800, 512, 512, True), (800, 2048, 512, True), (800, 512, 2048, True),
+                                        (532, 512, 512, False), (37, 256, 128, True), (1, 32, 32, True),
+                                        (1024, 96, 64, False), (760, 1024, 512, True), (800, 256, 512, True)])
+def test_small_gemm_matches_fp32_product(dev, M, N, K, bias):
+    """The short-M HIP GEMM (include/gemm_small.h) against the fp32 product of the same bf16
+    operands, rounded once to bf16 (what addmm's fp32-accumulating GEMM returns): at most one bf16
+    ulp apart (summation order), and against torch.addmm itself."""
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    x = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(dev, torch.bfloat16)
+    b = torch.randn(N, generator=g).to(dev, torch.bfloat16) if bias else None
+    y = linear_mod.small_addmm(b, x, w)
+    assert y is not None and y.dtype == torch.bfloat16 and y.shape == (M, N)
+    ref = x.float() @ w.float().t() + (b.float() if bias else 0.0)
+    ulp = ref.abs().clamp_min(1e-30) * 2 ** -7
+    assert ((y.float() - ref).abs() <= ulp + 1e-6).all()
+    lib = torch.addmm(b, x, w.t()) if bias else torch.mm(x, w.t())
+    assert ((y.float() - lib.float()).abs() <= 2 * ulp + 1e-6).all()
+
+
+def test_small_gemm_strided_rows_and_refusals(dev):
+    """Row strides (a slice of a wider matrix, as the decoder's in_proj q/k rows of W) and the
+    shapes it leaves to the library (N % 32 != 0, more than SMALL_GEMM_MAX_ROWS rows)."""
+    x = torch.randn(200, 512, device=dev).to(torch.bfloat16)
+    w = torch.randn(1536, 512, device=dev).to(torch.bfloat16) / 20
+    y = linear_mod.small_addmm(None, x, w[512:1024])
+    torch.testing.assert_close(y.float(), (x.float() @ w[512:1024].float().t()), rtol=2 ** -7, atol=1e-3)
+    assert linear_mod.small_addmm(None, x, w[:100]) is None
+    assert linear_mod.small_addmm(None, torch.zeros(2048, 512, device=dev, dtype=torch.bfloat16), w) is None

@@ -5,7 +5,8 @@ run() { local name=$1 t=$2; shift 2; echo "=== $name $(date +%T)"; timeout -k 10
 run r03h_tests 600 python3 -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider \
   tests/test_gpu_op.py tests/test_gpu_prologue.py tests/test_gpu_bf16_composition.py tests/test_gpu_dvc_step.py tests/test_dvc.py \
   tests/test_train_step.py tests/test_gpu_linear.py \
-  -m gpu -k "tiles or orders or row_block or T4096 or prologue or composition or dvc or staged or cross or train or graph or linear or wgrad"
+  -m gpu -k "tiles or orders or row_block or T4096 or prologue or composition or dvc or staged or cross or train or graph or linear or wgrad or gemm"
+run r03h_gemm_ab 200 python3 -u tools/small_gemm_ab.py
 run r03h_bench 300 python3 -u bench.py --steps 20 --warmup 5 --cpu-baseline 0
 run r03h_bench_dvc 300 python3 -u bench.py --config dvc --steps 10 --warmup 3 --cpu-baseline 0 --timer-steps 1
 run r03h_bench_mm 300 python3 -u bench.py --config multimodal --steps 10 --warmup 3 --cpu-baseline 0

@@ -1,0 +1,48 @@
+#!/usr/bin/env python3
+"""The short-M HIP GEMM (models/modules/linear.py small_addmm) against torch.addmm (hipBLASLt) at
+the decoder / caption-decoder / audio shapes: HIP events over 50 calls, interleaved, median of 5."""
+import importlib
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+PKG = importlib.import_module("multimodal-feature-learning_amd")
+L = PKG.models.modules.linear
+
+
+def timed(fn, iters=50):
+    for _ in range(5):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1000
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    for M, N, K in [(800, 512, 512), (800, 256, 512), (800, 1024, 512), (800, 2048, 512), (800, 512, 2048),
+                    (532, 512, 512), (532, 10016, 512), (760, 512, 512), (760, 2048, 512)]:
+        x = torch.randn(M, K, device=dev).to(torch.bfloat16)
+        w = torch.randn(N, K, device=dev).to(torch.bfloat16)
+        b = torch.randn(N, device=dev).to(torch.bfloat16)
+        res = {"lib": [], "hip": []}
+        for _ in range(5):
+            res["lib"].append(timed(lambda: torch.addmm(b, x, w.t())))
+            res["hip"].append(timed(lambda: L.small_addmm(b, x, w)))
+        med = {k: round(statistics.median(v), 2) for k, v in res.items()}
+        print(json.dumps({"M": M, "N": N, "K": K, "us": med, "hip_TFs": round(2 * M * N * K / med["hip"] / 1e6, 1)}),
+              flush=True)
+
+
+if __name__ == "__main__":
+    main()
