@@ -28,6 +28,11 @@ extern "C" {
 int mfl_gemm_nt_bf16(const void* A, const void* Bt, const void* bias, void* C, int64_t M, int64_t N, int64_t K,
                      int64_t lda, int64_t ldb, int64_t ldc, void* stream);
 
+/* C[M, N] = A[M, K] . B[K, N] (+ bias[N]) with B row-major (K, N): a Linear layer's input gradient
+ * dX = dY . W, W stored (out, in).  Same requirements with ldb >= N (B's rows N-contiguous). */
+int mfl_gemm_nn_bf16(const void* A, const void* B, const void* bias, void* C, int64_t M, int64_t N, int64_t K,
+                     int64_t lda, int64_t ldb, int64_t ldc, void* stream);
+
 const char* mfl_gemm_last_error(void);
 
 #ifdef __cplusplus

@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "mfl_zero_masked_rows_batched",
     # include/gemm_small.h
     "mfl_gemm_nt_bf16",
+    "mfl_gemm_nn_bf16",
     "mfl_gemm_last_error",
     "msda_hip_last_error",
     "msda_hip_abi_version",
@@ -122,6 +123,8 @@ def _declare(lib):
                                                   vp, f32, vp, vp, vp]
     lib.mfl_gemm_nt_bf16.restype = i32
     lib.mfl_gemm_nt_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
+    lib.mfl_gemm_nn_bf16.restype = i32
+    lib.mfl_gemm_nn_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
     lib.mfl_gemm_last_error.restype = ctypes.c_char_p
     lib.mfl_relu_dropout_forward.restype = i32
     lib.mfl_relu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]

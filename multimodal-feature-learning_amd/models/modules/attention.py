@@ -29,7 +29,7 @@ from ... import msda as _msda
 from ...utils.preds_postprocess import SegmentMemory
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
-from .linear import Linear, _AutocastLinear, _addmm, _bias_grad, _defer, _weight_grad, linear_pair
+from .linear import Linear, _AutocastLinear, _addmm, _bias_grad, _defer, _mm_nn, _weight_grad, linear_pair
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
            "masked_scores_softmax", "mask_padding_rows", "mha_self_attention"]
@@ -108,7 +108,7 @@ class _QueryPrologue(torch.autograd.Function):
         x2, wc, y, aw, ref = ctx.saved_tensors
         nig = ctx.needs_input_grad
         g2, g_ref = _msda.prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, ctx.shapes, need_ref=nig[9])
-        gx = torch.mm(g2, wc).view(ctx.x_shape) if nig[0] else None
+        gx = _mm_nn(g2, wc).view(ctx.x_shape) if nig[0] else None
         wa, ba, wb, bb = ctx.params
         na = wa.shape[0]
         rest = (None, None, None, None, g_ref, None, None)
@@ -391,8 +391,8 @@ class _InProjection(torch.autograd.Function):
         gqk = gqk.reshape(-1, 2 * e).to(wc.dtype)
         gv = gv.reshape(-1, e).to(wc.dtype)
         nig = ctx.needs_input_grad
-        dqk = torch.mm(gqk, wc[:2 * e]).view(ctx.shape) if nig[0] else None
-        dv = torch.mm(gv, wc[2 * e:]).view(ctx.shape) if nig[1] else None
+        dqk = _mm_nn(gqk, wc[:2 * e]).view(ctx.shape) if nig[0] else None
+        dv = _mm_nn(gv, wc[2 * e:]).view(ctx.shape) if nig[1] else None
         w, b = ctx.params  # weight / bias gradients batched with the other short-K layers' (linear.py)
         if nig[2] and nig[3] and _defer((gqk, a2, w, 0, b), (gv, v2, w, 2 * e, b)):
             return dqk, dv, None, None, None, None

@@ -37,7 +37,7 @@ import torch.nn.functional as F
 from torch import nn
 
 __all__ = ["Linear", "split_k_chunks", "linear_pair", "deferred_weight_grads", "flush_point",
-           "flat_grad_destinations", "small_addmm"]
+           "flat_grad_destinations", "small_addmm", "small_mm_nn"]
 
 DEFER_MAX_ROWS = 4096  # GEMM K (input rows) up to which weight gradients are queued and batched
 
@@ -171,6 +171,38 @@ def small_addmm(bias, x2, w):
     return out
 
 
+def small_mm_nn(g2, w):
+    """``g2 @ w`` for bf16 g2 (M, N) with M <= SMALL_GEMM_MAX_ROWS and w (N, K) row-major — a Linear
+    layer's input gradient — on the short-M HIP GEMM (mfl_gemm_nn_bf16); None where it does not apply."""
+    M, N = g2.shape
+    K = w.shape[1]
+    if not (g2.is_cuda and g2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 0 < M <= SMALL_GEMM_MAX_ROWS
+            and K % 32 == 0 and N % 32 == 0 and g2.stride(1) == 1 and w.stride(1) == 1
+            and g2.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and g2.stride(0) >= N and w.stride(0) >= K
+            and g2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
+        return None
+    import os
+    if os.environ.get("MFL_SMALL_GEMM", "1") == "0":
+        return None
+    from ... import _native, _trace
+    lib = _native.load_library()
+    out = torch.empty(M, K, dtype=torch.bfloat16, device=g2.device)
+    rc = lib.mfl_gemm_nn_bf16(g2.data_ptr(), w.data_ptr(), None, out.data_ptr(), M, K, N, g2.stride(0), w.stride(0), K,
+                              _native.stream_handle(g2.device))
+    if rc == 2:  # MFL_GEMM_UNSUPPORTED
+        return None
+    if rc != 0:
+        raise RuntimeError("mfl_gemm_nn_bf16 failed: " + lib.mfl_gemm_last_error().decode())
+    _trace.hit("small_gemm_nn")
+    return out
+
+
+def _mm_nn(g2, w):
+    """``g2 @ w`` (a Linear layer's input gradient): the short-M HIP GEMM where it applies."""
+    y = small_mm_nn(g2, w)
+    return torch.mm(g2, w) if y is None else y
+
+
 def _addmm(bias, x2, w):
     """``bias + x2 @ w.T`` (``x2 @ w.T`` without bias): the short-M HIP GEMM where it applies."""
     y = small_addmm(bias, x2, w)
@@ -300,7 +332,7 @@ class _AutocastLinear(torch.autograd.Function):
         gx = gw = gb = None
         nig = ctx.needs_input_grad
         if nig[0]:
-            gx = torch.mm(g2, wc).view(ctx.x_shape)
+            gx = _mm_nn(g2, wc).view(ctx.x_shape)
         if nig[1] and (not ctx.has_bias or nig[2]) and _defer((g2, x2, ctx.weight, 0, ctx.bias if ctx.has_bias else None)):
             return gx, None, None, None, None
         if nig[1]:

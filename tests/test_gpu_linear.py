@@ -235,6 +235,7 @@ def test_dvc_core_step_with_batched_weight_grads(dev, monkeypatch):
     assert not bad, bad
 
 
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K,bias", [(800, 512, 512, True), (800, 2048, 512, True), (800, 512, 2048, True),
                                         (532, 512, 512, False), (37, 256, 128, True), (1, 32, 32, True),
                                         (1024, 96, 64, False), (760, 1024, 512, True), (800, 256, 512, True)])
@@ -255,6 +256,7 @@ def test_small_gemm_matches_fp32_product(dev, M, N, K, bias):
     assert ((y.float() - lib.float()).abs() <= 2 * ulp + 1e-6).all()
 
 
+@pytest.mark.gpu
 def test_small_gemm_strided_rows_and_refusals(dev):
     """Row strides (a slice of a wider matrix, as the decoder's in_proj q/k rows of W) and the
     shapes it leaves to the library (N % 32 != 0, more than SMALL_GEMM_MAX_ROWS rows)."""
@@ -264,3 +266,23 @@ def test_small_gemm_strided_rows_and_refusals(dev):
     torch.testing.assert_close(y.float(), (x.float() @ w[512:1024].float().t()), rtol=2 ** -7, atol=1e-3)
     assert linear_mod.small_addmm(None, x, w[:100]) is None
     assert linear_mod.small_addmm(None, torch.zeros(2048, 512, device=dev, dtype=torch.bfloat16), w) is None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K", [(800, 512, 512), (800, 2048, 512), (800, 512, 2048), (532, 512, 512),
+                                   (37, 128, 256), (1, 32, 32), (800, 512, 1024), (800, 512, 256), (760, 512, 96)])
+def test_small_gemm_nn_matches_fp32_product(dev, M, N, K):
+    """The short-M NN GEMM (dX = dY . W, W row-major (N, K); B staged in LDS and read transposed)
+    against the fp32 product of the same bf16 operands: at most one bf16 ulp apart."""
+    g = torch.Generator(device="cpu").manual_seed(M * 3 + K)
+    dy = torch.randn(M, N, generator=g).to(dev, torch.bfloat16)
+    w = (torch.randn(N, K, generator=g) / N ** 0.5).to(dev, torch.bfloat16)
+    y = linear_mod.small_mm_nn(dy, w)
+    assert y is not None and y.shape == (M, K)
+    ref = dy.float() @ w.float()
+    assert ((y.float() - ref).abs() <= ref.abs() * 2 ** -7 + 1e-6).all()
+    # a column slice of a wider weight (the in_proj q / k rows) keeps its row stride
+    w2 = (torch.randn(N, 2 * K, generator=g) / N ** 0.5).to(dev, torch.bfloat16)
+    y2 = linear_mod.small_mm_nn(dy, w2[:, :K])
+    ref2 = dy.float() @ w2[:, :K].float()
+    assert ((y2.float() - ref2).abs() <= ref2.abs() * 2 ** -7 + 1e-6).all()

@@ -35,10 +35,13 @@ def main():
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = torch.randn(N, K, device=dev).to(torch.bfloat16)
         b = torch.randn(N, device=dev).to(torch.bfloat16)
-        res = {"lib": [], "hip": []}
+        g = torch.randn(M, N, device=dev).to(torch.bfloat16)  # dgrad: g (M, N) . w (N, K)
+        res = {"lib": [], "hip": [], "lib_dgrad": [], "hip_dgrad": []}
         for _ in range(5):
             res["lib"].append(timed(lambda: torch.addmm(b, x, w.t())))
             res["hip"].append(timed(lambda: L.small_addmm(b, x, w)))
+            res["lib_dgrad"].append(timed(lambda: torch.mm(g, w)))
+            res["hip_dgrad"].append(timed(lambda: L.small_mm_nn(g, w)))
         med = {k: round(statistics.median(v), 2) for k, v in res.items()}
         print(json.dumps({"M": M, "N": N, "K": K, "us": med, "hip_TFs": round(2 * M * N * K / med["hip"] / 1e6, 1)}),
               flush=True)
