@@ -38,6 +38,16 @@ int mfl_zero_masked_rows(void* x, int64_t rows, int64_t row_bytes, const uint8_t
 
 /* The same on nbatch consecutive (rows x row_bytes) matrices sharing one mask of rows bytes: the
  * decoder's value projections of all layers, computed as one batch (models/modules/value_proj.py). */
+/* Backward of the DVC segment memory's gathered projections (utils/preds_postprocess.py,
+ * SegmentMemory.project: out[s, t] = keep[s, t] ? P[index[s], t] : bias, s < n segments, t < K tokens):
+ *   grad_src[b, t, :]  = sum of grad[s, t, :] over s with index[s] == b and keep[s, t]   (bf16, every row written)
+ *   bias_part[t, :]    = sum of grad[s, t, :] over s with !keep[s, t]                   (fp32; the bias gradient
+ *                        is its sum over t)
+ * fp32 sums in segment order.  grad (n, K, d) bf16, index (n,) int64 in [0, B), keep (n, K) bool (1 byte);
+ * d % 8 == 0, d <= 512, 16-byte aligned grad / grad_src. */
+int mfl_gather_keep_backward(const void* grad, const int64_t* index, const void* keep, int64_t n, int64_t B, int64_t K,
+                             int64_t d, void* grad_src, float* bias_part, void* stream);
+
 int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t row_bytes, const uint8_t* mask,
                                  void* stream);
 

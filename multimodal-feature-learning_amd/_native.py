@@ -55,6 +55,7 @@ EXPORTED_SYMBOLS = (
     "mfl_relu_dropout_last_error",
     "mfl_zero_masked_rows",
     "mfl_zero_masked_rows_batched",
+    "mfl_gather_keep_backward",
     # include/gemm_small.h
     "mfl_gemm_nt_bf16",
     "mfl_gemm_nn_bf16",
@@ -123,6 +124,8 @@ def _declare(lib):
                                                   vp, f32, vp, vp, vp]
     lib.mfl_gemm_nt_bf16.restype = i32
     lib.mfl_gemm_nt_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
+    lib.mfl_gather_keep_backward.restype = i32
+    lib.mfl_gather_keep_backward.argtypes = [vp, vp, vp, i64, i64, i64, i64, vp, vp, vp]
     lib.mfl_gemm_nn_bf16.restype = i32
     lib.mfl_gemm_nn_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
     lib.mfl_gemm_last_error.restype = ctypes.c_char_p

@@ -137,6 +137,66 @@ int status(const char* what) {
   return 0;
 }
 
+// Backward of the DVC segment memory's gathered projections (utils/preds_postprocess.py,
+// _GatherKeep): forward out[s, t] = keep[s, t] ? P[index[s], t] : bias.  Here
+//   grad_P[b, t] = sum over segments s with index[s] == b and keep[s, t] of g[s, t]
+//   bias partial row t = sum over segments s with !keep[s, t] of g[s, t]
+// in fp32, in segment order (deterministic).  One workgroup per token t: wave w sums clips
+// b = w, w + 4, ... (the segments' clip ids are read as scalars), each lane 8 channels; the four
+// waves' bias sums meet in LDS.  Every (s, t) row of g is read once.
+__global__ __launch_bounds__(256) void gather_keep_bwd_kernel(const uint16_t* __restrict__ g,
+                                                              const long long* __restrict__ index,
+                                                              const uint8_t* __restrict__ keep, int n, int B, int K,
+                                                              int d, uint16_t* __restrict__ gsrc,
+                                                              float* __restrict__ bpart) {
+  __shared__ float red[4][512];
+  const int t = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c0 = lane * 8;
+  const bool act = c0 < d;
+  float bacc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) bacc[i] = 0.f;
+  for (int b = w; b < B; b += 4) {
+    float acc[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
+    for (int s = 0; s < n; ++s) {
+      if (index[s] != b) continue;  // wave-uniform
+      const long long row = (long long)s * K + t;
+      const bool k = keep[row] != 0;
+      if (act) {
+        const uint4 v = *reinterpret_cast<const uint4*>(g + row * d + c0);
+        const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float lo = __uint_as_float(u[i] << 16), hi = __uint_as_float(u[i] & 0xffff0000u);
+          if (k) {
+            acc[2 * i] += lo;
+            acc[2 * i + 1] += hi;
+          } else {
+            bacc[2 * i] += lo;
+            bacc[2 * i + 1] += hi;
+          }
+        }
+      }
+    }
+    if (act) {
+      uint4 o;
+      uint32_t* op = reinterpret_cast<uint32_t*>(&o);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        op[i] = rne(acc[2 * i]) | (rne(acc[2 * i + 1]) << 16);
+      *reinterpret_cast<uint4*>(gsrc + ((long long)b * K + t) * d + c0) = o;
+    }
+  }
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) red[w][c0 + i] = bacc[i];
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < d; j += 256) bpart[(long long)t * d + j] = red[0][j] + red[1][j] + red[2][j] + red[3][j];
+}
+
 }  // namespace
 
 extern "C" {
@@ -188,6 +248,23 @@ int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t 
 
 int mfl_zero_masked_rows(void* x, int64_t rows, int64_t row_bytes, const uint8_t* mask, void* stream) {
   return mfl_zero_masked_rows_batched(x, 1, rows, row_bytes, mask, stream);
+}
+
+int mfl_gather_keep_backward(const void* grad, const int64_t* index, const void* keep, int64_t n, int64_t B, int64_t K,
+                             int64_t d, void* grad_src, float* bias_part, void* stream) {
+  g_err[0] = 0;
+  if (n < 0 || B < 0 || K < 0 || d <= 0 || d % 8 || d > 512 || (n > 0 && (!grad || !index || !keep)) ||
+      (B > 0 && K > 0 && (!grad_src || !bias_part)) || ((uintptr_t)grad & 15u) || ((uintptr_t)grad_src & 15u) ||
+      n > (1 << 20) || B > (1 << 20)) {
+    snprintf(g_err, sizeof(g_err), "mfl_gather_keep_backward: bad arguments (d %% 8 == 0, d <= 512, 16-B aligned)");
+    return 1;
+  }
+  if (K == 0) return 0;
+  hipLaunchKernelGGL(gather_keep_bwd_kernel, dim3((unsigned)K), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint16_t*>(grad), reinterpret_cast<const long long*>(index),
+                     static_cast<const uint8_t*>(keep), (int)n, (int)B, (int)K, (int)d,
+                     static_cast<uint16_t*>(grad_src), bias_part);
+  return status("gather-keep backward");
 }
 
 const char* mfl_relu_dropout_last_error(void) { return g_err; }

@@ -144,6 +144,22 @@ class _GatherKeep(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         index, keep = ctx.saved_tensors
+        B, K, d = ctx.p_shape
+        if (g.is_cuda and g.dtype == torch.bfloat16 and ctx.dtypes[0] == torch.bfloat16 and d % 8 == 0 and d <= 512
+                and all(ctx.needs_input_grad[:2])):
+            # one HIP pass over g: each source row's sum over the segments that read it, and the
+            # bias's partial sums per token (csrc/ffn_glue.hip, gather_keep_bwd_kernel)
+            from .. import _native
+            lib = _native.load_library()
+            g = g.contiguous()
+            gP = torch.empty(ctx.p_shape, dtype=torch.bfloat16, device=g.device)
+            part = torch.empty(K, d, dtype=torch.float32, device=g.device)
+            rc = lib.mfl_gather_keep_backward(g.data_ptr(), index.contiguous().data_ptr(),
+                                              keep.contiguous().data_ptr(), g.shape[0], B, K, d, gP.data_ptr(),
+                                              part.data_ptr(), _native.stream_handle(g.device))
+            if rc != 0:
+                raise RuntimeError("mfl_gather_keep_backward failed: " + lib.mfl_relu_dropout_last_error().decode())
+            return gP, part.sum(0).to(ctx.dtypes[1]), None, None
         k = keep[..., None]
         acc = torch.promote_types(g.dtype, torch.float32)  # fp32, or fp64 for fp64 memories
         g32 = g.to(acc)

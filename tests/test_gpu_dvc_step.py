@@ -103,3 +103,27 @@ def test_staged_graph_replay_matches_eager_bf16(dev):
     assert abs(lg - le) <= 1e-3 * abs(le), (lg, le)
     spread = (fe2 - fe).norm() / fe.norm()
     assert (fg - fe).norm() / fe.norm() <= 2 * spread + 1e-2, ((fg - fe).norm().item(), spread.item())
+
+
+def test_segment_memory_gather_backward_kernel(dev):
+    """The segment memory's gather backward (csrc/ffn_glue.hip, mfl_gather_keep_backward) against
+    the fp64 sums: the source rows' gradient summed over the segments that read them where kept
+    (bf16, rounded once), the bias's over every position not kept."""
+    from importlib import import_module
+    pp = import_module(PKG.__name__ + ".utils.preds_postprocess")
+    g0 = torch.Generator().manual_seed(9)
+    B, K, d, n = 5, 240, 512, 17
+    P = torch.randn(B, K, d, generator=g0).to(dev, torch.bfloat16).requires_grad_(True)
+    bias = torch.randn(d, generator=g0).to(dev, torch.bfloat16).requires_grad_(True)
+    index = torch.randint(0, B, (n,), generator=g0).to(dev)
+    keep = (torch.rand(n, K, generator=g0) < 0.4).to(dev)
+    out = pp._GatherKeep.apply(P, bias, index, keep)
+    ref = torch.where(keep[..., None], P.detach()[index], bias.detach())
+    assert torch.equal(out, ref)
+    g = torch.randn(n, K, d, generator=g0).to(dev, torch.bfloat16)
+    out.backward(g)
+    g64, k = g.double(), keep[..., None]
+    gP = torch.zeros(B, K, d, dtype=torch.float64, device=dev).index_add_(0, index, torch.where(k, g64, 0.0))
+    gb = torch.where(k, 0.0, g64).sum((0, 1))
+    torch.testing.assert_close(P.grad.double(), gP, rtol=2 ** -8, atol=1e-6)
+    torch.testing.assert_close(bias.grad.double(), gb, rtol=2 ** -7, atol=1e-2)

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""The short-M HIP GEMM (models/modules/linear.py small_addmm) against torch.addmm (hipBLASLt) at
-the decoder / caption-decoder / audio shapes: HIP events over 50 calls, interleaved, median of 5."""
+"""The short-M HIP GEMM (models/modules/linear.py small_addmm / small_mm_nn) against torch.addmm /
+torch.mm (hipBLASLt) at the decoder / caption-decoder / audio shapes: device time per call from 50
+calls captured in a HIP graph, interleaved, median of 5."""
 import importlib
 import json
 import os
@@ -16,13 +17,23 @@ L = PKG.models.modules.linear
 
 
 def timed(fn, iters=50):
-    for _ in range(5):
-        fn()
+    """Device time per call: ``iters`` calls captured in one HIP graph and replayed (no host
+    launch overhead in the measurement, as in the training step's graphs)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            fn()
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(iters):
+            fn()
+    g.replay()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
-    for _ in range(iters):
-        fn()
+    g.replay()
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / iters * 1000
@@ -31,7 +42,8 @@ def timed(fn, iters=50):
 def main():
     dev = torch.device("cuda", 0)
     for M, N, K in [(800, 512, 512), (800, 256, 512), (800, 1024, 512), (800, 2048, 512), (800, 512, 2048),
-                    (532, 512, 512), (532, 10016, 512), (760, 512, 512), (760, 2048, 512)]:
+                    (800, 512, 1024), (532, 512, 512), (532, 2048, 512), (532, 512, 2048), (760, 512, 512),
+                    (760, 2048, 512), (100, 512, 512), (1024, 512, 512)]:
         x = torch.randn(M, K, device=dev).to(torch.bfloat16)
         w = torch.randn(N, K, device=dev).to(torch.bfloat16)
         b = torch.randn(N, device=dev).to(torch.bfloat16)
