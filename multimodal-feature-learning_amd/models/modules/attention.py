@@ -451,14 +451,18 @@ class CrossAttention(nn.Module):
         Lk = k.shape[1]
         H, hd = self.num_heads, self.head_dim
         q = self.q_linear(q).reshape(B, Lq, H, hd).transpose(1, 2)
-        if isinstance(k, SegmentMemory):  # the DVC's cropped memory: projections of the clips' rows, gathered
+        segments = isinstance(k, SegmentMemory)
+        if segments:  # the DVC's cropped memory: projections of the clips' rows, gathered
             k = k.project(self.k_linear).reshape(B, Lk, H, hd).transpose(1, 2)
             v = v.project(self.v_linear).reshape(B, Lk, H, hd).transpose(1, 2)
         else:
             k = self.k_linear(k).reshape(B, Lk, H, hd).transpose(1, 2)
             v = self.v_linear(v).reshape(B, Lk, H, hd).transpose(1, 2)
         masked = self._mask(attn_mask, key_padding_mask)
-        if need_weights:
+        # the explicit form (the reference's own, attention.py:288-299) also for the caption
+        # decoder's segment cross-attention: ~20 queries over ~2,000 keys, where the fused kernel's
+        # backward took 148 us a call against tens for two small batched GEMMs and a softmax
+        if need_weights or (segments and Lq <= 64):
             att = self.attention_dropout(masked_scores_softmax(q @ k.transpose(-2, -1), masked, self.scale))
             out = att @ v
         else:
