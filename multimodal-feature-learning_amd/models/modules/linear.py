@@ -149,7 +149,10 @@ def small_addmm(bias, x2, w):
     off."""
     M, K = x2.shape
     N = w.shape[0]
+    # (graph-timed against hipBLASLt, tools/small_gemm_ab.py: ahead for N, K <= 512 — 800 x 256 x 512
+    # 4.3 vs 5.4 us, 800 x 512 x 512 6.2 vs 6.5 — behind from N or K = 1024 on)
     if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 0 < M <= SMALL_GEMM_MAX_ROWS
+            and N <= 512 and K <= 512
             and N % 32 == 0 and K % 32 == 0 and x2.stride(1) == 1 and w.stride(1) == 1
             and x2.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and x2.stride(0) >= K and w.stride(0) >= K
             and (bias is None or (bias.dtype == torch.bfloat16 and bias.is_contiguous() and bias.numel() == N))
@@ -176,7 +179,9 @@ def small_mm_nn(g2, w):
     layer's input gradient — on the short-M HIP GEMM (mfl_gemm_nn_bf16); None where it does not apply."""
     M, N = g2.shape
     K = w.shape[1]
+    # (ahead of hipBLASLt for N, K <= 512: 800 x 512 x 512 5.4 vs 7.4 us; behind from 1024 on)
     if not (g2.is_cuda and g2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 0 < M <= SMALL_GEMM_MAX_ROWS
+            and N <= 512 and K <= 512
             and K % 32 == 0 and N % 32 == 0 and g2.stride(1) == 1 and w.stride(1) == 1
             and g2.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and g2.stride(0) >= N and w.stride(0) >= K
             and g2.data_ptr() % 16 == 0 and w.data_ptr() % 16 == 0):
