@@ -235,9 +235,9 @@ def roofline(summary, traffic):
     tr = traffic.get(name) if traffic else None
     gathered = d["gather_bytes_per_launch"]
     return {"bound": "hbm", "kernel": name,
-            "timing": "HIP events around each MSDA C-ABI call on its launch stream (forward: msda_fwd16_kernel; "
-                      "encoder backward: win_tiles_kernel + win_bwd_kernel, the row-block MFMA backward), "
-                      "eager steps after the timed region",
+            "timing": "HIP events around each MSDA C-ABI call on its launch stream (encoder forward: "
+                      "msda_fwd16_tiles_kernel, which also writes the backward's tile intervals; encoder "
+                      "backward: win_bwd_kernel, the row-block MFMA backward), eager steps after the timed region",
             "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": tr,
             "algorithmic_bytes_per_launch": d["bytes_per_launch"], "avg_launch_ms": round(d["avg_ms"], 5),

@@ -91,13 +91,16 @@ def main():
                 value, loc, aw, gout = make(regime, args.B, Lq, shapes, M, P, dtype, dev)
                 fwd_b = msda.algorithmic_bytes("fwd", args.B, S, M, D, Lq, L, P, vb)
                 bwd_b = msda.algorithmic_bytes("bwd", args.B, S, M, D, Lq, L, P, vb)
+                # as the training step runs them: the forward also writes the row-block backward's
+                # tile intervals where that backward runs, and the backward reads them
+                _, tiles = msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True)
                 runs = {
-                    "fwd": (lambda: msda.msda_forward(value, shapes, starts, loc, aw), fwd_b),
+                    "fwd": (lambda: msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True), fwd_b),
                     "bwd_loc_aw": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout,
                                                               need_value=False), None),
                     "bwd_value": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout,
                                                              need_loc=False, need_aw=False), None),
-                    "bwd_all": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout), bwd_b),
+                    "bwd_all": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout, tiles=tiles), bwd_b),
                 }
                 off = (torch.randn(args.B, Lq, M, L, P) * 2).to(dev, dtype)
                 logits = torch.randn(args.B, Lq, M, L * P).to(dev, dtype)

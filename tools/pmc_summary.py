@@ -49,8 +49,10 @@ def main(root):
 # bench.py's launch names -> the kernels of that C-ABI call at the encoder shape (B=8, T=1024
 # pyramid, bf16; tools/pmc_msda.sh runs the encoder shape only, so one grid per kernel)
 CALL_KERNELS = {
-    "msda_fwd_S1920_Lq1920": ("msda_fwd16_kernel",),
-    "msda_bwd_S1920_Lq1920": ("win_tiles_kernel", "win_bwd_kernel"),  # row-block MFMA backward (msda_win.hip)
+    # the forward writes the row-block backward's tile intervals (msda_fwd16_tiles_kernel); the
+    # backward is the row-block MFMA kernel alone (msda_win.hip)
+    "msda_fwd_S1920_Lq1920": ("msda_fwd16_tiles_kernel",),
+    "msda_bwd_S1920_Lq1920": ("win_bwd_kernel",),
 }
 
 
