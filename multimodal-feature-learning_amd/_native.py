@@ -60,6 +60,12 @@ EXPORTED_SYMBOLS = (
     "mfl_gemm_nt_bf16",
     "mfl_gemm_nn_bf16",
     "mfl_gemm_last_error",
+    # include/seg_attention.h
+    "mfl_seg_attention_forward",
+    "mfl_seg_attention_backward",
+    "mfl_seg_attention_bias_parts",
+    "mfl_seg_attention_workspace_bytes",
+    "mfl_seg_attention_last_error",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -129,6 +135,18 @@ def _declare(lib):
     lib.mfl_gemm_nn_bf16.restype = i32
     lib.mfl_gemm_nn_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
     lib.mfl_gemm_last_error.restype = ctypes.c_char_p
+    lib.mfl_seg_attention_forward.restype = i32
+    lib.mfl_seg_attention_forward.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, f32, vp,
+                                              vp, vp, vp]
+    lib.mfl_seg_attention_backward.restype = i32
+    lib.mfl_seg_attention_backward.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, f32, vp,
+                                               vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.mfl_seg_attention_bias_parts.restype = i64
+    lib.mfl_seg_attention_bias_parts.argtypes = [i64, i64]
+    lib.mfl_seg_attention_workspace_bytes.restype = i64
+    lib.mfl_seg_attention_workspace_bytes.argtypes = [i64, i64]
+    lib.mfl_seg_attention_last_error.restype = ctypes.c_char_p
+    lib.mfl_seg_attention_last_error.argtypes = []
     lib.mfl_relu_dropout_forward.restype = i32
     lib.mfl_relu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]
     lib.mfl_relu_dropout_backward.restype = i32

@@ -158,15 +158,24 @@ class UnimodalDeformableDVC(nn.Module):
             memory_list.append(mem)
             memory_mask_list.append(memory_mask)
             pred_memory_mask_list.append(pred_memory_mask)
-            if is_training:
-                captions = obj['cap_tensor'][:, :-1]
-                padding_mask = obj['cap_mask'][:, :-1]
-                tgt_mask = make_tgt_mask(captions, padding_mask)
-                cross_mask = pred_memory_mask if self.use_differentiable_mask else memory_mask
-                # only the last caption layer's word probabilities are read (:281): the head runs on it alone
-                output_caption = self.unimodal_caption_decoder(captions, mem, tgt_mask=tgt_mask, memory_mask=cross_mask,
-                                                               tgt_padding_mask=padding_mask, last_only=True)
-                outputs_captions.append(output_caption[-1])
+        if is_training:
+            # the reference decodes every level's segments in its own caption decoder call (:261-283);
+            # the calls are independent (same weights, per-segment rows), so they run as ONE call over
+            # the levels' segments stacked along the batch — six times the rows per GEMM, and each
+            # weight's gradient produced once instead of accumulated over the levels
+            captions = obj['cap_tensor'][:, :-1]
+            padding_mask = obj['cap_mask'][:, :-1]
+            tgt_mask = make_tgt_mask(captions, padding_mask)
+            cross = pred_memory_mask_list if self.use_differentiable_mask else memory_mask_list
+            counts = [m.shape[0] for m in memory_list]
+            reps = len(counts)
+            stacked = (SegmentMemory.cat(memory_list) if all(isinstance(m, SegmentMemory) for m in memory_list)
+                       else torch.cat(memory_list))
+            # only the last caption layer's word probabilities are read (:281): the head runs on it alone
+            output_caption = self.unimodal_caption_decoder(
+                captions.repeat(reps, 1), stacked, tgt_mask=tgt_mask.repeat(reps, 1, 1, 1),
+                memory_mask=torch.cat(cross), tgt_padding_mask=padding_mask.repeat(reps, 1), last_only=True)
+            outputs_captions = list(output_caption[-1].split(counts))
 
         mask_out = memory_mask_list[-1].squeeze().float() if self.use_differentiable_mask else None
         if is_training:

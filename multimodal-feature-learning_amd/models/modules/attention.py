@@ -27,6 +27,7 @@ from torch.nn.init import constant_, xavier_uniform_
 
 from ... import msda as _msda
 from ...utils.preds_postprocess import SegmentMemory
+from .seg_attention import segment_attention, segment_key_mask
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
 from .linear import Linear, _AutocastLinear, _addmm, _bias_grad, _defer, _mm_nn, _weight_grad, linear_pair
@@ -450,8 +451,15 @@ class CrossAttention(nn.Module):
         B, Lq, _ = q.shape
         Lk = k.shape[1]
         H, hd = self.num_heads, self.head_dim
-        q = self.q_linear(q).reshape(B, Lq, H, hd).transpose(1, 2)
         segments = isinstance(k, SegmentMemory)
+        key_mask = segment_key_mask(q, k, attn_mask, key_padding_mask, H) if segments and v is k else False
+        if key_mask is not False and not need_weights:
+            # the DVC caption decoder's cross-attention into the matched segments: HIP kernels that
+            # read each segment's projected rows in place (models/modules/seg_attention.py)
+            out = segment_attention(self.q_linear(q), k, v, self.k_linear, self.v_linear, key_mask, H, self.scale,
+                                    self.attention_dropout)
+            return self.projection_layer(out), None
+        q = self.q_linear(q).reshape(B, Lq, H, hd).transpose(1, 2)
         if segments:  # the DVC's cropped memory: projections of the clips' rows, gathered
             k = k.project(self.k_linear).reshape(B, Lk, H, hd).transpose(1, 2)
             v = v.project(self.v_linear).reshape(B, Lk, H, hd).transpose(1, 2)

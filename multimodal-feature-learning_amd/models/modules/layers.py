@@ -12,6 +12,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
+from .add_norm import add_layer_norm
 from .attention import CrossAttention, masked_scores_softmax
 from .linear import Linear
 
@@ -135,9 +136,17 @@ class UnimodalCaptionDecoderLayer(nn.Module):
             x = x + self._sa_block(self.layer_norm_1(x), tgt_mask, tgt_padding_mask)
             x = x + self._ca_block(self.layer_norm_2(x), memory, memory_mask, memory_padding_mask)
             return x + self.mlp(self.layer_norm_3(x))
-        x = self.layer_norm_1(x + self._sa_block(x, tgt_mask, tgt_padding_mask))
-        x = self.layer_norm_2(x + self._ca_block(x, memory, memory_mask, memory_padding_mask))
-        return self.layer_norm_3(x + self.mlp(x))
+        # post-norm: norm(x + dropout(branch)) as one fused kernel each way under autocast (the
+        # residual add of the fp32 stream and the 16-bit branch alone took ~60 us a call in ATen's
+        # mixed-dtype elementwise kernel); exactly the three modules' composition otherwise
+        x = add_layer_norm(x, self.self_attention(x, x, x, attn_mask=tgt_mask, key_padding_mask=tgt_padding_mask)[0],
+                           self.layer_norm_1, self.projection_dropout_1)
+        x = add_layer_norm(x, self.cross_attention(x, memory, memory, attn_mask=memory_mask,
+                                                   key_padding_mask=memory_padding_mask)[0],
+                           self.layer_norm_2, self.projection_dropout_2)
+        m = self.mlp
+        h = m.dropout_1(m.activation_layer(m.fully_connected_1(x)))
+        return add_layer_norm(x, m.fully_connected_2(h), self.layer_norm_3, m.dropout_2)
 
     def _sa_block(self, x, attn_mask, key_padding_mask):
         x = self.self_attention(x, x, x, attn_mask=attn_mask, key_padding_mask=key_padding_mask,

@@ -107,6 +107,15 @@ class SegmentMemory:
         return cls(memory, torch.arange(B, device=memory.device),
                    torch.ones(B, K, dtype=torch.bool, device=memory.device))
 
+    @staticmethod
+    def cat(memories):
+        """The segments of several crops of one source, stacked (torch.cat along the segments)."""
+        first = memories[0]
+        if any(m.source is not first.source for m in memories):
+            raise ValueError("SegmentMemory.cat: crops of different sources")
+        return SegmentMemory(first.source, torch.cat([m.index for m in memories]),
+                             torch.cat([m.keep for m in memories]), first.cache)
+
     def __getitem__(self, rows):
         if not isinstance(rows, torch.Tensor) or rows.dim() != 1:
             raise TypeError("SegmentMemory: only 1-D index tensors select segments")
@@ -119,13 +128,20 @@ class SegmentMemory:
     def materialize(self):
         return torch.where(self.keep[..., None], self.source[self.index], self.source.new_zeros(()))
 
-    def project(self, linear):
-        """``linear(self.materialize())`` from one projection of the source per step."""
+    def projected(self, linear):
+        """(``linear(source)`` — computed once per step and cached —, the bias a zeroed row projects
+        to, or None): what a kernel reading the crop in place needs (models/modules/seg_attention.py)."""
         P = self.cache.get(linear)
         if P is None:
             P = linear(self.source)
             self.cache[linear] = P
-        bias = linear.bias.to(P.dtype) if linear.bias is not None else P.new_zeros(P.shape[-1])
+        return P, (linear.bias.to(P.dtype) if linear.bias is not None else None)
+
+    def project(self, linear):
+        """``linear(self.materialize())`` from one projection of the source per step."""
+        P, bias = self.projected(linear)
+        if bias is None:
+            bias = P.new_zeros(P.shape[-1])
         return _GatherKeep.apply(P, bias, self.index, self.keep)
 
 

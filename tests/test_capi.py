@@ -10,7 +10,7 @@ import pytest
 from conftest import PKG, ROOT
 
 HEADERS = [os.path.join(ROOT, "include", h)
-           for h in ("msda_hip.h", "flat_adamw.h", "add_layernorm.h", "ffn_glue.h", "gemm_small.h")]
+           for h in ("msda_hip.h", "flat_adamw.h", "add_layernorm.h", "ffn_glue.h", "gemm_small.h", "seg_attention.h")]
 
 
 def declared_symbols():

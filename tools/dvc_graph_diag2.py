@@ -15,6 +15,13 @@ from conftest import PKG  # noqa: E402
 
 
 def main():
+    for flag in os.environ.get("DIAG_SEG", "1,0").split(","):
+        os.environ["MFL_SEG_ATTENTION"] = flag
+        print(f"== MFL_SEG_ATTENTION={flag}")
+        run()
+
+
+def run():
     model, obj = _small(torch.device("cuda", 0))
     tg = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.StagedDVCLoss(obj, model), lr=1e-4, use_bf16=True,
                                         graph=True)
@@ -40,16 +47,14 @@ def main():
     print(f"rel diff: replay-replay {rel(r1, r2):.4g} eager-eager {rel(e1, e2):.4g} replay-eager {rel(r1, e1):.4g}")
     names = {id(p): n for n, p in model.named_parameters()}
     groups = {}
-    off = 0
-    for p in tg.params:
-        k = p.numel()
-        g = names[id(p)].split(".")[0]
+    for i, p in enumerate(tg.params):
+        k, off = p.numel(), tg._offs[i]
+        g = ".".join(names[id(p)].split(".")[:3])
         a, b = r1[1][off:off + k], e1[1][off:off + k]
         d = groups.setdefault(g, [0.0, 0.0])
         d[0] += (a - b).norm().item() ** 2
         d[1] += b.norm().item() ** 2
-        off += k
-    for g, (dd, bb) in sorted(groups.items(), key=lambda kv: -kv[1][0]):
+    for g, (dd, bb) in sorted(groups.items(), key=lambda kv: -kv[1][0])[:12]:
         print(f"{g:40s} rel {(dd ** 0.5) / max(bb ** 0.5, 1e-12):.4g}  norm {bb ** 0.5:.4g}")
 
 
