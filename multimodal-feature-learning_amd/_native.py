@@ -142,7 +142,7 @@ def _declare(lib):
     lib.mfl_seg_attention_backward.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, f32, vp,
                                                vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mfl_seg_attention_bias_parts.restype = i64
-    lib.mfl_seg_attention_bias_parts.argtypes = [i64, i64]
+    lib.mfl_seg_attention_bias_parts.argtypes = [i64]
     lib.mfl_seg_attention_workspace_bytes.restype = i64
     lib.mfl_seg_attention_workspace_bytes.argtypes = [i64, i64]
     lib.mfl_seg_attention_last_error.restype = ctypes.c_char_p

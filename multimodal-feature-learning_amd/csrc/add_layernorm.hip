@@ -186,75 +186,49 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
   for (int c = 0; c < CH; ++c)
 #pragma unroll
     for (int k = 0; k < 4; ++k) dg[c][k] = db[c][k] = 0.f;
-  // the wave's rows: i = 0 .. RPB / kWaves - 1; the next row's inputs are loaded while the current
-  // one computes (one dependent HBM round trip a row otherwise: the loop was latency-bound)
-  struct RowIn {
-    float a[CH][4], b[CH][4], go[CH][4];
-    float mean, rstd;
-  };
-  auto load_row = [&](long long row, RowIn& in) {
-    const long long base = row * d;
-    in.mean = mean_in[row];
-    in.rstd = rstd_in[row];
-#pragma unroll
-    for (int c = 0; c < CH; ++c) {
-      const int col = c * 256 + lane * 4;
-      Vec4<RT>::load(r + base + col, in.a[c]);
-      Vec4<YT>::load(y + base + col, in.b[c]);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) in.go[c][k] = 0.f;
-      // d out = its fp32 gradient + the bf16 copy's + the (out + pos) copy's, summed in fp32
-      if (dout) Vec4<float>::load(dout + base + col, in.go[c]);
-      if (dout16) {
-        float t[4];
-        Vec4<uint16_t>::load(dout16 + base + col, t);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) in.go[c][k] += t[k];
-      }
-      if (dq16) {
-        float t[4];
-        Vec4<uint16_t>::load(dq16 + base + col, t);
-        if (dpos) Vec4<float>::store(dpos + base + col, t);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) in.go[c][k] += t[k];
-      }
-    }
-  };
-  constexpr int NR = RPB / kWaves;
-  const long long row0 = (long long)blockIdx.x * RPB + wave;
-  RowIn cur, nxt;
-  if (row0 < rows) load_row(row0, cur);
-  for (int i = 0; i < NR; ++i) {
-    const long long row = row0 + (long long)i * kWaves;
+  for (int i = 0; i < RPB / kWaves; ++i) {
+    const long long row = (long long)blockIdx.x * RPB + i * kWaves + wave;
     if (row >= rows) break;  // wave-uniform
-    const bool more = i + 1 < NR && row + kWaves < rows;
-    if (more) load_row(row + kWaves, nxt);
     const long long base = row * d;
-    const float mean = cur.mean, rstd = cur.rstd;
+    const float mean = mean_in[row], rstd = rstd_in[row];
     float xh[CH][4], g[CH][4], kp[CH][4];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int c = 0; c < CH; ++c) {
       const int col = c * 256 + lane * 4;
-      float b[4], ga[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) b[k] = cur.b[c][k];
+      float a[4], b[4], go[4] = {0.f, 0.f, 0.f, 0.f}, ga[4];
+      Vec4<RT>::load(r + base + col, a);
+      Vec4<YT>::load(y + base + col, b);
       if (drop.seed_ptr) {
         drop4<YT>(b, seed, thresh, drop.scale, base + col, kp[c]);
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) kp[c][k] = 1.f;
       }
+      // d out = its fp32 gradient + the bf16 copy's + the (out + pos) copy's, summed in fp32
+      if (dout) Vec4<float>::load(dout + base + col, go);
+      if (dout16) {
+        float t[4];
+        Vec4<uint16_t>::load(dout16 + base + col, t);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) go[k] += t[k];
+      }
+      if (dq16) {
+        float t[4];
+        Vec4<uint16_t>::load(dq16 + base + col, t);
+        if (dpos) Vec4<float>::store(dpos + base + col, t);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) go[k] += t[k];
+      }
       Vec4<float>::load(gamma + col, ga);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float go = cur.go[c][k];
-        xh[c][k] = (add_z<RT, YT>(cur.a[c][k], b[k]) - mean) * rstd;
-        g[c][k] = go * ga[k];
+        xh[c][k] = (add_z<RT, YT>(a[k], b[k]) - mean) * rstd;
+        g[c][k] = go[k] * ga[k];
         s1 += g[c][k];
         s2 += g[c][k] * xh[c][k];
-        dg[c][k] += go * xh[c][k];
-        db[c][k] += go;
+        dg[c][k] += go[k] * xh[c][k];
+        db[c][k] += go[k];
       }
     }
     const float m1 = wave_sum(s1) / (float)d, m2 = wave_sum(s2) / (float)d;
@@ -269,7 +243,6 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
       for (int k = 0; k < 4; ++k) dx[k] *= kp[c][k];
       Vec4<YT>::store(dy + base + col, dx);
     }
-    if (more) cur = nxt;
   }
   // gamma / beta partials of the block: waves meet in LDS, fixed order
   __shared__ float red[kWaves][2][CH * 256];

@@ -38,6 +38,8 @@ constexpr int KB = 32;       // keys per block
 constexpr int kWaves = 4;
 constexpr int kThreads = 64 * kWaves;
 constexpr int kRS = 144;     // LDS row stride (bytes): 64 bf16 + 16 B, 16-B aligned
+constexpr int kMaxBlk = 256;     // key blocks per segment held as LDS bit words: K <= 8192
+constexpr int kListChunk = 1024;  // segments scanned per pass of seg_attn_bwd_dkv's clip list
 constexpr float kNegInf = -INFINITY;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
@@ -78,18 +80,25 @@ __device__ __forceinline__ bf16x8 zero8() {
 }
 __device__ __forceinline__ bf16x8 load8(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// the attention-dropout keep bits (the same 64-bit mix as add_layernorm.hip's branch dropout)
-__device__ __forceinline__ uint32_t drop_bits(uint64_t seed, uint64_t e) {
-  uint64_t x = seed * 0x9E3779B97F4A7C15ull + e;
-  x ^= x >> 33;
-  x *= 0xff51afd7ed558ccdull;
-  x ^= x >> 33;
-  x *= 0xc4ceb9fe1a85ec53ull;
-  x ^= x >> 33;
-  return (uint32_t)x;
+// the attention-dropout keep bits: a 32-bit mix (murmur3's finaliser) of the element index and the
+// seed folded to 32 bits — a few full-rate integer ops per element (the scores of one block take 32
+// draws a lane); the index ((s * H + h) * Lq + i) * K + j fits 32 bits (checked on the host)
+__device__ __forceinline__ uint32_t drop_bits(uint32_t key, uint32_t e) {
+  uint32_t x = e * 0x9E3779B1u + key;
+  x ^= x >> 16;
+  x *= 0x85EBCA6Bu;
+  x ^= x >> 13;
+  x *= 0xC2B2AE35u;
+  x ^= x >> 16;
+  return x;
 }
-__device__ __forceinline__ float drop_mul(uint64_t seed, uint32_t thresh, float dscale, uint64_t e) {
-  return (drop_bits(seed, e) >> 8) >= thresh ? dscale : 0.f;
+__device__ __forceinline__ float drop_mul(uint32_t key, uint32_t thresh, float dscale, uint32_t e) {
+  return (drop_bits(key, e) >> 8) >= thresh ? dscale : 0.f;
+}
+__device__ __forceinline__ uint32_t drop_key(const int64_t* seed) {
+  if (!seed) return 0u;
+  const uint64_t v = (uint64_t)seed[0];
+  return (uint32_t)v ^ (uint32_t)(v >> 32);
 }
 
 // key / query kk (0..31) of a block -> its LDS row, so that rows 8g .. 8g+7 hold kk = 4g..4g+3 and
@@ -113,44 +122,32 @@ struct BlockMasks {
   uint32_t in, live, keep;  // bit kk: key j0+kk exists / is unmasked / reads the projected row
 };
 
-__device__ __forceinline__ BlockMasks block_masks(const Args& a, int s, int j0, int lane) {
-  const int j = j0 + (lane & 31);
-  const bool lo = lane < 32 && j < a.K;
-  const long long e = (long long)s * a.K + j;
-  BlockMasks m;
-  m.in = (uint32_t)__ballot(lo);
-  m.live = (uint32_t)__ballot(lo && (a.masked == nullptr || a.masked[e] == 0));
-  m.keep = (uint32_t)__ballot(lo && a.keep[e] != 0);
-  return m;
+__device__ __forceinline__ uint32_t in_mask(int j0, int K) {
+  return j0 + KB <= K ? 0xffffffffu : (j0 >= K ? 0u : (1u << (K - j0)) - 1u);
 }
 
-// whether segment s has any unmasked key (all threads of the block call it)
-__device__ __forceinline__ bool segment_dead(const Args& a, int s) {
+// the segment's unmasked / kept-row bits per 32-key block into LDS; returns whether every key is
+// masked (block-wide: the barrier also publishes the words)
+__device__ __forceinline__ bool segment_bits(const Args& a, int s, uint32_t* s_live, uint32_t* s_keep, int nblk,
+                                             int wave, int lane) {
   int any = 0;
-  if (a.masked == nullptr) {
-    any = 1;
-  } else {
-    for (int j = threadIdx.x; j < a.K; j += kThreads) any |= a.masked[(long long)s * a.K + j] == 0;
+  for (int blk = wave; blk < nblk; blk += kWaves) {
+    const int j = blk * KB + (lane & 31);
+    const bool lo = lane < 32 && j < a.K;
+    const long long e = (long long)s * a.K + j;
+    const uint32_t live = (uint32_t)__ballot(lo && (a.masked == nullptr || a.masked[e] == 0));
+    const uint32_t keep = (uint32_t)__ballot(lo && a.keep[e] != 0);
+    if (lane == 0) {
+      s_live[blk] = live;
+      s_keep[blk] = keep;
+    }
+    any |= live != 0u;
   }
   return !__syncthreads_or(any);
 }
 
-// 32 rows (keys kk of the block) x 64 head dims of the projected rows (or the bias) into LDS at perm_row
-__device__ __forceinline__ void stage_rows(unsigned char* tile, const uint16_t* base, const uint16_t* bias,
-                                           const BlockMasks& m, int d, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int c = lane + 64 * i, kk = c >> 3, part = c & 7;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if ((m.in >> kk) & 1u) {
-      const uint16_t* row = ((m.keep >> kk) & 1u) ? base + (long long)kk * d : bias;
-      if (row) v = *reinterpret_cast<const uint4*>(row + part * 8);
-    }
-    *reinterpret_cast<uint4*>(tile + perm_row(kk) * kRS + part * 16) = v;
-  }
-}
-
-// A-operand fragments of the block's rows (row kt*16 + li, head dims ks*32 + 8g ..)
+// fragments of the block's 32 rows (row kt*16 + li, head dims ks*32 + 8g ..): the A operand of a
+// product reducing over head dims, and, stored at perm_row, the LDS tile of a transposed B operand
 __device__ __forceinline__ void row_frags(bf16x8 (&f)[2][2], const uint16_t* base, const uint16_t* bias,
                                           const BlockMasks& m, int d, int g, int li) {
 #pragma unroll
@@ -163,15 +160,32 @@ __device__ __forceinline__ void row_frags(bf16x8 (&f)[2][2], const uint16_t* bas
   }
 }
 
-__global__ __launch_bounds__(kThreads) void seg_attn_fwd(Args a) {
+__device__ __forceinline__ void store_frags(unsigned char* tile, const bf16x8 (&f)[2][2], int g, int li) {
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      *reinterpret_cast<bf16x8*>(tile + perm_row(kt * 16 + li) * kRS + (ks * 32 + 8 * g) * 2) = f[kt][ks];
+}
+
+// the wave's next block at or after `from` (stride kWaves) with a non-zero weight on some key
+__device__ __forceinline__ int next_active(const uint32_t* s_live, int from, int nblk, bool dead) {
+  int bb = from;
+  while (bb < nblk && !dead && s_live[bb] == 0u) bb += kWaves;
+  return bb;
+}
+
+__global__ __launch_bounds__(kThreads, 2) void seg_attn_fwd(Args a) {
   __shared__ __attribute__((aligned(16))) unsigned char s_v[kWaves][KB * kRS];
   __shared__ float s_m[kWaves][QT], s_l[kWaves][QT];
   __shared__ float s_o[kWaves][QT][HD + 1];
+  __shared__ uint32_t s_live[kMaxBlk], s_keep[kMaxBlk];
   const int s = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int d = a.H * HD;
   const long long b = a.index[s];
-  const bool dead = segment_dead(a, s);
+  const int nblk = (a.K + KB - 1) / KB;
+  const bool dead = segment_bits(a, s, s_live, s_keep, nblk, wave, lane);
   bf16x8 qf[2][2];  // B operand of S^T = K Q^T: column = query qt*16 + li
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt) {
@@ -186,21 +200,26 @@ __global__ __launch_bounds__(kThreads) void seg_attn_fwd(Args a) {
   for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) o[qt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const uint64_t seed = a.seed ? (uint64_t)a.seed[0] : 0;
+  const uint32_t seed = drop_key(a.seed);
   const uint32_t thresh = (uint32_t)fminf(a.p * 16777216.f, 16777216.f);
   const float dscale = 1.f / (1.f - a.p);
   const uint16_t* bk = a.bk ? a.bk + h * HD : nullptr;
   const uint16_t* bv = a.bv ? a.bv + h * HD : nullptr;
   unsigned char* const sv = s_v[wave];
-  const int nblk = (a.K + KB - 1) / KB;
-  for (int blk = wave; blk < nblk; blk += kWaves) {
-    const int j0 = blk * KB;
-    const BlockMasks mk = block_masks(a, s, j0, lane);
-    if (!dead && mk.live == 0u) continue;  // wave-uniform: no weight on any key of the block
-    const long long rbase = (b * a.K + j0) * d + h * HD;
-    bf16x8 kf[2][2];
+  // software-pipelined over the wave's blocks: the next block's K / V rows load while this one computes
+  int blk = next_active(s_live, wave, nblk, dead);
+  bf16x8 kf[2][2], vf[2][2];
+  if (blk < nblk) {
+    const BlockMasks mk{in_mask(blk * KB, a.K), s_live[blk], s_keep[blk]};
+    const long long rbase = (b * a.K + blk * KB) * d + h * HD;
     row_frags(kf, a.pk + rbase, bk, mk, d, g, li);
-    stage_rows(sv, a.pv + rbase, bv, mk, d, lane);
+    row_frags(vf, a.pv + rbase, bv, mk, d, g, li);
+  }
+  while (blk < nblk) {
+    const int j0 = blk * KB;
+    const BlockMasks mk{in_mask(j0, a.K), s_live[blk], s_keep[blk]};
+    wave_lds_fence();
+    store_frags(sv, vf, g, li);
     float sc[2][2][4];  // [kt][qt][r]: key kt*16 + 4g + r, query qt*16 + li
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -216,6 +235,13 @@ __global__ __launch_bounds__(kThreads) void seg_attn_fwd(Args a) {
           sc[kt][qt][r] = !in ? kNegInf : dead ? 0.f : live ? t[r] * a.scale : kNegInf;
         }
       }
+    const int nb = next_active(s_live, blk + kWaves, nblk, dead);
+    if (nb < nblk) {
+      const BlockMasks mn{in_mask(nb * KB, a.K), s_live[nb], s_keep[nb]};
+      const long long rbase = (b * a.K + nb * KB) * d + h * HD;
+      row_frags(kf, a.pk + rbase, bk, mn, d, g, li);
+      row_frags(vf, a.pv + rbase, bv, mn, d, g, li);
+    }
     float alpha[2];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
@@ -253,7 +279,7 @@ __global__ __launch_bounds__(kThreads) void seg_attn_fwd(Args a) {
         for (int r = 0; r < 4; ++r) {
           float p = sc[kt][qt][r];
           if (a.seed) {
-            const uint64_t e = ((uint64_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kt * 16 + 4 * g + r);
+            const uint32_t e = ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kt * 16 + 4 * g + r);
             p *= drop_mul(seed, thresh, dscale, e);
           }
           pa[qt][kt * 4 + r] = tobf(p);
@@ -274,7 +300,7 @@ __global__ __launch_bounds__(kThreads) void seg_attn_fwd(Args a) {
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) o[qt][cb] = mfma(pa[qt], vb, o[qt][cb]);
     }
-    wave_lds_fence();
+    blk = nb;
   }
   if (g == 0) {
 #pragma unroll
@@ -321,16 +347,17 @@ __global__ __launch_bounds__(kThreads) void seg_attn_fwd(Args a) {
   }
 }
 
-__global__ __launch_bounds__(kThreads) void seg_attn_bwd_dq(Args a) {
+__global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   __shared__ __attribute__((aligned(16))) unsigned char s_k[kWaves][KB * kRS];
   __shared__ float s_dq[kWaves][QT][HD + 1];
   __shared__ float s_D[QT];
+  __shared__ uint32_t s_live[kMaxBlk], s_keep[kMaxBlk];
+  __shared__ float s_bias[kWaves][2][HD];
   const int s = blockIdx.x / a.H, h = blockIdx.x % a.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int d = a.H * HD;
   const long long b = a.index[s];
-  const bool dead = segment_dead(a, s);
-  if (h == 0 && tid == 0) a.dead[s] = dead ? 1 : 0;
+  const int nblk = (a.K + KB - 1) / KB;
   {  // D = rowsum(dO * O) of the head: 8 threads a query
     const int qi = tid >> 3, c0 = (tid & 7) * 8;
     float acc = 0.f;
@@ -351,7 +378,8 @@ __global__ __launch_bounds__(kThreads) void seg_attn_bwd_dq(Args a) {
       a.D[((long long)s * a.H + h) * QT + qi] = acc;
     }
   }
-  __syncthreads();
+  const bool dead = segment_bits(a, s, s_live, s_keep, nblk, wave, lane);  // (its barrier publishes s_D)
+  if (h == 0 && tid == 0) a.dead[s] = dead ? 1 : 0;
   bf16x8 qf[2][2], df[2][2];  // B operands: column = query qt*16 + li
   float lse[2], Dq[2];
 #pragma unroll
@@ -371,42 +399,87 @@ __global__ __launch_bounds__(kThreads) void seg_attn_bwd_dq(Args a) {
   for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) dq[qt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const uint64_t seed = a.seed ? (uint64_t)a.seed[0] : 0;
+  // per query, over the keys that read the bias row (keep = 0) with a non-zero weight: the sums of
+  // dS and of P' — the bias gradients are sum_q cS[q] Q[q] and sum_q cA[q] dO[q]
+  float cS[2] = {0.f, 0.f}, cA[2] = {0.f, 0.f};
+  const uint32_t seed = drop_key(a.seed);
   const uint32_t thresh = (uint32_t)fminf(a.p * 16777216.f, 16777216.f);
   const float dscale = 1.f / (1.f - a.p);
   const uint16_t* bk = a.bk ? a.bk + h * HD : nullptr;
   const uint16_t* bv = a.bv ? a.bv + h * HD : nullptr;
   unsigned char* const sk = s_k[wave];
-  const int nblk = (a.K + KB - 1) / KB;
+  if (dead) {  // uniform weights exp(-lse) on every key; only the bias rows' P' sums are needed
+    for (int bb = wave; bb < nblk; bb += kWaves) {
+      const uint32_t zr = in_mask(bb * KB, a.K) & ~s_keep[bb];
+      if (zr == 0u) continue;
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int qi = qt * 16 + li;
+        const float p = __expf(-lse[qt]);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int kk = kt * 16 + 4 * g + r;
+            if (!((zr >> kk) & 1u)) continue;
+            cA[qt] += a.seed ? p * drop_mul(seed, thresh, dscale, ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K +
+                                                                      (bb * KB + kk))
+                             : p;
+          }
+      }
+    }
+  }
   // a segment with every key masked has constant scores: no gradient reaches q (nor k)
-  for (int blk = wave; !dead && blk < nblk; blk += kWaves) {
-    const int j0 = blk * KB;
-    const BlockMasks mk = block_masks(a, s, j0, lane);
-    if (mk.live == 0u) continue;
-    const long long rbase = (b * a.K + j0) * d + h * HD;
-    bf16x8 kf[2][2], vf[2][2];
+  int blk = dead ? nblk : next_active(s_live, wave, nblk, false);
+  bf16x8 kf[2][2], vf[2][2];
+  if (blk < nblk) {
+    const BlockMasks mk{in_mask(blk * KB, a.K), s_live[blk], s_keep[blk]};
+    const long long rbase = (b * a.K + blk * KB) * d + h * HD;
     row_frags(kf, a.pk + rbase, bk, mk, d, g, li);
     row_frags(vf, a.pv + rbase, bv, mk, d, g, li);
-    stage_rows(sk, a.pk + rbase, bk, mk, d, lane);
+  }
+  while (blk < nblk) {
+    const int j0 = blk * KB;
+    const BlockMasks mk{in_mask(j0, a.K), s_live[blk], s_keep[blk]};
+    wave_lds_fence();
+    store_frags(sk, kf, g, li);
+    f32x4 st[2][2], dp[2][2];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        st[kt][qt] = dp[kt][qt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        st[kt][qt] = mfma(kf[kt][0], qf[qt][0], st[kt][qt]);
+        st[kt][qt] = mfma(kf[kt][1], qf[qt][1], st[kt][qt]);
+        dp[kt][qt] = mfma(vf[kt][0], df[qt][0], dp[kt][qt]);
+        dp[kt][qt] = mfma(vf[kt][1], df[qt][1], dp[kt][qt]);
+      }
+    const int nb = next_active(s_live, blk + kWaves, nblk, false);
+    if (nb < nblk) {
+      const BlockMasks mn{in_mask(nb * KB, a.K), s_live[nb], s_keep[nb]};
+      const long long rbase = (b * a.K + nb * KB) * d + h * HD;
+      row_frags(kf, a.pk + rbase, bk, mn, d, g, li);
+      row_frags(vf, a.pv + rbase, bv, mn, d, g, li);
+    }
     bf16x8 da[2];  // A operand of dQ += dS K: row = query qt*16 + li, k slots = keys 4g.. | 16+4g..
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
-        f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-        st = mfma(kf[kt][0], qf[qt][0], st);
-        st = mfma(kf[kt][1], qf[qt][1], st);
-        dp = mfma(vf[kt][0], df[qt][0], dp);
-        dp = mfma(vf[kt][1], df[qt][1], dp);
         const int qi = qt * 16 + li;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int kk = kt * 16 + 4 * g + r;
           const bool live = (mk.live >> kk) & 1u;
-          const float p = live ? __expf(st[r] * a.scale - lse[qt]) : 0.f;
-          float dpv = dp[r];
-          if (a.seed) dpv *= drop_mul(seed, thresh, dscale, ((uint64_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk));
-          da[qt][kt * 4 + r] = tobf(p * (dpv - Dq[qt]) * a.scale);
+          const float p = live ? __expf(st[kt][qt][r] * a.scale - lse[qt]) : 0.f;
+          const float dm =
+              a.seed ? drop_mul(seed, thresh, dscale, ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk)) : 1.f;
+          const float ds = p * (dp[kt][qt][r] * dm - Dq[qt]) * a.scale;
+          da[qt][kt * 4 + r] = tobf(ds);
+          if (!((mk.keep >> kk) & 1u)) {
+            cS[qt] += ds;
+            cA[qt] += p * dm;
+          }
         }
       }
     wave_lds_fence();
@@ -416,7 +489,7 @@ __global__ __launch_bounds__(kThreads) void seg_attn_bwd_dq(Args a) {
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) dq[qt][cb] = mfma(da[qt], kb, dq[qt][cb]);
     }
-    wave_lds_fence();
+    blk = nb;
   }
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
@@ -424,7 +497,41 @@ __global__ __launch_bounds__(kThreads) void seg_attn_bwd_dq(Args a) {
     for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
       for (int r = 0; r < 4; ++r) s_dq[wave][qt * 16 + 4 * g + r][cb * 16 + li] = dq[qt][cb][r];
+  {  // the wave's bias partials: sum over its queries of cS Q / cA dO (head dims ks*32 + 8g + j)
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      cS[qt] += __shfl_xor(cS[qt], 16);
+      cS[qt] += __shfl_xor(cS[qt], 32);
+      cA[qt] += __shfl_xor(cA[qt], 16);
+      cA[qt] += __shfl_xor(cA[qt], 32);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float vk = 0.f, vv = 0.f;
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
+          vk += cS[qt] * (float)qf[qt][ks][j];
+          vv += cA[qt] * (float)df[qt][ks][j];
+        }
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          vk += __shfl_xor(vk, o);
+          vv += __shfl_xor(vv, o);
+        }
+        if (li == 0) {
+          s_bias[wave][0][ks * 32 + 8 * g + j] = vk;
+          s_bias[wave][1][ks * 32 + 8 * g + j] = vv;
+        }
+      }
+  }
   __syncthreads();
+  if (tid < 2 * HD) {  // (H, n, 2, 64) partials: this (segment, head)'s
+    const int kv = tid >> 6, c = tid & 63;
+    a.dbias[(((long long)h * a.n + s) * 2 + kv) * HD + c] =
+        s_bias[0][kv][c] + s_bias[1][kv][c] + s_bias[2][kv][c] + s_bias[3][kv][c];
+  }
   const int qi = tid >> 3, c0 = (tid & 7) * 8;
   if (qi < a.Lq) {
     uint16_t v[8];
@@ -444,10 +551,42 @@ __global__ __launch_bounds__(kThreads) void seg_attn_bwd_dq(Args a) {
   }
 }
 
-__global__ __launch_bounds__(kThreads) void seg_attn_bwd_dkv(Args a, int nkg) {
+// one segment's operands of seg_attn_bwd_dkv, loaded a segment ahead
+struct SegPrefetch {
+  uint4 q, dout;      // the thread's 16 B of Q / dO (query tid >> 3, part tid & 7)
+  float lse, D;       // query tid & 31
+  int dead;
+  uint32_t mb, kb;    // key j0 + (lane & 31): masked / kept bytes
+};
+
+__device__ __forceinline__ void load_segment(const Args& a, int s, int h, int d, int j0, bool on, int tid, int lane,
+                                             SegPrefetch& p) {
+  const int qi = tid >> 3, part = tid & 7;
+  p.q = p.dout = make_uint4(0u, 0u, 0u, 0u);
+  if (qi < a.Lq) {
+    const long long off = ((long long)s * a.Lq + qi) * d + h * HD + part * 8;
+    p.q = *reinterpret_cast<const uint4*>(a.q + off);
+    p.dout = *reinterpret_cast<const uint4*>(a.dout + off);
+  }
+  p.lse = a.lse[((long long)s * a.H + h) * QT + (tid & 31)];
+  p.D = a.D[((long long)s * a.H + h) * QT + (tid & 31)];
+  p.dead = a.dead[s];
+  const int j = j0 + (lane & 31);
+  p.mb = 1u;
+  p.kb = 0u;
+  if (on && lane < 32 && j < a.K) {
+    const long long e = (long long)s * a.K + j;
+    p.mb = a.masked ? a.masked[e] : 0u;
+    p.kb = a.keep[e];
+  }
+}
+
+__global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg) {
   __shared__ __attribute__((aligned(16))) unsigned char s_q[QT * kRS];
   __shared__ __attribute__((aligned(16))) unsigned char s_do[QT * kRS];
   __shared__ float s_lse[QT], s_D[QT];
+  __shared__ int s_list[kListChunk];
+  __shared__ int s_wcnt[kWaves];
   int bid = blockIdx.x;
   const int kgrp = bid % nkg;
   bid /= nkg;
@@ -458,9 +597,11 @@ __global__ __launch_bounds__(kThreads) void seg_attn_bwd_dkv(Args a, int nkg) {
   const int blk = kgrp * kWaves + wave;
   const bool on = blk < nblk;  // wave-uniform
   const int j0 = blk * KB;
+  const uint32_t inm = on ? in_mask(j0, a.K) : 0u;
   const long long rbase = ((long long)b * a.K + j0) * d + h * HD;
-  // B operands of S = Q K^T and dP = dO V^T: column = key kt*16 + li; the projected rows and the bias
-  bf16x8 kP[2][2], vP[2][2], kZ[2], vZ[2];
+  // B operands of S = Q K^T and dP = dO V^T: column = key kt*16 + li (the projected rows; keys a
+  // segment reads as the bias row get no contribution here — seg_attn_bwd_dq sums those)
+  bf16x8 kP[2][2], vP[2][2];
 #pragma unroll
   for (int kt = 0; kt < 2; ++kt) {
     const bool ok = on && j0 + kt * 16 + li < a.K;
@@ -471,98 +612,100 @@ __global__ __launch_bounds__(kThreads) void seg_attn_bwd_dkv(Args a, int nkg) {
       vP[kt][ks] = ok ? load8(a.pv + off) : zero8();
     }
   }
+  f32x4 dk[2][4], dv[2][4];
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    kZ[ks] = a.bk ? load8(a.bk + h * HD + ks * 32 + 8 * g) : zero8();
-    vZ[ks] = a.bv ? load8(a.bv + h * HD + ks * 32 + 8 * g) : zero8();
-  }
-  f32x4 dk[2][4], dv[2][4], zk[4], zv[4];
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    zk[cb] = zv[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int cb = 0; cb < 4; ++cb)
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) dk[kt][cb] = dv[kt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  const uint64_t seed = a.seed ? (uint64_t)a.seed[0] : 0;
+  const uint32_t seed = drop_key(a.seed);
   const uint32_t thresh = (uint32_t)fminf(a.p * 16777216.f, 16777216.f);
   const float dscale = 1.f / (1.f - a.p);
-  for (int s = 0; s < a.n; ++s) {
-    if (a.index[s] != b) continue;  // block-uniform
-    __syncthreads();                // the previous segment's LDS reads are done
-    {
-      const int qi = tid >> 3, part = tid & 7;
-      uint4 xq = make_uint4(0u, 0u, 0u, 0u), xd = xq;
-      if (qi < a.Lq) {
-        const long long off = ((long long)s * a.Lq + qi) * d + h * HD + part * 8;
-        xq = *reinterpret_cast<const uint4*>(a.q + off);
-        xd = *reinterpret_cast<const uint4*>(a.dout + off);
-      }
-      *reinterpret_cast<uint4*>(s_q + perm_row(qi) * kRS + part * 16) = xq;
-      *reinterpret_cast<uint4*>(s_do + perm_row(qi) * kRS + part * 16) = xd;
-      if (tid < QT) {
-        s_lse[tid] = a.lse[((long long)s * a.H + h) * QT + tid];
-        s_D[tid] = a.D[((long long)s * a.H + h) * QT + tid];
-      }
+  for (int c0 = 0; c0 < a.n; c0 += kListChunk) {
+    // the segments of this chunk that read clip b, in order (4 candidates a thread, block prefix sum)
+    int flags = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int s = c0 + tid * 4 + i;
+      if (s < a.n && a.index[s] == b) flags |= 1 << i;
     }
-    const bool dead = a.dead[s] != 0;
+    const int cnt = __popc(flags);
+    int x = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o);
+      if (lane >= o) x += y;
+    }
+    __syncthreads();  // the previous chunk's list reads are done
+    if (lane == 63) s_wcnt[wave] = x;
     __syncthreads();
-    if (!on) continue;
-    const BlockMasks mk = block_masks(a, s, j0, lane);
-    const uint32_t wts = dead ? mk.in : mk.live;  // keys with a non-zero weight
-    if (wts == 0u) continue;
-    const bool zrows = (wts & ~mk.keep) != 0u;  // some weighted key reads the bias row
-    bf16x8 kf[2][2], vf[2][2];
+    int pos = x - cnt;
+    for (int w = 0; w < wave; ++w) pos += s_wcnt[w];
 #pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const bool kp = (mk.keep >> (kt * 16 + li)) & 1u;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        kf[kt][ks] = kp ? kP[kt][ks] : kZ[ks];
-        vf[kt][ks] = kp ? vP[kt][ks] : vZ[ks];
+    for (int i = 0; i < 4; ++i)
+      if ((flags >> i) & 1) s_list[pos++] = c0 + tid * 4 + i;
+    const int total = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
+    __syncthreads();
+    SegPrefetch pf;
+    if (total > 0) load_segment(a, s_list[0], h, d, j0, on, tid, lane, pf);
+    for (int it = 0; it < total; ++it) {
+      const int s = s_list[it];
+      __syncthreads();  // the previous segment's LDS reads are done
+      *reinterpret_cast<uint4*>(s_q + perm_row(tid >> 3) * kRS + (tid & 7) * 16) = pf.q;
+      *reinterpret_cast<uint4*>(s_do + perm_row(tid >> 3) * kRS + (tid & 7) * 16) = pf.dout;
+      if (tid < QT) {
+        s_lse[tid] = pf.lse;
+        s_D[tid] = pf.D;
       }
-    }
-    bf16x8 aa[2], sa[2];  // A operands (row = key kt*16 + li, k slots = queries 4g.. | 16+4g..): P', dS
+      const bool dead = pf.dead != 0;
+      const bool lo = lane < 32;
+      BlockMasks mk;
+      mk.in = inm;
+      mk.live = (uint32_t)__ballot(lo && pf.mb == 0u) & inm;
+      mk.keep = (uint32_t)__ballot(lo && pf.kb != 0u) & inm;
+      __syncthreads();
+      if (it + 1 < total) load_segment(a, s_list[it + 1], h, d, j0, on, tid, lane, pf);  // in flight meanwhile
+      if (!on) continue;
+      const uint32_t wts = (dead ? mk.in : mk.live) & mk.keep;  // kept keys with a non-zero weight
+      if (wts == 0u) continue;
+      bf16x8 aa[2], sa[2];  // A operands (row = key kt*16 + li, k slots = queries 4g.. | 16+4g..): P', dS
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
-      bf16x8 qa[2], oa[2];
+      for (int qt = 0; qt < 2; ++qt) {
+        bf16x8 qa[2], oa[2];
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int row = perm_row(qt * 16 + li);
-        qa[ks] = *reinterpret_cast<const bf16x8*>(s_q + row * kRS + (ks * 32 + 8 * g) * 2);
-        oa[ks] = *reinterpret_cast<const bf16x8*>(s_do + row * kRS + (ks * 32 + 8 * g) * 2);
-      }
+        for (int ks = 0; ks < 2; ++ks) {
+          const int row = perm_row(qt * 16 + li);
+          qa[ks] = *reinterpret_cast<const bf16x8*>(s_q + row * kRS + (ks * 32 + 8 * g) * 2);
+          oa[ks] = *reinterpret_cast<const bf16x8*>(s_do + row * kRS + (ks * 32 + 8 * g) * 2);
+        }
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-        st = mfma(qa[0], kf[kt][0], st);
-        st = mfma(qa[1], kf[kt][1], st);
-        dp = mfma(oa[0], vf[kt][0], dp);
-        dp = mfma(oa[1], vf[kt][1], dp);
-        const int kk = kt * 16 + li;
-        const bool w = (wts >> kk) & 1u;
+        for (int kt = 0; kt < 2; ++kt) {
+          f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+          st = mfma(qa[0], kP[kt][0], st);
+          st = mfma(qa[1], kP[kt][1], st);
+          dp = mfma(oa[0], vP[kt][0], dp);
+          dp = mfma(oa[1], vP[kt][1], dp);
+          const int kk = kt * 16 + li;
+          const bool w = (wts >> kk) & 1u;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int qi = qt * 16 + 4 * g + r;
-          const float p = !w ? 0.f : __expf((dead ? 0.f : st[r] * a.scale) - s_lse[qi]);
-          const float dm = a.seed ? drop_mul(seed, thresh, dscale, ((uint64_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk))
-                                  : 1.f;
-          aa[kt][qt * 4 + r] = tobf(p * dm);
-          sa[kt][qt * 4 + r] = tobf(dead ? 0.f : p * (dp[r] * dm - s_D[qi]) * a.scale);
+          for (int r = 0; r < 4; ++r) {
+            const int qi = qt * 16 + 4 * g + r;
+            const float p = !w ? 0.f : __expf((dead ? 0.f : st[r] * a.scale) - s_lse[qi]);
+            const float dm = a.seed ? drop_mul(seed, thresh, dscale,
+                                               ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk))
+                                    : 1.f;
+            aa[kt][qt * 4 + r] = tobf(p * dm);
+            sa[kt][qt * 4 + r] = tobf(dead ? 0.f : p * (dp[r] * dm - s_D[qi]) * a.scale);
+          }
         }
       }
-    }
-    wave_lds_fence();
+      wave_lds_fence();
 #pragma unroll
-    for (int cb = 0; cb < 4; ++cb) {
-      const bf16x8 ob = tr_b(s_do, g, li, cb), qb = tr_b(s_q, g, li, cb);
+      for (int cb = 0; cb < 4; ++cb) {
+        const bf16x8 ob = tr_b(s_do, g, li, cb), qb = tr_b(s_q, g, li, cb);
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const bool kp = (mk.keep >> (kt * 16 + li)) & 1u;
-        dv[kt][cb] = mfma(kp ? aa[kt] : zero8(), ob, dv[kt][cb]);
-        dk[kt][cb] = mfma(kp ? sa[kt] : zero8(), qb, dk[kt][cb]);
-        if (zrows) {
-          zv[cb] = mfma(kp ? zero8() : aa[kt], ob, zv[cb]);
-          zk[cb] = mfma(kp ? zero8() : sa[kt], qb, zk[cb]);
+        for (int kt = 0; kt < 2; ++kt) {
+          dv[kt][cb] = mfma(aa[kt], ob, dv[kt][cb]);
+          dk[kt][cb] = mfma(sa[kt], qb, dk[kt][cb]);
         }
       }
     }
@@ -582,23 +725,6 @@ __global__ __launch_bounds__(kThreads) void seg_attn_bwd_dkv(Args a, int nkg) {
         }
       }
   }
-  // bias partial sums of the wave: column sums of zk / zv (rows = keys)
-  const long long P = (long long)a.B * nkg * kWaves;
-  const long long part = ((long long)b * nkg + kgrp) * kWaves + wave;
-#pragma unroll
-  for (int cb = 0; cb < 4; ++cb) {
-    float sk = zk[cb][0] + zk[cb][1] + zk[cb][2] + zk[cb][3];
-    float sv = zv[cb][0] + zv[cb][1] + zv[cb][2] + zv[cb][3];
-    sk += __shfl_xor(sk, 16);
-    sk += __shfl_xor(sk, 32);
-    sv += __shfl_xor(sv, 16);
-    sv += __shfl_xor(sv, 32);
-    if (g == 0) {
-      float* dst = a.dbias + (((long long)h * P + part) * 2) * HD + cb * 16 + li;
-      dst[0] = sk;
-      dst[HD] = sv;
-    }
-  }
 }
 
 int fail(const char* msg) {
@@ -611,6 +737,8 @@ bool aligned16(const void* p) { return p == nullptr || (reinterpret_cast<uintptr
 int check(const Args& a) {
   if (a.n < 0 || a.B <= 0 || a.K <= 0 || a.H <= 0) return fail("seg_attention: bad sizes");
   if (a.Lq < 1 || a.Lq > QT) return fail("seg_attention: Lq must be in [1, 32]");
+  if (a.K > kMaxBlk * KB) return fail("seg_attention: K must be <= 8192");
+  if ((double)a.n * a.H * a.Lq * a.K >= 4294967296.0) return fail("seg_attention: n * H * Lq * K must be < 2^32");
   if (!(a.p >= 0.f && a.p < 1.f)) return fail("seg_attention: p_drop must be in [0, 1)");
   if (!a.q || !a.pk || !a.pv || !a.index || !a.keep || !a.lse) return fail("seg_attention: null pointer");
   if (!aligned16(a.q) || !aligned16(a.pk) || !aligned16(a.pv) || !aligned16(a.bk) || !aligned16(a.bv))
@@ -647,10 +775,7 @@ int mfl_seg_attention_forward(const void* q, const void* pk, const void* pv, con
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }
 
-int64_t mfl_seg_attention_bias_parts(int64_t B, int64_t K) {
-  const int64_t nblk = (K + KB - 1) / KB;
-  return B * ((nblk + kWaves - 1) / kWaves) * kWaves;
-}
+int64_t mfl_seg_attention_bias_parts(int64_t n) { return n; }
 
 int64_t mfl_seg_attention_workspace_bytes(int64_t n, int64_t H) { return n * H * QT * 4 + ((n * 4 + 15) / 16) * 16; }
 

@@ -16,17 +16,16 @@ pytestmark = pytest.mark.gpu
 
 def _drop_keep(seed, n, H, Lq, K, p):
     """The kernels' keep bits (seg_attention.hip drop_bits) for element ((s*H + h)*Lq + i)*K + j."""
+    key = np.uint32((seed & 0xffffffff) ^ (seed >> 32))
     with np.errstate(over="ignore"):
-        e = np.arange(n * H * Lq * K, dtype=np.uint64)
-        x = np.uint64(seed) * np.uint64(0x9E3779B97F4A7C15) + e
-        x ^= x >> np.uint64(33)
-        x *= np.uint64(0xff51afd7ed558ccd)
-        x ^= x >> np.uint64(33)
-        x *= np.uint64(0xc4ceb9fe1a85ec53)
-        x ^= x >> np.uint64(33)
-    bits = (x & np.uint64(0xffffffff)).astype(np.uint32) >> np.uint32(8)
+        x = np.arange(n * H * Lq * K, dtype=np.uint32) * np.uint32(0x9E3779B1) + key
+        x ^= x >> np.uint32(16)
+        x *= np.uint32(0x85EBCA6B)
+        x ^= x >> np.uint32(13)
+        x *= np.uint32(0xC2B2AE35)
+        x ^= x >> np.uint32(16)
     thresh = np.uint32(min(p * 16777216.0, 16777216.0))
-    return torch.from_numpy((bits >= thresh).reshape(n, H, Lq, K))
+    return torch.from_numpy(((x >> np.uint32(8)) >= thresh).reshape(n, H, Lq, K))
 
 
 def _reference(q, pk, pv, bk, bv, index, keep, masked, H, scale, drop=None, p=0.0):
