@@ -551,40 +551,47 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   }
 }
 
-// one segment's operands of seg_attn_bwd_dkv, loaded a segment ahead
+// one segment's operands of seg_attn_bwd_dkv, loaded a segment ahead by each wave: the wave's Q /
+// dO rows as fragments (row qt*16 + li, head dims ks*32 + 8g ..), lse / D of query lane & 31, the
+// masked / kept bytes of key j0 + (lane & 31), the dead flag
 struct SegPrefetch {
-  uint4 q, dout;      // the thread's 16 B of Q / dO (query tid >> 3, part tid & 7)
-  float lse, D;       // query tid & 31
+  bf16x8 q[2][2], o[2][2];
+  float lse, D;
+  uint32_t mb, kb;
   int dead;
-  uint32_t mb, kb;    // key j0 + (lane & 31): masked / kept bytes
 };
 
-__device__ __forceinline__ void load_segment(const Args& a, int s, int h, int d, int j0, bool on, int tid, int lane,
+__device__ __forceinline__ void load_segment(const Args& a, int s, int h, int d, int j0, int g, int li, int lane,
                                              SegPrefetch& p) {
-  const int qi = tid >> 3, part = tid & 7;
-  p.q = p.dout = make_uint4(0u, 0u, 0u, 0u);
-  if (qi < a.Lq) {
-    const long long off = ((long long)s * a.Lq + qi) * d + h * HD + part * 8;
-    p.q = *reinterpret_cast<const uint4*>(a.q + off);
-    p.dout = *reinterpret_cast<const uint4*>(a.dout + off);
+#pragma unroll
+  for (int qt = 0; qt < 2; ++qt) {
+    const int qi = qt * 16 + li;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const long long off = ((long long)s * a.Lq + qi) * d + h * HD + ks * 32 + 8 * g;
+      p.q[qt][ks] = qi < a.Lq ? load8(a.q + off) : zero8();
+      p.o[qt][ks] = qi < a.Lq ? load8(a.dout + off) : zero8();
+    }
   }
-  p.lse = a.lse[((long long)s * a.H + h) * QT + (tid & 31)];
-  p.D = a.D[((long long)s * a.H + h) * QT + (tid & 31)];
+  p.lse = a.lse[((long long)s * a.H + h) * QT + (lane & 31)];
+  p.D = a.D[((long long)s * a.H + h) * QT + (lane & 31)];
   p.dead = a.dead[s];
   const int j = j0 + (lane & 31);
   p.mb = 1u;
   p.kb = 0u;
-  if (on && lane < 32 && j < a.K) {
+  if (lane < 32 && j < a.K) {
     const long long e = (long long)s * a.K + j;
     p.mb = a.masked ? a.masked[e] : 0u;
     p.kb = a.keep[e];
   }
 }
 
+// waves run independently over the clip's segment list (no block barriers): each stages its own
+// copy of a segment's Q / dO rows in LDS and prefetches the next segment's while it computes
 __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg) {
-  __shared__ __attribute__((aligned(16))) unsigned char s_q[QT * kRS];
-  __shared__ __attribute__((aligned(16))) unsigned char s_do[QT * kRS];
-  __shared__ float s_lse[QT], s_D[QT];
+  __shared__ __attribute__((aligned(16))) unsigned char s_q[kWaves][QT * kRS];
+  __shared__ __attribute__((aligned(16))) unsigned char s_do[kWaves][QT * kRS];
+  __shared__ float s_lse[kWaves][QT], s_D[kWaves][QT];
   __shared__ int s_list[kListChunk];
   __shared__ int s_wcnt[kWaves];
   int bid = blockIdx.x;
@@ -599,6 +606,8 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg)
   const int j0 = blk * KB;
   const uint32_t inm = on ? in_mask(j0, a.K) : 0u;
   const long long rbase = ((long long)b * a.K + j0) * d + h * HD;
+  unsigned char* const sq = s_q[wave];
+  unsigned char* const sd = s_do[wave];
   // B operands of S = Q K^T and dP = dO V^T: column = key kt*16 + li (the projected rows; keys a
   // segment reads as the bias row get no contribution here — seg_attn_bwd_dq sums those)
   bf16x8 kP[2][2], vP[2][2];
@@ -645,28 +654,26 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg)
       if ((flags >> i) & 1) s_list[pos++] = c0 + tid * 4 + i;
     const int total = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
     __syncthreads();
+    if (!on) continue;  // (the barriers above are the last ones of the chunk)
     SegPrefetch pf;
-    if (total > 0) load_segment(a, s_list[0], h, d, j0, on, tid, lane, pf);
+    if (total > 0) load_segment(a, s_list[0], h, d, j0, g, li, lane, pf);
     for (int it = 0; it < total; ++it) {
       const int s = s_list[it];
-      __syncthreads();  // the previous segment's LDS reads are done
-      *reinterpret_cast<uint4*>(s_q + perm_row(tid >> 3) * kRS + (tid & 7) * 16) = pf.q;
-      *reinterpret_cast<uint4*>(s_do + perm_row(tid >> 3) * kRS + (tid & 7) * 16) = pf.dout;
-      if (tid < QT) {
-        s_lse[tid] = pf.lse;
-        s_D[tid] = pf.D;
+      wave_lds_fence();  // the previous segment's LDS reads are issued before these writes
+      store_frags(sq, pf.q, g, li);
+      store_frags(sd, pf.o, g, li);
+      if (lane < QT) {
+        s_lse[wave][lane] = pf.lse;
+        s_D[wave][lane] = pf.D;
       }
       const bool dead = pf.dead != 0;
       const bool lo = lane < 32;
-      BlockMasks mk;
-      mk.in = inm;
-      mk.live = (uint32_t)__ballot(lo && pf.mb == 0u) & inm;
-      mk.keep = (uint32_t)__ballot(lo && pf.kb != 0u) & inm;
-      __syncthreads();
-      if (it + 1 < total) load_segment(a, s_list[it + 1], h, d, j0, on, tid, lane, pf);  // in flight meanwhile
-      if (!on) continue;
-      const uint32_t wts = (dead ? mk.in : mk.live) & mk.keep;  // kept keys with a non-zero weight
+      const uint32_t live = (uint32_t)__ballot(lo && pf.mb == 0u) & inm;
+      const uint32_t keep = (uint32_t)__ballot(lo && pf.kb != 0u) & inm;
+      if (it + 1 < total) load_segment(a, s_list[it + 1], h, d, j0, g, li, lane, pf);  // in flight meanwhile
+      const uint32_t wts = (dead ? inm : live) & keep;  // kept keys with a non-zero weight
       if (wts == 0u) continue;
+      wave_lds_fence();
       bf16x8 aa[2], sa[2];  // A operands (row = key kt*16 + li, k slots = queries 4g.. | 16+4g..): P', dS
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
@@ -674,8 +681,8 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const int row = perm_row(qt * 16 + li);
-          qa[ks] = *reinterpret_cast<const bf16x8*>(s_q + row * kRS + (ks * 32 + 8 * g) * 2);
-          oa[ks] = *reinterpret_cast<const bf16x8*>(s_do + row * kRS + (ks * 32 + 8 * g) * 2);
+          qa[ks] = *reinterpret_cast<const bf16x8*>(sq + row * kRS + (ks * 32 + 8 * g) * 2);
+          oa[ks] = *reinterpret_cast<const bf16x8*>(sd + row * kRS + (ks * 32 + 8 * g) * 2);
         }
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
@@ -689,19 +696,18 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int qi = qt * 16 + 4 * g + r;
-            const float p = !w ? 0.f : __expf((dead ? 0.f : st[r] * a.scale) - s_lse[qi]);
+            const float p = !w ? 0.f : __expf((dead ? 0.f : st[r] * a.scale) - s_lse[wave][qi]);
             const float dm = a.seed ? drop_mul(seed, thresh, dscale,
                                                ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk))
                                     : 1.f;
             aa[kt][qt * 4 + r] = tobf(p * dm);
-            sa[kt][qt * 4 + r] = tobf(dead ? 0.f : p * (dp[r] * dm - s_D[qi]) * a.scale);
+            sa[kt][qt * 4 + r] = tobf(dead ? 0.f : p * (dp[r] * dm - s_D[wave][qi]) * a.scale);
           }
         }
       }
-      wave_lds_fence();
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        const bf16x8 ob = tr_b(s_do, g, li, cb), qb = tr_b(s_q, g, li, cb);
+        const bf16x8 ob = tr_b(sd, g, li, cb), qb = tr_b(sq, g, li, cb);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           dv[kt][cb] = mfma(aa[kt], ob, dv[kt][cb]);
