@@ -136,11 +136,11 @@ def _declare(lib):
     lib.mfl_gemm_nn_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
     lib.mfl_gemm_last_error.restype = ctypes.c_char_p
     lib.mfl_seg_attention_forward.restype = i32
-    lib.mfl_seg_attention_forward.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, f32, vp,
-                                              vp, vp, vp]
+    lib.mfl_seg_attention_forward.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, f32,
+                                              vp, vp, vp, vp]
     lib.mfl_seg_attention_backward.restype = i32
-    lib.mfl_seg_attention_backward.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, f32, vp,
-                                               vp, vp, vp, vp, vp, vp, vp, vp, vp]
+    lib.mfl_seg_attention_backward.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32, f32,
+                                               vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]
     lib.mfl_seg_attention_bias_parts.restype = i64
     lib.mfl_seg_attention_bias_parts.argtypes = [i64]
     lib.mfl_seg_attention_workspace_bytes.restype = i64

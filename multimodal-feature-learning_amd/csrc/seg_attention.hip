@@ -52,6 +52,7 @@ thread_local char g_err[256] = "";
 struct Args {
   const uint16_t *q, *pk, *pv, *bk, *bv;
   const int64_t* index;
+  const int32_t* order;  // segments in dispatch order (sorted by clip: the clip's rows stay in L2), or null
   const uint8_t *keep, *masked;
   int n, B, K, Lq, H;
   float scale, p;
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_fwd(Args a) {
   __shared__ float s_m[kWaves][QT], s_l[kWaves][QT];
   __shared__ float s_o[kWaves][QT][HD + 1];
   __shared__ uint32_t s_live[kMaxBlk], s_keep[kMaxBlk];
-  const int s = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int s = a.order ? a.order[blockIdx.x / a.H] : (int)(blockIdx.x / a.H), h = blockIdx.x % a.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int d = a.H * HD;
   const long long b = a.index[s];
@@ -353,7 +354,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   __shared__ float s_D[QT];
   __shared__ uint32_t s_live[kMaxBlk], s_keep[kMaxBlk];
   __shared__ float s_bias[kWaves][2][HD];
-  const int s = blockIdx.x / a.H, h = blockIdx.x % a.H;
+  const int s = a.order ? a.order[blockIdx.x / a.H] : (int)(blockIdx.x / a.H), h = blockIdx.x % a.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int d = a.H * HD;
   const long long b = a.index[s];
@@ -586,28 +587,32 @@ __device__ __forceinline__ void load_segment(const Args& a, int s, int h, int d,
   }
 }
 
-// waves run independently over the clip's segment list (no block barriers): each stages its own
-// copy of a segment's Q / dO rows in LDS and prefetches the next segment's while it computes
-__global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg) {
-  __shared__ __attribute__((aligned(16))) unsigned char s_q[kWaves][QT * kRS];
-  __shared__ __attribute__((aligned(16))) unsigned char s_do[kWaves][QT * kRS];
+// one workgroup per (clip, head, 32-key block); its 4 waves take the clip's segments round-robin
+// (the DVC's composed crops send most segments to a few clips: a wave per block walked all of a heavy
+// clip's segments alone) without block barriers — each stages its own copy of a segment's Q / dO
+// rows in LDS and prefetches its next segment's while it computes — and add their partial dK / dV
+// through LDS at the end
+__global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
+  constexpr int kStage = 2 * QT * kRS;                  // a wave's Q + dO rows
+  constexpr int kPart = 2 * 2 * 4 * 64 * 16;            // a wave's dK + dV tiles (f32x4 a lane)
+  constexpr int kUnion = (kWaves - 1) * kPart > kWaves * kStage ? (kWaves - 1) * kPart : kWaves * kStage;
+  __shared__ __attribute__((aligned(16))) unsigned char s_buf[kUnion];
   __shared__ float s_lse[kWaves][QT], s_D[kWaves][QT];
   __shared__ int s_list[kListChunk];
   __shared__ int s_wcnt[kWaves];
+  const int nblk = (a.K + KB - 1) / KB;
   int bid = blockIdx.x;
-  const int kgrp = bid % nkg;
-  bid /= nkg;
+  const int blk = bid % nblk;
+  bid /= nblk;
   const int h = bid % a.H, b = bid / a.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
   const int d = a.H * HD;
-  const int nblk = (a.K + KB - 1) / KB;
-  const int blk = kgrp * kWaves + wave;
-  const bool on = blk < nblk;  // wave-uniform
+  const bool on = true;
   const int j0 = blk * KB;
-  const uint32_t inm = on ? in_mask(j0, a.K) : 0u;
+  const uint32_t inm = in_mask(j0, a.K);
   const long long rbase = ((long long)b * a.K + j0) * d + h * HD;
-  unsigned char* const sq = s_q[wave];
-  unsigned char* const sd = s_do[wave];
+  unsigned char* const sq = s_buf + wave * kStage;
+  unsigned char* const sd = sq + QT * kRS;
   // B operands of S = Q K^T and dP = dO V^T: column = key kt*16 + li (the projected rows; keys a
   // segment reads as the bias row get no contribution here — seg_attn_bwd_dq sums those)
   bf16x8 kP[2][2], vP[2][2];
@@ -654,10 +659,9 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg)
       if ((flags >> i) & 1) s_list[pos++] = c0 + tid * 4 + i;
     const int total = s_wcnt[0] + s_wcnt[1] + s_wcnt[2] + s_wcnt[3];
     __syncthreads();
-    if (!on) continue;  // (the barriers above are the last ones of the chunk)
     SegPrefetch pf;
-    if (total > 0) load_segment(a, s_list[0], h, d, j0, g, li, lane, pf);
-    for (int it = 0; it < total; ++it) {
+    if (wave < total) load_segment(a, s_list[wave], h, d, j0, g, li, lane, pf);
+    for (int it = wave; it < total; it += kWaves) {
       const int s = s_list[it];
       wave_lds_fence();  // the previous segment's LDS reads are issued before these writes
       store_frags(sq, pf.q, g, li);
@@ -670,7 +674,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg)
       const bool lo = lane < 32;
       const uint32_t live = (uint32_t)__ballot(lo && pf.mb == 0u) & inm;
       const uint32_t keep = (uint32_t)__ballot(lo && pf.kb != 0u) & inm;
-      if (it + 1 < total) load_segment(a, s_list[it + 1], h, d, j0, g, li, lane, pf);  // in flight meanwhile
+      if (it + kWaves < total) load_segment(a, s_list[it + kWaves], h, d, j0, g, li, lane, pf);  // in flight meanwhile
       const uint32_t wts = (dead ? inm : live) & keep;  // kept keys with a non-zero weight
       if (wts == 0u) continue;
       wave_lds_fence();
@@ -716,7 +720,28 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a, int nkg)
       }
     }
   }
-  if (on) {
+  __syncthreads();  // every wave is done with its staging rows (the buffer becomes the partials)
+  f32x4* const part = reinterpret_cast<f32x4*>(s_buf);
+  if (wave > 0) {
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        part[(((wave - 1) * 2 + 0) * 8 + kt * 4 + cb) * 64 + lane] = dk[kt][cb];
+        part[(((wave - 1) * 2 + 1) * 8 + kt * 4 + cb) * 64 + lane] = dv[kt][cb];
+      }
+  }
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int w = 1; w < kWaves; ++w)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          dk[kt][cb] += part[(((w - 1) * 2 + 0) * 8 + kt * 4 + cb) * 64 + lane];
+          dv[kt][cb] += part[(((w - 1) * 2 + 1) * 8 + kt * 4 + cb) * 64 + lane];
+        }
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -757,7 +782,8 @@ int check(const Args& a) {
 extern "C" {
 
 int mfl_seg_attention_forward(const void* q, const void* pk, const void* pv, const void* bias_k, const void* bias_v,
-                              const int64_t* index, const uint8_t* keep, const uint8_t* masked, int64_t n, int64_t B,
+                              const int64_t* index, const int32_t* order, const uint8_t* keep, const uint8_t* masked,
+                              int64_t n, int64_t B,
                               int64_t K, int64_t Lq, int64_t H, float scale, float p_drop, const int64_t* seed,
                               void* out, float* lse, void* stream) {
   Args a{};
@@ -767,6 +793,7 @@ int mfl_seg_attention_forward(const void* q, const void* pk, const void* pv, con
   a.bk = static_cast<const uint16_t*>(bias_k);
   a.bv = static_cast<const uint16_t*>(bias_v);
   a.index = index;
+  a.order = order;
   a.keep = keep;
   a.masked = masked;
   a.n = (int)n, a.B = (int)B, a.K = (int)K, a.Lq = (int)Lq, a.H = (int)H;
@@ -786,7 +813,8 @@ int64_t mfl_seg_attention_bias_parts(int64_t n) { return n; }
 int64_t mfl_seg_attention_workspace_bytes(int64_t n, int64_t H) { return n * H * QT * 4 + ((n * 4 + 15) / 16) * 16; }
 
 int mfl_seg_attention_backward(const void* q, const void* pk, const void* pv, const void* bias_k, const void* bias_v,
-                               const int64_t* index, const uint8_t* keep, const uint8_t* masked, int64_t n, int64_t B,
+                               const int64_t* index, const int32_t* order, const uint8_t* keep, const uint8_t* masked,
+                              int64_t n, int64_t B,
                                int64_t K, int64_t Lq, int64_t H, float scale, float p_drop, const int64_t* seed,
                                const void* out, const float* lse, const void* dout, void* dq, void* dpk, void* dpv,
                                float* dbias_part, void* workspace, void* stream) {
@@ -797,6 +825,7 @@ int mfl_seg_attention_backward(const void* q, const void* pk, const void* pv, co
   a.bk = static_cast<const uint16_t*>(bias_k);
   a.bv = static_cast<const uint16_t*>(bias_v);
   a.index = index;
+  a.order = order;
   a.keep = keep;
   a.masked = masked;
   a.n = (int)n, a.B = (int)B, a.K = (int)K, a.Lq = (int)Lq, a.H = (int)H;
@@ -816,8 +845,8 @@ int mfl_seg_attention_backward(const void* q, const void* pk, const void* pv, co
     return fail("seg_attention: operands must be 16-byte aligned");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (n > 0) hipLaunchKernelGGL(seg_attn_bwd_dq, dim3((unsigned)(n * H)), dim3(kThreads), 0, st, a);
-  const int nblk = (int)((K + KB - 1) / KB), nkg = (nblk + kWaves - 1) / kWaves;
-  hipLaunchKernelGGL(seg_attn_bwd_dkv, dim3((unsigned)(B * H * nkg)), dim3(kThreads), 0, st, a, nkg);
+  const int nblk = (int)((K + KB - 1) / KB);
+  hipLaunchKernelGGL(seg_attn_bwd_dkv, dim3((unsigned)(B * H * nblk)), dim3(kThreads), 0, st, a);
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

@@ -14,5 +14,5 @@ run bench_fp32 400 python3 -u bench.py --steps 10 --warmup 3 --dtype fp32 --cpu-
 run bench_multimodal 400 python3 -u bench.py --steps 10 --warmup 3 --config multimodal --cpu-baseline 0
 run bench_T4096 400 python3 -u bench.py --steps 10 --warmup 3 --T 4096 --cpu-baseline 0
 run bench_sparse 400 python3 -u bench.py --steps 5 --warmup 2 --config sparse --cpu-baseline 0
-run bench_dvc 400 python3 -u bench.py --steps 5 --warmup 2 --config dvc --cpu-baseline 0
+run bench_dvc 400 python3 -u bench.py --steps 20 --warmup 3 --config dvc --cpu-baseline 0
 run gemm_census 300 python3 -u tools/gemm_census.py gpurun_out/gemm_census.csv

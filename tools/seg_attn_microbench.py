@@ -40,8 +40,9 @@ def make(n=168, B=8, K=1920, Lq=19, H=8, skew=False, windows=False, seed=0):
     return q, pk, pv, bk, bv, index.to(dev), keep.to(dev), (~live).to(dev)
 
 
-def run(name, p, **kw):
+def run(name, p, sort=True, **kw):
     q, pk, pv, bk, bv, index, keep, masked = make(**kw)
+    order = torch.argsort(index, stable=True).to(torch.int32) if sort else None
     leaves = [t.clone().requires_grad_(True) for t in (q, pk, pv, bk, bv)]
     seed = torch.tensor([12345], dtype=torch.int64, device=q.device) if p > 0 else None
     gout = torch.randn_like(q)
@@ -49,7 +50,7 @@ def run(name, p, **kw):
     for i in range(6):
         if i == 2:
             start.record()
-        out = SA._SegmentAttention.apply(*leaves, index, keep, masked, 8, 0.125, p, seed)
+        out = SA._SegmentAttention.apply(*leaves, index, keep, masked, 8, 0.125, p, seed, order)
         out.backward(gout)
     end.record()
     torch.cuda.synchronize()
@@ -57,6 +58,7 @@ def run(name, p, **kw):
 
 
 def main():
+    run("uniform, all live, p=0, unsorted", 0.0, sort=False)
     run("uniform, all live, p=0", 0.0)
     run("uniform, all live, p=0.1", 0.1)
     run("skewed, all live, p=0.1", 0.1, skew=True)
