@@ -375,12 +375,19 @@ class StagedDVCLoss:
         return state['costs']
 
     def host(self, state, cpu):
-        from .utils.preds_postprocess import get_src_permutation_idx
+        """get_src_permutation_idx (utils/preds_postprocess.py) of every level, written with numpy
+        into the pinned buffer: (clip, prediction) pairs ordered by target within each clip."""
+        import numpy as np
         self.level_indices = self._matcher.solve_levels(cpu, state['cost_meta'])
+        ih = self.idx_host.numpy()
         for lvl, ind in enumerate(self.level_indices):
-            b, s = get_src_permutation_idx(ind)
-            self.idx_host[lvl, 0].copy_(b)
-            self.idx_host[lvl, 1].copy_(s)
+            off = 0
+            for b, (src, tgt) in enumerate(ind):
+                s, t = src.numpy(), tgt.numpy()
+                k = len(s)
+                ih[lvl, 0, off:off + k] = b
+                ih[lvl, 1, off:off + k] = s[np.argsort(t, kind="stable")]
+                off += k
 
     def upload(self):
         self.idx_dev.copy_(self.idx_host, non_blocking=True)

@@ -5,6 +5,7 @@ scipy's ``linear_sum_assignment`` on the host, as in the reference.  The referen
 device->host copy per call (``.cpu()`` :86) plus two syncing asserts (utils/box_ops.py:59-60), once
 per decoder level; ``match_levels`` builds every level's cost matrix and the well-formedness flags
 on the device and moves them in ONE copy."""
+import numpy as np
 import torch
 from scipy.optimize import linear_sum_assignment
 from torch import nn
@@ -61,19 +62,24 @@ class HungarianMatcher(nn.Module):
     @staticmethod
     def solve_levels(host, meta):
         """The host half: the reference's syncing asserts (utils/box_ops.py:59-60) and scipy's
-        linear_sum_assignment per clip and level (reference :86-94)."""
+        linear_sum_assignment per clip and level (reference :86-94), on numpy views of the one
+        copied buffer (the per-clip torch indexing and conversions were most of the host step)."""
         shapes, sizes, n_tgt, n_flags = meta
-        ok = host[-n_flags:]
+        h = host.numpy() if isinstance(host, torch.Tensor) else np.asarray(host)
+        ok = h[-n_flags:]
         assert bool(ok[:-1].all()), "Segment start > Segment end (from output)"
         assert bool(ok[-1]), "Segment start > Segment end (from target)"
+        bounds = np.cumsum([0] + list(sizes))
         result, off = [], 0
         for B, Q in shapes:
             n = B * Q * n_tgt
-            cost = host[off:off + n].view(B, Q, -1)
+            cost = h[off:off + n].reshape(B, Q, n_tgt)
             off += n
-            result.append([
-                (torch.as_tensor(i, dtype=torch.int64), torch.as_tensor(j, dtype=torch.int64))
-                for i, j in (linear_sum_assignment(c[b]) for b, c in enumerate(cost.split(sizes, -1)))])
+            level = []
+            for b in range(B):
+                i, j = linear_sum_assignment(cost[b, :, bounds[b]:bounds[b + 1]])
+                level.append((torch.from_numpy(i.astype(np.int64)), torch.from_numpy(j.astype(np.int64))))
+            result.append(level)
         return result
 
 

@@ -189,3 +189,31 @@ def test_mha_self_attention_matches_module():
     gb = torch.autograd.grad(ref, [tgt] + list(mha.parameters()), g)
     for a, b in zip(ga, gb):
         torch.testing.assert_close(a, b, rtol=1e-10, atol=1e-10)
+
+
+def test_segment_memory_crops_compose_and_stack():
+    """SegmentMemory (utils/preds_postprocess.py): a crop of a crop is the materialised crop of the
+    materialised crop (reference unimodal_deformable_dvc.py:235 rebinds the memory), the
+    projection of a crop is the projection of its materialisation (kept rows: the source row's
+    projection; zeroed rows: the bias), and ``cat`` stacks crops of one source along the segments."""
+    import torch
+    from conftest import PKG
+    SM = PKG.utils.preds_postprocess.SegmentMemory
+    g = torch.Generator().manual_seed(4)
+    B, K, d = 3, 40, 16
+    src = torch.randn(B, K, d, generator=g, dtype=torch.float64)
+    m0 = SM.of(src)
+    bid1 = torch.tensor([0, 2, 2, 1])
+    keep1 = torch.rand(4, K, generator=g) < 0.6
+    m1 = m0.select(bid1, keep1)
+    ref1 = torch.where(keep1[..., None], src[bid1], 0.0)
+    assert torch.equal(m1.materialize(), ref1)
+    bid2 = torch.tensor([1, 0, 3, 3, 2])
+    keep2 = torch.rand(5, K, generator=g) < 0.7
+    m2 = m1.select(bid2, keep2)
+    assert torch.equal(m2.materialize(), torch.where(keep2[..., None], ref1[bid2], 0.0))
+    lin = torch.nn.Linear(d, d).double()
+    assert torch.allclose(m2.project(lin), lin(m2.materialize()), rtol=0, atol=1e-12)
+    both = SM.cat([m1, m2])
+    assert torch.equal(both.materialize(), torch.cat([m1.materialize(), m2.materialize()]))
+    assert both.cache is m1.cache
