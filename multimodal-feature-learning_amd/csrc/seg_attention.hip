@@ -176,10 +176,16 @@ __device__ __forceinline__ int next_active(const uint32_t* s_live, int from, int
   return bb;
 }
 
-__global__ __launch_bounds__(kThreads, 2) void seg_attn_fwd(Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned char s_v[kWaves][KB * kRS];
+// the waves' staging tiles (block loop) and their partial O (final combine) share one LDS buffer:
+// 36 KB a workgroup, so LDS admits 4 workgroups per CU and the VGPRs 3
+constexpr int kStageBytes = kWaves * KB * kRS;
+constexpr int kPartBytes = kWaves * QT * (HD + 1) * 4;
+constexpr int kRawBytes = kStageBytes > kPartBytes ? kStageBytes : kPartBytes;
+
+__global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned char s_raw[kRawBytes];
   __shared__ float s_m[kWaves][QT], s_l[kWaves][QT];
-  __shared__ float s_o[kWaves][QT][HD + 1];
+  float(*const s_o)[QT][HD + 1] = reinterpret_cast<float(*)[QT][HD + 1]>(s_raw);
   __shared__ uint32_t s_live[kMaxBlk], s_keep[kMaxBlk];
   const int s = a.order ? a.order[blockIdx.x / a.H] : (int)(blockIdx.x / a.H), h = blockIdx.x % a.H;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
@@ -206,7 +212,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_fwd(Args a) {
   const float dscale = 1.f / (1.f - a.p);
   const uint16_t* bk = a.bk ? a.bk + h * HD : nullptr;
   const uint16_t* bv = a.bv ? a.bv + h * HD : nullptr;
-  unsigned char* const sv = s_v[wave];
+  unsigned char* const sv = s_raw + wave * KB * kRS;
   // software-pipelined over the wave's blocks: the next block's K / V rows load while this one computes
   int blk = next_active(s_live, wave, nblk, dead);
   bf16x8 kf[2][2], vf[2][2];
@@ -310,6 +316,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_fwd(Args a) {
       s_l[wave][qt * 16 + li] = l[qt];
     }
   }
+  __syncthreads();  // every wave is done with its staging tile (the buffer becomes the partial O)
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
@@ -349,8 +356,8 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_fwd(Args a) {
 }
 
 __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned char s_k[kWaves][KB * kRS];
-  __shared__ float s_dq[kWaves][QT][HD + 1];
+  __shared__ __attribute__((aligned(16))) unsigned char s_raw[kRawBytes];  // staging tiles, then partial dQ
+  float(*const s_dq)[QT][HD + 1] = reinterpret_cast<float(*)[QT][HD + 1]>(s_raw);
   __shared__ float s_D[QT];
   __shared__ uint32_t s_live[kMaxBlk], s_keep[kMaxBlk];
   __shared__ float s_bias[kWaves][2][HD];
@@ -408,7 +415,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   const float dscale = 1.f / (1.f - a.p);
   const uint16_t* bk = a.bk ? a.bk + h * HD : nullptr;
   const uint16_t* bv = a.bv ? a.bv + h * HD : nullptr;
-  unsigned char* const sk = s_k[wave];
+  unsigned char* const sk = s_raw + wave * KB * kRS;
   if (dead) {  // uniform weights exp(-lse) on every key; only the bias rows' P' sums are needed
     for (int bb = wave; bb < nblk; bb += kWaves) {
       const uint32_t zr = in_mask(bb * KB, a.K) & ~s_keep[bb];
@@ -492,6 +499,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
     }
     blk = nb;
   }
+  __syncthreads();  // every wave is done with its staging tile (the buffer becomes the partial dQ)
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
