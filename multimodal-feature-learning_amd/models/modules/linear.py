@@ -231,13 +231,15 @@ _dest = None  # flat_grad_destinations: {"views": {id(param): flat view}, "claim
 
 
 @contextlib.contextmanager
-def flat_grad_destinations(views):
+def flat_grad_destinations(views, may_claim=None):
     """Inside (the trainer's backward): the first gradient produced for a parameter in ``views``
     ({id(param): its fp32 view of the flat gradient buffer}) is written straight into that view,
     which autograd then hands to the parameter as its .grad — instead of a fresh tensor copied
-    into the flat buffer afterwards (one 171 MB copy pass per step at the bench shape)."""
+    into the flat buffer afterwards (one 171 MB copy pass per step at the bench shape).
+    ``may_claim(param)``, when given, vetoes a view at the time it would be handed out (the
+    trainer refuses the views of gradient buckets it has already all-reduced or is reducing)."""
     global _dest
-    prev, _dest = _dest, {"views": views, "claimed": set()}
+    prev, _dest = _dest, {"views": views, "claimed": set(), "may_claim": may_claim}
     try:
         yield
     finally:
@@ -253,6 +255,8 @@ def _claim(param):
         return None
     v = d["views"].get(id(param))
     if v is None or id(param) in d["claimed"]:
+        return None
+    if d["may_claim"] is not None and not d["may_claim"](param):
         return None
     d["claimed"].add(id(param))
     return v.view_as(v)  # a fresh view object: autograd adopts it as .grad instead of cloning

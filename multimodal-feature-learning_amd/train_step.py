@@ -186,6 +186,8 @@ class FlatGradTrainer:
         self._frozen = None       # (views of their values / moments / shadow, scratch copies)
         self._frozen_keep = []    # earlier scratch sets, alive while a captured graph may read them
         self._late = False
+        self._late_parts = {}       # param index -> local gradient that arrived after its bucket's reduce
+        self._late_global = False   # some rank had a late gradient on the last eager step
         self._bucket_of = {}
         for bi, (_, _, idx) in enumerate(self.buckets):
             for i in idx:
@@ -224,17 +226,27 @@ class FlatGradTrainer:
         def hook(p):
             if self._pending is None:  # backward outside _forward_backward (user code): nothing to do
                 return
-            if self._got[i]:
-                # a second gradient for i this step (a deferred weight gradient delivered beside an
-                # autograd one): its bucket may be reduced already, so reduce everything again
-                self._late = True
+            if p.grad is None:
+                # autograd runs the hook for an input whose backward returned no gradient (a deferred
+                # weight gradient, delivered later by _deliver): nothing arrived yet
                 return
-            self._got[i] = True
+            if not self._overlap_now:  # every bucket is copied once after the backward
+                self._got[i] = True
+                return
             b = self._bucket_of[i]
-            if i in self._known_unused or b < self._next_flush:
-                # a parameter found unused got a gradient (its bucket may be reduced already):
-                # after the backward the whole buffer is reduced again (_forward_backward)
-                self._late = True
+            if b < self._next_flush:
+                # a gradient for a parameter whose bucket is reduced already (one found unused last
+                # step): kept aside and reduced after the backward (_find_unused).  It is a local
+                # tensor: the reduced bucket's views are never handed out (_may_claim)
+                if p.grad.data_ptr() == self.grad_views[i].data_ptr():
+                    raise RuntimeError("FlatGradTrainer: a reduced bucket's gradient view was written")
+                self._late_add(i, p.grad)
+                return
+            first = not self._got[i]
+            self._got[i] = True
+            if not first or i in self._known_unused:
+                # a second gradient (added into p.grad before the flush), or a parameter the bucket
+                # does not wait for: either way the bucket's copy takes p.grad as it stands
                 return
             self._pending[b] -= 1
             if self._pending[b] == 0:
@@ -359,11 +371,13 @@ class FlatGradTrainer:
         self._ready = [n == 0 for n in self._pending]
         self._next_flush = 0
         self._late = False
+        self._late_parts = {}
         self._works = []
         try:
             # the short-K layers' weight gradients are batched (models/modules/linear.py) and
             # handed over by _deliver, at the model's flush points or after the backward
-            with deferred_weight_grads(self._deliver) as queue, flat_grad_destinations(self._grad_dest):
+            with deferred_weight_grads(self._deliver) as queue, flat_grad_destinations(self._grad_dest,
+                                                                                      self._may_claim):
                 self._flush_ready()
                 loss.backward()  # overlap: complete buckets are copied and all-reduced from the hooks, in order
                 queue.flush()
@@ -387,14 +401,36 @@ class FlatGradTrainer:
                 self.params[i].grad = None
         return loss.detach()
 
+    def _may_claim(self, p):
+        """Whether the backward may write p's gradient straight into its flat view (linear._claim):
+        not once p's bucket is reduced (or being reduced on the comm stream), and not for a
+        parameter found unused, which its bucket does not wait for (the bucket could be copied and
+        reduced, the view zeroed, while the producing kernel is still queued)."""
+        if not self._overlap_now or self._pending is None:
+            return True
+        i = self._index.get(id(p))
+        return i is None or (i not in self._known_unused and self._bucket_of[i] >= self._next_flush)
+
+    def _late_add(self, i, grad):
+        self._late = True
+        self._got[i] = True
+        prev = self._late_parts.get(i)
+        self._late_parts[i] = grad if prev is None else prev + grad
+
     def _deliver(self, p, grad):
         """A batched weight / bias gradient for parameter p: set (or added to) p.grad, then the
-        parameter's post-accumulate step (bucket hand-over) as autograd's hook would run it."""
+        parameter's post-accumulate step (bucket hand-over) as autograd's hook would run it.  Once
+        p's bucket is reduced, the gradient is kept aside instead (never added into the reduced
+        view, which the comm stream may still be reading)."""
+        i = self._index.get(id(p))
+        if (i is not None and self._pending is not None and self._overlap_now
+                and self._bucket_of[i] < self._next_flush):
+            self._late_add(i, grad)
+            return
         if p.grad is None:
             p.grad = grad
         else:
             p.grad.add_(grad)
-        i = self._index.get(id(p))
         if i is not None and i in self._hooks:
             self._hooks[i](p)
 
@@ -404,20 +440,23 @@ class FlatGradTrainer:
         The fused update leaves their values, moments and bf16 shadow as they were before it (saved
         and restored around the update kernels, captured with the update graph), so weight decay
         never touches them.  A step on which some rank gave a gradient to a parameter found unused
-        before (its bucket was reduced without it) reduces the whole gradient buffer once more."""
+        before, or a gradient delivered after its bucket was reduced, has those late gradients
+        (kept aside by _late_add) summed over ranks in one more all-reduce, which every rank joins,
+        and added to the reduced buffer."""
         flags = [1 if g else 0 for g in self._got] + [1 if self._late else 0]
         if self.world > 1:
             t = torch.tensor(flags, dtype=torch.int32, device=self.device)
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.pg)
             flags = t.tolist()
+        self._late_global = bool(flags[-1])
         if flags[-1] and self._overlap_now:
-            # the local gradients are still attached to the parameters: reduce them all again
-            for v, p in zip(self.grad_views, self.params):
-                if p.grad is not None:
-                    v.copy_(p.grad)
-                else:
-                    v.zero_()
-            dist.all_reduce(self.flat_grad, group=self.pg)
+            late = torch.zeros_like(self.flat_grad)
+            for i, g in self._late_parts.items():
+                off = self._offs[i]
+                late[off:off + g.numel()].copy_(g.reshape(-1))
+            dist.all_reduce(late, group=self.pg)
+            self.flat_grad.add_(late)
+        self._late_parts = {}
         unused = [i for i, g in enumerate(flags[:-1]) if g == 0]
         if unused == self._unused:
             return
@@ -510,12 +549,19 @@ class FlatGradTrainer:
                 self._request_host.copy_(self.loss_fn.request(self._stage_state), non_blocking=True)
             pool = self._g_a.pool()
         self._g_fb = torch.cuda.CUDAGraph()
-        self._overlap_now = self.overlap and self.capture_collectives
+        # a step with late gradients (the last warm-up step had one on some rank) needs the extra
+        # reduce decided on the host after the backward: such a step is captured with one
+        # all-reduce between the two graphs instead of the overlapped bucket collectives
+        self._overlap_now = self.overlap and self.capture_collectives and not self._late_global
         try:
             with torch.cuda.graph(self._g_fb, pool=pool, capture_error_mode="thread_local"):
                 self._loss = self._forward_backward(batch, cache_casts=False, stage_state=self._stage_state)
         finally:
             self._fb_reduces, self._overlap_now = self._overlap_now, self.overlap
+        if self._fb_reduces and self._late:
+            # (the captured bucket reduces would replay without this rank's late gradients)
+            raise RuntimeError("FlatGradTrainer.capture: a gradient arrived after its bucket was reduced inside the "
+                               "captured backward; capture with capture_collectives=False")
         self._g_up = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self._g_up, pool=self._g_fb.pool(), capture_error_mode="thread_local"):
             self._update()

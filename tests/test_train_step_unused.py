@@ -3,6 +3,7 @@ the reference runs DDP with find_unused_parameters=True (main.py:85) and torch A
 parameter on exactly the steps where its grad is None.  The trainer finds the unused set after
 every eager step, reduces its buckets in a fixed order whatever order each rank's backward
 completes them in, and reduces again on a step where a parameter found unused gets a gradient."""
+import importlib
 import os
 import socket
 import tempfile
@@ -14,6 +15,8 @@ import torch.multiprocessing as mp
 from torch import nn
 
 from conftest import PKG, ROOT
+
+LIN = importlib.import_module(PKG.__name__ + ".models.modules.linear")
 
 
 class Branchy(nn.Module):
@@ -29,6 +32,63 @@ class Branchy(nn.Module):
         if use_b:
             h = h + self.b(x)
         return self.c(h)
+
+
+class _ClaimLinear(torch.autograd.Function):
+    """x W^T + b whose backward writes the weight / bias gradients into the trainer's flat views when
+    it hands them out (linear._claim, as the autocast Linear's weight-gradient GEMM does)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.params = (w, b)
+        return x @ w.t() + b
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        wp, bp = ctx.params
+        gw, gb = gy.t() @ x, gy.sum(0)
+        dw, db = LIN._claim(wp), LIN._claim(bp)
+        if dw is not None:
+            gw = dw.copy_(gw)
+        if db is not None:
+            gb = db.copy_(gb)
+        return gy @ w, gw, gb
+
+
+class _DeferLinear(torch.autograd.Function):
+    """x W^T + b whose weight / bias gradients are queued and delivered after the backward
+    (linear._defer, the short-K layers' path)."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        ctx.save_for_backward(x, w)
+        ctx.params = (w, b)
+        return x @ w.t() + b
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, w = ctx.saved_tensors
+        wp, bp = ctx.params
+        if LIN._defer((gy, x, wp, 0, bp)):
+            return gy @ w, None, None
+        return gy @ w, gy.t() @ x, gy.sum(0)
+
+
+class Claimy(Branchy):
+    """Branchy whose layers write gradients in place (a, c; c used twice: a claimed view plus an
+    autograd contribution) or deliver them late (b, the branch some ranks skip)."""
+
+    def forward(self, x, use_b, plain=False):
+        cl = (lambda t, m: torch.nn.functional.linear(t, m.weight, m.bias)) if plain else \
+            (lambda t, m: _ClaimLinear.apply(t, m.weight, m.bias))
+        dl = (lambda t, m: torch.nn.functional.linear(t, m.weight, m.bias)) if plain else \
+            (lambda t, m: _DeferLinear.apply(t, m.weight, m.bias))
+        h = torch.tanh(cl(x, self.a))
+        if use_b:
+            h = h + dl(x, self.b)
+        return cl(h, self.c) + 0.5 * cl(h * h, self.c)
 
 
 def loss_fn(out):
@@ -77,7 +137,7 @@ def _free_port():
 PLAN = [(True, False), (False, False), (True, False), (False, True)]
 
 
-def _rank_main(rank, world, port, out_path):
+def _rank_main(rank, world, port, out_path, kind="branchy"):
     import sys
     sys.path.insert(0, ROOT)
     import importlib
@@ -85,7 +145,7 @@ def _rank_main(rank, world, port, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        model = Branchy()
+        model = Claimy() if kind == "claimy" else Branchy()
         # one bucket per parameter: b's buckets complete in a different order (or not at all) per rank
         tr = pkg.train_step.FlatGradTrainer(model, loss_fn, lr=1e-2, weight_decay=0.5, use_bf16=False,
                                             graph=False, bucket_mb=1e-6)
@@ -103,23 +163,28 @@ def _rank_main(rank, world, port, out_path):
         dist.destroy_process_group()
 
 
-def test_gloo_ranks_with_different_unused_parameters():
+@pytest.mark.parametrize("kind", ["branchy", "claimy"])
+def test_gloo_ranks_with_different_unused_parameters(kind):
+    """kind "claimy": gradients written straight into the flat buffer's views and deferred
+    gradients delivered after the backward — a parameter found unused that comes back on one rank
+    must be reduced once (not twice, and never added into an already-reduced view)."""
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "res")
-        mp.start_processes(_rank_main, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+        mp.start_processes(_rank_main, args=(2, _free_port(), out, kind), nprocs=2, join=True, start_method="spawn")
         r = [torch.load(f"{out}.{k}", weights_only=True) for k in range(2)]
     # reference: each rank's batch on the step's parameters, the gradients averaged
     for step, use in enumerate(PLAN):
         assert torch.equal(r[0][step]["params"], r[1][step]["params"])
         grads = []
         for rank in range(2):
-            m = Branchy()
+            m = Claimy() if kind == "claimy" else Branchy()
             off = 0
             with torch.no_grad():
                 for p in m.parameters():
                     p.copy_(r[0][step]["params"][off:off + p.numel()].view_as(p))
                     off += p.numel()
-            loss_fn(m(_x(10 * step + rank), use[rank])).backward()
+            x = _x(10 * step + rank)
+            loss_fn(m(x, use[rank], plain=True) if kind == "claimy" else m(x, use[rank])).backward()
             grads.append(torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
                                     for p in m.parameters()]))
         want = (grads[0] + grads[1]) / 2
