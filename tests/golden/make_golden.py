@@ -1091,6 +1091,141 @@ def mm_dvc_case(ref, seed=83):
         torch.set_default_dtype(torch.float32)
 
 
+DVC256 = dict(d_model=256, heads=8, ff=1024, enc_layers=2, dec_layers=2, caption_depth=2, num_queries=10,
+              num_classes=20, T=64, seq_len=12, seed=89)
+
+
+def dvc256_args():
+    """Namespaces of cfg.dvc / cfg.dvc.detr / cfg.dvc.caption (config_dvc_train.py) at d=256, 8 heads,
+    2 + 2 layers, ff 1024, T=64, caption depth 2; dropout 0 (shared by the fixture and its GPU test)."""
+    c = DVC256
+    ns = types.SimpleNamespace
+    d = c["d_model"]
+    detr = ns(feature_dim=d, d_model=d, num_heads=c["heads"], num_feature_levels=4, dec_n_points=4, enc_n_points=4,
+              enc_layers=c["enc_layers"], dec_layers=c["dec_layers"], transformer_dropout_prob=0.0,
+              transformer_ff_dim=c["ff"], video_rescale_len=c["T"], return_intermediate=True, hidden_dropout_prob=0.0,
+              layer_norm_eps=1e-12)
+    caption = ns(d_model=d, depth=c["caption_depth"], num_heads=c["heads"], mlp_ratio=4, qkv_bias=True,
+                 positional_embedding_dropout=0.0, attention_dropout=0.0, projection_dropout=0.0, bridge_dropout=0.0,
+                 mlp_dropout_1=0.0, mlp_dropout_2=0.0, pre_norm=False, model_official=None, weight_init=True,
+                 weight_load=False, emb_weights_req_grad=True, return_intermediate=True)
+    matcher = ns(cost_class=1, cost_segment=5, cost_giou=2, cost_alpha=0.25, cost_gamma=2.0)
+    return detr, caption, matcher
+
+
+DVC256_KEYS = ("pred_logits", "pred_segments", "pred_count", "pred_captions", "pred_memory_mask")
+
+
+def dvc256_loss(out, w):
+    """The fixture's loss: fixed random weights on every training output, plus the aux levels'
+    captions and segments (as deformable_dvc_f64), in the weights' dtype."""
+    dt = w["pred_logits"].dtype
+    loss = sum((out[k].to(dt) * w[k]).sum() for k in DVC256_KEYS)
+    return loss + sum((o["pred_captions"].to(dt) * 0.5).sum() + (o["pred_segments"].to(dt) * 0.5).sum()
+                      for o in out["aux_outputs"])
+
+
+def deformable_dvc_bf16_d256_case(ref):
+    """The reference's UnimodalDeformableDVC training forward + backward at d=256 (8 heads, 2 + 2 layers,
+    ff 1024, caption depth 2, T=64, B=2, 10 queries, dropout 0) — the size at which the bench's fused
+    bf16 paths engage — run by the reference in fp64 (the truth) and in fp32 under
+    torch.autocast('cpu', bfloat16) (the reference's own bf16 run), with deformable_dvc_f64's one
+    argument-order fix of the caption-decoder call.  Parameters from regen_parameters (no state_dict
+    stored).  The seed is the first from DVC256['seed'] on at which the bf16 run matches the same
+    (clip, prediction) pairs as fp64 on every decoder level, so the GPU test compares like with like;
+    the matching costs' smallest margin (second-best minus chosen cost per target) is stored."""
+    import copy
+    import models.matcher as ref_matcher  # noqa: E402
+    import models.deformable.unimodal_deformable_dvc as ref_ddvc  # noqa: E402
+    c = dict(DVC256)
+    detr, caption, mcfg = dvc256_args()
+    vocab = {w: i for i, w in enumerate(SPARSE_DVC_VOCAB)}
+
+    def fix_call(model):
+        dec = model.unimodal_caption_decoder
+        real_forward = type(dec).forward
+        dec.forward = lambda tgt, memory, tgt_mask=None, a4=None, a5=None: real_forward(dec, tgt, memory, tgt_mask, a5,
+                                                                                        a4)
+        return model
+
+    def build():
+        matcher = ref_matcher.build_matcher(mcfg)
+        return fix_call(ref_ddvc.UnimodalDeformableDVC(['video'], c["num_queries"], c["d_model"], c["num_classes"],
+                                                       True, matcher, 0.5, 10, vocab, c["seq_len"], None, detr, caption,
+                                                       use_differentiable_mask=True))
+
+    def run(model, obj, w, dtype, autocast):
+        model.train()
+        model.zero_grad()
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            out, caps, indices, indices_aux, mask = model(obj, is_training=True)
+        loss = dvc256_loss(out, {k: v.to(dtype) for k, v in w.items()})
+        loss.backward()
+        return dict(out={k: out[k].detach().float() for k in DVC256_KEYS}, loss=loss.detach().double(),
+                    aux_captions=torch.stack([o["pred_captions"].detach().float() for o in out["aux_outputs"]]),
+                    indices=[torch.stack(list(t)) for t in indices],
+                    indices_aux=[[torch.stack(list(t)) for t in lv] for lv in indices_aux],
+                    grads=sampled_grads({"dvc": model}))
+
+    for attempt in range(12):
+        seed = DVC256["seed"] + attempt
+        torch.manual_seed(seed)
+        model = build()
+        sums = regen_parameters(model, seed)
+        obj32 = sparse_dvc_batch(seed, c["d_model"], c["T"], torch.float32, len(vocab), c["seq_len"])
+        gen = torch.Generator().manual_seed(seed + 2)
+        with torch.no_grad():
+            probe = model(obj32, is_training=True)[0]
+        w = {k: torch.randn(probe[k].shape, generator=gen, dtype=torch.float64) for k in DVC256_KEYS}
+        m64 = fix_call(copy.deepcopy(model).double())
+        obj64 = sparse_dvc_batch(seed, c["d_model"], c["T"], torch.float64, len(vocab), c["seq_len"])
+        torch.set_default_dtype(torch.float64)  # the duration embedding allocates with the default dtype
+        try:
+            truth = run(m64, obj64, w, torch.float64, False)
+            margin = min_assignment_margin(m64, obj64)
+        finally:
+            torch.set_default_dtype(torch.float32)
+        bf16 = run(model, obj32, w, torch.float32, True)
+        same = all(torch.equal(a, b) for a, b in zip(truth["indices"], bf16["indices"])) and all(
+            torch.equal(a, b) for la, lb in zip(truth["indices_aux"], bf16["indices_aux"]) for a, b in zip(la, lb))
+        print(f"dvc256 seed {seed}: bf16 matching == fp64: {same}; smallest cost margin {margin:.4f}")
+        if same and margin > 5e-2:
+            break
+    else:
+        raise RuntimeError("no seed with the same matching in bf16 and fp64")
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    print("dvc256: reference bf16 vs fp64: " + " ".join(
+        f"{k} {rel(bf16['out'][k], truth['out'][k]):.3e}" for k in DVC256_KEYS) + f" loss {rel(bf16['loss'], truth['loss']):.3e}")
+    c["seed"] = seed
+    return dict(config={k: torch.tensor(v) for k, v in c.items()}, param_abs_sums=sums, weights=w,
+                margin=torch.tensor(margin, dtype=torch.float64), truth=truth, bf16=bf16)
+
+
+def min_assignment_margin(model, obj):
+    """How far the fixture's matchings are from a tie: over every decoder level and clip, the smallest
+    increase of the optimal assignment cost when one matched (prediction, target) pair is forbidden
+    (scipy's solver on the reference matcher's cost, models/matcher.py:64-92, in fp64)."""
+    from scipy.optimize import linear_sum_assignment
+    from utils.box_ops import generalized_box_iou, segment_cl_to_xy  # noqa: E402
+    with torch.no_grad():
+        out = model(obj, is_training=True)[0]
+    mt = model.matcher
+    worst = float("inf")
+    for o in [out] + list(out["aux_outputs"]):
+        for b, t in enumerate(obj["video_target"]):
+            seg, tseg = o["pred_segments"][b].double(), t["segments"].double()
+            cost = (mt.cost_segment * torch.cdist(seg, tseg, p=1)
+                    - mt.cost_giou * generalized_box_iou(segment_cl_to_xy(seg), segment_cl_to_xy(tseg))).numpy()
+            rows, cols = linear_sum_assignment(cost)
+            best = cost[rows, cols].sum()
+            for r, cc in zip(rows, cols):
+                c2 = cost.copy()
+                c2[r, cc] = 1e9
+                r2, k2 = linear_sum_assignment(c2)
+                worst = min(worst, c2[r2, k2].sum() - best)
+    return worst
+
+
 def main():
     torch.set_num_threads(min(8, os.cpu_count() or 1))
     ref = import_reference()
@@ -1113,6 +1248,7 @@ def main():
         "mm_dvc_f64": lambda: mm_dvc_case(ref),
         "transformer_bf16_d256": lambda: transformer_bf16_d256_case(ref),
         "caption_bf16": lambda: caption_bf16_case(ref),
+        "deformable_dvc_bf16_d256": lambda: deformable_dvc_bf16_d256_case(ref),
     }
     wanted = sys.argv[1:] or list(cases)
     for name, fn in cases.items():

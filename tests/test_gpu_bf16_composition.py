@@ -205,3 +205,72 @@ def test_caption_decoder_bf16_matches_reference_bf16(golden, dev):
         ref_gap = g[key]["bf16_gap"].item()
         print(f"{key}: bf16 path gap {gap:.4f} (reference bf16 {ref_gap:.4f})")
         assert gap <= 1.5 * ref_gap + 0.05, (key, gap, ref_gap)
+
+
+def test_dvc_training_step_bf16_matches_reference_bf16(golden, dev):
+    """deformable_dvc_bf16_d256: the reference's UnimodalDeformableDVC training forward + backward at
+    d=256 (8 heads, 2 + 2 layers, caption depth 2, T=64, B=2), fp64 and under bf16 autocast
+    (unimodal_deformable_dvc.py:103-300, engine.py:55-134).  Ours runs exactly as bench.py
+    --config dvc runs the step's math — inside FlatGradTrainer (bf16 shadow weights), bf16 autocast,
+    the fused paths and the segment cross-attention kernels — and must match the same (clip,
+    prediction) pairs on every decoder level (the fixture's seed keeps every matching > 0.05 cost
+    from a tie), with every output and sampled parameter gradient as close to the fp64 run as the
+    reference's own bf16 run is (check(): <= 1.5 x its error + slack)."""
+    g = golden("deformable_dvc_bf16_d256")
+    c = {k: int(v) for k, v in g["config"].items()}
+    detr, caption, mcfg = MG.dvc256_args()
+    vocab = {w: i for i, w in enumerate(MG.SPARSE_DVC_VOCAB)}
+    model = M.deformable.unimodal_deformable_dvc.UnimodalDeformableDVC(
+        ['video'], c["num_queries"], c["d_model"], c["num_classes"], True, M.matcher.build_matcher(mcfg), 0.5, 10, vocab,
+        c["seq_len"], None, detr, caption, use_differentiable_mask=True)
+    _check_param_sums(model, c["seed"], g["param_abs_sums"])
+    model = model.to(dev)
+    obj = MG.sparse_dvc_batch(c["seed"], c["d_model"], c["T"], torch.float32, len(vocab), c["seq_len"])
+    obj = {k: (v.to(dev) if isinstance(v, torch.Tensor) else
+               [{kk: vv.to(dev) if isinstance(vv, torch.Tensor) else vv for kk, vv in t.items()} for t in v]
+               if k == 'video_target' else v) for k, v in obj.items()}
+    w = {k: v.to(dev, torch.float32) for k, v in g["weights"].items()}
+    res = {}
+
+    def loss_fn(result):
+        res["r"] = result
+        return MG.dvc256_loss(result[0], w)
+
+    trainer = PKG.train_step.FlatGradTrainer(model, loss_fn, use_bf16=True, graph=False)
+    model.train()
+    PKG._trace.clear()
+    trainer._forward_backward((obj,))
+    torch.cuda.synchronize()
+    hits = dict(PKG._trace.hits)
+    for path in ("add_ln_carry", "linear_shadow", "query_prologue", "msda_bfloat16", "seg_attention"):
+        assert hits.get(path, 0) > 0, (path, hits)
+    out, _, indices, indices_aux, _ = res["r"]
+    truth, ref16 = g["truth"], g["bf16"]
+    for ours, want in zip(indices, truth["indices"]):
+        assert torch.equal(torch.stack([t.cpu() for t in ours]), want)
+    for lv, want_lv in zip(indices_aux, truth["indices_aux"]):
+        for ours, want in zip(lv, want_lv):
+            assert torch.equal(torch.stack([t.cpu() for t in ours]), want)
+    report, fails = [], []
+    for k in MG.DVC256_KEYS:
+        check(k, out[k].float(), truth["out"][k], ref16["out"][k], report=report, fails=fails)
+    check("aux_captions", torch.stack([o["pred_captions"].float() for o in out["aux_outputs"]]), truth["aux_captions"],
+          ref16["aux_captions"], report=report, fails=fails)
+    loss = MG.dvc256_loss(out, {k: v.double() for k, v in w.items()})
+    check("loss", loss.reshape(1), truth["loss"].reshape(1), ref16["loss"].reshape(1), report=report, fails=fails)
+    params = dict(model.named_parameters())
+    n = 0
+    for k, t in truth["grads"]["dvc"].items():
+        if t["norm"].item() < 1e-9:
+            continue
+        flat = params[k].grad.reshape(-1)
+        s = flat[MG.grad_sample_index("dvc." + k, flat.numel()).to(dev)]
+        bound = check(k, s, t["sample"], ref16["grads"]["dvc"][k]["sample"], slack=5e-3, report=report, fails=fails)
+        e_norm = abs(flat.double().norm().item() / t["norm"].item() - 1)
+        if e_norm > bound:
+            fails.append((k, "norm", e_norm, bound))
+        n += 1
+    for r in report:
+        print("dvc bf16 (name, ours vs fp64, reference bf16 vs fp64):", r)
+    assert n >= 100, n
+    assert not fails, fails
