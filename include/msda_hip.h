@@ -174,6 +174,51 @@ int msda_hip_prologue_backward_ex(const void* grad_loc, const void* grad_attn, c
                                   int64_t in_stride, void* grad_offsets, void* grad_logits, void* grad_ref,
                                   void* stream);
 
+/* Coordinate layouts (ABI v7).  The reference's (and every entry point above) is
+ * (batch, num_query, num_heads, num_levels, num_point): one (query, head)'s 64 bytes hold its
+ * four levels, so in the backward four row blocks (one per level) each write 16 of them and the
+ * line leaves L2 four times partially written.  Level-major puts one (batch, head, level)'s
+ * coordinates of consecutive queries side by side, (batch, num_heads, num_levels, num_query,
+ * num_point): a row block reads and writes whole lines.  It is internal to the fused MSDeformAttn
+ * path (prologue -> forward -> backward -> prologue backward all in this library); the
+ * extension API keeps the reference layout. */
+#define MSDA_COORD_API 0
+#define MSDA_COORD_LEVEL_MAJOR 1
+
+/* Whether a call may use MSDA_COORD_LEVEL_MAJOR: its backward takes the row-block path fed by the
+ * forward's tile intervals (msda_hip_forward_tiles_bytes > 0) and the prologue's level-major
+ * kernel covers it (num_levels * num_point == 16, num_point % 4 == 0, num_heads <= 8). */
+int msda_hip_level_major_ok(int value_dtype, const int64_t* spatial_shapes, int64_t num_levels, int64_t batch,
+                            int64_t spatial_size, int64_t num_heads, int64_t channels, int64_t num_query,
+                            int64_t num_point);
+
+/* msda_hip_forward_tiles / msda_hip_backward_tiles / the _ex prologue pair with a coordinate
+ * layout tag; sampling_loc, attn_weight, grad_loc and grad_attn are in that layout (the prologue's
+ * offsets / logits rows and reference points are as in the _ex entry points). */
+int msda_hip_forward_tiles_layout(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                                  const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                                  const void* attn_weight, void* output, void* tiles, int64_t batch,
+                                  int64_t spatial_size, int64_t num_heads, int64_t channels, int64_t num_query,
+                                  int64_t num_point, int padding_mode, int coord_layout, void* stream);
+int msda_hip_backward_tiles_layout(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                                   const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                                   const void* attn_weight, const void* grad_output, void* grad_value,
+                                   void* grad_loc, void* grad_attn, void* workspace, const void* tiles,
+                                   int64_t batch, int64_t spatial_size, int64_t num_heads, int64_t channels,
+                                   int64_t num_query, int64_t num_point, int padding_mode, int coord_layout,
+                                   void* stream);
+int msda_hip_prologue_forward_layout(const void* sampling_offsets, const void* attn_logits, int dtype,
+                                     const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
+                                     int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,
+                                     int64_t num_point, int64_t in_stride, int coord_layout, void* sampling_loc,
+                                     void* attn_weight, void* stream);
+int msda_hip_prologue_backward_layout(const void* grad_loc, const void* grad_attn, const void* attn_weight,
+                                      const void* sampling_offsets, int dtype, const void* reference_points,
+                                      int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
+                                      int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
+                                      int64_t in_stride, int coord_layout, void* grad_offsets, void* grad_logits,
+                                      void* grad_ref, void* stream);
+
 /* Sparse-DETR decoder attention map.  Replaces attn_map_to_flat_grid
  * (reference utils/dam.py:20-73): per (row, head), the attention weight of every sample is
  * scattered onto the two tokens around loc * T_l of its level with the reference's margins

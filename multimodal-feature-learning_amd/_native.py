@@ -19,8 +19,9 @@ LIB_PATH = os.environ.get("MSDA_HIP_LIB", LIB_PATH)
 # keep in sync with include/msda_hip.h
 DTYPE_TAGS = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2, torch.float16: 3}
 PAD_TAGS = {"border": 0, "zeros": 1}
+COORD_API, COORD_LEVEL_MAJOR = 0, 1
 MAX_LEVELS = 16
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 # every symbol include/msda_hip.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
@@ -35,6 +36,11 @@ EXPORTED_SYMBOLS = (
     "msda_hip_prologue_forward_ex",
     "msda_hip_prologue_backward_ex",
     "msda_hip_dam_flat_grid",
+    "msda_hip_level_major_ok",
+    "msda_hip_forward_tiles_layout",
+    "msda_hip_backward_tiles_layout",
+    "msda_hip_prologue_forward_layout",
+    "msda_hip_prologue_backward_layout",
     # include/flat_adamw.h (training-step runtime, same library)
     "flat_adamw_workspace_bytes",
     "flat_adamw_step",
@@ -103,6 +109,20 @@ def _declare(lib):
     lib.msda_hip_prologue_backward.restype = i32
     lib.msda_hip_prologue_backward.argtypes = [vp, vp, vp, vp, i32, vp, i32, p64, i64, i64, i64, i64, i64,
                                                vp, vp, vp, vp]
+    lib.msda_hip_level_major_ok.restype = i32
+    lib.msda_hip_level_major_ok.argtypes = [i32, p64, i64, i64, i64, i64, i64, i64, i64]
+    lib.msda_hip_forward_tiles_layout.restype = i32
+    lib.msda_hip_forward_tiles_layout.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp,
+                                                  i64, i64, i64, i64, i64, i64, i32, i32, vp]
+    lib.msda_hip_backward_tiles_layout.restype = i32
+    lib.msda_hip_backward_tiles_layout.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp, vp, vp, vp, vp,
+                                                   i64, i64, i64, i64, i64, i64, i32, i32, vp]
+    lib.msda_hip_prologue_forward_layout.restype = i32
+    lib.msda_hip_prologue_forward_layout.argtypes = [vp, vp, i32, vp, i32, p64, i64, i64, i64, i64, i64, i64, i32,
+                                                     vp, vp, vp]
+    lib.msda_hip_prologue_backward_layout.restype = i32
+    lib.msda_hip_prologue_backward_layout.argtypes = [vp, vp, vp, vp, i32, vp, i32, p64, i64, i64, i64, i64, i64,
+                                                      i64, i32, vp, vp, vp, vp]
     lib.msda_hip_dam_flat_grid.restype = i32
     lib.msda_hip_dam_flat_grid.argtypes = [vp, vp, p64, p64, i64, i64, i64, i64, i64, vp, vp]
     f32 = ctypes.c_float

@@ -359,6 +359,28 @@ __device__ __forceinline__ void load_coords16(const float* __restrict__ p, int L
   }
 }
 
+// The same L*P coordinates from the level-major layout (MSDA_COORD_LEVEL_MAJOR, (B, M, L, Lq, P)):
+// level l's P floats at base + l * cl.
+template <int N>
+__device__ __forceinline__ void load_coords16_lm(const float* __restrict__ base, long long cl, int L, int P,
+                                                 float (&r)[N]) {
+  if (P % 4 == 0) {
+#pragma unroll
+    for (int c = 0; c < N / 4; ++c) {
+      const int l = (4 * c) / P, p0 = (4 * c) % P;
+      if (4 * c < L * P) {
+        const float4 x = *reinterpret_cast<const float4*>(base + l * cl + p0);
+        r[4 * c] = x.x; r[4 * c + 1] = x.y; r[4 * c + 2] = x.z; r[4 * c + 3] = x.w;
+      } else {
+        r[4 * c] = r[4 * c + 1] = r[4 * c + 2] = r[4 * c + 3] = 0.f;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < N; ++j) r[j] = j < L * P ? base[(j / P) * cl + j % P] : 0.f;
+  }
+}
+
 // One (b, q, m) item's output chunk: the body of msda_fwd16_kernel (vb: the item's head and
 // lane offset in its clip's value rows; rs: the row stride, tap offsets inside a clip fit 32 bits)
 template <typename scalar_t, int VEC, bool ZEROS>
@@ -404,7 +426,7 @@ __device__ __forceinline__ void fwd16_item(const scalar_t* __restrict__ vb, cons
   store_vec<scalar_t, VEC>(op, acc);
 }
 
-template <typename scalar_t, int VEC, int G, bool ZEROS>
+template <typename scalar_t, int VEC, int G, bool ZEROS, bool LM>
 __global__ __launch_bounds__(256) void msda_fwd16_kernel(
     const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     scalar_t* __restrict__ out, const Levels lv, const int L, const int P, const int S, const int M,
@@ -417,8 +439,15 @@ __global__ __launch_bounds__(256) void msda_fwd16_kernel(
   const long long b = item / M / Lq;
   const int LP = L * P;
   float lr[kLPMax], ar[kLPMax];
-  load_coords16(loc + item * LP, LP, lr);
-  load_coords16(aw + item * LP, LP, ar);
+  if constexpr (LM) {
+    const long long q = (item / M) % Lq;
+    const long long c0 = ((b * M + m) * L * Lq + q) * P;
+    load_coords16_lm(loc + c0, (long long)Lq * P, L, P, lr);
+    load_coords16_lm(aw + c0, (long long)Lq * P, L, P, ar);
+  } else {
+    load_coords16(loc + item * LP, LP, lr);
+    load_coords16(aw + item * LP, LP, ar);
+  }
   fwd16_item<scalar_t, VEC, ZEROS>(value + (b * S * M + m) * (long long)D + lg * VEC, lr, ar, lv, P, LP, M * D,
                                    out + item * D + lg * VEC);
 }
@@ -431,7 +460,7 @@ __global__ __launch_bounds__(256) void msda_fwd16_kernel(
 // waves) and written once, no atomics — the backward then skips its interval prepass (a kernel
 // that re-read all of loc: 11 us at the bench's encoder call).  Items in (b, m, q) order: each
 // still reads its 64-B loc / aw rows and writes its 128-B output row whole.
-template <typename scalar_t, bool ZEROS, int P>
+template <typename scalar_t, bool ZEROS, int P, bool LM>
 __global__ __launch_bounds__(256) void msda_fwd16_tiles_kernel(
     const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     scalar_t* __restrict__ out, int2* __restrict__ tiles, const Levels lv, const int L, const int S, const int M,
@@ -455,8 +484,14 @@ __global__ __launch_bounds__(256) void msda_fwd16_tiles_kernel(
   if (q < Lq) {
     const long long item = (b * Lq + q) * M + m;
     float lr[kLPMax], ar[kLPMax];
-    load_coords16(loc + item * LP, LP, lr);
-    load_coords16(aw + item * LP, LP, ar);
+    if constexpr (LM) {
+      const long long c0 = ((b * M + m) * L * Lq + q) * P;
+      load_coords16_lm(loc + c0, (long long)Lq * P, L, P, lr);
+      load_coords16_lm(aw + c0, (long long)Lq * P, L, P, ar);
+    } else {
+      load_coords16(loc + item * LP, LP, lr);
+      load_coords16(aw + item * LP, LP, ar);
+    }
     fwd16_item<scalar_t, VEC, ZEROS>(value + (b * S * M + m) * (long long)D + lg * VEC, lr, ar, lv, P, LP, M * D,
                                      out + item * D + lg * VEC);
 #pragma unroll
@@ -2141,7 +2176,8 @@ int fast16_group(const Problem& pr) {
 
 template <typename scalar_t, typename coord_t, int VEC>
 int run_forward(const Problem& pr, const void* value, const void* loc, const void* aw, void* out,
-                int pad, hipStream_t st, void* tiles = nullptr) {
+                int pad, hipStream_t st, void* tiles = nullptr, int layout = MSDA_COORD_API) {
+  const bool lm = layout == MSDA_COORD_LEVEL_MAJOR;
   const long long n_items = pr.B * pr.Lq * pr.M;
   if (n_items == 0) return MSDA_OK;
   const int gshift = group_shift_for(pr.D / VEC);
@@ -2159,8 +2195,14 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
       const unsigned tblocks = (unsigned)(pr.B * pr.M * ntile);
       auto* tl = static_cast<int2*>(tiles);
 #define MSDA_FT(Z, PP)                                                                              \
-  hipLaunchKernelGGL((msda_fwd16_tiles_kernel<scalar_t, Z, PP>), dim3(tblocks), dim3(256), 0, st, v, lc, a, o, \
-                     tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile)
+  do {                                                                                            \
+    if (lm)                                                                                       \
+      hipLaunchKernelGGL((msda_fwd16_tiles_kernel<scalar_t, Z, PP, true>), dim3(tblocks), dim3(256), 0, st, v, lc, \
+                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
+    else                                                                                          \
+      hipLaunchKernelGGL((msda_fwd16_tiles_kernel<scalar_t, Z, PP, false>), dim3(tblocks), dim3(256), 0, st, v, lc, \
+                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
+  } while (0)
 #define MSDA_FT_P(Z)                                                                                \
   switch (pr.P) {                                                                                 \
     case 1: MSDA_FT(Z, 1); break;                                                                 \
@@ -2179,9 +2221,16 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
     if (G > 0) {
       const unsigned fblocks = (unsigned)((n_items * G + 255) / 256);
 #define MSDA_F16(GG, Z)                                                                            \
-  hipLaunchKernelGGL((msda_fwd16_kernel<scalar_t, VEC, GG, Z>), dim3(fblocks), dim3(256), 0, st, v,  \
-                     lc, a, o, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D,        \
-                     (int)pr.Lq, n_items)
+  do {                                                                                           \
+    if (lm)                                                                                      \
+      hipLaunchKernelGGL((msda_fwd16_kernel<scalar_t, VEC, GG, Z, true>), dim3(fblocks), dim3(256), 0, st, v, \
+                         lc, a, o, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D,    \
+                         (int)pr.Lq, n_items);                                                   \
+    else                                                                                         \
+      hipLaunchKernelGGL((msda_fwd16_kernel<scalar_t, VEC, GG, Z, false>), dim3(fblocks), dim3(256), 0, st, v, \
+                         lc, a, o, pr.lv, (int)pr.L, (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D,    \
+                         (int)pr.Lq, n_items);                                                   \
+  } while (0)
 #define MSDA_F16_G(Z)                                                                              \
   switch (G) {                                                                                   \
     case 1: MSDA_F16(1, Z); break;                                                               \
@@ -2197,6 +2246,11 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
 #undef MSDA_F16
       return launch_status("forward");
     }
+  }
+  if (lm) {
+    set_error("msda forward: the level-major coordinate layout needs fp32 coordinates, L*P <= 16 with L*P %% 4 == 0 "
+              "and D a power-of-two number of 16-byte chunks");
+    return MSDA_ERR_ARG;
   }
   if (pad == MSDA_PAD_ZEROS)
     hipLaunchKernelGGL((msda_fwd_kernel<scalar_t, coord_t, VEC, true>), dim3(blocks), dim3(256), 0,
@@ -2789,7 +2843,8 @@ bool forward_tiles_ok(const Problem& pr, int value_dtype) {
 template <typename scalar_t, typename coord_t>
 int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
                  const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
-                 int value_dtype, int pad, hipStream_t st, const void* tiles = nullptr) {
+                 int value_dtype, int pad, hipStream_t st, const void* tiles = nullptr,
+                 int layout = MSDA_COORD_API) {
   if constexpr (std::is_same<coord_t, float>::value) {
     const int ns = pr.B * pr.M * pr.S > 0 ? fused_bwd_rows<scalar_t, coord_t>(pr, value_dtype, gval) : 0;
     // sparse or tiny calls (every level at most 4 samples a row: decoder-like; or at most 512
@@ -2807,9 +2862,18 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
           sh.T[l] = pr.lv.T[l];
           sh.start[l] = pr.lv.start[l];
         }
-        msda_win_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, tiles, &sh, pad == MSDA_PAD_ZEROS, st);
+        if (msda_win_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, tiles, &sh, pad == MSDA_PAD_ZEROS,
+                              layout, st) < 0) {
+          set_error("msda backward: level-major coordinates need the forward's tile intervals");
+          return MSDA_ERR_ARG;
+        }
         return launch_status("backward rows (mfma)");
       }
+    }
+    if (layout != MSDA_COORD_API) {
+      set_error("msda backward: the level-major coordinate layout needs the row-block path (bf16 values, D = 64, "
+                "the forward's tile intervals)");
+      return MSDA_ERR_ARG;
     }
     PairPlan pp;
     if (gval != nullptr && pr.B * pr.M * pr.S > 0 && !(sparse && ns > 0) &&
@@ -3156,11 +3220,203 @@ __global__ __launch_bounds__(256) void msda_prologue16_bwd_kernel(
   }
 }
 
+// Level-major variants (MSDA_COORD_LEVEL_MAJOR, (B, M, L, Lq, P); num_point a multiple of 4, L*P == 16,
+// M <= 8): one workgroup of 32 M threads per (b, tile of 32 queries), thread (m, i) the item
+// (b, q0 + i, m), so level l's P coordinates of 32 consecutive queries are one contiguous store
+// (the backward's row blocks then read and write whole lines).  Same arithmetic as
+// msda_prologue16_*_kernel; grad_ref sums the heads through LDS in head order.
+template <int P>
+__device__ __forceinline__ void store_level_lm(float* __restrict__ dst, long long cl, const float (&r)[16]) {
+#pragma unroll
+  for (int l = 0; l < 16 / P; ++l)
+#pragma unroll
+    for (int c = 0; c < P / 4; ++c)
+      *reinterpret_cast<float4*>(dst + l * cl + 4 * c) =
+          make_float4(r[l * P + 4 * c], r[l * P + 4 * c + 1], r[l * P + 4 * c + 2], r[l * P + 4 * c + 3]);
+}
+template <int P>
+__device__ __forceinline__ void load_level_lm(const float* __restrict__ src, long long cl, float (&r)[16]) {
+#pragma unroll
+  for (int l = 0; l < 16 / P; ++l)
+#pragma unroll
+    for (int c = 0; c < P / 4; ++c) {
+      const float4 x = *reinterpret_cast<const float4*>(src + l * cl + 4 * c);
+      r[l * P + 4 * c] = x.x; r[l * P + 4 * c + 1] = x.y; r[l * P + 4 * c + 2] = x.z; r[l * P + 4 * c + 3] = x.w;
+    }
+}
+
+template <typename scalar_t, int P>
+__global__ __launch_bounds__(256) void msda_prologue16lm_fwd_kernel(
+    const scalar_t* __restrict__ off, const scalar_t* __restrict__ logits, const float* __restrict__ ref,
+    const int ref_dim, float* __restrict__ loc, float* __restrict__ aw, const Levels lv, const int M,
+    const long long Lq, const int ntile, const long long is) {
+#pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
+  static_assert(P % 4 == 0 && 16 % P == 0, "level-major prologue: P in {4, 8, 16}");
+  constexpr int L = 16 / P;
+  const long long b = blockIdx.x / ntile;
+  const long long q = (long long)(blockIdx.x % ntile) * 32 + (threadIdx.x & 31);
+  const int m = (int)(threadIdx.x >> 5);
+  if (q >= Lq || m >= M) return;
+  const long long bq = b * Lq + q;
+  const long long ii = bq * is + m * 16;
+  float x[16], v[16];
+  load16s<scalar_t>(logits + ii, x);
+  load16s<scalar_t>(off + ii, v);
+  float mx = x[0];
+#pragma unroll
+  for (int j = 1; j < 16; ++j) mx = x[j] > mx ? x[j] : mx;
+  float sum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    x[j] = expf(x[j] - mx);
+    sum += x[j];
+  }
+#pragma unroll
+  for (int j = 0; j < 16; ++j) x[j] = x[j] / sum;
+  const long long cl = Lq * P;
+  const long long c0 = (b * M + m) * L * cl + q * P;
+  store_level_lm<P>(aw + c0, cl, x);
+  const float* __restrict__ rb = ref + bq * L * ref_dim;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int l = j / P;
+    const float r0 = rb[l * ref_dim];
+    if (ref_dim == 1) {
+      v[j] = r0 + round_to<scalar_t>(v[j] / (float)lv.T[l]);
+    } else {
+      v[j] = r0 + (round_to<scalar_t>(v[j] / (float)P) * rb[l * 2 + 1]) * 0.5f;
+    }
+  }
+  store_level_lm<P>(loc + c0, cl, v);
+}
+
+template <typename scalar_t, int P>
+__global__ __launch_bounds__(256) void msda_prologue16lm_bwd_kernel(
+    const float* __restrict__ grad_loc, const float* __restrict__ grad_aw, const float* __restrict__ aw,
+    const scalar_t* __restrict__ off, const float* __restrict__ ref, const int ref_dim,
+    scalar_t* __restrict__ grad_off, scalar_t* __restrict__ grad_logits, float* __restrict__ grad_ref,
+    const Levels lv, const int M, const long long Lq, const int ntile, const long long is) {
+#pragma clang fp contract(off)  // PyTorch evaluates these as separate kernels: no FMA fusion
+  static_assert(P % 4 == 0 && 16 % P == 0, "level-major prologue: P in {4, 8, 16}");
+  constexpr int L = 16 / P;
+  __shared__ float s_ref[2][L][8][32];
+  const long long b = blockIdx.x / ntile;
+  const int i = (int)(threadIdx.x & 31);
+  const long long q = (long long)(blockIdx.x % ntile) * 32 + i;
+  const int m = (int)(threadIdx.x >> 5);
+  const bool active = q < Lq && m < M;  // every thread stays for the grad_ref sums
+  const long long bq = b * Lq + (active ? q : 0);
+  const int mm = active ? m : 0;
+  const long long ii = bq * is + mm * 16;
+  const long long cl = Lq * P;
+  const long long c0 = (b * M + mm) * L * cl + (active ? q : 0) * P;
+  if (grad_logits != nullptr) {
+    float g[16], y[16];
+    load_level_lm<P>(grad_aw + c0, cl, g);
+    load_level_lm<P>(aw + c0, cl, y);
+    float dot = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) dot += g[j] * y[j];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) g[j] = y[j] * (g[j] - dot);
+    if (active) store16s<scalar_t>(grad_logits + ii, g);
+  }
+  if (grad_off == nullptr && grad_ref == nullptr) return;  // uniform
+  float gl[16], o[16];
+  load_level_lm<P>(grad_loc + c0, cl, gl);
+  const bool box = ref_dim == 2;
+  if (box) load16s<scalar_t>(off + ii, o);
+  const float* __restrict__ rb = ref + bq * L * ref_dim;
+  float go[16], s1[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int l = j / P;
+    if (!box) {
+      go[j] = round_to<scalar_t>(gl[j]) / (float)lv.T[l];
+      s1[j] = 0.f;
+    } else {
+      const float gh = gl[j] * 0.5f;
+      go[j] = round_to<scalar_t>(gh * rb[l * 2 + 1]) / (float)P;
+      s1[j] = gh * round_to<scalar_t>(o[j] / (float)P);
+    }
+  }
+  if (grad_off != nullptr && active) store16s<scalar_t>(grad_off + ii, go);
+  if (grad_ref == nullptr) return;  // uniform
+#pragma unroll
+  for (int l = 0; l < L; ++l) {
+    float a0 = 0.f, a1 = 0.f;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      a0 += active ? gl[l * P + p] : 0.f;
+      a1 += active ? s1[l * P + p] : 0.f;
+    }
+    if (m < 8) {
+      s_ref[0][l][m][i] = a0;
+      s_ref[1][l][m][i] = a1;
+    }
+  }
+  __syncthreads();
+  if (m == 0 && q < Lq) {
+#pragma unroll
+    for (int l = 0; l < L; ++l) {
+      float a0 = 0.f, a1 = 0.f;
+      for (int h = 0; h < M; ++h) {
+        a0 += s_ref[0][l][h][i];
+        a1 += s_ref[1][l][h][i];
+      }
+      grad_ref[(bq * L + l) * ref_dim] = a0;
+      if (box) grad_ref[(bq * L + l) * 2 + 1] = a1;
+    }
+  }
+}
+
+// the level-major prologue's coverage (msda_prologue16lm_*_kernel)
+bool prologue_lm_ok(long long M, long long L, long long P) {
+  return L * P == 16 && (P == 4 || P == 8 || P == 16) && M >= 1 && M <= 8;
+}
+
 template <typename scalar_t, typename coord_t>
 int run_prologue(bool fwd, const Problem& pr, int ref_dim, const void* off, const void* logits,
                  const void* ref, void* loc, void* aw, const void* grad_loc, const void* grad_aw,
-                 void* grad_off, void* grad_logits, void* grad_ref, long long is, hipStream_t st) {
+                 void* grad_off, void* grad_logits, void* grad_ref, long long is, hipStream_t st,
+                 int layout = MSDA_COORD_API) {
   const long long n_queries = pr.B * pr.Lq;
+  if (layout == MSDA_COORD_LEVEL_MAJOR) {
+    if constexpr (std::is_same<coord_t, double>::value) {
+      set_error("msda prologue: the level-major layout needs fp32 coordinates");
+      return MSDA_ERR_ARG;
+    } else {
+      if (!prologue_lm_ok(pr.M, pr.L, pr.P)) {
+        set_error("msda prologue: the level-major layout needs num_levels*num_point == 16, num_point in {4, 8, 16} "
+                  "and num_heads <= 8");
+        return MSDA_ERR_ARG;
+      }
+      if (n_queries == 0) return MSDA_OK;
+      const int ntile = (int)((pr.Lq + 31) / 32);
+      const unsigned blocks = (unsigned)(pr.B * ntile);
+      const unsigned threads = (unsigned)(32 * pr.M);
+      auto* o = static_cast<const scalar_t*>(off);
+      auto* rf = static_cast<const float*>(ref);
+#define MSDA_PLM(PP)                                                                                  \
+  do {                                                                                              \
+    if (fwd)                                                                                        \
+      hipLaunchKernelGGL((msda_prologue16lm_fwd_kernel<scalar_t, PP>), dim3(blocks), dim3(threads), 0, st, o, \
+                         static_cast<const scalar_t*>(logits), rf, ref_dim, static_cast<float*>(loc),     \
+                         static_cast<float*>(aw), pr.lv, (int)pr.M, pr.Lq, ntile, is);               \
+    else                                                                                            \
+      hipLaunchKernelGGL((msda_prologue16lm_bwd_kernel<scalar_t, PP>), dim3(blocks), dim3(threads), 0, st, \
+                         static_cast<const float*>(grad_loc), static_cast<const float*>(grad_aw),    \
+                         static_cast<const float*>(aw), o, rf, ref_dim, static_cast<scalar_t*>(grad_off), \
+                         static_cast<scalar_t*>(grad_logits), static_cast<float*>(grad_ref), pr.lv, (int)pr.M, \
+                         pr.Lq, ntile, is);                                                          \
+  } while (0)
+      if (pr.P == 4) MSDA_PLM(4);
+      else if (pr.P == 8) MSDA_PLM(8);
+      else MSDA_PLM(16);
+#undef MSDA_PLM
+      return launch_status(fwd ? "prologue forward (level-major)" : "prologue backward (level-major)");
+    }
+  }
   if (n_queries == 0) return MSDA_OK;
   if constexpr (!std::is_same<coord_t, double>::value) {
     const int Mi = (int)pr.M;
@@ -3262,20 +3518,24 @@ int check_prologue(const int64_t* shapes, int64_t L, int64_t B, int64_t Lq, int6
 int dispatch_prologue(bool fwd, int dtype, const Problem& pr, int ref_dim, const void* off,
                       const void* logits, const void* ref, void* loc, void* aw, const void* grad_loc,
                       const void* grad_aw, void* grad_off, void* grad_logits, void* grad_ref,
-                      long long is, hipStream_t st) {
+                      long long is, hipStream_t st, int layout = MSDA_COORD_API) {
+  if (layout != MSDA_COORD_API && layout != MSDA_COORD_LEVEL_MAJOR) {
+    set_error("msda prologue: unknown coordinate layout %d", layout);
+    return MSDA_ERR_ARG;
+  }
   switch (dtype) {
     case MSDA_DTYPE_F32:
       return run_prologue<float, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw, grad_off,
-                                        grad_logits, grad_ref, is, st);
+                                        grad_logits, grad_ref, is, st, layout);
     case MSDA_DTYPE_F64:
       return run_prologue<double, double>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
-                                          grad_off, grad_logits, grad_ref, is, st);
+                                          grad_off, grad_logits, grad_ref, is, st, layout);
     case MSDA_DTYPE_BF16:
       return run_prologue<bf16_t, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
-                                         grad_off, grad_logits, grad_ref, is, st);
+                                         grad_off, grad_logits, grad_ref, is, st, layout);
     case MSDA_DTYPE_F16:
       return run_prologue<f16_t, float>(fwd, pr, ref_dim, off, logits, ref, loc, aw, grad_loc, grad_aw,
-                                        grad_off, grad_logits, grad_ref, is, st);
+                                        grad_off, grad_logits, grad_ref, is, st, layout);
     default:
       set_error("msda prologue: unknown dtype %d", dtype);
       return MSDA_ERR_ARG;
@@ -3362,7 +3622,7 @@ hipError_t zero_f32(float* p, long long n, hipStream_t st) {
 
 extern "C" {
 
-int msda_hip_abi_version(void) { return 6; }
+int msda_hip_abi_version(void) { return 7; }
 
 const char* msda_hip_last_error(void) { return g_last_error; }
 
@@ -3495,7 +3755,7 @@ static int forward_entry(const void* value, int value_dtype, const int64_t* spat
                          const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
                          const void* attn_weight, void* output, void* tiles, int64_t batch, int64_t spatial_size,
                          int64_t num_heads, int64_t channels, int64_t num_query, int64_t num_point,
-                         int padding_mode, void* stream) {
+                         int padding_mode, void* stream, int layout = MSDA_COORD_API) {
   g_last_error[0] = 0;
   Problem pr;
   int rc = check_problem(spatial_shapes, level_start, num_levels, batch, spatial_size, num_heads,
@@ -3516,13 +3776,22 @@ static int forward_entry(const void* value, int value_dtype, const int64_t* spat
     return MSDA_ERR_ARG;
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
+  if (layout != MSDA_COORD_API && layout != MSDA_COORD_LEVEL_MAJOR) {
+    set_error("msda_hip_forward: unknown coordinate layout %d", layout);
+    return MSDA_ERR_ARG;
+  }
   if (tiles != nullptr) {
     if (!forward_tiles_ok(pr, value_dtype)) {
       set_error("msda_hip_forward_tiles: the call's backward does not take the row-block path "
                 "(msda_hip_forward_tiles_bytes is 0)");
       return MSDA_ERR_ARG;
     }
-    return run_forward<bf16_t, float, 8>(pr, value, sampling_loc, attn_weight, output, padding_mode, st, tiles);
+    return run_forward<bf16_t, float, 8>(pr, value, sampling_loc, attn_weight, output, padding_mode, st, tiles,
+                                         layout);
+  }
+  if (layout != MSDA_COORD_API) {
+    set_error("msda_hip_forward: the level-major coordinate layout goes with the tiles forward");
+    return MSDA_ERR_ARG;
   }
   const int vec = pick_vec(value_dtype, pr.D);
   switch (value_dtype) {
@@ -3589,7 +3858,8 @@ static int backward_entry(const void* value, int value_dtype, const int64_t* spa
                           const void* attn_weight, const void* grad_output, void* grad_value,
                           void* grad_loc, void* grad_attn, void* workspace, const void* tiles, int64_t batch,
                           int64_t spatial_size, int64_t num_heads, int64_t channels,
-                          int64_t num_query, int64_t num_point, int padding_mode, void* stream) {
+                          int64_t num_query, int64_t num_point, int padding_mode, void* stream,
+                          int layout = MSDA_COORD_API) {
   g_last_error[0] = 0;
   Problem pr;
   int rc = check_problem(spatial_shapes, level_start, num_levels, batch, spatial_size, num_heads,
@@ -3644,6 +3914,10 @@ static int backward_entry(const void* value, int value_dtype, const int64_t* spa
     set_error("msda_hip_backward_tiles: the call does not take the row-block path (no tiles forward)");
     return MSDA_ERR_ARG;
   }
+  if (layout != MSDA_COORD_API && (layout != MSDA_COORD_LEVEL_MAJOR || !tiles_do)) {
+    set_error("msda_hip_backward: coordinate layout %d needs the forward's tile intervals of a row-block call", layout);
+    return MSDA_ERR_ARG;
+  }
   if (grad_value == nullptr && grad_loc == nullptr && grad_attn == nullptr) return MSDA_OK;
   hipStream_t st = static_cast<hipStream_t>(stream);
   switch (value_dtype) {
@@ -3655,7 +3929,7 @@ static int backward_entry(const void* value, int value_dtype, const int64_t* spa
                                           grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
     case MSDA_DTYPE_BF16:
       return run_backward<bf16_t, float>(pr, value, sampling_loc, attn_weight, grad_output, grad_value,
-                                         grad_loc, grad_attn, workspace, value_dtype, padding_mode, st, tiles);
+                                         grad_loc, grad_attn, workspace, value_dtype, padding_mode, st, tiles, layout);
     default:
       return run_backward<f16_t, float>(pr, value, sampling_loc, attn_weight, grad_output, grad_value,
                                         grad_loc, grad_attn, workspace, value_dtype, padding_mode, st);
@@ -3687,6 +3961,95 @@ int msda_hip_backward_tiles(const void* value, int value_dtype, const int64_t* s
   return backward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
                         grad_output, grad_value, grad_loc, grad_attn, workspace, tiles, batch, spatial_size,
                         num_heads, channels, num_query, num_point, padding_mode, stream);
+}
+
+int msda_hip_level_major_ok(int value_dtype, const int64_t* spatial_shapes, int64_t num_levels, int64_t batch,
+                            int64_t spatial_size, int64_t num_heads, int64_t channels, int64_t num_query,
+                            int64_t num_point) {
+  return prologue_lm_ok(num_heads, num_levels, num_point) &&
+         msda_hip_forward_tiles_bytes(value_dtype, spatial_shapes, num_levels, batch, spatial_size, num_heads,
+                                      channels, num_query, num_point) > 0;
+}
+
+int msda_hip_forward_tiles_layout(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                                  const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                                  const void* attn_weight, void* output, void* tiles, int64_t batch,
+                                  int64_t spatial_size, int64_t num_heads, int64_t channels, int64_t num_query,
+                                  int64_t num_point, int padding_mode, int coord_layout, void* stream) {
+  if (tiles == nullptr) {
+    g_last_error[0] = 0;
+    set_error("msda_hip_forward_tiles_layout: null tiles");
+    return MSDA_ERR_ARG;
+  }
+  return forward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
+                       output, tiles, batch, spatial_size, num_heads, channels, num_query, num_point,
+                       padding_mode, stream, coord_layout);
+}
+
+int msda_hip_backward_tiles_layout(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                                   const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                                   const void* attn_weight, const void* grad_output, void* grad_value,
+                                   void* grad_loc, void* grad_attn, void* workspace, const void* tiles,
+                                   int64_t batch, int64_t spatial_size, int64_t num_heads, int64_t channels,
+                                   int64_t num_query, int64_t num_point, int padding_mode, int coord_layout,
+                                   void* stream) {
+  if (tiles == nullptr) {
+    g_last_error[0] = 0;
+    set_error("msda_hip_backward_tiles_layout: null tiles");
+    return MSDA_ERR_ARG;
+  }
+  return backward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
+                        grad_output, grad_value, grad_loc, grad_attn, workspace, tiles, batch, spatial_size,
+                        num_heads, channels, num_query, num_point, padding_mode, stream, coord_layout);
+}
+
+int msda_hip_prologue_forward_layout(const void* sampling_offsets, const void* attn_logits, int dtype,
+                                     const void* reference_points, int ref_dim, const int64_t* spatial_shapes,
+                                     int64_t num_levels, int64_t batch, int64_t num_query, int64_t num_heads,
+                                     int64_t num_point, int64_t in_stride, int coord_layout, void* sampling_loc,
+                                     void* attn_weight, void* stream) {
+  g_last_error[0] = 0;
+  Problem pr;
+  int rc = check_prologue(spatial_shapes, num_levels, batch, num_query, num_heads, num_point, ref_dim, &pr);
+  if (rc) return rc;
+  if (in_stride < num_heads * num_levels * num_point) {
+    set_error("msda_hip_prologue_forward: in_stride %lld < num_heads * num_levels * num_point", (long long)in_stride);
+    return MSDA_ERR_ARG;
+  }
+  if (batch * num_query > 0 && (sampling_offsets == nullptr || attn_logits == nullptr ||
+                                reference_points == nullptr || sampling_loc == nullptr || attn_weight == nullptr)) {
+    set_error("msda_hip_prologue_forward: null pointer");
+    return MSDA_ERR_ARG;
+  }
+  return dispatch_prologue(true, dtype, pr, ref_dim, sampling_offsets, attn_logits, reference_points,
+                           sampling_loc, attn_weight, nullptr, nullptr, nullptr, nullptr, nullptr, in_stride,
+                           static_cast<hipStream_t>(stream), coord_layout);
+}
+
+int msda_hip_prologue_backward_layout(const void* grad_loc, const void* grad_attn, const void* attn_weight,
+                                      const void* sampling_offsets, int dtype, const void* reference_points,
+                                      int ref_dim, const int64_t* spatial_shapes, int64_t num_levels,
+                                      int64_t batch, int64_t num_query, int64_t num_heads, int64_t num_point,
+                                      int64_t in_stride, int coord_layout, void* grad_offsets, void* grad_logits,
+                                      void* grad_ref, void* stream) {
+  g_last_error[0] = 0;
+  Problem pr;
+  int rc = check_prologue(spatial_shapes, num_levels, batch, num_query, num_heads, num_point, ref_dim, &pr);
+  if (rc) return rc;
+  if (in_stride < num_heads * num_levels * num_point) {
+    set_error("msda_hip_prologue_backward: in_stride %lld < num_heads * num_levels * num_point", (long long)in_stride);
+    return MSDA_ERR_ARG;
+  }
+  const bool need_loc_side = grad_offsets != nullptr || grad_ref != nullptr;
+  if (batch * num_query > 0 &&
+      ((need_loc_side && grad_loc == nullptr) || (grad_logits != nullptr && (grad_attn == nullptr || attn_weight == nullptr)) ||
+       (ref_dim == 2 && need_loc_side && (reference_points == nullptr || sampling_offsets == nullptr)))) {
+    set_error("msda_hip_prologue_backward: null pointer");
+    return MSDA_ERR_ARG;
+  }
+  return dispatch_prologue(false, dtype, pr, ref_dim, sampling_offsets, nullptr, reference_points, nullptr,
+                           const_cast<void*>(attn_weight), grad_loc, grad_attn, grad_offsets, grad_logits,
+                           grad_ref, in_stride, static_cast<hipStream_t>(stream), coord_layout);
 }
 
 }  // extern "C"

@@ -18,6 +18,11 @@ struct WinShape {
   // chunks c of every level, chunk c = level l's blocks [cs_l(c), cs_l(c+1)); the blocks of one
   // (b, m) in chunk order are seq[cs[c] .. cs[c+1]) as (level << 12 | block)
   int nchunk, ppx;
+  // coordinate strides (floats): element (b, q, m, l, p) of loc / aw / grad_loc / grad_attn sits at
+  // b cb + q cq + m cm + l cl + p (set by msda_win_backward from the layout tag)
+  long long cb, cm;
+  int cq, cl;
+  int exp;  // profiling only (MSDA_HIP_WIN_EXP bitmask, 0 in production): skip parts of win_bwd_kernel
   unsigned short cs[kWinMaxChunks + 1];
   unsigned short seq[kWinMaxSeq];
 };
@@ -50,7 +55,20 @@ __attribute__((visibility("hidden"))) size_t msda_win_workspace_bytes(long long 
                                                                      long long Lq);
 __attribute__((visibility("hidden"))) int msda_win_supported(int value_dtype_is_bf16, long long D, long long P, long long Lq,
                                                                   long long row_floats);
+// Coordinate layouts of loc / aw and their gradients: the reference's (B, Lq, M, L, P), or
+// level-major (B, M, L, Lq, P) — one (b, m, level)'s coordinates of consecutive queries contiguous
+// (include/msda_hip.h, MSDA_COORD_*)
+struct CoordStrides {
+  long long cb, cm;
+  int cq, cl;
+};
+__host__ __device__ inline CoordStrides coord_strides(int layout, long long Lq, long long M, long long L, long long P) {
+  if (layout == 1) return CoordStrides{M * L * Lq * P, L * Lq * P, (int)P, (int)(Lq * P)};
+  return CoordStrides{Lq * M * L * P, L * P, (int)(M * L * P), (int)P};
+}
+
 __attribute__((visibility("hidden"))) int msda_win_backward(const void* value, const void* loc, const void* aw,
                                                             const void* gout, void* gval, void* gloc, void* gaw,
                                                             void* workspace, const void* tiles_ready,
-                                                            const WinShape* shape, int zeros, hipStream_t st);
+                                                            const WinShape* shape, int zeros, int coord_layout,
+                                                            hipStream_t st);

@@ -181,7 +181,7 @@ __device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory")
 // added through LDS at the end — for calls with few row blocks (short pyramids: video queries on
 // the audio pyramid), where one wave per block leaves the chip mostly idle.
 template <bool ZEROS, bool COORDS, int P, int W>
-__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) void win_bwd_kernel(
+__global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ? 2 : 4))) void win_bwd_kernel(
     const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     const uint16_t* __restrict__ gout, uint16_t* __restrict__ gval, float* __restrict__ gloc,
     float* __restrict__ gaw, const int2* __restrict__ tiles, const WinShape sh) {
@@ -245,13 +245,13 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
   }
   const int m = (int)(bm % (unsigned)sh.M);
   const long long b = bm / (unsigned)sh.M;
-  const int T = sh.T[l], LP = sh.L * P;
+  const int T = sh.T[l];
   const int r0 = k * kRW;
   const int rs = sh.M * 64;                           // grad_out / value row stride (elements)
-  const int qstride = sh.M * LP;                      // coordinate stride of one query
+  const int qstride = sh.cq;                          // coordinate stride of one query
   const uint16_t* __restrict__ vl = value + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
   const uint16_t* __restrict__ gb = gout + (b * sh.Lq * sh.M + m) * 64;
-  const long long cbase = (b * sh.Lq * sh.M + m) * (long long)LP + l * P;
+  const long long cbase = b * sh.cb + m * sh.cm + (long long)l * sh.cl;
   // per-lane constant parts of the addresses
   int soff[SPL];
 #pragma unroll
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
 
     // 2a. grad_value of the 16 rows += C . G, 32 compacted samples per MFMA step: C built in LDS
     // (zeroed, then each sample writes c0 on its base row and c1 on the next, where in the block)
-    for (int ks = 0; ks < nk; ++ks) {
+    for (int ks = 0; ks < ((sh.exp & 1) ? 0 : nk); ++ks) {
       {
         uint4* z = reinterpret_cast<uint4*>(s_c + (lane >> 2) * kGS + (lane & 3) * 32);
         z[0] = make_uint4(0u, 0u, 0u, 0u);
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
     }
     // 2b. dots of the tile's 32 queries with rows r0 .. r0+16 (2 query halves x 2 row blocks; of
     // the second block only row r0+16 is kept, its other columns read row r0+16 again)
-    if (COORDS) {
+    if (COORDS && !(sh.exp & 4)) {
 #pragma unroll
       for (int tt = 0; tt < 4; ++tt) {
         const int qh = tt >> 1, cb = tt & 1;
@@ -444,7 +444,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(4))) voi
         const bool in = (NS >= 64 || lane < NS) && q0 + s / P < sh.Lq;
         const Taps& t = tp[j];
         const bool own = t.live ? (t.base >= r0 && t.base < r0 + kRW) || (t.base < 0 && k == 0) : k == 0;
-        if (in && own) {
+        if (in && own && !(sh.exp & 2)) {
           const int qi = s / P;
           const float d0 = t.ok0 ? s_d[(t.base - r0) * kDQS + qi] : 0.f;
           const float d1 = t.ok1 ? s_d[(t.base + 1 - r0) * kDQS + qi] : 0.f;
@@ -527,8 +527,13 @@ static bool win_chunk_order(WinShape& sh) {
 
 int msda_win_backward(const void* value, const void* loc, const void* aw, const void* gout, void* gval,
                       void* gloc, void* gaw, void* workspace, const void* tiles_ready, const WinShape* shape,
-                      int zeros, hipStream_t st) {
+                      int zeros, int coord_layout, hipStream_t st) {
   WinShape sh = *shape;
+  // (the interval prepass reads whole query rows: the reference layout; level-major calls bring
+  // the forward's intervals)
+  if (coord_layout != 0 && tiles_ready == nullptr) return -1;
+  const CoordStrides cs = coord_strides(coord_layout, sh.Lq, sh.M, sh.L, sh.P);
+  sh.cb = cs.cb; sh.cm = cs.cm; sh.cq = cs.cq; sh.cl = cs.cl;
   sh.ntile = (int)((sh.Lq + kQT - 1) / kQT);
   int nb = 0;
   for (int l = 0; l < sh.L; ++l) {
@@ -546,6 +551,8 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   const bool chunked = win_chunk_order(sh) &&
                        (order_env == 1 || (order_env != 0 && (long long)sh.ppx * sh.nblk >= 2048));
   if (!chunked) sh.nchunk = 0;
+  const char* xe = getenv("MSDA_HIP_WIN_EXP");  // profiling: skip parts of the kernel (results are wrong)
+  sh.exp = xe ? atoi(xe) : 0;
   // tile intervals: written by the forward (msda_fwd16_tiles_kernel) or by the prepass below
   auto* tiles = static_cast<int2*>(tiles_ready != nullptr ? const_cast<void*>(tiles_ready) : workspace);
   const unsigned tile_wgs = tiles_ready != nullptr ? 0u : (unsigned)(sh.B * sh.ntile);

@@ -90,16 +90,16 @@ class _QueryPrologue(torch.autograd.Function):
     same: each output column is its own dot product over the input, in the GEMM's dtype."""
 
     @staticmethod
-    def forward(ctx, x, wa, ba, wb, bb, wca, bca, wcb, bcb, ref, shapes, dims):
+    def forward(ctx, x, wa, ba, wb, bb, wca, bca, wcb, bcb, ref, shapes, dims, layout=0):
         from ... import _trace
         _trace.hit("query_prologue")
         B, Lq, M, L, P = dims
         wc, bc = _rows_view(wca, wcb), _rows_view(bca, bcb)
         x2 = x.reshape(-1, x.shape[-1])
         y = _addmm(bc, x2, wc)
-        loc, aw = _msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes)
+        loc, aw = _msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes, layout)
         ctx.save_for_backward(x2, wc, y, aw, ref)
-        ctx.shapes, ctx.x_shape = shapes, x.shape
+        ctx.shapes, ctx.x_shape, ctx.layout = shapes, x.shape, layout
         ctx.params = (wa, ba, wb, bb)
         return loc, aw
 
@@ -108,11 +108,12 @@ class _QueryPrologue(torch.autograd.Function):
     def backward(ctx, grad_loc, grad_aw):
         x2, wc, y, aw, ref = ctx.saved_tensors
         nig = ctx.needs_input_grad
-        g2, g_ref = _msda.prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, ctx.shapes, need_ref=nig[9])
+        g2, g_ref = _msda.prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, ctx.shapes, need_ref=nig[9],
+                                                 layout=ctx.layout)
         gx = _mm_nn(g2, wc).view(ctx.x_shape) if nig[0] else None
         wa, ba, wb, bb = ctx.params
         na = wa.shape[0]
-        rest = (None, None, None, None, g_ref, None, None)
+        rest = (None, None, None, None, g_ref, None, None, None)
         if all(nig[1:5]) and _defer((g2[:, :na], x2, wa, 0, ba), (g2[:, na:], x2, wb, 0, bb)):
             return (gx, None, None, None, None) + rest
         gwa = gwb = gba = gbb = None
@@ -212,12 +213,22 @@ class MSDeformAttn(nn.Module):
             wcb, bcb = b._low(dt)
             if wca is None or wcb is None:
                 wca, bca, wcb, bcb = a.weight.to(dt), a.bias.to(dt), b.weight.to(dt), b.bias.to(dt)
+            # the coordinates stay level-major between the prologue, the MSDA kernels and their
+            # backward (whole 128-B lines per row block, include/msda_hip.h MSDA_COORD_LEVEL_MAJOR)
+            # where the call takes the row-block backward; the is_sparse returns keep the
+            # reference layout
+            layout = (_msda.LEVEL_MAJOR if not is_sparse and torch.is_grad_enabled()
+                      and _msda.level_major_ok(value, shapes, Len_q, self.n_points) else 0)
             with torch.autocast("cuda", enabled=False):
                 sampling_locations, attention_weights = _QueryPrologue.apply(
                     query.to(dt), a.weight, a.bias, b.weight, b.bias, wca, bca, wcb, bcb,
                     reference_points.float().contiguous(), tuple(int(t) for t in shapes),
-                    (N, Len_q, self.n_heads, self.n_levels, self.n_points))
-            output = ms_deform_attn_core_pytorch(value, shapes, sampling_locations, attention_weights)
+                    (N, Len_q, self.n_heads, self.n_levels, self.n_points), layout)
+            if layout:
+                output = _msda.msda_apply(value, shapes, starts, sampling_locations, attention_weights, "border",
+                                          layout=layout)
+            else:
+                output = ms_deform_attn_core_pytorch(value, shapes, sampling_locations, attention_weights)
             output = self.output_proj(output)
             if is_sparse:
                 return output, sampling_locations.unsqueeze(-1), attention_weights

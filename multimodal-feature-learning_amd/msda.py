@@ -16,8 +16,10 @@ from . import _native
 __all__ = [
     "host_levels", "msda_forward", "msda_backward", "MSDAFunction", "msda_apply", "KernelTimer",
     "algorithmic_bytes", "gathered_bytes", "prologue_supported", "prologue_forward", "prologue_backward", "MSDAPrologueFunction",
-    "msda_prologue_apply",
+    "msda_prologue_apply", "level_major_ok", "LEVEL_MAJOR",
 ]
+
+LEVEL_MAJOR = 1  # coordinate layout tag (include/msda_hip.h MSDA_COORD_LEVEL_MAJOR): loc / aw (B, M, L, Lq, P)
 
 _timer = None  # KernelTimer while bench.py measures; None otherwise
 
@@ -141,7 +143,32 @@ def _coord_dtype(value):
     return torch.float64 if value.dtype == torch.float64 else torch.float32
 
 
-def _check_inputs(value, loc, aw, shapes, starts):
+def _coord_dims(loc, layout):
+    """(Lq, M, L, P) of a coordinate tensor in the reference layout (B, Lq, M, L, P) or level-major
+    (B, M, L, Lq, P)."""
+    if layout == LEVEL_MAJOR:
+        _, M, L, Lq, P = loc.shape
+    else:
+        _, Lq, M, L, P = loc.shape
+    return Lq, M, L, P
+
+
+def level_major_ok(value, shapes, Lq, P):
+    """Whether an MSDA call on ``value`` (B, S, M, D) with Lq queries and P points may keep its
+    coordinates level-major (msda_hip_level_major_ok: its backward takes the row-block path fed by
+    the forward's tile intervals, and the prologue's level-major kernel covers it)."""
+    import os
+    if os.environ.get("MSDA_HIP_LEVEL_MAJOR", "1") == "0":  # A/B switch: the reference layout throughout
+        return False
+    if not value.is_cuda or value.dtype not in _native.DTYPE_TAGS or value.dim() != 4:
+        return False
+    B, S, M, D = value.shape
+    lib = _native.load_library()
+    return bool(lib.msda_hip_level_major_ok(_native.DTYPE_TAGS[value.dtype], _native.host_i64_array(shapes),
+                                            len(shapes), B, S, M, D, Lq, P))
+
+
+def _check_inputs(value, loc, aw, shapes, starts, layout=0):
     if value.dtype not in _native.DTYPE_TAGS:
         raise TypeError(f"MSDA: unsupported value dtype {value.dtype}")
     for name, t in (("value", value), ("sampling_loc", loc), ("attn_weight", aw)):
@@ -158,7 +185,8 @@ def _check_inputs(value, loc, aw, shapes, starts):
                          f"{tuple(loc.shape)} / {tuple(aw.shape)}")
     if tuple(loc.shape) != tuple(aw.shape):
         raise ValueError(f"sampling_loc {tuple(loc.shape)} and attn_weight {tuple(aw.shape)} differ")
-    if loc.shape[0] != B or loc.shape[2] != M or loc.shape[3] != len(shapes):
+    _, lm, ll, _ = _coord_dims(loc, layout)
+    if loc.shape[0] != B or lm != M or ll != len(shapes):
         raise ValueError(f"shape mismatch: value {tuple(value.shape)}, loc {tuple(loc.shape)}, "
                          f"{len(shapes)} levels")
     if len(shapes) > _native.MAX_LEVELS:
@@ -170,18 +198,20 @@ def _check_inputs(value, loc, aw, shapes, starts):
         raise ValueError(f"levels {shapes} starting at {starts} exceed spatial size {S}")
 
 
-def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_tiles=False):
+def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_tiles=False, layout=0):
     """out (B, Lq, M*D) = MSDA(value (B,S,M,D), loc/aw (B,Lq,M,L,P)) on the HIP kernel.
 
     ``want_tiles``: also return the backward's row intervals when the call's backward takes the
-    row-block path (``msda_hip_forward_tiles``; None otherwise): ``(out, tiles)``."""
-    _check_inputs(value, loc, aw, shapes, starts)
+    row-block path (``msda_hip_forward_tiles``; None otherwise): ``(out, tiles)``.
+    ``layout=LEVEL_MAJOR``: loc / aw are (B, M, L, Lq, P) (``msda_hip_forward_tiles_layout``; the
+    call must satisfy ``level_major_ok``; tiles are always written)."""
+    _check_inputs(value, loc, aw, shapes, starts, layout)
     lib = _native.load_library()
     B, S, M, D = value.shape
-    Lq, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
+    Lq, _, L, P = _coord_dims(loc, layout)
     out = torch.empty((B, Lq, M * D), dtype=value.dtype, device=value.device)
     tiles = None
-    if want_tiles:
+    if want_tiles or layout == LEVEL_MAJOR:
         nb = lib.msda_hip_forward_tiles_bytes(_native.DTYPE_TAGS[value.dtype], _native.host_i64_array(shapes), L,
                                               B, S, M, D, Lq, P)
         if nb:
@@ -193,7 +223,11 @@ def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_til
             _native.host_i64_array(shapes), _native.host_i64_array(starts), L,
             loc.data_ptr(), aw.data_ptr(), out.data_ptr())
     tail = (B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
-    if tiles is None:
+    if layout == LEVEL_MAJOR:
+        if tiles is None:
+            raise RuntimeError("MSDA: the level-major coordinate layout needs a row-block call (level_major_ok)")
+        rc = lib.msda_hip_forward_tiles_layout(*args, tiles.data_ptr(), *tail[:-1], layout, tail[-1])
+    elif tiles is None:
         rc = lib.msda_hip_forward(*args, *tail)
     else:
         rc = lib.msda_hip_forward_tiles(*args, tiles.data_ptr(), *tail)
@@ -205,13 +239,14 @@ def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_til
 
 
 def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="border",
-                  need_value=True, need_loc=True, need_aw=True, tiles=None):
+                  need_value=True, need_loc=True, need_aw=True, tiles=None, layout=0):
     """(grad_value, grad_loc, grad_aw) of msda_forward; unneeded ones come back None.
-    ``tiles``: the row intervals ``msda_forward(..., want_tiles=True)`` returned for these inputs."""
-    _check_inputs(value, loc, aw, shapes, starts)
+    ``tiles``: the row intervals ``msda_forward(..., want_tiles=True)`` returned for these inputs
+    (required with ``layout=LEVEL_MAJOR``; grad_loc / grad_aw then come back level-major too)."""
+    _check_inputs(value, loc, aw, shapes, starts, layout)
     grad_output = grad_output.to(value.dtype).contiguous()
     B, S, M, D = value.shape
-    Lq, L, P = loc.shape[1], loc.shape[3], loc.shape[4]
+    Lq, _, L, P = _coord_dims(loc, layout)
     if tuple(grad_output.shape) != (B, Lq, M * D):
         raise ValueError(f"grad_output must be {(B, Lq, M * D)}, got {tuple(grad_output.shape)}")
     lib = _native.load_library()
@@ -233,7 +268,11 @@ def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="bor
             loc.data_ptr(), aw.data_ptr(), grad_output.data_ptr(),
             ptr(gv), ptr(gl), ptr(ga), ptr(ws))
     tail = (B, S, M, D, Lq, P, _native.PAD_TAGS[padding_mode], _native.stream_handle(value.device))
-    if tiles is None:
+    if layout == LEVEL_MAJOR:
+        if tiles is None:
+            raise RuntimeError("MSDA: a level-major backward needs the forward's tile intervals")
+        rc = lib.msda_hip_backward_tiles_layout(*args, tiles.data_ptr(), *tail[:-1], layout, tail[-1])
+    elif tiles is None:
         rc = lib.msda_hip_backward(*args, *tail)
     else:
         rc = lib.msda_hip_backward_tiles(*args, tiles.data_ptr(), *tail)
@@ -250,14 +289,17 @@ class MSDAFunction(Function):
     grads for value / loc / aw, ``once_differentiable`` like the reference."""
 
     @staticmethod
-    def forward(ctx, value, loc, aw, shapes, starts, padding_mode):
+    def forward(ctx, value, loc, aw, shapes, starts, padding_mode, layout=0):
         from . import _trace
         _trace.hit("msda_" + str(value.dtype).replace("torch.", ""))
-        ctx.meta = (shapes, starts, padding_mode)
+        if layout == LEVEL_MAJOR:
+            _trace.hit("msda_level_major")
+        ctx.meta = (shapes, starts, padding_mode, layout)
         ctx.save_for_backward(value, loc, aw)
         # the row intervals of the row-block backward come with the forward (it reads loc anyway)
-        if any(ctx.needs_input_grad[:3]):
-            out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode, want_tiles=True)
+        if any(ctx.needs_input_grad[:3]) or layout == LEVEL_MAJOR:
+            out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode, want_tiles=True,
+                                          layout=layout)
         else:
             out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode), None
         return out
@@ -266,18 +308,19 @@ class MSDAFunction(Function):
     @once_differentiable
     def backward(ctx, grad_output):
         value, loc, aw = ctx.saved_tensors
-        shapes, starts, padding_mode = ctx.meta
+        shapes, starts, padding_mode, layout = ctx.meta
         nv, nl, na = ctx.needs_input_grad[:3]
         gv, gl, ga = msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode,
-                                   need_value=nv, need_loc=nl, need_aw=na, tiles=ctx.tiles)
+                                   need_value=nv, need_loc=nl, need_aw=na, tiles=ctx.tiles, layout=layout)
         ctx.tiles = None
         if gv is not None:
             gv._mfl_private = True  # fresh, referenced by nothing else: consumers may write it in place
-        return gv, gl, ga, None, None, None
+        return gv, gl, ga, None, None, None, None
 
 
-def msda_apply(value, shapes, starts, loc, aw, padding_mode="border"):
-    """Differentiable MSDA on normalised inputs: value (B,S,M,D); loc, aw (B,Lq,M,L,P).
+def msda_apply(value, shapes, starts, loc, aw, padding_mode="border", layout=0):
+    """Differentiable MSDA on normalised inputs: value (B,S,M,D); loc, aw (B,Lq,M,L,P) — or
+    (B,M,L,Lq,P) with ``layout=LEVEL_MAJOR`` (the fused MSDeformAttn path's internal layout).
 
     Casts loc / aw to the coordinate dtype (fp32, or fp64 for fp64 values) and makes
     everything contiguous outside the Function, so autograd tracks those copies."""
@@ -285,7 +328,7 @@ def msda_apply(value, shapes, starts, loc, aw, padding_mode="border"):
     value = value.contiguous()
     loc = loc.to(cd).contiguous()
     aw = aw.to(cd).contiguous()
-    return MSDAFunction.apply(value, loc, aw, tuple(shapes), tuple(starts), padding_mode)
+    return MSDAFunction.apply(value, loc, aw, tuple(shapes), tuple(starts), padding_mode, layout)
 
 
 # --- MSDA prologue -------------------------------------------------------
@@ -350,9 +393,10 @@ def prologue_backward(grad_loc, grad_aw, aw, offsets, ref, shapes, need_off=True
     return g_off, g_log, g_ref
 
 
-def prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes):
+def prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes, layout=0):
     """``prologue_forward`` on the output of ONE query-projection GEMM: y (B*Lq, 2*M*L*P), each
-    row [sampling offsets | attention logits] (``msda_hip_prologue_forward_ex``, read in place)."""
+    row [sampling offsets | attention logits] (``msda_hip_prologue_forward_ex``, read in place).
+    ``layout=LEVEL_MAJOR``: loc / aw written (B, M, L, Lq, P) (``msda_hip_prologue_forward_layout``)."""
     n = M * L * P
     if y.dim() != 2 or tuple(y.shape) != (B * Lq, 2 * n) or not y.is_contiguous() or not y.is_cuda:
         raise ValueError(f"MSDA prologue rows: y must be a contiguous device (B*Lq, 2*M*L*P) tensor, got "
@@ -361,21 +405,22 @@ def prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes):
     if ref.dtype != cd or tuple(ref.shape[:3]) != (B, Lq, L) or not ref.is_contiguous():
         raise ValueError(f"MSDA prologue rows: reference_points {tuple(ref.shape)} {ref.dtype}")
     lib = _native.load_library()
-    loc = torch.empty((B, Lq, M, L, P), dtype=cd, device=y.device)
+    loc = torch.empty((B, M, L, Lq, P) if layout == LEVEL_MAJOR else (B, Lq, M, L, P), dtype=cd, device=y.device)
     aw = torch.empty_like(loc)
     base = y.data_ptr()
-    rc = lib.msda_hip_prologue_forward_ex(
+    rc = lib.msda_hip_prologue_forward_layout(
         base, base + n * y.element_size(), _native.DTYPE_TAGS[y.dtype], ref.data_ptr(), ref.shape[3],
-        _native.host_i64_array(shapes), L, B, Lq, M, P, 2 * n, loc.data_ptr(), aw.data_ptr(),
+        _native.host_i64_array(shapes), L, B, Lq, M, P, 2 * n, layout, loc.data_ptr(), aw.data_ptr(),
         _native.stream_handle(y.device))
-    _native.check(rc, "msda_hip_prologue_forward_ex")
+    _native.check(rc, "msda_hip_prologue_forward_layout")
     return loc, aw
 
 
-def prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, shapes, need_ref=True):
+def prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, shapes, need_ref=True, layout=0):
     """``prologue_backward`` into ONE (B*Lq, 2*M*L*P) buffer of [grad offsets | grad logits] rows
-    (the dgrad GEMM's input) -> (g2, grad_ref or None)."""
-    B, Lq, M, L, P = aw.shape
+    (the dgrad GEMM's input) -> (g2, grad_ref or None); grad_loc / grad_aw / aw in ``layout``."""
+    B = aw.shape[0]
+    Lq, M, L, P = _coord_dims(aw, layout)
     n = M * L * P
     cd = aw.dtype
     lib = _native.load_library()
@@ -384,11 +429,11 @@ def prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, shapes, need_ref=True)
     g2 = torch.empty_like(y)
     g_ref = torch.empty_like(ref) if need_ref else None
     base, ybase = g2.data_ptr(), y.data_ptr()
-    rc = lib.msda_hip_prologue_backward_ex(
+    rc = lib.msda_hip_prologue_backward_layout(
         grad_loc.data_ptr(), grad_aw.data_ptr(), aw.data_ptr(), ybase, _native.DTYPE_TAGS[y.dtype], ref.data_ptr(),
-        ref.shape[3], _native.host_i64_array(shapes), L, B, Lq, M, P, 2 * n, base, base + n * g2.element_size(),
-        None if g_ref is None else g_ref.data_ptr(), _native.stream_handle(y.device))
-    _native.check(rc, "msda_hip_prologue_backward_ex")
+        ref.shape[3], _native.host_i64_array(shapes), L, B, Lq, M, P, 2 * n, layout, base,
+        base + n * g2.element_size(), None if g_ref is None else g_ref.data_ptr(), _native.stream_handle(y.device))
+    _native.check(rc, "msda_hip_prologue_backward_layout")
     return g2, g_ref
 
 

@@ -477,3 +477,88 @@ torch.save([t.cpu() for t in r1] + [t.cpu() for t in r2], sys.argv[1])
         assert torch.equal(a, b)
     for a, b in zip(d[:3], outs["0"][:3]):
         torch.testing.assert_close(a.float(), b.float(), rtol=2e-2, atol=2e-2)
+
+
+def _to_level_major(t):
+    """(B, Lq, M, L, P) -> the level-major coordinate layout (B, M, L, Lq, P), contiguous."""
+    return t.permute(0, 2, 3, 1, 4).contiguous()
+
+
+def _from_level_major(t):
+    return t.permute(0, 3, 1, 2, 4).contiguous()
+
+
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("case", [0, 5, 6])
+def test_level_major_layout_equals_reference_layout(dev, monkeypatch, case, padding):
+    """Coordinates kept level-major (MSDA_COORD_LEVEL_MAJOR, (B, M, L, Lq, P): the fused module
+    path's layout) give the reference layout's forward and backward bit for bit: every row block
+    visits the same samples in the same order, only the coordinate addresses differ."""
+    monkeypatch.delenv("MSDA_HIP_BWD_WIN", raising=False)
+    shapes, B, M, Lq, P, kind = WIN_CASES[case]
+    D = 64
+    value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=90 + case)
+    if kind == "local":
+        loc = local_locations(B, Lq, M, shapes, P, seed=91 + case)
+    starts = O.level_starts(shapes)
+    v, lc, a, g = (t.cuda() for t in (value, loc, aw, gout))
+    assert msda.level_major_ok(v, shapes, Lq, P)
+    out, tiles = msda.msda_forward(v, shapes, starts, lc, a, padding, want_tiles=True)
+    ref = msda.msda_backward(v, shapes, starts, lc, a, g, padding, tiles=tiles)
+    lcm, am = _to_level_major(lc), _to_level_major(a)
+    out_m, tiles_m = msda.msda_forward(v, shapes, starts, lcm, am, padding, layout=msda.LEVEL_MAJOR)
+    assert torch.equal(out, out_m) and torch.equal(tiles, tiles_m)
+    gv, gl, ga = msda.msda_backward(v, shapes, starts, lcm, am, g, padding, tiles=tiles_m, layout=msda.LEVEL_MAJOR)
+    assert torch.equal(ref[0], gv)
+    assert torch.equal(ref[1], _from_level_major(gl))
+    assert torch.equal(ref[2], _from_level_major(ga))
+
+
+def test_level_major_refused_without_row_block_path(dev):
+    """A call whose backward does not take the row-block path (decoder-like: 100 queries) is not
+    level-major capable, and the layout entry points refuse it (no silent misread)."""
+    shapes, B, M, D, Lq, P = [1024, 512, 256, 128], 2, 8, 64, 100, 4
+    value, loc, aw, gout = (t.cuda() for t in rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=95))
+    assert not msda.level_major_ok(value, shapes, Lq, P)
+    with pytest.raises(RuntimeError, match="level-major"):
+        msda.msda_forward(value, shapes, O.level_starts(shapes), _to_level_major(loc), _to_level_major(aw),
+                          layout=msda.LEVEL_MAJOR)
+
+
+@pytest.mark.parametrize("layout", ["reference", "level_major"])
+def test_bf16_T1024_bench_instantiation_matches_oracle(dev, monkeypatch, layout):
+    """The configs[1] encoder call exactly as the bench step runs it: bf16 values, B=8, T=1024
+    (S = Lq = 1920), M=8, D=64, P=4, no environment forcing, through the autograd Function — the
+    forward writes the tile intervals (msda_fwd16_tiles_kernel) and the backward takes the
+    row-block MFMA kernel fed by them; "level_major": with the module path's level-major
+    coordinates.  Clips 0 and 7 against the oracle on the same bf16-rounded inputs in fp32
+    (reference semantics attention.py:331-383)."""
+    for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH",
+              "MSDA_HIP_LEVEL_MAJOR"):
+        monkeypatch.delenv(k, raising=False)
+    shapes, B, M, D, P = [1024, 512, 256, 128], 8, 8, 64, 4
+    Lq = sum(shapes)
+    value, _, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=97, lo=0.0, hi=1.0)
+    loc = local_locations(B, Lq, M, shapes, P, seed=98)
+    starts = O.level_starts(shapes)
+    lm = layout == "level_major"
+    v = value.cuda().requires_grad_(True)
+    lc = (_to_level_major(loc) if lm else loc).cuda().requires_grad_(True)
+    a = (_to_level_major(aw) if lm else aw).cuda().requires_grad_(True)
+    assert msda.level_major_ok(v, shapes, Lq, P)
+    PKG._trace.clear()
+    out = msda.msda_apply(v, shapes, starts, lc, a, "border", layout=msda.LEVEL_MAJOR if lm else 0)
+    out.backward(gout.cuda())
+    torch.cuda.synchronize()
+    assert PKG._trace.hits.get("msda_bfloat16", 0) == 1
+    assert (PKG._trace.hits.get("msda_level_major", 0) == 1) == lm
+    gl, ga = (_from_level_major(t.grad) if lm else t.grad for t in (lc, a))
+    eps = 2 ** -8
+    for b in (0, B - 1):
+        v32, g32 = value[b:b + 1].float(), gout[b:b + 1].float()
+        r_out = O.msda_forward(_np(v32), shapes, _np(loc[b:b + 1]), _np(aw[b:b + 1]))
+        r_gv, r_gl, r_ga = O.msda_backward(_np(v32), shapes, _np(loc[b:b + 1]), _np(aw[b:b + 1]), _np(g32))
+        np.testing.assert_allclose(_np(out[b:b + 1]), r_out, rtol=eps, atol=eps * np.abs(r_out).max())
+        np.testing.assert_allclose(_np(v.grad[b:b + 1]), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
+        np.testing.assert_allclose(_np(ga[b:b + 1]), r_ga, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(_np(gl[b:b + 1]), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))

@@ -168,3 +168,62 @@ def test_query_prologue_matches_two_projection_form(dev, Lq, ref_dim):
     for n, u, v in zip(("x", "ref", "w_off", "b_off", "w_aw", "b_aw"), g1, g2):
         err = (u.float() - v.float()).norm() / v.float().norm().clamp_min(1e-12)
         assert err < 2e-2, (n, err.item())
+
+
+@pytest.mark.parametrize("ref_dim", [1, 2])
+@pytest.mark.parametrize("B,Lq,M,L,P", [(8, 1920, 8, 4, 4), (2, 77, 4, 2, 8), (3, 45, 8, 1, 16)])
+def test_level_major_rows_equal_reference_layout(dev, ref_dim, B, Lq, M, L, P):
+    """The level-major prologue (msda_hip_prologue_*_layout with MSDA_COORD_LEVEL_MAJOR: loc / aw
+    (B, M, L, Lq, P), one workgroup per 32 queries x all heads) against the reference-layout
+    kernels on one [offsets | logits] row buffer: locations, weights and the offsets / logits
+    gradients bit for bit; the reference-point gradient sums the heads in another order (fp32
+    rounding only)."""
+    shapes = [1024, 512, 256, 128][:L] if L <= 4 else [64] * L
+    n = M * L * P
+    g = torch.Generator().manual_seed(3)
+    y = (torch.randn(B * Lq, 2 * n, generator=g) * 2).to(dev, torch.bfloat16)
+    ref = torch.rand(B, Lq, L, ref_dim, generator=g).to(dev)
+    gl = torch.randn(B, Lq, M, L, P, generator=g).to(dev)
+    ga = torch.randn(B, Lq, M, L, P, generator=g).to(dev)
+    loc, aw = msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes)
+    loc_m, aw_m = msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes, layout=msda.LEVEL_MAJOR)
+    assert tuple(loc_m.shape) == (B, M, L, Lq, P)
+    assert torch.equal(loc, loc_m.permute(0, 3, 1, 2, 4)) and torch.equal(aw, aw_m.permute(0, 3, 1, 2, 4))
+    g2, gr = msda.prologue_backward_rows(gl, ga, aw, y, ref, shapes)
+    lmj = lambda t: t.permute(0, 2, 3, 1, 4).contiguous()  # noqa: E731
+    g2m, grm = msda.prologue_backward_rows(lmj(gl), lmj(ga), aw_m, y, ref, shapes, layout=msda.LEVEL_MAJOR)
+    assert torch.equal(g2, g2m)
+    torch.testing.assert_close(grm, gr, rtol=1e-5, atol=1e-6)
+
+
+def test_module_level_major_path_matches_reference_layout(dev, monkeypatch):
+    """MSDeformAttn at the bench's encoder call under bf16 autocast (B=8, T=1024 pyramid, 8 heads):
+    the fused path keeps the coordinates level-major between the prologue, the MSDA kernels and
+    their backward; against the same module with the reference layout throughout
+    (MSDA_HIP_LEVEL_MAJOR=0): the output bit for bit, every gradient to fp32 rounding of the
+    reference-point sums."""
+    torch.manual_seed(1)
+    attn = PKG.models.modules.attention.MSDeformAttn(512, 4, 8, 4).to(dev)
+    shapes = [1024, 512, 256, 128]
+    S = sum(shapes)
+    g = torch.Generator().manual_seed(2)
+    q = torch.randn(8, S, 512, generator=g).to(dev)
+    x = torch.randn(8, S, 512, generator=g).to(dev)
+    ref = torch.cat([(torch.arange(t) + 0.5) / t for t in shapes]).view(1, S, 1, 1).expand(8, S, 4, 1).to(dev)
+    gout = torch.randn(8, S, 512, generator=g).to(dev)
+    st, lsi = torch.tensor(shapes, device=dev), torch.tensor([0, 1024, 1536, 1792], device=dev)
+    runs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("MSDA_HIP_LEVEL_MAJOR", flag)
+        attn.zero_grad()
+        qq, xx = q.clone().requires_grad_(True), x.clone().requires_grad_(True)
+        PKG._trace.clear()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            y = attn(qq, ref, xx, st, lsi)
+        y.float().backward(gout)
+        torch.cuda.synchronize()
+        assert (PKG._trace.hits.get("msda_level_major", 0) > 0) == (flag == "1")
+        runs.append((y.detach(), qq.grad, xx.grad) + tuple(p.grad.clone() for p in attn.parameters()))
+    assert torch.equal(runs[0][0], runs[1][0])
+    for a, b in zip(runs[0][1:], runs[1][1:]):
+        torch.testing.assert_close(a, b, rtol=2e-3, atol=1e-5)

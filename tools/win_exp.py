@@ -1,0 +1,42 @@
+#!/usr/bin/env python3
+"""Where the row-block backward's time goes: win_bwd_kernel at the bench's encoder call (B=8,
+T=1024 pyramid, bf16) with parts skipped through MSDA_HIP_WIN_EXP (profiling only; results
+wrong): 1 = no grad_value MFMA / C build, 2 = no coordinate-gradient stores, 4 = no dots and no
+coordinate gradients.  HIP-event averages over --iters launches, plus the forward for reference."""
+import argparse
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from msda_microbench import make, timeit, msda  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--iters", type=int, default=50)
+    ap.add_argument("--regimes", default="init,trained")
+    ap.add_argument("--exps", default="0,1,2,4,5,7")
+    ap.add_argument("--T", type=int, default=1024)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    shapes = [args.T, args.T // 2, args.T // 4, args.T // 8]
+    S, Lq, M, P, B = sum(shapes), sum(shapes), 8, 4, 8
+    starts = [sum(shapes[:i]) for i in range(4)]
+    for regime in args.regimes.split(","):
+        value, loc, aw, gout = make(regime, B, Lq, shapes, M, P, torch.bfloat16, dev)
+        _, tiles = msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True)
+        us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True), args.iters)
+        print(json.dumps({"regime": regime, "T": args.T, "kernel": "fwd_tiles", "us": round(us, 2)}), flush=True)
+        for e in args.exps.split(","):
+            os.environ["MSDA_HIP_WIN_EXP"] = e
+            us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout, tiles=tiles), args.iters)
+            print(json.dumps({"regime": regime, "T": args.T, "kernel": "bwd_win", "exp": int(e), "us": round(us, 2)}),
+                  flush=True)
+        os.environ["MSDA_HIP_WIN_EXP"] = "0"
+
+
+if __name__ == "__main__":
+    main()
