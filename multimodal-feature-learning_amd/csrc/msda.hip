@@ -529,6 +529,186 @@ __global__ __launch_bounds__(256) void msda_fwd16_tiles_kernel(
   }
 }
 
+// LDS-staged variant of msda_fwd16_tiles_kernel (same items, same output and tile intervals bit
+// for bit).  The workgroup's 32 queries of one head sample each level inside the row interval the
+// tiles kernel reduces anyway; here the interval is reduced FIRST, the value rows of every level
+// whose interval fits the workgroup's row budget are copied into LDS once (8 lanes a 128-B row,
+// coalesced), and the taps then read LDS instead of gathering 16-B fragments from L2: an encoder
+// tile touches ~90 rows per head (~12 KB) where its taps gathered 128 KB.  Levels that do not fit
+// (a coarse-level query tile spans a quarter of the finest level) keep the global gathers, as
+// does any tap outside its level's staged rows (never, by construction: make_taps and
+// win_sample_rows give the same rows).
+constexpr int kFwdStageRows = 256;  // staged rows a workgroup (144-B stride: 36 KB)
+constexpr int kFwdRowStride = 144;
+
+template <typename scalar_t, bool ZEROS, int P, bool LM>
+__global__ __launch_bounds__(256) void msda_fwd16_lds_kernel(
+    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    scalar_t* __restrict__ out, int2* __restrict__ tiles, const Levels lv, const int L, const int S, const int M,
+    const int Lq, const int ntile) {
+  constexpr int VEC = 8, D = 64, NL = kLPMax / P;
+  __shared__ int2 s_iv[4][NL];
+  __shared__ int s_off[NL], s_lo[NL], s_n[NL + 1];
+  __shared__ __attribute__((aligned(16))) unsigned char s_rows[kFwdStageRows * kFwdRowStride];
+  const unsigned wg = xcd_block(blockIdx.x, gridDim.x);
+  const unsigned bm = wg / (unsigned)ntile;
+  const int tile = (int)(wg % (unsigned)ntile);
+  const int m = (int)(bm % (unsigned)M);
+  const long long b = bm / (unsigned)M;
+  const int i = threadIdx.x >> 3, lg = threadIdx.x & 7;
+  const int q = tile * kWinQT + i;
+  const int LP = L * P;
+  const int rs = M * D;
+  int lo[NL], hi[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    lo[l] = kWinNone;
+    hi[l] = -kWinNone;
+  }
+  float lr[kLPMax], ar[kLPMax];
+  const bool valid = q < Lq;
+  const long long item = (b * Lq + (valid ? q : 0)) * M + m;
+  if (valid) {
+    if constexpr (LM) {
+      const long long c0 = ((b * M + m) * L * Lq + q) * P;
+      load_coords16_lm(loc + c0, (long long)Lq * P, L, P, lr);
+      load_coords16_lm(aw + c0, (long long)Lq * P, L, P, ar);
+    } else {
+      load_coords16(loc + item * LP, LP, lr);
+      load_coords16(aw + item * LP, LP, ar);
+    }
+#pragma unroll
+    for (int j = 0; j < kLPMax; ++j) {
+      if (j < LP) {
+        const int2 r = win_sample_rows(lr[j], lv.T[j / P], ZEROS);
+        lo[j / P] = min(lo[j / P], r.x);
+        hi[j / P] = max(hi[j / P], r.y);
+      }
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      lo[l] = min(lo[l], __shfl_xor(lo[l], o));
+      hi[l] = max(hi[l], __shfl_xor(hi[l], o));
+    }
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int l = 0; l < NL; ++l) s_iv[w][l] = make_int2(lo[l], hi[l]);
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < L) {
+    int2 iv = s_iv[0][threadIdx.x];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) {
+      const int2 o = s_iv[v][threadIdx.x];
+      iv.x = min(iv.x, o.x);
+      iv.y = max(iv.y, o.y);
+    }
+    tiles[((long long)bm * L + threadIdx.x) * ntile + tile] = iv;
+    s_iv[0][threadIdx.x] = iv;  // (each thread rewrites only its own level's slot)
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // levels staged greedily in order while they fit the row budget
+    int used = 0;
+    for (int l = 0; l < L; ++l) {
+      const int a = max(s_iv[0][l].x, 0), z = min(s_iv[0][l].y, lv.T[l] - 1);
+      const int n = z - a + 1;
+      if (n > 0 && used + n <= kFwdStageRows) {
+        s_off[l] = used;
+        s_lo[l] = a;
+        s_n[l] = n;
+        used += n;
+      } else {
+        s_off[l] = -1;
+        s_lo[l] = 0;
+        s_n[l] = 0;
+      }
+    }
+    s_n[NL] = used;
+  }
+  __syncthreads();
+  const int used = s_n[NL];
+  const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D + lg * VEC;
+  {  // stage: row k of the budget is row s_lo[l] + (k - s_off[l]) of its level l (8 loads in flight)
+    constexpr int kU = 8;
+    uint4 v[kU];
+    int dst[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) {
+      const int k = i + 32 * u;
+      dst[u] = -1;
+      v[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (k < used) {
+        // (levels are packed in level order: the staged level holding k is the last with s_off <= k)
+        int l = 0;
+        for (int x = 0; x < L; ++x)
+          if (s_off[x] >= 0 && k >= s_off[x]) l = x;
+        const int row = s_lo[l] + (k - s_off[l]);
+        v[u] = *reinterpret_cast<const uint4*>(vb + (long long)(lv.start[l] + row) * rs);
+        dst[u] = k;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kU; ++u)
+      if (dst[u] >= 0) *reinterpret_cast<uint4*>(s_rows + dst[u] * kFwdRowStride + lg * 16) = v[u];
+  }
+  __syncthreads();
+  if (!valid) return;
+  int soff[NL], slo[NL], sn[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    soff[l] = s_off[l];
+    slo[l] = s_lo[l];
+    sn[l] = s_n[l];
+  }
+  f32x2 acc2[VEC / 2];
+#pragma unroll
+  for (int e = 0; e < VEC / 2; ++e) acc2[e] = f32x2{0.f, 0.f};
+  auto fetch = [&](bool ok, int l, int row) -> uint4 {
+    if (!ok) return make_uint4(0u, 0u, 0u, 0u);
+    const int k = row - slo[l];
+    if (soff[l] >= 0 && (unsigned)k < (unsigned)sn[l])
+      return *reinterpret_cast<const uint4*>(s_rows + (soff[l] + k) * kFwdRowStride + lg * 16);
+    return *reinterpret_cast<const uint4*>(vb + (long long)(lv.start[l] + row) * rs);
+  };
+#pragma unroll
+  for (int j0 = 0; j0 < kLPMax; j0 += 4) {
+    if (j0 < LP) {
+      uint4 r0[4], r1[4];
+      float c0[4], c1[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int l = (j0 + u) / P;
+        const Taps<float> t = make_taps<float, ZEROS>(lr[j0 + u], lv.T[l]);
+        r0[u] = fetch(t.ok0, l, t.i0);
+        r1[u] = fetch(t.ok1, l, t.i1);
+        c0[u] = ar[j0 + u] * t.w0;
+        c1[u] = ar[j0 + u] * t.w1;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        f32x2 x0[VEC / 2], x1[VEC / 2];
+        cvt16x2<scalar_t, VEC>(r0[u], x0);
+        cvt16x2<scalar_t, VEC>(r1[u], x1);
+        const f32x2 k0{c0[u], c0[u]}, k1{c1[u], c1[u]};
+#pragma unroll
+        for (int e = 0; e < VEC / 2; ++e) acc2[e] = pk_fma(x1[e], k1, pk_fma(x0[e], k0, acc2[e]));
+      }
+    }
+  }
+  float acc[VEC];
+#pragma unroll
+  for (int e = 0; e < VEC / 2; ++e) {
+    acc[2 * e] = acc2[e].x;
+    acc[2 * e + 1] = acc2[e].y;
+  }
+  store_vec<scalar_t, VEC>(out + item * D + lg * VEC, acc);
+}
+
 // ---------------------------------------------------------------------------------
 // backward
 // ---------------------------------------------------------------------------------
@@ -2174,6 +2354,8 @@ int fast16_group(const Problem& pr) {
   return (int)g;
 }
 
+int env_int(const char* name, int dflt);
+
 template <typename scalar_t, typename coord_t, int VEC>
 int run_forward(const Problem& pr, const void* value, const void* loc, const void* aw, void* out,
                 int pad, hipStream_t st, void* tiles = nullptr, int layout = MSDA_COORD_API) {
@@ -2193,10 +2375,18 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
     if (tiles != nullptr) {  // the caller checked forward_tiles_ok: 16-bit values, D = 64 (G = 8)
       const int ntile = (int)((pr.Lq + kWinQT - 1) / kWinQT);
       const unsigned tblocks = (unsigned)(pr.B * pr.M * ntile);
+      // value rows staged in LDS per workgroup (msda_fwd16_lds_kernel); MSDA_HIP_FWD_LDS=0: gathers
+      const bool fwd_lds = env_int("MSDA_HIP_FWD_LDS", 1) != 0;
       auto* tl = static_cast<int2*>(tiles);
 #define MSDA_FT(Z, PP)                                                                              \
   do {                                                                                            \
-    if (lm)                                                                                       \
+    if (fwd_lds && lm)                                                                            \
+      hipLaunchKernelGGL((msda_fwd16_lds_kernel<scalar_t, Z, PP, true>), dim3(tblocks), dim3(256), 0, st, v, lc, \
+                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
+    else if (fwd_lds)                                                                             \
+      hipLaunchKernelGGL((msda_fwd16_lds_kernel<scalar_t, Z, PP, false>), dim3(tblocks), dim3(256), 0, st, v, lc, \
+                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
+    else if (lm)                                                                                  \
       hipLaunchKernelGGL((msda_fwd16_tiles_kernel<scalar_t, Z, PP, true>), dim3(tblocks), dim3(256), 0, st, v, lc, \
                          a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
     else                                                                                          \

@@ -562,3 +562,25 @@ def test_bf16_T1024_bench_instantiation_matches_oracle(dev, monkeypatch, layout)
         np.testing.assert_allclose(_np(v.grad[b:b + 1]), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
         np.testing.assert_allclose(_np(ga[b:b + 1]), r_ga, rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(_np(gl[b:b + 1]), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))
+
+
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("case", range(len(WIN_CASES)))
+def test_lds_staged_forward_equals_gather_forward(dev, monkeypatch, case, padding):
+    """The LDS-staged tiles forward (msda_fwd16_lds_kernel: each workgroup's per-level row
+    intervals staged in LDS, taps read there; levels over the row budget gathered from global)
+    gives the gathering tiles forward's output and tile intervals bit for bit."""
+    monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
+    shapes, B, M, Lq, P, kind = WIN_CASES[case]
+    value, loc, aw, _ = rand_case(shapes, B, M, 64, Lq, P, torch.bfloat16, seed=100 + case)
+    if kind == "clustered":
+        loc = clustered_locations(B, Lq, M, shapes, P, seed=101 + case)
+    elif kind == "local":
+        loc = local_locations(B, Lq, M, shapes, P, seed=101 + case)
+    starts = O.level_starts(shapes)
+    v, lc, a = (t.cuda() for t in (value, loc, aw))
+    runs = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("MSDA_HIP_FWD_LDS", flag)
+        runs.append(msda.msda_forward(v, shapes, starts, lc, a, padding, want_tiles=True))
+    assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])

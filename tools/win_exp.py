@@ -28,8 +28,21 @@ def main():
     for regime in args.regimes.split(","):
         value, loc, aw, gout = make(regime, B, Lq, shapes, M, P, torch.bfloat16, dev)
         _, tiles = msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True)
-        us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True), args.iters)
-        print(json.dumps({"regime": regime, "T": args.T, "kernel": "fwd_tiles", "us": round(us, 2)}), flush=True)
+        for flag in ("0", "1"):
+            os.environ["MSDA_HIP_FWD_LDS"] = flag
+            us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True), args.iters)
+            print(json.dumps({"regime": regime, "T": args.T, "kernel": "fwd_tiles", "lds": int(flag),
+                              "us": round(us, 2)}), flush=True)
+        lm = msda.LEVEL_MAJOR
+        loc_m, aw_m = loc.permute(0, 2, 3, 1, 4).contiguous(), aw.permute(0, 2, 3, 1, 4).contiguous()
+        us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc_m, aw_m, layout=lm), args.iters)
+        print(json.dumps({"regime": regime, "T": args.T, "kernel": "fwd_tiles_level_major", "lds": 1,
+                          "us": round(us, 2)}), flush=True)
+        _, tiles_m = msda.msda_forward(value, shapes, starts, loc_m, aw_m, layout=lm)
+        us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc_m, aw_m, gout, tiles=tiles_m, layout=lm),
+                    args.iters)
+        print(json.dumps({"regime": regime, "T": args.T, "kernel": "bwd_win_level_major", "us": round(us, 2)}),
+              flush=True)
         for e in args.exps.split(","):
             os.environ["MSDA_HIP_WIN_EXP"] = e
             us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout, tiles=tiles), args.iters)
