@@ -52,11 +52,16 @@ WORKLOADS = {
            "proposals, Hungarian matching of every decoder level, matched-segment crop, context mask, caption "
            "decoder (depth 6, vocab 10000, seq_len 20) teacher-forced on every level, criterion-shaped loss, "
            "backward, AdamW (engine.py:55-134)",
+    "decode": "configs[4]'s caption AR decode at configs[1] scale: UnimodalDeformableDVC inference (T=1024 d=512 L=4, "
+              "100 queries, 6 + 6 layers; proposals, matching, crops, KV-cached greedy decode of 19 words with the "
+              "caption decoder depth 6, vocab 10000) on 8 clips (28 events), no_grad, bf16 autocast "
+              "(engine.py:159-293 evaluate -> unimodal_deformable_dvc.py:304-354)",
 }
 MODELS = {"video": "DeformableDVCCore (UnimodalDeformableDVC proposal path)",
           "multimodal": "MultimodalDVCCore (MultimodalDeformableDVC proposal path)",
           "sparse": "SparseDVCCore (UnimodalSparseDVC proposal path)",
-          "dvc": "UnimodalDeformableDVC (full training forward)"}
+          "dvc": "UnimodalDeformableDVC (full training forward)",
+          "decode": "UnimodalDeformableDVC (inference: greedy caption decode)"}
 
 
 def workload_label(args):
@@ -78,11 +83,13 @@ def parse():
     p.add_argument("--T", type=int, default=1024)
     p.add_argument("--queries", type=int, default=100)
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
-    p.add_argument("--config", default="video", choices=["video", "multimodal", "sparse", "dvc"],
+    p.add_argument("--config", default="video", choices=["video", "multimodal", "sparse", "dvc", "decode"],
                    help="video: configs[1], the headline line.  multimodal: configs[2] (video + audio T_a=50, "
                         "SURVEY 8(d)); sparse: the Sparse-DETR DVC (rho=0.3; top-k width from the shapes, so it is "
                         "graph-captured too); dvc: the full UnimodalDeformableDVC training step (matching on the "
-                        "host: eager), with a per-phase breakdown.  Only 'video' is the BASELINE metric's workload.")
+                        "host: eager), with a per-phase breakdown; decode: inference captions/s (KV-cached "
+                        "greedy decode), the reference's re-decode loop timed on the CPU beside it.  Only 'video' is "
+                        "the BASELINE metric's workload.")
     p.add_argument("--audio-T", type=int, default=50, help="audio length (reference audio_rescale_len)")
     p.add_argument("--dropout", type=float, default=0.1)
     p.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU reference path (rank 0, N=1)")
@@ -121,7 +128,7 @@ def usable_cores():
 
 def build_model(args, device):
     torch.manual_seed(0)
-    if args.config == "dvc":
+    if args.config in ("dvc", "decode"):
         return PKG.dvc_core.build_dvc(num_queries=args.queries, T=args.T, dropout=args.dropout).to(device)
     core = {"video": PKG.dvc_core.DeformableDVCCore, "multimodal": PKG.dvc_core.MultimodalDVCCore,
             "sparse": PKG.dvc_core.SparseDVCCore}[args.config]
@@ -129,7 +136,7 @@ def build_model(args, device):
 
 
 def build_batch(args, rank, device):
-    if args.config == "dvc":
+    if args.config in ("dvc", "decode"):
         return (PKG.dvc_core.synthetic_dvc_batch(args.batch, T=args.T, seed=1000 + rank, device=device),)
     video, mask, dur = PKG.dvc_core.synthetic_clips(args.batch, T=args.T, seed=1000 + rank, device=device)
     if args.config == "multimodal":
@@ -214,6 +221,66 @@ def cpu_baseline(args):
             "cpu": cpu_model_name(),
             "sample": f"{args.cpu_clips} clips (B=1, T={args.T}) fwd+bwd+AdamW in fp32 after 1 warm-up clip; "
                       "oracle/msda_grid_sample.py core (reference attention.py:331-383) + stock PyTorch layers"}
+
+
+def decode_cpu_baseline(args):
+    """The reference's inference path on this host: the same UnimodalDeformableDVC on the CPU in fp32,
+    MSDA core = the per-level grid_sample restatement, captions by the reference's re-decode loop
+    (oracle/cpu_model.py redecode_greedy: the whole decoder over the full prefix for every word) —
+    one clip, 1 warm-up + --cpu-clips timed."""
+    from oracle.cpu_model import oracle_core, reference_decode
+    cores = usable_cores()
+    torch.set_num_threads(cores)
+    model = build_model(args, "cpu").eval()
+    obj = PKG.dvc_core.synthetic_dvc_batch(1, T=args.T, seed=0)
+    n_caps, times = 0, []
+    with torch.no_grad(), oracle_core(PKG), reference_decode(PKG):
+        for i in range(1 + args.cpu_clips):
+            t0 = time.perf_counter()
+            _, caps, _, _, _ = model(obj, is_training=False)
+            if i:
+                times.append(time.perf_counter() - t0)
+                n_caps += caps.shape[0]
+    return {"value": round(n_caps / sum(times), 4), "unit": "captions/s", "cores": cores, "kind": "port",
+            "cpu": cpu_model_name(),
+            "sample": f"{args.cpu_clips} x 1 clip (T={args.T}, {n_caps // max(1, args.cpu_clips)} events) inference in "
+                      "fp32 after 1 warm-up: proposals with the oracle/msda_grid_sample.py core, the last level's "
+                      "captions by the reference's full re-decode per word (unimodal_deformable_dvc.py:318-338; the "
+                      "reference also re-decodes the 5 other levels every word, not charged here)"}
+
+
+def run_decode(args, model, batch, world, rank):
+    """--config decode: inference steps (no_grad, bf16 autocast) of UnimodalDeformableDVC; returns
+    (elapsed s, captions per step, phases ms per step)."""
+    model.eval()
+    obj = batch[0]
+    phases = PhaseTimer()
+    model.forward_stage_proposals = phases.wrap("proposals + matching costs", model.forward_stage_proposals)
+    dec = model.unimodal_caption_decoder
+    dec.greedy_decode = phases.wrap("greedy decode (KV cache, last level)", dec.greedy_decode)
+
+    def step():
+        with torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+            return model(obj, is_training=False)[1].shape[0]
+
+    for _ in range(args.warmup + 1):
+        n_caps = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    phases.on = True
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    phases.on = False
+    ph = phases.summary(args.steps, 1000 * elapsed / args.steps)
+    ph["rest (matching on the host, crops, caption probabilities)"] = ph.pop("backward + loss + AdamW (rest of the step)")
+    return elapsed, n_caps, ph
 
 
 def msda_source_sha16():
@@ -322,6 +389,9 @@ def main():
             dist.broadcast(t.data, src=0)
     use_bf16 = args.dtype == "bf16"
     batch = build_batch(args, rank, device)
+    if args.config == "decode":
+        decode_main(args, model, batch, world, rank, device)
+        return
     graph = bool(args.graph)  # dvc: two graphs around the host matching (StagedDVCLoss)
     trainer = PKG.train_step.FlatGradTrainer(model, loss_fn(args, batch, model), lr=1e-4, weight_decay=1e-4,
                                              max_norm=0.1, use_bf16=use_bf16, graph=graph)
@@ -402,6 +472,42 @@ def main():
             result["phases_ms_per_step"] = graph_phases
         if args.cpu_baseline and world == 1 and args.config == "video":
             result["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def decode_main(args, model, batch, world, rank, device):
+    """bench.py --config decode: one JSON line, captions/s of the whole job (ranks decode their own
+    clips: replicas, no collective), the reference's CPU re-decode beside it."""
+    elapsed, n_caps, ph = run_decode(args, model, batch, world, rank)
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    timer = PKG.msda.KernelTimer()
+    with timer, torch.no_grad(), torch.autocast("cuda", dtype=torch.bfloat16):
+        model(batch[0], is_training=False)
+    torch.cuda.synchronize()
+    if rank == 0:
+        caps = world * n_caps * args.steps
+        result = {
+            "metric": "captions/sec greedy caption decode (UnimodalDeformableDVC inference, T=1024 d=512 L=4, "
+                      "100 queries), MI355X",
+            "value": round(caps / elapsed, 3), "unit": "captions/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "bf16",
+            "data": "synthetic (ActivityNet-shaped features N(0,1), random-init weights)",
+            "config": {"workload": WORKLOADS["decode"], "model": MODELS["decode"], "global_batch": world * args.batch,
+                       "per_gpu_batch": args.batch, "captions_per_step_per_gpu": n_caps, "seq_len": args.T,
+                       "caption_words": 19, "d_model": 512, "levels": 4, "queries": args.queries,
+                       "parallelism": f"replicas{world}", "execution": "eager (host matching inside)"},
+            "clips_per_s": round(world * args.batch * args.steps / elapsed, 3),
+            "phases_ms_per_step": ph,
+            "roofline": roofline(timer.summary(), {}),
+            "cpu_baseline": decode_cpu_baseline(args) if args.cpu_baseline and world == 1 else None,
+        }
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.barrier()

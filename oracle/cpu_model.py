@@ -24,3 +24,52 @@ def oracle_core(pkg):
         yield
     finally:
         att.ms_deform_attn_core_pytorch = original
+
+
+def redecode_greedy(decoder, memory, key_mask, bos, eos, pad, length, faster_eval=False):
+    """The reference's caption decode loop (models/deformable/unimodal_deformable_dvc.py:304-354):
+    for every word the whole decoder re-runs over the full (length)-token prefix, <pad> beyond the
+    words chosen so far, and row w of the last layer's softmax picks word w; a caption stops at its
+    first <eos> unless ``faster_eval``.  Returns (captions, the input of the last word's pass) as the
+    KV-cached ``greedy_decode`` does."""
+    import torch
+    n = memory.shape[0]
+    captions = torch.full((n, length), pad, dtype=torch.int32, device=memory.device)
+    captions[:, 0] = bos
+    mask4 = None if key_mask is None else key_mask[:, None, None, :]
+    done = [False] * n
+    last_input = None
+    look = torch.ones(length, length, dtype=torch.bool, device=memory.device).triu(1)
+    for w in range(1, length):
+        padding = captions == pad
+        tgt_mask = look[None, None] | padding[:, None, None, :]
+        probs = decoder(captions, memory, tgt_mask=tgt_mask, memory_mask=mask4, tgt_padding_mask=padding)[-1]
+        tok = probs.argmax(dim=2)
+        if w == length - 1:
+            last_input = captions.clone()
+        if faster_eval:
+            captions[:, w] = tok[:, w].int()
+        else:
+            for i in range(n):
+                if not done[i]:
+                    captions[i, w] = tok[i, w]
+                    if int(tok[i, w]) == eos:
+                        done[i] = True
+    return captions, last_input
+
+
+@contextlib.contextmanager
+def reference_decode(pkg):
+    """Within the block, ``UnimodalCaptionDecoder.greedy_decode`` is the reference's re-decode loop
+    (``redecode_greedy``) instead of the KV-cached one (bench.py --config decode's CPU leg)."""
+    cls = pkg.models.unimodal_caption_decoder.UnimodalCaptionDecoder
+    original = cls.greedy_decode
+
+    def greedy(self, memory, memory_key_mask, bos, eos, pad, length, faster_eval=False):
+        return redecode_greedy(self, memory, memory_key_mask, bos, eos, pad, length, faster_eval)
+
+    cls.greedy_decode = greedy
+    try:
+        yield
+    finally:
+        cls.greedy_decode = original

@@ -370,3 +370,23 @@ def test_staged_dvc_loss_equals_eager_loss_cpu():
         loss_s = tr._forward_backward((obj,))
     torch.testing.assert_close(loss_s, loss_e.detach(), rtol=1e-6, atol=1e-6)
     assert torch.isfinite(tr.flat_grad).all() and tr.flat_grad.abs().sum() > 0
+
+
+@pytest.mark.parametrize("faster_eval", [False, True])
+def test_oracle_redecode_loop_matches_kv_cached_decode(faster_eval):
+    """bench.py --config decode's CPU leg decodes with oracle/cpu_model.redecode_greedy (the
+    reference's full re-decode per word, unimodal_deformable_dvc.py:318-354): the same captions as
+    the KV-cached greedy_decode, and the same input for the final word's pass."""
+    from oracle.cpu_model import redecode_greedy
+    torch.manual_seed(6)
+    V, d, n, length, K = 40, 32, 4, 9, 15
+    dec = M.unimodal_caption_decoder.UnimodalCaptionDecoder(V, d_model=d, depth=2, num_heads=4, pre_norm=False,
+                                                            return_intermediate=True).double().eval()
+    with torch.no_grad():
+        dec.head.weight.mul_(8.0)
+        mem = torch.randn(n, K, d, dtype=torch.float64)
+        kmask = torch.zeros(n, K, dtype=torch.bool)
+        kmask[2, 7:] = True
+        caps, last = dec.greedy_decode(mem, kmask, 2, 3, 1, length, faster_eval)
+        caps_r, last_r = redecode_greedy(dec, mem, kmask, 2, 3, 1, length, faster_eval)
+    assert torch.equal(caps, caps_r) and torch.equal(last, last_r)
