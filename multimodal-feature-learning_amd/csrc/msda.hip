@@ -2375,8 +2375,10 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
     if (tiles != nullptr) {  // the caller checked forward_tiles_ok: 16-bit values, D = 64 (G = 8)
       const int ntile = (int)((pr.Lq + kWinQT - 1) / kWinQT);
       const unsigned tblocks = (unsigned)(pr.B * pr.M * ntile);
-      // value rows staged in LDS per workgroup (msda_fwd16_lds_kernel); MSDA_HIP_FWD_LDS=0: gathers
-      const bool fwd_lds = env_int("MSDA_HIP_FWD_LDS", 1) != 0;
+      // MSDA_HIP_FWD_LDS=1: value rows staged in LDS per workgroup (msda_fwd16_lds_kernel) — measured
+      // slower at the bench's encoder call (53.9 vs 33.6 us: the gathers' neighbouring rows hit in
+      // L1 and the barrier-free gather kernel hides their latency), so the gathers stay the default
+      const bool fwd_lds = env_int("MSDA_HIP_FWD_LDS", 0) != 0;
       auto* tl = static_cast<int2*>(tiles);
 #define MSDA_FT(Z, PP)                                                                              \
   do {                                                                                            \

@@ -1091,7 +1091,7 @@ def mm_dvc_case(ref, seed=83):
         torch.set_default_dtype(torch.float32)
 
 
-DVC256 = dict(d_model=256, heads=8, ff=1024, enc_layers=2, dec_layers=2, caption_depth=2, num_queries=10,
+DVC256 = dict(d_model=256, heads=4, ff=1024, enc_layers=2, dec_layers=2, caption_depth=2, num_queries=10,
               num_classes=20, T=64, seq_len=12, seed=89)
 
 
@@ -1113,6 +1113,9 @@ def dvc256_args():
     return detr, caption, matcher
 
 
+# the last segment-head layer scaled up: spread-out proposals, so every matching is far from a tie
+DVC256_SCALE = {"segment_embedding.0.layers.2.weight": 6.0}
+
 DVC256_KEYS = ("pred_logits", "pred_segments", "pred_count", "pred_captions", "pred_memory_mask")
 
 
@@ -1126,14 +1129,15 @@ def dvc256_loss(out, w):
 
 
 def deformable_dvc_bf16_d256_case(ref):
-    """The reference's UnimodalDeformableDVC training forward + backward at d=256 (8 heads, 2 + 2 layers,
+    """The reference's UnimodalDeformableDVC training forward + backward at d=256 (4 heads of 64, 2 + 2 layers,
     ff 1024, caption depth 2, T=64, B=2, 10 queries, dropout 0) — the size at which the bench's fused
     bf16 paths engage — run by the reference in fp64 (the truth) and in fp32 under
     torch.autocast('cpu', bfloat16) (the reference's own bf16 run), with deformable_dvc_f64's one
     argument-order fix of the caption-decoder call.  Parameters from regen_parameters (no state_dict
     stored).  The seed is the first from DVC256['seed'] on at which the bf16 run matches the same
-    (clip, prediction) pairs as fp64 on every decoder level, so the GPU test compares like with like;
-    the matching costs' smallest margin (second-best minus chosen cost per target) is stored."""
+    (clip, prediction) pairs as fp64 on every decoder level; the GPU test runs the step on those
+    pairs (the matching's own arithmetic is pinned in fp64 by deformable_dvc_f64).  The matching
+    costs' smallest margin (cost increase when one matched pair is forbidden) is stored."""
     import copy
     import models.matcher as ref_matcher  # noqa: E402
     import models.deformable.unimodal_deformable_dvc as ref_ddvc  # noqa: E402
@@ -1171,7 +1175,7 @@ def deformable_dvc_bf16_d256_case(ref):
         seed = DVC256["seed"] + attempt
         torch.manual_seed(seed)
         model = build()
-        sums = regen_parameters(model, seed)
+        sums = regen_parameters(model, seed, scale=DVC256_SCALE)
         obj32 = sparse_dvc_batch(seed, c["d_model"], c["T"], torch.float32, len(vocab), c["seq_len"])
         gen = torch.Generator().manual_seed(seed + 2)
         with torch.no_grad():
@@ -1189,7 +1193,7 @@ def deformable_dvc_bf16_d256_case(ref):
         same = all(torch.equal(a, b) for a, b in zip(truth["indices"], bf16["indices"])) and all(
             torch.equal(a, b) for la, lb in zip(truth["indices_aux"], bf16["indices_aux"]) for a, b in zip(la, lb))
         print(f"dvc256 seed {seed}: bf16 matching == fp64: {same}; smallest cost margin {margin:.4f}")
-        if same and margin > 5e-2:
+        if same:
             break
     else:
         raise RuntimeError("no seed with the same matching in bf16 and fp64")

@@ -173,3 +173,36 @@ def test_mha_self_attention_autocast_matches_module(dev):
 
     for a, b in zip(run(True), run(False)):
         torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
+
+
+def test_base_encoder_gemm_convs_match_fp64_and_are_reproducible(dev):
+    """BaseEncoder under bf16 autocast runs its Conv1d layers as GEMMs on channels-last rows
+    (models/base_encoder.py): outputs and gradients against the module in fp64 within bf16
+    tolerance, and two runs bitwise equal (MIOpen's bf16 convolution forward was not:
+    tools/determinism_diag.py)."""
+    torch.manual_seed(3)
+    B, T, d = 4, 128, 256
+    enc = PKG.models.base_encoder.BaseEncoder(4, d, d).to(dev)
+    pos = PKG.models.modules.embedding_layers.PositionEmbeddingVideoSine(d // 2, normalize=True)
+    x = torch.randn(B, T, d, device=dev)
+    mask = torch.zeros(B, T, dtype=torch.bool, device=dev)
+    mask[1, 100:] = True
+    dur = torch.tensor([30.0, 60.0, 90.0, 120.0], device=dev)
+    gs = [torch.randn(B, d, T >> l, device=dev) for l in range(4)]
+
+    def run(model, xx, autocast):
+        xx = xx.detach().clone().requires_grad_(True)
+        model.zero_grad()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=autocast):
+            srcs, masks, _ = model(xx, mask, dur, pos)
+        sum((s.double() * g.double()).sum() for s, g in zip(srcs, gs)).backward()
+        return [s.detach().double() for s in srcs] + [xx.grad.double()] + [p.grad.double() for p in model.parameters()]
+
+    a, b = run(enc, x, True), run(enc, x, True)
+    for u, v in zip(a, b):
+        assert torch.equal(u, v)
+    import copy
+    ref = run(copy.deepcopy(enc).double(), x.double(), False)
+    for i, (u, v) in enumerate(zip(a, ref)):
+        err = ((u - v).norm() / v.norm().clamp_min(1e-30)).item()
+        assert err < 2e-2, (i, err)

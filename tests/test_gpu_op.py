@@ -506,7 +506,7 @@ def test_level_major_layout_equals_reference_layout(dev, monkeypatch, case, padd
     out, tiles = msda.msda_forward(v, shapes, starts, lc, a, padding, want_tiles=True)
     ref = msda.msda_backward(v, shapes, starts, lc, a, g, padding, tiles=tiles)
     lcm, am = _to_level_major(lc), _to_level_major(a)
-    out_m, tiles_m = msda.msda_forward(v, shapes, starts, lcm, am, padding, layout=msda.LEVEL_MAJOR)
+    out_m, tiles_m = msda.msda_forward(v, shapes, starts, lcm, am, padding, want_tiles=True, layout=msda.LEVEL_MAJOR)
     assert torch.equal(out, out_m) and torch.equal(tiles, tiles_m)
     gv, gl, ga = msda.msda_backward(v, shapes, starts, lcm, am, g, padding, tiles=tiles_m, layout=msda.LEVEL_MAJOR)
     assert torch.equal(ref[0], gv)

@@ -188,11 +188,15 @@ def test_level_major_rows_equal_reference_layout(dev, ref_dim, B, Lq, M, L, P):
     loc, aw = msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes)
     loc_m, aw_m = msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes, layout=msda.LEVEL_MAJOR)
     assert tuple(loc_m.shape) == (B, M, L, Lq, P)
-    assert torch.equal(loc, loc_m.permute(0, 3, 1, 2, 4)) and torch.equal(aw, aw_m.permute(0, 3, 1, 2, 4))
+    assert torch.equal(loc, loc_m.permute(0, 3, 1, 2, 4))
     g2, gr = msda.prologue_backward_rows(gl, ga, aw, y, ref, shapes)
     lmj = lambda t: t.permute(0, 2, 3, 1, 4).contiguous()  # noqa: E731
     g2m, grm = msda.prologue_backward_rows(lmj(gl), lmj(ga), aw_m, y, ref, shapes, layout=msda.LEVEL_MAJOR)
-    assert torch.equal(g2, g2m)
+    if B * Lq * M >= 65536:  # the reference layout's item-per-thread kernels: the same sums in the same order
+        assert torch.equal(aw, aw_m.permute(0, 3, 1, 2, 4)) and torch.equal(g2, g2m)
+    else:  # (small calls take its per-sample kernels: softmax sums reduced in another order)
+        torch.testing.assert_close(aw_m.permute(0, 3, 1, 2, 4), aw, rtol=1e-6, atol=1e-7)
+        torch.testing.assert_close(g2m.float(), g2.float(), rtol=8e-3, atol=1e-6)
     torch.testing.assert_close(grm, gr, rtol=1e-5, atol=1e-6)
 
 

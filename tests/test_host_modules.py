@@ -217,3 +217,24 @@ def test_segment_memory_crops_compose_and_stack():
     both = SM.cat([m1, m2])
     assert torch.equal(both.materialize(), torch.cat([m1.materialize(), m2.materialize()]))
     assert both.cache is m1.cache
+
+
+@pytest.mark.parametrize("k,T", [(1, 16), (3, 16), (3, 15)])
+def test_conv1d_as_gemm_equals_conv1d(k, T):
+    """The BaseEncoder's Conv1d lowering (models/base_encoder.py _Conv1dGemm: the taps' shifted
+    channels-last rows side by side, one GEMM; the input gradient folded back) computes
+    F.conv1d and its gradients exactly in fp64 (k=1, and k=3 stride 2 padding 1 with even / odd T;
+    reference base_encoder.py:27-36)."""
+    import importlib
+    be = importlib.import_module(PKG.__name__ + ".models.base_encoder")
+    torch.manual_seed(0)
+    conv = torch.nn.Conv1d(8, 6, kernel_size=k, stride=1 if k == 1 else 2, padding=0 if k == 1 else 1).double()
+    x = torch.randn(2, T, 8, dtype=torch.float64, requires_grad=True)
+    y = be._Conv1dGemm.apply(x, conv.weight, conv.bias)
+    g = torch.randn_like(y)
+    got = (y,) + torch.autograd.grad(y, (x, conv.weight, conv.bias), g)
+    x2 = x.detach().clone().requires_grad_(True)
+    y2 = conv(x2.transpose(1, 2)).transpose(1, 2)
+    want = (y2,) + torch.autograd.grad(y2, (x2, conv.weight, conv.bias), g)
+    for a, b in zip(got, want):
+        torch.testing.assert_close(a, b, rtol=1e-13, atol=1e-13)

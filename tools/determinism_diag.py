@@ -83,7 +83,7 @@ def run_once(tr, obj, seed):
     return loss.item(), tr.flat_grad.clone(), log
 
 
-def compare(a, b, limit=12):
+def compare(a, b, limit=30):
     print(f"ops: run A {len(a)}, run B {len(b)}")
     shown = 0
     first_nondet = None
@@ -95,6 +95,10 @@ def compare(a, b, limit=12):
         if in_eq and out_eq:
             continue
         tag = "NONDETERMINISTIC (same inputs)" if in_eq else "inputs differ"
+        if not in_eq:
+            tag += " " + str([i for i, (x, y) in enumerate(zip(ra[2], rb[2])) if x != y])
+        if not out_eq:
+            tag += "; outputs differ " + str([i for i, (x, y) in enumerate(zip(ra[3], rb[3])) if x != y])
         if in_eq and first_nondet is None:
             first_nondet = k
         if shown < limit:

@@ -38,7 +38,7 @@ def main():
         us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc_m, aw_m, layout=lm), args.iters)
         print(json.dumps({"regime": regime, "T": args.T, "kernel": "fwd_tiles_level_major", "lds": 1,
                           "us": round(us, 2)}), flush=True)
-        _, tiles_m = msda.msda_forward(value, shapes, starts, loc_m, aw_m, layout=lm)
+        _, tiles_m = msda.msda_forward(value, shapes, starts, loc_m, aw_m, want_tiles=True, layout=lm)
         us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc_m, aw_m, gout, tiles=tiles_m, layout=lm),
                     args.iters)
         print(json.dumps({"regime": regime, "T": args.T, "kernel": "bwd_win_level_major", "us": round(us, 2)}),
