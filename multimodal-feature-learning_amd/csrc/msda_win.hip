@@ -188,17 +188,14 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
   constexpr int NS = kQT * P;                  // samples per tile
   constexpr int SPL = NS >= 64 ? NS / 64 : 1;  // samples per lane
   __shared__ __attribute__((aligned(16))) unsigned char s_g_w[W][kQT * kGS];     // grad_out rows of the tile
-  __shared__ __attribute__((aligned(16))) unsigned char s_v_w[W][kVRows * kGS];  // the block's value rows
-  // C of one MFMA step ([row][hi 32 | lo 32], step 2a), then the dots ([q][row - r0], 2b / 3): in
-  // turn, in the wave's LDS order
-  constexpr int kCBytes = kRW * kGS > kVRows * kDQS * 4 ? kRW * kGS : kVRows * kDQS * 4;
-  __shared__ __attribute__((aligned(16))) unsigned char s_c_w[W][kCBytes];
+  // C of one MFMA step ([row][hi 32 | lo 32], step 2a) and the dots ([row - r0][q], 2b / 3)
+  __shared__ __attribute__((aligned(16))) unsigned char s_c_w[W][kRW * kGS];
+  __shared__ __attribute__((aligned(16))) float s_d_w[W][kVRows * kDQS];
   __shared__ int s_q_w[W][NS + kQT];  // query row (in the tile) of each compacted sample, padded
   const int wid = W > 1 ? (int)(threadIdx.x >> 6) : 0;
   unsigned char* const s_g = s_g_w[wid];
-  unsigned char* const s_v = s_v_w[wid];
   unsigned char* const s_c = s_c_w[wid];
-  float* const s_d = reinterpret_cast<float*>(s_c);
+  float* const s_d = s_d_w[wid];
   int* const s_q = s_q_w[wid];
 
   const int lane = (int)(threadIdx.x & 63), g = lane >> 4, li = lane & 15;
@@ -259,14 +256,19 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
     const int s = lane + 64 * j;
     soff[j] = (s / P) * qstride + s % P;
   }
-  const int grow = lane >> 3, gch = lane & 7;  // grad_out piece (row grow + 8 i, 16-byte chunk gch)
-
-  // the block's value rows r0 .. r0+16 (zeros outside the level)
-  for (int c = lane; c < kVRows * 8; c += 64) {
-    const int row = c >> 3, ch = c & 7, x = r0 + row;
-    uint4 v = make_uint4(0u, 0u, 0u, 0u);
-    if (x < T) v = *reinterpret_cast<const uint4*>(vl + (long long)x * rs + ch * 8);
-    *reinterpret_cast<uint4*>(s_v + row * kGS + ch * 16) = v;
+  // The dots' B operands, constant over the block's visits, in registers: lane (li, g) holds
+  // channels ks*32 + 8g .. +7 of value row r0 + li (vb[0][ks]) and of row r0 + 16 (vb[1][ks])
+  // (zeros outside the level) — the dots then read no LDS
+  bf16x8 vb[2][2];
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb) {
+    const int x = r0 + (cb == 0 ? li : kRW);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (x < T) v = *reinterpret_cast<const uint4*>(vl + (long long)x * rs + ks * 32 + 8 * g);
+      vb[cb][ks] = __builtin_bit_cast(bf16x8, v);
+    }
   }
   // the query tiles whose row interval meets [r0, r0 + 15]: 64 tiles per ballot mask, walked
   // bit by bit (wave-uniform); the next visit is known one visit ahead for the prefetch
@@ -301,7 +303,9 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
 #pragma unroll
   for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // a visit's inputs in registers: SPL samples and 4 grad_out pieces per lane
+  // a visit's inputs in registers: SPL samples and 4 grad_out pieces per lane (rows grow + 8 i,
+  // 16-byte chunk gch: 8 lanes a 128-B row, coalesced)
+  const int grow = lane >> 3, gch = lane & 7;
   float rl[SPL], ra[SPL];
   uint4 rg[4];
   auto fetch = [&](int tile) {
@@ -309,6 +313,18 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
     const float* __restrict__ lt = loc + cbase + (long long)q0 * qstride;
     const float* __restrict__ at = aw + cbase + (long long)q0 * qstride;
     const uint16_t* __restrict__ gt = gb + (long long)q0 * rs;
+    if (sh.exp & 32) {  // (profiling: no coordinate loads)
+#pragma unroll
+      for (int j = 0; j < SPL; ++j) {
+        rl[j] = ((float)(q0 + (lane + 64 * j) / P) + 0.5f) / (float)sh.Lq;
+        ra[j] = 0.25f;
+      }
+    }
+    if (sh.exp & 8) {  // (profiling: no grad_out loads)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rg[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+    if (sh.exp & 40) return;
     if (q0 + kQT <= sh.Lq) {  // a whole tile (wave-uniform)
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
@@ -371,6 +387,27 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(s_g + (grow + 8 * i) * kGS + gch * 16) = rg[i];
     wave_lds_fence();
+    // 2b. dots of the tile's 32 queries with rows r0 .. r0+16 (2 query halves x 2 row blocks; of
+    // the second block only row r0+16 is kept, its other columns read row r0+16 again): the A
+    // fragments (grad_out rows) read once from LDS, the B fragments (value rows) block-constant in
+    // registers; into LDS at once (lane (g, li) holds queries qh*16 + 4g .. +3 of row li (cb 0) /
+    // row 16 (cb 1), one 16-B store)
+    if (COORDS && !(sh.exp & 4)) {
+#pragma unroll
+      for (int qh = 0; qh < 2; ++qh) {
+        bf16x8 av[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          av[ks] = *reinterpret_cast<const bf16x8*>(s_g + (qh * 16 + li) * kGS + (ks * 32 + 8 * g) * 2);
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], vb[cb][ks], d, 0, 0, 0);
+          if (cb == 0 || li == 0) *reinterpret_cast<f32x4*>(s_d + (cb * 16 + li) * kDQS + qh * 16 + 4 * g) = d;
+        }
+      }
+    }
     const int next = next_tile();
     if (next >= 0) fetch(next);  // in flight during the compute below
 
@@ -415,25 +452,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
       }
       wave_lds_fence();  // this step's C reads before the next step's zeroing
     }
-    // 2b. dots of the tile's 32 queries with rows r0 .. r0+16 (2 query halves x 2 row blocks; of
-    // the second block only row r0+16 is kept, its other columns read row r0+16 again)
     if (COORDS && !(sh.exp & 4)) {
-#pragma unroll
-      for (int tt = 0; tt < 4; ++tt) {
-        const int qh = tt >> 1, cb = tt & 1;
-        const int vrow = cb == 0 ? li : kRW;
-        f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          const int off = (ks * 32 + 8 * g) * 2;
-          const bf16x8 av = *reinterpret_cast<const bf16x8*>(s_g + (qh * 16 + li) * kGS + off);
-          const bf16x8 bv = *reinterpret_cast<const bf16x8*>(s_v + vrow * kGS + off);
-          d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, d, 0, 0, 0);
-        }
-        // lane (g, li) holds queries qh*16 + 4g .. +3 of row li (cb 0) / row 16 (cb 1): one 16-B store
-        if (cb == 0 || li == 0)
-          *reinterpret_cast<f32x4*>(s_d + (cb * 16 + li) * kDQS + qh * 16 + 4 * g) = d;
-      }
       wave_lds_fence();
       // 3. coordinate gradients of the samples this block owns (base row in it; the level's first
       // block also owns the samples with no tap on the map)

@@ -75,12 +75,11 @@ def test_staged_graph_steps_track_eager_steps(dev):
 
 def test_staged_graph_replay_matches_eager_bf16(dev):
     """Under bf16 autocast (the bench's regime): replays of graph A + host matching + graph B give
-    the eager staged step's loss and gradient on the same weights, to within the eager step's own
-    run-to-run spread: the bf16 backward is not bitwise reproducible (fp32 atomics in the index
-    gathers' backward, rounded into bf16 activations gradients downstream; two eager steps on the
-    same weights differ by 1-10 % of the gradient norm at this tiny random model, tools/dvc_graph_diag2.py —
-    the spread sits in the proposal path, not the caption decoder), so replay-vs-eager is held to twice
-    the largest eager-vs-eager difference of three steps; the loss to 1e-3."""
+    the eager staged step's loss and gradient on the same weights.  Two eager steps give the same
+    loss bit for bit (tools/determinism_diag.py: the spread of round 3 came from MIOpen's bf16
+    Conv1d forward, replaced by GEMMs in models/base_encoder.py); their gradients agree to
+    ~3e-4 (the attention kernels' backward is not bitwise reproducible), so replay-vs-eager
+    gradients are held to 3e-3 relative — a 1 % gradient error fails."""
     model, obj = _small(dev)
     tg = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.StagedDVCLoss(obj, model), lr=1e-4, use_bf16=True,
                                         graph=True)
@@ -100,13 +99,12 @@ def test_staged_graph_replay_matches_eager_bf16(dev):
         torch.cuda.synchronize()
         return loss, tg.flat_grad.clone()
 
-    (lg, fg), (le, fe) = replay(), eager()
-    others = [eager()[1] for _ in range(2)]
-    assert abs(lg - le) <= 1e-3 * abs(le), (lg, le)
+    (lg, fg), (le, fe), (le2, fe2) = replay(), eager(), eager()
     rel = lambda a, b: ((a - b).norm() / b.norm()).item()  # noqa: E731
-    # one eager pair's difference ranges ~1 % .. 10 % (tools/dvc_graph_diag2.py): the largest of three
-    spread = max(rel(others[0], fe), rel(others[1], fe), rel(others[0], others[1]))
-    assert rel(fg, fe) <= 2 * spread + 2e-2, (rel(fg, fe), spread)
+    assert le == le2, (le, le2)
+    assert rel(fe2, fe) <= 1e-3, rel(fe2, fe)
+    assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)
+    assert rel(fg, fe) <= 3e-3, rel(fg, fe)
 
 
 def test_segment_memory_gather_backward_kernel(dev):

@@ -202,7 +202,14 @@ def test_base_encoder_gemm_convs_match_fp64_and_are_reproducible(dev):
     for u, v in zip(a, b):
         assert torch.equal(u, v)
     import copy
-    ref = run(copy.deepcopy(enc).double(), x.double(), False)
+    # the fp64 reference on the host (reference base_encoder.py:49-89 as the module computes it)
+    cpu = torch.device("cpu")
+    enc64, pos64 = copy.deepcopy(enc).to(cpu).double(), pos
+    x64, m64, d64 = x.to(cpu).double().requires_grad_(True), mask.to(cpu), dur.to(cpu)
+    srcs64, _, _ = enc64(x64, m64, d64, pos64)
+    sum((s * g.to(cpu).double()).sum() for s, g in zip(srcs64, gs)).backward()
+    ref = [t.detach() for t in srcs64] + [x64.grad] + [p.grad for p in enc64.parameters()]
+    a = [t.cpu() for t in a]
     for i, (u, v) in enumerate(zip(a, ref)):
         err = ((u - v).norm() / v.norm().clamp_min(1e-30)).item()
         assert err < 2e-2, (i, err)

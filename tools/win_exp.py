@@ -2,7 +2,7 @@
 """Where the row-block backward's time goes: win_bwd_kernel at the bench's encoder call (B=8,
 T=1024 pyramid, bf16) with parts skipped through MSDA_HIP_WIN_EXP (profiling only; results
 wrong): 1 = no grad_value MFMA / C build, 2 = no coordinate-gradient stores, 4 = no dots and no
-coordinate gradients.  HIP-event averages over --iters launches, plus the forward for reference."""
+coordinate gradients, 8 = no grad_out loads, 32 = no coordinate loads (synthetic locations).  HIP-event averages over --iters launches, plus the forward for reference."""
 import argparse
 import json
 import os
@@ -18,7 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=50)
     ap.add_argument("--regimes", default="init,trained")
-    ap.add_argument("--exps", default="0,1,2,4,5,7")
+    ap.add_argument("--exps", default="0,1,2,4,5,7,13,37,45")
     ap.add_argument("--T", type=int, default=1024)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
