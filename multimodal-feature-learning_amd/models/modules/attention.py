@@ -28,6 +28,7 @@ from torch.nn.init import constant_, xavier_uniform_
 from ... import msda as _msda
 from ...utils.preds_postprocess import SegmentMemory
 from .seg_attention import segment_attention, segment_key_mask
+from .value_proj import linear_group, linear_group_supported
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
 from .linear import Linear, _AutocastLinear, _addmm, _bias_grad, _defer, _mm_nn, _weight_grad, linear_pair
@@ -470,6 +471,13 @@ class CrossAttention(nn.Module):
             out = segment_attention(self.q_linear(q), k, v, self.k_linear, self.v_linear, key_mask, H, self.scale,
                                     self.attention_dropout)
             return self.projection_layer(out), None
+        if q is k and k is v and not segments and linear_group_supported(
+                (self.q_linear, self.k_linear, self.v_linear), q):
+            # self-attention: the three projections of the same rows as one GEMM each way
+            q, k, v = (t.reshape(B, Lq, H, hd).transpose(1, 2)
+                       for t in linear_group((self.q_linear, self.k_linear, self.v_linear), q))
+            masked = self._mask(attn_mask, key_padding_mask)
+            return self._attend(q, k, v, masked, need_weights, segments, Lq)
         q = self.q_linear(q).reshape(B, Lq, H, hd).transpose(1, 2)
         if segments:  # the DVC's cropped memory: projections of the clips' rows, gathered
             k = k.project(self.k_linear).reshape(B, Lk, H, hd).transpose(1, 2)
@@ -478,6 +486,10 @@ class CrossAttention(nn.Module):
             k = self.k_linear(k).reshape(B, Lk, H, hd).transpose(1, 2)
             v = self.v_linear(v).reshape(B, Lk, H, hd).transpose(1, 2)
         masked = self._mask(attn_mask, key_padding_mask)
+        return self._attend(q, k, v, masked, need_weights, segments, Lq)
+
+    def _attend(self, q, k, v, masked, need_weights, segments, Lq):
+        """(projection_layer(softmax(scale q k^T masked) v), weights or None) of head-split q / k / v."""
         # the explicit form (the reference's own, attention.py:288-299) also for the caption
         # decoder's segment cross-attention: ~20 queries over ~2,000 keys, where the fused kernel's
         # backward took 148 us a call against tens for two small batched GEMMs and a softmax

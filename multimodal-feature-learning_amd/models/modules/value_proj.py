@@ -22,7 +22,7 @@ from torch.autograd import Function
 
 from .linear import Linear, _bias_grad, _weight_grad
 
-__all__ = ["layer_values", "layer_values_supported"]
+__all__ = ["layer_values", "layer_values_supported", "linear_group", "linear_group_supported"]
 
 _PAD = 16  # [x | 1 | 0 ...]: K padded to a multiple of 16 elements
 
@@ -119,3 +119,28 @@ def layer_values(attns, src, mask=None):
     low = [a.value_proj._low(torch.bfloat16) for a in attns]
     with torch.autocast("cuda", enabled=False):
         return _LayerValues.apply(x.contiguous(), mask, n, *ws, *bs, *[lw[0] for lw in low], *[lw[1] for lw in low])
+
+
+class _Holder:
+    """Presents a Linear as an object with ``value_proj`` (the interface layer_values reads)."""
+
+    def __init__(self, linear):
+        self.value_proj = linear
+
+
+def linear_group_supported(linears, x):
+    """Whether ``linear_group`` takes these Linear layers (same shape, biases) on input x
+    (MFL_LINEAR_GROUP=0: never, for A/B runs)."""
+    import os
+    if os.environ.get("MFL_LINEAR_GROUP", "1") == "0":
+        return False
+    return len(linears) >= 2 and layer_values_supported([_Holder(lin) for lin in linears], x, None)
+
+
+def linear_group(linears, x):
+    """``[lin(x) for lin in linears]`` under bf16 autocast as one batched GEMM each way (the
+    _LayerValues GEMMs without a mask): the caption decoder's 2 x depth cross-attention key / value
+    projections of the clip memory, and each self-attention's q / k / v projections of the same
+    rows.  The input gradient is one K-concatenated GEMM (the sum over the layers inside its K
+    loop: no fp32 gradient adds), the weight gradients one split-K GEMM."""
+    return layer_values([_Holder(lin) for lin in linears], x, None)

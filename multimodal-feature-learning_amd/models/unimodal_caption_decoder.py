@@ -14,6 +14,7 @@ from .load_weights import init_encoder_block_weights
 from .modules.embedding_layers import PositionalEncoding, VocabularyEmbedder
 from .modules.layers import CaptionKVCache, UnimodalCaptionDecoderLayer
 from .modules.linear import Linear
+from ..utils.preds_postprocess import SegmentMemory
 
 __all__ = ["UnimodalCaptionDecoder", "build_unimodal_caption_decoder", "greedy_decode"]
 
@@ -80,6 +81,10 @@ class UnimodalCaptionDecoder(nn.Module):
         """``last_only``: the head and softmax on the last layer only, (1, N, L, vocab) — the row
         ``[-1]`` of the full result, for callers that read nothing else (the DVC training forward)."""
         tgt = self.positional_encoding(self.target_embedding(tgt))
+        if isinstance(memory, SegmentMemory):
+            # every layer's cross-attention keys / values of the clip memory in one GEMM each way
+            memory.project_group([lin for layer in self.decoder
+                                  for lin in (layer.cross_attention.k_linear, layer.cross_attention.v_linear)])
         intermediate = []
         for layer in self.decoder:
             tgt = layer(tgt, memory, tgt_mask, memory_mask, tgt_padding_mask, memory_padding_mask)

@@ -137,6 +137,19 @@ class SegmentMemory:
             self.cache[linear] = P
         return P, (linear.bias.to(P.dtype) if linear.bias is not None else None)
 
+    def project_group(self, linears):
+        """Project the source by every Linear of ``linears`` not cached yet, all at once (one batched
+        GEMM each way, value_proj.linear_group: the caption decoder's cross-attention key / value
+        projections of all its layers), and cache them for ``projected``."""
+        from ..models.modules.value_proj import linear_group, linear_group_supported
+        todo = [lin for lin in linears if lin not in self.cache]
+        if not linear_group_supported(todo, self.source):
+            return
+        from .. import _trace
+        _trace.hit("memory_projection_group")
+        for lin, p in zip(todo, linear_group(todo, self.source)):
+            self.cache[lin] = p
+
     def project(self, linear):
         """``linear(self.materialize())`` from one projection of the source per step."""
         P, bias = self.projected(linear)

@@ -175,6 +175,7 @@ def test_mha_self_attention_autocast_matches_module(dev):
         torch.testing.assert_close(a, b, rtol=3e-2, atol=3e-2 * b.abs().max().item())
 
 
+@pytest.mark.gpu
 def test_base_encoder_gemm_convs_match_fp64_and_are_reproducible(dev):
     """BaseEncoder under bf16 autocast runs its Conv1d layers as GEMMs on channels-last rows
     (models/base_encoder.py): outputs and gradients against the module in fp64 within bf16
@@ -213,3 +214,30 @@ def test_base_encoder_gemm_convs_match_fp64_and_are_reproducible(dev):
     for i, (u, v) in enumerate(zip(a, ref)):
         err = ((u - v).norm() / v.norm().clamp_min(1e-30)).item()
         assert err < 2e-2, (i, err)
+
+
+@pytest.mark.gpu
+def test_linear_group_matches_separate_projections(dev, monkeypatch):
+    """value_proj.linear_group (the caption decoder's grouped key / value projections of the clip
+    memory and its self-attention q / k / v): outputs and every gradient against the same Linear
+    layers applied one by one under bf16 autocast (MFL_LINEAR_GROUP=0): outputs bit for bit (each
+    output column is its own fp32-accumulated product, one rounding), gradients to bf16 / fp32
+    summation order."""
+    torch.manual_seed(4)
+    lins = torch.nn.ModuleList([PKG.models.modules.linear.Linear(512, 512) for _ in range(5)]).to(dev)
+    x = torch.randn(3, 700, 512, device=dev)
+    gs = [torch.randn(3, 700, 512, device=dev) for _ in lins]
+    runs = []
+    for grouped in (True, False):
+        lins.zero_grad()
+        xx = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            outs = (PKG.models.modules.value_proj.linear_group(list(lins), xx) if grouped
+                    else [lin(xx) for lin in lins])
+        sum((o.float() * g).sum() for o, g in zip(outs, gs)).backward()
+        runs.append(([o.detach() for o in outs], xx.grad, [p.grad.clone() for p in lins.parameters()]))
+    for a, b in zip(runs[0][0], runs[1][0]):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(runs[0][1], runs[1][1], rtol=2e-2, atol=2e-2)
+    for a, b in zip(runs[0][2], runs[1][2]):
+        torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
