@@ -3010,8 +3010,10 @@ bool win_applies(int value_dtype, long long D, long long Lq, long long P, long l
   int minT = 1 << 30;
   for (int l = 0; l < L; ++l) minT = min(minT, T[l]);
   // encoder-like calls, or queries far outnumbering the rows (configs[2]'s video queries on the
-  // 95-row audio pyramid: 8 waves a row block, 51.6 us against the pair kernel's 63.3)
-  return (minT >= 64 && 2 * Lq >= S) || Lq >= 4 * S;
+  // 95-row audio pyramid: 8 waves a row block, 51.6 us against the pair kernel's 63.3), or the
+  // Sparse-DETR encoder's position-sorted top-k queries (a third of the pyramid's tokens, each
+  // sampling around its own position: 577 queries over the T = 1024 pyramid)
+  return (minT >= 64 && 2 * Lq >= S) || Lq >= 4 * S || (minT >= 64 && Lq * P >= 2048);
 }
 
 // The backward of this call takes the row-block MFMA path (msda_win.hip) when handed a workspace

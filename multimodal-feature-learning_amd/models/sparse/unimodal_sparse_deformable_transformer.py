@@ -235,8 +235,23 @@ class DeformableTransformerEncoder(nn.Module):
         sparsified = backbone_topk_proposals is not None
         reference_points = self.get_reference_points(temporal_shapes, valid_ratios, device=src.device)
         tgt = None
+        inv = None
         if sparsified:
             topk = backbone_topk_proposals
+            if sparse_token_nums is not None:
+                # (the keep mask below is by score rank: taken before the reorder)
+                rank_keep = (torch.arange(topk.shape[1], device=topk.device)[None, :]
+                             < sparse_token_nums.to(topk.device)[:, None])
+            if topk.is_cuda:
+                # the refined tokens in position order: every layer treats them independently and scatters
+                # them back by position, so the order is free — and with neighbouring tokens next to each
+                # other the MSDA backward takes the row-block kernel (each query tile touches a short row
+                # interval) instead of the per-tap kernel.  The returned per-token tensors are put back
+                # into score order (``inv``), as the reference returns them.
+                topk, order = topk.sort(dim=1)
+                inv = torch.argsort(order, dim=1)
+                if sparse_token_nums is not None:
+                    rank_keep = rank_keep.gather(1, order)
             B, N, S_, P_ = reference_points.shape
             reference_points = torch.gather(reference_points.view(B, N, -1), 1,
                                             topk.unsqueeze(-1).expand(-1, -1, S_ * P_)).view(B, -1, S_, P_)
@@ -249,8 +264,7 @@ class DeformableTransformerEncoder(nn.Module):
             if sparse_token_nums is not None:
                 # clip i keeps only its first sparse_token_nums[i] top-k tokens (reference :445-448
                 # scatters them one clip at a time): the others write back their own old value
-                keep = (torch.arange(topk.shape[1], device=topk.device)[None, :]
-                        < sparse_token_nums.to(topk.device)[:, None]).unsqueeze(-1)
+                keep = rank_keep.unsqueeze(-1)
         locs, weights, inter = [], [], []
         for layer in self.layers:
             tgt, sampling_locations, attn_weights = layer(output, pos, reference_points, temporal_shapes,
@@ -267,6 +281,16 @@ class DeformableTransformerEncoder(nn.Module):
                 inter.append(tgt)
         sampling_locations_enc = torch.stack(locs, dim=1)
         attn_weights_enc = torch.stack(weights, dim=1)
+        if inv is not None:  # back into score order (B, layers, k, ...)
+            def unsort(t, dim):
+                shape = [1] * t.dim()
+                shape[0], shape[dim] = inv.shape[0], inv.shape[1]
+                return t.gather(dim, inv.view(shape).expand(*t.shape[:dim], inv.shape[1], *t.shape[dim + 1:]))
+            sampling_locations_enc = unsort(sampling_locations_enc, 2)
+            attn_weights_enc = unsort(attn_weights_enc, 2)
+            inter = [unsort(t, 1) for t in inter]
+            if output_proposals is not None:
+                output_proposals = unsort(output_proposals, 1)
         if self.aux_heads:
             from ..modules.misc_modules import predict_event_num_with_depth
             enc_inter_tgt = torch.stack(inter)
