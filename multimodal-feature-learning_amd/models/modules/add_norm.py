@@ -120,7 +120,8 @@ def add_layer_norm(r, y, norm: nn.LayerNorm, dropout=None):
     if (r.is_cuda and torch.is_autocast_enabled("cuda") and isinstance(norm, nn.LayerNorm)
             and norm.elementwise_affine and norm.bias is not None and tuple(norm.normalized_shape) == (d,)
             and norm.weight.dtype == torch.float32 and r.shape == y.shape and r.dtype in _TAGS
-            and y.dtype in _TAGS and d % 256 == 0 and d <= 1024 and r.numel() > 0):
+            and y.dtype in _TAGS and d % 256 == 0 and d <= 1024 and r.numel() > 0
+            and y.device == r.device and norm.weight.device == r.device):
         p_drop, seed = _drop_args(dropout, r.device)
         with torch.autocast("cuda", enabled=False):
             return _AddLayerNorm.apply(r.contiguous(), y.contiguous(), norm.weight, norm.bias, norm.eps, p_drop, seed)
@@ -191,7 +192,7 @@ def carry_supported(r, norm) -> bool:
             and torch.get_autocast_dtype("cuda") == torch.bfloat16 and isinstance(norm, nn.LayerNorm)
             and norm.elementwise_affine and norm.bias is not None and tuple(norm.normalized_shape) == (d,)
             and norm.weight.dtype == torch.float32 and r.dtype in _TAGS and d % 256 == 0 and d <= 1024
-            and r.numel() > 0)
+            and r.numel() > 0 and norm.weight.device == r.device)
 
 
 def add_layer_norm_carry(r, y, norm: nn.LayerNorm, pos=None, dropout=None):

@@ -239,7 +239,7 @@ class MSDeformAttn(nn.Module):
         sampling_offsets, attention_weights = linear_pair(query, self.sampling_offsets, self.attention_weights)
         sampling_offsets = sampling_offsets.view(N, Len_q, self.n_heads, self.n_levels, self.n_points)
         attention_weights = attention_weights.view(N, Len_q, self.n_heads, self.n_levels * self.n_points)
-        if (query.is_cuda and reference_points.shape[-1] in (1, 2)
+        if (query.is_cuda and reference_points.shape[-1] in (1, 2) and reference_points.device == query.device
                 and attention_weights.dtype == sampling_offsets.dtype
                 and _msda.prologue_supported(self.n_heads, self.n_levels, self.n_points)):
             # softmax + location arithmetic in one HIP kernel each way
@@ -348,7 +348,7 @@ def mha_self_attention(mha, tgt, query_pos, query_mask, carried=None):
     w, b = mha.in_proj_weight, mha.in_proj_bias
     x_qk = tgt if query_pos is None else tgt + query_pos
     if (tgt.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
-            and w.dtype == torch.float32 and mha.out_proj.bias is not None):
+            and w.dtype == torch.float32 and mha.out_proj.bias is not None and w.device == tgt.device):
         # the projections as the autocast Linear's: bf16 weights from the trainer's shadow, fp32
         # weight / bias gradients straight from the GEMMs (no per-use casts, no slice-gradient adds)
         sh = getattr(mha, "_mfl_shadow", None)

@@ -151,7 +151,10 @@ def small_addmm(bias, x2, w):
     N = w.shape[0]
     # (graph-timed against hipBLASLt, tools/small_gemm_ab.py: ahead for N, K <= 512 — 800 x 256 x 512
     # 4.3 vs 5.4 us, 800 x 512 x 512 6.2 vs 6.5 — behind from N or K = 1024 on)
+    # (operands on another device than x2 — a module left on the host — go to torch.addmm, which
+    # raises; their pointers must never reach the kernel)
     if not (x2.is_cuda and x2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 0 < M <= SMALL_GEMM_MAX_ROWS
+            and w.device == x2.device and (bias is None or bias.device == x2.device)
             and N <= 512 and K <= 512
             and N % 32 == 0 and K % 32 == 0 and x2.stride(1) == 1 and w.stride(1) == 1
             and x2.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and x2.stride(0) >= K and w.stride(0) >= K
@@ -181,6 +184,7 @@ def small_mm_nn(g2, w):
     K = w.shape[1]
     # (ahead of hipBLASLt for N, K <= 512: 800 x 512 x 512 5.4 vs 7.4 us; behind from 1024 on)
     if not (g2.is_cuda and g2.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and 0 < M <= SMALL_GEMM_MAX_ROWS
+            and w.device == g2.device
             and N <= 512 and K <= 512
             and K % 32 == 0 and N % 32 == 0 and g2.stride(1) == 1 and w.stride(1) == 1
             and g2.stride(0) % 8 == 0 and w.stride(0) % 8 == 0 and g2.stride(0) >= N and w.stride(0) >= K
@@ -416,6 +420,7 @@ class Linear(nn.Linear):
     def _autocast_dtype(self, x):
         """The 16-bit autocast dtype this layer computes in for input x, or None (F.linear)."""
         if (x.is_cuda and torch.is_autocast_enabled("cuda") and self.weight.dtype == torch.float32
+                and self.weight.device == x.device
                 and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16)):
             return torch.get_autocast_dtype("cuda")
         return None
@@ -434,8 +439,7 @@ class Linear(nn.Linear):
         self._shadow = (weight_bf16, bias_bf16, self.weight._version)
 
     def forward(self, x):
-        if (x.is_cuda and torch.is_autocast_enabled("cuda") and self.weight.dtype == torch.float32
-                and torch.get_autocast_dtype("cuda") in (torch.bfloat16, torch.float16)):
+        if self._autocast_dtype(x) is not None:
             dt = torch.get_autocast_dtype("cuda")
             wc = bc = None
             sh = self._shadow

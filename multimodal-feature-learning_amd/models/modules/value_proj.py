@@ -94,6 +94,7 @@ def layer_values_supported(attns, src, mask):
     for a in attns:
         vp = getattr(a, "value_proj", None)
         if (not isinstance(vp, Linear) or vp.bias is None or vp.weight.dtype != torch.float32
+                or vp.weight.device != src.device
                 or vp.weight.shape != p0.weight.shape):
             return False
     if src.shape[-1] != p0.weight.shape[1] or src.numel() == 0 or src.dtype not in (torch.float32, torch.bfloat16):

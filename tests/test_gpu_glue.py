@@ -184,7 +184,7 @@ def test_base_encoder_gemm_convs_match_fp64_and_are_reproducible(dev):
     torch.manual_seed(3)
     B, T, d = 4, 128, 256
     enc = PKG.models.base_encoder.BaseEncoder(4, d, d).to(dev)
-    pos = PKG.models.modules.embedding_layers.PositionEmbeddingVideoSine(d // 2, normalize=True)
+    pos = PKG.models.modules.embedding_layers.PositionEmbeddingVideoSine(d // 2, normalize=True).to(dev)
     x = torch.randn(B, T, d, device=dev)
     mask = torch.zeros(B, T, dtype=torch.bool, device=dev)
     mask[1, 100:] = True
@@ -205,7 +205,7 @@ def test_base_encoder_gemm_convs_match_fp64_and_are_reproducible(dev):
     import copy
     # the fp64 reference on the host (reference base_encoder.py:49-89 as the module computes it)
     cpu = torch.device("cpu")
-    enc64, pos64 = copy.deepcopy(enc).to(cpu).double(), pos
+    enc64, pos64 = copy.deepcopy(enc).to(cpu).double(), copy.deepcopy(pos).to(cpu)
     x64, m64, d64 = x.to(cpu).double().requires_grad_(True), mask.to(cpu), dur.to(cpu)
     srcs64, _, _ = enc64(x64, m64, d64, pos64)
     sum((s * g.to(cpu).double()).sum() for s, g in zip(srcs64, gs)).backward()
@@ -241,3 +241,24 @@ def test_linear_group_matches_separate_projections(dev, monkeypatch):
     torch.testing.assert_close(runs[0][1], runs[1][1], rtol=2e-2, atol=2e-2)
     for a, b in zip(runs[0][2], runs[1][2]):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_host_weights_never_reach_native_kernels(dev):
+    """A Linear / LayerNorm left on the host with a GPU input under bf16 autocast raises torch's
+    device-mismatch error instead of handing host pointers to a HIP kernel (the guards in
+    linear.py small_addmm / Linear._autocast_dtype and add_norm.py: an earlier version of
+    test_base_encoder_gemm_convs_match_fp64_and_are_reproducible built its position embedding on
+    the host and the short-M GEMM read the host weight's address)."""
+    lin = PKG.models.modules.linear.Linear(128, 128)
+    x = torch.randn(64, 128, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        with pytest.raises(RuntimeError):
+            lin(x)
+    w = torch.randn(128, 128, dtype=torch.bfloat16)
+    assert PKG.models.modules.linear.small_addmm(None, x.to(torch.bfloat16), w) is None
+    norm = torch.nn.LayerNorm(256)
+    r = torch.randn(4, 256, device=dev)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        with pytest.raises(RuntimeError):
+            PKG.models.modules.add_norm.add_layer_norm(r, r, norm)
