@@ -464,7 +464,7 @@ template <typename scalar_t, bool ZEROS, int P, bool LM>
 __global__ __launch_bounds__(256) void msda_fwd16_tiles_kernel(
     const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     scalar_t* __restrict__ out, int2* __restrict__ tiles, const Levels lv, const int L, const int S, const int M,
-    const int Lq, const int ntile) {
+    const int Lq, const int ntile, const QOrder qo) {
   constexpr int VEC = 8, D = 64, NL = kLPMax / P;
   __shared__ int2 s_iv[4][NL];
   const unsigned wg = xcd_block(blockIdx.x, gridDim.x);
@@ -473,7 +473,7 @@ __global__ __launch_bounds__(256) void msda_fwd16_tiles_kernel(
   const int m = (int)(bm % (unsigned)M);
   const long long b = bm / (unsigned)M;
   const int i = threadIdx.x >> 3, lg = threadIdx.x & 7;
-  const int q = tile * kWinQT + i;
+  const int q = tile * kWinQT + i < Lq ? qo_query(qo, tile * kWinQT + i) : Lq;  // (msda_win.h: the tile order)
   const int LP = L * P;
   int lo[NL], hi[NL];
 #pragma unroll
@@ -545,7 +545,7 @@ template <typename scalar_t, bool ZEROS, int P, bool LM>
 __global__ __launch_bounds__(256) void msda_fwd16_lds_kernel(
     const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     scalar_t* __restrict__ out, int2* __restrict__ tiles, const Levels lv, const int L, const int S, const int M,
-    const int Lq, const int ntile) {
+    const int Lq, const int ntile, const QOrder qo) {
   constexpr int VEC = 8, D = 64, NL = kLPMax / P;
   __shared__ int2 s_iv[4][NL];
   __shared__ int s_off[NL], s_lo[NL], s_n[NL + 1];
@@ -556,7 +556,7 @@ __global__ __launch_bounds__(256) void msda_fwd16_lds_kernel(
   const int m = (int)(bm % (unsigned)M);
   const long long b = bm / (unsigned)M;
   const int i = threadIdx.x >> 3, lg = threadIdx.x & 7;
-  const int q = tile * kWinQT + i;
+  const int q = tile * kWinQT + i < Lq ? qo_query(qo, tile * kWinQT + i) : Lq;  // (msda_win.h: the tile order)
   const int LP = L * P;
   const int rs = M * D;
   int lo[NL], hi[NL];
@@ -2380,20 +2380,21 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
       // L1 and the barrier-free gather kernel hides their latency), so the gathers stay the default
       const bool fwd_lds = env_int("MSDA_HIP_FWD_LDS", 0) != 0;
       auto* tl = static_cast<int2*>(tiles);
+      const QOrder qo = make_qorder(pr.Lq, pr.S, (int)pr.L, pr.lv.T, pr.lv.start);
 #define MSDA_FT(Z, PP)                                                                              \
   do {                                                                                            \
     if (fwd_lds && lm)                                                                            \
       hipLaunchKernelGGL((msda_fwd16_lds_kernel<scalar_t, Z, PP, true>), dim3(tblocks), dim3(256), 0, st, v, lc, \
-                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
+                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo);   \
     else if (fwd_lds)                                                                             \
       hipLaunchKernelGGL((msda_fwd16_lds_kernel<scalar_t, Z, PP, false>), dim3(tblocks), dim3(256), 0, st, v, lc, \
-                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
+                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo);   \
     else if (lm)                                                                                  \
       hipLaunchKernelGGL((msda_fwd16_tiles_kernel<scalar_t, Z, PP, true>), dim3(tblocks), dim3(256), 0, st, v, lc, \
-                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
+                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo);   \
     else                                                                                          \
       hipLaunchKernelGGL((msda_fwd16_tiles_kernel<scalar_t, Z, PP, false>), dim3(tblocks), dim3(256), 0, st, v, lc, \
-                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile);   \
+                         a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo);   \
   } while (0)
 #define MSDA_FT_P(Z)                                                                                \
   switch (pr.P) {                                                                                 \
@@ -3056,6 +3057,7 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
           sh.T[l] = pr.lv.T[l];
           sh.start[l] = pr.lv.start[l];
         }
+        sh.qo = make_qorder(pr.Lq, pr.S, (int)pr.L, pr.lv.T, pr.lv.start);
         if (msda_win_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, tiles, &sh, pad == MSDA_PAD_ZEROS,
                               layout, st) < 0) {
           set_error("msda backward: level-major coordinates need the forward's tile intervals");

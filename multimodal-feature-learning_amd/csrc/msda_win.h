@@ -3,6 +3,69 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stddef.h>
+#include <stdlib.h>
+
+// Query order of the row-block backward's tiles.  A tile is 32 queries; by default 32 consecutive
+// ones.  In an encoder self-attention call (Lq == S: the queries are the pyramid's tokens, level
+// by level) a tile of consecutive queries of a coarse level spans a large stretch of every finer
+// level (32 level-3 tokens of a 1024/512/256/128 pyramid: a quarter of level 0), so the row blocks
+// there each meet many tiles holding few of their samples.  Position order instead: chunk c holds
+// the tokens of every level covering the c-th T_{L-1}-th of the sequence (tokens c n_l .. c n_l +
+// n_l - 1 of level l, n_l = T_l / T_{L-1}), chunks in order, and a tile is 32 consecutive
+// entries of that order — every tile a short stretch of every level (bench encoder call: 720 ->
+// 416 visits per (b, m), tools/win_visits.py).  Grouping only: every sample is still handled once
+// per level by the blocks holding its taps, so results are the same bit for bit.
+constexpr int kQOrderMaxL = 4;
+struct QOrder {
+  int cs;        // entries per chunk (sum of n); 0: consecutive queries
+  float inv_cs;  // 1 / cs
+  int L;
+  int n[kQOrderMaxL], start[kQOrderMaxL];
+};
+
+// Position order when the call is encoder-shaped (Lq == S, 2 <= L <= 4, every T_l a multiple of
+// T_{L-1}, level starts the running sums, Lq < 2^22 so the float chunk division is exact);
+// MSDA_HIP_QORDER=0 keeps consecutive tiles.  The forward that writes the tile intervals and the
+// backward that reads them both call this on the same shapes.
+inline QOrder make_qorder(long long Lq, long long S, int L, const int* T, const int* start) {
+  QOrder o{};
+  const char* e = getenv("MSDA_HIP_QORDER");
+  if ((e != nullptr && atoi(e) == 0) || Lq != S || L < 2 || L > kQOrderMaxL || Lq >= (1LL << 22)) return o;
+  const int tc = T[L - 1];
+  if (tc < 1) return o;
+  int cs = 0, run = 0;
+  for (int l = 0; l < L; ++l) {
+    if (T[l] % tc != 0 || start[l] != run) return o;
+    o.n[l] = T[l] / tc;
+    o.start[l] = start[l];
+    cs += o.n[l];
+    run += T[l];
+  }
+  o.cs = cs;
+  o.inv_cs = 1.f / (float)cs;
+  o.L = L;
+  return o;
+}
+
+// The query at entry s (< Lq) of the tile order.
+__device__ __forceinline__ int qo_query(const QOrder& o, int s) {
+  if (o.cs == 0) return s;
+  const int c = (int)(((float)s + 0.5f) * o.inv_cs);
+  int j = s - c * o.cs, q = 0;
+  bool found = false;
+#pragma unroll
+  for (int l = 0; l < kQOrderMaxL; ++l) {
+    if (l < o.L && !found) {
+      if (j < o.n[l]) {
+        q = o.start[l] + c * o.n[l] + j;
+        found = true;
+      } else {
+        j -= o.n[l];
+      }
+    }
+  }
+  return q;
+}
 
 constexpr int kWinMaxChunks = 64;  // position chunks of the dispatch order
 constexpr int kWinMaxSeq = 512;    // row blocks of one (b, m) in the position-chunk order
@@ -22,6 +85,7 @@ struct WinShape {
   // b cb + q cq + m cm + l cl + p (set by msda_win_backward from the layout tag)
   long long cb, cm;
   int cq, cl;
+  QOrder qo;  // tile order of the queries (set by the caller: make_qorder)
   int exp;  // profiling only (MSDA_HIP_WIN_EXP bitmask, 0 in production): skip parts of win_bwd_kernel
   unsigned short cs[kWinMaxChunks + 1];
   unsigned short seq[kWinMaxSeq];

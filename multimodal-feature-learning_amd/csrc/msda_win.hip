@@ -117,13 +117,13 @@ __global__ __launch_bounds__(kThreads) void win_tiles_kernel(const float* __rest
   const int P = sh.P, n = (int)sh.M * sh.L * P;
   const int q0 = tile * kQT + w * kQPW;
   const int nq = (int)max(0LL, min((long long)kQPW, sh.Lq - q0));
-  const float* __restrict__ rows = loc + (b * sh.Lq + q0) * (long long)n;
   float x[kQPW][NJ];
 #pragma unroll
-  for (int u = 0; u < kQPW; ++u)
+  for (int u = 0; u < kQPW; ++u) {
+    const float* __restrict__ row = loc + (b * sh.Lq + (u < nq ? qo_query(sh.qo, q0 + u) : 0)) * (long long)n;
 #pragma unroll
-    for (int j = 0; j < NJ; ++j)
-      x[u][j] = (u < nq && lane + 64 * j < n) ? rows[(long long)u * n + lane + 64 * j] : 0.f;
+    for (int j = 0; j < NJ; ++j) x[u][j] = (u < nq && lane + 64 * j < n) ? row[lane + 64 * j] : 0.f;
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
     const int i = lane + 64 * j;
@@ -249,13 +249,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
   const uint16_t* __restrict__ vl = value + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
   const uint16_t* __restrict__ gb = gout + (b * sh.Lq * sh.M + m) * 64;
   const long long cbase = b * sh.cb + m * sh.cm + (long long)l * sh.cl;
-  // per-lane constant parts of the addresses
-  int soff[SPL];
-#pragma unroll
-  for (int j = 0; j < SPL; ++j) {
-    const int s = lane + 64 * j;
-    soff[j] = (s / P) * qstride + s % P;
-  }
+  // coordinate offset of sample s of the tile at entry q0 of the query order (sh.qo; the caller
+  // keeps q0 + s / P < Lq)
+  auto coff = [&](int q0, int s) -> long long {
+    return (long long)qo_query(sh.qo, q0 + s / P) * qstride + s % P;
+  };
   // The dots' B operands, constant over the block's visits, in registers: lane (li, g) holds
   // channels ks*32 + 8g .. +7 of value row r0 + li (vb[0][ks]) and of row r0 + 16 (vb[1][ks])
   // (zeros outside the level) — the dots then read no LDS
@@ -310,9 +308,8 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
   uint4 rg[4];
   auto fetch = [&](int tile) {
     const int q0 = tile * kQT;
-    const float* __restrict__ lt = loc + cbase + (long long)q0 * qstride;
-    const float* __restrict__ at = aw + cbase + (long long)q0 * qstride;
-    const uint16_t* __restrict__ gt = gb + (long long)q0 * rs;
+    const float* __restrict__ lt = loc + cbase;
+    const float* __restrict__ at = aw + cbase;
     if (sh.exp & 32) {  // (profiling: no coordinate loads)
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
@@ -329,23 +326,27 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
         const bool in = NS >= 64 || lane < NS;
-        rl[j] = in ? lt[soff[j]] : 0.f;
-        ra[j] = in ? at[soff[j]] : 0.f;
+        const long long o = coff(q0, in ? lane + 64 * j : 0);
+        rl[j] = in ? lt[o] : 0.f;
+        ra[j] = in ? at[o] : 0.f;
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) rg[i] = *reinterpret_cast<const uint4*>(gt + (grow + 8 * i) * rs + gch * 8);
+      for (int i = 0; i < 4; ++i)
+        rg[i] = *reinterpret_cast<const uint4*>(gb + (long long)qo_query(sh.qo, q0 + grow + 8 * i) * rs + gch * 8);
     } else {
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
         const int s = lane + 64 * j;
         const bool in = (NS >= 64 || lane < NS) && q0 + s / P < sh.Lq;
-        rl[j] = in ? lt[soff[j]] : 0.f;
-        ra[j] = in ? at[soff[j]] : 0.f;
+        const long long o = in ? coff(q0, s) : 0;
+        rl[j] = in ? lt[o] : 0.f;
+        ra[j] = in ? at[o] : 0.f;
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        rg[i] = q0 + grow + 8 * i < sh.Lq ? *reinterpret_cast<const uint4*>(gt + (grow + 8 * i) * rs + gch * 8)
-                                         : make_uint4(0u, 0u, 0u, 0u);
+        rg[i] = q0 + grow + 8 * i < sh.Lq
+                    ? *reinterpret_cast<const uint4*>(gb + (long long)qo_query(sh.qo, q0 + grow + 8 * i) * rs + gch * 8)
+                    : make_uint4(0u, 0u, 0u, 0u);
     }
   };
   int tile = next_tile();
@@ -456,7 +457,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
       wave_lds_fence();
       // 3. coordinate gradients of the samples this block owns (base row in it; the level's first
       // block also owns the samples with no tap on the map)
-      const long long tb = cbase + (long long)q0 * qstride;
+      const long long tb = cbase;
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
         const int s = lane + 64 * j;
@@ -465,10 +466,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
         const bool own = t.live ? (t.base >= r0 && t.base < r0 + kRW) || (t.base < 0 && k == 0) : k == 0;
         if (in && own && !(sh.exp & 2)) {
           const int qi = s / P;
+          const long long o = coff(q0, s);
           const float d0 = t.ok0 ? s_d[(t.base - r0) * kDQS + qi] : 0.f;
           const float d1 = t.ok1 ? s_d[(t.base + 1 - r0) * kDQS + qi] : 0.f;
-          if (gaw != nullptr) gaw[tb + soff[j]] = d0 * t.w0 + d1 * t.w1;
-          if (gloc != nullptr) gloc[tb + soff[j]] = ((d1 - d0) * a[j]) * t.gmul;
+          if (gaw != nullptr) gaw[tb + o] = d0 * t.w0 + d1 * t.w1;
+          if (gloc != nullptr) gloc[tb + o] = ((d1 - d0) * a[j]) * t.gmul;
         }
       }
     }

@@ -534,7 +534,7 @@ def test_bf16_T1024_bench_instantiation_matches_oracle(dev, monkeypatch, layout)
     coordinates.  Clips 0 and 7 against the oracle on the same bf16-rounded inputs in fp32
     (reference semantics attention.py:331-383)."""
     for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH",
-              "MSDA_HIP_LEVEL_MAJOR"):
+              "MSDA_HIP_LEVEL_MAJOR", "MSDA_HIP_QORDER"):
         monkeypatch.delenv(k, raising=False)
     shapes, B, M, D, P = [1024, 512, 256, 128], 8, 8, 64, 4
     Lq = sum(shapes)
@@ -562,6 +562,39 @@ def test_bf16_T1024_bench_instantiation_matches_oracle(dev, monkeypatch, layout)
         np.testing.assert_allclose(_np(v.grad[b:b + 1]), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
         np.testing.assert_allclose(_np(ga[b:b + 1]), r_ga, rtol=1e-4, atol=1e-4)
         np.testing.assert_allclose(_np(gl[b:b + 1]), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))
+
+
+@pytest.mark.parametrize("layout", ["reference", "level_major"])
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("shapes", [[64, 32, 16, 8], [1024, 512, 256, 128], [96, 48, 24]])
+def test_position_order_tiles_equal_consecutive_tiles(dev, monkeypatch, shapes, padding, layout):
+    """Encoder-shaped calls (Lq == S) group the row-block backward's query tiles in position order
+    (msda_win.h QOrder: every level's tokens of one stretch of the sequence together); grouping
+    only, so output, grad_value and the coordinate gradients equal those of tiles of consecutive
+    queries (MSDA_HIP_QORDER=0) bit for bit — ragged last tile (S = 120), 3 levels, both paddings
+    and coordinate layouts.  Trained-regime spread around each token's own position."""
+    for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH"):
+        monkeypatch.delenv(k, raising=False)
+    B, M, D, P = 2, 8, 64, 4
+    Lq = sum(shapes)
+    value, _, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=31, lo=0.0, hi=1.0)
+    loc = local_locations(B, Lq, M, shapes, P, seed=32)
+    starts = O.level_starts(shapes)
+    lm = layout == "level_major"
+    res = []
+    for qorder in ("1", "0"):
+        monkeypatch.setenv("MSDA_HIP_QORDER", qorder)
+        v = value.cuda().requires_grad_(True)
+        lc = (_to_level_major(loc) if lm else loc).cuda().requires_grad_(True)
+        a = (_to_level_major(aw) if lm else aw).cuda().requires_grad_(True)
+        PKG._trace.clear()
+        out = msda.msda_apply(v, shapes, starts, lc, a, padding, layout=msda.LEVEL_MAJOR if lm else 0)
+        out.backward(gout.cuda())
+        torch.cuda.synchronize()
+        assert PKG._trace.hits.get("msda_bfloat16", 0) == 1
+        res.append([out.detach(), v.grad, lc.grad, a.grad])
+    for x, y in zip(*res):
+        assert torch.equal(x, y)
 
 
 @pytest.mark.parametrize("padding", ["border", "zeros"])

@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--regimes", default="init,trained")
     ap.add_argument("--exps", default="0,1,2,4,5,7,13,37,45")
     ap.add_argument("--T", type=int, default=1024)
+    ap.add_argument("--qorders", default="1,0", help="MSDA_HIP_QORDER values (tile order of the queries)")
+    ap.add_argument("--fwd-lds", default="0", help="MSDA_HIP_FWD_LDS values to time")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     shapes = [args.T, args.T // 2, args.T // 4, args.T // 8]
@@ -27,27 +29,28 @@ def main():
     starts = [sum(shapes[:i]) for i in range(4)]
     for regime in args.regimes.split(","):
         value, loc, aw, gout = make(regime, B, Lq, shapes, M, P, torch.bfloat16, dev)
-        _, tiles = msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True)
-        for flag in ("0", "1"):
-            os.environ["MSDA_HIP_FWD_LDS"] = flag
-            us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True), args.iters)
-            print(json.dumps({"regime": regime, "T": args.T, "kernel": "fwd_tiles", "lds": int(flag),
-                              "us": round(us, 2)}), flush=True)
-        lm = msda.LEVEL_MAJOR
-        loc_m, aw_m = loc.permute(0, 2, 3, 1, 4).contiguous(), aw.permute(0, 2, 3, 1, 4).contiguous()
-        us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc_m, aw_m, layout=lm), args.iters)
-        print(json.dumps({"regime": regime, "T": args.T, "kernel": "fwd_tiles_level_major", "lds": 1,
-                          "us": round(us, 2)}), flush=True)
-        _, tiles_m = msda.msda_forward(value, shapes, starts, loc_m, aw_m, want_tiles=True, layout=lm)
-        us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc_m, aw_m, gout, tiles=tiles_m, layout=lm),
-                    args.iters)
-        print(json.dumps({"regime": regime, "T": args.T, "kernel": "bwd_win_level_major", "us": round(us, 2)}),
-              flush=True)
-        for e in args.exps.split(","):
-            os.environ["MSDA_HIP_WIN_EXP"] = e
-            us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout, tiles=tiles), args.iters)
-            print(json.dumps({"regime": regime, "T": args.T, "kernel": "bwd_win", "exp": int(e), "us": round(us, 2)}),
-                  flush=True)
+        for qo in args.qorders.split(","):
+            os.environ["MSDA_HIP_QORDER"] = qo
+            tag = {"regime": regime, "T": args.T, "qorder": int(qo)}
+            for flag in args.fwd_lds.split(","):
+                os.environ["MSDA_HIP_FWD_LDS"] = flag
+                us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True), args.iters)
+                print(json.dumps({**tag, "kernel": "fwd_tiles", "lds": int(flag), "us": round(us, 2)}), flush=True)
+            os.environ["MSDA_HIP_FWD_LDS"] = "0"
+            _, tiles = msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True)
+            lm = msda.LEVEL_MAJOR
+            loc_m, aw_m = loc.permute(0, 2, 3, 1, 4).contiguous(), aw.permute(0, 2, 3, 1, 4).contiguous()
+            us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc_m, aw_m, layout=lm), args.iters)
+            print(json.dumps({**tag, "kernel": "fwd_tiles_level_major", "us": round(us, 2)}), flush=True)
+            _, tiles_m = msda.msda_forward(value, shapes, starts, loc_m, aw_m, want_tiles=True, layout=lm)
+            us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc_m, aw_m, gout, tiles=tiles_m, layout=lm),
+                        args.iters)
+            print(json.dumps({**tag, "kernel": "bwd_win_level_major", "us": round(us, 2)}), flush=True)
+            for e in args.exps.split(","):
+                os.environ["MSDA_HIP_WIN_EXP"] = e
+                us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout, tiles=tiles), args.iters)
+                print(json.dumps({**tag, "kernel": "bwd_win", "exp": int(e), "us": round(us, 2)}), flush=True)
+            os.environ["MSDA_HIP_WIN_EXP"] = "0"
         os.environ["MSDA_HIP_WIN_EXP"] = "0"
 
 
