@@ -243,12 +243,15 @@ class DeformableTransformerEncoder(nn.Module):
                 rank_keep = (torch.arange(topk.shape[1], device=topk.device)[None, :]
                              < sparse_token_nums.to(topk.device)[:, None])
             if topk.is_cuda:
-                # the refined tokens in position order: every layer treats them independently and scatters
-                # them back by position, so the order is free — and with neighbouring tokens next to each
-                # other the MSDA backward takes the row-block kernel (each query tile touches a short row
-                # interval) instead of the per-tap kernel.  The returned per-token tensors are put back
-                # into score order (``inv``), as the reference returns them.
-                topk, order = topk.sort(dim=1)
+                # the refined tokens in position order (their reference points; tokens of every level
+                # interleaved): every layer treats them independently and scatters them back by index,
+                # so the order is free — and with neighbouring tokens next to each other the MSDA
+                # backward takes the row-block kernel (each query tile touches a short row interval of
+                # every level) instead of the per-tap kernel.  The returned per-token tensors are put
+                # back into score order (``inv``), as the reference returns them.
+                key = reference_points[:, :, 0, 0].gather(1, topk)
+                order = key.sort(dim=1, stable=True)[1]
+                topk = topk.gather(1, order)
                 inv = torch.argsort(order, dim=1)
                 if sparse_token_nums is not None:
                     rank_keep = rank_keep.gather(1, order)

@@ -597,6 +597,52 @@ def test_position_order_tiles_equal_consecutive_tiles(dev, monkeypatch, shapes, 
         assert torch.equal(x, y)
 
 
+def test_bf16_sparse_bench_instantiation_matches_oracle(dev, monkeypatch):
+    """The Sparse-DETR encoder call of the sparse bench line (rho = 0.3: 577 of the 1920 tokens of
+    the T = 1024 pyramid, B = 8, bf16, reference coordinate layout), default path with no
+    environment forcing, through the autograd Function: the top-k tokens in position order as
+    models/sparse/unimodal_sparse_deformable_transformer.py hands them over (reference points of
+    every level interleaved), each sampling around its own position, so the backward takes the
+    row-block kernel (win_applies: Lq P >= 2048 on >= 64-row levels).  Clips 0 and 7 against the
+    oracle on the same bf16-rounded inputs in fp32 (reference attention.py:331-383, sparse
+    transformer :210-218, 425-450)."""
+    for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH",
+              "MSDA_HIP_QORDER"):
+        monkeypatch.delenv(k, raising=False)
+    shapes, B, M, D, P, Lq = [1024, 512, 256, 128], 8, 8, 64, 4, 577
+    S = sum(shapes)
+    value, _, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=113, lo=0.0, hi=1.0)
+    pos = torch.cat([(torch.arange(T, dtype=torch.float64) + 0.5) / T for T in shapes])
+    gen = torch.Generator().manual_seed(114)
+    loc = torch.empty(B, Lq, M, len(shapes), P, dtype=torch.float64)
+    for b in range(B):
+        tok = torch.randperm(S, generator=gen)[:Lq]
+        tok = tok[pos[tok].sort(stable=True)[1]]
+        for l, T in enumerate(shapes):
+            off = (torch.rand(Lq, M, P, generator=gen, dtype=torch.float64) * 8 - 4) / T
+            loc[b, :, :, l] = pos[tok][:, None, None] + off
+    loc = loc.float()
+    starts = O.level_starts(shapes)
+    v = value.cuda().requires_grad_(True)
+    lc, a = loc.cuda().requires_grad_(True), aw.cuda().requires_grad_(True)
+    out = msda.msda_apply(v, shapes, starts, lc, a, "border")
+    out.backward(gout.cuda())
+    torch.cuda.synchronize()
+    lib = PKG._native.load_library()
+    nb = lib.msda_hip_forward_tiles_bytes(PKG._native.DTYPE_TAGS[torch.bfloat16], PKG._native.host_i64_array(shapes),
+                                          len(shapes), B, S, M, D, Lq, P)
+    assert nb > 0  # the tiles forward + row-block backward take this call
+    eps = 2 ** -8
+    for b in (0, B - 1):
+        v32, g32 = value[b:b + 1].float(), gout[b:b + 1].float()
+        r_out = O.msda_forward(_np(v32), shapes, _np(loc[b:b + 1]), _np(aw[b:b + 1]))
+        r_gv, r_gl, r_ga = O.msda_backward(_np(v32), shapes, _np(loc[b:b + 1]), _np(aw[b:b + 1]), _np(g32))
+        np.testing.assert_allclose(_np(out[b:b + 1]), r_out, rtol=eps, atol=eps * np.abs(r_out).max())
+        np.testing.assert_allclose(_np(v.grad[b:b + 1]), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
+        np.testing.assert_allclose(_np(a.grad[b:b + 1]), r_ga, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(_np(lc.grad[b:b + 1]), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))
+
+
 @pytest.mark.parametrize("padding", ["border", "zeros"])
 @pytest.mark.parametrize("case", range(len(WIN_CASES)))
 def test_lds_staged_forward_equals_gather_forward(dev, monkeypatch, case, padding):
