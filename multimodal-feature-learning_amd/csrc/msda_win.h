@@ -14,7 +14,9 @@
 // n_l - 1 of level l, n_l = T_l / T_{L-1}), chunks in order, and a tile is 32 consecutive
 // entries of that order — every tile a short stretch of every level (bench encoder call: 720 ->
 // 416 visits per (b, m), tools/win_visits.py).  Grouping only: every sample is still handled once
-// per level by the blocks holding its taps, so results are the same bit for bit.
+// per level by the blocks holding its taps — the forward output and the coordinate gradients are
+// the same bit for bit; grad_value rows add the same terms in another order (fp32 accumulation,
+// one bf16 rounding).
 constexpr int kQOrderMaxL = 4;
 struct QOrder {
   int cs;        // entries per chunk (sum of n); 0: consecutive queries
@@ -23,14 +25,20 @@ struct QOrder {
   int n[kQOrderMaxL], start[kQOrderMaxL];
 };
 
-// Position order when the call is encoder-shaped (Lq == S, 2 <= L <= 4, every T_l a multiple of
-// T_{L-1}, level starts the running sums, Lq < 2^22 so the float chunk division is exact);
-// MSDA_HIP_QORDER=0 keeps consecutive tiles.  The forward that writes the tile intervals and the
-// backward that reads them both call this on the same shapes.
+// Measured (tools/win_exp.py, bench encoder call, one MI355X): fewer visits but SLOWER — backward
+// 49.3 / 57.3 us (init / trained sampling) against 46.5 / 51.9 with consecutive tiles, the tiles
+// forward 35.3 against 31.0: the grad_out loads of a visit (exp 8 in win_exp) cost 13.8 against
+// 9.1 us — a tile's rows now come from four separate stretches of grad_out.  So consecutive tiles
+// stay the default and MSDA_HIP_QORDER=1 opts in (A/B).  (The Sparse-DETR encoder instead hands
+// its top-k queries over already sorted by position: models/sparse/.)
+// Position order applies when the call is encoder-shaped (Lq == S, 2 <= L <= 4, every T_l a
+// multiple of T_{L-1}, level starts the running sums, Lq < 2^22 so the float chunk division is
+// exact).  The forward that writes the tile intervals and the backward that reads them both call
+// this on the same shapes.
 inline QOrder make_qorder(long long Lq, long long S, int L, const int* T, const int* start) {
   QOrder o{};
   const char* e = getenv("MSDA_HIP_QORDER");
-  if ((e != nullptr && atoi(e) == 0) || Lq != S || L < 2 || L > kQOrderMaxL || Lq >= (1LL << 22)) return o;
+  if (e == nullptr || atoi(e) != 1 || Lq != S || L < 2 || L > kQOrderMaxL || Lq >= (1LL << 22)) return o;
   const int tc = T[L - 1];
   if (tc < 1) return o;
   int cs = 0, run = 0;

@@ -31,8 +31,8 @@ def make(regime, B, Lq, shapes, M, P, dtype, dev, seed=0):
         ref = torch.cat([(torch.arange(t, dtype=torch.float32) + 0.5) / t for t in shapes])
     elif Lq == 1920:  # cross-modal: the video tokens' reference points over the audio pyramid
         ref = torch.cat([(torch.arange(t, dtype=torch.float32) + 0.5) / t for t in (1024, 512, 256, 128)])
-    else:
-        ref = torch.rand(Lq, generator=g)
+    else:  # the Sparse-DETR encoder's top-k tokens, handed over in position order
+        ref = torch.rand(Lq, generator=g).sort()[0]
     ref = ref.view(1, Lq, 1, 1, 1).expand(B, Lq, M, L, P)
     T = torch.tensor(shapes, dtype=torch.float32).view(1, 1, 1, L, 1)
     theta = torch.arange(M, dtype=torch.float32) * (2 * 3.141592653589793 / M)

@@ -20,18 +20,20 @@ def main():
     ap.add_argument("--regimes", default="init,trained")
     ap.add_argument("--exps", default="0,1,2,4,5,7,13,37,45")
     ap.add_argument("--T", type=int, default=1024)
+    ap.add_argument("--lq", type=int, default=0, help="queries (0: S, the encoder call; 577: the sparse encoder)")
     ap.add_argument("--qorders", default="1,0", help="MSDA_HIP_QORDER values (tile order of the queries)")
     ap.add_argument("--fwd-lds", default="0", help="MSDA_HIP_FWD_LDS values to time")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     shapes = [args.T, args.T // 2, args.T // 4, args.T // 8]
-    S, Lq, M, P, B = sum(shapes), sum(shapes), 8, 4, 8
+    S, M, P, B = sum(shapes), 8, 4, 8
+    Lq = args.lq or S
     starts = [sum(shapes[:i]) for i in range(4)]
     for regime in args.regimes.split(","):
         value, loc, aw, gout = make(regime, B, Lq, shapes, M, P, torch.bfloat16, dev)
         for qo in args.qorders.split(","):
             os.environ["MSDA_HIP_QORDER"] = qo
-            tag = {"regime": regime, "T": args.T, "qorder": int(qo)}
+            tag = {"regime": regime, "T": args.T, "Lq": Lq, "qorder": int(qo)}
             for flag in args.fwd_lds.split(","):
                 os.environ["MSDA_HIP_FWD_LDS"] = flag
                 us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True), args.iters)
