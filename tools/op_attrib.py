@@ -1,0 +1,80 @@
+#!/usr/bin/env python3
+"""Which Python call sites launch the step's small kernels: torch.profiler over eager steps of a
+bench.py workload (same model, batch and trainer as bench.py builds them), device time grouped by
+(op, innermost package frames).  The graph replay runs the same kernels (bench.py's eager timer
+steps rely on that too).
+
+usage: op_attrib.py [--config core|dvc|sparse] [--steps 2] [--top 60] [--frames 4]"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+from torch.profiler import ProfilerActivity, profile  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="core")
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--top", type=int, default=60)
+    ap.add_argument("--frames", type=int, default=4)
+    a = ap.parse_args()
+    sys.argv = [sys.argv[0], "--config", a.config, "--graph", "0", "--cpu-baseline", "0"]
+    import bench
+    args = bench.parse()
+    dev = torch.device("cuda", 0)
+    bench.PKG._native.load_library()
+    model = bench.build_model(args, dev)
+    batch = bench.build_batch(args, 0, dev)
+    trainer = bench.PKG.train_step.FlatGradTrainer(model, bench.loss_fn(args, batch, model), lr=1e-4,
+                                                   weight_decay=1e-4, max_norm=0.1, use_bf16=True, graph=False)
+    trainer.capture(batch)
+    for _ in range(2):
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    # shapes of the caption decoder's segment attention calls (csrc/seg_attention.hip)
+    SA = bench.PKG.models.modules.seg_attention._SegmentAttention
+    fwd0, seen = SA.forward, []
+
+    def fwd(ctx, q, pk, pv, bias_k, bias_v, index, keep, masked, *rest):
+        live = keep if masked is None else keep & ~masked
+        seen.append((tuple(q.shape), tuple(pk.shape), live.sum(1).float().mean().item(),
+                     keep.sum(1).float().mean().item()))
+        return fwd0(ctx, q, pk, pv, bias_k, bias_v, index, keep, masked, *rest)
+    SA.forward = staticmethod(fwd)
+    trainer.step(batch)
+    torch.cuda.synchronize()
+    SA.forward = fwd0
+    for s in seen:
+        print("seg_attention q", s[0], "memory", s[1], f"unmasked keys/segment {s[2]:.0f}, keep {s[3]:.0f}")
+    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+        for _ in range(a.steps):
+            trainer.step(batch)
+        torch.cuda.synchronize()
+
+    pkg_dir = os.path.join(ROOT, "multimodal-feature-learning_amd")
+    rows = {}
+    for evt in prof.events():
+        dt = getattr(evt, "self_device_time_total", None)
+        if dt is None:
+            dt = evt.self_cuda_time_total
+        if not dt:
+            continue
+        frames = [f for f in (evt.stack or []) if pkg_dir in f or "bench.py" in f]
+        where = " <- ".join(f.replace(pkg_dir + "/", "") for f in frames[:a.frames]) or "(no package frame)"
+        key = (evt.name[:60], where)
+        r = rows.setdefault(key, [0.0, 0])
+        r[0] += dt
+        r[1] += 1
+    total = sum(v[0] for v in rows.values())
+    print(f"device time {total / a.steps / 1e3:.2f} ms/step over {a.steps} eager steps ({args.config})")
+    for (name, where), (t, n) in sorted(rows.items(), key=lambda kv: -kv[1][0])[:a.top]:
+        print(f"{t / a.steps:9.1f} us {n / a.steps:6.1f}x  {name}\n            {where}")
+
+
+if __name__ == "__main__":
+    main()
