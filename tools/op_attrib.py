@@ -4,7 +4,7 @@ bench.py workload (same model, batch and trainer as bench.py builds them), devic
 (op, innermost package frames).  The graph replay runs the same kernels (bench.py's eager timer
 steps rely on that too).
 
-usage: op_attrib.py [--config core|dvc|sparse] [--steps 2] [--top 60] [--frames 4]"""
+usage: op_attrib.py [--config video|dvc|sparse] [--steps 2] [--top 60] [--frames 4]"""
 import argparse
 import os
 import sys
@@ -18,7 +18,7 @@ from torch.profiler import ProfilerActivity, profile  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--config", default="core")
+    ap.add_argument("--config", default="video")
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--top", type=int, default=60)
     ap.add_argument("--frames", type=int, default=4)

@@ -1,44 +1,90 @@
 #!/usr/bin/env python3
-"""Which PyTorch ops launch the step's small kernels?  One eager bench step (bf16 autocast,
-B=8, T=1024) under torch.profiler; prints the aten ops by device time with call counts and
-the most frequent input shapes of the elementwise ones.  Diagnostic only."""
+"""Census of the glue ops of one eager bench step (copies, casts, cats, reductions, fills, adds …):
+each aten op with its argument shapes / dtypes and the innermost package frames that issued it
+(backward ops of built-in autograd nodes carry no Python frame: their shapes name them), ranked
+by output bytes.  A TorchDispatchMode sees every op of the forward and of the backward.
+
+usage: op_census.py [--config video|dvc|sparse] [--top 80]"""
+import argparse
 import collections
-import importlib
 import os
 import sys
-
-import torch
-from torch.profiler import ProfilerActivity, profile
+import traceback
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-PKG = importlib.import_module("multimodal-feature-learning_amd")
+
+import torch  # noqa: E402
+from torch.utils._python_dispatch import TorchDispatchMode  # noqa: E402
+
+GLUE = ("copy", "_to_copy", "cat", "sum", "add", "fill", "zero", "mul", "div", "sub", "clone", "contiguous",
+        "stack", "index", "gather", "scatter", "where", "masked", "expand", "repeat", "mean", "neg", "exp",
+        "pow", "sqrt", "cumsum", "ne", "eq", "lt", "gt", "le", "ge", "bitwise", "logical", "copy_", "full",
+        "empty_strided", "new_zeros", "zeros", "ones", "arange", "select_backward", "slice_backward",
+        "constant_pad", "nonzero", "sort", "argsort", "topk")
+
+
+def sig(x):
+    if isinstance(x, torch.Tensor):
+        return f"{str(x.dtype).replace('torch.', '')}{list(x.shape)}"
+    if isinstance(x, (list, tuple)):
+        return "[" + ",".join(sig(y) for y in x[:4]) + ("…" if len(x) > 4 else "") + "]"
+    return ""
+
+
+def nbytes(out):
+    if isinstance(out, torch.Tensor):
+        return out.numel() * out.element_size()
+    if isinstance(out, (list, tuple)):
+        return sum(nbytes(o) for o in out)
+    return 0
+
+
+class Census(TorchDispatchMode):
+    def __init__(self, pkg_dir):
+        super().__init__()
+        self.pkg_dir = pkg_dir
+        self.rows = collections.defaultdict(lambda: [0, 0])
+
+    def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+        out = func(*args, **(kwargs or {}))
+        name = str(func.overloadpacket.__name__)
+        if any(g in name for g in GLUE):
+            fr = [f for f in traceback.extract_stack()[:-1] if self.pkg_dir in f.filename or "bench.py" in f.filename]
+            where = " <- ".join(f"{os.path.relpath(f.filename, self.pkg_dir)}:{f.lineno}" for f in fr[::-1][:3])
+            key = (name, " ".join(s for s in (sig(a) for a in args) if s), where or "(autograd node)")
+            r = self.rows[key]
+            r[0] += 1
+            r[1] += nbytes(out)
+        return out
 
 
 def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="video")
+    ap.add_argument("--top", type=int, default=80)
+    a = ap.parse_args()
+    sys.argv = [sys.argv[0], "--config", a.config, "--graph", "0", "--cpu-baseline", "0"]
+    import bench
+    args = bench.parse()
     dev = torch.device("cuda", 0)
-    torch.manual_seed(0)
-    model = PKG.dvc_core.DeformableDVCCore(d_model=512, num_queries=100, dropout=0.1).to(dev)
-    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, graph=False)
-    batch = PKG.dvc_core.synthetic_clips(8, T=1024, device=dev)
-    print("params:", len(tr.params), "elements:", tr.flat_grad.numel())
+    bench.PKG._native.load_library()
+    model = bench.build_model(args, dev)
+    batch = bench.build_batch(args, 0, dev)
+    trainer = bench.PKG.train_step.FlatGradTrainer(model, bench.loss_fn(args, batch, model), lr=1e-4,
+                                                   weight_decay=1e-4, max_norm=0.1, use_bf16=True, graph=False)
+    trainer.capture(batch)
     for _ in range(2):
-        tr.eager_step(batch)
+        trainer.step(batch)
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], record_shapes=True) as prof:
-        tr.eager_step(batch)
-        torch.cuda.synchronize()
-    ka = prof.key_averages()
-    rows = sorted(ka, key=lambda e: -e.device_time_total)[:40]
-    for e in rows:
-        print(f"{e.key[:60]:60s} calls={e.count:5d} dev_ms={e.device_time_total / 1e3:8.3f}")
-    shapes = collections.Counter()
-    for e in prof.key_averages(group_by_input_shape=True):
-        if e.key in ("aten::add_", "aten::mul", "aten::add", "aten::copy_", "aten::_to_copy", "aten::sum",
-                     "aten::mul_", "aten::div", "aten::fill_", "aten::zero_"):
-            shapes[(e.key, str(e.input_shapes)[:120])] += e.count
-    for (k, s), n in shapes.most_common(40):
-        print(f"{n:5d} {k:16s} {s}")
+    c = Census(os.path.join(ROOT, "multimodal-feature-learning_amd"))
+    with c:
+        trainer.step(batch)
+    torch.cuda.synchronize()
+    tot_n = sum(v[0] for v in c.rows.values())
+    print(f"{a.config}: {tot_n} glue ops in one step, {sum(v[1] for v in c.rows.values()) / 1e6:.1f} MB written")
+    for (name, s, where), (n, b) in sorted(c.rows.items(), key=lambda kv: -kv[1][1])[:a.top]:
+        print(f"{b / 1e6:8.2f} MB {n:4d}x  {name} {s[:110]}\n              {where}")
 
 
 if __name__ == "__main__":
