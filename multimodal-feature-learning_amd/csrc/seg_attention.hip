@@ -55,6 +55,7 @@ struct Args {
   const int32_t* order;  // segments in dispatch order (sorted by clip: the clip's rows stay in L2), or null
   const uint8_t *keep, *masked;
   int n, B, K, Lq, H;
+  int vbits;  // keep / masked rows readable 16 bytes at a time (K % 16 == 0, 16-byte aligned)
   float scale, p;
   const int64_t* seed;
   uint16_t* out;
@@ -127,11 +128,66 @@ __device__ __forceinline__ uint32_t in_mask(int j0, int K) {
   return j0 + KB <= K ? 0xffffffffu : (j0 >= K ? 0u : (1u << (K - j0)) - 1u);
 }
 
+// bit i of the result: byte i of v is non-zero (nonzero) / zero (!nonzero)
+__device__ __forceinline__ uint32_t byte_bits16(uint4 v, bool nonzero) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  uint32_t r = 0u;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) r |= (uint32_t)((((w[i >> 2] >> (8 * (i & 3))) & 0xffu) != 0u) == nonzero) << i;
+  return r;
+}
+
+// the unmasked / kept-row bits of keys j0 .. j0+31 of segment s (masked to the keys that exist)
+__device__ __forceinline__ void block_bits(const Args& a, int s, int j0, uint32_t& live, uint32_t& keep) {
+  const uint32_t inm = in_mask(j0, a.K);
+  const long long e = (long long)s * a.K + j0;
+  if (a.vbits) {
+    const bool two = j0 + 16 < a.K;
+    keep = byte_bits16(*reinterpret_cast<const uint4*>(a.keep + e), true) |
+           (two ? byte_bits16(*reinterpret_cast<const uint4*>(a.keep + e + 16), true) << 16 : 0u);
+    live = a.masked == nullptr
+               ? inm
+               : byte_bits16(*reinterpret_cast<const uint4*>(a.masked + e), false) |
+                     (two ? byte_bits16(*reinterpret_cast<const uint4*>(a.masked + e + 16), false) << 16 : 0u);
+  } else {
+    live = keep = 0u;
+    for (int kk = 0; kk < KB && j0 + kk < a.K; ++kk) {
+      keep |= (uint32_t)(a.keep[e + kk] != 0) << kk;
+      live |= (uint32_t)(a.masked == nullptr || a.masked[e + kk] == 0) << kk;
+    }
+  }
+  live &= inm;
+  keep &= inm;
+}
+
 // the segment's unmasked / kept-row bits per 32-key block into LDS; returns whether every key is
-// masked (block-wide: the barrier also publishes the words)
+// masked (block-wide: the barrier also publishes the words).  With 16-byte rows (a.vbits) every
+// thread turns 16 keys' bytes into bits with one load of each mask — one round trip for K <= 4096
+// (the byte-per-lane loop below costs a dependent round trip per 4 blocks: at the DVC step's
+// K = 1920 that scan was most of the kernels' time)
 __device__ __forceinline__ bool segment_bits(const Args& a, int s, uint32_t* s_live, uint32_t* s_keep, int nblk,
                                              int wave, int lane) {
   int any = 0;
+  if (a.vbits) {
+    const int nch = a.K >> 4;  // 16-key chunks; chunk c = half (c & 1) of block c / 2
+    const int tid = wave * 64 + lane;
+    for (int c0 = 0; c0 < nch; c0 += kThreads) {
+      const int c = c0 + tid;
+      uint32_t lv = 0u, kp = 0u;
+      if (c < nch) {
+        const long long e = (long long)s * a.K + 16 * c;
+        kp = byte_bits16(*reinterpret_cast<const uint4*>(a.keep + e), true);
+        lv = a.masked == nullptr ? 0xffffu : byte_bits16(*reinterpret_cast<const uint4*>(a.masked + e), false);
+      }
+      const uint32_t lv1 = __shfl_xor(lv, 1), kp1 = __shfl_xor(kp, 1);  // (c and c ^ 1: neighbouring lanes)
+      if (c < nch && (c & 1) == 0) {
+        s_live[c >> 1] = lv | (lv1 << 16);
+        s_keep[c >> 1] = kp | (kp1 << 16);
+      }
+      any |= lv != 0u;
+    }
+    return !__syncthreads_or(any);
+  }
   for (int blk = wave; blk < nblk; blk += kWaves) {
     const int j = blk * KB + (lane & 31);
     const bool lo = lane < 32 && j < a.K;
@@ -644,11 +700,16 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
   const float dscale = 1.f / (1.f - a.p);
   for (int c0 = 0; c0 < a.n; c0 += kListChunk) {
     // the segments of this chunk that read clip b, in order (4 candidates a thread, block prefix sum)
+    // (only those giving some kept key of this block a non-zero weight: the others add nothing)
     int flags = 0;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int s = c0 + tid * 4 + i;
-      if (s < a.n && a.index[s] == b) flags |= 1 << i;
+      if (s < a.n && a.index[s] == b) {
+        uint32_t lv, kp;
+        block_bits(a, s, j0, lv, kp);
+        if (((a.dead[s] != 0 ? inm : lv) & kp) != 0u) flags |= 1 << i;
+      }
     }
     const int cnt = __popc(flags);
     int x = cnt;
@@ -805,6 +866,7 @@ int mfl_seg_attention_forward(const void* q, const void* pk, const void* pv, con
   a.keep = keep;
   a.masked = masked;
   a.n = (int)n, a.B = (int)B, a.K = (int)K, a.Lq = (int)Lq, a.H = (int)H;
+  a.vbits = K % 16 == 0 && aligned16(keep) && aligned16(masked);
   a.scale = scale, a.p = seed ? p_drop : 0.f, a.seed = seed;
   a.out = static_cast<uint16_t*>(out);
   a.lse = lse;
@@ -837,6 +899,7 @@ int mfl_seg_attention_backward(const void* q, const void* pk, const void* pv, co
   a.keep = keep;
   a.masked = masked;
   a.n = (int)n, a.B = (int)B, a.K = (int)K, a.Lq = (int)Lq, a.H = (int)H;
+  a.vbits = K % 16 == 0 && aligned16(keep) && aligned16(masked);
   a.scale = scale, a.p = seed ? p_drop : 0.f, a.seed = seed;
   a.out = static_cast<uint16_t*>(const_cast<void*>(out));
   a.lse = const_cast<float*>(lse);

@@ -73,6 +73,7 @@ CASES = [
     (5, 2, 1000, 32, 8, ()),         # K not a multiple of 32, full 32-query tile
     (3, 3, 64, 1, 2, (1,)),          # one query, two heads
     (7, 1, 333, 11, 4, (0, 6)),
+    (4, 2, 240, 19, 8, (2,)),        # K a multiple of 16, not of 32 (16-byte mask rows, half last block)
 ]
 
 
