@@ -19,7 +19,7 @@ from .models.deformable.multimodal_deformable_transformer import MultimodalDefor
 from .models.deformable.unimodal_deformable_transformer import DeformableTransformer
 from .models.sparse.unimodal_sparse_deformable_transformer import SparseDeformableTransformer
 from .models.modules.embedding_layers import FFN, PositionEmbeddingVideoSine
-from .models.modules.misc_modules import inverse_sigmoid, predict_event_num, predict_event_num_with_depth
+from .models.modules.misc_modules import inverse_sigmoid, level_heads, predict_event_num, predict_event_num_with_depth
 from .utils.dam import attn_map_to_flat_grid
 from .models.modules.linear import Linear
 
@@ -74,23 +74,7 @@ class DeformableDVCCore(nn.Module):
                 "hs": hs, "inter_references": inter, "memory": memory}
 
 
-def _level_heads(core, hs):
-    """Class / segment / count heads on every decoder level of hs (depth, B, Q, d), stacked over
-    levels (reference unimodal_deformable_dvc.py:197-203, heads applied per level).  The reference
-    builds the per-level heads as ONE shared module (:72-74), so here each head runs once over the
-    stacked levels (row-wise layers: the same numbers, a sixth of the launches, and no per-level
-    select whose backward writes a full-size zero gradient per level); distinct per-level heads
-    run level by level."""
-    heads = (core.class_embedding, core.segment_embedding, core.count_head)
-    if all(all(m is h[0] for m in h) for h in heads):
-        return (core.class_embedding[0](hs).softmax(dim=-1), core.segment_embedding[0](hs).sigmoid(),
-                predict_event_num_with_depth(core.count_head[0], hs))
-    classes, segments, counts = [], [], []
-    for lvl, h in enumerate(hs.unbind(0)):
-        classes.append(core.class_embedding[lvl](h).softmax(dim=-1))
-        segments.append(core.segment_embedding[lvl](h).sigmoid())
-        counts.append(predict_event_num(core.count_head[lvl], h))
-    return torch.stack(classes), torch.stack(segments), torch.stack(counts)
+_level_heads = level_heads  # (models/modules/misc_modules.py)
 
 
 def synthetic_clips(batch, T=1024, feature_dim=512, padded=False, seed=0, device="cpu", dtype=torch.float32):

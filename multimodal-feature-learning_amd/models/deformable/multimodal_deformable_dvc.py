@@ -31,7 +31,7 @@ from ..dvc_common import append_end_token, context_mask, look_ahead_mask, make_p
 from ..modules.embedding_layers import PositionEmbeddingVideoSine
 from ..modules.layers import FFN, ContextMaskModel
 from ..modules.linear import Linear
-from ..modules.misc_modules import inverse_sigmoid, predict_event_num
+from ..modules.misc_modules import inverse_sigmoid, predict_event_num, predict_event_num_with_depth
 from ..multimodal_caption_decoder import build_multimodal_caption_decoder
 from ...utils.preds_postprocess import crop_segments
 from .multimodal_deformable_transformer import build_multimodal_deformable_transformer
@@ -104,15 +104,25 @@ class MultimodalDeformableDVC(nn.Module):
                                                               a[5], False)
         if not self.aux_loss:
             query_features, inter_references = query_features[-1:], inter_references[-1:]
-        classes, counts, segments = [], [], []
-        for lvl in range(query_features.shape[0]):
-            classes.append(self.class_embedding[lvl](query_features[lvl]).softmax(dim=-1))
-            seg = self.segment_embedding[lvl](query_features[lvl])
-            counts.append(predict_event_num(self.count_head[lvl], query_features[lvl]))
-            reference = inverse_sigmoid(init_reference if lvl == 0 else inter_references[lvl - 1])
-            assert reference.shape[-1] in (1, 2)
-            segments.append((seg + reference).sigmoid())  # ``output_segment[..., :2] += reference`` (:220-226)
-        heads = (torch.stack(classes), torch.stack(segments), torch.stack(counts))
+        nl = query_features.shape[0]
+        refs = [init_reference if lvl == 0 else inter_references[lvl - 1] for lvl in range(nl)]
+        assert all(r.shape[-1] in (1, 2) for r in refs)
+        shared = all(all(m is h[0] for m in h) for h in (self.class_embedding, self.segment_embedding, self.count_head))
+        if shared and all(r.shape == refs[0].shape for r in refs):
+            # the reference's heads are one shared module per kind (:72-74): one call over the stacked
+            # levels (row-wise layers; each weight's gradient from one GEMM, not six accumulated)
+            heads = (self.class_embedding[0](query_features).softmax(dim=-1),
+                     # ``output_segment[..., :2] += reference`` (:220-226)
+                     (self.segment_embedding[0](query_features) + inverse_sigmoid(torch.stack(refs))).sigmoid(),
+                     predict_event_num_with_depth(self.count_head[0], query_features))
+        else:
+            classes, counts, segments = [], [], []
+            for lvl in range(nl):
+                classes.append(self.class_embedding[lvl](query_features[lvl]).softmax(dim=-1))
+                seg = self.segment_embedding[lvl](query_features[lvl])
+                counts.append(predict_event_num(self.count_head[lvl], query_features[lvl]))
+                segments.append((seg + inverse_sigmoid(refs[lvl])).sigmoid())
+            heads = (torch.stack(classes), torch.stack(segments), torch.stack(counts))
         out = {'pred_logits': heads[0][-1], 'pred_count': heads[2][-1], 'pred_segments': heads[1][-1]}
         return out, query_features, video_memory, audio_memory, heads
 

@@ -29,7 +29,7 @@ from ..dvc_common import (append_end_token, context_mask, make_padding_mask, mak
 from ..modules.embedding_layers import PositionEmbeddingVideoSine
 from ..modules.layers import FFN, ContextMaskModel
 from ..modules.linear import Linear
-from ..modules.misc_modules import predict_event_num
+from ..modules.misc_modules import level_heads
 from ...utils.preds_postprocess import SegmentMemory
 from ..unimodal_caption_decoder import build_unimodal_caption_decoder
 from .unimodal_deformable_transformer import build_unimodal_deformable_transformer
@@ -93,12 +93,8 @@ class UnimodalDeformableDVC(nn.Module):
         _, tgt, reference_points, qw = tr.prepare_decoder_input_query(B, qw)
         query_features, _ = tr.forward_decoder(tgt, reference_points, memory, shapes, starts, valid, qw,
                                                mask_flatten, proposals_mask, False)
-        classes, counts, segments = [], [], []
-        for lvl in range(query_features.shape[0]):
-            classes.append(self.class_embedding[lvl](query_features[lvl]).softmax(dim=-1))
-            segments.append(self.segment_embedding[lvl](query_features[lvl]).sigmoid())
-            counts.append(predict_event_num(self.count_head[lvl], query_features[lvl]))
-        heads = (torch.stack(classes), torch.stack(segments), torch.stack(counts))
+        # reference :197-203 applies the (shared) heads level by level: one call over the stacked levels
+        heads = level_heads(self, query_features)
         out = {'pred_logits': heads[0][-1], 'pred_segments': heads[1][-1], 'pred_count': heads[2][-1]}
         return out, query_features, memory, heads
 
