@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--B", type=int, default=8)
     ap.add_argument("--shapes", default="enc,dec")
     ap.add_argument("--kernels", default="fwd,bwd_loc_aw,bwd_value,bwd_all,prologue_fwd,prologue_bwd")
+    ap.add_argument("--layout", default="reference", choices=["reference", "level_major"],
+                    help="coordinate layout of fwd / bwd_all (level_major: the bench step's encoder calls)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     M, L, P, D = 8, 4, 4, 64
@@ -93,14 +95,20 @@ def main():
                 bwd_b = msda.algorithmic_bytes("bwd", args.B, S, M, D, Lq, L, P, vb)
                 # as the training step runs them: the forward also writes the row-block backward's
                 # tile intervals where that backward runs, and the backward reads them
-                _, tiles = msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True)
+                lay, lc, a = 0, loc, aw
+                if args.layout == "level_major" and msda.level_major_ok(value, shapes, Lq, P):
+                    lay = msda.LEVEL_MAJOR
+                    lc, a = loc.permute(0, 2, 3, 1, 4).contiguous(), aw.permute(0, 2, 3, 1, 4).contiguous()
+                _, tiles = msda.msda_forward(value, shapes, starts, lc, a, want_tiles=True, layout=lay)
                 runs = {
-                    "fwd": (lambda: msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True), fwd_b),
+                    "fwd": (lambda: msda.msda_forward(value, shapes, starts, lc, a, want_tiles=True, layout=lay),
+                            fwd_b),
                     "bwd_loc_aw": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout,
                                                               need_value=False), None),
                     "bwd_value": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout,
                                                              need_loc=False, need_aw=False), None),
-                    "bwd_all": (lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout, tiles=tiles), bwd_b),
+                    "bwd_all": (lambda: msda.msda_backward(value, shapes, starts, lc, a, gout, tiles=tiles, layout=lay),
+                                bwd_b),
                 }
                 off = (torch.randn(args.B, Lq, M, L, P) * 2).to(dev, dtype)
                 logits = torch.randn(args.B, Lq, M, L * P).to(dev, dtype)
