@@ -15,6 +15,7 @@ state_dicts load unchanged.
 """
 import copy
 import math
+import os
 
 import torch
 import torch.nn.functional as F
@@ -24,7 +25,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..deformable.unimodal_deformable_transformer import encoder_reference_points, level_metadata
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.linear import Linear
-from ..modules.add_norm import add_layer_norm
+from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 from ..modules.ffn import relu_dropout
 from ..modules.misc_modules import inverse_sigmoid
 
@@ -209,6 +210,20 @@ class DeformableTransformerEncoderLayer(nn.Module):
         out = add_layer_norm(query, attn, self.norm1, dropout=self.dropout1)
         return self.forward_ffn(out), sampling_locations, attn_weights
 
+    def forward_carry(self, value, tgt, query, next_pos, reference_points, temporal_shapes, level_start_index,
+                      padding_mask=None):
+        """``forward`` on the top-k tokens with the 16-bit operands carried between layers (bf16
+        autocast on the GPU, as the dense encoder's ``forward_carry``): ``value`` is the whole
+        memory in bf16 (the MSDA value), ``query`` this layer's ``tgt + pos`` (bf16 from the previous
+        layer's fused add + LayerNorm, or fp32 in the first layer).  Returns (tgt, bf16(tgt),
+        bf16(tgt + next_pos) or None, sampling_locations, attn_weights)."""
+        attn, sampling_locations, attn_weights = self.self_attn(query, reference_points, value, temporal_shapes,
+                                                                level_start_index, padding_mask, is_sparse=True)
+        t1, t1_16, _ = add_layer_norm_carry(tgt, attn, self.norm1, dropout=self.dropout1)
+        hidden = relu_dropout(self.linear1(t1_16), self.activation, self.dropout2)
+        out, out16, q16 = add_layer_norm_carry(t1, self.linear2(hidden), self.norm2, next_pos, self.dropout3)
+        return out, out16, q16, sampling_locations, attn_weights
+
 
 class DeformableTransformerEncoder(nn.Module):
     """reference :363-470"""
@@ -269,7 +284,33 @@ class DeformableTransformerEncoder(nn.Module):
                 # scatters them one clip at a time): the others write back their own old value
                 keep = rank_keep.unsqueeze(-1)
         locs, weights, inter = [], [], []
-        for layer in self.layers:
+        carry = (sparsified and self.layers and os.environ.get("MFL_SPARSE_CARRY", "1") != "0"
+                 and all(type(layer) is DeformableTransformerEncoderLayer for layer in self.layers)
+                 and carry_supported(tgt, self.layers[0].norm1))
+        if carry:
+            # bf16 operands carried between the layers as the dense encoder does (no per-layer pos add,
+            # casts of the whole memory or gradient-accumulation kernels): value16 is bf16(output)
+            # kept up to date by the same scatter; the last one is the decoder's bf16 memory
+            value16 = output.to(torch.get_autocast_dtype("cuda"))
+            query = tgt + pos
+            for i, layer in enumerate(self.layers):
+                next_pos = pos if i + 1 < len(self.layers) else None
+                tgt, tgt16, q16, sampling_locations, attn_weights = layer.forward_carry(
+                    value16, tgt, query, next_pos, reference_points, temporal_shapes, level_start_index,
+                    padding_mask)
+                locs.append(sampling_locations)
+                weights.append(attn_weights)
+                new, new16 = tgt, tgt16
+                if sparse_token_nums is not None:
+                    new = torch.where(keep, tgt, torch.gather(output, 1, idx))
+                    new16 = torch.where(keep, tgt16, torch.gather(value16, 1, idx))
+                output = output.scatter(1, idx, new)
+                value16 = value16.scatter(1, idx, new16)
+                query = q16
+                if self.aux_heads:
+                    inter.append(tgt)
+            output._mfl_bf16 = value16
+        for layer in (self.layers if not carry else ()):
             tgt, sampling_locations, attn_weights = layer(output, pos, reference_points, temporal_shapes,
                                                           level_start_index, padding_mask,
                                                           tgt=tgt if sparsified else None)

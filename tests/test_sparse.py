@@ -124,3 +124,34 @@ def test_sparse_step_is_graph_captured(dev):
     for _ in range(3):
         lg, le = tg.step(batch).item(), te.step(batch).item()
         assert abs(lg - le) <= 1e-2 * abs(le) + 1e-2
+
+
+@pytest.mark.gpu
+def test_sparse_encoder_carry_matches_plain_bf16(dev, monkeypatch):
+    """Under bf16 autocast the Sparse-DETR encoder carries its 16-bit operands between layers
+    (``DeformableTransformerEncoderLayer.forward_carry``: bf16(tgt + pos) and bf16(tgt) from the
+    fused add + LayerNorm, the whole memory's bf16 copy kept up to date by the same scatter as the
+    fp32 memory).  Against the plain layer path (MFL_SPARSE_CARRY=0) on padded clips (per-clip
+    top-k counts: the keep masks): the forward is the same arithmetic, bit for bit; gradients are
+    the same terms summed in another order (fp32), within 1e-2 relative."""
+    torch.manual_seed(0)
+    core = PKG.dvc_core.SparseDVCCore(d_model=256, num_queries=10, feature_dim=256, num_heads=4, enc_layers=3,
+                                      dec_layers=2, ff_dim=512, dropout=0.0).to(dev)
+    video, mask, dur = PKG.dvc_core.synthetic_clips(3, T=128, feature_dim=256, padded=True, seed=7, device=dev)
+    res = []
+    for carry in ("1", "0"):
+        monkeypatch.setenv("MFL_SPARSE_CARRY", carry)
+        core.zero_grad(set_to_none=True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = core(video, mask, dur)
+            loss = PKG.dvc_core.sparse_workload_loss(out)
+        loss.backward()
+        res.append(([out[k].detach().float().clone() for k in ("memory", "hs", "all_segments", "all_counts")],
+                    {n: p.grad.detach().clone() for n, p in core.named_parameters() if p.grad is not None}))
+    (fa, ga), (fb, gb) = res
+    for x, y in zip(fa, fb):
+        assert torch.equal(x, y)
+    assert ga.keys() == gb.keys() and len(ga) > 20
+    for n in ga:
+        err = ((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-30)).item()
+        assert err < 1e-2, (n, err)
