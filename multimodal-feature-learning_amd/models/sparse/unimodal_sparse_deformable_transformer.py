@@ -300,7 +300,7 @@ class DeformableTransformerEncoder(nn.Module):
                     padding_mask)
                 locs.append(sampling_locations)
                 weights.append(attn_weights)
-                new, new16 = tgt, tgt16
+                new, new16 = tgt, tgt16.to(value16.dtype)  # (a no-op on the fused path)
                 if sparse_token_nums is not None:
                     new = torch.where(keep, tgt, torch.gather(output, 1, idx))
                     new16 = torch.where(keep, tgt16, torch.gather(value16, 1, idx))
