@@ -240,7 +240,11 @@ class FlatGradTrainer:
                 # tensor: the reduced bucket's views are never handed out (_may_claim)
                 if p.grad.data_ptr() == self.grad_views[i].data_ptr():
                     raise RuntimeError("FlatGradTrainer: a reduced bucket's gradient view was written")
+                # p.grad holds only what arrived since the flush (_flush_bucket released the copied
+                # part): keep it aside and release it too, so a further late gradient is again
+                # just its own increment
                 self._late_add(i, p.grad)
+                p.grad = None
                 return
             first = not self._got[i]
             self._got[i] = True
@@ -274,6 +278,14 @@ class FlatGradTrainer:
             torch._foreach_copy_([v for v, _ in got], [g for _, g in got])
         if missing:
             torch._foreach_zero_(missing)
+        if self._pending is not None:
+            # inside the backward: the copied gradients are released, so a gradient that arrives
+            # for one of these parameters after the reduce (autograd's accumulation after a deferred
+            # delivery, or a parameter found unused last step) reaches the hook as its increment
+            # alone, never as a running total whose copied part would be reduced twice.
+            # (_attach_grads hands the flat views back after the backward.)
+            for i in idx:
+                self.params[i].grad = None
         if self._overlap_now:
             cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
             if cur is not None:

@@ -91,6 +91,22 @@ class Claimy(Branchy):
         return cl(h, self.c) + 0.5 * cl(h * h, self.c)
 
 
+class Mixy(Branchy):
+    """b gets a deferred gradient (delivered at a flush point inside the backward, which completes
+    and reduces b's bucket) and then an autograd gradient from a second use: the late part must be
+    reduced as its own increment, not as p.grad's running total (which would count the deferred
+    part twice)."""
+
+    def forward(self, x, use_b, plain=False):
+        h0 = torch.tanh(torch.nn.functional.linear(x, self.a.weight, self.a.bias))
+        y2 = torch.nn.functional.linear(h0, self.b.weight, self.b.bias)  # autograd's gradient of b: after the flush
+        h1 = torch.sin(torch.nn.functional.linear(x, self.a.weight, self.a.bias))
+        f = LIN.flush_point(h1)  # created after y2: its backward (and the queue flush) runs first
+        y1 = torch.nn.functional.linear(f, self.b.weight, self.b.bias) if plain else \
+            _DeferLinear.apply(f, self.b.weight, self.b.bias)
+        return self.c(y2 + y1 if use_b else y2 + 0.5 * y1)
+
+
 def loss_fn(out):
     return out.square().sum()
 
@@ -145,7 +161,7 @@ def _rank_main(rank, world, port, out_path, kind="branchy"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        model = Claimy() if kind == "claimy" else Branchy()
+        model = {"claimy": Claimy, "mixy": Mixy}.get(kind, Branchy)()
         # one bucket per parameter: b's buckets complete in a different order (or not at all) per rank
         tr = pkg.train_step.FlatGradTrainer(model, loss_fn, lr=1e-2, weight_decay=0.5, use_bf16=False,
                                             graph=False, bucket_mb=1e-6)
@@ -163,7 +179,7 @@ def _rank_main(rank, world, port, out_path, kind="branchy"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind", ["branchy", "claimy"])
+@pytest.mark.parametrize("kind", ["branchy", "claimy", "mixy"])
 def test_gloo_ranks_with_different_unused_parameters(kind):
     """kind "claimy": gradients written straight into the flat buffer's views and deferred
     gradients delivered after the backward — a parameter found unused that comes back on one rank
@@ -177,19 +193,23 @@ def test_gloo_ranks_with_different_unused_parameters(kind):
         assert torch.equal(r[0][step]["params"], r[1][step]["params"])
         grads = []
         for rank in range(2):
-            m = Claimy() if kind == "claimy" else Branchy()
+            m = {"claimy": Claimy, "mixy": Mixy}.get(kind, Branchy)()
             off = 0
             with torch.no_grad():
                 for p in m.parameters():
                     p.copy_(r[0][step]["params"][off:off + p.numel()].view_as(p))
                     off += p.numel()
             x = _x(10 * step + rank)
-            loss_fn(m(x, use[rank], plain=True) if kind == "claimy" else m(x, use[rank])).backward()
+            loss_fn(m(x, use[rank], plain=True) if kind != "branchy" else m(x, use[rank])).backward()
             grads.append(torch.cat([(p.grad if p.grad is not None else torch.zeros_like(p)).reshape(-1)
                                     for p in m.parameters()]))
         want = (grads[0] + grads[1]) / 2
         for rank in range(2):
             torch.testing.assert_close(r[rank][step]["grad"], want, rtol=1e-6, atol=1e-7)
+        if kind == "mixy":  # b always used; its autograd gradient arrives after its bucket's reduce
+            assert r[0][step]["unused"] == r[1][step]["unused"] == []
+            assert r[0][step]["late"] and r[1][step]["late"]
+            continue
         assert r[0][step]["unused"] == r[1][step]["unused"] == ([] if any(use) else [2, 3])
         # step 2: b was found unused after step 1 and rank 0 uses it again -> reduced once more
         assert r[0][step]["late"] == (step == 2)

@@ -52,7 +52,10 @@ class Census(TorchDispatchMode):
         if any(g in name for g in GLUE):
             fr = [f for f in traceback.extract_stack()[:-1] if self.pkg_dir in f.filename or "bench.py" in f.filename]
             where = " <- ".join(f"{os.path.relpath(f.filename, self.pkg_dir)}:{f.lineno}" for f in fr[::-1][:3])
-            key = (name, " ".join(s for s in (sig(a) for a in args) if s), where or "(autograd node)")
+            if not where:  # backward: the autograd node being run (accumulation adds run between nodes)
+                node = torch._C._current_autograd_node()
+                where = f"(node {node.name()})" if node is not None else "(autograd engine: input accumulation)"
+            key = (name, " ".join(s for s in (sig(a) for a in args) if s), where)
             r = self.rows[key]
             r[0] += 1
             r[1] += nbytes(out)
