@@ -452,6 +452,24 @@ __global__ __launch_bounds__(256) void msda_fwd16_kernel(
                                    out + item * D + lg * VEC);
 }
 
+// The tiles buffer's tail (msda_win.h): the persistent backward's queue words zeroed and the tile
+// order stored, by one lane of the forward's first workgroup (plain vector stores)
+__device__ __forceinline__ void write_tiles_tail(int2* tiles, long long ntiles_all, const QOrder& qo) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  unsigned* t = reinterpret_cast<unsigned*>(tiles + ntiles_all);
+#pragma unroll
+  for (int i = 0; i < (int)(kWinTailBytes / sizeof(unsigned)); ++i) t[i] = 0u;  // (every tail byte defined)
+  QOrder* o = reinterpret_cast<QOrder*>(reinterpret_cast<char*>(t) + kWinQOrderOffset);
+  o->cs = qo.cs;
+  o->inv_cs = qo.inv_cs;
+  o->L = qo.L;
+#pragma unroll
+  for (int l = 0; l < kQOrderMaxL; ++l) {
+    o->n[l] = qo.n[l];
+    o->start[l] = qo.start[l];
+  }
+}
+
 // msda_fwd16_kernel for D = 64 16-bit values (G = 8 lanes an item) that also writes the
 // row-block backward's tile intervals (msda_win.hip): for every (b, m, level, query tile of 32)
 // the rows [lo, hi] its samples touch or own (win_sample_rows, msda_win.h).  One 256-thread
@@ -467,6 +485,7 @@ __global__ __launch_bounds__(256) void msda_fwd16_tiles_kernel(
     const int Lq, const int ntile, const QOrder qo) {
   constexpr int VEC = 8, D = 64, NL = kLPMax / P;
   __shared__ int2 s_iv[4][NL];
+  write_tiles_tail(tiles, (long long)gridDim.x * L, qo);
   const unsigned wg = xcd_block(blockIdx.x, gridDim.x);
   const unsigned bm = wg / (unsigned)ntile;
   const int tile = (int)(wg % (unsigned)ntile);
@@ -529,6 +548,185 @@ __global__ __launch_bounds__(256) void msda_fwd16_tiles_kernel(
   }
 }
 
+
+// msda_fwd16_tiles_kernel with each wave's value rows staged in its own LDS slice (no workgroup
+// barrier on the data path).  A wave holds 8 consecutive queries of one (b, m) (8 lanes an item, as
+// msda_fwd16_tiles_kernel); in an encoder call their samples of one level fall in a short window of
+// rows (8 consecutive tokens of a level cover 1-64 rows of another, plus the sampling spread: 18-24 %
+// of the 64 rows their taps gather, tools/win_visits.py-style count over the microbench sampling), so
+// per level the wave reduces its window [lo, hi], loads those rows once (8 lanes a 128-B row,
+// coalesced) into its LDS slice and reads the taps there; a level whose window exceeds CAP
+// (CAP) rows keeps the global gathers.  The next level's rows are loaded into registers while the current
+// level's taps are read (one LDS slice: a wave's LDS accesses are in order).  Same taps, same weights,
+// same fp32 accumulation order as fwd16_item: the output is msda_fwd16_tiles_kernel's bit for bit;
+// the tile intervals are written the same way (win_sample_rows).  VERDICT r4 item 6: the gathering
+// forward moved 503 MB of row fragments out of L2 per encoder call (14.7 TB/s, 34 us).
+// CAP: staged rows a wave (48: 6 KB, three waves a SIMD by registers; 32: 4 KB, four)
+template <typename scalar_t, bool ZEROS, int P, bool LM, int CAP>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CAP <= 32 ? 4 : 3))) void msda_fwd16_stage_kernel(
+    const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    scalar_t* __restrict__ out, int2* __restrict__ tiles, const Levels lv, const int L, const int S, const int M,
+    const int Lq, const int ntile, const QOrder qo) {
+  constexpr int VEC = 8, D = 64, NL = kLPMax / P, NR = CAP / 8;
+  __shared__ int2 s_iv[4][NL];
+  __shared__ uint4 s_rows[4][CAP * 8];  // per wave: row k, chunk c at [k * 8 + c]
+  write_tiles_tail(tiles, (long long)gridDim.x * L, qo);
+  const unsigned wg = xcd_block(blockIdx.x, gridDim.x);
+  const unsigned bm = wg / (unsigned)ntile;
+  const int tile = (int)(wg % (unsigned)ntile);
+  const int m = (int)(bm % (unsigned)M);
+  const long long b = bm / (unsigned)M;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = threadIdx.x >> 3, lg = threadIdx.x & 7, kr = lane >> 3;
+  const int q = tile * kWinQT + i < Lq ? qo_query(qo, tile * kWinQT + i) : Lq;  // (msda_win.h: the tile order)
+  const bool valid = q < Lq;
+  const int LP = L * P;
+  const int rs = M * D;
+  uint4* const slice = s_rows[w];
+  float lr[kLPMax], ar[kLPMax];
+  if (valid) {
+    if constexpr (LM) {
+      const long long c0 = ((b * M + m) * L * Lq + q) * P;
+      load_coords16_lm(loc + c0, (long long)Lq * P, L, P, lr);
+      load_coords16_lm(aw + c0, (long long)Lq * P, L, P, ar);
+    } else {
+      const long long item = (b * Lq + q) * M + m;
+      load_coords16(loc + item * LP, LP, lr);
+      load_coords16(aw + item * LP, LP, ar);
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < kLPMax; ++j) lr[j] = ar[j] = 0.f;
+  }
+  const scalar_t* __restrict__ vb = value + (b * S * M + m) * (long long)D + lg * VEC;
+  // the rows level l's valid taps of this wave touch: (lo, n); n = 0 without any
+  auto window = [&](int l, int& lo, int& n) {
+    int a = 1 << 30, z = -1;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      if (valid && l * P + p < LP) {
+        const Taps<float> t = make_taps<float, ZEROS>(lr[l * P + p], lv.T[l]);
+        if (t.ok0) { a = min(a, t.i0); z = max(z, t.i0); }
+        if (t.ok1) { a = min(a, t.i1); z = max(z, t.i1); }
+      }
+    }
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      a = min(a, __shfl_xor(a, o));
+      z = max(z, __shfl_xor(z, o));
+    }
+    lo = a;
+    n = z >= a ? z - a + 1 : 0;
+  };
+  uint4 rg[NR];
+  auto load_rows = [&](int l, int lo, int n) {
+    const scalar_t* __restrict__ vl = vb + (long long)(lv.start[l] + lo) * rs;
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      if (kr + 8 * k < n) rg[k] = *reinterpret_cast<const uint4*>(vl + (kr + 8 * k) * rs);
+  };
+  auto store_rows = [&](int n) {
+#pragma unroll
+    for (int k = 0; k < NR; ++k)
+      if (kr + 8 * k < n) slice[(kr + 8 * k) * 8 + lg] = rg[k];
+  };
+  f32x2 acc2[VEC / 2];
+#pragma unroll
+  for (int e = 0; e < VEC / 2; ++e) acc2[e] = f32x2{0.f, 0.f};
+  int lo_c = 0, n_c = 0;
+  window(0, lo_c, n_c);
+  bool st_c = n_c > 0 && n_c <= CAP;
+  if (st_c) {
+    load_rows(0, lo_c, n_c);
+    store_rows(n_c);
+  }
+  for (int l = 0; l < L; ++l) {
+    int lo_n = 0, n_n = 0;
+    bool st_n = false;
+    if (l + 1 < L) {  // the next level's rows in flight while this level's taps are read
+      window(l + 1, lo_n, n_n);
+      st_n = n_n > 0 && n_n <= CAP;
+      if (st_n) load_rows(l + 1, lo_n, n_n);
+    }
+    const scalar_t* __restrict__ vl = vb + (long long)lv.start[l] * rs;
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int j = l * P + p;
+      if (j < LP) {
+        const Taps<float> t = make_taps<float, ZEROS>(lr[j], lv.T[l]);
+        uint4 r0, r1;
+        if (st_c) {
+          r0 = t.ok0 ? slice[(t.i0 - lo_c) * 8 + lg] : make_uint4(0u, 0u, 0u, 0u);
+          r1 = t.ok1 ? slice[(t.i1 - lo_c) * 8 + lg] : make_uint4(0u, 0u, 0u, 0u);
+        } else {
+          r0 = load16_if(t.ok0, vl + t.i0 * rs);
+          r1 = load16_if(t.ok1, vl + t.i1 * rs);
+        }
+        const float c0 = ar[j] * t.w0, c1 = ar[j] * t.w1;
+        f32x2 x0[VEC / 2], x1[VEC / 2];
+        cvt16x2<scalar_t, VEC>(r0, x0);
+        cvt16x2<scalar_t, VEC>(r1, x1);
+        const f32x2 k0{c0, c0}, k1{c1, c1};
+#pragma unroll
+        for (int e = 0; e < VEC / 2; ++e) acc2[e] = pk_fma(x1[e], k1, pk_fma(x0[e], k0, acc2[e]));
+      }
+    }
+    if (st_n) store_rows(n_n);  // (after this level's LDS reads: in order within the wave)
+    lo_c = lo_n;
+    n_c = n_n;
+    st_c = st_n;
+  }
+  if (valid) {
+    float acc[VEC];
+#pragma unroll
+    for (int e = 0; e < VEC / 2; ++e) {
+      acc[2 * e] = acc2[e].x;
+      acc[2 * e + 1] = acc2[e].y;
+    }
+    store_vec<scalar_t, VEC>(out + ((b * Lq + q) * M + m) * D + lg * VEC, acc);
+  }
+  // tile intervals (as msda_fwd16_tiles_kernel)
+  int lo[NL], hi[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    lo[l] = kWinNone;
+    hi[l] = -kWinNone;
+  }
+  if (valid) {
+#pragma unroll
+    for (int j = 0; j < kLPMax; ++j) {
+      if (j < LP) {
+        const int2 r = win_sample_rows(lr[j], lv.T[j / P], ZEROS);
+        lo[j / P] = min(lo[j / P], r.x);
+        hi[j / P] = max(hi[j / P], r.y);
+      }
+    }
+  }
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+#pragma unroll
+    for (int o = 8; o < 64; o <<= 1) {
+      lo[l] = min(lo[l], __shfl_xor(lo[l], o));
+      hi[l] = max(hi[l], __shfl_xor(hi[l], o));
+    }
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int l = 0; l < NL; ++l) s_iv[w][l] = make_int2(lo[l], hi[l]);
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < L) {
+    int2 iv = s_iv[0][threadIdx.x];
+#pragma unroll
+    for (int v = 1; v < 4; ++v) {
+      const int2 o = s_iv[v][threadIdx.x];
+      iv.x = min(iv.x, o.x);
+      iv.y = max(iv.y, o.y);
+    }
+    tiles[((long long)bm * L + threadIdx.x) * ntile + tile] = iv;
+  }
+}
+
 // LDS-staged variant of msda_fwd16_tiles_kernel (same items, same output and tile intervals bit
 // for bit).  The workgroup's 32 queries of one head sample each level inside the row interval the
 // tiles kernel reduces anyway; here the interval is reduced FIRST, the value rows of every level
@@ -550,6 +748,7 @@ __global__ __launch_bounds__(256) void msda_fwd16_lds_kernel(
   __shared__ int2 s_iv[4][NL];
   __shared__ int s_off[NL], s_lo[NL], s_n[NL + 1];
   __shared__ __attribute__((aligned(16))) unsigned char s_rows[kFwdStageRows * kFwdRowStride];
+  write_tiles_tail(tiles, (long long)gridDim.x * L, qo);
   const unsigned wg = xcd_block(blockIdx.x, gridDim.x);
   const unsigned bm = wg / (unsigned)ntile;
   const int tile = (int)(wg % (unsigned)ntile);
@@ -2379,6 +2578,8 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
       // slower at the bench's encoder call (53.9 vs 33.6 us: the gathers' neighbouring rows hit in
       // L1 and the barrier-free gather kernel hides their latency), so the gathers stay the default
       const bool fwd_lds = env_int("MSDA_HIP_FWD_LDS", 0) != 0;
+      // per-wave staged rows (msda_fwd16_stage_kernel; MSDA_HIP_FWD_STAGE=0: the gathering kernel)
+      const int fwd_stage = fwd_lds ? 0 : env_int("MSDA_HIP_FWD_STAGE", 1);  // 1: 48 rows a wave, 2: 32
       auto* tl = static_cast<int2*>(tiles);
       const QOrder qo = make_qorder(pr.Lq, pr.S, (int)pr.L, pr.lv.T, pr.lv.start);
 #define MSDA_FT(Z, PP)                                                                              \
@@ -2389,6 +2590,15 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
     else if (fwd_lds)                                                                             \
       hipLaunchKernelGGL((msda_fwd16_lds_kernel<scalar_t, Z, PP, false>), dim3(tblocks), dim3(256), 0, st, v, lc, \
                          a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo);   \
+    else if (fwd_stage == 2 && lm && PP <= 4)                                                     \
+      hipLaunchKernelGGL((msda_fwd16_stage_kernel<scalar_t, Z, PP, true, 32>), dim3(tblocks), dim3(256), 0, st, v, \
+                         lc, a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo); \
+    else if (fwd_stage && lm && PP <= 4)                                                          \
+      hipLaunchKernelGGL((msda_fwd16_stage_kernel<scalar_t, Z, PP, true, 48>), dim3(tblocks), dim3(256), 0, st, v, \
+                         lc, a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo); \
+    else if (fwd_stage && PP <= 4)                                                                \
+      hipLaunchKernelGGL((msda_fwd16_stage_kernel<scalar_t, Z, PP, false, 48>), dim3(tblocks), dim3(256), 0, st, v, \
+                         lc, a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo); \
     else if (lm)                                                                                  \
       hipLaunchKernelGGL((msda_fwd16_tiles_kernel<scalar_t, Z, PP, true>), dim3(tblocks), dim3(256), 0, st, v, lc, \
                          a, o, tl, pr.lv, (int)pr.L, (int)pr.S, (int)pr.M, (int)pr.Lq, ntile, qo);   \
@@ -3058,8 +3268,14 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
           sh.start[l] = pr.lv.start[l];
         }
         sh.qo = make_qorder(pr.Lq, pr.S, (int)pr.L, pr.lv.T, pr.lv.start);
-        if (msda_win_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, tiles, &sh, pad == MSDA_PAD_ZEROS,
-                              layout, st) < 0) {
+        const int wrc = msda_win_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, tiles, &sh,
+                                          pad == MSDA_PAD_ZEROS, layout, st);
+        if (wrc == -2) {
+          set_error("msda backward: MSDA_HIP_WIN_EXP is a profiling switch that skips parts of the kernel (wrong "
+                    "gradients); it needs MSDA_HIP_PROFILING=1");
+          return MSDA_ERR_ARG;
+        }
+        if (wrc < 0) {
           set_error("msda backward: level-major coordinates need the forward's tile intervals");
           return MSDA_ERR_ARG;
         }

@@ -93,7 +93,8 @@ struct WinShape {
   // b cb + q cq + m cm + l cl + p (set by msda_win_backward from the layout tag)
   long long cb, cm;
   int cq, cl;
-  QOrder qo;  // tile order of the queries (set by the caller: make_qorder)
+  QOrder qo;  // tile order of the queries (set by the caller: make_qorder; ignored when qo_dev)
+  int qo_dev;  // 1: the tiles came from the forward, which stored its QOrder in the tiles tail
   int exp;  // profiling only (MSDA_HIP_WIN_EXP bitmask, 0 in production): skip parts of win_bwd_kernel
   unsigned short cs[kWinMaxChunks + 1];
   unsigned short seq[kWinMaxSeq];
@@ -101,6 +102,17 @@ struct WinShape {
 
 constexpr int kWinQT = 32;          // queries per tile of the row-block backward
 constexpr int kWinNone = 1 << 29;   // an empty interval is (kWinNone, -kWinNone)
+// After the tile intervals, the tiles buffer holds the persistent backward's work queue: 8 per-XCD
+// heads and 8 done counters (unsigned).  The tiles forward zeroes them; the backward leaves them
+// zero (its last wave of each queue resets both), so one forward's buffer serves any number of
+// backwards, eager or replayed.
+constexpr int kWinQueueWords = 16;
+// Then the query order the forward grouped its tiles by (a QOrder, written by the tiles forward):
+// the backward reads it from there, so the two always agree whatever the environment does between
+// them (MSDA_HIP_QORDER is read by the forward only).
+constexpr size_t kWinQOrderOffset = kWinQueueWords * sizeof(unsigned);
+constexpr size_t kWinTailBytes = 128;
+static_assert(kWinQOrderOffset + sizeof(QOrder) <= kWinTailBytes, "tiles tail too small");
 
 // The rows [lo, hi] a sample at normalised location `loc` on a T-row level touches or owns in
 // the row-block backward: its taps base and base + 1 (base = floor of the sample position, as

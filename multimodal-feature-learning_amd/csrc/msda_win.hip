@@ -245,6 +245,11 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
   const int T = sh.T[l];
   const int r0 = k * kRW;
   const int rs = sh.M * 64;                           // grad_out / value row stride (elements)
+  // the query order of the tiles: the forward's (stored in the tiles tail) when it wrote them
+  const QOrder qo = sh.qo_dev ? *reinterpret_cast<const QOrder*>(
+                                    reinterpret_cast<const char*>(tiles + sh.B * sh.M * sh.L * sh.ntile) +
+                                    kWinQOrderOffset)
+                              : sh.qo;
   const int qstride = sh.cq;                          // coordinate stride of one query
   const uint16_t* __restrict__ vl = value + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
   const uint16_t* __restrict__ gb = gout + (b * sh.Lq * sh.M + m) * 64;
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
   // coordinate offset of sample s of the tile at entry q0 of the query order (sh.qo; the caller
   // keeps q0 + s / P < Lq)
   auto coff = [&](int q0, int s) -> long long {
-    return (long long)qo_query(sh.qo, q0 + s / P) * qstride + s % P;
+    return (long long)qo_query(qo, q0 + s / P) * qstride + s % P;
   };
   // The dots' B operands, constant over the block's visits, in registers: lane (li, g) holds
   // channels ks*32 + 8g .. +7 of value row r0 + li (vb[0][ks]) and of row r0 + 16 (vb[1][ks])
@@ -332,7 +337,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        rg[i] = *reinterpret_cast<const uint4*>(gb + (long long)qo_query(sh.qo, q0 + grow + 8 * i) * rs + gch * 8);
+        rg[i] = *reinterpret_cast<const uint4*>(gb + (long long)qo_query(qo, q0 + grow + 8 * i) * rs + gch * 8);
     } else {
 #pragma unroll
       for (int j = 0; j < SPL; ++j) {
@@ -345,7 +350,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
 #pragma unroll
       for (int i = 0; i < 4; ++i)
         rg[i] = q0 + grow + 8 * i < sh.Lq
-                    ? *reinterpret_cast<const uint4*>(gb + (long long)qo_query(sh.qo, q0 + grow + 8 * i) * rs + gch * 8)
+                    ? *reinterpret_cast<const uint4*>(gb + (long long)qo_query(qo, q0 + grow + 8 * i) * rs + gch * 8)
                     : make_uint4(0u, 0u, 0u, 0u);
     }
   };
@@ -509,11 +514,335 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// win_lm_kernel: the row-block backward for level-major coordinates with the forward's tile
+// intervals (the encoder calls: MSDeformAttn's prologue writes level-major locations / weights),
+// one wave per 16-row block as win_bwd_kernel, restructured for residency and latency
+// (profiles/r05_*: the one-block-per-workgroup kernel averaged 2.5 resident waves per SIMD of its
+// 4, 38 % of its wave time parked on memory, LDS bank conflicts 0.74 extra cycles an LDS op):
+//  * persistent waves: a grid of about as many single-wave workgroups as the chip holds, each
+//    popping row blocks from a per-XCD queue (one returning atomic per block, issued a block ahead
+//    so its latency hides under the block's visits) in the coarsest-level-first order — no wave
+//    start-up per block, and the long coarse blocks spread over the waves before the short ones;
+//  * 7.2 KB of LDS a wave (20+ waves per CU): the grad_out tile in 128-B rows with an XOR swizzle
+//    of the 16-B chunks (conflict-free for the row writes, the dots' A reads and the transposed B
+//    reads) instead of 144-B padded rows, and the dots buffer reused for the coefficient tile C
+//    (phases reordered: dots -> coordinate gradients -> grad_value);
+//  * 32-bit offsets from per-block base pointers (level-major: a tile's coordinates of one level
+//    are 32 P contiguous floats);
+//  * the next visit's coordinates and grad_out rows are requested right after the current tile's
+//    rows reach LDS, before the dots.
+// Same arithmetic as win_bwd_kernel per visit (the same taps, the same bf16 hi + lo coefficient
+// split, the same MFMA products in the same order), so its outputs are bit for bit those of
+// win_bwd_kernel with consecutive tiles (tests/test_gpu_op.py).
+// ---------------------------------------------------------------------------------------------
+constexpr int kLmRow = 128;     // bytes per grad_out / coefficient row in LDS
+#ifndef LM_WAVES
+#define LM_WAVES 4
+#endif
+constexpr int kLmWavesPerXcd = 32 * 4 * LM_WAVES;  // 32 CUs x 4 SIMDs x the waves a SIMD holds (the grid cap per queue)
+
+// the swizzled byte offset of 16-B chunk c of row r: chunk c ^ f(r), f(r) in {0, 2, 4, 6} from
+// bits 1 and 3 of r — rows {0,1,2,3,8,9,10,11} (a 32-lane half of a transposed read) land on 16
+// distinct bank quads, and so do the row reads of the dots
+__device__ __forceinline__ int lm_sw(int r, int c) {
+  return r * kLmRow + ((c ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2))) << 4);
+}
+
+template <bool ZEROS, bool COORDS, int P>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LM_WAVES))) void win_lm_kernel(
+    const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    const uint16_t* __restrict__ gout, uint16_t* __restrict__ gval, float* __restrict__ gloc,
+    float* __restrict__ gaw, const int2* __restrict__ tiles, unsigned* __restrict__ queue, const WinShape sh) {
+  constexpr int NS = kQT * P;                  // samples per tile and level
+  constexpr int SPL = NS >= 64 ? NS / 64 : 1;  // samples per lane
+  __shared__ __attribute__((aligned(16))) unsigned char s_g[kQT * kLmRow];  // the tile's grad_out rows
+  // dots [row - r0][q] (kVRows x kDQS floats), then, once the coordinate gradients have read them,
+  // the coefficient tile C [16 rows][hi 32 | lo 32] bf16 of each MFMA step
+  __shared__ __attribute__((aligned(16))) float s_cd[kVRows * kDQS];
+  __shared__ int s_q[NS + kQT];  // query (in the tile) of each compacted sample, padded
+  unsigned char* const s_c = reinterpret_cast<unsigned char*>(s_cd);
+  const int lane = (int)threadIdx.x, g = lane >> 4, li = lane & 15;
+  const int grow = lane >> 3, gch = lane & 7;
+  // LDS offsets fixed per lane: grad_out row writes (rows grow, grow + 8), and the row reads of
+  // chunks g / 4 + g of row li (the dots' A operand, rows li and 16 + li; the C tile's hi / lo)
+  const int wg0 = lm_sw(grow, gch), wg1 = lm_sw(grow + 8, gch);
+  const int wa0 = lm_sw(li, g), wa1 = lm_sw(li, 4 + g);
+  const unsigned x8 = blockIdx.x & 7u;
+  const unsigned nwx = gridDim.x >> 3;  // waves of this queue (the grid is 8 nwx)
+  unsigned* const head = queue + x8;
+  unsigned* const done = queue + 8 + x8;
+  const long long ntiles_all = sh.B * sh.M * sh.L * (long long)sh.ntile;
+  const QOrder qo = *reinterpret_cast<const QOrder*>(reinterpret_cast<const char*>(tiles + ntiles_all) +
+                                                     kWinQOrderOffset);
+  // queue slots of this XCD: level l (coarsest first) has cl = ceil(B M nbl / 8) slots, slot i of
+  // it is block x8 cl + i of the level (none past its end)
+  unsigned nsx = 0;
+  for (int l = 0; l < sh.L; ++l)
+    nsx += (unsigned)((sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + 7) / 8);
+  const int rs = sh.M * 64;  // grad_out / value row stride (elements)
+  const int cq = qo.cs == 0 ? 1 : 0;  // (uniform) consecutive tiles
+
+  unsigned slot;
+  {
+    unsigned v = 0;
+    if (lane == 0) v = atomicAdd(head, 1u);
+    slot = (unsigned)__builtin_amdgcn_readfirstlane((int)v);
+  }
+  while (slot < nsx) {
+    unsigned nxt = 0;  // the next block, returned while this one runs
+    if (lane == 0) nxt = atomicAdd(head, 1u);
+    int l = sh.L - 1;
+    int j = -1;  // (B M nblk < 2^31: checked by the host)
+    {
+      unsigned s = slot;
+      for (; l >= 0; --l) {
+        const unsigned nl = (unsigned)sh.B * (unsigned)sh.M * (unsigned)(sh.blk0[l + 1] - sh.blk0[l]);
+        const unsigned cl = (nl + 7u) / 8u;
+        if (s < cl) {
+          const unsigned jj = x8 * cl + s;
+          j = jj < nl ? (int)jj : -1;  // (past the level's end on this queue: none)
+          break;
+        }
+        s -= cl;
+      }
+    }
+    if (j >= 0) {
+      const unsigned nbl = (unsigned)(sh.blk0[l + 1] - sh.blk0[l]);
+      const unsigned bm = (unsigned)j / nbl;
+      const int k = (int)((unsigned)j - bm * nbl);
+      const int m = (int)(bm % (unsigned)sh.M);
+      const long long b = bm / (unsigned)sh.M;
+      const int T = sh.T[l];
+      const int r0 = k * kRW;
+      const uint16_t* __restrict__ vl = value + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
+      const uint16_t* __restrict__ gb = gout + (b * sh.Lq * sh.M + m) * 64;
+      const long long cbase = ((long long)bm * sh.L + l) * sh.Lq * P;  // level-major (b, m, l, q, p)
+      const float* __restrict__ lt = loc + cbase;
+      const float* __restrict__ at = aw + cbase;
+      bf16x8 vb[2][2];  // the dots' B operands: value rows r0 + li and r0 + 16 (zeros past T)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int x = r0 + (cb == 0 ? li : kRW);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          uint4 v = make_uint4(0u, 0u, 0u, 0u);
+          if (x < T) v = *reinterpret_cast<const uint4*>(vl + x * rs + ks * 32 + 8 * g);
+          vb[cb][ks] = __builtin_bit_cast(bf16x8, v);
+        }
+      }
+      const int2* __restrict__ tl = tiles + ((long long)bm * sh.L + l) * sh.ntile;
+      auto chunk_mask = [&](int t0) -> unsigned long long {
+        const int t = min(t0 + lane, sh.ntile - 1);
+        const int2 iv = tl[t];
+        return __ballot(t0 + lane < sh.ntile && iv.x <= r0 + kRW - 1 && iv.y >= r0);
+      };
+      int cur_t0 = 0;
+      unsigned long long mask = chunk_mask(0);
+      auto next_tile = [&]() -> int {
+        while (mask == 0ull) {
+          cur_t0 += 64;
+          if (cur_t0 >= sh.ntile) return -1;
+          mask = chunk_mask(cur_t0);
+        }
+        const int t = cur_t0 + __builtin_ctzll(mask);
+        mask &= mask - 1ull;
+        return t;
+      };
+      // the query of entry e of the tile order
+      auto qry = [&](int e) -> int { return cq ? e : qo_query(qo, e); };
+
+      f32x4 acc[4];
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+      float rl[SPL], ra[SPL];
+      uint4 rg[4];
+      auto fetch = [&](int tile) {
+        const int q0 = tile * kQT;
+        if (cq && q0 + kQT <= sh.Lq) {  // a whole tile of consecutive queries (uniform)
+#pragma unroll
+          for (int jj = 0; jj < SPL; ++jj) {
+            const bool in = NS >= 64 || lane < NS;
+            const int o = q0 * P + (in ? lane + 64 * jj : 0);
+            rl[jj] = in ? lt[o] : 0.f;
+            ra[jj] = in ? at[o] : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            rg[i] = *reinterpret_cast<const uint4*>(gb + (q0 + grow + 8 * i) * rs + gch * 8);
+        } else {
+#pragma unroll
+          for (int jj = 0; jj < SPL; ++jj) {
+            const int s = lane + 64 * jj;
+            const bool in = (NS >= 64 || lane < NS) && q0 + s / P < sh.Lq;
+            const int o = in ? qry(q0 + s / P) * P + s % P : 0;
+            rl[jj] = in ? lt[o] : 0.f;
+            ra[jj] = in ? at[o] : 0.f;
+          }
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            rg[i] = q0 + grow + 8 * i < sh.Lq
+                        ? *reinterpret_cast<const uint4*>(gb + qry(q0 + grow + 8 * i) * rs + gch * 8)
+                        : make_uint4(0u, 0u, 0u, 0u);
+        }
+      };
+      int tile = next_tile();
+      if (tile >= 0) fetch(tile);
+
+      while (tile >= 0) {
+        const int q0 = tile * kQT;
+        // rows grow + 8 i: the swizzle of rows grow + 16 / grow + 24 is that of grow / grow + 8
+        *reinterpret_cast<uint4*>(s_g + wg0) = rg[0];
+        *reinterpret_cast<uint4*>(s_g + wg1) = rg[1];
+        *reinterpret_cast<uint4*>(s_g + wg0 + 16 * kLmRow) = rg[2];
+        *reinterpret_cast<uint4*>(s_g + wg1 + 16 * kLmRow) = rg[3];
+        // 1. taps of the visit's samples (registers); the samples with a tap in the block's rows
+        // compacted (ballot): position kp, coefficients split into bf16 hi / lo
+        Taps tp[SPL];
+        float a[SPL];
+        int kp[SPL], dr[SPL];
+        uint32_t ch[SPL], cl[SPL];
+        int n = 0;
+#pragma unroll
+        for (int jj = 0; jj < SPL; ++jj) {
+          const int s = lane + 64 * jj;
+          const bool in = (NS >= 64 || lane < NS) && q0 + s / P < sh.Lq;
+          tp[jj] = make_taps<ZEROS>(rl[jj], T);
+          tp[jj].live = tp[jj].live && in;
+          a[jj] = ra[jj];
+          dr[jj] = tp[jj].base - r0;
+          const bool sel = tp[jj].live && dr[jj] >= -1 && dr[jj] <= kRW - 1;
+          const unsigned long long bal = __ballot(sel);
+          const int below = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32),
+                                                           __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+          kp[jj] = sel ? n + below : -1;
+          const float c0 = tp[jj].ok0 ? a[jj] * tp[jj].w0 : 0.f;
+          const float c1 = tp[jj].ok1 ? a[jj] * tp[jj].w1 : 0.f;
+          const uint32_t u0 = __float_as_uint(c0) & 0xffff0000u, u1 = __float_as_uint(c1) & 0xffff0000u;
+          ch[jj] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
+          cl[jj] = (uint32_t)(uint16_t)bf16_bits(c0 - __uint_as_float(u0)) |
+                   ((uint32_t)(uint16_t)bf16_bits(c1 - __uint_as_float(u1)) << 16);
+          if (sel) s_q[kp[jj]] = s / P;
+          n += __popcll(bal);
+        }
+        const int nk = (n + 31) >> 5;
+        if (lane < nk * 32 - n) s_q[n + lane] = 0;  // padding columns: C is zero there
+        wave_lds_fence();
+        if constexpr (COORDS) {
+          // 2. dots of the tile's 32 queries with rows r0 .. r0+16 (MFMA, B operands in registers)
+#pragma unroll
+          for (int qh = 0; qh < 2; ++qh) {
+            bf16x8 av[2];
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks)
+              av[ks] = *reinterpret_cast<const bf16x8*>(s_g + (ks ? wa1 : wa0) + qh * 16 * kLmRow);
+            f32x4 d[2];
+#pragma unroll
+            for (int cb = 0; cb < 2; ++cb) {
+              d[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+              for (int ks = 0; ks < 2; ++ks)
+                d[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[ks], vb[cb][ks], d[cb], 0, 0, 0);
+            }
+            *reinterpret_cast<f32x4*>(s_cd + li * kDQS + qh * 16 + 4 * g) = d[0];
+            if (li == 0) *reinterpret_cast<f32x4*>(s_cd + kRW * kDQS + qh * 16 + 4 * g) = d[1];
+          }
+          wave_lds_fence();
+          // 3. coordinate gradients of the samples this block owns (base row in it; the level's
+          // first block also owns the samples with no tap on the map)
+#pragma unroll
+          for (int jj = 0; jj < SPL; ++jj) {
+            const int s = lane + 64 * jj;
+            const bool in = (NS >= 64 || lane < NS) && q0 + s / P < sh.Lq;
+            const Taps& t = tp[jj];
+            const bool own = t.live ? (t.base >= r0 && t.base < r0 + kRW) || (t.base < 0 && k == 0) : k == 0;
+            if (in && own) {
+              const int qi = s / P;
+              const int o = cq ? q0 * P + s : qry(q0 + qi) * P + s % P;
+              const float d0 = t.ok0 ? s_cd[(t.base - r0) * kDQS + qi] : 0.f;
+              const float d1 = t.ok1 ? s_cd[(t.base + 1 - r0) * kDQS + qi] : 0.f;
+              if (gaw != nullptr) gaw[cbase + o] = d0 * t.w0 + d1 * t.w1;
+              if (gloc != nullptr) gloc[cbase + o] = ((d1 - d0) * a[jj]) * t.gmul;
+            }
+          }
+          wave_lds_fence();  // the dots' reads before C overwrites them
+        }
+        // the next visit's inputs, in flight during the grad_value steps
+        const int next = next_tile();
+        if (next >= 0) fetch(next);
+        // 4. grad_value of the 16 rows += C . G, 32 compacted samples per MFMA step
+        for (int ks = 0; ks < nk; ++ks) {
+          {
+            uint4* z = reinterpret_cast<uint4*>(s_c + (lane >> 2) * kLmRow + (lane & 3) * 32);
+            z[0] = make_uint4(0u, 0u, 0u, 0u);
+            z[1] = make_uint4(0u, 0u, 0u, 0u);
+          }
+          wave_lds_fence();
+#pragma unroll
+          for (int jj = 0; jj < SPL; ++jj) {
+            const int col = kp[jj] - 32 * ks;
+            if (col >= 0 && col < 32) {
+              const int cc = col >> 3, cw = (col & 7) * 2;
+              if (dr[jj] >= 0) {
+                *reinterpret_cast<uint16_t*>(s_c + lm_sw(dr[jj], cc) + cw) = (uint16_t)ch[jj];
+                *reinterpret_cast<uint16_t*>(s_c + lm_sw(dr[jj], 4 + cc) + cw) = (uint16_t)cl[jj];
+              }
+              if (dr[jj] + 1 < kRW) {
+                *reinterpret_cast<uint16_t*>(s_c + lm_sw(dr[jj] + 1, cc) + cw) = (uint16_t)(ch[jj] >> 16);
+                *reinterpret_cast<uint16_t*>(s_c + lm_sw(dr[jj] + 1, 4 + cc) + cw) = (uint16_t)(cl[jj] >> 16);
+              }
+            }
+          }
+          wave_lds_fence();
+          const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(s_c + wa0);
+          const bf16x8 alo = *reinterpret_cast<const bf16x8*>(s_c + wa1);
+          const int qq = li >> 2, pp = li & 3;
+          const int rowa = s_q[ks * 32 + 8 * g + qq], rowb = s_q[ks * 32 + 8 * g + 4 + qq];
+#pragma unroll
+          for (int cb = 0; cb < 4; ++cb) {
+            const int c = 2 * cb + (pp >> 1), w8 = (pp & 1) * 8;
+            const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(s_g + lm_sw(rowa, c) + w8));
+            const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(s_g + lm_sw(rowb, c) + w8));
+            const bf16x8 bv = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, acc[cb], 0, 0, 0);
+            acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, acc[cb], 0, 0, 0);
+          }
+          wave_lds_fence();  // this step's C reads before the next step's zeroing
+        }
+        wave_lds_fence();  // this visit's LDS reads before the next visit's writes
+        tile = next;
+      }
+      // grad_value rows r0 + 4g + jj, channels 16 cb + li (every row of the block, zeros included)
+      if (gval != nullptr) {
+        uint16_t* __restrict__ gvl = gval + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int x = r0 + 4 * g + jj;
+          if (x < T) {
+#pragma unroll
+            for (int cb = 0; cb < 4; ++cb) gvl[x * rs + cb * 16 + li] = (uint16_t)bf16_bits(acc[cb][jj]);
+          }
+        }
+      }
+    }
+    slot = (unsigned)__builtin_amdgcn_readfirstlane((int)nxt);
+  }
+  // every wave of this queue pops once past its end; the last to do so resets the queue for the
+  // next launch on this tiles buffer
+  if (lane == 0) {
+    const unsigned d = atomicAdd(done, 1u);
+    if (d == nwx - 1u) {
+      atomicExch(head, 0u);
+      atomicExch(done, 0u);
+    }
+  }
+}
 }  // namespace
 
 size_t msda_win_workspace_bytes(long long B, long long M, long long L, long long Lq) {
   const long long ntile = (Lq + kQT - 1) / kQT;
-  return (size_t)(B * M * L * ntile) * sizeof(int2);
+  return (size_t)(B * M * L * ntile) * sizeof(int2) + kWinTailBytes;
 }
 
 int msda_win_supported(int value_dtype_is_bf16, long long D, long long P, long long Lq, long long row_floats) {
@@ -564,16 +893,69 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   sh.blk0[sh.L] = nb;
   sh.nblk = nb;
   if (sh.B * sh.M == 0 || nb == 0) return 0;
+  const long long nblocks = sh.B * sh.M * (long long)nb;
+  // the persistent level-major kernel (win_lm_kernel): the forward's tiles (and their tail: queue,
+  // query order), many blocks (one wave each), 32-bit element offsets within a clip
+  // (MSDA_HIP_WIN_LM=0: the per-block kernel, for A/B)
+  const char* lme = getenv("MSDA_HIP_WIN_LM");
+  const bool lm_kernel = coord_layout == 1 && tiles_ready != nullptr && nblocks > 4096 && sh.P <= 4 &&
+                         (lme == nullptr || atoi(lme) != 0) && sh.Lq * sh.M * 64 < (1LL << 31) &&
+                         sh.S * sh.M * 64 < (1LL << 31) && sh.L * sh.Lq * sh.P < (1LL << 31) && nblocks < (1LL << 31) &&
+                         getenv("MSDA_HIP_WIN_EXP") == nullptr && getenv("MSDA_HIP_WIN_SPLIT") == nullptr;
   // position-chunk order where the blocks are many (T = 4096: 3,840 an XCD; 245 -> 219 us at the
   // configs[3] call), coarsest-level-first where they are few and the longest blocks set the tail
   // (T = 1024: 960 an XCD; 55 against 64 us, tools/win_tiles_ab.py).  MSDA_HIP_WIN_ORDER: 0 / 1 forces.
   const char* oe = getenv("MSDA_HIP_WIN_ORDER");
   const int order_env = oe ? atoi(oe) : -1;
+  if (lm_kernel) {
+    sh.qo_dev = 1;
+    sh.exp = 0;
+    unsigned nsx = 0;
+    for (int l = 0; l < sh.L; ++l) nsx += (unsigned)((sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + 7) / 8);
+    const unsigned nwx = nsx < (unsigned)kLmWavesPerXcd ? nsx : (unsigned)kLmWavesPerXcd;
+    const long long ntiles_all = sh.B * sh.M * sh.L * (long long)sh.ntile;
+    auto* tl = static_cast<const int2*>(tiles_ready);
+    auto* q = reinterpret_cast<unsigned*>(const_cast<int2*>(tl + ntiles_all));
+    const bool coords = gloc != nullptr || gaw != nullptr;
+    auto* v = static_cast<const uint16_t*>(value);
+    auto* lc = static_cast<const float*>(loc);
+    auto* a = static_cast<const float*>(aw);
+    auto* g = static_cast<const uint16_t*>(gout);
+    auto* gv = static_cast<uint16_t*>(gval);
+    auto* gl = static_cast<float*>(gloc);
+    auto* ga = static_cast<float*>(gaw);
+#define WIN_LM(Z, C, N) \
+  hipLaunchKernelGGL((win_lm_kernel<Z, C, N>), dim3(8u * nwx), dim3(64), 0, st, v, lc, a, g, gv, gl, ga, tl, q, sh)
+#define WIN_LM_P(Z, C)                                                  \
+  do {                                                                  \
+    switch (sh.P) {                                                     \
+      case 1: WIN_LM(Z, C, 1); break;                                   \
+      case 2: WIN_LM(Z, C, 2); break;                                   \
+      default: WIN_LM(Z, C, 4); break;                                  \
+    }                                                                   \
+  } while (0)
+    if (zeros) {
+      if (coords) WIN_LM_P(true, true); else WIN_LM_P(true, false);
+    } else {
+      if (coords) WIN_LM_P(false, true); else WIN_LM_P(false, false);
+    }
+#undef WIN_LM_P
+#undef WIN_LM
+    return 0;
+  }
   const bool chunked = win_chunk_order(sh) &&
                        (order_env == 1 || (order_env != 0 && (long long)sh.ppx * sh.nblk >= 2048));
   if (!chunked) sh.nchunk = 0;
-  const char* xe = getenv("MSDA_HIP_WIN_EXP");  // profiling: skip parts of the kernel (results are wrong)
+  // profiling only: MSDA_HIP_WIN_EXP skips parts of the kernel (the results are WRONG), so it is
+  // honoured only together with MSDA_HIP_PROFILING=1 (tools/win_exp.py); alone it is an error, never
+  // silently wrong gradients in training
+  const char* xe = getenv("MSDA_HIP_WIN_EXP");
   sh.exp = xe ? atoi(xe) : 0;
+  if (sh.exp != 0) {
+    const char* pe = getenv("MSDA_HIP_PROFILING");
+    if (pe == nullptr || atoi(pe) != 1) return -2;
+  }
+  sh.qo_dev = tiles_ready != nullptr ? 1 : 0;
   // tile intervals: written by the forward (msda_fwd16_tiles_kernel) or by the prepass below
   auto* tiles = static_cast<int2*>(tiles_ready != nullptr ? const_cast<void*>(tiles_ready) : workspace);
   const unsigned tile_wgs = tiles_ready != nullptr ? 0u : (unsigned)(sh.B * sh.ntile);
@@ -607,7 +989,6 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   auto* ga = static_cast<float*>(gaw);
   // waves per row block: enough waves for the chip when the blocks are few (MSDA_HIP_WIN_SPLIT
   // forces 1 / 4 / 8)
-  const long long nblocks = sh.B * sh.M * (long long)sh.nblk;
   int W = nblocks <= 1024 ? 8 : nblocks <= 4096 ? 4 : 1;
   if (const char* e = getenv("MSDA_HIP_WIN_SPLIT")) {
     const int f = atoi(e);

@@ -291,6 +291,8 @@ class DeformableTransformerEncoder(nn.Module):
             # bf16 operands carried between the layers as the dense encoder does (no per-layer pos add,
             # casts of the whole memory or gradient-accumulation kernels): value16 is bf16(output)
             # kept up to date by the same scatter; the last one is the decoder's bf16 memory
+            from ... import _trace
+            _trace.hit("sparse_carry")
             value16 = output.to(torch.get_autocast_dtype("cuda"))
             query = tgt + pos
             for i, layer in enumerate(self.layers):

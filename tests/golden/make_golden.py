@@ -49,9 +49,14 @@ Fixtures:
   caption_bf16.pt            UnimodalCaptionDecoder at d=512, 8 heads, depth 2, vocab 10000, seq_len 20:
                              teacher-forced forward + gradients of -sum p(target word) and the reference's
                              greedy re-decode loop (unimodal_deformable_dvc.py:304-354), fp64 and bf16 autocast.
+  sparse_bf16_d256.pt        BaseEncoder + SparseDeformableTransformer (rho 0.3, 2 enc + 2 dec, d=256, 4 heads
+                             of 64, ff 1024), T=64, B=2 (one padded clip), dropout 0: fp64 and bf16 autocast,
+                             the seed chosen so that both runs select the same top-k tokens with a margin;
+                             outputs, mask prediction, top-k, sampled gradients.
 
 usage: make_golden.py [case ...]   (default: every case; e.g. ``make_golden.py dam sparse``)
 """
+import math
 import os
 import sys
 import types
@@ -661,6 +666,125 @@ def transformer_bf16_d256_case(ref):
                 truth=truth, bf16=bf16)
 
 
+SPARSE256 = dict(d_model=256, heads=4, ff=1024, Q=10, B=2, T=64, rho_pct=30, seed0=300)
+
+
+def sparse256_inputs(seed):
+    """Inputs of sparse_bf16_d256 (regenerable: the GPU test calls this too): two clips of T=64
+    features, the second padded from frame 40."""
+    c = SPARSE256
+    gen = torch.Generator().manual_seed(seed)
+    video = torch.randn((c["B"], c["T"], c["d_model"]), generator=gen, dtype=torch.float64).float()
+    mask = torch.zeros(c["B"], c["T"], dtype=torch.bool)
+    mask[1, 40:] = True
+    durations = torch.tensor([41.0, 97.5], dtype=torch.float32)
+    return video, mask, durations, gen
+
+
+def sparse256_modules(ref_or_ours, sparse_cls, embedding_layers, base_encoder):
+    c = SPARSE256
+    d = c["d_model"]
+    return torch.nn.ModuleDict(dict(
+        pos_embed=embedding_layers.PositionEmbeddingVideoSine(d // 2, normalize=True),
+        base_encoder=base_encoder.BaseEncoder(4, d, d),
+        transformer=sparse_cls(d_model=d, num_head=c["heads"], num_encoder_layers=2, num_decoder_layers=2,
+                               dim_feedforward=c["ff"], dropout=0.0, return_intermediate_dec=True,
+                               num_feature_levels=4, dec_n_points=4, enc_n_points=4, rho=c["rho_pct"] / 100),
+        query_embedding=torch.nn.Embedding(c["Q"], 2 * d)))
+
+
+def sparse256_forward(mods, video, mask, durations):
+    """The Sparse-DETR transformer's training forward (reference
+    models/sparse/unimodal_sparse_deformable_transformer.py:152-290): BaseEncoder pyramid, mask
+    predictor + top-k token selection (rho), sparse encoder over the selected tokens scattered back
+    into the memory, query decoder.  Returns (memory, hs, mask_prediction, topk, sparse_token_nums)."""
+    c = SPARSE256
+    srcs, masks, pos = mods["base_encoder"](video, mask, durations, mods["pos_embed"])
+    tr = mods["transformer"]
+    (src_flatten, shapes, starts, valid, lvl_pos, mask_flatten, proposals, topk, mask_pred,
+     stn) = tr.prepare_encoder_inputs(srcs, masks, pos)
+    memory = tr.forward_encoder(src_flatten, shapes, starts, valid, lvl_pos, mask_flatten, proposals, topk, stn)[0]
+    B = video.shape[0]
+    qmask = torch.ones(B, c["Q"], dtype=torch.bool, device=video.device)
+    _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, mods["query_embedding"].weight)
+    hs = tr.forward_decoder(tgt, refp, memory, shapes, starts, valid, qpos, mask_flatten, qmask, False)[0]
+    return memory, hs, mask_pred, topk, stn
+
+
+def topk_sets(topk, stn):
+    """Each clip's selected tokens as a sorted tensor (the encoder refines topk[i, :stn[i]])."""
+    return [topk[i, :int(stn[i])].sort().values for i in range(topk.shape[0])]
+
+
+def topk_margin(mask_pred, stn):
+    """Smallest gap, over clips, between the last selected and the first unselected fp64 score, in
+    units of the bf16 spacing at that magnitude (a margin of many units: bf16 rounding cannot swap
+    the two)."""
+    m = float("inf")
+    for i in range(mask_pred.shape[0]):
+        s = mask_pred[i].double().sort(descending=True).values
+        k = int(stn[i])
+        if k >= s.numel():
+            continue
+        gap = (s[k - 1] - s[k]).item()
+        mag = max(abs(s[k - 1].item()), abs(s[k].item()), 1e-30)
+        ulp = 2.0 ** (math.floor(math.log2(mag)) - 7)
+        m = min(m, gap / ulp)
+    return m
+
+
+def sparse_bf16_d256_case(ref):
+    """The reference's default-active Sparse-DETR transformer (rho 0.3, 2 + 2 layers, d=256, 4 heads of
+    64 channels: the bench kernels' D) behind PositionEmbeddingVideoSine + BaseEncoder, T=64, B=2 with
+    one padded clip, dropout 0, in fp64 (the truth) and in fp32 under torch.autocast('cpu', bfloat16)
+    (the reference's own bf16 run).  Loss (hs w_hs).sum() + (memory w_mem).sum() + (mask_pred w_mp).sum().
+    The seed is the first from seed0 whose bf16 run selects the fp64 run's tokens in every clip with a
+    score margin of at least 16 bf16 spacings (so a bf16 implementation can be held to that selection)."""
+    c = SPARSE256
+    Q, d = c["Q"], c["d_model"]
+
+    def run(mods, video, mask, durations, w, dtype, autocast):
+        v = video.to(dtype).requires_grad_(True)
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            memory, hs, mask_pred, topk, stn = sparse256_forward(mods, v, mask, durations.to(dtype))
+        loss = ((hs.to(dtype) * w[0].to(dtype)).sum() + (memory.to(dtype) * w[1].to(dtype)).sum()
+                + (mask_pred.to(dtype) * w[2].to(dtype)).sum())
+        loss.backward()
+        return dict(memory=memory.detach().float(), hs=hs.detach().float(), mask_pred=mask_pred.detach().float(),
+                    topk=topk, stn=stn, grad_video=v.grad.float(), loss=loss.detach().double(),
+                    grads=sampled_grads(dict(mods.items())))
+
+    import copy
+    for seed in range(c["seed0"], c["seed0"] + 50):
+        named = sparse256_modules(ref, ref.sparse.SparseDeformableTransformer, ref.embedding_layers, ref.base_encoder)
+        sums = regen_parameters(named, seed)
+        video, mask, durations, gen = sparse256_inputs(seed)
+        w = [torch.randn(sh, generator=gen, dtype=torch.float64).float()
+             for sh in ((2, c["B"], Q, d), (c["B"], 120, d), (c["B"], 120))]
+        m64 = copy.deepcopy(named).double()
+        torch.set_default_dtype(torch.float64)
+        try:
+            truth = run(m64, video, mask, durations, w, torch.float64, False)
+        finally:
+            torch.set_default_dtype(torch.float32)
+        bf16 = run(named, video, mask, durations, w, torch.float32, True)
+        same = all(torch.equal(a, b) for a, b in zip(topk_sets(truth["topk"], truth["stn"]),
+                                                      topk_sets(bf16["topk"], bf16["stn"])))
+        margin = topk_margin(truth["mask_pred"], truth["stn"])
+        print(f"sparse256 seed {seed}: bf16 selects the fp64 tokens {same}, margin {margin:.1f} bf16 spacings")
+        if same and margin >= 16:
+            break
+    else:
+        raise RuntimeError("no seed with a clear top-k margin")
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    print("sparse256: reference bf16 vs fp64: memory %.3e hs %.3e mask_pred %.3e grad_video %.3e" % (
+        rel(bf16["memory"], truth["memory"]), rel(bf16["hs"], truth["hs"]), rel(bf16["mask_pred"], truth["mask_pred"]),
+        rel(bf16["grad_video"], truth["grad_video"])))
+    cfg = dict(c, seed=seed)
+    return dict(config={k: torch.tensor(v) for k, v in cfg.items()}, param_abs_sums=sums, weights=w,
+                margin=torch.tensor(margin), truth=truth, bf16=bf16)
+
+
 CAPTION = dict(vocab=10000, seq_len=20, d_model=512, depth=2, heads=8, N=6, K=40, seed=101, head_scale=8.0,
                bos=2, eos=3, pad=1)
 
@@ -1253,6 +1377,7 @@ def main():
         "transformer_bf16_d256": lambda: transformer_bf16_d256_case(ref),
         "caption_bf16": lambda: caption_bf16_case(ref),
         "deformable_dvc_bf16_d256": lambda: deformable_dvc_bf16_d256_case(ref),
+        "sparse_bf16_d256": lambda: sparse_bf16_d256_case(ref),
     }
     wanted = sys.argv[1:] or list(cases)
     for name, fn in cases.items():

@@ -43,9 +43,10 @@ def test_abi_version_and_workspace():
     for dt in (0, 3):
         assert lib.msda_hip_backward_workspace_bytes(dt, B, S, M, D, Lq, L, P) == 0
     # bf16 may take the row-block MFMA backward (the encoder's calls): its tile intervals
-    assert lib.msda_hip_backward_workspace_bytes(2, B, S, M, D, Lq, L, P) == B * M * L * (Lq // 32) * 8
+    # the row-block path: one int2 interval per (b, m, level, query tile), then the 128-B tail (queue, tile order)
+    assert lib.msda_hip_backward_workspace_bytes(2, B, S, M, D, Lq, L, P) == B * M * L * (Lq // 32) * 8 + 128
     assert lib.msda_hip_backward_workspace_bytes(3, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * 4 * Lq * P * 12
-    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * (4 * Lq // 32) * 8
+    assert lib.msda_hip_backward_workspace_bytes(2, 8, 4 * S, M, D, 4 * Lq, L, P) == 8 * M * L * (4 * Lq // 32) * 8 + 128
     # split path (sort + pull): fp64, or heads not made of 16-byte chunks with few workgroups —
     # row table + per-row tap lists
     f64 = lib.msda_hip_backward_workspace_bytes(1, B, S, M, D, Lq, L, P)

@@ -243,7 +243,7 @@ def test_bf16_T4096_bench_instantiation_matches_oracle(dev, path, monkeypatch):
     if path == "pair":
         assert ws >= B * M * 4 * Lq * P * 12  # the workspace-staged pair path (12 B per sample)
     else:
-        assert ws == B * M * 4 * ((Lq + 31) // 32) * 8  # the row-block path's tile intervals only
+        assert ws == B * M * 4 * ((Lq + 31) // 32) * 8 + 128  # the row-block path's tile intervals + tail only
     value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=41, lo=0.0, hi=1.0)
     out, gv, gl, ga = run_hip(value, shapes, loc, aw, gout)
     assert gv.dtype == torch.bfloat16
@@ -368,7 +368,10 @@ def test_forward_tiles_equal_backward_prepass(dev, monkeypatch, case, padding):
     v, lc, a, g = (t.cuda() for t in (value, loc, aw, gout))
     out = msda.msda_forward(v, shapes, starts, lc, a, padding)
     out_t, tiles = msda.msda_forward(v, shapes, starts, lc, a, padding, want_tiles=True)
-    assert tiles is not None and tiles.numel() == B * M * len(shapes) * ((Lq + 31) // 32) * 8
+    n_iv = B * M * len(shapes) * ((Lq + 31) // 32) * 8  # the intervals, then the 128-B tail (msda_win.h)
+    assert tiles is not None and tiles.numel() == n_iv + 128
+    tail = tiles[n_iv:].view(torch.int32).cpu()
+    assert torch.all(tail[:16] == 0)  # the persistent backward's queue words, zeroed by the forward
     assert torch.equal(out, out_t)
     ref = msda.msda_backward(v, shapes, starts, lc, a, g, padding)
     got = msda.msda_backward(v, shapes, starts, lc, a, g, padding, tiles=tiles)
@@ -376,7 +379,7 @@ def test_forward_tiles_equal_backward_prepass(dev, monkeypatch, case, padding):
         assert torch.equal(r, x)
     # intervals: every (b, m, level, tile) interval holds each of its samples' base rows (up to
     # one row of slack: this float64 restatement may floor differently at exact row boundaries)
-    iv = tiles.view(torch.int32).view(B, M, len(shapes), -1, 2).cpu()
+    iv = tiles[:n_iv].view(torch.int32).view(B, M, len(shapes), -1, 2).cpu()
     x = loc.double()
     for l, T in enumerate(shapes):
         if padding == "border":
@@ -523,6 +526,91 @@ def test_level_major_refused_without_row_block_path(dev):
     with pytest.raises(RuntimeError, match="level-major"):
         msda.msda_forward(value, shapes, O.level_starts(shapes), _to_level_major(loc), _to_level_major(aw),
                           layout=msda.LEVEL_MAJOR)
+
+
+LM_CASES = [
+    # shapes,                  B, M, P: every case has > 4096 row blocks (the persistent kernel's calls)
+    ([1024, 512, 256, 128],    8, 8, 4),   # the bench's encoder call
+    ([1000, 500, 250, 125],    8, 8, 4),   # ragged: T not a multiple of 16, Lq not of 32
+    ([1000, 500, 250, 125],    8, 8, 2),
+    ([2048, 1024, 512],        2, 16, 1),
+]
+
+
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("case", range(len(LM_CASES)))
+def test_persistent_level_major_backward_equals_per_block_kernel(dev, monkeypatch, case, padding):
+    """win_lm_kernel (persistent waves over per-XCD queues in the tiles buffer's tail) gives the
+    per-block row kernel's gradients bit for bit (same visits in the same order, same MFMA
+    products), and its queues reset themselves: three backwards on one forward's tiles agree, and
+    the queue words are zero afterwards."""
+    for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH", "MSDA_HIP_QORDER",
+              "MSDA_HIP_WIN_LM"):
+        monkeypatch.delenv(k, raising=False)
+    shapes, B, M, P = LM_CASES[case]
+    D, Lq = 64, sum(shapes)
+    value, _, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=120 + case, lo=0.0, hi=1.0)
+    loc = local_locations(B, Lq, M, shapes, P, seed=121 + case)
+    starts = O.level_starts(shapes)
+    v, g = value.cuda(), gout.cuda()
+    lcm, am = _to_level_major(loc).cuda(), _to_level_major(aw).cuda()
+    assert msda.level_major_ok(v, shapes, Lq, P)
+    _, tiles = msda.msda_forward(v, shapes, starts, lcm, am, padding, want_tiles=True, layout=msda.LEVEL_MAJOR)
+    runs = [msda.msda_backward(v, shapes, starts, lcm, am, g, padding, tiles=tiles, layout=msda.LEVEL_MAJOR)
+            for _ in range(3)]
+    n_iv = B * M * len(shapes) * ((Lq + 31) // 32) * 8
+    torch.cuda.synchronize()
+    assert torch.all(tiles[n_iv:].view(torch.int32)[:16].cpu() == 0)
+    monkeypatch.setenv("MSDA_HIP_WIN_LM", "0")
+    ref = msda.msda_backward(v, shapes, starts, lcm, am, g, padding, tiles=tiles, layout=msda.LEVEL_MAJOR)
+    for run in runs:
+        for r, x in zip(ref, run):
+            assert torch.equal(r, x)
+
+
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("case", range(len(WIN_CASES)))
+@pytest.mark.parametrize("stage", ["1", "2"])
+def test_staged_forward_equals_gathering_forward(dev, monkeypatch, case, padding, stage):
+    """msda_fwd16_stage_kernel (each wave's rows of a level staged in its LDS slice when the window
+    fits, 48 / 32 rows; global gathers otherwise) gives the gathering tiles forward's output and tile
+    intervals bit for bit, in both coordinate layouts — on encoder-like local sampling (windows
+    staged) and on uniform / clustered sampling (windows over the cap: the fallback)."""
+    for k in ("MSDA_HIP_FWD_LDS", "MSDA_HIP_QORDER", "MSDA_HIP_BWD_WIN"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
+    shapes, B, M, Lq, P, kind = WIN_CASES[case]
+    D = 64
+    value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=140 + case)
+    if kind == "clustered":
+        loc = clustered_locations(B, Lq, M, shapes, P, seed=141 + case)
+    elif kind == "local" or (kind == "uniform" and Lq == sum(shapes)):
+        loc = local_locations(B, Lq, M, shapes, P, seed=141 + case)
+    starts = O.level_starts(shapes)
+    v, lc, a = value.cuda(), loc.cuda(), aw.cuda()
+    for layout in (0, msda.LEVEL_MAJOR):
+        if layout and not msda.level_major_ok(v, shapes, Lq, P):
+            continue
+        lcx, ax = (_to_level_major(lc), _to_level_major(a)) if layout else (lc, a)
+        monkeypatch.setenv("MSDA_HIP_FWD_STAGE", "0")
+        ref = msda.msda_forward(v, shapes, starts, lcx, ax, padding, want_tiles=True, layout=layout)
+        monkeypatch.setenv("MSDA_HIP_FWD_STAGE", stage)
+        got = msda.msda_forward(v, shapes, starts, lcx, ax, padding, want_tiles=True, layout=layout)
+        assert torch.equal(ref[0], got[0]) and torch.equal(ref[1], got[1])
+
+
+def test_profiling_switch_refused_in_training(dev, monkeypatch):
+    """MSDA_HIP_WIN_EXP skips parts of the row-block kernel (wrong gradients, profiling only): set
+    without MSDA_HIP_PROFILING=1 the backward raises instead of silently returning them."""
+    shapes, B, M, D, P = [256, 128, 64, 32], 2, 8, 64, 4
+    Lq = sum(shapes)
+    value, loc, aw, gout = (t.cuda() for t in rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=130))
+    starts = O.level_starts(shapes)
+    monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
+    monkeypatch.delenv("MSDA_HIP_PROFILING", raising=False)
+    monkeypatch.setenv("MSDA_HIP_WIN_EXP", "1")
+    with pytest.raises(RuntimeError, match="MSDA_HIP_WIN_EXP"):
+        msda.msda_backward(value, shapes, starts, loc, aw, gout, "border", tiles=None)
 
 
 @pytest.mark.parametrize("layout", ["reference", "level_major"])

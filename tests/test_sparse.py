@@ -152,6 +152,7 @@ def test_sparse_encoder_carry_matches_plain_bf16(dev, monkeypatch):
     for x, y in zip(fa, fb):
         assert torch.equal(x, y)
     assert ga.keys() == gb.keys() and len(ga) > 20
-    for n in ga:
-        err = ((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-30)).item()
-        assert err < 1e-2, (n, err)
+    errs = {n: ((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-30)).item() for n in ga}
+    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
+    print("carry vs plain, largest relative gradient differences:", worst)
+    assert worst[0][1] < 2e-3, worst

@@ -23,7 +23,10 @@ def main():
     ap.add_argument("--lq", type=int, default=0, help="queries (0: S, the encoder call; 577: the sparse encoder)")
     ap.add_argument("--qorders", default="1,0", help="MSDA_HIP_QORDER values (tile order of the queries)")
     ap.add_argument("--fwd-lds", default="0", help="MSDA_HIP_FWD_LDS values to time")
+    ap.add_argument("--fwd-stage", default="1,2,0", help="MSDA_HIP_FWD_STAGE values (per-wave staged forward) to time")
+    ap.add_argument("--lm", default="1,0", help="MSDA_HIP_WIN_LM values (persistent level-major kernel) to time")
     args = ap.parse_args()
+    os.environ["MSDA_HIP_PROFILING"] = "1"  # (MSDA_HIP_WIN_EXP is refused without it)
     dev = torch.device("cuda", 0)
     shapes = [args.T, args.T // 2, args.T // 4, args.T // 8]
     S, M, P, B = sum(shapes), 8, 4, 8
@@ -42,12 +45,21 @@ def main():
             _, tiles = msda.msda_forward(value, shapes, starts, loc, aw, want_tiles=True)
             lm = msda.LEVEL_MAJOR
             loc_m, aw_m = loc.permute(0, 2, 3, 1, 4).contiguous(), aw.permute(0, 2, 3, 1, 4).contiguous()
-            us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc_m, aw_m, layout=lm), args.iters)
-            print(json.dumps({**tag, "kernel": "fwd_tiles_level_major", "us": round(us, 2)}), flush=True)
+            for flag in args.fwd_stage.split(","):
+                os.environ["MSDA_HIP_FWD_STAGE"] = flag
+                us = timeit(lambda: msda.msda_forward(value, shapes, starts, loc_m, aw_m, want_tiles=True, layout=lm),
+                            args.iters)
+                print(json.dumps({**tag, "kernel": "fwd_tiles_level_major", "stage": int(flag), "us": round(us, 2)}),
+                      flush=True)
+            os.environ.pop("MSDA_HIP_FWD_STAGE", None)
             _, tiles_m = msda.msda_forward(value, shapes, starts, loc_m, aw_m, want_tiles=True, layout=lm)
-            us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc_m, aw_m, gout, tiles=tiles_m, layout=lm),
-                        args.iters)
-            print(json.dumps({**tag, "kernel": "bwd_win_level_major", "us": round(us, 2)}), flush=True)
+            for flag in args.lm.split(","):
+                os.environ["MSDA_HIP_WIN_LM"] = flag
+                us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc_m, aw_m, gout, tiles=tiles_m,
+                                                       layout=lm), args.iters)
+                print(json.dumps({**tag, "kernel": "bwd_win_level_major", "lm": int(flag), "us": round(us, 2)}),
+                      flush=True)
+            os.environ.pop("MSDA_HIP_WIN_LM", None)
             for e in args.exps.split(","):
                 os.environ["MSDA_HIP_WIN_EXP"] = e
                 us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout, tiles=tiles), args.iters)
