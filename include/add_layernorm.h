@@ -57,6 +57,19 @@ int mfl_add_layernorm_backward_ex(const float* dout, const uint16_t* dout16, con
                                   float* dbeta, float* dpos, float p_drop, const int64_t* seed, void* workspace,
                                   void* stream);
 
+/* As mfl_add_layernorm_backward_ex, and (each optional):
+ *   dpos_accumulate != 0: dpos += dq16 (a pos shared by several layers — the encoder's level position
+ *     embedding, the decoder's query_pos — gets its summed gradient in one buffer instead of one fp32
+ *     tensor per layer added together by autograd);
+ *   dy_colsum (fp32, d): the column sums of dy as stored (rounded to y's dtype), summed in fp32 — the
+ *     bias gradient of the Linear layer that produced y (reference: its bias.grad = dy.sum(0)).
+ * The workspace (mfl_add_layernorm_workspace_bytes) covers both. */
+int mfl_add_layernorm_backward_ex2(const float* dout, const uint16_t* dout16, const uint16_t* dq16, const void* r,
+                                   int r_dtype, const void* y, int y_dtype, const float* gamma, const float* mean,
+                                   const float* rstd, int64_t rows, int64_t d, void* dr, void* dy, float* dgamma,
+                                   float* dbeta, float* dpos, int dpos_accumulate, float* dy_colsum, float p_drop,
+                                   const int64_t* seed, void* workspace, void* stream);
+
 const char* mfl_add_layernorm_last_error(void);
 
 #ifdef __cplusplus

@@ -27,6 +27,14 @@ int mfl_relu_dropout_forward(const void* x, int64_t n, float p_drop, const int64
 int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float p_drop, int dropped, void* dx,
                               void* stream);
 
+/* mfl_relu_dropout_backward on a (rows x cols) row-major matrix (cols % 8 == 0) that also writes
+ * colsum[j] = sum over rows of dx[:, j] as stored (bf16, summed in fp32, fixed order): the bias
+ * gradient of the Linear layer whose output the activation read (reference linear1.bias.grad).
+ * `workspace`: mfl_relu_dropout_colsum_workspace_bytes(rows, cols) bytes. */
+size_t mfl_relu_dropout_colsum_workspace_bytes(int64_t rows, int64_t cols);
+int mfl_relu_dropout_backward_colsum(const void* dy, const void* out, int64_t rows, int64_t cols, float p_drop,
+                                     int dropped, void* dx, float* colsum, void* workspace, void* stream);
+
 /*
  * x.view(rows, row_bytes).masked_fill_(mask[:, None], 0) in place: `value.masked_fill(
  * input_padding_mask[..., None], 0)` of MSDeformAttn.forward (reference

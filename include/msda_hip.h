@@ -116,10 +116,9 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
  *                                 MSDA_HIP_BWD_WIN=0, and must be sized as for msda_hip_backward
  *                                 whenever msda_hip_backward_workspace_bytes differs from the
  *                                 tiles size)
- * The buffer is opaque: after the intervals it holds a 128-byte tail (the persistent backward's
- * work-queue words, which every backward leaves as the forward wrote them, and the query order the
- * forward grouped its tiles by), so one forward's tiles serve any number of backwards on the same
- * inputs, but not two backwards running at the same time on different streams. */
+ * The buffer is opaque: after the intervals it holds a 128-byte tail (the query order the forward
+ * grouped its tiles by, which the backward reads, so both always agree); one forward's tiles serve
+ * any number of backwards on the same inputs. */
 size_t msda_hip_forward_tiles_bytes(int value_dtype, const int64_t* spatial_shapes, int64_t num_levels,
                                     int64_t batch, int64_t spatial_size, int64_t num_heads, int64_t channels,
                                     int64_t num_query, int64_t num_point);

@@ -54,10 +54,13 @@ EXPORTED_SYMBOLS = (
     "mfl_add_layernorm_backward",
     "mfl_add_layernorm_forward_ex",
     "mfl_add_layernorm_backward_ex",
+    "mfl_add_layernorm_backward_ex2",
     "mfl_add_layernorm_last_error",
     # include/ffn_glue.h
     "mfl_relu_dropout_forward",
     "mfl_relu_dropout_backward",
+    "mfl_relu_dropout_colsum_workspace_bytes",
+    "mfl_relu_dropout_backward_colsum",
     "mfl_relu_dropout_last_error",
     "mfl_zero_masked_rows",
     "mfl_zero_masked_rows_batched",
@@ -148,6 +151,9 @@ def _declare(lib):
     lib.mfl_add_layernorm_backward_ex.restype = i32
     lib.mfl_add_layernorm_backward_ex.argtypes = [vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, vp, vp, vp,
                                                   vp, f32, vp, vp, vp]
+    lib.mfl_add_layernorm_backward_ex2.restype = i32
+    lib.mfl_add_layernorm_backward_ex2.argtypes = [vp, vp, vp, vp, i32, vp, i32, vp, vp, vp, i64, i64, vp, vp, vp, vp,
+                                                   vp, i32, vp, f32, vp, vp, vp]
     lib.mfl_gemm_nt_bf16.restype = i32
     lib.mfl_gemm_nt_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
     lib.mfl_gather_keep_backward.restype = i32
@@ -171,6 +177,10 @@ def _declare(lib):
     lib.mfl_relu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]
     lib.mfl_relu_dropout_backward.restype = i32
     lib.mfl_relu_dropout_backward.argtypes = [vp, vp, i64, f32, i32, vp, vp]
+    lib.mfl_relu_dropout_colsum_workspace_bytes.restype = ctypes.c_size_t
+    lib.mfl_relu_dropout_colsum_workspace_bytes.argtypes = [i64, i64]
+    lib.mfl_relu_dropout_backward_colsum.restype = i32
+    lib.mfl_relu_dropout_backward_colsum.argtypes = [vp, vp, i64, i64, f32, i32, vp, vp, vp, vp]
     lib.mfl_zero_masked_rows.restype = i32
     lib.mfl_zero_masked_rows.argtypes = [vp, i64, i64, vp, vp]
     lib.mfl_zero_masked_rows_batched.restype = i32

@@ -177,15 +177,16 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
     const float* __restrict__ dout, const RT* __restrict__ r, const YT* __restrict__ y,
     const float* __restrict__ gamma, const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
     long long rows, int d, RT* __restrict__ dr, YT* __restrict__ dy, float* __restrict__ part,
-    const uint16_t* __restrict__ dout16, const uint16_t* __restrict__ dq16, float* __restrict__ dpos, Drop drop) {
+    const uint16_t* __restrict__ dout16, const uint16_t* __restrict__ dq16, float* __restrict__ dpos, Drop drop,
+    int dpos_acc, int ysum) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const uint64_t seed = drop.seed_ptr ? (uint64_t)drop.seed_ptr[0] : 0;
   const uint32_t thresh = drop_thresh(drop.p);
-  float dg[CH][4], db[CH][4];
+  float dg[CH][4], db[CH][4], ys[CH][4];
 #pragma unroll
   for (int c = 0; c < CH; ++c)
 #pragma unroll
-    for (int k = 0; k < 4; ++k) dg[c][k] = db[c][k] = 0.f;
+    for (int k = 0; k < 4; ++k) dg[c][k] = db[c][k] = ys[c][k] = 0.f;
   for (int i = 0; i < RPB / kWaves; ++i) {
     const long long row = (long long)blockIdx.x * RPB + i * kWaves + wave;
     if (row >= rows) break;  // wave-uniform
@@ -216,7 +217,16 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
       if (dq16) {
         float t[4];
         Vec4<uint16_t>::load(dq16 + base + col, t);
-        if (dpos) Vec4<float>::store(dpos + base + col, t);
+        if (dpos) {
+          if (dpos_acc) {  // the gradient of a pos shared by several layers, summed in place
+            float o[4];
+            Vec4<float>::load(dpos + base + col, o);
+            float sum[4] = {o[0] + t[0], o[1] + t[1], o[2] + t[2], o[3] + t[3]};
+            Vec4<float>::store(dpos + base + col, sum);
+          } else {
+            Vec4<float>::store(dpos + base + col, t);
+          }
+        }
 #pragma unroll
         for (int k = 0; k < 4; ++k) go[k] += t[k];
       }
@@ -242,30 +252,38 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
 #pragma unroll
       for (int k = 0; k < 4; ++k) dx[k] *= kp[c][k];
       Vec4<YT>::store(dy + base + col, dx);
+      if (ysum) {  // column sums of dy as stored (the producing Linear's bias gradient)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          ys[c][k] += sizeof(YT) == 2 ? __uint_as_float(Vec4<uint16_t>::rne(dx[k]) << 16) : dx[k];
+      }
     }
   }
   // gamma / beta partials of the block: waves meet in LDS, fixed order
-  __shared__ float red[kWaves][2][CH * 256];
+  __shared__ float red[kWaves][3][CH * 256];
+  const int np = ysum ? 3 : 2;  // partial rows per block: dgamma, dbeta (, dy column sums)
 #pragma unroll
   for (int c = 0; c < CH; ++c)
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       red[wave][0][c * 256 + lane * 4 + k] = dg[c][k];
       red[wave][1][c * 256 + lane * 4 + k] = db[c][k];
+      red[wave][2][c * 256 + lane * 4 + k] = ys[c][k];
     }
   __syncthreads();
-  for (int j = threadIdx.x; j < 2 * d; j += kWaves * 64) {
+  for (int j = threadIdx.x; j < np * d; j += kWaves * 64) {
     const int which = j / d, col = j - which * d;
     float t = 0.f;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) t += red[w][which][col];
-    part[(long long)blockIdx.x * 2 * d + j] = t;
+    part[(long long)blockIdx.x * np * d + j] = t;
   }
 }
 
 // dgamma / dbeta = sum over the backward blocks' partials (16 groups x 64 columns per block)
 __global__ __launch_bounds__(1024) void add_ln_param_final(const float* __restrict__ part, int nblk, int d2,
-                                                          float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                          float* __restrict__ dysum, int d) {
   __shared__ float red[16][64];
   const int c_l = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + c_l;
@@ -288,8 +306,9 @@ __global__ __launch_bounds__(1024) void add_ln_param_final(const float* __restri
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) t += red[i][c_l];
-    const int half = d2 / 2;
-    if (c < half) dgamma[c] = t; else dbeta[c - half] = t;
+    if (c < d) dgamma[c] = t;
+    else if (c < 2 * d) dbeta[c - d] = t;
+    else dysum[c - 2 * d] = t;
   }
 }
 
@@ -327,7 +346,8 @@ int fwd(const void* r, const void* y, const float* gamma, const float* beta, int
 
 #define MFL_ALN_BWD_R(CHN, R)                                                                              \
   hipLaunchKernelGGL((add_ln_bwd<RT, YT, CHN, R>), dim3(blocks), dim3(kWaves * 64), 0, st, dout, rp, yp, gamma, \
-                     mean, rstd, (long long)rows, (int)d, drp, dyp, part, dout16, dq16, dpos, drop)
+                     mean, rstd, (long long)rows, (int)d, drp, dyp, part, dout16, dq16, dpos, drop, dpos_acc, \
+                     dysum != nullptr ? 1 : 0)
 #define MFL_ALN_BWD(CHN)                                                                                   \
   do {                                                                                                     \
     if (rpb == kBwdRowsShort) MFL_ALN_BWD_R(CHN, kBwdRowsShort); else MFL_ALN_BWD_R(CHN, kBwdRows);        \
@@ -336,7 +356,8 @@ int fwd(const void* r, const void* y, const float* gamma, const float* beta, int
 template <typename RT, typename YT>
 int bwd(const float* dout, const void* r, const void* y, const float* gamma, const float* mean, const float* rstd,
         int64_t rows, int64_t d, void* dr, void* dy, float* dgamma, float* dbeta, void* workspace,
-        const uint16_t* dout16, const uint16_t* dq16, float* dpos, Drop drop, hipStream_t st) {
+        const uint16_t* dout16, const uint16_t* dq16, float* dpos, Drop drop, hipStream_t st, int dpos_acc = 0,
+        float* dysum = nullptr) {
   const int rpb = bwd_rows_per_block(rows);
   const unsigned blocks = (unsigned)((rows + rpb - 1) / rpb);
   auto* rp = static_cast<const RT*>(r);
@@ -352,9 +373,9 @@ int bwd(const float* dout, const void* r, const void* y, const float* gamma, con
   }
   int rc;
   if ((rc = status("backward"))) return rc;
-  const int d2 = (int)(2 * d);
+  const int d2 = (int)((dysum != nullptr ? 3 : 2) * d);
   hipLaunchKernelGGL(add_ln_param_final, dim3((unsigned)((d2 + 63) / 64)), dim3(1024), 0, st, part, (int)blocks, d2,
-                     dgamma, dbeta);
+                     dgamma, dbeta, dysum, (int)d);
   return status("backward params");
 }
 #undef MFL_ALN_BWD
@@ -382,7 +403,7 @@ extern "C" {
 size_t mfl_add_layernorm_workspace_bytes(int64_t rows, int64_t d) {
   if (rows <= 0 || d <= 0) return 0;
   const int rpb = bwd_rows_per_block(rows);
-  return (size_t)((rows + rpb - 1) / rpb) * 2 * (size_t)d * sizeof(float);
+  return (size_t)((rows + rpb - 1) / rpb) * 3 * (size_t)d * sizeof(float);  // (dgamma, dbeta, dy column sums)
 }
 
 int mfl_add_layernorm_forward_ex(const void* r, int r_dtype, const void* y, int y_dtype, const float* gamma,
@@ -447,6 +468,42 @@ int mfl_add_layernorm_backward_ex(const float* dout, const uint16_t* dout16, con
   const Drop drop{seed, p_drop, seed ? 1.f / (1.f - p_drop) : 1.f};
 #define MFL_ALN_BWD_ARGS \
   dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, dout16, dq16, dpos, drop, st
+  if (r_dtype == 0)
+    return y_dtype == 0 ? bwd<float, float>(MFL_ALN_BWD_ARGS) : bwd<float, uint16_t>(MFL_ALN_BWD_ARGS);
+  return y_dtype == 0 ? bwd<uint16_t, float>(MFL_ALN_BWD_ARGS) : bwd<uint16_t, uint16_t>(MFL_ALN_BWD_ARGS);
+#undef MFL_ALN_BWD_ARGS
+}
+
+int mfl_add_layernorm_backward_ex2(const float* dout, const uint16_t* dout16, const uint16_t* dq16, const void* r,
+                                   int r_dtype, const void* y, int y_dtype, const float* gamma, const float* mean,
+                                   const float* rstd, int64_t rows, int64_t d, void* dr, void* dy, float* dgamma,
+                                   float* dbeta, float* dpos, int dpos_accumulate, float* dy_colsum, float p_drop,
+                                   const int64_t* seed, void* workspace, void* stream) {
+  g_err[0] = 0;
+  if (seed && !(p_drop >= 0.f && p_drop < 1.f)) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: dropout p must be in [0, 1)");
+    return 1;
+  }
+  if (!shape_ok(rows, d) || (r_dtype != 0 && r_dtype != 2) || (y_dtype != 0 && y_dtype != 2)) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: needs d %% 256 == 0, d <= 1024, fp32/bf16 inputs");
+    return 1;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (rows == 0) {
+    if (zero_f32(dgamma, d, st) != hipSuccess || zero_f32(dbeta, d, st) != hipSuccess ||
+        (dy_colsum && zero_f32(dy_colsum, d, st) != hipSuccess))
+      return 2;
+    return 0;
+  }
+  if ((!dout && !dout16 && !dq16) || !r || !y || !gamma || !mean || !rstd || !dr || !dy || !dgamma || !dbeta ||
+      !workspace || (dpos_accumulate && !dpos)) {
+    snprintf(g_err, sizeof(g_err), "mfl_add_layernorm_backward: null pointer");
+    return 1;
+  }
+  const Drop drop{seed, p_drop, seed ? 1.f / (1.f - p_drop) : 1.f};
+  const int acc = dpos_accumulate ? 1 : 0;
+#define MFL_ALN_BWD_ARGS \
+  dout, r, y, gamma, mean, rstd, rows, d, dr, dy, dgamma, dbeta, workspace, dout16, dq16, dpos, drop, st, acc, dy_colsum
   if (r_dtype == 0)
     return y_dtype == 0 ? bwd<float, float>(MFL_ALN_BWD_ARGS) : bwd<float, uint16_t>(MFL_ALN_BWD_ARGS);
   return y_dtype == 0 ? bwd<uint16_t, float>(MFL_ALN_BWD_ARGS) : bwd<uint16_t, uint16_t>(MFL_ALN_BWD_ARGS);

@@ -89,6 +89,59 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_bwd(const uint4* __rest
   }
 }
 
+// relu_dropout_bwd on a (rows x cols) matrix that also sums each column of dx as stored (bf16): the
+// bias gradient of the Linear layer that produced the hidden (linear1), which then needs no
+// column-sum pass over dx.  One block = kRdRows rows x 256 vectors of 8 columns; per-block column
+// partials in fixed order, summed by relu_dropout_colsum_final in fixed order (deterministic).
+constexpr int kRdRows = 32;
+
+__global__ __launch_bounds__(kThreads) void relu_dropout_bwd_colsum(const uint4* __restrict__ dy,
+                                                                   const uint4* __restrict__ out, long long rows,
+                                                                   int cvec, float scale, uint4* __restrict__ dx,
+                                                                   float* __restrict__ part) {
+  const int c = blockIdx.y * kThreads + threadIdx.x;
+  if (c >= cvec) return;
+  const long long r0 = (long long)blockIdx.x * kRdRows;
+  float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  for (int rr = 0; rr < kRdRows; ++rr) {
+    const long long row = r0 + rr;
+    if (row >= rows) break;
+    const long long i = row * cvec + c;
+    const uint4 g = dy[i], y = out[i];
+    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, yw[4] = {y.x, y.y, y.z, y.w};
+    uint32_t o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float a = !(lo(yw[j]) <= 0.f) ? lo(gw[j]) * scale : 0.f;
+      const float b = !(hi(yw[j]) <= 0.f) ? hi(gw[j]) * scale : 0.f;
+      o[j] = rne(a) | (rne(b) << 16);
+      sum[2 * j] += lo(o[j]);
+      sum[2 * j + 1] += hi(o[j]);
+    }
+    dx[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  float4* pp = reinterpret_cast<float4*>(part + (long long)blockIdx.x * cvec * 8 + (long long)c * 8);
+  pp[0] = make_float4(sum[0], sum[1], sum[2], sum[3]);
+  pp[1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
+}
+
+// colsum[j] = sum over the row groups' partials (four independent chains, fixed order)
+__global__ __launch_bounds__(kThreads) void relu_dropout_colsum_final(const float* __restrict__ part, int ngroups,
+                                                                     int cols, float* __restrict__ colsum) {
+  const int j = blockIdx.x * kThreads + threadIdx.x;
+  if (j >= cols) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int k = 0;
+  for (; k + 3 < ngroups; k += 4) {
+    s0 += part[(long long)k * cols + j];
+    s1 += part[(long long)(k + 1) * cols + j];
+    s2 += part[(long long)(k + 2) * cols + j];
+    s3 += part[(long long)(k + 3) * cols + j];
+  }
+  for (; k < ngroups; ++k) s0 += part[(long long)k * cols + j];
+  colsum[j] = (s0 + s1) + (s2 + s3);
+}
+
 // value.masked_fill(padding_mask[..., None], 0) of MSDeformAttn (reference attention.py:462-463) in
 // place, and the same on its gradient: one wave per row reads the row's mask byte and stores zeros
 // only when the row is padding, so an all-valid batch costs the mask read, not a pass over value.
@@ -224,6 +277,39 @@ int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float 
                      static_cast<const uint4*>(dy), static_cast<const uint4*>(out), nvec, scale,
                      static_cast<uint4*>(dx));
   return status("backward");
+}
+
+size_t mfl_relu_dropout_colsum_workspace_bytes(int64_t rows, int64_t cols) {
+  if (rows <= 0 || cols <= 0) return 0;
+  return (size_t)((rows + kRdRows - 1) / kRdRows) * (size_t)cols * sizeof(float);
+}
+
+int mfl_relu_dropout_backward_colsum(const void* dy, const void* out, int64_t rows, int64_t cols, float p_drop,
+                                     int dropped, void* dx, float* colsum, void* workspace, void* stream) {
+  g_err[0] = 0;
+  if (rows < 0 || cols <= 0 || cols % 8 != 0 || cols / 8 > 65535LL * kThreads || rows / kRdRows >= (1LL << 31)) {
+    snprintf(g_err, sizeof(g_err), "mfl_relu_dropout_backward_colsum: cols must be a positive multiple of 8");
+    return 1;
+  }
+  if (!args_ok("mfl_relu_dropout_backward_colsum", rows * cols, dy, out, dx, p_drop)) return 1;
+  if (!colsum || (rows > 0 && !workspace)) {
+    snprintf(g_err, sizeof(g_err), "mfl_relu_dropout_backward_colsum: null colsum / workspace");
+    return 1;
+  }
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  const float scale = dropped ? 1.f / (1.f - p_drop) : 1.f;
+  const int cvec = (int)(cols / 8);
+  const long long groups = (rows + kRdRows - 1) / kRdRows;
+  if (groups > 0) {
+    hipLaunchKernelGGL(relu_dropout_bwd_colsum, dim3((unsigned)groups, (unsigned)((cvec + kThreads - 1) / kThreads)),
+                       dim3(kThreads), 0, st, static_cast<const uint4*>(dy), static_cast<const uint4*>(out),
+                       (long long)rows, cvec, scale, static_cast<uint4*>(dx), static_cast<float*>(workspace));
+    int rc;
+    if ((rc = status("backward (column sums)"))) return rc;
+  }
+  hipLaunchKernelGGL(relu_dropout_colsum_final, dim3((unsigned)((cols + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     st, static_cast<const float*>(workspace), (int)groups, (int)cols, colsum);
+  return status("backward (column sums, final)");
 }
 
 int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t row_bytes, const uint8_t* mask,

@@ -2579,7 +2579,8 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
       // L1 and the barrier-free gather kernel hides their latency), so the gathers stay the default
       const bool fwd_lds = env_int("MSDA_HIP_FWD_LDS", 0) != 0;
       // per-wave staged rows (msda_fwd16_stage_kernel; MSDA_HIP_FWD_STAGE=0: the gathering kernel)
-      const int fwd_stage = fwd_lds ? 0 : env_int("MSDA_HIP_FWD_STAGE", 1);  // 1: 48 rows a wave, 2: 32
+      // (measured slower at the bench's encoder call: 76 / 66 us against 33.5, tools/win_exp.py, r05e)
+      const int fwd_stage = fwd_lds ? 0 : env_int("MSDA_HIP_FWD_STAGE", 0);  // 1: 48 rows a wave, 2: 32
       auto* tl = static_cast<int2*>(tiles);
       const QOrder qo = make_qorder(pr.Lq, pr.S, (int)pr.L, pr.lv.T, pr.lv.start);
 #define MSDA_FT(Z, PP)                                                                              \

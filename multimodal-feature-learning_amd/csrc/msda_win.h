@@ -102,14 +102,11 @@ struct WinShape {
 
 constexpr int kWinQT = 32;          // queries per tile of the row-block backward
 constexpr int kWinNone = 1 << 29;   // an empty interval is (kWinNone, -kWinNone)
-// After the tile intervals, the tiles buffer holds the persistent backward's work queue: 8 per-XCD
-// heads and 8 done counters (unsigned).  The tiles forward zeroes them; the backward leaves them
-// zero (its last wave of each queue resets both), so one forward's buffer serves any number of
-// backwards, eager or replayed.
-constexpr int kWinQueueWords = 16;
-// Then the query order the forward grouped its tiles by (a QOrder, written by the tiles forward):
-// the backward reads it from there, so the two always agree whatever the environment does between
-// them (MSDA_HIP_QORDER is read by the forward only).
+// After the tile intervals, the tiles buffer holds a 128-B tail written by the tiles forward (every
+// byte defined): 64 reserved bytes (zero), then the query order the forward grouped its tiles by (a
+// QOrder): the backward reads it from there, so the two always agree whatever the environment does
+// between them (MSDA_HIP_QORDER is read by the forward only).
+constexpr int kWinQueueWords = 16;  // (reserved words)
 constexpr size_t kWinQOrderOffset = kWinQueueWords * sizeof(unsigned);
 constexpr size_t kWinTailBytes = 128;
 static_assert(kWinQOrderOffset + sizeof(QOrder) <= kWinTailBytes, "tiles tail too small");

@@ -518,30 +518,25 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
 // ---------------------------------------------------------------------------------------------
 // win_lm_kernel: the row-block backward for level-major coordinates with the forward's tile
 // intervals (the encoder calls: MSDeformAttn's prologue writes level-major locations / weights),
-// one wave per 16-row block as win_bwd_kernel, restructured for residency and latency
-// (profiles/r05_*: the one-block-per-workgroup kernel averaged 2.5 resident waves per SIMD of its
-// 4, 38 % of its wave time parked on memory, LDS bank conflicts 0.74 extra cycles an LDS op):
-//  * persistent waves: a grid of about as many single-wave workgroups as the chip holds, each
-//    popping row blocks from a per-XCD queue (one returning atomic per block, issued a block ahead
-//    so its latency hides under the block's visits) in the coarsest-level-first order — no wave
-//    start-up per block, and the long coarse blocks spread over the waves before the short ones;
-//  * 7.2 KB of LDS a wave (20+ waves per CU): the grad_out tile in 128-B rows with an XOR swizzle
-//    of the 16-B chunks (conflict-free for the row writes, the dots' A reads and the transposed B
-//    reads) instead of 144-B padded rows, and the dots buffer reused for the coefficient tile C
-//    (phases reordered: dots -> coordinate gradients -> grad_value);
+// one wave per 16-row block as win_bwd_kernel (same dispatch order: coarsest level first, each
+// level in 8 contiguous chunks, chunk x on XCD x), with the per-visit work restructured:
+//  * 7.2 KB of LDS a wave instead of 10 KB: the grad_out tile in 128-B rows with an XOR swizzle of
+//    the 16-B chunks (conflict-free for the row writes, the dots' A reads and the transposed B reads
+//    of rows {0-3, 8-11} (+4, +16)) instead of 144-B padded rows, and the dots buffer reused for the
+//    coefficient tile C (phases reordered: dots -> coordinate gradients -> grad_value);
 //  * 32-bit offsets from per-block base pointers (level-major: a tile's coordinates of one level
-//    are 32 P contiguous floats);
-//  * the next visit's coordinates and grad_out rows are requested right after the current tile's
-//    rows reach LDS, before the dots.
-// Same arithmetic as win_bwd_kernel per visit (the same taps, the same bf16 hi + lo coefficient
-// split, the same MFMA products in the same order), so its outputs are bit for bit those of
-// win_bwd_kernel with consecutive tiles (tests/test_gpu_op.py).
+//    are 32 P contiguous floats), the compaction rank from mbcnt;
+//  * the next visit's coordinates and grad_out rows requested once the coordinate gradients are
+//    stored (rg / rl free), before the grad_value steps.
+// Measured at the bench's encoder call (tools/win_exp.py, r05g): 49.4 / 54.8 us (init / trained
+// sampling) against 51.0 / 55.7 for win_bwd_kernel on level-major coordinates.  Persistent variants
+// were slower or no better: waves popping blocks from per-XCD queues (a returning atomic per block)
+// 202 us; a static round-robin of blocks over a resident grid 51.5 / 58.3 us.
+// Same arithmetic per visit as win_bwd_kernel (the same taps, bf16 hi + lo coefficient split and
+// MFMA products in the same order), so its outputs are win_bwd_kernel's bit for bit
+// (tests/test_gpu_op.py::test_persistent_level_major_backward_equals_per_block_kernel).
 // ---------------------------------------------------------------------------------------------
-constexpr int kLmRow = 128;     // bytes per grad_out / coefficient row in LDS
-#ifndef LM_WAVES
-#define LM_WAVES 4
-#endif
-constexpr int kLmWavesPerXcd = 32 * 4 * LM_WAVES;  // 32 CUs x 4 SIMDs x the waves a SIMD holds (the grid cap per queue)
+constexpr int kLmRow = 128;  // bytes per grad_out / coefficient row in LDS
 
 // the swizzled byte offset of 16-B chunk c of row r: chunk c ^ f(r), f(r) in {0, 2, 4, 6} from
 // bits 1 and 3 of r — rows {0,1,2,3,8,9,10,11} (a 32-lane half of a transposed read) land on 16
@@ -551,10 +546,10 @@ __device__ __forceinline__ int lm_sw(int r, int c) {
 }
 
 template <bool ZEROS, bool COORDS, int P>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LM_WAVES))) void win_lm_kernel(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void win_lm_kernel(
     const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     const uint16_t* __restrict__ gout, uint16_t* __restrict__ gval, float* __restrict__ gloc,
-    float* __restrict__ gaw, const int2* __restrict__ tiles, unsigned* __restrict__ queue, const WinShape sh) {
+    float* __restrict__ gaw, const int2* __restrict__ tiles, const WinShape sh) {
   constexpr int NS = kQT * P;                  // samples per tile and level
   constexpr int SPL = NS >= 64 ? NS / 64 : 1;  // samples per lane
   __shared__ __attribute__((aligned(16))) unsigned char s_g[kQT * kLmRow];  // the tile's grad_out rows
@@ -570,29 +565,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LM_WAVES))) 
   const int wg0 = lm_sw(grow, gch), wg1 = lm_sw(grow + 8, gch);
   const int wa0 = lm_sw(li, g), wa1 = lm_sw(li, 4 + g);
   const unsigned x8 = blockIdx.x & 7u;
-  const unsigned nwx = gridDim.x >> 3;  // waves of this queue (the grid is 8 nwx)
-  unsigned* const head = queue + x8;
-  unsigned* const done = queue + 8 + x8;
   const long long ntiles_all = sh.B * sh.M * sh.L * (long long)sh.ntile;
   const QOrder qo = *reinterpret_cast<const QOrder*>(reinterpret_cast<const char*>(tiles + ntiles_all) +
                                                      kWinQOrderOffset);
-  // queue slots of this XCD: level l (coarsest first) has cl = ceil(B M nbl / 8) slots, slot i of
-  // it is block x8 cl + i of the level (none past its end)
-  unsigned nsx = 0;
-  for (int l = 0; l < sh.L; ++l)
-    nsx += (unsigned)((sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + 7) / 8);
+  // the slots of XCD x8 (blocks p with p % 8 == x8 share one): level l (coarsest first) has
+  // cl = ceil(B M nbl / 8) slots, slot i of it is block x8 cl + i of the level (none past its end)
   const int rs = sh.M * 64;  // grad_out / value row stride (elements)
   const int cq = qo.cs == 0 ? 1 : 0;  // (uniform) consecutive tiles
 
-  unsigned slot;
+  const unsigned slot = blockIdx.x >> 3;
   {
-    unsigned v = 0;
-    if (lane == 0) v = atomicAdd(head, 1u);
-    slot = (unsigned)__builtin_amdgcn_readfirstlane((int)v);
-  }
-  while (slot < nsx) {
-    unsigned nxt = 0;  // the next block, returned while this one runs
-    if (lane == 0) nxt = atomicAdd(head, 1u);
     int l = sh.L - 1;
     int j = -1;  // (B M nblk < 2^31: checked by the host)
     {
@@ -602,7 +584,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LM_WAVES))) 
         const unsigned cl = (nl + 7u) / 8u;
         if (s < cl) {
           const unsigned jj = x8 * cl + s;
-          j = jj < nl ? (int)jj : -1;  // (past the level's end on this queue: none)
+          j = jj < nl ? (int)jj : -1;  // (past the level's end on this XCD: none)
           break;
         }
         s -= cl;
@@ -826,16 +808,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(LM_WAVES))) 
         }
       }
     }
-    slot = (unsigned)__builtin_amdgcn_readfirstlane((int)nxt);
-  }
-  // every wave of this queue pops once past its end; the last to do so resets the queue for the
-  // next launch on this tiles buffer
-  if (lane == 0) {
-    const unsigned d = atomicAdd(done, 1u);
-    if (d == nwx - 1u) {
-      atomicExch(head, 0u);
-      atomicExch(done, 0u);
-    }
   }
 }
 }  // namespace
@@ -879,6 +851,16 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
                       void* gloc, void* gaw, void* workspace, const void* tiles_ready, const WinShape* shape,
                       int zeros, int coord_layout, hipStream_t st) {
   WinShape sh = *shape;
+  // profiling only: MSDA_HIP_WIN_EXP skips parts of the kernel (the results are WRONG), so it is
+  // honoured only together with MSDA_HIP_PROFILING=1 (tools/win_exp.py); alone it is an error, never
+  // silently wrong gradients in training
+  const char* xe = getenv("MSDA_HIP_WIN_EXP");
+  sh.exp = xe ? atoi(xe) : 0;
+  if (sh.exp != 0) {
+    const char* pe = getenv("MSDA_HIP_PROFILING");
+    if (pe == nullptr || atoi(pe) != 1) return -2;
+  }
+  sh.qo_dev = tiles_ready != nullptr ? 1 : 0;
   // (the interval prepass reads whole query rows: the reference layout; level-major calls bring
   // the forward's intervals)
   if (coord_layout != 0 && tiles_ready == nullptr) return -1;
@@ -894,14 +876,14 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   sh.nblk = nb;
   if (sh.B * sh.M == 0 || nb == 0) return 0;
   const long long nblocks = sh.B * sh.M * (long long)nb;
-  // the persistent level-major kernel (win_lm_kernel): the forward's tiles (and their tail: queue,
-  // query order), many blocks (one wave each), 32-bit element offsets within a clip
+  // the level-major row kernel (win_lm_kernel): the forward's tiles (and their tail: the query
+  // order), many blocks (one wave each), 32-bit element offsets within a clip
   // (MSDA_HIP_WIN_LM=0: the per-block kernel, for A/B)
   const char* lme = getenv("MSDA_HIP_WIN_LM");
   const bool lm_kernel = coord_layout == 1 && tiles_ready != nullptr && nblocks > 4096 && sh.P <= 4 &&
                          (lme == nullptr || atoi(lme) != 0) && sh.Lq * sh.M * 64 < (1LL << 31) &&
                          sh.S * sh.M * 64 < (1LL << 31) && sh.L * sh.Lq * sh.P < (1LL << 31) && nblocks < (1LL << 31) &&
-                         getenv("MSDA_HIP_WIN_EXP") == nullptr && getenv("MSDA_HIP_WIN_SPLIT") == nullptr;
+                         sh.exp == 0 && getenv("MSDA_HIP_WIN_SPLIT") == nullptr;
   // position-chunk order where the blocks are many (T = 4096: 3,840 an XCD; 245 -> 219 us at the
   // configs[3] call), coarsest-level-first where they are few and the longest blocks set the tail
   // (T = 1024: 960 an XCD; 55 against 64 us, tools/win_tiles_ab.py).  MSDA_HIP_WIN_ORDER: 0 / 1 forces.
@@ -912,10 +894,7 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
     sh.exp = 0;
     unsigned nsx = 0;
     for (int l = 0; l < sh.L; ++l) nsx += (unsigned)((sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + 7) / 8);
-    const unsigned nwx = nsx < (unsigned)kLmWavesPerXcd ? nsx : (unsigned)kLmWavesPerXcd;
-    const long long ntiles_all = sh.B * sh.M * sh.L * (long long)sh.ntile;
     auto* tl = static_cast<const int2*>(tiles_ready);
-    auto* q = reinterpret_cast<unsigned*>(const_cast<int2*>(tl + ntiles_all));
     const bool coords = gloc != nullptr || gaw != nullptr;
     auto* v = static_cast<const uint16_t*>(value);
     auto* lc = static_cast<const float*>(loc);
@@ -925,7 +904,7 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
     auto* gl = static_cast<float*>(gloc);
     auto* ga = static_cast<float*>(gaw);
 #define WIN_LM(Z, C, N) \
-  hipLaunchKernelGGL((win_lm_kernel<Z, C, N>), dim3(8u * nwx), dim3(64), 0, st, v, lc, a, g, gv, gl, ga, tl, q, sh)
+  hipLaunchKernelGGL((win_lm_kernel<Z, C, N>), dim3(8u * nsx), dim3(64), 0, st, v, lc, a, g, gv, gl, ga, tl, sh)
 #define WIN_LM_P(Z, C)                                                  \
   do {                                                                  \
     switch (sh.P) {                                                     \
@@ -946,16 +925,6 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   const bool chunked = win_chunk_order(sh) &&
                        (order_env == 1 || (order_env != 0 && (long long)sh.ppx * sh.nblk >= 2048));
   if (!chunked) sh.nchunk = 0;
-  // profiling only: MSDA_HIP_WIN_EXP skips parts of the kernel (the results are WRONG), so it is
-  // honoured only together with MSDA_HIP_PROFILING=1 (tools/win_exp.py); alone it is an error, never
-  // silently wrong gradients in training
-  const char* xe = getenv("MSDA_HIP_WIN_EXP");
-  sh.exp = xe ? atoi(xe) : 0;
-  if (sh.exp != 0) {
-    const char* pe = getenv("MSDA_HIP_PROFILING");
-    if (pe == nullptr || atoi(pe) != 1) return -2;
-  }
-  sh.qo_dev = tiles_ready != nullptr ? 1 : 0;
   // tile intervals: written by the forward (msda_fwd16_tiles_kernel) or by the prepass below
   auto* tiles = static_cast<int2*>(tiles_ready != nullptr ? const_cast<void*>(tiles_ready) : workspace);
   const unsigned tile_wgs = tiles_ready != nullptr ? 0u : (unsigned)(sh.B * sh.ntile);

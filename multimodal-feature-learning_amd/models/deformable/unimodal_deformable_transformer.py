@@ -19,7 +19,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear, flush_point
-from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
+from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported, pos_sink
 from ..modules.ffn import relu_dropout
 from ..modules.value_proj import layer_values, layer_values_supported
 
@@ -197,15 +197,16 @@ class DeformableTransformerEncoderLayer(nn.Module):
         return self.forward_ffn(src)
 
     def forward_carry(self, src, value, query, next_pos, reference_points, temporal_shapes, level_start_index,
-                      padding_mask=None):
+                      padding_mask=None, pos_acc=None):
         """``forward`` with the 16-bit operands carried between layers (bf16 autocast on the GPU):
         ``value`` / ``query`` are this layer's MSDA inputs (``src`` and ``src + pos`` in bf16, or
         the fp32 tensors themselves), and the fused add + LayerNorms hand back the next layer's
-        ``(src, value, query)`` (query = bf16(out + next_pos); None when next_pos is None)."""
+        ``(src, value, query)`` (query = bf16(out + next_pos); None when next_pos is None).
+        ``pos_acc``: next_pos came from ``pos_sink`` (its gradient summed in place)."""
         attn = self.self_attn(query, reference_points, value, temporal_shapes, level_start_index, padding_mask)
         src, src16, _ = add_layer_norm_carry(src, attn, self.norm1, dropout=self.dropout1)
         hidden = relu_dropout(self.linear1(src16), self.activation, self.dropout2)
-        return add_layer_norm_carry(src, self.linear2(hidden), self.norm2, next_pos, self.dropout3)
+        return add_layer_norm_carry(src, self.linear2(hidden), self.norm2, next_pos, self.dropout3, pos_acc=pos_acc)
 
 
 class DeformableTransformerEncoder(nn.Module):
@@ -226,12 +227,15 @@ class DeformableTransformerEncoder(nn.Module):
         if (self.layers and all(type(layer) is DeformableTransformerEncoderLayer for layer in self.layers)
                 and carry_supported(src, self.layers[0].norm1)):
             # bf16 operands carried from each fused add + LayerNorm to the next layer (no casts,
-            # no pos add, no gradient accumulation kernels between layers)
+            # no pos add, no gradient accumulation kernels between layers; pos's gradient summed in
+            # place by the fused backwards: add_norm.pos_sink)
+            pos, pos_acc = pos_sink(pos)
             value, query = src, DeformableTransformerEncoderLayer.with_pos_embed(src, pos)
             for i, layer in enumerate(self.layers):
                 next_pos = pos if i + 1 < len(self.layers) else None
                 out, value, query = layer.forward_carry(out, value, query, next_pos, reference_points,
-                                                        temporal_shapes, level_start_index, padding_mask)
+                                                        temporal_shapes, level_start_index, padding_mask,
+                                                        pos_acc=pos_acc)
                 if query is None:
                     query = value
             out._mfl_bf16 = value  # the last layer's bf16(out): the decoder's value projections read it
@@ -277,7 +281,7 @@ class DeformableTransformerDecoderLayer(nn.Module):
                                   src_padding_mask, query_mask, value)[0]
 
     def forward_carry(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
-                      src_padding_mask=None, query_mask=None, value=None, carried=None):
+                      src_padding_mask=None, query_mask=None, value=None, carried=None, pos_acc=None):
         """``forward`` returning ``(out, out16, q16)``: under bf16 autocast on the GPU the last fused add +
         LayerNorm also writes bf16(out) and bf16(out + query_pos), the next layer's self-attention
         inputs (``carried``); (out, None, None) otherwise."""
@@ -285,12 +289,13 @@ class DeformableTransformerDecoderLayer(nn.Module):
         if carry_supported(tgt, self.norm2) and (query_pos is None or query_pos.shape == tgt.shape):
             # bf16(tgt + query_pos) for the cross-attention query and bf16(tgt) for linear1 straight
             # from the fused add + LayerNorms (no pos add, no casts, no gradient accumulation)
-            tgt, tgt16, q16 = add_layer_norm_carry(tgt, sa, self.norm2, query_pos, self.dropout2)
+            tgt, tgt16, q16 = add_layer_norm_carry(tgt, sa, self.norm2, query_pos, self.dropout2, pos_acc=pos_acc)
             ca = self.cross_attn(q16 if q16 is not None else tgt16, reference_points, src, src_temporal_shapes,
                                  level_start_index, src_padding_mask, value=value)
             tgt, tgt16, _ = add_layer_norm_carry(tgt, ca, self.norm1, dropout=self.dropout1)
             hidden = relu_dropout(self.linear1(tgt16), self.activation, self.dropout3)
-            out, out16, q16 = add_layer_norm_carry(tgt, self.linear2(hidden), self.norm3, query_pos, self.dropout4)
+            out, out16, q16 = add_layer_norm_carry(tgt, self.linear2(hidden), self.norm3, query_pos, self.dropout4,
+                                                   pos_acc=pos_acc)
             return out, out16, q16
         tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         ca = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points, src, src_temporal_shapes,
@@ -327,6 +332,9 @@ class DeformableTransformerDecoder(nn.Module):
             # every layer projects the same memory: one batched GEMM each way (value_proj.py)
             values = layer_values(attns, src, src_padding_mask)
         carried = None
+        pos_acc = None
+        if all(type(layer) is DeformableTransformerDecoderLayer for layer in self.layers):
+            query_pos, pos_acc = pos_sink(query_pos)  # its gradient summed in place (add_norm.pos_sink)
         for lid, layer in enumerate(self.layers):
             if reference_points.shape[-1] == 2:
                 scale = torch.stack([src_valid_ratios, src_valid_ratios], -1)[:, None]
@@ -338,7 +346,8 @@ class DeformableTransformerDecoder(nn.Module):
                 # bf16 self-attention inputs carried from the previous layer's last add + LayerNorm
                 output, out16, q16 = layer.forward_carry(
                     output, query_pos, reference_points_input, src, src_temporal_shapes, src_level_start_index,
-                    src_padding_mask, query_padding_mask, values[lid] if values is not None else None, carried)
+                    src_padding_mask, query_padding_mask, values[lid] if values is not None else None, carried,
+                    pos_acc=pos_acc)
                 carried = (out16, q16)
             elif values is not None:
                 output = layer(output, query_pos, reference_points_input, src, src_temporal_shapes,

@@ -15,13 +15,60 @@ import torch
 from torch import nn
 from torch.autograd import Function
 
-__all__ = ["add_layer_norm", "add_layer_norm_carry", "seed_pool"]
+__all__ = ["add_layer_norm", "add_layer_norm_carry", "seed_pool", "pos_sink", "PosGradAcc"]
 
 _TAGS = {torch.float32: 0, torch.bfloat16: 2}
 
 
 def _ptr(t):
     return t.data_ptr() if t is not None else None
+
+
+def _attach_colsum(dy, colsum):
+    """Hand the column sums of ``dy`` (as stored) to the Linear layer whose output gradient it is
+    (linear.py: its bias gradient, no column-sum pass).  Tagged with dy's version counter: autograd
+    adding another gradient into dy in place would make them stale, and the consumer then ignores them."""
+    if colsum is not None:
+        dy._mfl_colsum = (colsum, dy._version)
+
+
+class PosGradAcc:
+    """The summed gradient of a pos read by several fused add + LayerNorms (the encoder's level
+    position embedding, the decoder's query_pos): each backward adds its dq16 into ``buf`` in its
+    own kernel (mfl_add_layernorm_backward_ex2, dpos_accumulate), and ``pos_sink``'s node hands the
+    sum to autograd once, after all of them (autograd runs a node after every consumer of its output)."""
+
+    def __init__(self):
+        self.buf = None
+
+
+class _PosSink(Function):
+    @staticmethod
+    def forward(ctx, pos, acc):
+        ctx.set_materialize_grads(False)
+        ctx.acc = acc
+        return pos.view_as(pos)
+
+    @staticmethod
+    def backward(ctx, g):
+        buf, ctx.acc.buf = ctx.acc.buf, None
+        if buf is None:
+            return g, None
+        if g is not None:  # the other (autograd) consumers' gradient
+            buf = buf.add_(g)
+        return buf, None
+
+
+def pos_sink(pos):
+    """``(pos', acc)``: give the layers ``pos'`` as their pos and ``acc`` as ``add_layer_norm_carry``'s
+    ``pos_acc``; the fused backwards then sum pos's gradient in place instead of autograd adding one
+    fp32 tensor per layer (reference: the gradient of ``tensor + pos`` summed over the layers).
+    ``(pos, None)`` where the fused path does not run."""
+    if (pos is None or not pos.requires_grad or not pos.is_cuda or pos.dtype != torch.float32
+            or not torch.is_autocast_enabled("cuda") or torch.get_autocast_dtype("cuda") != torch.bfloat16):
+        return pos, None
+    acc = PosGradAcc()
+    return _PosSink.apply(pos, acc), acc
 
 
 class _SeedPool:
@@ -103,13 +150,15 @@ class _AddLayerNorm(Function):
         dw = torch.empty(d, dtype=torch.float32, device=r.device)
         db = torch.empty(d, dtype=torch.float32, device=r.device)
         ws = torch.empty(max(lib.mfl_add_layernorm_workspace_bytes(rows, d), 4), dtype=torch.uint8, device=r.device)
-        rc = lib.mfl_add_layernorm_backward_ex(dout.data_ptr(), None, None, r.data_ptr(), _TAGS[r.dtype], y.data_ptr(),
-                                               _TAGS[y.dtype], weight.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
-                                               rows, d, dr.data_ptr(), dy.data_ptr(), dw.data_ptr(), db.data_ptr(),
-                                               None, ctx.p_drop, _ptr(seed), ws.data_ptr(),
-                                               _native.stream_handle(r.device))
+        ysum = torch.empty(d, dtype=torch.float32, device=r.device) if y.dtype != torch.float32 else None
+        rc = lib.mfl_add_layernorm_backward_ex2(dout.data_ptr(), None, None, r.data_ptr(), _TAGS[r.dtype], y.data_ptr(),
+                                                _TAGS[y.dtype], weight.data_ptr(), mean.data_ptr(), rstd.data_ptr(),
+                                                rows, d, dr.data_ptr(), dy.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                                                None, 0, _ptr(ysum), ctx.p_drop, _ptr(seed), ws.data_ptr(),
+                                                _native.stream_handle(r.device))
         if rc != 0:
             raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
+        _attach_colsum(dy, ysum)
         return dr, dy, dw, db, None, None, None
 
 
@@ -130,7 +179,7 @@ def add_layer_norm(r, y, norm: nn.LayerNorm, dropout=None):
 
 class _AddLayerNormCarry(Function):
     @staticmethod
-    def forward(ctx, r, y, weight, bias, pos, eps, p_drop, seed):
+    def forward(ctx, r, y, weight, bias, pos, eps, p_drop, seed, pos_acc=None):
         from ... import _native, _trace
         _trace.hit("add_ln_carry")
         lib = _native.load_library()
@@ -150,6 +199,8 @@ class _AddLayerNormCarry(Function):
             raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
         ctx.has_pos = pos is not None
         ctx.pos_needs_grad = pos is not None and pos.requires_grad
+        ctx.pos_acc = pos_acc if ctx.pos_needs_grad else None
+        ctx.n_grads = 9 if pos_acc is not None else 8  # (apply called without pos_acc: 8 inputs)
         ctx.p_drop = p_drop
         ctx.save_for_backward(r, y, weight, mean, rstd, seed)
         return out, out16, q16
@@ -162,7 +213,7 @@ class _AddLayerNormCarry(Function):
         d = r.shape[-1]
         rows = r.numel() // d
         if dout is None and dout16 is None and dq16 is None:
-            return None, None, None, None, None, None, None, None
+            return (None,) * ctx.n_grads
         dout = dout.to(torch.float32).contiguous() if dout is not None else None
         dout16 = dout16.to(torch.bfloat16).contiguous() if dout16 is not None else None
         dq16 = dq16.to(torch.bfloat16).contiguous() if dq16 is not None else None
@@ -170,19 +221,28 @@ class _AddLayerNormCarry(Function):
         dy = torch.empty_like(y)
         dw = torch.empty(d, dtype=torch.float32, device=r.device)
         db = torch.empty(d, dtype=torch.float32, device=r.device)
-        dpos = None
-        if ctx.pos_needs_grad:
+        dpos, acc, accumulate = None, ctx.pos_acc, 0
+        if acc is not None:
+            # the shared pos's summed gradient (PosGradAcc): the first backward writes it, the others add
+            if dq16 is not None:
+                accumulate = 1 if acc.buf is not None else 0
+                if acc.buf is None:
+                    acc.buf = torch.empty(r.shape, dtype=torch.float32, device=r.device)
+                dpos = acc.buf
+        elif ctx.pos_needs_grad:
             dpos = (torch.empty(r.shape, dtype=torch.float32, device=r.device) if dq16 is not None
                     else torch.zeros(r.shape, dtype=torch.float32, device=r.device))
+        ysum = torch.empty(d, dtype=torch.float32, device=r.device) if y.dtype != torch.float32 else None
         ws = torch.empty(max(lib.mfl_add_layernorm_workspace_bytes(rows, d), 4), dtype=torch.uint8, device=r.device)
-        rc = lib.mfl_add_layernorm_backward_ex(
+        rc = lib.mfl_add_layernorm_backward_ex2(
             _ptr(dout), _ptr(dout16), _ptr(dq16), r.data_ptr(), _TAGS[r.dtype], y.data_ptr(), _TAGS[y.dtype],
             weight.data_ptr(), mean.data_ptr(), rstd.data_ptr(), rows, d, dr.data_ptr(), dy.data_ptr(),
-            dw.data_ptr(), db.data_ptr(), _ptr(dpos) if dq16 is not None else None, ctx.p_drop, _ptr(seed),
-            ws.data_ptr(), _native.stream_handle(r.device))
+            dw.data_ptr(), db.data_ptr(), _ptr(dpos) if dq16 is not None else None, accumulate, _ptr(ysum),
+            ctx.p_drop, _ptr(seed), ws.data_ptr(), _native.stream_handle(r.device))
         if rc != 0:
             raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
-        return dr, dy, dw, db, dpos, None, None, None
+        _attach_colsum(dy, ysum)
+        return (dr, dy, dw, db, (None if acc is not None else dpos), None, None, None, None)[:ctx.n_grads]
 
 
 def carry_supported(r, norm) -> bool:
@@ -195,15 +255,19 @@ def carry_supported(r, norm) -> bool:
             and r.numel() > 0 and norm.weight.device == r.device)
 
 
-def add_layer_norm_carry(r, y, norm: nn.LayerNorm, pos=None, dropout=None):
+def add_layer_norm_carry(r, y, norm: nn.LayerNorm, pos=None, dropout=None, pos_acc=None):
     """``(out, out16, q16)`` with ``out = norm(r + dropout(y))`` (fp32 under autocast), ``out16`` its bf16
     copy and ``q16 = bf16(out + pos)`` (None without ``pos``).  Fused on the GPU under bf16
-    autocast; elsewhere ``(out, out, out + pos)``, which every consumer treats exactly as before."""
+    autocast; elsewhere ``(out, out, out + pos)``, which every consumer treats exactly as before.
+    ``pos_acc``: pos came from ``pos_sink`` and its gradient is summed there (see PosGradAcc)."""
     if (carry_supported(r, norm) and r.shape == y.shape and y.dtype in _TAGS
             and (pos is None or (pos.shape == r.shape and pos.dtype == torch.float32))):
         p_drop, seed = _drop_args(dropout, r.device)
+        args = (r.contiguous(), y.contiguous(), norm.weight, norm.bias, pos.contiguous() if pos is not None else None,
+                norm.eps, p_drop, seed)
+        if pos is not None and pos_acc is not None:
+            args += (pos_acc,)
         with torch.autocast("cuda", enabled=False):
-            return _AddLayerNormCarry.apply(r.contiguous(), y.contiguous(), norm.weight, norm.bias,
-                                            pos.contiguous() if pos is not None else None, norm.eps, p_drop, seed)
+            return _AddLayerNormCarry.apply(*args)
     out = add_layer_norm(r, y, norm, dropout)
     return out, out, (out + pos if pos is not None else None)

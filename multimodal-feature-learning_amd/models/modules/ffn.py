@@ -15,7 +15,7 @@ import torch.nn.functional as F
 from torch import nn
 from torch.autograd import Function
 
-from .add_norm import _drop_args, _ptr
+from .add_norm import _attach_colsum, _drop_args, _ptr
 
 __all__ = ["relu_dropout"]
 
@@ -42,10 +42,24 @@ class _ReluDropout(Function):
         (out,) = ctx.saved_tensors
         dy = dy.to(out.dtype).contiguous()
         dx = torch.empty_like(out)
-        rc = lib.mfl_relu_dropout_backward(dy.data_ptr(), out.data_ptr(), out.numel(), ctx.p_drop, int(ctx.dropped),
-                                           dx.data_ptr(), _native.stream_handle(out.device))
+        cols = out.shape[-1]
+        rows = out.numel() // cols if cols else 0
+        if cols % 8 == 0 and rows > 0:
+            # dx and its column sums in one pass: linear1's bias gradient, handed to it with dx
+            # (add_norm._attach_colsum; linear._given_colsum) instead of a column-sum pass over dx
+            colsum = torch.empty(cols, dtype=torch.float32, device=out.device)
+            ws = torch.empty(lib.mfl_relu_dropout_colsum_workspace_bytes(rows, cols), dtype=torch.uint8,
+                             device=out.device)
+            rc = lib.mfl_relu_dropout_backward_colsum(dy.data_ptr(), out.data_ptr(), rows, cols, ctx.p_drop,
+                                                      int(ctx.dropped), dx.data_ptr(), colsum.data_ptr(), ws.data_ptr(),
+                                                      _native.stream_handle(out.device))
+        else:
+            colsum = None
+            rc = lib.mfl_relu_dropout_backward(dy.data_ptr(), out.data_ptr(), out.numel(), ctx.p_drop,
+                                               int(ctx.dropped), dx.data_ptr(), _native.stream_handle(out.device))
         if rc != 0:
             raise RuntimeError(lib.mfl_relu_dropout_last_error().decode())
+        _attach_colsum(dx, colsum)
         return dx, None, None
 
 

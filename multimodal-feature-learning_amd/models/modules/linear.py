@@ -47,10 +47,11 @@ class _WgradQueue:
 
     def __init__(self, deliver):
         self.deliver = deliver
-        self.entries = []  # (dY (K, N), X (K, C), weight param, row offset, bias param or None)
+        # (dY (K, N), X (K, C), weight param, row offset, bias param or None, dY's column sums or None)
+        self.entries = []
 
-    def push(self, g2, x2, weight, row, bias):
-        self.entries.append((g2, x2, weight, row, bias))
+    def push(self, g2, x2, weight, row, bias, colsum=None):
+        self.entries.append((g2, x2, weight, row, bias, colsum))
 
     @torch.no_grad()
     def flush(self):
@@ -71,12 +72,14 @@ class _WgradQueue:
                 dw = torch.bmm(gs.transpose(1, 2), xs, out_dtype=torch.float32)
             else:  # (CPU unit tests of the queue: no 16-bit-in / fp32-out GEMM there)
                 dw = torch.bmm(gs.transpose(1, 2).float(), xs.float())
-            with_bias = [k for k, e in enumerate(es) if e[4] is not None]
-            db = gs.sum(1, dtype=torch.float32) if with_bias else None
-            for k, (_, _, w, row, b) in enumerate(es):
+            # bias gradients: the column sums handed over with dY (add_norm: the add + LayerNorm
+            # backward that produced dY summed them), else one reduction for the group
+            need = any(e[4] is not None and e[5] is None for e in es)
+            db = gs.sum(1, dtype=torch.float32) if need else None
+            for k, (_, _, w, row, b, cs) in enumerate(es):
                 parts.setdefault(w, []).append((row, dw[k]))
                 if b is not None:
-                    parts.setdefault(b, []).append((row, db[k]))
+                    parts.setdefault(b, []).append((row, cs if cs is not None else db[k]))
         for prm, ps in parts.items():
             ps.sort(key=lambda rp: rp[0])
             rows = [r for r, _ in ps]
@@ -108,8 +111,8 @@ def deferred_weight_grads(deliver):
 
 
 def _defer(*entries):
-    """Queue the (dY, X, weight, row offset, bias) products of one backward when a queue is active
-    and every K is short — all of them or none; True if queued."""
+    """Queue the (dY, X, weight, row offset, bias[, dY column sums]) products of one backward when a
+    queue is active and every K is short — all of them or none; True if queued."""
     q = _queue
     if q is None or any(e[0].shape[0] > DEFER_MAX_ROWS or e[2].dtype != torch.float32 for e in entries):
         return False
@@ -266,6 +269,19 @@ def _claim(param):
     return v.view_as(v)  # a fresh view object: autograd adopts it as .grad instead of cloning
 
 
+def _given_colsum(gy, n):
+    """The fp32 column sums handed over with the output gradient ``gy`` (add_norm._attach_colsum:
+    the fused add + LayerNorm backward that produced it summed them), or None — also when gy was
+    modified in place since (its version counter moved) or the shape does not match."""
+    t = getattr(gy, "_mfl_colsum", None)
+    if t is None:
+        return None
+    cs, ver = t
+    if ver != gy._version or tuple(cs.shape) != (n,):
+        return None
+    return cs
+
+
 def _bias_grad(g2, out=None):
     """fp32 column sum of dY (K, N) through mfl_colsum (one streaming pass, fixed order);
     torch's column reduction where the kernel's layout conditions do not hold.  ``out``: an fp32
@@ -341,17 +357,19 @@ class _AutocastLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gy):
         x2, wc = ctx.saved_tensors
+        cs = _given_colsum(gy, wc.shape[0]) if ctx.has_bias else None
         g2 = gy.reshape(-1, gy.shape[-1]).to(wc.dtype)
         gx = gw = gb = None
         nig = ctx.needs_input_grad
         if nig[0]:
             gx = _mm_nn(g2, wc).view(ctx.x_shape)
-        if nig[1] and (not ctx.has_bias or nig[2]) and _defer((g2, x2, ctx.weight, 0, ctx.bias if ctx.has_bias else None)):
+        if nig[1] and (not ctx.has_bias or nig[2]) and _defer((g2, x2, ctx.weight, 0, ctx.bias if ctx.has_bias else None,
+                                                                cs)):
             return gx, None, None, None, None
         if nig[1]:
             gw = _weight_grad(g2, x2, _claim(ctx.weight))
         if ctx.has_bias and nig[2]:
-            gb = _bias_grad(g2, _claim(ctx.bias))
+            gb = cs if cs is not None else _bias_grad(g2, _claim(ctx.bias))
         return gx, gw, gb, None, None
 
 

@@ -424,3 +424,50 @@ def test_decoder_self_attention_carry_matches_uncarried(dev, monkeypatch):
     assert len(g1) == len(g2)
     for a, b in zip(g1, g2):
         torch.testing.assert_close(a, b, rtol=1e-3, atol=1e-3 * b.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,d", [(15360, 512), (800, 512), (37, 1024)])
+def test_backward_ex2_dy_colsum_and_pos_accumulation(dev, rows, d):
+    """mfl_add_layernorm_backward_ex2: dy_colsum = the column sums of dy as stored (the producing
+    Linear's bias gradient, handed to it by add_norm._attach_colsum) and dpos_accumulate adds dq16 into
+    dpos (a pos shared by several layers: add_norm.pos_sink) — the other outputs as the _ex entry's."""
+    lib = PKG._native.load_library()
+    torch.manual_seed(3)
+    norm = torch.nn.LayerNorm(d).to(dev)
+    r = torch.randn(rows, d, device=dev)
+    y = torch.randn(rows, d, device=dev).bfloat16()
+    dout = torch.randn(rows, d, device=dev)
+    dq16 = torch.randn(rows, d, device=dev).bfloat16()
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    out = torch.empty(rows, d, device=dev)
+    sh = PKG._native.stream_handle(dev)
+    assert lib.mfl_add_layernorm_forward(r.data_ptr(), 0, y.data_ptr(), 2, norm.weight.data_ptr(), norm.bias.data_ptr(),
+                                         rows, d, norm.eps, out.data_ptr(), mean.data_ptr(), rstd.data_ptr(), sh) == 0
+    ws = torch.empty(lib.mfl_add_layernorm_workspace_bytes(rows, d), dtype=torch.uint8, device=dev)
+
+    def call(fn_ex2, dpos, acc, colsum):
+        dr, dy = torch.empty_like(r), torch.empty_like(y)
+        dw, db = torch.empty(d, device=dev), torch.empty(d, device=dev)
+        args = (dout.data_ptr(), None, dq16.data_ptr(), r.data_ptr(), 0, y.data_ptr(), 2, norm.weight.data_ptr(),
+                mean.data_ptr(), rstd.data_ptr(), rows, d, dr.data_ptr(), dy.data_ptr(), dw.data_ptr(), db.data_ptr(),
+                dpos.data_ptr())
+        if fn_ex2:
+            rc = lib.mfl_add_layernorm_backward_ex2(*args, acc, None if colsum is None else colsum.data_ptr(), 0.0,
+                                                    None, ws.data_ptr(), sh)
+        else:
+            rc = lib.mfl_add_layernorm_backward_ex(*args, 0.0, None, ws.data_ptr(), sh)
+        assert rc == 0, lib.mfl_add_layernorm_last_error()
+        return dr, dy, dw, db
+
+    dpos_ref = torch.empty(rows, d, device=dev)
+    ref = call(False, dpos_ref, 0, None)
+    dpos = torch.full((rows, d), 0.25, device=dev)
+    colsum = torch.empty(d, device=dev)
+    got = call(True, dpos, 1, colsum)
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+    torch.testing.assert_close(dpos, dq16.float() + 0.25, rtol=0, atol=0)
+    want = got[1].double().sum(0)
+    torch.testing.assert_close(colsum.double(), want, rtol=1e-5, atol=1e-5 * want.abs().max().item())

@@ -115,3 +115,35 @@ def test_graph_replays_draw_fresh_masks(dev):
         assert abs(m.float().mean().item() - 0.9) < 0.01
     assert (masks[0] != masks[1]).float().mean().item() > 0.1  # independent masks differ in ~18 %
     assert not torch.equal(norms[0], norms[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rows,cols", [(15360, 2048), (800, 2048), (37, 1024)])
+def test_backward_hands_over_column_sums(dev, rows, cols):
+    """The backward writes dx and its column sums in one pass (mfl_relu_dropout_backward_colsum) and
+    hands them to the Linear that produced h (linear1's bias gradient, linear._given_colsum): dx equal
+    to the plain kernel's, the sums equal to dx's fp64 column sums to fp32 rounding; the Linear's bias
+    gradient through them equals the one from its own column-sum pass."""
+    torch.manual_seed(5)
+    drop = torch.nn.Dropout(0.1).train()
+    lin = PKG.models.modules.linear.Linear(256, cols).to(dev)
+    x = torch.randn(rows, 256, device=dev)
+    dy = torch.randn(rows, cols, device=dev).bfloat16()
+    seed = torch.randint(0, 2 ** 62, (1,), device=dev, dtype=torch.int64)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        h = lin(x)
+    out = FF._ReluDropout.apply(h, 0.1, seed)
+    out.backward(dy)
+    g1 = lin.bias.grad.clone()
+    dx = torch.empty_like(out)
+    lib = PKG._native.load_library()
+    assert lib.mfl_relu_dropout_backward(dy.data_ptr(), out.data_ptr(), out.numel(), 0.1, 1, dx.data_ptr(),
+                                         PKG._native.stream_handle(dev)) == 0
+    want = dx.double().sum(0)
+    torch.testing.assert_close(g1.double(), want, rtol=1e-5, atol=1e-5 * want.abs().max().item())
+    lin.bias.grad = None
+    PKG.models.modules.linear._AutocastLinear.backward  # (the consumer: _given_colsum)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        h2 = lin(x)
+    h2.backward(dx)  # no handed-over sums: the Linear's own column-sum pass
+    torch.testing.assert_close(lin.bias.grad.double(), want, rtol=1e-5, atol=1e-5 * want.abs().max().item())

@@ -533,17 +533,17 @@ LM_CASES = [
     ([1024, 512, 256, 128],    8, 8, 4),   # the bench's encoder call
     ([1000, 500, 250, 125],    8, 8, 4),   # ragged: T not a multiple of 16, Lq not of 32
     ([1000, 500, 250, 125],    8, 8, 2),
-    ([2048, 1024, 512],        2, 16, 1),
+    ([2048, 1024, 512, 256],   2, 16, 1),
 ]
 
 
 @pytest.mark.parametrize("padding", ["border", "zeros"])
 @pytest.mark.parametrize("case", range(len(LM_CASES)))
-def test_persistent_level_major_backward_equals_per_block_kernel(dev, monkeypatch, case, padding):
-    """win_lm_kernel (persistent waves over per-XCD queues in the tiles buffer's tail) gives the
-    per-block row kernel's gradients bit for bit (same visits in the same order, same MFMA
-    products), and its queues reset themselves: three backwards on one forward's tiles agree, and
-    the queue words are zero afterwards."""
+def test_level_major_row_kernel_equals_per_block_kernel(dev, monkeypatch, case, padding):
+    """win_lm_kernel (the level-major row-block backward: swizzled LDS rows, reordered phases, the
+    tile order read from the tiles tail) gives win_bwd_kernel's gradients bit for bit (same visits in
+    the same order, same MFMA products); three backwards on one forward's tiles agree, and the
+    tail's reserved words stay zero."""
     for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH", "MSDA_HIP_QORDER",
               "MSDA_HIP_WIN_LM"):
         monkeypatch.delenv(k, raising=False)
@@ -554,8 +554,8 @@ def test_persistent_level_major_backward_equals_per_block_kernel(dev, monkeypatc
     starts = O.level_starts(shapes)
     v, g = value.cuda(), gout.cuda()
     lcm, am = _to_level_major(loc).cuda(), _to_level_major(aw).cuda()
-    assert msda.level_major_ok(v, shapes, Lq, P)
     _, tiles = msda.msda_forward(v, shapes, starts, lcm, am, padding, want_tiles=True, layout=msda.LEVEL_MAJOR)
+    assert tiles is not None
     runs = [msda.msda_backward(v, shapes, starts, lcm, am, g, padding, tiles=tiles, layout=msda.LEVEL_MAJOR)
             for _ in range(3)]
     n_iv = B * M * len(shapes) * ((Lq + 31) // 32) * 8

@@ -132,8 +132,12 @@ def test_sparse_encoder_carry_matches_plain_bf16(dev, monkeypatch):
     (``DeformableTransformerEncoderLayer.forward_carry``: bf16(tgt + pos) and bf16(tgt) from the
     fused add + LayerNorm, the whole memory's bf16 copy kept up to date by the same scatter as the
     fp32 memory).  Against the plain layer path (MFL_SPARSE_CARRY=0) on padded clips (per-clip
-    top-k counts: the keep masks): the forward is the same arithmetic, bit for bit; gradients are
-    the same terms summed in another order (fp32), within 1e-2 relative."""
+    top-k counts: the keep masks): the forward is the same arithmetic, bit for bit.  Gradients are
+    the same terms summed in another order (fp32), so each is held to the fp64 run of the same model:
+    within 2e-3 relative of the plain path's gradient, or — for a gradient whose sum cancels (the
+    BaseEncoder's biases: a sum over every token) — no further from the fp64 gradient than 1.5x the
+    plain path's own distance + 2e-3."""
+    import copy
     torch.manual_seed(0)
     core = PKG.dvc_core.SparseDVCCore(d_model=256, num_queries=10, feature_dim=256, num_heads=4, enc_layers=3,
                                       dec_layers=2, ff_dim=512, dropout=0.0).to(dev)
@@ -148,11 +152,29 @@ def test_sparse_encoder_carry_matches_plain_bf16(dev, monkeypatch):
         loss.backward()
         res.append(([out[k].detach().float().clone() for k in ("memory", "hs", "all_segments", "all_counts")],
                     {n: p.grad.detach().clone() for n, p in core.named_parameters() if p.grad is not None}))
+    core64 = copy.deepcopy(core).double()
+    core64.zero_grad(set_to_none=True)
+    torch.set_default_dtype(torch.float64)  # (tensors the model allocates with the default dtype)
+    try:
+        PKG.dvc_core.sparse_workload_loss(core64(video.double(), mask, dur.double())).backward()
+    finally:
+        torch.set_default_dtype(torch.float32)
+    g64 = {n: p.grad.detach() for n, p in core64.named_parameters() if p.grad is not None}
     (fa, ga), (fb, gb) = res
     for x, y in zip(fa, fb):
         assert torch.equal(x, y)
     assert ga.keys() == gb.keys() and len(ga) > 20
-    errs = {n: ((ga[n] - gb[n]).norm() / gb[n].norm().clamp_min(1e-30)).item() for n in ga}
-    worst = sorted(errs.items(), key=lambda kv: -kv[1])[:5]
-    print("carry vs plain, largest relative gradient differences:", worst)
-    assert worst[0][1] < 2e-3, worst
+
+    def rel(a, b):
+        return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+
+    rows, bad = [], []
+    for n in ga:
+        d_ab = rel(ga[n], gb[n])
+        e_a, e_b = rel(ga[n], g64[n]), rel(gb[n], g64[n])
+        rows.append((n, round(d_ab, 5), round(e_a, 5), round(e_b, 5)))
+        if d_ab >= 2e-3 and e_a > 1.5 * e_b + 2e-3:
+            bad.append(rows[-1])
+    print("carry vs plain (name, difference, carry vs fp64, plain vs fp64), largest:",
+          sorted(rows, key=lambda r: -r[1])[:6])
+    assert not bad, bad

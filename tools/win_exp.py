@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--fwd-lds", default="0", help="MSDA_HIP_FWD_LDS values to time")
     ap.add_argument("--fwd-stage", default="1,2,0", help="MSDA_HIP_FWD_STAGE values (per-wave staged forward) to time")
     ap.add_argument("--lm", default="1,0", help="MSDA_HIP_WIN_LM values (persistent level-major kernel) to time")
+    ap.add_argument("--lm-modes", default="0", help="MSDA_HIP_WIN_LM_MODE values (0 queue, 1 static, 2 one block a WG)")
     args = ap.parse_args()
     os.environ["MSDA_HIP_PROFILING"] = "1"  # (MSDA_HIP_WIN_EXP is refused without it)
     dev = torch.device("cuda", 0)
@@ -55,17 +56,20 @@ def main():
             _, tiles_m = msda.msda_forward(value, shapes, starts, loc_m, aw_m, want_tiles=True, layout=lm)
             for flag in args.lm.split(","):
                 os.environ["MSDA_HIP_WIN_LM"] = flag
-                us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc_m, aw_m, gout, tiles=tiles_m,
-                                                       layout=lm), args.iters)
-                print(json.dumps({**tag, "kernel": "bwd_win_level_major", "lm": int(flag), "us": round(us, 2)}),
-                      flush=True)
+                for mode in (args.lm_modes.split(",") if flag == "1" else ["-"]):
+                    os.environ["MSDA_HIP_WIN_LM_MODE"] = mode if mode != "-" else "0"
+                    us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc_m, aw_m, gout, tiles=tiles_m,
+                                                           layout=lm), args.iters)
+                    print(json.dumps({**tag, "kernel": "bwd_win_level_major", "lm": int(flag), "mode": mode,
+                                      "us": round(us, 2)}), flush=True)
             os.environ.pop("MSDA_HIP_WIN_LM", None)
+            os.environ.pop("MSDA_HIP_WIN_LM_MODE", None)
             for e in args.exps.split(","):
                 os.environ["MSDA_HIP_WIN_EXP"] = e
                 us = timeit(lambda: msda.msda_backward(value, shapes, starts, loc, aw, gout, tiles=tiles), args.iters)
                 print(json.dumps({**tag, "kernel": "bwd_win", "exp": int(e), "us": round(us, 2)}), flush=True)
-            os.environ["MSDA_HIP_WIN_EXP"] = "0"
-        os.environ["MSDA_HIP_WIN_EXP"] = "0"
+            os.environ.pop("MSDA_HIP_WIN_EXP", None)
+        os.environ.pop("MSDA_HIP_WIN_EXP", None)
 
 
 if __name__ == "__main__":
