@@ -94,6 +94,7 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_bwd(const uint4* __rest
 // column-sum pass over dx.  One block = kRdRows rows x 256 vectors of 8 columns; per-block column
 // partials in fixed order, summed by relu_dropout_colsum_final in fixed order (deterministic).
 constexpr int kRdRows = 32;
+constexpr int kRdUnroll = 8;  // rows whose loads are in flight together (one dependent row at a time: 2x slower)
 
 __global__ __launch_bounds__(kThreads) void relu_dropout_bwd_colsum(const uint4* __restrict__ dy,
                                                                    const uint4* __restrict__ out, long long rows,
@@ -102,44 +103,66 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_bwd_colsum(const uint4*
   const int c = blockIdx.y * kThreads + threadIdx.x;
   if (c >= cvec) return;
   const long long r0 = (long long)blockIdx.x * kRdRows;
+  // (the last block's rows past the end re-read its last row and add nothing: branch-free loads, so
+  // the compiler keeps kRdUnroll rows of loads in flight — with guarded loads it waited on each)
+  const int nr = (int)min((long long)kRdRows, rows - r0);
   float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int rr = 0; rr < kRdRows; ++rr) {
-    const long long row = r0 + rr;
-    if (row >= rows) break;
-    const long long i = row * cvec + c;
-    const uint4 g = dy[i], y = out[i];
-    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, yw[4] = {y.x, y.y, y.z, y.w};
-    uint32_t o[4];
+  const uint4* __restrict__ dyc = dy + r0 * cvec + c;
+  const uint4* __restrict__ outc = out + r0 * cvec + c;
+  uint4* __restrict__ dxc = dx + r0 * cvec + c;
+  for (int rr = 0; rr < kRdRows; rr += kRdUnroll) {
+    uint4 g[kRdUnroll], y[kRdUnroll];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const float a = !(lo(yw[j]) <= 0.f) ? lo(gw[j]) * scale : 0.f;
-      const float b = !(hi(yw[j]) <= 0.f) ? hi(gw[j]) * scale : 0.f;
-      o[j] = rne(a) | (rne(b) << 16);
-      sum[2 * j] += lo(o[j]);
-      sum[2 * j + 1] += hi(o[j]);
+    for (int u = 0; u < kRdUnroll; ++u) {
+      const int rw = min(rr + u, nr - 1);
+      g[u] = dyc[(long long)rw * cvec];
+      y[u] = outc[(long long)rw * cvec];
     }
-    dx[i] = make_uint4(o[0], o[1], o[2], o[3]);
+#pragma unroll
+    for (int u = 0; u < kRdUnroll; ++u) {
+      const bool live = rr + u < nr;
+      const uint32_t gw[4] = {g[u].x, g[u].y, g[u].z, g[u].w}, yw[4] = {y[u].x, y[u].y, y[u].z, y[u].w};
+      uint32_t o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float a = !(lo(yw[j]) <= 0.f) ? lo(gw[j]) * scale : 0.f;
+        const float b = !(hi(yw[j]) <= 0.f) ? hi(gw[j]) * scale : 0.f;
+        o[j] = rne(a) | (rne(b) << 16);
+        sum[2 * j] += live ? lo(o[j]) : 0.f;
+        sum[2 * j + 1] += live ? hi(o[j]) : 0.f;
+      }
+      if (live) dxc[(long long)(rr + u) * cvec] = make_uint4(o[0], o[1], o[2], o[3]);
+    }
   }
   float4* pp = reinterpret_cast<float4*>(part + (long long)blockIdx.x * cvec * 8 + (long long)c * 8);
   pp[0] = make_float4(sum[0], sum[1], sum[2], sum[3]);
   pp[1] = make_float4(sum[4], sum[5], sum[6], sum[7]);
 }
 
-// colsum[j] = sum over the row groups' partials (four independent chains, fixed order)
-__global__ __launch_bounds__(kThreads) void relu_dropout_colsum_final(const float* __restrict__ part, int ngroups,
-                                                                     int cols, float* __restrict__ colsum) {
-  const int j = blockIdx.x * kThreads + threadIdx.x;
-  if (j >= cols) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  int k = 0;
-  for (; k + 3 < ngroups; k += 4) {
-    s0 += part[(long long)k * cols + j];
-    s1 += part[(long long)(k + 1) * cols + j];
-    s2 += part[(long long)(k + 2) * cols + j];
-    s3 += part[(long long)(k + 3) * cols + j];
+// colsum[j] = sum over the row groups' partials: a block = 16 row strides x 64 columns (the row
+// groups dealt over the 16, two independent chains each, then the 16 added in LDS; fixed order)
+__global__ __launch_bounds__(1024) void relu_dropout_colsum_final(const float* __restrict__ part, int ngroups,
+                                                                 int cols, float* __restrict__ colsum) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + cl;
+  float s0 = 0.f, s1 = 0.f;
+  if (j < cols) {
+    int k = grp;
+    for (; k + 16 < ngroups; k += 32) {
+      s0 += part[(long long)k * cols + j];
+      s1 += part[(long long)(k + 16) * cols + j];
+    }
+    for (; k < ngroups; k += 16) s0 += part[(long long)k * cols + j];
   }
-  for (; k < ngroups; ++k) s0 += part[(long long)k * cols + j];
-  colsum[j] = (s0 + s1) + (s2 + s3);
+  red[grp][cl] = s0 + s1;
+  __syncthreads();
+  if (grp == 0 && j < cols) {
+    float t = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) t += red[i][cl];
+    colsum[j] = t;
+  }
 }
 
 // value.masked_fill(padding_mask[..., None], 0) of MSDeformAttn (reference attention.py:462-463) in
@@ -307,8 +330,8 @@ int mfl_relu_dropout_backward_colsum(const void* dy, const void* out, int64_t ro
     int rc;
     if ((rc = status("backward (column sums)"))) return rc;
   }
-  hipLaunchKernelGGL(relu_dropout_colsum_final, dim3((unsigned)((cols + kThreads - 1) / kThreads)), dim3(kThreads), 0,
-                     st, static_cast<const float*>(workspace), (int)groups, (int)cols, colsum);
+  hipLaunchKernelGGL(relu_dropout_colsum_final, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st,
+                     static_cast<const float*>(workspace), (int)groups, (int)cols, colsum);
   return status("backward (column sums, final)");
 }
 

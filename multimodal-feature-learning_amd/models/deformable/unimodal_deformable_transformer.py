@@ -316,6 +316,17 @@ class DeformableTransformerDecoder(nn.Module):
         self.return_intermediate = return_intermediate
         self.bbox_head = None
 
+    def flat_groups(self):
+        """Parameters a flat-buffer trainer should lay out back to back (train_step._flat_order): each
+        same-shape weight / bias of the layers, so that the layers' batched gradient GEMMs (the
+        deferred short-K queue, value_proj.layer_values) write one view of the flat gradient buffer."""
+        layers = [layer for layer in self.layers if type(layer) is DeformableTransformerDecoderLayer]
+        if len(layers) < 2:
+            return []
+        names = ("linear1.weight", "linear2.weight", "self_attn.out_proj.weight", "cross_attn.value_proj.weight",
+                 "cross_attn.value_proj.bias", "cross_attn.output_proj.weight")
+        return [tuple(layer.get_parameter(n) for layer in layers) for n in names]
+
     def forward(self, tgt, reference_points, src, src_temporal_shapes, src_level_start_index, src_valid_ratios,
                 query_pos=None, src_padding_mask=None, query_padding_mask=None, disable_iterative_refine=False):
         # the decoder's batched weight gradients are computed once the query's gradient is (the

@@ -39,7 +39,11 @@ from torch import nn
 __all__ = ["Linear", "split_k_chunks", "linear_pair", "deferred_weight_grads", "flush_point",
            "flat_grad_destinations", "small_addmm", "small_mm_nn"]
 
-DEFER_MAX_ROWS = 4096  # GEMM K (input rows) up to which weight gradients are queued and batched
+# GEMM K (input rows) up to which weight gradients are queued and batched: the decoder's 800 query
+# rows (each GEMM too small for the chip).  Not the caption decoder's ~3,200 word tokens (DVC step):
+# their GEMMs fill the chip alone, and batching them stacked every dY and X (~300 MB of copies a
+# step, tools/op_census.py --config dvc) and handed the gradients over as fresh tensors to copy.
+DEFER_MAX_ROWS = 1024
 
 
 class _WgradQueue:
@@ -66,9 +70,19 @@ class _WgradQueue:
         _trace.hit("wgrad_batched", len(entries))
         parts = {}  # param -> [(row offset, fp32 grad rows)]
         for (_, n_out, _, _), es in groups.items():
+            # whole weights of one shape laid out back to back in the trainer's flat gradient buffer
+            # (flat_groups, e.g. the decoder layers' linear1): the batched GEMM writes their gradients
+            # straight into that one view (no fresh tensors to copy into the buffer afterwards)
+            dest = None
+            if len(es) > 1 and es[0][0].is_cuda and all(e[3] == 0 and e[0].shape[1] == e[2].shape[0] for e in es):
+                es = sorted(es, key=lambda e: _dest_offset(e[2]))
+                dest = _claim_group([e[2] for e in es])
             gs = es[0][0][None] if len(es) == 1 else torch.stack([e[0] for e in es])
             xs = es[0][1][None] if len(es) == 1 else torch.stack([e[1] for e in es])
-            if gs.is_cuda:  # fp32 accumulate and output
+            if dest is not None:
+                dw = torch.bmm(gs.transpose(1, 2), xs, out_dtype=torch.float32,
+                               out=dest.view(len(es), gs.shape[2], xs.shape[2]))
+            elif gs.is_cuda:  # fp32 accumulate and output
                 dw = torch.bmm(gs.transpose(1, 2), xs, out_dtype=torch.float32)
             else:  # (CPU unit tests of the queue: no 16-bit-in / fp32-out GEMM there)
                 dw = torch.bmm(gs.transpose(1, 2).float(), xs.float())
@@ -280,6 +294,39 @@ def _given_colsum(gy, n):
     if ver != gy._version or tuple(cs.shape) != (n,):
         return None
     return cs
+
+
+def _dest_offset(param):
+    """Offset of param's flat gradient view (for ordering a group), or -1."""
+    d = _dest
+    v = None if d is None else d["views"].get(id(param))
+    return -1 if v is None else v.storage_offset()
+
+
+def _claim_group(params):
+    """One view of the flat gradient buffer covering the given parameters' gradient views, when they
+    lie back to back in this order (the trainer's flat_groups layout; stacked along dim 0), claimed for
+    all of them — or None, and nothing claimed (see _claim)."""
+    d = _dest
+    if d is None or len(params) < 2:
+        return None
+    views = [d["views"].get(id(p)) for p in params]
+    if any(v is None for v in views) or len({id(p) for p in params}) != len(params):
+        return None
+    if any(p.grad is not None or id(p) in d["claimed"] for p in params):
+        return None
+    if d["may_claim"] is not None and not all(d["may_claim"](p) for p in params):
+        return None
+    base, off = views[0], views[0].storage_offset()
+    for v in views:
+        if (v.storage_offset() != off or not v.is_contiguous() or v.shape[1:] != base.shape[1:]
+                or v.untyped_storage().data_ptr() != base.untyped_storage().data_ptr()):
+            return None
+        off += v.numel()
+    for p in params:
+        d["claimed"].add(id(p))
+    rows = sum(v.shape[0] for v in views)
+    return base.new_empty(0).set_(base.untyped_storage(), base.storage_offset(), (rows,) + tuple(base.shape[1:]))
 
 
 def _bias_grad(g2, out=None):

@@ -20,7 +20,7 @@ fp32-accumulated product + bias, as the reference's addmm):
 import torch
 from torch.autograd import Function
 
-from .linear import Linear, _bias_grad, _weight_grad
+from .linear import Linear, _bias_grad, _claim_group, _weight_grad
 
 __all__ = ["layer_values", "layer_values_supported", "linear_group", "linear_group_supported"]
 
@@ -62,6 +62,7 @@ class _LayerValues(Function):
             _zero_rows(y, n, k, mask)
         ctx.save_for_backward(x16, torch.cat(wcs, 0), mask)
         ctx.n, ctx.x_shape, ctx.x_dtype, ctx.c_out = n, x.shape, x.dtype, c_out
+        ctx.params = (w, b)  # (the parameters whose flat gradient views the backward may claim)
         return tuple(torch.ops.aten._unsafe_view(y[i], (*lead, c_out)) for i in range(n))
 
     @staticmethod
@@ -76,11 +77,14 @@ class _LayerValues(Function):
         nig = ctx.needs_input_grad
         dx = torch.mm(g, wcat).view(ctx.x_shape).to(ctx.x_dtype) if nig[0] else None
         dws = dbs = (None,) * n
+        ws, bs = ctx.params
+        # the n layers' weights (biases) back to back in the trainer's flat gradient buffer
+        # (flat_groups): the split-K sum (column sums) written straight into that one view
         if any(nig[3:3 + n]):
-            dw = _weight_grad(g, x16)
+            dw = _weight_grad(g, x16, _claim_group(ws) if all(nig[3:3 + n]) else None)
             dws = tuple(dw[i * c_out:(i + 1) * c_out] for i in range(n))
         if any(nig[3 + n:3 + 2 * n]):
-            db = _bias_grad(g)
+            db = _bias_grad(g, _claim_group(bs) if all(nig[3 + n:3 + 2 * n]) else None)
             dbs = tuple(db[i * c_out:(i + 1) * c_out] for i in range(n))
         return (dx, None, None) + dws + dbs + (None,) * (2 * n)
 

@@ -1237,6 +1237,8 @@ def dvc256_args():
     return detr, caption, matcher
 
 
+DVC256_MIN_MARGIN = 0.1
+
 # the last segment-head layer scaled up: spread-out proposals, so every matching is far from a tie
 DVC256_SCALE = {"segment_embedding.0.layers.2.weight": 6.0}
 
@@ -1259,7 +1261,8 @@ def deformable_dvc_bf16_d256_case(ref):
     torch.autocast('cpu', bfloat16) (the reference's own bf16 run), with deformable_dvc_f64's one
     argument-order fix of the caption-decoder call.  Parameters from regen_parameters (no state_dict
     stored).  The seed is the first from DVC256['seed'] on at which the bf16 run matches the same
-    (clip, prediction) pairs as fp64 on every decoder level; the GPU test runs the step on those
+    (clip, prediction) pairs as fp64 on every decoder level with a matching-cost margin of at least
+    DVC256_MIN_MARGIN (so our bf16 forward must give that matching too); the GPU test runs the step on those
     pairs (the matching's own arithmetic is pinned in fp64 by deformable_dvc_f64).  The matching
     costs' smallest margin (cost increase when one matched pair is forbidden) is stored."""
     import copy
@@ -1295,7 +1298,7 @@ def deformable_dvc_bf16_d256_case(ref):
                     indices_aux=[[torch.stack(list(t)) for t in lv] for lv in indices_aux],
                     grads=sampled_grads({"dvc": model}))
 
-    for attempt in range(12):
+    for attempt in range(60):
         seed = DVC256["seed"] + attempt
         torch.manual_seed(seed)
         model = build()
@@ -1317,7 +1320,9 @@ def deformable_dvc_bf16_d256_case(ref):
         same = all(torch.equal(a, b) for a, b in zip(truth["indices"], bf16["indices"])) and all(
             torch.equal(a, b) for la, lb in zip(truth["indices_aux"], bf16["indices_aux"]) for a, b in zip(la, lb))
         print(f"dvc256 seed {seed}: bf16 matching == fp64: {same}; smallest cost margin {margin:.4f}")
-        if same:
+        # a margin well above the bf16 noise of the costs (~0.01 here): any bf16 implementation of the
+        # forward must then give the same matching (the GPU test asserts ours does)
+        if same and margin >= DVC256_MIN_MARGIN:
             break
     else:
         raise RuntimeError("no seed with the same matching in bf16 and fp64")

@@ -41,15 +41,16 @@ def nbytes(out):
 
 
 class Census(TorchDispatchMode):
-    def __init__(self, pkg_dir):
+    def __init__(self, pkg_dir, everything=False):
         super().__init__()
         self.pkg_dir = pkg_dir
+        self.everything = everything
         self.rows = collections.defaultdict(lambda: [0, 0])
 
     def __torch_dispatch__(self, func, types, args=(), kwargs=None):
         out = func(*args, **(kwargs or {}))
         name = str(func.overloadpacket.__name__)
-        if any(g in name for g in GLUE):
+        if self.everything or any(g in name for g in GLUE):
             fr = [f for f in traceback.extract_stack()[:-1] if self.pkg_dir in f.filename or "bench.py" in f.filename]
             where = " <- ".join(f"{os.path.relpath(f.filename, self.pkg_dir)}:{f.lineno}" for f in fr[::-1][:3])
             if not where:  # backward: the autograd node being run (accumulation adds run between nodes)
@@ -69,6 +70,7 @@ def main():
     ap.add_argument("--cpu", action="store_true", help="fp32 on the host (the autograd structure: accumulation adds, "
                                                        "selects; not the GPU fast paths)")
     ap.add_argument("--extra", default="", help="more bench.py arguments, e.g. '--batch 1 --T 256'")
+    ap.add_argument("--ops", default="", help="comma list: only these aten ops (e.g. sum,mean,norm)")
     a = ap.parse_args()
     sys.argv = [sys.argv[0], "--config", a.config, "--graph", "0", "--cpu-baseline", "0"] + a.extra.split()
     import bench
@@ -89,14 +91,16 @@ def main():
         trainer.step(batch)
     if not a.cpu:
         torch.cuda.synchronize()
-    c = Census(os.path.join(ROOT, "multimodal-feature-learning_amd"))
+    c = Census(os.path.join(ROOT, "multimodal-feature-learning_amd"), everything=bool(a.ops))
     with c:
         trainer.step(batch)
     if not a.cpu:
         torch.cuda.synchronize()
     tot_n = sum(v[0] for v in c.rows.values())
     print(f"{a.config}: {tot_n} glue ops in one step, {sum(v[1] for v in c.rows.values()) / 1e6:.1f} MB written")
-    for (name, s, where), (n, b) in sorted(c.rows.items(), key=lambda kv: -kv[1][1])[:a.top]:
+    keep = set(a.ops.split(",")) if a.ops else None
+    items = [kv for kv in c.rows.items() if keep is None or kv[0][0] in keep]
+    for (name, s, where), (n, b) in sorted(items, key=lambda kv: -kv[1][1])[:a.top]:
         print(f"{b / 1e6:8.2f} MB {n:4d}x  {name} {s[:110]}\n              {where}")
 
 
