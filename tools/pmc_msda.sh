@@ -1,11 +1,11 @@
 #!/bin/bash
 # rocprofv3 PMC passes over the MSDA kernels at the bench's call shapes (bf16, B=8, init
-# regime), one counter group per pass (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE do not
+# regime, level-major coordinates as the bench step runs them), one counter group per pass (MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE do not
 # fit one pass; no --pmc together with sys/runtime traces).  Summarised per kernel and grid
 # by tools/pmc_summary.py.
 set -u
 cd "${GRAFT_REPO_ROOT:-.}"; mkdir -p gpurun_out/pmc; export TMPDIR=/tmp
-ARGS=${MICRO_ARGS:-"--dtypes bf16 --regimes init --iters 3 --shapes enc --kernels fwd,bwd_all"}
+ARGS=${MICRO_ARGS:-"--dtypes bf16 --regimes init --iters 3 --shapes enc --kernels fwd,bwd_all --layout level_major"}
 run() { # name counters...
   local name=$1; shift
   rm -rf gpurun_out/pmc/$name

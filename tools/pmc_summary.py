@@ -50,9 +50,10 @@ def main(root):
 # pyramid, bf16; tools/pmc_msda.sh runs the encoder shape only, so one grid per kernel)
 CALL_KERNELS = {
     # the forward writes the row-block backward's tile intervals (msda_fwd16_tiles_kernel); the
-    # backward is the row-block MFMA kernel alone (msda_win.hip)
+    # backward is the row-block MFMA kernel alone (msda_win.hip): with the bench's level-major
+    # coordinates (MICRO_ARGS --layout level_major) the one-block-per-workgroup win_lm_kernel
     "msda_fwd_S1920_Lq1920": ("msda_fwd16_tiles_kernel",),
-    "msda_bwd_S1920_Lq1920": ("win_bwd_kernel",),
+    "msda_bwd_S1920_Lq1920": ("win_lm_kernel",),
 }
 
 
