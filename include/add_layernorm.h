@@ -70,6 +70,17 @@ int mfl_add_layernorm_backward_ex2(const float* dout, const uint16_t* dout16, co
                                    float* dbeta, float* dpos, int dpos_accumulate, float* dy_colsum, float p_drop,
                                    const int64_t* seed, void* workspace, void* stream);
 
+/* The carried operands of an encoder's first layer (n fp32 elements, n % 8 == 0, 16-byte aligned):
+ * v16 = bf16(src) (optional), q16 = bf16(src + pos) (pos optional: bf16(src)) — the layer's value
+ * projection input and query (reference with_pos_embed, unimodal_deformable_transformer.py:241,
+ * each cast by autocast at its Linear).  Backward: dsrc = dr + dv16 + dq16 (each optional, fp32
+ * sum), and dpos (optional) = dq16, or dpos += dq16 with dpos_accumulate (a shared pos's
+ * accumulator). */
+int mfl_carry_entry_forward(const float* src, const float* pos, int64_t n, uint16_t* v16, uint16_t* q16,
+                            void* stream);
+int mfl_carry_entry_backward(const float* dr, const uint16_t* dv16, const uint16_t* dq16, int64_t n, float* dsrc,
+                             float* dpos, int dpos_accumulate, void* stream);
+
 const char* mfl_add_layernorm_last_error(void);
 
 #ifdef __cplusplus

@@ -59,6 +59,21 @@ int mfl_gather_keep_backward(const void* grad, const int64_t* index, const void*
 int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t row_bytes, const uint8_t* mask,
                                  void* stream);
 
+/* The flattened level position embedding of prepare_encoder_inputs (reference
+ * models/deformable/unimodal_deformable_transformer.py:90-134, `torch.cat([pos_l.transpose(1, 2) +
+ * level_embed[l].view(1, 1, -1) for l], 1)`): out[b, start_l + t, c] = pos[l][b, c, t] +
+ * level_embed[l, c], fp32; pos: a host array of L device pointers to contiguous (B, N, T[l]) fp32
+ * tensors, out (B, sum T, N) contiguous, start_l the running sum of T.  1 <= L <= 16. */
+int mfl_level_pos_flatten(const float* const* pos, const int64_t* T, int64_t L, int64_t B, int64_t N,
+                          const float* level_embed, float* out, void* stream);
+
+/* Its backward for the level embedding: out[l, c] (+)= sum over b and t < T[l] of g[b, start_l + t, c]
+ * (g (B, sum T, N) fp32 contiguous, N % 4 == 0, 16-byte aligned; fixed summation order).
+ * accumulate != 0 adds into out.  workspace: mfl_level_colsum_workspace_bytes(T, L, B, N) bytes. */
+size_t mfl_level_colsum_workspace_bytes(const int64_t* T, int64_t L, int64_t B, int64_t N);
+int mfl_level_colsum(const float* g, const int64_t* T, int64_t L, int64_t B, int64_t N, float* out, int accumulate,
+                     void* workspace, void* stream);
+
 const char* mfl_relu_dropout_last_error(void);
 
 #ifdef __cplusplus

@@ -39,11 +39,20 @@ int flat_adamw_step(float* params, const float* grads, float* exp_avg, float* ex
  * workspace: mfl_colsum_workspace_bytes(K, N) bytes. */
 size_t mfl_colsum_workspace_bytes(int64_t K, int64_t N);
 int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void* workspace, void* stream);
+/* As mfl_colsum; accumulate != 0: out += the column sums (each sum formed first, then added). */
+int mfl_colsum_ex(const void* x, int dtype, int64_t K, int64_t N, float* out, int accumulate, void* workspace,
+                  void* stream);
 
 /* out[i] = sum over k < s of part[k * n + i] (fp32, chunk order): the split-K partial products of
  * the autocast Linear's weight gradient summed into the fp32 gradient.  n % 4 == 0, 16-byte
  * aligned pointers. */
 int mfl_sum_slabs(const float* part, int64_t s, int64_t n, float* out, void* stream);
+/* groups sums at once: out[g * n + i] = sum over k < s of part[(g * s + k) * n + i]; accumulate != 0:
+ * out[g * n + i] += that sum (formed first, then added: the accumulation of a finished gradient).
+ * The weight gradients of a layer used several times in one backward (a shared module, the
+ * trainer's flat gradient views; models/modules/linear.py). */
+int mfl_sum_slabs_ex(const float* part, int64_t groups, int64_t s, int64_t n, float* out, int accumulate,
+                     void* stream);
 
 /* Text of the last error of flat_adamw_step / mfl_colsum / mfl_sum_slabs on the calling thread. */
 const char* flat_adamw_last_error(void);

@@ -47,7 +47,9 @@ EXPORTED_SYMBOLS = (
     "flat_adamw_last_error",
     "mfl_colsum_workspace_bytes",
     "mfl_colsum",
+    "mfl_colsum_ex",
     "mfl_sum_slabs",
+    "mfl_sum_slabs_ex",
     # include/add_layernorm.h
     "mfl_add_layernorm_workspace_bytes",
     "mfl_add_layernorm_forward",
@@ -55,12 +57,17 @@ EXPORTED_SYMBOLS = (
     "mfl_add_layernorm_forward_ex",
     "mfl_add_layernorm_backward_ex",
     "mfl_add_layernorm_backward_ex2",
+    "mfl_carry_entry_forward",
+    "mfl_carry_entry_backward",
     "mfl_add_layernorm_last_error",
     # include/ffn_glue.h
     "mfl_relu_dropout_forward",
     "mfl_relu_dropout_backward",
     "mfl_relu_dropout_colsum_workspace_bytes",
     "mfl_relu_dropout_backward_colsum",
+    "mfl_level_pos_flatten",
+    "mfl_level_colsum_workspace_bytes",
+    "mfl_level_colsum",
     "mfl_relu_dropout_last_error",
     "mfl_zero_masked_rows",
     "mfl_zero_masked_rows_batched",
@@ -139,6 +146,10 @@ def _declare(lib):
     lib.mfl_sum_slabs.argtypes = [vp, i64, i64, vp, vp]
     lib.mfl_colsum.restype = i32
     lib.mfl_colsum.argtypes = [vp, i32, i64, i64, vp, vp, vp]
+    lib.mfl_colsum_ex.restype = i32
+    lib.mfl_colsum_ex.argtypes = [vp, i32, i64, i64, vp, i32, vp, vp]
+    lib.mfl_sum_slabs_ex.restype = i32
+    lib.mfl_sum_slabs_ex.argtypes = [vp, i64, i64, i64, vp, i32, vp]
     lib.mfl_add_layernorm_workspace_bytes.restype = ctypes.c_size_t
     lib.mfl_add_layernorm_workspace_bytes.argtypes = [i64, i64]
     lib.mfl_add_layernorm_forward.restype = i32
@@ -158,6 +169,16 @@ def _declare(lib):
     lib.mfl_gemm_nt_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
     lib.mfl_gather_keep_backward.restype = i32
     lib.mfl_gather_keep_backward.argtypes = [vp, vp, vp, i64, i64, i64, i64, vp, vp, vp]
+    lib.mfl_carry_entry_forward.restype = i32
+    lib.mfl_carry_entry_forward.argtypes = [vp, vp, i64, vp, vp, vp]
+    lib.mfl_carry_entry_backward.restype = i32
+    lib.mfl_carry_entry_backward.argtypes = [vp, vp, vp, i64, vp, vp, i32, vp]
+    lib.mfl_level_pos_flatten.restype = i32
+    lib.mfl_level_pos_flatten.argtypes = [vp, p64, i64, i64, i64, vp, vp, vp]
+    lib.mfl_level_colsum_workspace_bytes.restype = ctypes.c_size_t
+    lib.mfl_level_colsum_workspace_bytes.argtypes = [p64, i64, i64, i64]
+    lib.mfl_level_colsum.restype = i32
+    lib.mfl_level_colsum.argtypes = [vp, p64, i64, i64, i64, vp, i32, vp, vp]
     lib.mfl_gemm_nn_bf16.restype = i32
     lib.mfl_gemm_nn_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
     lib.mfl_gemm_last_error.restype = ctypes.c_char_p

@@ -312,6 +312,73 @@ __global__ __launch_bounds__(1024) void add_ln_param_final(const float* __restri
   }
 }
 
+// The carried operands of an encoder's first layer (models/modules/add_norm.py, carry_entry): the
+// layer reads src (fp32) as its residual, bf16(src) as the value projection's input and
+// bf16(src + pos) as the query (reference with_pos_embed, unimodal_deformable_transformer.py:241;
+// autocast casts each at its Linear).  One pass writes both bf16 copies; its backward sums the
+// three gradients of src in one pass (dr + dv16 + dq16, fp32) and dq16 into pos's gradient (or
+// its shared accumulator).  8 elements a thread.
+__global__ __launch_bounds__(256) void carry_entry_fwd(const float* __restrict__ src, const float* __restrict__ pos,
+                                                       long long n8, uint16_t* __restrict__ v16,
+                                                       uint16_t* __restrict__ q16) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long long)gridDim.x * 256) {
+    float a[4], b[4], pa[4], pb[4];
+    Vec4<float>::load(src + 8 * i, a);
+    Vec4<float>::load(src + 8 * i + 4, b);
+    if (v16) {
+      Vec4<uint16_t>::store(v16 + 8 * i, a);
+      Vec4<uint16_t>::store(v16 + 8 * i + 4, b);
+    }
+    if (pos) {
+      Vec4<float>::load(pos + 8 * i, pa);
+      Vec4<float>::load(pos + 8 * i + 4, pb);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        pa[k] = a[k] + pa[k];
+        pb[k] = b[k] + pb[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        pa[k] = a[k];
+        pb[k] = b[k];
+      }
+    }
+    Vec4<uint16_t>::store(q16 + 8 * i, pa);
+    Vec4<uint16_t>::store(q16 + 8 * i + 4, pb);
+  }
+}
+
+__global__ __launch_bounds__(256) void carry_entry_bwd(const float* __restrict__ dr, const uint16_t* __restrict__ dv16,
+                                                       const uint16_t* __restrict__ dq16, long long n4,
+                                                       float* __restrict__ dsrc, float* __restrict__ dpos,
+                                                       int dpos_accumulate) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float s[4] = {0.f, 0.f, 0.f, 0.f}, v[4], q[4] = {0.f, 0.f, 0.f, 0.f};
+    if (dr) Vec4<float>::load(dr + 4 * i, s);
+    if (dv16) {
+      Vec4<uint16_t>::load(dv16 + 4 * i, v);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] += v[k];
+    }
+    if (dq16) {
+      Vec4<uint16_t>::load(dq16 + 4 * i, q);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s[k] += q[k];
+    }
+    Vec4<float>::store(dsrc + 4 * i, s);
+    if (dpos) {
+      if (dpos_accumulate) {
+        float o[4];
+        Vec4<float>::load(dpos + 4 * i, o);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) q[k] = o[k] + q[k];
+      }
+      Vec4<float>::store(dpos + 4 * i, q);
+    }
+  }
+}
+
 int status(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -520,6 +587,38 @@ int mfl_add_layernorm_backward(const float* dout, const void* r, int r_dtype, co
   }
   return mfl_add_layernorm_backward_ex(dout, nullptr, nullptr, r, r_dtype, y, y_dtype, gamma, mean, rstd, rows, d, dr,
                                        dy, dgamma, dbeta, nullptr, 0.f, nullptr, workspace, stream);
+}
+
+int mfl_carry_entry_forward(const float* src, const float* pos, int64_t n, uint16_t* v16, uint16_t* q16,
+                            void* stream) {
+  g_err[0] = 0;
+  if (n < 0 || n % 8 || (n > 0 && (!src || !q16)) ||
+      (((uintptr_t)src | (uintptr_t)pos | (uintptr_t)v16 | (uintptr_t)q16) & 15u)) {
+    snprintf(g_err, sizeof(g_err), "mfl_carry_entry_forward: n %% 8 == 0 and 16-byte aligned buffers needed");
+    return 1;
+  }
+  if (n == 0) return 0;
+  const long long n8 = n / 8;
+  const unsigned blocks = (unsigned)std::min<long long>((n8 + 255) / 256, 8192);
+  hipLaunchKernelGGL(carry_entry_fwd, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), src, pos, n8,
+                     v16, q16);
+  return status("carry entry forward");
+}
+
+int mfl_carry_entry_backward(const float* dr, const uint16_t* dv16, const uint16_t* dq16, int64_t n, float* dsrc,
+                             float* dpos, int dpos_accumulate, void* stream) {
+  g_err[0] = 0;
+  if (n < 0 || n % 8 || (n > 0 && !dsrc) ||
+      (((uintptr_t)dr | (uintptr_t)dv16 | (uintptr_t)dq16 | (uintptr_t)dsrc | (uintptr_t)dpos) & 15u)) {
+    snprintf(g_err, sizeof(g_err), "mfl_carry_entry_backward: n %% 8 == 0 and 16-byte aligned buffers needed");
+    return 1;
+  }
+  if (n == 0) return 0;
+  const long long n4 = n / 4;
+  const unsigned blocks = (unsigned)std::min<long long>((n4 + 255) / 256, 8192);
+  hipLaunchKernelGGL(carry_entry_bwd, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), dr, dv16, dq16,
+                     n4, dsrc, dpos, dpos_accumulate);
+  return status("carry entry backward");
 }
 
 const char* mfl_add_layernorm_last_error(void) { return g_err; }

@@ -273,6 +273,126 @@ __global__ __launch_bounds__(256) void gather_keep_bwd_kernel(const uint16_t* __
   for (int j = threadIdx.x; j < d; j += 256) bpart[(long long)t * d + j] = red[0][j] + red[1][j] + red[2][j] + red[3][j];
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// The flattened level position embedding of prepare_encoder_inputs (reference
+// models/deformable/unimodal_deformable_transformer.py:90-134, also the multimodal and sparse
+// transformers): lvl_pos[b, start_l + t, :] = pos_l[b, :, t] + level_embed[l, :], and the level
+// embedding's gradient, the per-level column sums of lvl_pos's gradient.  ATen ran the forward as
+// four transposed adds and a cat (an extra pass over the (B, S, d) result), the backward as four
+// sum_to_size reductions (24-71 us each at the bench shape: a keep-last-dim reduction over 1-8 K
+// rows with 128 workgroups) plus a zero fill, copy and add per level.
+constexpr int kLpMaxL = 16;
+struct LevelTable {
+  const float* pos[kLpMaxL];
+  int T[kLpMaxL], start[kLpMaxL];
+  int blk0[kLpMaxL + 1];  // first workgroup / chunk of each level
+  int L, tiles_c;         // levels; 64-column tiles (flatten) or 256-column groups (colsum)
+};
+constexpr int kLpT = 32;  // positions per transpose tile
+// one workgroup a (level, b, 32 positions, 64 channels) tile: coalesced reads along t, LDS
+// transpose (33-float rows), coalesced writes along channels
+__global__ __launch_bounds__(256) void level_pos_flatten_kernel(const LevelTable tb, const float* __restrict__ emb,
+                                                                long long B, int N, long long S, float* __restrict__ out) {
+  __shared__ float tile[64][kLpT + 1];
+  int l = 0;
+  while (l + 1 < tb.L && (int)blockIdx.x >= tb.blk0[l + 1]) ++l;
+  const int j = (int)blockIdx.x - tb.blk0[l];
+  const int nt = (tb.T[l] + kLpT - 1) / kLpT;
+  const int ct = j % tb.tiles_c, tt = (j / tb.tiles_c) % nt;
+  const long long b = j / (tb.tiles_c * nt);
+  const int T = tb.T[l], c0 = ct * 64, t0 = tt * kLpT;
+  const float* __restrict__ pl = tb.pos[l] + b * (long long)N * T;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 t-lanes x 8 c-rows
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = c0 + ty + 8 * i, t = t0 + tx;
+    tile[ty + 8 * i][tx] = (c < N && t < T) ? pl[(long long)c * T + t] : 0.f;
+  }
+  __syncthreads();
+  const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;  // 64 c-lanes x 4 t-rows
+  const int c = c0 + cx;
+  const float e = c < N ? emb[(long long)l * N + c] : 0.f;
+  float* __restrict__ ob = out + (b * S + tb.start[l]) * (long long)N;
+#pragma unroll
+  for (int i = 0; i < kLpT / 4; ++i) {
+    const int tl = ry + 4 * i, t = t0 + tl;
+    if (c < N && t < T) ob[(long long)t * N + c] = tile[cx][tl] + e;
+  }
+}
+
+constexpr int kLcRows = 64;  // rows per colsum chunk (within one (level, b) segment)
+// partial column sums of one chunk: 64 column lanes (float4) x 4 row lanes, fixed order
+__global__ __launch_bounds__(256) void level_colsum_partial(const LevelTable tb, const float* __restrict__ g,
+                                                            long long B, int N, long long S, float* __restrict__ part) {
+  __shared__ float4 red[4][64];
+  const int k = (int)blockIdx.y;
+  int l = 0;
+  while (l + 1 < tb.L && k >= tb.blk0[l + 1]) ++l;
+  const int nch = (tb.T[l] + kLcRows - 1) / kLcRows;
+  const int j = k - tb.blk0[l];
+  const long long b = j / nch;
+  const int r0 = (j % nch) * kLcRows;
+  const int r1 = min(tb.T[l], r0 + kLcRows);
+  const int cl = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int c = ((int)blockIdx.x * 64 + cl) * 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (c < N) {
+    const float* __restrict__ gb = g + (b * S + tb.start[l]) * (long long)N + c;
+    for (int r = r0 + rl; r < r1; r += 4) {
+      const float4 v = *reinterpret_cast<const float4*>(gb + (long long)r * N);
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+  }
+  red[rl][cl] = a;
+  __syncthreads();
+  if (rl == 0 && c < N) {
+    float4 t = red[0][cl];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      const float4 v = red[i][cl];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    *reinterpret_cast<float4*>(part + (long long)k * N + c) = t;
+  }
+}
+
+// out[l, c] (+)= sum over the level's chunks (4 chunk lanes x 64 columns a workgroup, fixed order)
+__global__ __launch_bounds__(256) void level_colsum_final(const LevelTable tb, const float* __restrict__ part, int N,
+                                                          float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int l = (int)blockIdx.y;
+  const int cl = threadIdx.x & 63, kl = threadIdx.x >> 6;
+  const int c = (int)blockIdx.x * 64 + cl;
+  float a = 0.f;
+  if (c < N)
+    for (int k = tb.blk0[l] + kl; k < tb.blk0[l + 1]; k += 4) a += part[(long long)k * N + c];
+  red[kl][cl] = a;
+  __syncthreads();
+  if (kl == 0 && c < N) {
+    const float t = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    out[(long long)l * N + c] = accumulate ? out[(long long)l * N + c] + t : t;
+  }
+}
+
+bool level_table(const int64_t* T, int64_t L, int64_t B, int64_t N, int rows_per_unit, int cols_per_unit,
+                 LevelTable& tb) {
+  if (L < 1 || L > kLpMaxL || B < 1 || N < 1) return false;
+  tb.L = (int)L;
+  tb.tiles_c = (int)((N + cols_per_unit - 1) / cols_per_unit);
+  long long run = 0, blk = 0;
+  for (int l = 0; l < L; ++l) {
+    if (T[l] < 1 || T[l] > (1 << 24)) return false;
+    tb.T[l] = (int)T[l];
+    tb.start[l] = (int)run;
+    tb.blk0[l] = (int)blk;
+    run += T[l];
+    blk += B * ((T[l] + rows_per_unit - 1) / rows_per_unit) * (cols_per_unit == 64 ? tb.tiles_c : 1);
+    if (blk > (1LL << 30) || run > (1LL << 30)) return false;
+  }
+  tb.blk0[L] = (int)blk;
+  return true;
+}
 }  // namespace
 
 extern "C" {
@@ -374,6 +494,57 @@ int mfl_gather_keep_backward(const void* grad, const int64_t* index, const void*
                      static_cast<const uint8_t*>(keep), (int)n, (int)B, (int)K, (int)d,
                      static_cast<uint16_t*>(grad_src), bias_part);
   return status("gather-keep backward");
+}
+
+int mfl_level_pos_flatten(const float* const* pos, const int64_t* T, int64_t L, int64_t B, int64_t N,
+                          const float* level_embed, float* out, void* stream) {
+  g_err[0] = 0;
+  LevelTable tb{};
+  if (!pos || !T || !level_embed || !out || !level_table(T, L, B, N, kLpT, 64, tb)) {
+    snprintf(g_err, sizeof(g_err), "mfl_level_pos_flatten: bad arguments (1 <= L <= %d levels, B, N >= 1)", kLpMaxL);
+    return 1;
+  }
+  for (int l = 0; l < L; ++l) {
+    if (!pos[l]) {
+      snprintf(g_err, sizeof(g_err), "mfl_level_pos_flatten: null level pointer");
+      return 1;
+    }
+    tb.pos[l] = pos[l];
+  }
+  long long S = 0;
+  for (int l = 0; l < L; ++l) S += T[l];
+  hipLaunchKernelGGL(level_pos_flatten_kernel, dim3((unsigned)tb.blk0[L]), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     tb, level_embed, (long long)B, (int)N, S, out);
+  return status("level pos flatten");
+}
+
+size_t mfl_level_colsum_workspace_bytes(const int64_t* T, int64_t L, int64_t B, int64_t N) {
+  LevelTable tb{};
+  if (!T || !level_table(T, L, B, N, kLcRows, 256, tb)) return 0;
+  return (size_t)tb.blk0[L] * (size_t)N * sizeof(float);
+}
+
+int mfl_level_colsum(const float* g, const int64_t* T, int64_t L, int64_t B, int64_t N, float* out, int accumulate,
+                     void* workspace, void* stream) {
+  g_err[0] = 0;
+  LevelTable tb{};
+  if (!g || !T || !out || !workspace || N % 4 != 0 || ((uintptr_t)g & 15u) || ((uintptr_t)workspace & 15u) ||
+      !level_table(T, L, B, N, kLcRows, 256, tb)) {
+    snprintf(g_err, sizeof(g_err),
+             "mfl_level_colsum: bad arguments (1 <= L <= %d, N %% 4 == 0, 16-B aligned g and workspace)", kLpMaxL);
+    return 1;
+  }
+  long long S = 0;
+  for (int l = 0; l < L; ++l) S += T[l];
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(level_colsum_partial, dim3((unsigned)((N / 4 + 63) / 64), (unsigned)tb.blk0[L]), dim3(256), 0, st,
+                     tb, g, (long long)B, (int)N, S, part);
+  int rc;
+  if ((rc = status("level colsum partial"))) return rc;
+  hipLaunchKernelGGL(level_colsum_final, dim3((unsigned)((N + 63) / 64), (unsigned)L), dim3(256), 0, st, tb, part,
+                     (int)N, out, accumulate);
+  return status("level colsum final");
 }
 
 const char* mfl_relu_dropout_last_error(void) { return g_err; }

@@ -224,7 +224,7 @@ constexpr int kSmallCL = 2;     // 16-byte column lanes per block
 constexpr int kSmallRL = 128;   // row lanes per block
 template <typename T>
 __global__ __launch_bounds__(kSmallCL * kSmallRL) void colsum_small(const T* __restrict__ x, long long K, int N,
-                                                                   float* __restrict__ out) {
+                                                                   float* __restrict__ out, int accumulate) {
   constexpr int V = 16 / sizeof(T);
   constexpr int C = kSmallCL * V;                 // columns per block
   constexpr int G = kSmallCL * kSmallRL / C;      // row groups of stage 2
@@ -259,7 +259,7 @@ __global__ __launch_bounds__(kSmallCL * kSmallRL) void colsum_small(const T* __r
 #pragma unroll
     for (int g = 0; g < G; ++g) t += red2[g][threadIdx.x];
     const int col = blockIdx.x * C + threadIdx.x;
-    if (col < N) out[col] = t;
+    if (col < N) out[col] = accumulate ? out[col] + t : t;
   }
 }
 
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kSmallCL * kSmallRL) void colsum_small(const T* __r
 // groups (fixed order: deterministic).
 constexpr int kFinGroups = 16;
 __global__ __launch_bounds__(kFinGroups * 64) void colsum_final(const float* __restrict__ part, int nchunks, int N,
-                                                               float* __restrict__ out) {
+                                                               float* __restrict__ out, int accumulate) {
   __shared__ float red[kFinGroups][64];
   const int c_l = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + c_l;
@@ -289,23 +289,32 @@ __global__ __launch_bounds__(kFinGroups * 64) void colsum_final(const float* __r
     float t = 0.f;
 #pragma unroll
     for (int i = 0; i < kFinGroups; ++i) t += red[i][c_l];
-    out[c] = t;
+    out[c] = accumulate ? out[c] + t : t;
   }
 }
 
 // Split-K weight gradient of the autocast Linear (models/modules/linear.py): the fp32 partial
 // products of the K chunks, (s, n) row-major, summed over the chunks in chunk order — one read of
 // the partials and one write, 16 bytes a lane (torch's dim-0 sum of the (8, 512, 512) partials:
-// ~10 us).
+// ~10 us).  G groups of s slabs each (group g's sum into out + g n), and with `accumulate` the sum
+// is added to out (out + sum, the sum formed first: autograd's accumulation of a finished
+// gradient, bit for bit).
 __global__ __launch_bounds__(256) void sum_slabs_kernel(const float4* __restrict__ part, int s, long long n4,
-                                                        float4* __restrict__ out) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    float4 a = part[i];
+                                                        float4* __restrict__ out, int accumulate) {
+  const float4* __restrict__ pg = part + (long long)blockIdx.y * s * n4;  // group blockIdx.y
+  out += (long long)blockIdx.y * n4;
+  for (long long j = (long long)blockIdx.x * 256 + threadIdx.x; j < n4; j += (long long)gridDim.x * 256) {
+    const long long i = j;
+    float4 a = pg[i];
     for (int k = 1; k < s; ++k) {
-      const float4 b = part[(long long)k * n4 + i];
+      const float4 b = pg[(long long)k * n4 + i];
       a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
     }
-    out[i] = a;
+    if (accumulate) {
+      const float4 o = out[j];
+      a.x = o.x + a.x; a.y = o.y + a.y; a.z = o.z + a.z; a.w = o.w + a.w;
+    }
+    out[j] = a;
   }
 }
 
@@ -381,6 +390,11 @@ size_t mfl_colsum_workspace_bytes(int64_t K, int64_t N) {
 }
 
 int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void* workspace, void* stream) {
+  return mfl_colsum_ex(x, dtype, K, N, out, 0, workspace, stream);
+}
+
+int mfl_colsum_ex(const void* x, int dtype, int64_t K, int64_t N, float* out, int accumulate, void* workspace,
+                  void* stream) {
   g_err[0] = 0;
   const int elt = dtype == 0 ? 4 : 2;
   if (K < 0 || N <= 0 || out == nullptr || (K > 0 && (x == nullptr || workspace == nullptr)) ||
@@ -390,6 +404,7 @@ int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void*
   }
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (K == 0) {
+    if (accumulate) return 0;
     return zero_f32(out, N, st) == hipSuccess ? 0 : 2;
   }
   const int V = 16 / elt;
@@ -397,13 +412,13 @@ int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void*
     const dim3 g1((unsigned)((N / V + kSmallCL - 1) / kSmallCL));
     if (dtype == 0)
       hipLaunchKernelGGL(colsum_small<float>, g1, dim3(kSmallCL * kSmallRL), 0, st, static_cast<const float*>(x),
-                         (long long)K, (int)N, out);
+                         (long long)K, (int)N, out, accumulate);
     else if (dtype == 2)
       hipLaunchKernelGGL(colsum_small<uint16_t>, g1, dim3(kSmallCL * kSmallRL), 0, st,
-                         static_cast<const uint16_t*>(x), (long long)K, (int)N, out);
+                         static_cast<const uint16_t*>(x), (long long)K, (int)N, out, accumulate);
     else
       hipLaunchKernelGGL(colsum_small<_Float16>, g1, dim3(kSmallCL * kSmallRL), 0, st,
-                         static_cast<const _Float16*>(x), (long long)K, (int)N, out);
+                         static_cast<const _Float16*>(x), (long long)K, (int)N, out, accumulate);
     return status("colsum small");
   }
   const long long chunks = std::min<long long>(256, std::max<long long>(1, (K + 63) / 64));
@@ -422,22 +437,29 @@ int mfl_colsum(const void* x, int dtype, int64_t K, int64_t N, float* out, void*
   int rc;
   if ((rc = status("colsum partial"))) return rc;
   hipLaunchKernelGGL(colsum_final, dim3((unsigned)((N + 63) / 64)), dim3(kFinGroups * 64), 0, st, part, (int)chunks,
-                     (int)N, out);
+                     (int)N, out, accumulate);
   return status("colsum final");
 }
 
 int mfl_sum_slabs(const float* part, int64_t s, int64_t n, float* out, void* stream) {
+  return mfl_sum_slabs_ex(part, 1, s, n, out, 0, stream);
+}
+
+int mfl_sum_slabs_ex(const float* part, int64_t groups, int64_t s, int64_t n, float* out, int accumulate,
+                     void* stream) {
   g_err[0] = 0;
-  if (s <= 0 || s > (1 << 20) || n < 0 || n % 4 != 0 || (n > 0 && (part == nullptr || out == nullptr)) ||
+  if (s <= 0 || s > (1 << 20) || groups <= 0 || groups > 65535 || n < 0 || n % 4 != 0 || groups * n > (1LL << 40) ||
+      (n > 0 && (part == nullptr || out == nullptr)) ||
       ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out)) & 15u)) {
-    snprintf(g_err, sizeof(g_err), "mfl_sum_slabs: bad arguments (s > 0, n %% 4 == 0, 16-B aligned pointers)");
+    snprintf(g_err, sizeof(g_err),
+             "mfl_sum_slabs: bad arguments (s > 0, groups > 0, n %% 4 == 0, 16-B aligned pointers)");
     return 1;
   }
   if (n == 0) return 0;
   const long long n4 = n / 4;
-  const unsigned blocks = (unsigned)std::min<long long>((n4 + 255) / 256, 8192);
-  hipLaunchKernelGGL(sum_slabs_kernel, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream),
-                     reinterpret_cast<const float4*>(part), (int)s, n4, reinterpret_cast<float4*>(out));
+  const unsigned blocks = (unsigned)std::max<long long>(1, std::min<long long>((n4 + 255) / 256, 8192 / groups));
+  hipLaunchKernelGGL(sum_slabs_kernel, dim3(blocks, (unsigned)groups), dim3(256), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const float4*>(part), (int)s, n4, reinterpret_cast<float4*>(out), accumulate);
   return status("sum slabs");
 }
 

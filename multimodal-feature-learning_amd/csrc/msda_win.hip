@@ -545,6 +545,11 @@ __device__ __forceinline__ int lm_sw(int r, int c) {
   return r * kLmRow + ((c ^ ((((r >> 1) & 1) << 1) | (((r >> 3) & 1) << 2))) << 4);
 }
 
+// the coefficient tile C's layout: chunk c ^ (r & 7).  Its b16 stores bank on (a / 4) mod 32, where
+// the 128-B row drops out: XOR-ing the chunk with all three low row bits spreads the stores of
+// different rows; the A-operand reads (rows li, chunk g / 4 + g) still meet 16 distinct bank quads
+__device__ __forceinline__ int lm_csw(int r, int c) { return r * kLmRow + ((c ^ (r & 7)) << 4); }
+
 template <bool ZEROS, bool COORDS, int P>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void win_lm_kernel(
     const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
@@ -756,9 +761,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
         // 4. grad_value of the 16 rows += C . G, 32 compacted samples per MFMA step
         for (int ks = 0; ks < nk; ++ks) {
           {
-            uint4* z = reinterpret_cast<uint4*>(s_c + (lane >> 2) * kLmRow + (lane & 3) * 32);
+            // 8 consecutive lanes zero one whole 128-B row (a ds_write_b128 bank group: 32 distinct
+            // banks; two rows per group were a 2-way conflict in all 8 groups)
+            uint4* z = reinterpret_cast<uint4*>(s_c + (lane >> 3) * kLmRow + (lane & 7) * 16);
             z[0] = make_uint4(0u, 0u, 0u, 0u);
-            z[1] = make_uint4(0u, 0u, 0u, 0u);
+            z[8 * kLmRow / 16] = make_uint4(0u, 0u, 0u, 0u);
           }
           wave_lds_fence();
 #pragma unroll
@@ -767,18 +774,18 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
             if (col >= 0 && col < 32) {
               const int cc = col >> 3, cw = (col & 7) * 2;
               if (dr[jj] >= 0) {
-                *reinterpret_cast<uint16_t*>(s_c + lm_sw(dr[jj], cc) + cw) = (uint16_t)ch[jj];
-                *reinterpret_cast<uint16_t*>(s_c + lm_sw(dr[jj], 4 + cc) + cw) = (uint16_t)cl[jj];
+                *reinterpret_cast<uint16_t*>(s_c + lm_csw(dr[jj], cc) + cw) = (uint16_t)ch[jj];
+                *reinterpret_cast<uint16_t*>(s_c + lm_csw(dr[jj], 4 + cc) + cw) = (uint16_t)cl[jj];
               }
               if (dr[jj] + 1 < kRW) {
-                *reinterpret_cast<uint16_t*>(s_c + lm_sw(dr[jj] + 1, cc) + cw) = (uint16_t)(ch[jj] >> 16);
-                *reinterpret_cast<uint16_t*>(s_c + lm_sw(dr[jj] + 1, 4 + cc) + cw) = (uint16_t)(cl[jj] >> 16);
+                *reinterpret_cast<uint16_t*>(s_c + lm_csw(dr[jj] + 1, cc) + cw) = (uint16_t)(ch[jj] >> 16);
+                *reinterpret_cast<uint16_t*>(s_c + lm_csw(dr[jj] + 1, 4 + cc) + cw) = (uint16_t)(cl[jj] >> 16);
               }
             }
           }
           wave_lds_fence();
-          const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(s_c + wa0);
-          const bf16x8 alo = *reinterpret_cast<const bf16x8*>(s_c + wa1);
+          const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(s_c + lm_csw(li, g));
+          const bf16x8 alo = *reinterpret_cast<const bf16x8*>(s_c + lm_csw(li, 4 + g));
           const int qq = li >> 2, pp = li & 3;
           const int rowa = s_q[ks * 32 + 8 * g + qq], rowb = s_q[ks * 32 + 8 * g + 4 + qq];
 #pragma unroll

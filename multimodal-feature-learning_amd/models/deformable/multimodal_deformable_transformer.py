@@ -13,10 +13,11 @@ import torch
 from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
+from ..modules.pyramid import level_pos_flatten
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
-from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
+from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_entry, carry_supported, pos_sink
 from ..modules.ffn import relu_dropout
 from ..modules.value_proj import layer_values, layer_values_supported
 from .unimodal_deformable_transformer import (_get_activation_fn, _get_clones, encoder_reference_points,
@@ -79,8 +80,7 @@ class MultimodalDeformableTransformer(nn.Module):
     def prepare_encoder_inputs(self, srcs, masks, pos_embeds):
         """One modality's pyramid -> flattened inputs (reference :87-131)."""
         src_flatten = torch.cat([s.transpose(1, 2) for s in srcs], 1)
-        lvl_pos_embed_flatten = torch.cat(
-            [p.transpose(1, 2) + self.level_embed[lvl].view(1, 1, -1) for lvl, p in enumerate(pos_embeds)], 1)
+        lvl_pos_embed_flatten = level_pos_flatten(pos_embeds, self.level_embed)
         mask_flatten = torch.cat(list(masks), 1)
         temporal_shapes, level_start_index = level_metadata([s.shape[-1] for s in srcs], src_flatten.device)
         valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
@@ -139,19 +139,21 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
 
     def forward_carry(self, video, audio, video_next_pos, audio_next_pos, video_reference_points,
                       video_temporal_shapes, video_level_start_index, video_padding_mask, audio_reference_points,
-                      audio_temporal_shapes, audio_level_start_index, audio_padding_mask):
+                      audio_temporal_shapes, audio_level_start_index, audio_padding_mask, pos_accs=(None, None)):
         """``forward`` with each stream as ``(src, value, query)``: the MSDA self-attention inputs
         arrive as bf16 copies (``src``, ``src + pos``) from the previous layer's fused FFN add +
         LayerNorm, and this layer's FFNs hand the next layer its copies (query = bf16(out +
-        next_pos); None when next_pos is None)."""
+        next_pos); None when next_pos is None).  ``pos_accs``: the (video, audio) next_pos came
+        from ``pos_sink`` (their gradients summed in place by the fused backwards)."""
         def self_block(stream, ref, shapes, starts, mask):
             src, value, query = stream
             attn = self.self_attn(query, ref, value, shapes, starts, mask)
             return add_layer_norm_carry(src, attn, self.norm1, dropout=self.dropout1)[1]
 
-        def ffn(x, next_pos):
+        def ffn(x, next_pos, pos_acc):
             hidden = relu_dropout(self.linear1(x), self.activation, self.dropout2)
-            out, out16, q16 = add_layer_norm_carry(x, self.linear2(hidden), self.norm2, next_pos, self.dropout3)
+            out, out16, q16 = add_layer_norm_carry(x, self.linear2(hidden), self.norm2, next_pos, self.dropout3,
+                                                   pos_acc=pos_acc)
             return out, out16, (q16 if q16 is not None else out16)
 
         v16 = self_block(video, video_reference_points, video_temporal_shapes, video_level_start_index,
@@ -162,7 +164,8 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
                                                video_level_start_index, video_padding_mask)
         audio_attended_visual = self.self_attn(v16, video_reference_points, a16, audio_temporal_shapes,
                                                audio_level_start_index, audio_padding_mask)
-        return ffn(audio_attended_visual, video_next_pos), ffn(visual_attended_audio, audio_next_pos)
+        return (ffn(audio_attended_visual, video_next_pos, pos_accs[0]),
+                ffn(visual_attended_audio, audio_next_pos, pos_accs[1]))
 
     def _self_block(self, src, pos, ref, shapes, starts, mask):
         """``norm1(src + dropout1(self_attn(src + pos, src)))`` as its bf16 copy (under bf16 autocast
@@ -208,15 +211,20 @@ class MultimodalDeformableTransformerEncoder(nn.Module):
         if (self.layers and all(type(layer) is MultimodalDeformableTransformerEncoderLayer for layer in self.layers)
                 and carry_supported(video_src, self.layers[0].norm2) and carry_supported(audio_src, self.layers[0].norm2)
                 and all(p is None or p.dtype == torch.float32 for p in (video_pos, audio_pos))):
-            # bf16 MSDA operands carried from each layer's fused FFN add + LayerNorm to the next
+            # bf16 MSDA operands carried from each layer's fused FFN add + LayerNorm to the next;
+            # each pos's gradient summed in place by those fused backwards (add_norm.pos_sink)
             wp = MultimodalDeformableTransformerEncoderLayer.with_pos_embed
-            v, a = (video_src, video_src, wp(video_src, video_pos)), (audio_src, audio_src, wp(audio_src, audio_pos))
+            video_pos, vacc = pos_sink(video_pos)
+            audio_pos, aacc = pos_sink(audio_pos)
+            # (src, bf16(src), bf16(src + pos)) of each stream in one pass where the fused kernel applies
+            v = carry_entry(video_src, video_pos, vacc) or (video_src, video_src, wp(video_src, video_pos))
+            a = carry_entry(audio_src, audio_pos, aacc) or (audio_src, audio_src, wp(audio_src, audio_pos))
             for i, layer in enumerate(self.layers):
                 last = i + 1 == len(self.layers)
                 v, a = layer.forward_carry(v, a, None if last else video_pos, None if last else audio_pos,
                                            video_ref, video_temporal_shapes, video_level_start_index,
                                            video_padding_mask, audio_ref, audio_temporal_shapes,
-                                           audio_level_start_index, audio_padding_mask)
+                                           audio_level_start_index, audio_padding_mask, pos_accs=(vacc, aacc))
             v[0]._mfl_bf16, a[0]._mfl_bf16 = v[1], a[1]  # bf16(out): the decoder's value projections read them
             return v[0], a[0]
         for layer in self.layers:

@@ -16,10 +16,11 @@ import torch.nn.functional as F
 from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
+from ..modules.pyramid import level_pos_flatten
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear, flush_point
-from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported, pos_sink
+from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_entry, carry_supported, pos_sink
 from ..modules.ffn import relu_dropout
 from ..modules.value_proj import layer_values, layer_values_supported
 
@@ -128,8 +129,7 @@ class DeformableTransformer(nn.Module):
                 lvl_pos_embed_flatten (B, S, d_model), mask_flatten (B, S)
         (reference :90-134)"""
         src_flatten = torch.cat([s.transpose(1, 2) for s in srcs], 1)
-        lvl_pos_embed_flatten = torch.cat(
-            [p.transpose(1, 2) + self.level_embed[lvl].view(1, 1, -1) for lvl, p in enumerate(pos_embeds)], 1)
+        lvl_pos_embed_flatten = level_pos_flatten(pos_embeds, self.level_embed)
         mask_flatten = torch.cat(list(masks), 1)
         temporal_shapes, level_start_index = level_metadata([s.shape[-1] for s in srcs], src_flatten.device)
         valid_ratios = torch.stack([self.get_valid_ratio(m) for m in masks], 1)
@@ -230,7 +230,11 @@ class DeformableTransformerEncoder(nn.Module):
             # no pos add, no gradient accumulation kernels between layers; pos's gradient summed in
             # place by the fused backwards: add_norm.pos_sink)
             pos, pos_acc = pos_sink(pos)
-            value, query = src, DeformableTransformerEncoderLayer.with_pos_embed(src, pos)
+            entry = carry_entry(src, pos, pos_acc)  # (src, bf16(src), bf16(src + pos)) in one pass
+            if entry is not None:
+                out, value, query = entry
+            else:
+                value, query = src, DeformableTransformerEncoderLayer.with_pos_embed(src, pos)
             for i, layer in enumerate(self.layers):
                 next_pos = pos if i + 1 < len(self.layers) else None
                 out, value, query = layer.forward_carry(out, value, query, next_pos, reference_points,

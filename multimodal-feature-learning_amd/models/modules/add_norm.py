@@ -15,7 +15,7 @@ import torch
 from torch import nn
 from torch.autograd import Function
 
-__all__ = ["add_layer_norm", "add_layer_norm_carry", "seed_pool", "pos_sink", "PosGradAcc"]
+__all__ = ["add_layer_norm", "add_layer_norm_carry", "seed_pool", "pos_sink", "PosGradAcc", "carry_entry"]
 
 _TAGS = {torch.float32: 0, torch.bfloat16: 2}
 
@@ -271,3 +271,77 @@ def add_layer_norm_carry(r, y, norm: nn.LayerNorm, pos=None, dropout=None, pos_a
             return _AddLayerNormCarry.apply(*args)
     out = add_layer_norm(r, y, norm, dropout)
     return out, out, (out + pos if pos is not None else None)
+
+
+class _CarryEntry(Function):
+    """(src, bf16(src), bf16(src + pos)): an encoder's first-layer operands in one pass, and one pass
+    back summing src's three gradients (csrc/add_layernorm.hip carry_entry_*)."""
+
+    @staticmethod
+    def forward(ctx, src, pos, acc):
+        from ... import _native, _trace
+        _trace.hit("carry_entry")
+        lib = _native.load_library()
+        v16 = torch.empty(src.shape, dtype=torch.bfloat16, device=src.device)
+        q16 = torch.empty(src.shape, dtype=torch.bfloat16, device=src.device)
+        rc = lib.mfl_carry_entry_forward(src.data_ptr(), _ptr(pos), src.numel(), v16.data_ptr(), q16.data_ptr(),
+                                         _native.stream_handle(src.device))
+        if rc != 0:
+            raise RuntimeError("mfl_carry_entry_forward failed: " + lib.mfl_add_layernorm_last_error().decode())
+        ctx.set_materialize_grads(False)
+        ctx.acc, ctx.has_pos, ctx.shape = acc, pos is not None, src.shape
+        return src.view_as(src), v16, q16
+
+    @staticmethod
+    def backward(ctx, dr, dv16, dq16):
+        from ... import _native
+        lib = _native.load_library()
+        nig = ctx.needs_input_grad
+        ref = next(t for t in (dr, dv16, dq16) if t is not None) if any(
+            t is not None for t in (dr, dv16, dq16)) else None
+        if ref is None:
+            return None, None, None
+        dev = ref.device
+        n = 1
+        for k in ctx.shape:
+            n *= k
+        dr = dr.contiguous() if dr is not None and dr.dtype == torch.float32 else (None if dr is None else dr.float())
+        dv16 = None if dv16 is None else dv16.to(torch.bfloat16).contiguous()
+        dq16 = None if dq16 is None else dq16.to(torch.bfloat16).contiguous()
+        dsrc = torch.empty(ctx.shape, dtype=torch.float32, device=dev) if nig[0] else None
+        dpos, acc_flag, out_pos = None, 0, None
+        if ctx.has_pos and nig[1] and dq16 is not None:
+            if ctx.acc is not None:
+                if ctx.acc.buf is None:
+                    ctx.acc.buf = torch.empty(ctx.shape, dtype=torch.float32, device=dev)
+                else:
+                    acc_flag = 1
+                dpos = ctx.acc.buf
+            else:
+                dpos = out_pos = torch.empty(ctx.shape, dtype=torch.float32, device=dev)
+        if dsrc is None:  # (the kernel always writes dsrc: a scratch buffer when src needs no gradient)
+            dsrc_buf = torch.empty(ctx.shape, dtype=torch.float32, device=dev)
+        else:
+            dsrc_buf = dsrc
+        rc = lib.mfl_carry_entry_backward(_ptr(dr), _ptr(dv16), _ptr(dq16), n, dsrc_buf.data_ptr(), _ptr(dpos),
+                                          acc_flag, _native.stream_handle(dev))
+        if rc != 0:
+            raise RuntimeError("mfl_carry_entry_backward failed: " + lib.mfl_add_layernorm_last_error().decode())
+        return dsrc, out_pos, None
+
+
+def carry_entry(src, pos=None, pos_acc=None):
+    """``(src, bf16(src), bf16(src + pos))`` — the first carried layer's residual, value and query
+    operands (reference ``with_pos_embed(src, pos)``, unimodal_deformable_transformer.py:241, cast by
+    autocast at each Linear) — from one fused kernel each way under bf16 autocast on the GPU;
+    None where it does not apply (the caller keeps the composition).  ``pos_acc``: pos came from
+    ``pos_sink`` and its gradient is summed there."""
+    if not (src.is_cuda and src.dtype == torch.float32 and src.is_contiguous() and src.numel() % 8 == 0
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and src.data_ptr() % 16 == 0):
+        return None
+    if pos is not None and not (pos.is_cuda and pos.dtype == torch.float32 and pos.is_contiguous()
+                                and pos.shape == src.shape and pos.data_ptr() % 16 == 0):
+        return None
+    return _CarryEntry.apply(src, pos, pos_acc)
+

@@ -31,7 +31,8 @@ from .seg_attention import segment_attention, segment_key_mask
 from .value_proj import linear_group, linear_group_supported
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
-from .linear import Linear, _AutocastLinear, _addmm, _bias_grad, _claim_group, _defer, _mm_nn, _weight_grad, linear_pair
+from .linear import (Linear, _AutocastLinear, _accum_group, _addmm, _bias_grad, _claim_group, _defer, _mm_nn,
+                     _weight_grad, linear_pair)
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
            "masked_scores_softmax", "mask_padding_rows", "mha_self_attention"]
@@ -120,12 +121,22 @@ class _QueryPrologue(torch.autograd.Function):
         gwa = gwb = gba = gbb = None
         # [W_off; W_aw] and [b_off; b_aw] lie back to back in the trainer's flat gradient buffer
         # (flat_groups): the products are written straight into those views when they can be claimed
+        # (a module called several times in one backward — the multimodal encoder's shared
+        # self-attention: a later call adds its products into the view an earlier one claimed)
         if nig[1] or nig[3]:
-            gw = _weight_grad(g2, x2, _claim_group((wa, wb)) if nig[1] and nig[3] else None)
-            gwa, gwb = gw[:na], gw[na:]
+            acc = _accum_group((wa, wb)) if nig[1] and nig[3] else None
+            if acc is not None:
+                _weight_grad(g2, x2, acc, accumulate=True)
+            else:
+                gw = _weight_grad(g2, x2, _claim_group((wa, wb)) if nig[1] and nig[3] else None)
+                gwa, gwb = gw[:na], gw[na:]
         if nig[2] or nig[4]:
-            gbias = _bias_grad(g2, _claim_group((ba, bb)) if nig[2] and nig[4] else None)
-            gba, gbb = gbias[:na], gbias[na:]
+            acc = _accum_group((ba, bb)) if nig[2] and nig[4] else None
+            if acc is not None:
+                _bias_grad(g2, acc, accumulate=True)
+            else:
+                gbias = _bias_grad(g2, _claim_group((ba, bb)) if nig[2] and nig[4] else None)
+                gba, gbb = gbias[:na], gbias[na:]
         return (gx, gwa, gba, gwb, gbb) + rest
 
 

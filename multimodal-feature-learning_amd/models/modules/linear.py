@@ -49,13 +49,38 @@ DEFER_MAX_ROWS = 1024
 class _WgradQueue:
     """Queued weight / bias gradient products of one backward (see the module docstring)."""
 
-    def __init__(self, deliver):
+    def __init__(self, deliver, target=None):
         self.deliver = deliver
+        # target(param): the tensor a finished gradient for param may be added into in place (the
+        # trainer: param.grad while its bucket is not reduced), or None.  deliver(param, None) then
+        # means "added into target(param)"
+        self.target = target
         # (dY (K, N), X (K, C), weight param, row offset, bias param or None, dY's column sums or None)
         self.entries = []
 
     def push(self, g2, x2, weight, row, bias, colsum=None):
         self.entries.append((g2, x2, weight, row, bias, colsum))
+
+    def _finish(self, prm, ts, dest=None):
+        """Hand parameter prm the sum of its full-shape gradient products ts: added in place into
+        target(prm) when there is one (one kernel, no fresh tensor), else summed into dest (its
+        claimed flat view) or a fresh tensor — a single product is handed over as it is."""
+        tgt = self.target(prm) if self.target is not None and ACCUMULATE_IN_PLACE else None
+        if tgt is not None:
+            from ... import _trace
+            _trace.hit("wgrad_into_grad")
+            _sum_into(ts, tgt, accumulate=True)
+            self.deliver(prm, None)
+            return
+        if len(ts) == 1 and dest is None:
+            self.deliver(prm, ts[0])
+            return
+        out = dest if dest is not None else torch.empty(prm.shape, dtype=torch.float32, device=ts[0].device)
+        if len(ts) == 1:
+            out.copy_(ts[0])
+        else:
+            _sum_into(ts, out, accumulate=False)
+        self.deliver(prm, out)
 
     @torch.no_grad()
     def flush(self):
@@ -68,18 +93,24 @@ class _WgradQueue:
             groups.setdefault((g2.shape[0], g2.shape[1], x2.shape[1], g2.dtype), []).append(e)
         from ... import _trace
         _trace.hit("wgrad_batched", len(entries))
-        parts = {}  # param -> [(row offset, fp32 grad rows)]
+        parts = {}  # param -> [(row offset, fp32 grad rows)] (weights of several row blocks)
         for (_, n_out, _, _), es in groups.items():
+            # one parameter's products next to each other, the parameters in flat-buffer order
+            es = sorted(es, key=lambda e: (_dest_offset(e[2]), id(e[2]), e[3]))
+            uniq = list({id(e[2]): e[2] for e in es}.values())
+            uses = [sum(1 for e in es if e[2] is w) for w in uniq]
+            full = all(e[3] == 0 and e[0].shape[1] == e[2].shape[0] for e in es)
             # whole weights of one shape laid out back to back in the trainer's flat gradient buffer
-            # (flat_groups, e.g. the decoder layers' linear1): the batched GEMM writes their gradients
-            # straight into that one view (no fresh tensors to copy into the buffer afterwards)
+            # (flat_groups, e.g. the decoder layers' linear1): the batched GEMM (or the sum of a
+            # shared weight's products) writes their gradients straight into that one view
             dest = None
-            if len(es) > 1 and es[0][0].is_cuda and all(e[3] == 0 and e[0].shape[1] == e[2].shape[0] for e in es):
-                es = sorted(es, key=lambda e: _dest_offset(e[2]))
-                dest = _claim_group([e[2] for e in es])
+            if (es[0][0].is_cuda and full and len(set(uses)) == 1 and (ACCUMULATE_IN_PLACE or uses[0] == 1)
+                    and not any(self.target is not None and self.target(w) is not None for w in uniq)):
+                dest = (_claim_group(uniq, returned=False) if len(uniq) > 1
+                        else _claim(uniq[0], returned=False) if uses[0] > 1 else None)
             gs = es[0][0][None] if len(es) == 1 else torch.stack([e[0] for e in es])
             xs = es[0][1][None] if len(es) == 1 else torch.stack([e[1] for e in es])
-            if dest is not None:
+            if dest is not None and uses[0] == 1:
                 dw = torch.bmm(gs.transpose(1, 2), xs, out_dtype=torch.float32,
                                out=dest.view(len(es), gs.shape[2], xs.shape[2]))
             elif gs.is_cuda:  # fp32 accumulate and output
@@ -90,10 +121,30 @@ class _WgradQueue:
             # backward that produced dY summed them), else one reduction for the group
             need = any(e[4] is not None and e[5] is None for e in es)
             db = gs.sum(1, dtype=torch.float32) if need else None
+            bias_parts = {}
             for k, (_, _, w, row, b, cs) in enumerate(es):
-                parts.setdefault(w, []).append((row, dw[k]))
+                if not full:
+                    parts.setdefault(w, []).append((row, dw[k]))
                 if b is not None:
-                    parts.setdefault(b, []).append((row, cs if cs is not None else db[k]))
+                    if full:
+                        bias_parts.setdefault(b, []).append(cs if cs is not None else db[k])
+                    else:
+                        parts.setdefault(b, []).append((row, cs if cs is not None else db[k]))
+            if full:
+                if dest is not None and uses[0] == 1:
+                    for k, w in enumerate(uniq):
+                        self.deliver(w, dw[k])
+                elif dest is not None:  # every weight's u products summed into its view, one kernel
+                    _sum_slabs(dw, dest.view(len(uniq), -1), groups=len(uniq))
+                    for k, w in enumerate(uniq):
+                        self.deliver(w, dest[k * w.shape[0]:(k + 1) * w.shape[0]].view_as(w))
+                else:
+                    k0 = 0
+                    for w, u in zip(uniq, uses):
+                        self._finish(w, [dw[k] for k in range(k0, k0 + u)])
+                        k0 += u
+            for b, ts in bias_parts.items():
+                self._finish(b, ts)
         for prm, ps in parts.items():
             ps.sort(key=lambda rp: rp[0])
             rows = [r for r, _ in ps]
@@ -109,15 +160,38 @@ class _WgradQueue:
             self.deliver(prm, grad)
 
 
+def _sum_into(ts, out, accumulate):
+    """out (+)= the sum of the equal-shape fp32 tensors ts (formed first, in list order): one slab-sum
+    kernel when they are consecutive slabs of one buffer (a batched GEMM's outputs), else adds."""
+    n = ts[0].numel()
+    base = ts[0]
+    adjacent = (out.is_cuda and all(t.is_contiguous() and t.dtype == torch.float32 for t in ts)
+                and all(t.untyped_storage().data_ptr() == base.untyped_storage().data_ptr()
+                        and t.storage_offset() == base.storage_offset() + i * n for i, t in enumerate(ts)))
+    if adjacent and out.is_contiguous():
+        part = base.new_empty(0).set_(base.untyped_storage(), base.storage_offset(), (len(ts), n))
+        _sum_slabs(part, out.view(-1), accumulate=accumulate)
+        return out
+    acc = ts[0] if len(ts) == 1 else torch.stack(ts).sum(0)
+    if accumulate:
+        out.add_(acc.view_as(out))
+    else:
+        out.copy_(acc.view_as(out))
+    return out
+
+
 _queue = None
 
 
 @contextlib.contextmanager
-def deferred_weight_grads(deliver):
+def deferred_weight_grads(deliver, target=None):
     """Queue the short-K layers' weight / bias gradients of the backward run inside; the caller
-    calls ``flush()`` on the yielded queue after the backward (flush points flush earlier)."""
+    calls ``flush()`` on the yielded queue after the backward (flush points flush earlier).
+    ``deliver(param, grad)`` receives each parameter's gradient; with ``target(param)`` given (a
+    tensor to add a finished gradient into, or None) a gradient may instead be added into that
+    tensor in place, announced as ``deliver(param, None)``."""
     global _queue
-    prev, _queue = _queue, _WgradQueue(deliver)
+    prev, _queue = _queue, _WgradQueue(deliver, target)
     try:
         yield _queue
     finally:
@@ -248,7 +322,10 @@ def split_k_chunks(k, min_chunk=1024, max_split=8):
     return 1
 
 
-_dest = None  # flat_grad_destinations: {"views": {id(param): flat view}, "claimed": set()}
+_dest = None  # flat_grad_destinations: {"views": {id(param): flat view}, "claimed": set(), ...}
+# later products of a parameter added into the view / .grad in place (False: autograd's accumulation,
+# for A/B tests)
+ACCUMULATE_IN_PLACE = True
 
 
 @contextlib.contextmanager
@@ -258,19 +335,27 @@ def flat_grad_destinations(views, may_claim=None):
     which autograd then hands to the parameter as its .grad — instead of a fresh tensor copied
     into the flat buffer afterwards (one 171 MB copy pass per step at the bench shape).
     ``may_claim(param)``, when given, vetoes a view at the time it would be handed out (the
-    trainer refuses the views of gradient buckets it has already all-reduced or is reducing)."""
+    trainer refuses the views of gradient buckets it has already all-reduced or is reducing).
+    A parameter used several times in the backward (a module shared by several calls: the
+    multimodal encoder's self-attention, the decoder's cross-attention over two memories): the
+    later producers add their products into the view the first one handed to autograd
+    (``_accum_target``) and return no gradient — autograd's accumulation into .grad happens only
+    once all of them have run, so the view then holds the whole sum (the same sum, added in the
+    same order: the products are formed first, then added)."""
     global _dest
-    prev, _dest = _dest, {"views": views, "claimed": set(), "may_claim": may_claim}
+    prev, _dest = _dest, {"views": views, "claimed": set(), "may_claim": may_claim, "returned": {}, "groups": {}}
     try:
         yield
     finally:
         _dest = prev
 
 
-def _claim(param):
+def _claim(param, returned=True):
     """The flat view ``param``'s gradient may be written into, or None: once per backward and
     only while the parameter has no gradient yet (a later producer's result is added by autograd,
-    into that view or a copy of it)."""
+    into that view or a copy of it, or added into the view itself: _accum_target).  ``returned``:
+    the caller hands the view to autograd as the parameter's gradient (later producers may add
+    into it until autograd has accumulated it)."""
     d = _dest
     if d is None or param is None or param.grad is not None:
         return None
@@ -280,7 +365,35 @@ def _claim(param):
     if d["may_claim"] is not None and not d["may_claim"](param):
         return None
     d["claimed"].add(id(param))
+    if returned:
+        d["returned"][id(param)] = v
     return v.view_as(v)  # a fresh view object: autograd adopts it as .grad instead of cloning
+
+
+def _accum_target(param):
+    """The flat view an earlier producer of this backward wrote ``param``'s gradient into and handed
+    to autograd, while autograd has not accumulated it yet (param.grad is None): a later producer
+    adds its product into it in place and returns no gradient.  None otherwise."""
+    d = _dest
+    if d is None or param is None or param.grad is not None or not ACCUMULATE_IN_PLACE:
+        return None
+    v = d["returned"].get(id(param))
+    if v is not None:
+        from ... import _trace
+        _trace.hit("grad_accum_view")
+    return v
+
+
+def _accum_group(params):
+    """_accum_target for parameters claimed together (_claim_group): their one view, or None."""
+    d = _dest
+    if d is None or any(p.grad is not None for p in params) or not ACCUMULATE_IN_PLACE:
+        return None
+    v = d["groups"].get(tuple(id(p) for p in params))
+    if v is not None:
+        from ... import _trace
+        _trace.hit("grad_accum_view")
+    return v
 
 
 def _given_colsum(gy, n):
@@ -303,7 +416,7 @@ def _dest_offset(param):
     return -1 if v is None else v.storage_offset()
 
 
-def _claim_group(params):
+def _claim_group(params, returned=True):
     """One view of the flat gradient buffer covering the given parameters' gradient views, when they
     lie back to back in this order (the trainer's flat_groups layout; stacked along dim 0), claimed for
     all of them — or None, and nothing claimed (see _claim)."""
@@ -326,48 +439,65 @@ def _claim_group(params):
     for p in params:
         d["claimed"].add(id(p))
     rows = sum(v.shape[0] for v in views)
-    return base.new_empty(0).set_(base.untyped_storage(), base.storage_offset(), (rows,) + tuple(base.shape[1:]))
+    g = base.new_empty(0).set_(base.untyped_storage(), base.storage_offset(), (rows,) + tuple(base.shape[1:]))
+    if returned:
+        for p, v in zip(params, views):
+            d["returned"][id(p)] = v
+        d["groups"][tuple(id(p) for p in params)] = g
+    return g
 
 
-def _bias_grad(g2, out=None):
+def _bias_grad(g2, out=None, accumulate=False):
     """fp32 column sum of dY (K, N) through mfl_colsum (one streaming pass, fixed order);
     torch's column reduction where the kernel's layout conditions do not hold.  ``out``: an fp32
-    (N,) destination (a flat-buffer view)."""
+    (N,) destination (a flat-buffer view); ``accumulate``: added into it."""
     if g2.dtype not in (torch.bfloat16, torch.float16) or (g2.shape[1] * 2) % 16 or not g2.is_contiguous():
         r = g2.sum(0, dtype=torch.float32)
-        return r if out is None else out.copy_(r)
+        if out is None:
+            return r
+        return out.add_(r) if accumulate else out.copy_(r)
     from ... import _native
     lib = _native.load_library()
     K, N = g2.shape
     if out is None:
         out = torch.empty(N, dtype=torch.float32, device=g2.device)
     ws = torch.empty(lib.mfl_colsum_workspace_bytes(K, N), dtype=torch.uint8, device=g2.device)
-    rc = lib.mfl_colsum(g2.data_ptr(), _native.DTYPE_TAGS[g2.dtype], K, N, out.data_ptr(), ws.data_ptr(),
-                        _native.stream_handle(g2.device))
+    rc = lib.mfl_colsum_ex(g2.data_ptr(), _native.DTYPE_TAGS[g2.dtype], K, N, out.data_ptr(), 1 if accumulate else 0,
+                           ws.data_ptr(), _native.stream_handle(g2.device))
     if rc != 0:
         raise RuntimeError("mfl_colsum failed: " + lib.flat_adamw_last_error().decode())
     return out
 
 
-def _sum_slabs(part, out=None):
+def _sum_slabs(part, out=None, accumulate=False, groups=1):
     """part.sum(0) of the fp32 split-K partials (s, n_out, n_in) through mfl_sum_slabs (one pass,
-    chunk order), into ``out`` if given."""
+    chunk order), into ``out`` if given (added into it with ``accumulate``).  ``groups`` > 1: part's
+    groups * s slabs are ``groups`` consecutive runs of s, each summed into its own part of out
+    (groups, n_out, n_in)."""
+    s = part.shape[0] // groups
     n = part[0].numel()
-    if n % 4 or not part.is_contiguous():
-        return part.sum(0) if out is None else torch.sum(part, 0, out=out)
+    if n % 4 or not part.is_contiguous() or not part.is_cuda or (out is not None and not out.is_contiguous()):
+        r = part.reshape(groups, s, -1).sum(1)
+        r = r.view(part.shape[1:]) if groups == 1 else r.view((groups,) + tuple(part.shape[1:]))
+        if out is None:
+            return r
+        return out.add_(r.view_as(out)) if accumulate else out.copy_(r.view_as(out))
     from ... import _native
     lib = _native.load_library()
     if out is None:
-        out = torch.empty(part.shape[1:], dtype=torch.float32, device=part.device)
-    rc = lib.mfl_sum_slabs(part.data_ptr(), part.shape[0], n, out.data_ptr(), _native.stream_handle(part.device))
+        out = torch.empty(((groups,) if groups > 1 else ()) + tuple(part.shape[1:]), dtype=torch.float32,
+                          device=part.device)
+    rc = lib.mfl_sum_slabs_ex(part.data_ptr(), groups, s, n, out.data_ptr(), 1 if accumulate else 0,
+                              _native.stream_handle(part.device))
     if rc != 0:
         raise RuntimeError("mfl_sum_slabs failed: " + lib.flat_adamw_last_error().decode())
     return out
 
 
-def _weight_grad(g2, x2, out=None):
+def _weight_grad(g2, x2, out=None, accumulate=False):
     """fp32 dW = dY^T X of 16-bit dY (K, N) and X (K, C): K split into chunks, one strided-batched
-    GEMM with fp32 partial outputs, then their sum (into ``out`` if given)."""
+    GEMM with fp32 partial outputs, then their sum (into ``out`` if given; added into it with
+    ``accumulate``)."""
     k, n_out, n_in = x2.shape[0], g2.shape[1], x2.shape[1]
     s = split_k_chunks(k)
     if s > 1:
@@ -375,9 +505,11 @@ def _weight_grad(g2, x2, out=None):
         # extra 8-32 MB pass per call, ~0.3 ms per step, tools/op_census.py)
         part = torch.bmm(g2.view(s, k // s, n_out).transpose(1, 2), x2.view(s, k // s, n_in),
                          out_dtype=torch.float32)
-        return _sum_slabs(part, out)
+        return _sum_slabs(part, out, accumulate)
     r = torch.mm(g2.t(), x2, out_dtype=torch.float32)
-    return r if out is None else out.copy_(r)
+    if out is None:
+        return r
+    return out.add_(r) if accumulate else out.copy_(r)
 
 
 class _AutocastLinear(torch.autograd.Function):
@@ -414,9 +546,20 @@ class _AutocastLinear(torch.autograd.Function):
                                                                 cs)):
             return gx, None, None, None, None
         if nig[1]:
-            gw = _weight_grad(g2, x2, _claim(ctx.weight))
+            acc = _accum_target(ctx.weight)  # (a shared layer: added into an earlier call's view)
+            if acc is not None:
+                _weight_grad(g2, x2, acc, accumulate=True)
+            else:
+                gw = _weight_grad(g2, x2, _claim(ctx.weight))
         if ctx.has_bias and nig[2]:
-            gb = cs if cs is not None else _bias_grad(g2, _claim(ctx.bias))
+            acc = _accum_target(ctx.bias)
+            if acc is not None:
+                if cs is not None:
+                    acc.add_(cs)
+                else:
+                    _bias_grad(g2, acc, accumulate=True)
+            else:
+                gb = cs if cs is not None else _bias_grad(g2, _claim(ctx.bias))
         return gx, gw, gb, None, None
 
 

@@ -1,0 +1,94 @@
+"""The flattened level position embedding of ``prepare_encoder_inputs``.
+
+Reference (models/deformable/unimodal_deformable_transformer.py:90-134, and the multimodal / sparse
+transformers): ``lvl_pos_embed_flatten = torch.cat([pos_l.transpose(1, 2) + level_embed[l].view(1, 1, -1)
+for l], 1)``.  ATen runs that as four transposed adds and a cat (one more pass over the (B, S, d)
+result), and its backward sums ``level_embed``'s gradient with four ``sum_to_size`` reductions —
+24-71 us each at the bench shape (keep-last-dim reductions over 1-8 K rows on 128 workgroups) —
+plus a zero fill, copy and add per level: ~0.25 ms a step.  Here (bf16 training on the GPU and fp32
+position embeddings) one HIP kernel writes the flattened sum (include/ffn_glue.h,
+mfl_level_pos_flatten) and two write the level embedding's gradient (mfl_level_colsum); the
+position embeddings' gradients are transposed views of the incoming gradient, as autograd's own.
+"""
+import ctypes
+
+import torch
+from torch.autograd import Function
+
+__all__ = ["level_pos_flatten"]
+
+
+def _reference(pos_embeds, level_embed):
+    return torch.cat([p.transpose(1, 2) + level_embed[lvl].view(1, 1, -1) for lvl, p in enumerate(pos_embeds)], 1)
+
+
+class _LevelPosFlatten(Function):
+    @staticmethod
+    def forward(ctx, level_embed, *poses):
+        from ... import _native, _trace
+        _trace.hit("level_pos_flatten")
+        lib = _native.load_library()
+        L = len(poses)
+        B, N = poses[0].shape[0], poses[0].shape[1]
+        T = [p.shape[2] for p in poses]
+        out = torch.empty(B, sum(T), N, dtype=torch.float32, device=level_embed.device)
+        ptrs = (ctypes.c_void_p * L)(*[p.data_ptr() for p in poses])
+        rc = lib.mfl_level_pos_flatten(ptrs, (ctypes.c_int64 * L)(*T), L, B, N, level_embed.data_ptr(), out.data_ptr(),
+                                       _native.stream_handle(out.device))
+        if rc != 0:
+            raise RuntimeError("mfl_level_pos_flatten failed: " + lib.mfl_relu_dropout_last_error().decode())
+        ctx.T, ctx.B, ctx.N = T, B, N
+        ctx.level_embed = level_embed
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ... import _native
+        from .linear import _accum_target, _claim
+        T, B, N = ctx.T, ctx.B, ctx.N
+        L = len(T)
+        nig = ctx.needs_input_grad
+        g = g.contiguous()
+        dlevel = None
+        if nig[0]:
+            lib = _native.load_library()
+            t64 = (ctypes.c_int64 * L)(*T)
+            ws = torch.empty(lib.mfl_level_colsum_workspace_bytes(t64, L, B, N), dtype=torch.uint8, device=g.device)
+            # the trainer's flat gradient view: claimed, or (a second pyramid — the multimodal audio
+            # stream shares level_embed) added into where the first call wrote
+            acc = _accum_target(ctx.level_embed)
+            out = acc if acc is not None else _claim(ctx.level_embed)
+            if out is None:
+                out = torch.empty(ctx.level_embed.shape, dtype=torch.float32, device=g.device)
+            rc = lib.mfl_level_colsum(g.data_ptr(), t64, L, B, N, out.data_ptr(), 1 if acc is not None else 0,
+                                      ws.data_ptr(), _native.stream_handle(g.device))
+            dlevel = None if acc is not None else out
+            if rc != 0:
+                raise RuntimeError("mfl_level_colsum failed: " + lib.mfl_relu_dropout_last_error().decode())
+        dposes, s = [], 0
+        for lvl, t in enumerate(T):
+            dposes.append(g[:, s:s + t].transpose(1, 2) if nig[1 + lvl] else None)
+            s += t
+        return (dlevel, *dposes)
+
+
+def _supported(pos_embeds, level_embed):
+    if not (level_embed.is_cuda and level_embed.dtype == torch.float32 and level_embed.is_contiguous()
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    if not 1 <= len(pos_embeds) <= 16 or level_embed.dim() != 2 or level_embed.shape[0] != len(pos_embeds):
+        return False
+    B, N = pos_embeds[0].shape[0], pos_embeds[0].shape[1]
+    if N % 4 or level_embed.shape[1] != N:
+        return False
+    return all(p.is_cuda and p.device == level_embed.device and p.dtype == torch.float32 and p.dim() == 3
+               and p.is_contiguous() and p.shape[0] == B and p.shape[1] == N and p.shape[2] > 0 for p in pos_embeds)
+
+
+def level_pos_flatten(pos_embeds, level_embed):
+    """``torch.cat([p.transpose(1, 2) + level_embed[l].view(1, 1, -1) for l, p in enumerate(pos_embeds)], 1)``
+    (pos_embeds: (B, d, T_l) per level): the HIP kernels under bf16 autocast on the GPU, the reference
+    composition elsewhere."""
+    if not _supported(pos_embeds, level_embed):
+        return _reference(pos_embeds, level_embed)
+    return _LevelPosFlatten.apply(level_embed, *pos_embeds)

@@ -20,7 +20,7 @@ fp32-accumulated product + bias, as the reference's addmm):
 import torch
 from torch.autograd import Function
 
-from .linear import Linear, _bias_grad, _claim_group, _weight_grad
+from .linear import Linear, _accum_group, _bias_grad, _claim_group, _weight_grad
 
 __all__ = ["layer_values", "layer_values_supported", "linear_group", "linear_group_supported"]
 
@@ -80,12 +80,21 @@ class _LayerValues(Function):
         ws, bs = ctx.params
         # the n layers' weights (biases) back to back in the trainer's flat gradient buffer
         # (flat_groups): the split-K sum (column sums) written straight into that one view
+        # (the same layers used again in this backward: added into the view an earlier call claimed)
         if any(nig[3:3 + n]):
-            dw = _weight_grad(g, x16, _claim_group(ws) if all(nig[3:3 + n]) else None)
-            dws = tuple(dw[i * c_out:(i + 1) * c_out] for i in range(n))
+            acc = _accum_group(ws) if all(nig[3:3 + n]) else None
+            if acc is not None:
+                _weight_grad(g, x16, acc, accumulate=True)
+            else:
+                dw = _weight_grad(g, x16, _claim_group(ws) if all(nig[3:3 + n]) else None)
+                dws = tuple(dw[i * c_out:(i + 1) * c_out] for i in range(n))
         if any(nig[3 + n:3 + 2 * n]):
-            db = _bias_grad(g, _claim_group(bs) if all(nig[3 + n:3 + 2 * n]) else None)
-            dbs = tuple(db[i * c_out:(i + 1) * c_out] for i in range(n))
+            acc = _accum_group(bs) if all(nig[3 + n:3 + 2 * n]) else None
+            if acc is not None:
+                _bias_grad(g, acc, accumulate=True)
+            else:
+                db = _bias_grad(g, _claim_group(bs) if all(nig[3 + n:3 + 2 * n]) else None)
+                dbs = tuple(db[i * c_out:(i + 1) * c_out] for i in range(n))
         return (dx, None, None) + dws + dbs + (None,) * (2 * n)
 
 

@@ -388,8 +388,8 @@ class FlatGradTrainer:
         try:
             # the short-K layers' weight gradients are batched (models/modules/linear.py) and
             # handed over by _deliver, at the model's flush points or after the backward
-            with deferred_weight_grads(self._deliver) as queue, flat_grad_destinations(self._grad_dest,
-                                                                                      self._may_claim):
+            with deferred_weight_grads(self._deliver, self._accum_target) as queue, \
+                    flat_grad_destinations(self._grad_dest, self._may_claim):
                 self._flush_ready()
                 loss.backward()  # overlap: complete buckets are copied and all-reduced from the hooks, in order
                 queue.flush()
@@ -429,17 +429,33 @@ class FlatGradTrainer:
         prev = self._late_parts.get(i)
         self._late_parts[i] = grad if prev is None else prev + grad
 
+    def _reduced(self, p):
+        """Whether p's bucket is reduced (or being reduced) already in this backward."""
+        i = self._index.get(id(p))
+        return (i is not None and self._pending is not None and self._overlap_now
+                and self._bucket_of[i] < self._next_flush)
+
+    def _accum_target(self, p):
+        """Where a batched gradient for p may be added in place (linear._WgradQueue): p.grad while
+        p's bucket is not reduced, else None."""
+        g = p.grad
+        if g is None or self._reduced(p) or g.dtype != torch.float32 or g.shape != p.shape or not g.is_contiguous():
+            return None
+        return g
+
     def _deliver(self, p, grad):
         """A batched weight / bias gradient for parameter p: set (or added to) p.grad, then the
         parameter's post-accumulate step (bucket hand-over) as autograd's hook would run it.  Once
         p's bucket is reduced, the gradient is kept aside instead (never added into the reduced
-        view, which the comm stream may still be reading)."""
+        view, which the comm stream may still be reading).  grad None: the queue already added it
+        into p.grad (_accum_target)."""
         i = self._index.get(id(p))
-        if (i is not None and self._pending is not None and self._overlap_now
-                and self._bucket_of[i] < self._next_flush):
+        if grad is not None and self._reduced(p):
             self._late_add(i, grad)
             return
-        if p.grad is None:
+        if grad is None:
+            pass
+        elif p.grad is None:
             p.grad = grad
         else:
             p.grad.add_(grad)

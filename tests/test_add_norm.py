@@ -471,3 +471,34 @@ def test_backward_ex2_dy_colsum_and_pos_accumulation(dev, rows, d):
     torch.testing.assert_close(dpos, dq16.float() + 0.25, rtol=0, atol=0)
     want = got[1].double().sum(0)
     torch.testing.assert_close(colsum.double(), want, rtol=1e-5, atol=1e-5 * want.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_acc", [False, True])
+def test_carry_entry_matches_composition(dev, with_acc):
+    """add_norm.carry_entry (csrc/add_layernorm.hip carry_entry_*): (src, bf16(src), bf16(src + pos))
+    are autocast's casts of the reference's with_pos_embed (unimodal_deformable_transformer.py:241)
+    bit for bit; src's gradient is the sum of its three gradients, pos's the query's (also through a
+    pos_sink accumulator shared with another consumer)."""
+    g = torch.Generator(device=dev).manual_seed(3)
+    shape = (4, 960, 512)
+    src = torch.randn(shape, device=dev, generator=g, requires_grad=True)
+    pos0 = torch.randn(shape, device=dev, generator=g, requires_grad=True)
+    dr, dv, dq = (torch.randn(shape, device=dev, generator=g) for _ in range(3))
+    dv, dq = dv.bfloat16(), dq.bfloat16()
+    extra = torch.randn(shape, device=dev, generator=g)
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        pos, acc = AN.pos_sink(pos0) if with_acc else (pos0, None)
+        PKG._trace.clear()
+        r, v16, q16 = AN.carry_entry(src, pos, acc)
+        assert PKG._trace.hits.get("carry_entry", 0) == 1
+        other = (pos * 2.0).sum() if with_acc else None  # another consumer of pos (autograd's gradient)
+    assert torch.equal(v16, src.detach().bfloat16()) and torch.equal(q16, (src.detach() + pos0.detach()).bfloat16())
+    loss = (r * dr).sum() + (v16.float() * dv.float()).sum() + (q16.float() * dq.float()).sum()
+    if other is not None:
+        loss = loss + other
+    gs, gp = torch.autograd.grad(loss, [src, pos0])
+    torch.testing.assert_close(gs, dr + dv.float() + dq.float(), rtol=1e-6, atol=1e-6)
+    want_p = dq.float() + (2.0 if with_acc else 0.0)
+    torch.testing.assert_close(gp, want_p, rtol=1e-6, atol=1e-6)
+    del extra

@@ -262,3 +262,29 @@ def test_host_weights_never_reach_native_kernels(dev):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         with pytest.raises(RuntimeError):
             PKG.models.modules.add_norm.add_layer_norm(r, r, norm)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [(1024, 512, 256, 128), (50, 25, 13, 7)])
+def test_level_pos_flatten_matches_reference(dev, T):
+    """models/modules/pyramid.py (mfl_level_pos_flatten / mfl_level_colsum): the flattened level
+    position embedding of prepare_encoder_inputs (reference unimodal_deformable_transformer.py:90-134)
+    is the reference composition bit for bit; its gradients are the reference's (the position
+    embeddings' exactly, the level embedding's per-level column sums up to fp32 summation order)."""
+    pyr = PKG.models.modules.pyramid
+    g = torch.Generator(device=dev).manual_seed(11)
+    B, N = 3, 512
+    poses = [torch.randn(B, N, t, device=dev, generator=g, requires_grad=True) for t in T]
+    emb = torch.randn(len(T), N, device=dev, generator=g, requires_grad=True)
+    go = torch.randn(B, sum(T), N, device=dev, generator=g)
+    PKG._trace.clear()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out = pyr.level_pos_flatten(poses, emb)
+    assert PKG._trace.hits.get("level_pos_flatten", 0) == 1
+    ref = pyr._reference(poses, emb)
+    assert torch.equal(out, ref)
+    got = torch.autograd.grad(out, [emb] + poses, go)
+    want = torch.autograd.grad(ref, [emb] + poses, go)
+    torch.testing.assert_close(got[0], want[0], rtol=1e-5, atol=1e-4)
+    for a, b in zip(got[1:], want[1:]):
+        assert torch.equal(a, b)

@@ -288,3 +288,25 @@ def test_small_gemm_nn_matches_fp32_product(dev, M, N, K):
     assert y2 is not None
     ref2 = dy.float() @ w2[:, :K].float()
     assert ((y2.float() - ref2).abs() <= ref2.abs() * 2 ** -7 + 1e-6).all()
+
+
+@pytest.mark.gpu
+def test_slab_and_column_sums_accumulate(dev):
+    """mfl_sum_slabs_ex / mfl_colsum_ex (include/flat_adamw.h): grouped slab sums, and both sums
+    added into an existing gradient (sum formed first, then added) — the in-place accumulation of a
+    shared layer's weight / bias products (linear._accum_target)."""
+    L = PKG.models.modules.linear
+    g = torch.Generator(device=dev).manual_seed(5)
+    part = torch.randn(3, 4, 64, 32, device=dev, generator=g)
+    out = torch.randn(3, 64, 32, device=dev, generator=g)
+    want = out + part.sum(1)
+    L._sum_slabs(part.view(12, 64, 32), out, accumulate=True, groups=3)
+    torch.testing.assert_close(out, want, rtol=1e-6, atol=1e-6)
+    fresh = L._sum_slabs(part.view(12, 64, 32)[:4])
+    torch.testing.assert_close(fresh, part[0].sum(0), rtol=1e-6, atol=1e-6)
+    for k in (300, 9000):  # one-pass and partials + final column sums
+        g2 = torch.randn(k, 512, device=dev, generator=g).bfloat16()
+        base = torch.randn(512, device=dev, generator=g)
+        want = base + g2.float().sum(0)
+        L._bias_grad(g2, base, accumulate=True)
+        torch.testing.assert_close(base, want, rtol=1e-5, atol=1e-4)

@@ -418,3 +418,38 @@ def test_flat_order_lays_query_projection_pairs_back_to_back():
         for a, b in m.flat_groups():
             assert pos[id(b)] == pos[id(a)] + 1
             assert b.data_ptr() == a.data_ptr() + a.numel() * a.element_size()
+
+
+@pytest.mark.gpu
+def test_shared_layer_gradients_accumulate_into_flat_views(dev, monkeypatch):
+    """configs[2]'s encoder calls one self-attention module four times a layer (the two video calls
+    take the weight-gradient GEMMs, the two short audio ones the deferred queue) and its decoder one
+    cross-attention twice: in the trainer a later call adds its weight / bias products into the flat
+    view an earlier call handed to autograd (linear._accum_target / _accum_group), and the queue adds
+    its batched products into .grad in place (the trainer's _accum_target).  The flat gradient is the
+    one autograd's own accumulation gives (linear.ACCUMULATE_IN_PLACE = False: the same sums, formed
+    then added in the same order)."""
+    small = dict(d_model=64, num_queries=6, feature_dim=64, enc_layers=2, dec_layers=2, ff_dim=128, dropout=0.0)
+    video, vmask, dur = PKG.dvc_core.synthetic_clips(2, T=512, feature_dim=64, padded=True, device=dev)
+    audio, amask, _ = PKG.dvc_core.synthetic_clips(2, T=16, feature_dim=64, padded=True, seed=9, device=dev)
+    batch = (video, vmask, audio, amask, dur)
+
+    def run(in_place):
+        monkeypatch.setattr(PKG.models.modules.linear, "ACCUMULATE_IN_PLACE", in_place)
+        torch.manual_seed(0)
+        model = PKG.dvc_core.MultimodalDVCCore(num_classes=5, **small).to(dev)
+        tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.multimodal_workload_loss, lr=1e-3, use_bf16=True,
+                                            graph=False)
+        PKG._trace.clear()
+        loss = tr._forward_backward(batch)
+        torch.cuda.synchronize()
+        return loss, tr.flat_grad.clone(), dict(PKG._trace.hits), [p.numel() for p in tr.params], tr._offs
+
+    loss_r, ref, hits_r, sizes, offs = run(False)
+    loss, got, hits, _, _ = run(True)
+    assert hits_r.get("grad_accum_view", 0) == 0 and hits_r.get("wgrad_into_grad", 0) == 0, hits_r
+    assert hits.get("grad_accum_view", 0) > 0 and hits.get("wgrad_into_grad", 0) > 0, hits
+    assert torch.equal(loss, loss_r)
+    for i, (n, off) in enumerate(zip(sizes, offs)):
+        a, b = got[off:off + n].double(), ref[off:off + n].double()
+        assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item() + 1e-9, i
