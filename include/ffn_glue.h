@@ -66,6 +66,11 @@ int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t 
  * tensors, out (B, sum T, N) contiguous, start_l the running sum of T.  1 <= L <= 16. */
 int mfl_level_pos_flatten(const float* const* pos, const int64_t* T, int64_t L, int64_t B, int64_t N,
                           const float* level_embed, float* out, void* stream);
+/* As mfl_level_pos_flatten; channels_last (host array of L flags, may be NULL): level l's (B, N, T[l])
+ * tensor is the transposed view of contiguous (B, T[l], N) rows (element (b, c, t) at (b T + t) N + c),
+ * as the position embedding module returns it. */
+int mfl_level_pos_flatten_ex(const float* const* pos, const int* channels_last, const int64_t* T, int64_t L,
+                             int64_t B, int64_t N, const float* level_embed, float* out, void* stream);
 
 /* Its backward for the level embedding: out[l, c] (+)= sum over b and t < T[l] of g[b, start_l + t, c]
  * (g (B, sum T, N) fp32 contiguous, N % 4 == 0, 16-byte aligned; fixed summation order).

@@ -66,6 +66,7 @@ EXPORTED_SYMBOLS = (
     "mfl_relu_dropout_colsum_workspace_bytes",
     "mfl_relu_dropout_backward_colsum",
     "mfl_level_pos_flatten",
+    "mfl_level_pos_flatten_ex",
     "mfl_level_colsum_workspace_bytes",
     "mfl_level_colsum",
     "mfl_relu_dropout_last_error",
@@ -175,6 +176,8 @@ def _declare(lib):
     lib.mfl_carry_entry_backward.argtypes = [vp, vp, vp, i64, vp, vp, i32, vp]
     lib.mfl_level_pos_flatten.restype = i32
     lib.mfl_level_pos_flatten.argtypes = [vp, p64, i64, i64, i64, vp, vp, vp]
+    lib.mfl_level_pos_flatten_ex.restype = i32
+    lib.mfl_level_pos_flatten_ex.argtypes = [vp, vp, p64, i64, i64, i64, vp, vp, vp]
     lib.mfl_level_colsum_workspace_bytes.restype = ctypes.c_size_t
     lib.mfl_level_colsum_workspace_bytes.argtypes = [p64, i64, i64, i64]
     lib.mfl_level_colsum.restype = i32

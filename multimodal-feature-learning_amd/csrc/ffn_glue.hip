@@ -285,6 +285,8 @@ __global__ __launch_bounds__(256) void gather_keep_bwd_kernel(const uint16_t* __
 constexpr int kLpMaxL = 16;
 struct LevelTable {
   const float* pos[kLpMaxL];
+  long long sb[kLpMaxL];  // pos[l] element strides: batch; channel (1 or T, the other is the t stride)
+  int sc1[kLpMaxL];       // 1: channels contiguous ((B, T, N) rows viewed as (B, N, T)), 0: positions contiguous
   int T[kLpMaxL], start[kLpMaxL];
   int blk0[kLpMaxL + 1];  // first workgroup / chunk of each level
   int L, tiles_c;         // levels; 64-column tiles (flatten) or 256-column groups (colsum)
@@ -302,12 +304,21 @@ __global__ __launch_bounds__(256) void level_pos_flatten_kernel(const LevelTable
   const int ct = j % tb.tiles_c, tt = (j / tb.tiles_c) % nt;
   const long long b = j / (tb.tiles_c * nt);
   const int T = tb.T[l], c0 = ct * 64, t0 = tt * kLpT;
-  const float* __restrict__ pl = tb.pos[l] + b * (long long)N * T;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 t-lanes x 8 c-rows
+  const float* __restrict__ pl = tb.pos[l] + b * tb.sb[l];
+  if (tb.sc1[l]) {  // element (c, t) at t N + c: 64 c-lanes x 4 t-rows, coalesced along c
+    const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int c = c0 + ty + 8 * i, t = t0 + tx;
-    tile[ty + 8 * i][tx] = (c < N && t < T) ? pl[(long long)c * T + t] : 0.f;
+    for (int i = 0; i < kLpT / 4; ++i) {
+      const int c = c0 + cx, t = t0 + ry + 4 * i;
+      tile[cx][ry + 4 * i] = (c < N && t < T) ? pl[(long long)t * N + c] : 0.f;
+    }
+  } else {  // element (c, t) at c T + t: 32 t-lanes x 8 c-rows, coalesced along t
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int c = c0 + ty + 8 * i, t = t0 + tx;
+      tile[ty + 8 * i][tx] = (c < N && t < T) ? pl[(long long)c * T + t] : 0.f;
+    }
   }
   __syncthreads();
   const int cx = threadIdx.x & 63, ry = threadIdx.x >> 6;  // 64 c-lanes x 4 t-rows
@@ -498,6 +509,11 @@ int mfl_gather_keep_backward(const void* grad, const int64_t* index, const void*
 
 int mfl_level_pos_flatten(const float* const* pos, const int64_t* T, int64_t L, int64_t B, int64_t N,
                           const float* level_embed, float* out, void* stream) {
+  return mfl_level_pos_flatten_ex(pos, nullptr, T, L, B, N, level_embed, out, stream);
+}
+
+int mfl_level_pos_flatten_ex(const float* const* pos, const int* channels_last, const int64_t* T, int64_t L,
+                             int64_t B, int64_t N, const float* level_embed, float* out, void* stream) {
   g_err[0] = 0;
   LevelTable tb{};
   if (!pos || !T || !level_embed || !out || !level_table(T, L, B, N, kLpT, 64, tb)) {
@@ -510,6 +526,8 @@ int mfl_level_pos_flatten(const float* const* pos, const int64_t* T, int64_t L, 
       return 1;
     }
     tb.pos[l] = pos[l];
+    tb.sb[l] = N * T[l];
+    tb.sc1[l] = channels_last != nullptr && channels_last[l] ? 1 : 0;
   }
   long long S = 0;
   for (int l = 0; l < L; ++l) S += T[l];

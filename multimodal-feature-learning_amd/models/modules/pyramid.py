@@ -33,8 +33,9 @@ class _LevelPosFlatten(Function):
         T = [p.shape[2] for p in poses]
         out = torch.empty(B, sum(T), N, dtype=torch.float32, device=level_embed.device)
         ptrs = (ctypes.c_void_p * L)(*[p.data_ptr() for p in poses])
-        rc = lib.mfl_level_pos_flatten(ptrs, (ctypes.c_int64 * L)(*T), L, B, N, level_embed.data_ptr(), out.data_ptr(),
-                                       _native.stream_handle(out.device))
+        cl = (ctypes.c_int * L)(*[0 if p.is_contiguous() else 1 for p in poses])
+        rc = lib.mfl_level_pos_flatten_ex(ptrs, cl, (ctypes.c_int64 * L)(*T), L, B, N, level_embed.data_ptr(),
+                                          out.data_ptr(), _native.stream_handle(out.device))
         if rc != 0:
             raise RuntimeError("mfl_level_pos_flatten failed: " + lib.mfl_relu_dropout_last_error().decode())
         ctx.T, ctx.B, ctx.N = T, B, N
@@ -81,8 +82,11 @@ def _supported(pos_embeds, level_embed):
     B, N = pos_embeds[0].shape[0], pos_embeds[0].shape[1]
     if N % 4 or level_embed.shape[1] != N:
         return False
+    # (B, N, T) contiguous, or the transposed view of contiguous (B, T, N) rows (the position
+    # embedding's own layout)
     return all(p.is_cuda and p.device == level_embed.device and p.dtype == torch.float32 and p.dim() == 3
-               and p.is_contiguous() and p.shape[0] == B and p.shape[1] == N and p.shape[2] > 0 for p in pos_embeds)
+               and p.shape[0] == B and p.shape[1] == N and p.shape[2] > 0
+               and (p.is_contiguous() or p.transpose(1, 2).is_contiguous()) for p in pos_embeds)
 
 
 def level_pos_flatten(pos_embeds, level_embed):

@@ -274,7 +274,10 @@ def test_level_pos_flatten_matches_reference(dev, T):
     pyr = PKG.models.modules.pyramid
     g = torch.Generator(device=dev).manual_seed(11)
     B, N = 3, 512
-    poses = [torch.randn(B, N, t, device=dev, generator=g, requires_grad=True) for t in T]
+    # level 1 as the position embedding returns it: a transposed view of (B, T, N) rows
+    leaves = [torch.randn((B, t, N) if i == 1 else (B, N, t), device=dev, generator=g, requires_grad=True)
+              for i, t in enumerate(T)]
+    poses = [x.transpose(1, 2) if i == 1 else x for i, x in enumerate(leaves)]
     emb = torch.randn(len(T), N, device=dev, generator=g, requires_grad=True)
     go = torch.randn(B, sum(T), N, device=dev, generator=g)
     PKG._trace.clear()
@@ -283,8 +286,8 @@ def test_level_pos_flatten_matches_reference(dev, T):
     assert PKG._trace.hits.get("level_pos_flatten", 0) == 1
     ref = pyr._reference(poses, emb)
     assert torch.equal(out, ref)
-    got = torch.autograd.grad(out, [emb] + poses, go)
-    want = torch.autograd.grad(ref, [emb] + poses, go)
+    got = torch.autograd.grad(out, [emb] + leaves, go)
+    want = torch.autograd.grad(ref, [emb] + leaves, go)
     torch.testing.assert_close(got[0], want[0], rtol=1e-5, atol=1e-4)
     for a, b in zip(got[1:], want[1:]):
         assert torch.equal(a, b)

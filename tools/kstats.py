@@ -7,7 +7,7 @@ import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
 top = int(sys.argv[2]) if len(sys.argv) > 2 else 25
-steps = sum(int(r["Calls"]) for r in rows if "msda_bwd_pair_kernel" in r["Name"] or "win_bwd_kernel" in r["Name"]) / 6
+steps = sum(int(r["Calls"]) for r in rows if "msda_bwd_pair_kernel" in r["Name"] or "win_bwd_kernel" in r["Name"] or "win_lm_kernel" in r["Name"]) / 6
 cat = collections.Counter()
 calls = collections.Counter()
 for r in rows:
