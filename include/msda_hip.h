@@ -52,6 +52,8 @@ extern "C" {
 #define MSDA_OK 0
 #define MSDA_ERR_ARG 1    /* bad size / dtype / pointer                          */
 #define MSDA_ERR_LAUNCH 2 /* hipGetLastError after a launch                       */
+#define MSDA_ERR_UNSUPPORTED 3 /* a valid request this call's kernel path cannot honour (ABI v8:
+                                  msda_hip_backward_ex's strided grad_value); nothing was launched */
 
 #define MSDA_MAX_LEVELS 16
 
@@ -99,6 +101,20 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
                       void* grad_loc, void* grad_attn, void* workspace, int64_t batch,
                       int64_t spatial_size, int64_t num_heads, int64_t channels,
                       int64_t num_query, int64_t num_point, int padding_mode, void* stream);
+
+/* ABI v8: msda_hip_backward with grad_value rows grad_value_row_stride elements apart (element
+ * (b, s, h, c) at (b * spatial_size + s) * grad_value_row_stride + h * channels + c; a multiple of 8,
+ * >= num_heads * channels; 0 = contiguous): lets a caller collect several calls' value gradients
+ * side by side in one buffer (the decoder layers' value projections read them as one GEMM operand,
+ * models/modules/value_proj.py) without a stacking copy.  Honoured by the per-tap fused backward
+ * (sparse / decoder-like calls); other calls return MSDA_ERR_UNSUPPORTED and launch nothing. */
+int msda_hip_backward_ex(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                         const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                         const void* attn_weight, const void* grad_output, void* grad_value,
+                         void* grad_loc, void* grad_attn, void* workspace, int64_t batch,
+                         int64_t spatial_size, int64_t num_heads, int64_t channels,
+                         int64_t num_query, int64_t num_point, int padding_mode, int64_t grad_value_row_stride,
+                         void* stream);
 
 /* Forward that also hands the backward its row intervals (ABI v5; an extension: the reference's
  * extension has no forward-to-backward state beyond the saved inputs).  For calls whose backward

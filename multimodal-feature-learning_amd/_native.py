@@ -21,12 +21,13 @@ DTYPE_TAGS = {torch.float32: 0, torch.float64: 1, torch.bfloat16: 2, torch.float
 PAD_TAGS = {"border": 0, "zeros": 1}
 COORD_API, COORD_LEVEL_MAJOR = 0, 1
 MAX_LEVELS = 16
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # every symbol include/msda_hip.h declares (checked by tests/test_capi.py)
 EXPORTED_SYMBOLS = (
     "msda_hip_forward",
     "msda_hip_backward",
+    "msda_hip_backward_ex",
     "msda_hip_backward_workspace_bytes",
     "msda_hip_forward_tiles_bytes",
     "msda_hip_forward_tiles",
@@ -100,6 +101,9 @@ def _declare(lib):
     lib.msda_hip_backward.restype = i32
     lib.msda_hip_backward.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp, vp, vp, vp,
                                       i64, i64, i64, i64, i64, i64, i32, vp]
+    lib.msda_hip_backward_ex.restype = i32
+    lib.msda_hip_backward_ex.argtypes = [vp, i32, p64, p64, i64, vp, vp, vp, vp, vp, vp, vp,
+                                         i64, i64, i64, i64, i64, i64, i32, i64, vp]
     lib.msda_hip_forward_tiles_bytes.restype = ctypes.c_size_t
     lib.msda_hip_forward_tiles_bytes.argtypes = [i32, p64, i64, i64, i64, i64, i64, i64, i64]
     lib.msda_hip_forward_tiles.restype = i32
@@ -243,6 +247,9 @@ def load_library():
 
 def last_error():
     return load_library().msda_hip_last_error().decode(errors="replace")
+
+
+MSDA_ERR_UNSUPPORTED = 3  # include/msda_hip.h
 
 
 def check(rc, what):

@@ -1395,7 +1395,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
     const scalar_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     const scalar_t* __restrict__ gout, scalar_t* __restrict__ gval, float* __restrict__ gloc,
     float* __restrict__ gaw, const Levels lv, const int L, const int P, const int S, const int M,
-    const int D, const int Lq, const int sort_rows) {
+    const int D, const int Lq, const int sort_rows, const int gv_rs) {
   static_assert(NSLOT > 0, "fused backward needs whole 16-byte chunks per lane");
   extern __shared__ __attribute__((aligned(16))) unsigned char smem_raw[];
   const unsigned blk = xcd_block(blockIdx.x, gridDim.x);
@@ -1522,7 +1522,9 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
   const scalar_t* __restrict__ gb = gout + (b * Lq * M + m) * (long long)D + c_l * CPL;
   const long long vofs = ((b * S + lv.start[l]) * M + m) * (long long)D + c_l * CPL;
   const scalar_t* __restrict__ vl = value + vofs;
-  scalar_t* __restrict__ gvl = gval + vofs;
+  // grad_value rows gv_rs elements apart (M * D, or a caller's strided slot: the decoder layers'
+  // stacked value gradients, models/modules/value_proj.py)
+  scalar_t* __restrict__ gvl = gval + ((b * S + lv.start[l]) * gv_rs + (long long)m * D + c_l * CPL);
   // Per wave iteration NS slots of LPR lanes; SPR consecutive slots share one value row
   // (slots-per-row, from the level's average taps per row: 1 for the fine levels, up to NS for
   // the coarsest), each taking every SPR-th entry of the row's list, so a long row is not walked
@@ -1589,7 +1591,7 @@ __global__ __launch_bounds__(kGvThreads) void msda_bwd_fused_kernel(
         a[2 * e] = acc[e].x;
         a[2 * e + 1] = acc[e].y;
       }
-      store_vec_nt<scalar_t, CPL>(gvl + row * rs, a);
+      store_vec_nt<scalar_t, CPL>(gvl + row * gv_rs, a);
     }
   }
   MSDA_PH(5);
@@ -2487,6 +2489,7 @@ __global__ __launch_bounds__(256) void msda_bwd_coord_kernel(
 struct Problem {
   long long B, S, M, D, Lq, L, P;
   Levels lv;
+  long long gv_rs = 0;  // grad_value row stride in elements (0: M * D, the contiguous layout)
 };
 
 int check_problem(const int64_t* shapes, const int64_t* starts, int64_t L, int64_t B,
@@ -3000,6 +3003,7 @@ int run_backward_fused(const Problem& pr, int ns, const void* value, const void*
   // gathers per batch: 8 when the finest level's rows average >= 8 taps (encoder-like
   // calls), 4 for sparse levels (decoder-like: few taps per row, row-set changes dominate)
   const bool wide = (long long)2 * pr.Lq * pr.P >= 8LL * maxT;
+  const int gv_rs = (int)(pr.gv_rs > 0 ? pr.gv_rs : pr.M * pr.D);
 #ifndef MSDA_FUSED_UW
 #define MSDA_FUSED_UW 8
 #endif
@@ -3009,7 +3013,7 @@ int run_backward_fused(const Problem& pr, int ns, const void* value, const void*
     hipLaunchKernelGGL((msda_bwd_fused_kernel<scalar_t, NSL, Z, C, UU>), dim3(blocks),          \
                        dim3(kGvThreads), lds, st, v, lc, a, g, gv, gl, ga, pr.lv, (int)pr.L,      \
                        (int)pr.P, (int)pr.S, (int)pr.M, (int)pr.D, (int)pr.Lq,                  \
-                       deterministic_rows);                                                     \
+                       deterministic_rows, gv_rs);                                              \
   } while (0)
 #define MSDA_FU(NSL, Z, C)                                                                        \
   do {                                                                                          \
@@ -3259,6 +3263,14 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     int minT = 1 << 30;
     for (int l = 0; l < pr.L; ++l) minT = min(minT, pr.lv.T[l]);
     const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1) || pr.Lq * pr.P <= 512;
+    if (pr.gv_rs > 0 && pr.gv_rs != pr.M * pr.D) {
+      // a strided grad_value: only the per-tap fused kernel writes it (the calls that ask for it,
+      // the decoders' cross-attentions, take that path); others report it unsupported
+      if (gval != nullptr && ns > 0 && sparse && layout == MSDA_COORD_API && tiles == nullptr)
+        return run_backward_fused<scalar_t>(pr, ns, value, loc, aw, gout, gval, gloc, gaw, pad, st);
+      set_error("msda backward: a strided grad_value needs the fused per-tap path");
+      return MSDA_ERR_UNSUPPORTED;
+    }
     if constexpr (std::is_same<scalar_t, bf16_t>::value) {
       // (gval may be null: the row-block kernel then writes the coordinate gradients only)
       if ((workspace != nullptr || tiles != nullptr) && win_takes(pr, value_dtype)) {
@@ -3294,6 +3306,10 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
       return run_backward_pair<scalar_t>(pr, pp, value, loc, aw, gout, gval, gloc, gaw, workspace, pad, st);
     if (ns > 0)
       return run_backward_fused<scalar_t>(pr, ns, value, loc, aw, gout, gval, gloc, gaw, pad, st);
+  }
+  if (pr.gv_rs > 0 && pr.gv_rs != pr.M * pr.D) {
+    set_error("msda backward: a strided grad_value needs the fused per-tap path");
+    return MSDA_ERR_UNSUPPORTED;
   }
   SideStream* side = nullptr;
   // worth a fork / join (~5 us) only when the coordinate kernel is long (encoder-sized calls)
@@ -4035,7 +4051,7 @@ hipError_t zero_f32(float* p, long long n, hipStream_t st) {
 
 extern "C" {
 
-int msda_hip_abi_version(void) { return 7; }
+int msda_hip_abi_version(void) { return 8; }
 
 const char* msda_hip_last_error(void) { return g_last_error; }
 
@@ -4272,12 +4288,19 @@ static int backward_entry(const void* value, int value_dtype, const int64_t* spa
                           void* grad_loc, void* grad_attn, void* workspace, const void* tiles, int64_t batch,
                           int64_t spatial_size, int64_t num_heads, int64_t channels,
                           int64_t num_query, int64_t num_point, int padding_mode, void* stream,
-                          int layout = MSDA_COORD_API) {
+                          int layout = MSDA_COORD_API, int64_t gval_row_stride = 0) {
   g_last_error[0] = 0;
   Problem pr;
   int rc = check_problem(spatial_shapes, level_start, num_levels, batch, spatial_size, num_heads,
                          channels, num_query, num_point, &pr);
   if (rc) return rc;
+  if (gval_row_stride != 0 && (gval_row_stride < pr.M * pr.D || gval_row_stride % 8 != 0 ||
+                               pr.B * pr.S * gval_row_stride >= (1LL << 31))) {
+    set_error("msda_hip_backward_ex: grad_value row stride must be >= num_heads * channels, a multiple of 8, "
+              "and the strided grad_value under 2^31 elements");
+    return MSDA_ERR_ARG;
+  }
+  pr.gv_rs = gval_row_stride;
   if (padding_mode != MSDA_PAD_BORDER && padding_mode != MSDA_PAD_ZEROS) {
     set_error("msda: unknown padding_mode %d", padding_mode);
     return MSDA_ERR_ARG;
@@ -4358,6 +4381,19 @@ int msda_hip_backward(const void* value, int value_dtype, const int64_t* spatial
   return backward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
                         grad_output, grad_value, grad_loc, grad_attn, workspace, nullptr, batch, spatial_size,
                         num_heads, channels, num_query, num_point, padding_mode, stream);
+}
+
+int msda_hip_backward_ex(const void* value, int value_dtype, const int64_t* spatial_shapes,
+                         const int64_t* level_start, int64_t num_levels, const void* sampling_loc,
+                         const void* attn_weight, const void* grad_output, void* grad_value,
+                         void* grad_loc, void* grad_attn, void* workspace, int64_t batch,
+                         int64_t spatial_size, int64_t num_heads, int64_t channels,
+                         int64_t num_query, int64_t num_point, int padding_mode, int64_t grad_value_row_stride,
+                         void* stream) {
+  return backward_entry(value, value_dtype, spatial_shapes, level_start, num_levels, sampling_loc, attn_weight,
+                        grad_output, grad_value, grad_loc, grad_attn, workspace, nullptr, batch, spatial_size,
+                        num_heads, channels, num_query, num_point, padding_mode, stream, MSDA_COORD_API,
+                        grad_value_row_stride);
 }
 
 int msda_hip_backward_tiles(const void* value, int value_dtype, const int64_t* spatial_shapes,

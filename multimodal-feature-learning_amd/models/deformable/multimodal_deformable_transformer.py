@@ -267,6 +267,30 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
         attn = self.cross_attn(self.with_pos_embed(tgt, query_pos), ref, src, shapes, starts, mask, value=value)
         return add_layer_norm(tgt, attn, self.norm1, dropout=self.dropout1)
 
+    def forward_carry(self, tgt, query_pos, reference_points_input_video, reference_points_input_audio, query_mask,
+                      video_src, video_temporal_shapes, video_level_start_index, video_src_padding_mask, audio_src,
+                      audio_temporal_shapes, audio_level_start_index, audio_src_padding_mask, video_value=None,
+                      audio_value=None, carried=None, pos_acc=None):
+        """``forward`` returning ``(out, out16, q16)`` with the bf16 operands carried between the fused
+        add + LayerNorms (bf16 autocast on the GPU): the self-attention add + LayerNorm hands both
+        cross-attentions ONE query bf16(tgt + query_pos) (no pos adds or casts, its two gradients
+        summed by autograd once), the FFN's the next layer's self-attention inputs (``carried``);
+        query_pos's gradient summed in place (``pos_acc``, add_norm.pos_sink).  Same math as
+        ``forward`` (reference :410-432)."""
+        sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask, carried)
+        tgt, _, q16 = add_layer_norm_carry(tgt, sa, self.norm2, query_pos, self.dropout2, pos_acc=pos_acc)
+        query = q16 if q16 is not None else tgt
+        ca_v = self.cross_attn(query, reference_points_input_video, video_src, video_temporal_shapes,
+                               video_level_start_index, video_src_padding_mask, value=video_value)
+        tgt_video = add_layer_norm(tgt, ca_v, self.norm1, dropout=self.dropout1)
+        ca_a = self.cross_attn(query, reference_points_input_audio, audio_src, audio_temporal_shapes,
+                               audio_level_start_index, audio_src_padding_mask, value=audio_value)
+        tgt_audio = add_layer_norm(tgt, ca_a, self.norm1, dropout=self.dropout1)
+        bridged = self.linear3(self.norm4(torch.cat([tgt_video, tgt_audio], dim=-1)))
+        t = relu_dropout(bridged, self.activation, self.dropout5)
+        hidden = relu_dropout(self.linear1(t), self.activation, self.dropout3)
+        return add_layer_norm_carry(t, self.linear2(hidden), self.norm3, query_pos, self.dropout4, pos_acc=pos_acc)
+
     def forward(self, tgt, query_pos, reference_points_input_video, reference_points_input_audio, query_mask,
                 video_src, video_temporal_shapes, video_level_start_index, video_src_padding_mask, audio_src,
                 audio_temporal_shapes, audio_level_start_index, audio_src_padding_mask, video_value=None,
@@ -314,13 +338,29 @@ class MultimodalDeformableTransformerDecoder(nn.Module):
             # every layer projects the same two memories: one batched GEMM each way per memory
             vvals = layer_values(attns, video_src, video_padding_mask)
             avals = layer_values(attns, audio_src, audio_padding_mask)
+        carry = (all(type(layer) is MultimodalDeformableTransformerDecoderLayer for layer in self.layers)
+                 and carry_supported(output, self.layers[0].norm2)
+                 and (query_pos is None or (query_pos.shape == output.shape and query_pos.dtype == torch.float32)))
+        carried = pos_acc = None
+        if carry:
+            if query_pos is not None and not query_pos.is_contiguous():
+                query_pos = query_pos.contiguous()  # once, not per layer (the fused layers read it flat)
+            query_pos, pos_acc = pos_sink(query_pos)  # its gradient summed in place (add_norm.pos_sink)
         for lid, layer in enumerate(self.layers):
             ref_v = self._per_level(reference_points, video_valid_ratios)
             ref_a = self._per_level(reference_points, audio_valid_ratios)
             extra = {} if vvals is None else {"video_value": vvals[lid], "audio_value": avals[lid]}
-            output = layer(output, query_pos, ref_v, ref_a, query_padding_mask, video_src, video_temporal_shapes,
-                           video_level_start_index, video_padding_mask, audio_src, audio_temporal_shapes,
-                           audio_level_start_index, audio_padding_mask, **extra)
+            if carry:
+                # bf16 operands carried between the fused add + LayerNorms (forward_carry)
+                output, out16, q16 = layer.forward_carry(
+                    output, query_pos, ref_v, ref_a, query_padding_mask, video_src, video_temporal_shapes,
+                    video_level_start_index, video_padding_mask, audio_src, audio_temporal_shapes,
+                    audio_level_start_index, audio_padding_mask, carried=carried, pos_acc=pos_acc, **extra)
+                carried = (out16, q16)
+            else:
+                output = layer(output, query_pos, ref_v, ref_a, query_padding_mask, video_src, video_temporal_shapes,
+                               video_level_start_index, video_padding_mask, audio_src, audio_temporal_shapes,
+                               audio_level_start_index, audio_padding_mask, **extra)
             if not disable_iterative_refine and self.bbox_head is not None:
                 delta = self.bbox_head[lid](output)
                 if reference_points.shape[-1] == 2:

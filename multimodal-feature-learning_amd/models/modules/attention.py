@@ -214,7 +214,10 @@ class MSDeformAttn(nn.Module):
             value = self.value_proj(input_flatten)
             if input_padding_mask is not None:
                 value = mask_padding_rows(value, input_padding_mask)
+        dest = getattr(value, "_mfl_grad_dest", None)  # (value_proj.layer_values' gradient slot)
         value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
+        if dest is not None:
+            value._mfl_grad_dest = dest.view(value.shape)
 
         a, b = self.sampling_offsets, self.attention_weights
         dt = a._autocast_dtype(query) if isinstance(a, Linear) else None

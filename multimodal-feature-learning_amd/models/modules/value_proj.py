@@ -63,15 +63,35 @@ class _LayerValues(Function):
         ctx.save_for_backward(x16, torch.cat(wcs, 0), mask)
         ctx.n, ctx.x_shape, ctx.x_dtype, ctx.c_out = n, x.shape, x.dtype, c_out
         ctx.params = (w, b)  # (the parameters whose flat gradient views the backward may claim)
-        return tuple(torch.ops.aten._unsafe_view(y[i], (*lead, c_out)) for i in range(n))
+        outs = tuple(torch.ops.aten._unsafe_view(y[i], (*lead, c_out)) for i in range(n))
+        if x.is_cuda:
+            # the backward's G = [g_1 | ... | g_n]: each layer's value gradient may be written straight
+            # into its column block (the MSDA backward's strided grad_value, msda_hip_backward_ex)
+            # instead of stacked afterwards (a (tokens x n d) copy)
+            G = torch.empty(k, n * c_out, dtype=dt, device=x.device)
+            slots = G.view(k, n, c_out)
+            for i, o in enumerate(outs):
+                o._mfl_grad_dest = slots[:, i].view(*lead, c_out)
+            ctx.G = G
+        else:
+            ctx.G = None
+        return outs
 
     @staticmethod
     def backward(ctx, *gs):
         x16, wcat, mask = ctx.saved_tensors
         n, c_out = ctx.n, ctx.c_out
         k = x16.shape[0]
-        g = torch.stack([gi.reshape(k, c_out).to(wcat.dtype) if gi is not None
-                         else x16.new_zeros(k, c_out) for gi in gs], dim=1).view(k, n * c_out)
+        G, ctx.G = ctx.G, None
+        if G is not None and all(gi is not None and gi.dtype == G.dtype and gi.data_ptr() == G.data_ptr() + i * c_out *
+                                 G.element_size() and gi.reshape(k, c_out).stride() == (n * c_out, 1)
+                                 for i, gi in enumerate(gs)):
+            from ... import _trace
+            _trace.hit("layer_values_slots")
+            g = G  # every layer's gradient already in its column block
+        else:
+            g = torch.stack([gi.reshape(k, c_out).to(wcat.dtype) if gi is not None
+                             else x16.new_zeros(k, c_out) for gi in gs], dim=1).view(k, n * c_out)
         if mask is not None:
             _zero_rows(g, 1, k, mask)
         nig = ctx.needs_input_grad

@@ -238,11 +238,73 @@ def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_til
     return (out, tiles) if want_tiles else out
 
 
+def _strided_slot(dest, value):
+    """dest's row stride when it is a (B, S, M, D) view with value's shape and dtype whose rows are
+    whole (h, c) blocks a fixed stride apart (msda_hip_backward_ex), else 0."""
+    if dest is None or dest.shape != value.shape or dest.dtype != value.dtype or dest.device != value.device:
+        return 0
+    B, S, M, D = value.shape
+    st = dest.stride()
+    rs = st[1]
+    if st[3] != 1 or st[2] != D or st[0] != S * rs or rs < M * D or rs % 8 or dest.data_ptr() % 16:
+        return 0
+    return rs
+
+
 def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="border",
-                  need_value=True, need_loc=True, need_aw=True, tiles=None, layout=0):
+                  need_value=True, need_loc=True, need_aw=True, tiles=None, layout=0, grad_value_out=None):
     """(grad_value, grad_loc, grad_aw) of msda_forward; unneeded ones come back None.
     ``tiles``: the row intervals ``msda_forward(..., want_tiles=True)`` returned for these inputs
-    (required with ``layout=LEVEL_MAJOR``; grad_loc / grad_aw then come back level-major too)."""
+    (required with ``layout=LEVEL_MAJOR``; grad_loc / grad_aw then come back level-major too).
+    ``grad_value_out``: a strided (B, S, M, D) slot to write grad_value into (msda_hip_backward_ex;
+    the decoder layers' stacked value gradients): returned as grad_value when the call's kernel path
+    writes it, else ignored (a fresh grad_value comes back)."""
+    rs = _strided_slot(grad_value_out, value) if need_value and layout == 0 and tiles is None else 0
+    if rs:
+        rc_ex = _backward_ex(value, shapes, starts, loc, aw, grad_output, padding_mode, need_loc, need_aw,
+                             grad_value_out, rs)
+        if rc_ex is not None:
+            return rc_ex
+    return _backward(value, shapes, starts, loc, aw, grad_output, padding_mode, need_value, need_loc, need_aw,
+                     tiles, layout)
+
+
+def _backward_ex(value, shapes, starts, loc, aw, grad_output, padding_mode, need_loc, need_aw, gv, rs):
+    """msda_hip_backward_ex into the strided slot gv; None when the call's path does not take it."""
+    _check_inputs(value, loc, aw, shapes, starts, 0)
+    grad_output = grad_output.to(value.dtype).contiguous()
+    B, S, M, D = value.shape
+    Lq, _, L, P = _coord_dims(loc, 0)
+    if tuple(grad_output.shape) != (B, Lq, M * D):
+        raise ValueError(f"grad_output must be {(B, Lq, M * D)}, got {tuple(grad_output.shape)}")
+    lib = _native.load_library()
+    gl = torch.empty_like(loc) if need_loc else None
+    ga = torch.empty_like(aw) if need_aw else None
+    ws = None
+    nbytes = lib.msda_hip_backward_workspace_bytes(_native.DTYPE_TAGS[value.dtype], B, S, M, D, Lq, L, P)
+    if nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=value.device)
+    ptr = lambda t: None if t is None else t.data_ptr()  # noqa: E731
+    timer = _timer
+    if timer is not None:
+        ev0 = timer._begin()
+    rc = lib.msda_hip_backward_ex(value.data_ptr(), _native.DTYPE_TAGS[value.dtype], _native.host_i64_array(shapes),
+                                  _native.host_i64_array(starts), L, loc.data_ptr(), aw.data_ptr(),
+                                  grad_output.data_ptr(), gv.data_ptr(), ptr(gl), ptr(ga), ptr(ws), B, S, M, D, Lq, P,
+                                  _native.PAD_TAGS[padding_mode], rs, _native.stream_handle(value.device))
+    if rc == _native.MSDA_ERR_UNSUPPORTED:
+        return None
+    _native.check(rc, "msda_hip_backward_ex")
+    if timer is not None:
+        timer._end("bwd", (S, Lq), algorithmic_bytes("bwd", B, S, M, D, Lq, L, P, value.element_size()), ev0,
+                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()))
+    from . import _trace
+    _trace.hit("msda_grad_value_slot")
+    return gv, gl, ga
+
+
+def _backward(value, shapes, starts, loc, aw, grad_output, padding_mode, need_value, need_loc, need_aw, tiles,
+              layout):
     _check_inputs(value, loc, aw, shapes, starts, layout)
     grad_output = grad_output.to(value.dtype).contiguous()
     B, S, M, D = value.shape
@@ -296,6 +358,8 @@ class MSDAFunction(Function):
             _trace.hit("msda_level_major")
         ctx.meta = (shapes, starts, padding_mode, layout)
         ctx.save_for_backward(value, loc, aw)
+        # a strided slot for grad_value offered by value's producer (value_proj.layer_values)
+        ctx.gdest = getattr(value, "_mfl_grad_dest", None)
         # the row intervals of the row-block backward come with the forward (it reads loc anyway)
         if any(ctx.needs_input_grad[:3]) or layout == LEVEL_MAJOR:
             out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode, want_tiles=True,
@@ -310,10 +374,12 @@ class MSDAFunction(Function):
         value, loc, aw = ctx.saved_tensors
         shapes, starts, padding_mode, layout = ctx.meta
         nv, nl, na = ctx.needs_input_grad[:3]
+        gdest, ctx.gdest = ctx.gdest, None
         gv, gl, ga = msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode,
-                                   need_value=nv, need_loc=nl, need_aw=na, tiles=ctx.tiles, layout=layout)
+                                   need_value=nv, need_loc=nl, need_aw=na, tiles=ctx.tiles, layout=layout,
+                                   grad_value_out=gdest)
         ctx.tiles = None
-        if gv is not None:
+        if gv is not None and gv is not gdest:
             gv._mfl_private = True  # fresh, referenced by nothing else: consumers may write it in place
         return gv, gl, ga, None, None, None, None
 

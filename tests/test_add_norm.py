@@ -502,3 +502,50 @@ def test_carry_entry_matches_composition(dev, with_acc):
     want_p = dq.float() + (2.0 if with_acc else 0.0)
     torch.testing.assert_close(gp, want_p, rtol=1e-6, atol=1e-6)
     del extra
+
+
+@pytest.mark.gpu
+def test_multimodal_decoder_carry_matches_uncarried(dev, monkeypatch):
+    """Multimodal decoder stack with the bf16 operands carried between its fused add + LayerNorms
+    (MultimodalDeformableTransformerDecoderLayer.forward_carry: one bf16(tgt + query_pos) for both
+    cross-attentions, query_pos's gradient summed in place) against the layer-by-layer stack: forward
+    bit-identical (dropout 0); gradients held to the fp32 run as in the encoder test above."""
+    MT = PKG.models.deformable.multimodal_deformable_transformer
+    torch.manual_seed(5)
+    B, d, Q, vs, as_ = 2, 512, 30, [128, 64, 32, 16], [50, 25, 13, 7]
+    layer = MT.MultimodalDeformableTransformerDecoderLayer(d, 1024, 0.0, "relu", 4, 8, 4)
+    dec = MT.MultimodalDeformableTransformerDecoder(layer, 3, return_intermediate=True).to(dev)
+
+    def meta(shapes):
+        ts = torch.tensor(shapes, device=dev)
+        return ts, torch.cat([ts.new_zeros(1), ts.cumsum(0)[:-1]])
+    vts, vlsi = meta(vs)
+    ats, alsi = meta(as_)
+    ones = torch.ones(B, 4, device=dev)
+    t0, qp0 = torch.randn(B, Q, d, device=dev), torch.randn(B, Q, d, device=dev)
+    ref = torch.rand(B, Q, 1, device=dev)
+    qmask = torch.ones(B, Q, dtype=torch.bool, device=dev)
+    mv0, ma0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
+    w = torch.randn(d, device=dev)
+
+    def run(amp=True):
+        dec.zero_grad(set_to_none=True)
+        t, qp = t0.clone().requires_grad_(True), qp0.clone().requires_grad_(True)
+        mv, ma = mv0.clone().requires_grad_(True), ma0.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            hs, _ = dec(t, ref, qp, qmask, mv, vts, vlsi, ones, None, ma, ats, alsi, ones, None)
+        (hs.float() * w).sum().backward()
+        return hs.detach(), [t.grad, qp.grad, mv.grad, ma.grad] + [p.grad.clone() for p in dec.parameters()
+                                                                   if p.grad is not None]
+
+    PKG._trace.clear()
+    o1, g1 = run()
+    assert PKG._trace.hits.get("add_ln_carry", 0) >= 6  # two carried add + LayerNorms per layer
+    monkeypatch.setattr(MT, "carry_supported", lambda *a: False)
+    o2, g2 = run()
+    _, g3 = run(amp=False)
+    torch.testing.assert_close(o1, o2, rtol=0, atol=0)
+    assert len(g1) == len(g2) == len(g3)
+    for a, b, c in zip(g1, g2, g3):
+        torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -7 * b.abs().max().item())
+        assert (a - c).norm() <= 1.25 * (b - c).norm() + 1e-6 * c.norm()

@@ -755,3 +755,90 @@ def test_lds_staged_forward_equals_gather_forward(dev, monkeypatch, case, paddin
         monkeypatch.setenv("MSDA_HIP_FWD_LDS", flag)
         runs.append(msda.msda_forward(v, shapes, starts, lc, a, padding, want_tiles=True))
     assert torch.equal(runs[0][0], runs[1][0]) and torch.equal(runs[0][1], runs[1][1])
+
+
+@pytest.mark.gpu
+def test_strided_grad_value_slot_matches_contiguous(dev):
+    """msda_hip_backward_ex (ABI v8): a decoder-like call (the per-tap fused backward) writes
+    grad_value into a strided column block of a wider buffer — the decoder layers' stacked value
+    gradients (value_proj.layer_values) — with the values of the contiguous backward and nothing
+    outside the block touched; an encoder-like call, whose path cannot write the slot, reports it and
+    the wrapper returns a fresh grad_value instead."""
+    B, M, D, P, n = 8, 8, 64, 4, 3  # (B M L >= 256: the fused path's own condition)
+    for shapes, Lq, slot_expected in (([64, 32, 16, 8], 50, True), ([256, 128, 64, 32], 480, False)):
+        starts = O.level_starts(shapes)
+        S = sum(shapes)
+        value, loc, aw, gout = (t.to(dev) for t in rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, 41))
+        G = torch.full((B * S, n * M * D), float("nan"), dtype=torch.bfloat16, device=dev)
+        slot = G.view(B * S, n, M * D)[:, 1].view(B, S, M, D)
+        PKG._trace.clear()
+        gv, gl, ga = msda.msda_backward(value, shapes, starts, loc, aw, gout, grad_value_out=slot)
+        want_v, want_l, want_a = msda.msda_backward(value, shapes, starts, loc, aw, gout)
+        torch.cuda.synchronize()
+        took = PKG._trace.hits.get("msda_grad_value_slot", 0) == 1
+        assert took == slot_expected and (gv is slot) == slot_expected
+        # (per-row fp32 sums in list order: the fused kernel's order may differ run to run)
+        torch.testing.assert_close(gv.float(), want_v.float(), rtol=1e-2, atol=1e-2)
+        torch.testing.assert_close(gl, want_l, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(ga, want_a, rtol=1e-4, atol=1e-4)
+        others = G.view(B * S, n, M * D)[:, [0, 2]]
+        assert torch.isnan(others.float()).all()
+        if not slot_expected:
+            assert torch.isnan(slot.float()).all()
+
+
+@pytest.mark.gpu
+def test_bf16_unsorted_topk_call_takes_row_block_correctly(dev, monkeypatch):
+    """win_applies' clause for Lq P >= 2048 on >= 64-row levels also takes query sets that
+    are NOT position-ordered (each tile's intervals then span a whole level).  The same 577-of-1920
+    top-k call as the sparse bench line with the tokens in random (score) order: the row-block backward
+    still matches the oracle, and its time is reported against the pair kernel's on the same inputs
+    (MSDA_HIP_BWD_WIN=0) — allowed to be slower, not pathologically (<= 4x)."""
+    for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH",
+              "MSDA_HIP_QORDER"):
+        monkeypatch.delenv(k, raising=False)
+    shapes, B, M, D, P, Lq = [1024, 512, 256, 128], 8, 8, 64, 4, 577
+    S = sum(shapes)
+    value, _, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=115, lo=0.0, hi=1.0)
+    pos = torch.cat([(torch.arange(T, dtype=torch.float64) + 0.5) / T for T in shapes])
+    gen = torch.Generator().manual_seed(116)
+    loc = torch.empty(B, Lq, M, len(shapes), P, dtype=torch.float64)
+    for b in range(B):
+        tok = torch.randperm(S, generator=gen)[:Lq]  # score order: no sort by position
+        for l, T in enumerate(shapes):
+            off = (torch.rand(Lq, M, P, generator=gen, dtype=torch.float64) * 8 - 4) / T
+            loc[b, :, :, l] = pos[tok][:, None, None] + off
+    loc = loc.float()
+    starts = O.level_starts(shapes)
+    vd, ld, ad, gd = value.cuda(), loc.cuda(), aw.cuda(), gout.cuda()
+    lib = PKG._native.load_library()
+    nb = lib.msda_hip_forward_tiles_bytes(PKG._native.DTYPE_TAGS[torch.bfloat16], PKG._native.host_i64_array(shapes),
+                                          len(shapes), B, S, M, D, Lq, P)
+    assert nb > 0  # the row-block path takes it
+
+    def timed(env):
+        if env is None:
+            monkeypatch.delenv("MSDA_HIP_BWD_WIN", raising=False)
+        else:
+            monkeypatch.setenv("MSDA_HIP_BWD_WIN", env)
+        _, tiles = msda.msda_forward(vd, shapes, starts, ld, ad, want_tiles=True)
+        res = msda.msda_backward(vd, shapes, starts, ld, ad, gd, tiles=tiles)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            msda.msda_backward(vd, shapes, starts, ld, ad, gd, tiles=tiles)
+        e1.record()
+        torch.cuda.synchronize()
+        return res, e0.elapsed_time(e1) / 10 * 1e3
+
+    (gv, gl, ga), t_win = timed(None)
+    _, t_pair = timed("0")
+    print(f"unsorted top-k backward: row-block {t_win:.1f} us, pair {t_pair:.1f} us")
+    assert t_win <= 4 * t_pair, (t_win, t_pair)
+    eps = 2 ** -8
+    v32, g32 = value[:1].float(), gout[:1].float()
+    r_gv, r_gl, r_ga = O.msda_backward(_np(v32), shapes, _np(loc[:1]), _np(aw[:1]), _np(g32))
+    np.testing.assert_allclose(_np(gv[:1]), r_gv, rtol=eps, atol=eps * np.abs(r_gv).max())
+    np.testing.assert_allclose(_np(ga[:1]), r_ga, rtol=1e-4, atol=1e-4)
+    np.testing.assert_allclose(_np(gl[:1]), r_gl, rtol=1e-4, atol=2e-5 * max(shapes))

@@ -446,10 +446,15 @@ def test_shared_layer_gradients_accumulate_into_flat_views(dev, monkeypatch):
         return loss, tr.flat_grad.clone(), dict(PKG._trace.hits), [p.numel() for p in tr.params], tr._offs
 
     loss_r, ref, hits_r, sizes, offs = run(False)
+    _, ref2, _, _, _ = run(False)
     loss, got, hits, _, _ = run(True)
     assert hits_r.get("grad_accum_view", 0) == 0 and hits_r.get("wgrad_into_grad", 0) == 0, hits_r
     assert hits.get("grad_accum_view", 0) > 0 and hits.get("wgrad_into_grad", 0) > 0, hits
     assert torch.equal(loss, loss_r)
+    # not bit for bit: the decoders' per-tap MSDA backward sums each value row's list in the order its
+    # atomics placed the taps, which varies run to run, and bf16 GEMMs carry that upstream.  So the
+    # in-place run must be as close to autograd's as two autograd runs are to each other.
     for i, (n, off) in enumerate(zip(sizes, offs)):
-        a, b = got[off:off + n].double(), ref[off:off + n].double()
-        assert (a - b).abs().max().item() <= 1e-6 * b.abs().max().item() + 1e-9, i
+        a, b, c = got[off:off + n].double(), ref[off:off + n].double(), ref2[off:off + n].double()
+        spread = (b - c).abs().max().item()
+        assert (a - b).abs().max().item() <= 4 * spread + 1e-6 * b.abs().max().item() + 1e-9, i
