@@ -79,6 +79,18 @@ size_t mfl_level_colsum_workspace_bytes(const int64_t* T, int64_t L, int64_t B, 
 int mfl_level_colsum(const float* g, const int64_t* T, int64_t L, int64_t B, int64_t N, float* out, int accumulate,
                      void* workspace, void* stream);
 
+/* The whole flattened level position embedding of a pyramid (reference PositionEmbeddingVideoSine,
+ * models/modules/embedding_layers.py:185-227, per level, then prepare_encoder_inputs' level_embed add
+ * and flatten, unimodal_deformable_transformer.py:90-134): for level l, clip b, position t and
+ * x = the number of non-padding positions in [0, t] of masks[l][b] (normalize: (x - 0.5) /
+ * (x_last + eps) * scale), out[b, start_l + t, c] = sin(x / dim_t[c]) for even c < npf, cos(x /
+ * dim_t[c]) for odd c < npf, dur[b, c - npf] for c >= npf; plus level_embed[l, c].  masks: host array
+ * of L device pointers to (B, T[l]) bool; dim_t (npf) fp32; dur (B, npf) fp32; level_embed (L, 2 npf)
+ * fp32; out (B, sum T, 2 npf) fp32.  1 <= L <= 16. */
+int mfl_pyramid_pos_flatten(const uint8_t* const* masks, const int64_t* T, int64_t L, int64_t B, int64_t npf,
+                            const float* dim_t, const float* dur, const float* level_embed, int normalize,
+                            float scale, float eps, float* out, void* stream);
+
 const char* mfl_relu_dropout_last_error(void);
 
 #ifdef __cplusplus

@@ -70,6 +70,7 @@ EXPORTED_SYMBOLS = (
     "mfl_level_pos_flatten_ex",
     "mfl_level_colsum_workspace_bytes",
     "mfl_level_colsum",
+    "mfl_pyramid_pos_flatten",
     "mfl_relu_dropout_last_error",
     "mfl_zero_masked_rows",
     "mfl_zero_masked_rows_batched",
@@ -184,6 +185,8 @@ def _declare(lib):
     lib.mfl_level_pos_flatten_ex.argtypes = [vp, vp, p64, i64, i64, i64, vp, vp, vp]
     lib.mfl_level_colsum_workspace_bytes.restype = ctypes.c_size_t
     lib.mfl_level_colsum_workspace_bytes.argtypes = [p64, i64, i64, i64]
+    lib.mfl_pyramid_pos_flatten.restype = i32
+    lib.mfl_pyramid_pos_flatten.argtypes = [vp, p64, i64, i64, i64, vp, vp, vp, i32, f32, f32, vp, vp]
     lib.mfl_level_colsum.restype = i32
     lib.mfl_level_colsum.argtypes = [vp, p64, i64, i64, i64, vp, i32, vp, vp]
     lib.mfl_gemm_nn_bf16.restype = i32

@@ -386,6 +386,86 @@ __global__ __launch_bounds__(256) void level_colsum_final(const LevelTable tb, c
   }
 }
 
+// The whole level position embedding of a pyramid in one pass (models/modules/pyramid.py,
+// pyramid_pos_flatten): for level l, clip b, position t with x = the count of non-padding positions
+// in [0, t] of that level's mask (reference PositionEmbeddingVideoSine, embedding_layers.py:203-219:
+// cumsum, normalised (x - 0.5) / (x_last + eps) * scale),
+//   out[b, start_l + t, c]        = sin(x / dim_t[c]) (c even) or cos(x / dim_t[c]) (c odd), c < npf
+//   out[b, start_l + t, npf + c]  = dur[b, c]                 (the duration embedding, every t)
+// plus level_embed[l, :] (prepare_encoder_inputs, unimodal_deformable_transformer.py:90-134).  The
+// reference's chain: ~15 kernels per level (cumsum, arange, pow, div, sin, cos, stack, duration
+// Linear, compare, cat, permute) and the flatten.  fp32 with the reference's operation order (no
+// contraction); dim_t is the module's own tensor.  One workgroup per (level, clip, 32 positions):
+// the mask counts before the chunk and over the level are recounted per workgroup (T <= 2^24 bytes).
+struct PosTable {
+  const unsigned char* mask[kLpMaxL];  // (B, T_l) bool, non-zero = padding
+  int T[kLpMaxL], start[kLpMaxL];
+  int blk0[kLpMaxL + 1];
+  int L;
+};
+constexpr int kPpRows = 32;
+__global__ __launch_bounds__(256) void pyramid_pos_kernel(const PosTable tb, const float* __restrict__ dim_t,
+                                                          const float* __restrict__ dur,
+                                                          const float* __restrict__ emb, int npf, long long S,
+                                                          int normalize, float scale, float eps,
+                                                          float* __restrict__ out) {
+#pragma clang fp contract(off)
+  __shared__ int s_red[2][4];
+  __shared__ float s_x[kPpRows];
+  int l = 0;
+  while (l + 1 < tb.L && (int)blockIdx.x >= tb.blk0[l + 1]) ++l;
+  const int T = tb.T[l];
+  const int nch = (T + kPpRows - 1) / kPpRows;
+  const int j = (int)blockIdx.x - tb.blk0[l];
+  const long long b = j / nch;
+  const int r0 = (j % nch) * kPpRows;
+  const unsigned char* __restrict__ m = tb.mask[l] + b * T;
+  int before = 0, total = 0;
+  for (int t = threadIdx.x; t < T; t += 256) {
+    const int nm = m[t] == 0 ? 1 : 0;
+    total += nm;
+    before += t < r0 ? nm : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    total += __shfl_xor(total, o);
+    before += __shfl_xor(before, o);
+  }
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_red[0][w] = before;
+    s_red[1][w] = total;
+  }
+  __syncthreads();
+  before = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
+  total = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
+  if (threadIdx.x < kPpRows) {
+    const int r = r0 + (int)threadIdx.x;
+    int c = before;
+    for (int t = r0; t <= r && t < T; ++t) c += m[t] == 0 ? 1 : 0;
+    float x = (float)c;  // (an exact integer, as the fp32 cumsum)
+    if (normalize) x = ((x - 0.5f) / ((float)total + eps)) * scale;
+    s_x[threadIdx.x] = x;
+  }
+  __syncthreads();
+  const int C = 2 * npf;
+  const int rows = min(kPpRows, T - r0);
+  float* __restrict__ ob = out + (b * S + tb.start[l] + r0) * (long long)C;
+  const float* __restrict__ el = emb + (long long)l * C;
+  const float* __restrict__ db = dur + b * npf;
+  for (int i = threadIdx.x; i < rows * C; i += 256) {
+    const int r = i / C, c = i - r * C;
+    float v;
+    if (c < npf) {
+      const float a = s_x[r] / dim_t[c];
+      v = (c & 1) ? cosf(a) : sinf(a);
+    } else {
+      v = db[c - npf];
+    }
+    ob[(long long)r * C + c] = v + el[c];
+  }
+}
+
 bool level_table(const int64_t* T, int64_t L, int64_t B, int64_t N, int rows_per_unit, int cols_per_unit,
                  LevelTable& tb) {
   if (L < 1 || L > kLpMaxL || B < 1 || N < 1) return false;
@@ -563,6 +643,40 @@ int mfl_level_colsum(const float* g, const int64_t* T, int64_t L, int64_t B, int
   hipLaunchKernelGGL(level_colsum_final, dim3((unsigned)((N + 63) / 64), (unsigned)L), dim3(256), 0, st, tb, part,
                      (int)N, out, accumulate);
   return status("level colsum final");
+}
+
+int mfl_pyramid_pos_flatten(const uint8_t* const* masks, const int64_t* T, int64_t L, int64_t B, int64_t npf,
+                            const float* dim_t, const float* dur, const float* level_embed, int normalize,
+                            float scale, float eps, float* out, void* stream) {
+  g_err[0] = 0;
+  if (!masks || !T || !dim_t || !dur || !level_embed || !out || L < 1 || L > kLpMaxL || B < 1 || npf < 1 ||
+      npf > (1 << 16)) {
+    snprintf(g_err, sizeof(g_err), "mfl_pyramid_pos_flatten: bad arguments (1 <= L <= %d)", kLpMaxL);
+    return 1;
+  }
+  PosTable tb{};
+  tb.L = (int)L;
+  long long run = 0, blk = 0;
+  for (int l = 0; l < L; ++l) {
+    if (!masks[l] || T[l] < 1 || T[l] > (1 << 24)) {
+      snprintf(g_err, sizeof(g_err), "mfl_pyramid_pos_flatten: bad level %d", l);
+      return 1;
+    }
+    tb.mask[l] = masks[l];
+    tb.T[l] = (int)T[l];
+    tb.start[l] = (int)run;
+    tb.blk0[l] = (int)blk;
+    run += T[l];
+    blk += B * ((T[l] + kPpRows - 1) / kPpRows);
+  }
+  if (blk > (1LL << 31) - 1) {
+    snprintf(g_err, sizeof(g_err), "mfl_pyramid_pos_flatten: too many rows");
+    return 1;
+  }
+  tb.blk0[L] = (int)blk;
+  hipLaunchKernelGGL(pyramid_pos_kernel, dim3((unsigned)blk), dim3(256), 0, static_cast<hipStream_t>(stream), tb, dim_t,
+                     dur, level_embed, (int)npf, run, normalize, scale, eps, out);
+  return status("pyramid pos flatten");
 }
 
 const char* mfl_relu_dropout_last_error(void) { return g_err; }

@@ -42,12 +42,14 @@ class _Conv1dGemm(torch.autograd.Function):
         y = torch.mm(cols, w2.t()) if bias is None else torch.addmm(bias.to(dt), cols, w2.t())
         ctx.save_for_backward(cols, w2)
         ctx.meta = (B, T, C, O, k, t_out, bias is not None)
+        ctx.params = (weight, bias)  # (whose flat gradient views the backward may claim)
         return y.view(B, t_out, O)
 
     @staticmethod
     def backward(ctx, gy):
-        from .modules.linear import _bias_grad, _weight_grad
+        from .modules.linear import _accum_target, _bias_grad, _claim, _weight_grad
         cols, w2 = ctx.saved_tensors
+        weight, bias = ctx.params
         B, T, C, O, k, t_out, has_bias = ctx.meta
         g2 = gy.reshape(B * t_out, O).to(w2.dtype)
         half = g2.is_cuda and g2.dtype in (torch.bfloat16, torch.float16)  # (else: fp32 / fp64 unit tests)
@@ -64,9 +66,21 @@ class _Conv1dGemm(torch.autograd.Function):
                 gxp[:, 2:2 * t_out + 1:2] += gc[:, :, 2]
                 gx = gxp[:, 1:T + 1].to(w2.dtype)
         if ctx.needs_input_grad[1]:
-            gw = (_weight_grad(g2, cols) if half else torch.mm(g2.t(), cols)).view(O, k, C).permute(0, 2, 1).contiguous()
+            gw_t = (_weight_grad(g2, cols) if half else torch.mm(g2.t(), cols)).view(O, k, C).permute(0, 2, 1)
+            # the trainer's flat gradient view: written in place (claimed), or added into when the
+            # encoder ran twice (configs[2]: the video and audio streams share the BaseEncoder)
+            acc = _accum_target(weight)
+            if acc is not None:
+                acc.add_(gw_t)
+            else:
+                v = _claim(weight)
+                gw = gw_t.contiguous() if v is None else v.copy_(gw_t)
         if has_bias and ctx.needs_input_grad[2]:
-            gb = _bias_grad(g2) if half else g2.sum(0)
+            acc = _accum_target(bias)
+            if acc is not None:
+                _bias_grad(g2, acc, accumulate=True) if half else acc.add_(g2.sum(0))
+            else:
+                gb = _bias_grad(g2, _claim(bias)) if half else g2.sum(0)
         return gx, gw, gb
 
 
@@ -124,9 +138,9 @@ class BaseEncoder(nn.Module):
         """``forward`` with every Conv1d as one GEMM on channels-last rows (_Conv1dGemm) and the
         GroupNorm on the (B, C, T) transpose, as the reference computes it; the returned srcs are
         (B, d_model, T_l) views of channels-last tensors (prepare_encoder_inputs transposes them back)."""
+        from .modules.pyramid import LevelPositions
         vf_nt = NestedTensor(vf.transpose(1, 2), mask, duration)
-        pos0 = pos_embed(vf_nt)
-        srcs, masks, poses = [], [], []
+        srcs, masks, dtypes = [], [], []
 
         def level(l, x_cl):
             conv, norm = self.input_proj[l][0], self.input_proj[l][1]
@@ -135,17 +149,18 @@ class BaseEncoder(nn.Module):
 
         srcs.append(level(0, vf))
         masks.append(mask)
-        poses.append(pos0)
         prev_cl = vf
         for l in range(1, self.num_feature_levels):
             src = level(l, prev_cl)
             prev_cl = src.transpose(1, 2)
             m = vf_nt.mask
             lmask = F.interpolate(m[None].float(), size=src.shape[-1:]).to(torch.bool)[0]
-            pos_l = pos_embed(NestedTensor(src, lmask, duration)).to(src.dtype)
             srcs.append(src)
             masks.append(lmask)
-            poses.append(pos_l)
+        # level 0's embedding in pos_embed's own dtype, the others cast to the level's (reference
+        # :62-89); computed when read — prepare_encoder_inputs flattens them from the masks instead
+        dtypes = [torch.float32] + [s.dtype for s in srcs[1:]]
+        poses = LevelPositions(pos_embed, [vf_nt.tensors] + srcs[1:], masks, duration, dtypes)
         return srcs, masks, poses
 
     def forward(self, vf, mask, duration, pos_embed):

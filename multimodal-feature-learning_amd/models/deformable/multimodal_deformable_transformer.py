@@ -318,6 +318,22 @@ class MultimodalDeformableTransformerDecoder(nn.Module):
         self.return_intermediate = return_intermediate
         self.bbox_head = None
 
+    def flat_groups(self):
+        """Parameters a flat-buffer trainer should lay out back to back (train_step._flat_order): each
+        same-shape weight of the layers, and the query prologue's [W_off; W_aw] pairs interleaved, so
+        that the deferred short-K queue's batched gradient GEMMs write one view of the flat gradient
+        buffer (linear._WgradQueue) — as the unimodal decoder's."""
+        layers = [layer for layer in self.layers if type(layer) is MultimodalDeformableTransformerDecoderLayer]
+        if len(layers) < 2:
+            return []
+        names = ("linear1.weight", "linear2.weight", "linear3.weight", "self_attn.out_proj.weight",
+                 "cross_attn.value_proj.weight", "cross_attn.value_proj.bias", "cross_attn.output_proj.weight")
+        groups = [tuple(layer.get_parameter(n) for layer in layers) for n in names]
+        for kind in ("weight", "bias"):
+            groups.append(tuple(layer.get_parameter(f"cross_attn.{n}.{kind}") for layer in layers
+                                for n in ("sampling_offsets", "attention_weights")))
+        return groups
+
     @staticmethod
     def _per_level(reference_points, valid_ratios):
         if reference_points.shape[-1] == 2:

@@ -329,7 +329,14 @@ class DeformableTransformerDecoder(nn.Module):
             return []
         names = ("linear1.weight", "linear2.weight", "self_attn.out_proj.weight", "cross_attn.value_proj.weight",
                  "cross_attn.value_proj.bias", "cross_attn.output_proj.weight")
-        return [tuple(layer.get_parameter(n) for layer in layers) for n in names]
+        groups = [tuple(layer.get_parameter(n) for layer in layers) for n in names]
+        # the query prologue's [W_off; W_aw] pairs of every layer interleaved: each pair stays back to
+        # back (MSDeformAttn.flat_groups, read as one tensor) and the 2 x layers weights (biases) form
+        # one run of the deferred queue's (800 x 128 x 512) batch
+        for kind in ("weight", "bias"):
+            groups.append(tuple(layer.get_parameter(f"cross_attn.{n}.{kind}") for layer in layers
+                                for n in ("sampling_offsets", "attention_weights")))
+        return groups
 
     def forward(self, tgt, reference_points, src, src_temporal_shapes, src_level_start_index, src_valid_ratios,
                 query_pos=None, src_padding_mask=None, query_padding_mask=None, disable_iterative_refine=False):

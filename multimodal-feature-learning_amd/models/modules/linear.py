@@ -82,6 +82,46 @@ class _WgradQueue:
             _sum_into(ts, out, accumulate=False)
         self.deliver(prm, out)
 
+    def _runs(self, groups):
+        """The batches of one flush: each shape group's entries sorted so one parameter's products
+        sit next to each other and the parameters follow the flat gradient buffer.  Split further
+        only where that lets a batch's GEMM write a claimed view of the flat gradient buffer: the
+        whole-weight products of parameters with no gradient yet are cut where their flat views stop
+        lying back to back (the decoder's self_attn.out_proj and cross_attn.output_proj share a shape
+        but are two runs) — unless that gives more than 3 batches (each costs a stacking copy, a GEMM
+        and possibly a bias reduction).  Row-block products (in_proj's q / k | v) and products added
+        into an existing .grad stay one batch each.  MFL_QUEUE_RUNS=0: one batch per shape (A/B)."""
+        import os
+        split = os.environ.get("MFL_QUEUE_RUNS", "1") != "0"
+        whole = lambda e: e[3] == 0 and e[0].shape[1] == e[2].shape[0]  # noqa: E731
+        has_t = lambda w: (self.target is not None and ACCUMULATE_IN_PLACE  # noqa: E731
+                           and self.target(w) is not None)
+        for es in groups.values():
+            es = sorted(es, key=lambda e: (_dest_offset(e[2]), id(e[2]), e[3]))
+            if not split:
+                yield es
+                continue
+            rows = [e for e in es if not whole(e)]
+            accs = [e for e in es if whole(e) and has_t(e[2])]
+            rest = [e for e in es if whole(e) and not has_t(e[2])]
+            runs, run, prev = [], [], None
+            for e in rest:
+                w = e[2]
+                off = _dest_offset(w)
+                if prev is not None and w is not prev[0]:
+                    if not (off >= 0 and prev[1] >= 0 and off == prev[1] + prev[0].numel()):
+                        runs.append(run)
+                        run = []
+                run.append(e)
+                prev = (w, off)
+            if run:
+                runs.append(run)
+            if len(runs) > 3:
+                runs = [rest]
+            for r in [rows, accs] + runs:
+                if r:
+                    yield r
+
     @torch.no_grad()
     def flush(self):
         entries, self.entries = self.entries, []
@@ -94,9 +134,7 @@ class _WgradQueue:
         from ... import _trace
         _trace.hit("wgrad_batched", len(entries))
         parts = {}  # param -> [(row offset, fp32 grad rows)] (weights of several row blocks)
-        for (_, n_out, _, _), es in groups.items():
-            # one parameter's products next to each other, the parameters in flat-buffer order
-            es = sorted(es, key=lambda e: (_dest_offset(e[2]), id(e[2]), e[3]))
+        for es in self._runs(groups):
             uniq = list({id(e[2]): e[2] for e in es}.values())
             uses = [sum(1 for e in es if e[2] is w) for w in uniq]
             full = all(e[3] == 0 and e[0].shape[1] == e[2].shape[0] for e in es)
@@ -106,8 +144,7 @@ class _WgradQueue:
             dest = None
             if (es[0][0].is_cuda and full and len(set(uses)) == 1 and (ACCUMULATE_IN_PLACE or uses[0] == 1)
                     and not any(self.target is not None and self.target(w) is not None for w in uniq)):
-                dest = (_claim_group(uniq, returned=False) if len(uniq) > 1
-                        else _claim(uniq[0], returned=False) if uses[0] > 1 else None)
+                dest = _claim_group(uniq, returned=False) if len(uniq) > 1 else _claim(uniq[0], returned=False)
             gs = es[0][0][None] if len(es) == 1 else torch.stack([e[0] for e in es])
             xs = es[0][1][None] if len(es) == 1 else torch.stack([e[1] for e in es])
             if dest is not None and uses[0] == 1:
@@ -152,7 +189,9 @@ class _WgradQueue:
             if len(ps) == 1 and ps[0][0] == 0 and ps[0][1].shape == prm.shape:
                 grad = ps[0][1]
             elif rows[0] == 0 and ends[-1] == prm.shape[0] and all(e == r for e, r in zip(ends[:-1], rows[1:])):
-                grad = torch.cat([g for _, g in ps])  # row blocks tiling the weight (in_proj q / k | v)
+                # row blocks tiling the weight (in_proj q / k | v): concatenated straight into its flat view
+                v = _claim(prm, returned=False) if ps[0][1].is_cuda else None
+                grad = torch.cat([g for _, g in ps]) if v is None else torch.cat([g for _, g in ps], out=v)
             else:  # a weight used several times
                 grad = torch.zeros(prm.shape, dtype=torch.float32, device=prm.device)
                 for row, g in ps:

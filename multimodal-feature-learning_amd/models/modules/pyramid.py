@@ -15,7 +15,7 @@ import ctypes
 import torch
 from torch.autograd import Function
 
-__all__ = ["level_pos_flatten"]
+__all__ = ["level_pos_flatten", "LevelPositions"]
 
 
 def _reference(pos_embeds, level_embed):
@@ -89,10 +89,130 @@ def _supported(pos_embeds, level_embed):
                and (p.is_contiguous() or p.transpose(1, 2).is_contiguous()) for p in pos_embeds)
 
 
+class LevelPositions(list):
+    """The per-level position embeddings of a pyramid (BaseEncoder's ``poses``), computed when first
+    read: ``pos_embed(NestedTensor(src_l, mask_l, duration))`` per level, as the reference does
+    (base_encoder.py:62-89).  ``level_pos_flatten`` reads the masks and durations instead and writes the
+    flattened embedding in one kernel (``_PyramidPos``) without ever building the per-level tensors."""
+
+    def __init__(self, pos_embed, srcs, masks, duration, dtypes):
+        super().__init__()
+        self.pos_embed, self.srcs, self.masks, self.duration, self.dtypes = pos_embed, srcs, masks, duration, dtypes
+        self._done = False
+
+    def _materialise(self):
+        if not self._done:
+            from .misc_modules import NestedTensor
+            super().extend(self.pos_embed(NestedTensor(s, m, self.duration)).to(dt)
+                           for s, m, dt in zip(self.srcs, self.masks, self.dtypes))
+            self._done = True
+
+    def __getitem__(self, i):
+        self._materialise()
+        return super().__getitem__(i)
+
+    def __iter__(self):
+        self._materialise()
+        return super().__iter__()
+
+    def __len__(self):
+        return len(self.masks)
+
+
+class _PyramidPos(Function):
+    """lvl_pos_embed_flatten of a pyramid from its masks and durations (mfl_pyramid_pos_flatten);
+    gradients for level_embed (per-level column sums) and for the duration embedding (per-clip column
+    sums of the duration half), the position embedding's only learned input."""
+
+    @staticmethod
+    def forward(ctx, level_embed, dur, masks, dim_t, npf, normalize, scale, eps):
+        from ... import _native, _trace
+        _trace.hit("pyramid_pos")
+        lib = _native.load_library()
+        L = len(masks)
+        B = masks[0].shape[0]
+        T = [m.shape[1] for m in masks]
+        out = torch.empty(B, sum(T), 2 * npf, dtype=torch.float32, device=level_embed.device)
+        ptrs = (ctypes.c_void_p * L)(*[m.data_ptr() for m in masks])
+        rc = lib.mfl_pyramid_pos_flatten(ptrs, (ctypes.c_int64 * L)(*T), L, B, npf, dim_t.data_ptr(), dur.data_ptr(),
+                                         level_embed.data_ptr(), 1 if normalize else 0, float(scale), float(eps),
+                                         out.data_ptr(), _native.stream_handle(out.device))
+        if rc != 0:
+            raise RuntimeError("mfl_pyramid_pos_flatten failed: " + lib.mfl_relu_dropout_last_error().decode())
+        ctx.T, ctx.B, ctx.npf = T, B, npf
+        ctx.level_embed = level_embed
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        from ... import _native
+        from .linear import _accum_target, _claim
+        T, B, npf = ctx.T, ctx.B, ctx.npf
+        L, N = len(T), 2 * npf
+        nig = ctx.needs_input_grad
+        g = g.contiguous()
+        lib = _native.load_library()
+
+        def colsum(t_list, nb, out, accumulate):
+            t64 = (ctypes.c_int64 * len(t_list))(*t_list)
+            ws = torch.empty(lib.mfl_level_colsum_workspace_bytes(t64, len(t_list), nb, N), dtype=torch.uint8,
+                             device=g.device)
+            rc = lib.mfl_level_colsum(g.data_ptr(), t64, len(t_list), nb, N, out.data_ptr(), 1 if accumulate else 0,
+                                      ws.data_ptr(), _native.stream_handle(g.device))
+            if rc != 0:
+                raise RuntimeError("mfl_level_colsum failed: " + lib.mfl_relu_dropout_last_error().decode())
+
+        dlevel = ddur = None
+        if nig[0]:
+            acc = _accum_target(ctx.level_embed)  # (the multimodal audio pyramid shares level_embed)
+            out = acc if acc is not None else _claim(ctx.level_embed)
+            if out is None:
+                out = torch.empty(ctx.level_embed.shape, dtype=torch.float32, device=g.device)
+            colsum(T, B, out, acc is not None)
+            dlevel = None if acc is not None else out
+        if nig[1]:
+            if B <= 16:  # per-clip column sums: the clips as the "levels" of one batch
+                per_clip = torch.empty(B, N, dtype=torch.float32, device=g.device)
+                colsum([sum(T)] * B, 1, per_clip, False)
+                ddur = per_clip[:, npf:]
+            else:
+                ddur = g[..., npf:].sum(1)
+        return dlevel, ddur, None, None, None, None, None, None
+
+
+def _pyramid_supported(pos, level_embed):
+    from .embedding_layers import PositionEmbeddingVideoSine
+    mod = pos.pos_embed
+    if not (type(mod) is PositionEmbeddingVideoSine and level_embed.is_cuda and level_embed.dtype == torch.float32
+            and level_embed.is_contiguous() and level_embed.dim() == 2 and level_embed.shape[0] == len(pos.masks)
+            and level_embed.shape[1] == 2 * mod.num_pos_feats and 1 <= len(pos.masks) <= 16
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+            and pos.duration is not None and all(dt == torch.float32 for dt in pos.dtypes)):
+        return False
+    B = pos.masks[0].shape[0]
+    return all(m.is_cuda and m.device == level_embed.device and m.dtype == torch.bool and m.dim() == 2
+               and m.shape[0] == B and m.shape[1] > 0 and m.is_contiguous() for m in pos.masks)
+
+
+def _pyramid_pos(pos, level_embed):
+    mod = pos.pos_embed
+    npf = mod.num_pos_feats
+    dev = level_embed.device
+    # dim_t exactly as the module computes it (embedding_layers.py: PositionEmbeddingVideoSine.forward)
+    dim_t = torch.arange(npf, dtype=torch.float32, device=dev)
+    dim_t = mod.temperature ** (2 * torch.div(dim_t, 2, rounding_mode='trunc') / npf)
+    dur = mod.duration_embedding(pos.duration).float().contiguous()
+    return _PyramidPos.apply(level_embed, dur, list(pos.masks), dim_t, npf, mod.normalize, mod.scale, 1e-6)
+
+
 def level_pos_flatten(pos_embeds, level_embed):
     """``torch.cat([p.transpose(1, 2) + level_embed[l].view(1, 1, -1) for l, p in enumerate(pos_embeds)], 1)``
     (pos_embeds: (B, d, T_l) per level): the HIP kernels under bf16 autocast on the GPU, the reference
-    composition elsewhere."""
+    composition elsewhere.  A ``LevelPositions`` is flattened from its masks and durations in one kernel
+    (its per-level tensors are never built)."""
+    if isinstance(pos_embeds, LevelPositions) and not pos_embeds._done and _pyramid_supported(pos_embeds,
+                                                                                              level_embed):
+        return _pyramid_pos(pos_embeds, level_embed)
     if not _supported(pos_embeds, level_embed):
         return _reference(pos_embeds, level_embed)
     return _LevelPosFlatten.apply(level_embed, *pos_embeds)

@@ -291,3 +291,43 @@ def test_level_pos_flatten_matches_reference(dev, T):
     torch.testing.assert_close(got[0], want[0], rtol=1e-5, atol=1e-4)
     for a, b in zip(got[1:], want[1:]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("normalize", [True, False])
+def test_pyramid_pos_matches_per_level_embeddings(dev, normalize):
+    """pyramid.LevelPositions + mfl_pyramid_pos_flatten: the flattened level position embedding of a
+    padded pyramid written from its masks and durations in one kernel equals the reference chain —
+    PositionEmbeddingVideoSine per level (embedding_layers.py:185-227, sin / cos of the normalised
+    mask cumsum, the duration embedding) cast and flattened with level_embed
+    (unimodal_deformable_transformer.py:90-134) — and so do the level_embed and duration-embedding
+    gradients."""
+    torch.manual_seed(13)
+    emb_mod = PKG.models.modules.embedding_layers.PositionEmbeddingVideoSine(256, normalize=normalize).to(dev)
+    pyr = PKG.models.modules.pyramid
+    B, Ts = 3, (96, 48, 24, 12)
+    lens = torch.tensor([96, 70, 31], device=dev)
+    masks = [(torch.arange(T, device=dev)[None] * 96 // T) >= lens[:, None] for T in Ts]
+    duration = torch.tensor([40.0, 100.0, 3.0], device=dev)
+    srcs = [torch.zeros(B, 512, T, device=dev) for T in Ts]
+    level_embed = torch.randn(len(Ts), 512, device=dev, requires_grad=True)
+    go = torch.randn(B, sum(Ts), 512, device=dev)
+
+    def run(fused):
+        emb_mod.zero_grad(set_to_none=True)
+        level_embed.grad = None
+        lp = pyr.LevelPositions(emb_mod, srcs, masks, duration, [torch.float32] * len(Ts))
+        if not fused:
+            list(lp)  # materialise: the per-level reference chain
+        PKG._trace.clear()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = pyr.level_pos_flatten(lp, level_embed)
+        assert (PKG._trace.hits.get("pyramid_pos", 0) == 1) == fused
+        (out * go).sum().backward()
+        return out.detach(), level_embed.grad.clone(), emb_mod.duration_embed_layer.weight.grad.clone()
+
+    o1, l1, w1 = run(True)
+    o2, l2, w2 = run(False)
+    torch.testing.assert_close(o1, o2, rtol=2e-6, atol=2e-6)
+    torch.testing.assert_close(l1, l2, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(w1, w2, rtol=1e-4, atol=1e-3)

@@ -25,8 +25,8 @@ GLUE = ("copy", "_to_copy", "cat", "sum", "add", "fill", "zero", "mul", "div", "
 
 
 def sig(x):
-    if isinstance(x, torch.Tensor):
-        return f"{str(x.dtype).replace('torch.', '')}{list(x.shape)}"
+    if isinstance(x, torch.Tensor):  # "~": not contiguous (a strided copy kernel)
+        return f"{str(x.dtype).replace('torch.', '')}{list(x.shape)}{'' if x.is_contiguous() else '~'}"
     if isinstance(x, (list, tuple)):
         return "[" + ",".join(sig(y) for y in x[:4]) + ("…" if len(x) > 4 else "") + "]"
     return ""
