@@ -81,6 +81,23 @@ int mfl_carry_entry_forward(const float* src, const float* pos, int64_t n, uint1
 int mfl_carry_entry_backward(const float* dr, const uint16_t* dv16, const uint16_t* dq16, int64_t n, float* dsrc,
                              float* dpos, int dpos_accumulate, void* stream);
 
+/* GroupNorm over channels-last rows (the BaseEncoder's nn.GroupNorm(G, C) after each level's Conv1d,
+ * reference models/base_encoder.py:27-36, which runs it on the (B, C, T) transpose; fp32 statistics over
+ * (T, C / G) per (b, g), as autocast's fp32 group_norm): x (B, T, C) bf16 contiguous; out32[b * stride +
+ * t * C + c] fp32 (the level's rows of the encoder's flattened input) and, optional, out16 (B, T, C) its
+ * bf16 copy; mean / rstd (B, G) saved for the backward.  C in {256, 512, 1024}, (C / G) % 8 == 0,
+ * 16-byte aligned buffers.  Backward: gt = g32 (rows as out32, optional) + g16 (optional); dx (B, T, C)
+ * bf16; dgamma / dbeta (C) fp32, added into with accumulate.  workspace:
+ * mfl_groupnorm_cl_workspace_bytes bytes (0: unsupported shape). */
+size_t mfl_groupnorm_cl_workspace_bytes(int64_t B, int64_t T, int64_t C, int64_t G);
+int mfl_groupnorm_cl_forward(const uint16_t* x, const float* gamma, const float* beta, int64_t B, int64_t T, int64_t C,
+                             int64_t G, float eps, float* out32, int64_t out32_batch_stride, uint16_t* out16,
+                             float* mean, float* rstd, void* workspace, void* stream);
+int mfl_groupnorm_cl_backward(const float* g32, int64_t g32_batch_stride, const uint16_t* g16, const uint16_t* x,
+                              const float* gamma, const float* mean, const float* rstd, int64_t B, int64_t T,
+                              int64_t C, int64_t G, uint16_t* dx, float* dgamma, float* dbeta, int accumulate,
+                              void* workspace, void* stream);
+
 const char* mfl_add_layernorm_last_error(void);
 
 #ifdef __cplusplus

@@ -58,6 +58,9 @@ EXPORTED_SYMBOLS = (
     "mfl_add_layernorm_forward_ex",
     "mfl_add_layernorm_backward_ex",
     "mfl_add_layernorm_backward_ex2",
+    "mfl_groupnorm_cl_workspace_bytes",
+    "mfl_groupnorm_cl_forward",
+    "mfl_groupnorm_cl_backward",
     "mfl_carry_entry_forward",
     "mfl_carry_entry_backward",
     "mfl_add_layernorm_last_error",
@@ -175,6 +178,13 @@ def _declare(lib):
     lib.mfl_gemm_nt_bf16.argtypes = [vp, vp, vp, vp, i64, i64, i64, i64, i64, i64, vp]
     lib.mfl_gather_keep_backward.restype = i32
     lib.mfl_gather_keep_backward.argtypes = [vp, vp, vp, i64, i64, i64, i64, vp, vp, vp]
+    lib.mfl_groupnorm_cl_workspace_bytes.restype = ctypes.c_size_t
+    lib.mfl_groupnorm_cl_workspace_bytes.argtypes = [i64, i64, i64, i64]
+    lib.mfl_groupnorm_cl_forward.restype = i32
+    lib.mfl_groupnorm_cl_forward.argtypes = [vp, vp, vp, i64, i64, i64, i64, f32, vp, i64, vp, vp, vp, vp, vp]
+    lib.mfl_groupnorm_cl_backward.restype = i32
+    lib.mfl_groupnorm_cl_backward.argtypes = [vp, i64, vp, vp, vp, vp, vp, i64, i64, i64, i64, vp, vp, vp, i32, vp,
+                                              vp]
     lib.mfl_carry_entry_forward.restype = i32
     lib.mfl_carry_entry_forward.argtypes = [vp, vp, i64, vp, vp, vp]
     lib.mfl_carry_entry_backward.restype = i32

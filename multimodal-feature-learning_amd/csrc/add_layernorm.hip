@@ -379,6 +379,264 @@ __global__ __launch_bounds__(256) void carry_entry_bwd(const float* __restrict__
   }
 }
 
+// GroupNorm over channels-last rows (models/base_encoder.py, BaseEncoder's
+// nn.GroupNorm(32, d_model) after each level's Conv1d; reference base_encoder.py:27-36): x (B, T, C)
+// bf16 (the convolution GEMM's output), G groups of C / G consecutive channels, statistics over
+// (T, C / G) per (b, g) in fp32 — ATen's group_norm on the (B, C, T) transpose, which autocast runs in
+// fp32.  The normalised rows go straight into the encoder's flattened (B, S, C) fp32 input at the
+// level's rows (no transpose copies, no cat) and, for the next level's convolution, as bf16.
+// Lanes: C / 8 column lanes of 8 channels (one 16-B load; 8 | C / G, so a lane lies in one group) x
+// 256 / (C / 8) row lanes; 32 rows a workgroup.
+constexpr int kGnRows = 32;
+__device__ __forceinline__ void load_bf16x8(const uint16_t* p, float (&v)[8]) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = __uint_as_float(w[k] << 16);
+    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void store_bf16x8(uint16_t* p, const float (&v)[8]) {
+  uint4 u;
+  u.x = Vec4<uint16_t>::rne(v[0]) | (Vec4<uint16_t>::rne(v[1]) << 16);
+  u.y = Vec4<uint16_t>::rne(v[2]) | (Vec4<uint16_t>::rne(v[3]) << 16);
+  u.z = Vec4<uint16_t>::rne(v[4]) | (Vec4<uint16_t>::rne(v[5]) << 16);
+  u.w = Vec4<uint16_t>::rne(v[6]) | (Vec4<uint16_t>::rne(v[7]) << 16);
+  *reinterpret_cast<uint4*>(p) = u;
+}
+
+// partial sums (sum, sum of squares) of every group over one workgroup's rows
+__global__ __launch_bounds__(256) void gn_cl_stats(const uint16_t* __restrict__ x, int T, int C, int G, int nch,
+                                                   float* __restrict__ part) {
+  __shared__ float rs[256], rss[256];
+  const int blk = (int)blockIdx.x;
+  const long long b = blk / nch;
+  const int r0 = (blk % nch) * kGnRows, r1 = min(T, r0 + kGnRows);
+  const int CL = C / 8, RL = 256 / CL;
+  const int cl = (int)threadIdx.x % CL, rl = (int)threadIdx.x / CL;
+  float sum = 0.f, sq = 0.f;
+  for (int r = r0 + rl; r < r1; r += RL) {
+    float v[8];
+    load_bf16x8(x + ((b * T + r) * C + cl * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      sum += v[k];
+      sq += v[k] * v[k];
+    }
+  }
+  rs[threadIdx.x] = sum;
+  rss[threadIdx.x] = sq;
+  __syncthreads();
+  if ((int)threadIdx.x < G) {
+    const int g = (int)threadIdx.x, lpg = C / G / 8;
+    float a = 0.f, q = 0.f;
+    for (int r = 0; r < RL; ++r)
+      for (int l = g * lpg; l < (g + 1) * lpg; ++l) {
+        a += rs[r * CL + l];
+        q += rss[r * CL + l];
+      }
+    part[((long long)blk * G + g) * 2] = a;
+    part[((long long)blk * G + g) * 2 + 1] = q;
+  }
+}
+
+// per (b, g) statistics from the partials, then out = x * (rstd gamma) + (beta - mean rstd gamma)
+// (ATen's fused parameters) in fp32 into out32 (rows of the level, batch stride sb) and bf16 out16
+__global__ __launch_bounds__(256) void gn_cl_apply(const uint16_t* __restrict__ x, const float* __restrict__ part,
+                                                   const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                   int T, int C, int G, int nch, float eps, float* __restrict__ out32,
+                                                   long long sb, uint16_t* __restrict__ out16,
+                                                   float* __restrict__ mean_out, float* __restrict__ rstd_out) {
+  __shared__ float s_mean[128], s_rstd[128];
+  const int blk = (int)blockIdx.x;
+  const long long b = blk / nch;
+  if ((int)threadIdx.x < G) {
+    const int g = (int)threadIdx.x;
+    float a = 0.f, q = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      a += part[((b * nch + c) * G + g) * 2];
+      q += part[((b * nch + c) * G + g) * 2 + 1];
+    }
+    const float n = (float)T * (float)(C / G);
+    const float mean = a / n;
+    const float var = fmaxf(q / n - mean * mean, 0.f);
+    const float rstd = 1.f / sqrtf(var + eps);
+    s_mean[g] = mean;
+    s_rstd[g] = rstd;
+    if (blk % nch == 0) {
+      mean_out[b * G + g] = mean;
+      rstd_out[b * G + g] = rstd;
+    }
+  }
+  __syncthreads();
+  const int r0 = (blk % nch) * kGnRows, r1 = min(T, r0 + kGnRows);
+  const int CL = C / 8, RL = 256 / CL;
+  const int cl = (int)threadIdx.x % CL, rl = (int)threadIdx.x / CL;
+  const int g = cl * 8 / (C / G);
+  float sc[8], bi[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = s_rstd[g] * gamma[cl * 8 + k];
+    bi[k] = -sc[k] * s_mean[g] + beta[cl * 8 + k];
+  }
+  for (int r = r0 + rl; r < r1; r += RL) {
+    float v[8];
+    load_bf16x8(x + ((b * T + r) * C + cl * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] * sc[k] + bi[k];
+    float* o = out32 + (b * sb + (long long)r * C + cl * 8);
+    *reinterpret_cast<float4*>(o) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(o + 4) = make_float4(v[4], v[5], v[6], v[7]);
+    if (out16 != nullptr) store_bf16x8(out16 + ((b * T + r) * C + cl * 8), v);
+  }
+}
+
+// backward partials per channel over one workgroup's rows: S1 = sum gt x, S0 = sum gt, gt = g32 + g16
+__global__ __launch_bounds__(256) void gn_cl_bwd_partial(const float* __restrict__ g32, long long sb,
+                                                         const uint16_t* __restrict__ g16,
+                                                         const uint16_t* __restrict__ x, int T, int C, int nch,
+                                                         float* __restrict__ part) {
+  __shared__ float s1[256][8], s0[256][8];
+  const int blk = (int)blockIdx.x;
+  const long long b = blk / nch;
+  const int r0 = (blk % nch) * kGnRows, r1 = min(T, r0 + kGnRows);
+  const int CL = C / 8, RL = 256 / CL;
+  const int cl = (int)threadIdx.x % CL, rl = (int)threadIdx.x / CL;
+  float a1[8], a0[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) a1[k] = a0[k] = 0.f;
+  for (int r = r0 + rl; r < r1; r += RL) {
+    float xv[8], gt[8];
+    load_bf16x8(x + ((b * T + r) * C + cl * 8), xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gt[k] = 0.f;
+    if (g32 != nullptr) {
+      const float* p = g32 + (b * sb + (long long)r * C + cl * 8);
+      const float4 u = *reinterpret_cast<const float4*>(p), w = *reinterpret_cast<const float4*>(p + 4);
+      gt[0] = u.x; gt[1] = u.y; gt[2] = u.z; gt[3] = u.w; gt[4] = w.x; gt[5] = w.y; gt[6] = w.z; gt[7] = w.w;
+    }
+    if (g16 != nullptr) {
+      float h[8];
+      load_bf16x8(g16 + ((b * T + r) * C + cl * 8), h);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gt[k] += h[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      a1[k] += gt[k] * xv[k];
+      a0[k] += gt[k];
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s1[threadIdx.x][k] = a1[k];
+    s0[threadIdx.x][k] = a0[k];
+  }
+  __syncthreads();
+  for (int c = (int)threadIdx.x; c < C; c += 256) {
+    const int l = c / 8, k = c % 8;
+    float t1 = 0.f, t0 = 0.f;
+    for (int r = 0; r < RL; ++r) {
+      t1 += s1[r * CL + l][k];
+      t0 += s0[r * CL + l][k];
+    }
+    part[((long long)blk * 2) * C + c] = t1;
+    part[((long long)blk * 2 + 1) * C + c] = t0;
+  }
+}
+
+// per clip: the channels' sums over the clip's chunks (kept for dgamma / dbeta) and the group
+// coefficients of dx = rstd gamma gt + c2 x + c3 (ATen's group_norm backward)
+__global__ __launch_bounds__(256) void gn_cl_bwd_coef(const float* __restrict__ part, const float* __restrict__ gamma,
+                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                      int T, int C, int G, int nch, float* __restrict__ sbc,
+                                                      float* __restrict__ coef) {
+  __shared__ float sds[1024], sdb[1024];
+  const long long b = blockIdx.x;
+  for (int c = (int)threadIdx.x; c < C; c += 256) {
+    float t1 = 0.f, t0 = 0.f;
+    for (int k = 0; k < nch; ++k) {
+      t1 += part[((b * nch + k) * 2) * C + c];
+      t0 += part[((b * nch + k) * 2 + 1) * C + c];
+    }
+    sbc[(b * 2) * C + c] = t1;
+    sbc[(b * 2 + 1) * C + c] = t0;
+    sds[c] = t1 * gamma[c];
+    sdb[c] = t0 * gamma[c];
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < G) {
+    const int g = (int)threadIdx.x, cpg = C / G;
+    float ds = 0.f, db = 0.f;
+    for (int c = g * cpg; c < (g + 1) * cpg; ++c) {
+      ds += sds[c];
+      db += sdb[c];
+    }
+    const float m = mean[b * G + g], rs = rstd[b * G + g];
+    const float s = 1.f / ((float)cpg * (float)T);
+    const float c2 = (db * m - ds) * rs * rs * rs * s;
+    const float c3 = -c2 * m - db * rs * s;
+    coef[(b * G + g) * 2] = c2;
+    coef[(b * G + g) * 2 + 1] = c3;
+  }
+}
+
+// dgamma[c] = sum_b (S1 - mean S0) rstd, dbeta[c] = sum_b S0 (added into out with accumulate)
+__global__ __launch_bounds__(256) void gn_cl_bwd_params(const float* __restrict__ sbc, const float* __restrict__ mean,
+                                                        const float* __restrict__ rstd, int B, int C, int G,
+                                                        float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                        int accumulate) {
+  const int c = (int)(blockIdx.x * 256 + threadIdx.x);
+  if (c >= C) return;
+  const int g = c / (C / G);
+  float dg = 0.f, dbt = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float s1 = sbc[((long long)b * 2) * C + c], s0 = sbc[((long long)b * 2 + 1) * C + c];
+    dg += (s1 - mean[b * G + g] * s0) * rstd[b * G + g];
+    dbt += s0;
+  }
+  if (dgamma != nullptr) dgamma[c] = accumulate ? dgamma[c] + dg : dg;
+  if (dbeta != nullptr) dbeta[c] = accumulate ? dbeta[c] + dbt : dbt;
+}
+
+__global__ __launch_bounds__(256) void gn_cl_bwd_apply(const float* __restrict__ g32, long long sb,
+                                                       const uint16_t* __restrict__ g16,
+                                                       const uint16_t* __restrict__ x, const float* __restrict__ gamma,
+                                                       const float* __restrict__ rstd, const float* __restrict__ coef,
+                                                       int T, int C, int G, int nch, uint16_t* __restrict__ dx) {
+  const int blk = (int)blockIdx.x;
+  const long long b = blk / nch;
+  const int r0 = (blk % nch) * kGnRows, r1 = min(T, r0 + kGnRows);
+  const int CL = C / 8, RL = 256 / CL;
+  const int cl = (int)threadIdx.x % CL, rl = (int)threadIdx.x / CL;
+  const int g = cl * 8 / (C / G);
+  const float rs = rstd[b * G + g], c2 = coef[(b * G + g) * 2], c3 = coef[(b * G + g) * 2 + 1];
+  float c1[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) c1[k] = rs * gamma[cl * 8 + k];
+  for (int r = r0 + rl; r < r1; r += RL) {
+    float xv[8], gt[8];
+    load_bf16x8(x + ((b * T + r) * C + cl * 8), xv);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gt[k] = 0.f;
+    if (g32 != nullptr) {
+      const float* p = g32 + (b * sb + (long long)r * C + cl * 8);
+      const float4 u = *reinterpret_cast<const float4*>(p), w = *reinterpret_cast<const float4*>(p + 4);
+      gt[0] = u.x; gt[1] = u.y; gt[2] = u.z; gt[3] = u.w; gt[4] = w.x; gt[5] = w.y; gt[6] = w.z; gt[7] = w.w;
+    }
+    if (g16 != nullptr) {
+      float h[8];
+      load_bf16x8(g16 + ((b * T + r) * C + cl * 8), h);
+#pragma unroll
+      for (int k = 0; k < 8; ++k) gt[k] += h[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) gt[k] = c1[k] * gt[k] + c2 * xv[k] + c3;
+    store_bf16x8(dx + ((b * T + r) * C + cl * 8), gt);
+  }
+}
+
 int status(const char* what) {
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
@@ -619,6 +877,75 @@ int mfl_carry_entry_backward(const float* dr, const uint16_t* dv16, const uint16
   hipLaunchKernelGGL(carry_entry_bwd, dim3(blocks), dim3(256), 0, static_cast<hipStream_t>(stream), dr, dv16, dq16,
                      n4, dsrc, dpos, dpos_accumulate);
   return status("carry entry backward");
+}
+
+static bool gn_cl_ok(int64_t B, int64_t T, int64_t C, int64_t G) {
+  return B >= 1 && T >= 1 && G >= 1 && G <= 128 && C % G == 0 && (C / G) % 8 == 0 && C % 8 == 0 && C <= 1024 &&
+         256 % (C / 8) == 0 && B * T * C < (1LL << 40) && T < (1 << 30);
+}
+
+size_t mfl_groupnorm_cl_workspace_bytes(int64_t B, int64_t T, int64_t C, int64_t G) {
+  if (!gn_cl_ok(B, T, C, G)) return 0;
+  const long long nch = (T + kGnRows - 1) / kGnRows;
+  const long long fwd = B * nch * G * 2, bwd = B * nch * 2 * C + B * 2 * C + B * G * 2;
+  return (size_t)std::max(fwd, bwd) * sizeof(float);
+}
+
+int mfl_groupnorm_cl_forward(const uint16_t* x, const float* gamma, const float* beta, int64_t B, int64_t T, int64_t C,
+                             int64_t G, float eps, float* out32, int64_t out32_batch_stride, uint16_t* out16,
+                             float* mean, float* rstd, void* workspace, void* stream) {
+  g_err[0] = 0;
+  if (!gn_cl_ok(B, T, C, G) || !x || !gamma || !beta || !out32 || !mean || !rstd || !workspace ||
+      out32_batch_stride < T * C || (((uintptr_t)x | (uintptr_t)out32 | (uintptr_t)out16) & 15u) ||
+      out32_batch_stride % 4) {
+    snprintf(g_err, sizeof(g_err), "mfl_groupnorm_cl_forward: bad arguments (C in {256, 512, 1024}, (C/G) %% 8 == 0, "
+                                   "16-B aligned buffers)");
+    return 1;
+  }
+  const int nch = (int)((T + kGnRows - 1) / kGnRows);
+  const unsigned grid = (unsigned)(B * nch);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(gn_cl_stats, dim3(grid), dim3(256), 0, st, x, (int)T, (int)C, (int)G, nch, part);
+  int rc;
+  if ((rc = status("groupnorm stats"))) return rc;
+  hipLaunchKernelGGL(gn_cl_apply, dim3(grid), dim3(256), 0, st, x, part, gamma, beta, (int)T, (int)C, (int)G, nch, eps,
+                     out32, (long long)out32_batch_stride, out16, mean, rstd);
+  return status("groupnorm apply");
+}
+
+int mfl_groupnorm_cl_backward(const float* g32, int64_t g32_batch_stride, const uint16_t* g16, const uint16_t* x,
+                              const float* gamma, const float* mean, const float* rstd, int64_t B, int64_t T,
+                              int64_t C, int64_t G, uint16_t* dx, float* dgamma, float* dbeta, int accumulate,
+                              void* workspace, void* stream) {
+  g_err[0] = 0;
+  if (!gn_cl_ok(B, T, C, G) || !x || !gamma || !mean || !rstd || !dx || !workspace ||
+      (g32 != nullptr && (g32_batch_stride < T * C || g32_batch_stride % 4)) ||
+      (((uintptr_t)x | (uintptr_t)g32 | (uintptr_t)g16 | (uintptr_t)dx) & 15u)) {
+    snprintf(g_err, sizeof(g_err), "mfl_groupnorm_cl_backward: bad arguments");
+    return 1;
+  }
+  const int nch = (int)((T + kGnRows - 1) / kGnRows);
+  const unsigned grid = (unsigned)(B * nch);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  auto* part = static_cast<float*>(workspace);
+  float* sbc = part + B * nch * 2 * C;
+  float* coef = sbc + B * 2 * C;
+  hipLaunchKernelGGL(gn_cl_bwd_partial, dim3(grid), dim3(256), 0, st, g32, (long long)g32_batch_stride, g16, x,
+                     (int)T, (int)C, nch, part);
+  int rc;
+  if ((rc = status("groupnorm backward partials"))) return rc;
+  hipLaunchKernelGGL(gn_cl_bwd_coef, dim3((unsigned)B), dim3(256), 0, st, part, gamma, mean, rstd, (int)T, (int)C,
+                     (int)G, nch, sbc, coef);
+  if ((rc = status("groupnorm backward coefficients"))) return rc;
+  if (dgamma != nullptr || dbeta != nullptr) {
+    hipLaunchKernelGGL(gn_cl_bwd_params, dim3((unsigned)((C + 255) / 256)), dim3(256), 0, st, sbc, mean, rstd, (int)B,
+                       (int)C, (int)G, dgamma, dbeta, accumulate);
+    if ((rc = status("groupnorm backward parameters"))) return rc;
+  }
+  hipLaunchKernelGGL(gn_cl_bwd_apply, dim3(grid), dim3(256), 0, st, g32, (long long)g32_batch_stride, g16, x, gamma,
+                     rstd, coef, (int)T, (int)C, (int)G, nch, dx);
+  return status("groupnorm backward apply");
 }
 
 const char* mfl_add_layernorm_last_error(void) { return g_err; }

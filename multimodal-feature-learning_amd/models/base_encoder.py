@@ -138,21 +138,38 @@ class BaseEncoder(nn.Module):
         """``forward`` with every Conv1d as one GEMM on channels-last rows (_Conv1dGemm) and the
         GroupNorm on the (B, C, T) transpose, as the reference computes it; the returned srcs are
         (B, d_model, T_l) views of channels-last tensors (prepare_encoder_inputs transposes them back)."""
-        from .modules.pyramid import LevelPositions
+        from .modules.pyramid import LevelPositions, group_norm_cl, group_norm_cl_supported
         vf_nt = NestedTensor(vf.transpose(1, 2), mask, duration)
         srcs, masks, dtypes = [], [], []
+        # the levels' lengths (k3 s2 p1 halves them), so the channels-last GroupNorm can write every
+        # level's rows into the encoder's flattened input directly (pyramid.flatten_levels)
+        Ts = [vf.shape[1]]
+        for _ in range(1, self.num_feature_levels):
+            Ts.append((Ts[-1] - 1) // 2 + 1)
+        flat = None
 
-        def level(l, x_cl):
+        def level(l, x_cl, want16):
+            nonlocal flat
             conv, norm = self.input_proj[l][0], self.input_proj[l][1]
             y = conv1d_gemm(conv, x_cl)
-            return F.group_norm(y.transpose(1, 2).contiguous(), norm.num_groups, norm.weight, norm.bias, norm.eps)
+            if group_norm_cl_supported(y, norm) and y.shape[1] == Ts[l]:
+                if flat is None:
+                    flat = torch.empty(y.shape[0], sum(Ts), y.shape[2], dtype=torch.float32, device=y.device)
+                out32, out16 = group_norm_cl(y, norm, flat, sum(Ts[:l]), want16)
+                src = out32.transpose(1, 2)
+                src._mfl_flat = flat
+                return src, out16
+            src = F.group_norm(y.transpose(1, 2).contiguous(), norm.num_groups, norm.weight, norm.bias, norm.eps)
+            return src, src.transpose(1, 2)
 
-        srcs.append(level(0, vf))
+        # level 1 convolves the input features as level 0 does, every later level the previous level
+        # (reference base_encoder.py:79-86)
+        src, _ = level(0, vf, False)
+        srcs.append(src)
         masks.append(mask)
         prev_cl = vf
         for l in range(1, self.num_feature_levels):
-            src = level(l, prev_cl)
-            prev_cl = src.transpose(1, 2)
+            src, prev_cl = level(l, prev_cl, l + 1 < self.num_feature_levels)
             m = vf_nt.mask
             lmask = F.interpolate(m[None].float(), size=src.shape[-1:]).to(torch.bool)[0]
             srcs.append(src)

@@ -13,7 +13,7 @@ import torch
 from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
-from ..modules.pyramid import level_pos_flatten
+from ..modules.pyramid import flatten_levels, level_pos_flatten
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear
@@ -79,7 +79,7 @@ class MultimodalDeformableTransformer(nn.Module):
 
     def prepare_encoder_inputs(self, srcs, masks, pos_embeds):
         """One modality's pyramid -> flattened inputs (reference :87-131)."""
-        src_flatten = torch.cat([s.transpose(1, 2) for s in srcs], 1)
+        src_flatten = flatten_levels(srcs)
         lvl_pos_embed_flatten = level_pos_flatten(pos_embeds, self.level_embed)
         mask_flatten = torch.cat(list(masks), 1)
         temporal_shapes, level_start_index = level_metadata([s.shape[-1] for s in srcs], src_flatten.device)

@@ -16,7 +16,7 @@ import torch.nn.functional as F
 from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
-from ..modules.pyramid import level_pos_flatten
+from ..modules.pyramid import flatten_levels, level_pos_flatten
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear, flush_point
@@ -128,7 +128,7 @@ class DeformableTransformer(nn.Module):
         :return src_flatten, temporal_shapes (L,), level_start_index (L,), valid_ratios (B, L),
                 lvl_pos_embed_flatten (B, S, d_model), mask_flatten (B, S)
         (reference :90-134)"""
-        src_flatten = torch.cat([s.transpose(1, 2) for s in srcs], 1)
+        src_flatten = flatten_levels(srcs)
         lvl_pos_embed_flatten = level_pos_flatten(pos_embeds, self.level_embed)
         mask_flatten = torch.cat(list(masks), 1)
         temporal_shapes, level_start_index = level_metadata([s.shape[-1] for s in srcs], src_flatten.device)

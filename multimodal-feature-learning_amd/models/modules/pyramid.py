@@ -15,7 +15,7 @@ import ctypes
 import torch
 from torch.autograd import Function
 
-__all__ = ["level_pos_flatten", "LevelPositions"]
+__all__ = ["level_pos_flatten", "LevelPositions", "group_norm_cl", "flatten_levels"]
 
 
 def _reference(pos_embeds, level_embed):
@@ -216,3 +216,125 @@ def level_pos_flatten(pos_embeds, level_embed):
     if not _supported(pos_embeds, level_embed):
         return _reference(pos_embeds, level_embed)
     return _LevelPosFlatten.apply(level_embed, *pos_embeds)
+
+
+class _GroupNormCL(Function):
+    """GroupNorm of channels-last bf16 rows x (B, T, C) (include/add_layernorm.h mfl_groupnorm_cl_*):
+    the fp32 output is written into ``flat`` (B, S, C) at rows [start, start + T) and returned as that
+    view; with ``want16`` also its bf16 copy (the next level's convolution input)."""
+
+    @staticmethod
+    def forward(ctx, x, weight, bias, groups, eps, flat, start, want16):
+        from ... import _native, _trace
+        _trace.hit("groupnorm_cl")
+        lib = _native.load_library()
+        B, T, C = x.shape
+        out32 = flat[:, start:start + T]
+        out16 = torch.empty(B, T, C, dtype=torch.bfloat16, device=x.device) if want16 else None
+        mean = torch.empty(B, groups, dtype=torch.float32, device=x.device)
+        rstd = torch.empty(B, groups, dtype=torch.float32, device=x.device)
+        ws = torch.empty(lib.mfl_groupnorm_cl_workspace_bytes(B, T, C, groups), dtype=torch.uint8, device=x.device)
+        rc = lib.mfl_groupnorm_cl_forward(x.data_ptr(), weight.data_ptr(), bias.data_ptr(), B, T, C, groups,
+                                          float(eps), out32.data_ptr(), flat.stride(0),
+                                          None if out16 is None else out16.data_ptr(), mean.data_ptr(),
+                                          rstd.data_ptr(), ws.data_ptr(), _native.stream_handle(x.device))
+        if rc != 0:
+            raise RuntimeError("mfl_groupnorm_cl_forward failed: " + lib.mfl_add_layernorm_last_error().decode())
+        ctx.save_for_backward(x, weight, mean, rstd)
+        ctx.groups, ctx.params = groups, (weight, bias)
+        ctx.set_materialize_grads(False)
+        return out32, out16
+
+    @staticmethod
+    def backward(ctx, g32, g16):
+        from ... import _native
+        from .linear import _accum_target, _claim
+        x, weight, mean, rstd = ctx.saved_tensors
+        B, T, C = x.shape
+        G = ctx.groups
+        lib = _native.load_library()
+        if g32 is not None and (g32.dtype != torch.float32 or g32.stride(2) != 1 or g32.stride(1) != C):
+            g32 = g32.float().contiguous()
+        if g16 is not None:
+            g16 = g16.to(torch.bfloat16).contiguous()
+        dx = torch.empty(B, T, C, dtype=torch.bfloat16, device=x.device)
+        nig = ctx.needs_input_grad
+        w, b = ctx.params
+        accs = (_accum_target(w), _accum_target(b)) if nig[1] and nig[2] else (None, None)
+        accumulate = accs[0] is not None and accs[1] is not None
+        if accumulate:  # (the multimodal audio pyramid shares the BaseEncoder)
+            dw, db = accs
+        else:
+            dw = (_claim(w) if nig[1] else None)
+            db = (_claim(b) if nig[2] else None)
+            dw = dw if dw is not None else torch.empty(C, dtype=torch.float32, device=x.device)
+            db = db if db is not None else torch.empty(C, dtype=torch.float32, device=x.device)
+        ws = torch.empty(lib.mfl_groupnorm_cl_workspace_bytes(B, T, C, G), dtype=torch.uint8, device=x.device)
+        rc = lib.mfl_groupnorm_cl_backward(None if g32 is None else g32.data_ptr(),
+                                           0 if g32 is None else g32.stride(0),
+                                           None if g16 is None else g16.data_ptr(), x.data_ptr(), weight.data_ptr(),
+                                           mean.data_ptr(), rstd.data_ptr(), B, T, C, G, dx.data_ptr(),
+                                           dw.data_ptr(), db.data_ptr(), 1 if accumulate else 0, ws.data_ptr(),
+                                           _native.stream_handle(x.device))
+        if rc != 0:
+            raise RuntimeError("mfl_groupnorm_cl_backward failed: " + lib.mfl_add_layernorm_last_error().decode())
+        if accumulate:
+            dw = db = None
+        return (dx, dw if nig[1] else None, db if nig[2] else None, None, None, None, None, None)
+
+
+def group_norm_cl_supported(x, norm):
+    from ... import _native
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3 and x.is_contiguous()
+            and isinstance(norm, torch.nn.GroupNorm) and norm.affine and norm.weight.dtype == torch.float32
+            and norm.weight.device == x.device and norm.num_channels == x.shape[2]
+            and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+        return False
+    B, T, C = x.shape
+    return _native.load_library().mfl_groupnorm_cl_workspace_bytes(B, T, C, norm.num_groups) > 0
+
+
+def group_norm_cl(x, norm, flat, start, want16):
+    """(out32, out16): ``F.group_norm`` of the channels-last x (B, T, C) as the reference's nn.GroupNorm on
+    its (B, C, T) transpose, the fp32 result written into ``flat`` (B, S, C) at rows [start, start + T)
+    (returned as that view, channels last) and its bf16 copy when ``want16``."""
+    with torch.autocast("cuda", enabled=False):
+        return _GroupNormCL.apply(x, norm.weight, norm.bias, norm.num_groups, norm.eps, flat, start, want16)
+
+
+class _JoinLevels(Function):
+    """The levels' rows, written by _GroupNormCL into one (B, S, C) buffer, as that buffer (no copy);
+    the backward hands each level its rows of the gradient."""
+
+    @staticmethod
+    def forward(ctx, flat, *levels):
+        ctx.bounds = [(lv.storage_offset() - flat.storage_offset()) // flat.shape[2] for lv in levels]
+        ctx.sizes = [lv.shape[1] for lv in levels]
+        return flat.view_as(flat)
+
+    @staticmethod
+    def backward(ctx, g):
+        return (None,) + tuple(g[:, s:s + t] for s, t in zip(ctx.bounds, ctx.sizes))
+
+
+def flatten_levels(srcs):
+    """``torch.cat([s.transpose(1, 2) for s in srcs], 1)`` (prepare_encoder_inputs, reference
+    unimodal_deformable_transformer.py:90-134) — without the copy when the levels are the consecutive
+    rows of one buffer (BaseEncoder's channels-last GroupNorm wrote them there)."""
+    rows = [s.transpose(1, 2) for s in srcs]
+    flat = getattr(srcs[0], "_mfl_flat", None)
+    if flat is not None and all(getattr(s, "_mfl_flat", None) is flat for s in srcs):
+        run = 0
+        ok = True
+        for r in rows:
+            if (r.untyped_storage().data_ptr() != flat.untyped_storage().data_ptr() or r.stride() != flat.stride()
+                    or r.storage_offset() != flat.storage_offset() + run * flat.shape[2]):
+                ok = False
+                break
+            run += r.shape[1]
+        if ok and run == flat.shape[1]:
+            from ... import _trace
+            _trace.hit("flatten_levels_view")
+            return _JoinLevels.apply(flat, *rows)
+    return torch.cat(rows, 1)
+

@@ -23,7 +23,7 @@ from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from ..deformable.unimodal_deformable_transformer import encoder_reference_points, level_metadata
-from ..modules.pyramid import level_pos_flatten
+from ..modules.pyramid import flatten_levels, level_pos_flatten
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.linear import Linear
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
@@ -124,7 +124,7 @@ class SparseDeformableTransformer(nn.Module):
         :return src_flatten, temporal_shapes, level_start_index, valid_ratios, lvl_pos_embed_flatten,
                 mask_flatten, backbone_output_proposals, backbone_topk_proposals (B, k),
                 backbone_mask_prediction (B, S), sparse_token_nums (B,)"""
-        src_flatten = torch.cat([s.transpose(1, 2) for s in srcs], 1)
+        src_flatten = flatten_levels(srcs)
         lvl_pos_embed_flatten = level_pos_flatten(pos_embeds, self.level_embed)
         mask_flatten = torch.cat(list(masks), 1)
         temporal_shapes, level_start_index = level_metadata([s.shape[-1] for s in srcs], src_flatten.device)

@@ -331,3 +331,34 @@ def test_pyramid_pos_matches_per_level_embeddings(dev, normalize):
     torch.testing.assert_close(o1, o2, rtol=2e-6, atol=2e-6)
     torch.testing.assert_close(l1, l2, rtol=1e-5, atol=1e-3)
     torch.testing.assert_close(w1, w2, rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,C,G", [(1024, 512, 32), (100, 256, 32), (37, 1024, 16)])
+def test_groupnorm_cl_matches_group_norm(dev, T, C, G):
+    """pyramid.group_norm_cl (mfl_groupnorm_cl_*): GroupNorm of channels-last bf16 rows written into a
+    flattened buffer equals the reference's nn.GroupNorm on the (B, C, T) transpose in fp32 (autocast's
+    group_norm), and so do its input / gamma / beta gradients, for a gradient arriving in fp32 rows of
+    the buffer plus one through the bf16 copy."""
+    pyr = PKG.models.modules.pyramid
+    g = torch.Generator(device=dev).manual_seed(21)
+    B = 3
+    x = (torch.randn(B, T, C, device=dev, generator=g) * 2 + 0.5).bfloat16().requires_grad_(True)
+    norm = torch.nn.GroupNorm(G, C).to(dev)
+    with torch.no_grad():
+        norm.weight.copy_(torch.randn(C, device=dev, generator=g))
+        norm.bias.copy_(torch.randn(C, device=dev, generator=g))
+    flat = torch.full((B, T + 5, C), float("nan"), device=dev)
+    g32 = torch.randn(B, T, C, device=dev, generator=g)
+    g16 = torch.randn(B, T, C, device=dev, generator=g).bfloat16()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        out32, out16 = pyr.group_norm_cl(x, norm, flat, 5, True)
+    ref = torch.nn.functional.group_norm(x.float().transpose(1, 2), G, norm.weight, norm.bias, norm.eps).transpose(1, 2)
+    torch.testing.assert_close(out32, ref, rtol=1e-4, atol=1e-4)
+    assert torch.equal(out16, out32.bfloat16())
+    assert torch.isnan(flat[:, :5]).all() and out32.data_ptr() == flat[:, 5:].data_ptr()
+    got = torch.autograd.grad([out32, out16], [x, norm.weight, norm.bias], [g32, g16])
+    want = torch.autograd.grad(ref, [x, norm.weight, norm.bias], g32 + g16.float())
+    torch.testing.assert_close(got[0].float(), want[0].float(), rtol=2e-2, atol=2e-2 * want[0].abs().max().item())
+    torch.testing.assert_close(got[1], want[1], rtol=1e-3, atol=1e-3 * want[1].abs().max().item())
+    torch.testing.assert_close(got[2], want[2], rtol=1e-3, atol=1e-3 * want[2].abs().max().item())
