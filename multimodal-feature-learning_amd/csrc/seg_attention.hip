@@ -62,6 +62,7 @@ struct Args {
   float* lse;
   const uint16_t* dout;
   uint16_t *dq, *dpk, *dpv;
+  long long rs_k, rs_v;  // dpk / dpv row strides (elements): d, or a caller's column block of a wider buffer
   float* dbias;  // (H, P, 2, 64)
   float* D;      // (n, H, 32)
   int* dead;     // (n)
@@ -817,11 +818,11 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
       for (int r = 0; r < 4; ++r) {
         const int key = j0 + kt * 16 + 4 * g + r;
         if (key >= a.K) continue;
-        const long long off = ((long long)b * a.K + key) * d + h * HD + li;
+        const long long row = (long long)b * a.K + key, col = h * HD + li;
 #pragma unroll
         for (int cb = 0; cb < 4; ++cb) {
-          a.dpk[off + cb * 16] = f2bf(dk[kt][cb][r]);
-          a.dpv[off + cb * 16] = f2bf(dv[kt][cb][r]);
+          a.dpk[row * a.rs_k + col + cb * 16] = f2bf(dk[kt][cb][r]);
+          a.dpv[row * a.rs_v + col + cb * 16] = f2bf(dv[kt][cb][r]);
         }
       }
   }
@@ -888,7 +889,23 @@ int mfl_seg_attention_backward(const void* q, const void* pk, const void* pv, co
                                int64_t K, int64_t Lq, int64_t H, float scale, float p_drop, const int64_t* seed,
                                const void* out, const float* lse, const void* dout, void* dq, void* dpk, void* dpv,
                                float* dbias_part, void* workspace, void* stream) {
+  return mfl_seg_attention_backward_ex(q, pk, pv, bias_k, bias_v, index, order, keep, masked, n, B, K, Lq, H, scale,
+                                       p_drop, seed, out, lse, dout, dq, dpk, dpv, 0, 0, dbias_part, workspace,
+                                       stream);
+}
+
+int mfl_seg_attention_backward_ex(const void* q, const void* pk, const void* pv, const void* bias_k,
+                                  const void* bias_v, const int64_t* index, const int32_t* order,
+                                  const uint8_t* keep, const uint8_t* masked, int64_t n, int64_t B, int64_t K,
+                                  int64_t Lq, int64_t H, float scale, float p_drop, const int64_t* seed,
+                                  const void* out, const float* lse, const void* dout, void* dq, void* dpk,
+                                  void* dpv, int64_t dpk_row_stride, int64_t dpv_row_stride, float* dbias_part,
+                                  void* workspace, void* stream) {
   Args a{};
+  const long long dmod = H * HD;
+  a.rs_k = dpk_row_stride > 0 ? dpk_row_stride : dmod;
+  a.rs_v = dpv_row_stride > 0 ? dpv_row_stride : dmod;
+  if (a.rs_k < dmod || a.rs_v < dmod) return fail("seg_attention: dK / dV row strides below the model width");
   a.q = static_cast<const uint16_t*>(q);
   a.pk = static_cast<const uint16_t*>(pk);
   a.pv = static_cast<const uint16_t*>(pv);

@@ -215,6 +215,11 @@ class MSDeformAttn(nn.Module):
             if input_padding_mask is not None:
                 value = mask_padding_rows(value, input_padding_mask)
         dest = getattr(value, "_mfl_grad_dest", None)  # (value_proj.layer_values' gradient slot)
+        if dest is not None:  # one consumer per slot: a second call on the same value writes its own
+            if getattr(value, "_mfl_grad_dest_taken", False):
+                dest = None
+            else:
+                value._mfl_grad_dest_taken = True
         value = value.view(N, Len_in, self.n_heads, self.d_model // self.n_heads)
         if dest is not None:
             value._mfl_grad_dest = dest.view(value.shape)

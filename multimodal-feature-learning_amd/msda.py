@@ -360,6 +360,11 @@ class MSDAFunction(Function):
         ctx.save_for_backward(value, loc, aw)
         # a strided slot for grad_value offered by value's producer (value_proj.layer_values)
         ctx.gdest = getattr(value, "_mfl_grad_dest", None)
+        if ctx.gdest is not None:
+            if getattr(value, "_mfl_grad_dest_taken", False):  # (one consumer per slot)
+                ctx.gdest = None
+            else:
+                value._mfl_grad_dest_taken = True
         # the row intervals of the row-block backward come with the forward (it reads loc anyway)
         if any(ctx.needs_input_grad[:3]) or layout == LEVEL_MAJOR:
             out, ctx.tiles = msda_forward(value, shapes, starts, loc, aw, padding_mode, want_tiles=True,
