@@ -16,7 +16,7 @@ from torch.nn.init import constant_, normal_, xavier_uniform_
 from ..modules.pyramid import flatten_levels, level_pos_flatten
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
-from ..modules.linear import Linear
+from ..modules.linear import Linear, mark_grad_sum
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_entry, carry_supported, pos_sink
 from ..modules.ffn import relu_dropout
 from ..modules.value_proj import layer_values, layer_values_supported
@@ -151,6 +151,8 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
             return add_layer_norm_carry(src, attn, self.norm1, dropout=self.dropout1)[1]
 
         def ffn(x, next_pos, pos_acc):
+            # x's two consumers (linear1, the residual) sum its gradient in one GEMM (mark_grad_sum)
+            mark_grad_sum(x)
             hidden = relu_dropout(self.linear1(x), self.activation, self.dropout2)
             out, out16, q16 = add_layer_norm_carry(x, self.linear2(hidden), self.norm2, next_pos, self.dropout3,
                                                    pos_acc=pos_acc)
@@ -160,6 +162,10 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
                          video_padding_mask)
         a16 = self_block(audio, audio_reference_points, audio_temporal_shapes, audio_level_start_index,
                          audio_padding_mask)
+        # each stream is the value of one cross-modal call and the query of the other: the two input
+        # gradients summed in one GEMM (mark_grad_sum)
+        mark_grad_sum(v16)
+        mark_grad_sum(a16)
         visual_attended_audio = self.self_attn(a16, audio_reference_points, v16, video_temporal_shapes,
                                                video_level_start_index, video_padding_mask)
         audio_attended_visual = self.self_attn(v16, video_reference_points, a16, audio_temporal_shapes,

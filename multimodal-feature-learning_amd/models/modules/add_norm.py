@@ -177,6 +177,10 @@ def add_layer_norm(r, y, norm: nn.LayerNorm, dropout=None):
     return norm(r + (dropout(y) if dropout is not None else y))
 
 
+def _gsum_tagged(r):
+    return bool(getattr(r, "_mfl_gsum", False))
+
+
 class _AddLayerNormCarry(Function):
     @staticmethod
     def forward(ctx, r, y, weight, bias, pos, eps, p_drop, seed, pos_acc=None):
@@ -202,6 +206,7 @@ class _AddLayerNormCarry(Function):
         ctx.pos_acc = pos_acc if ctx.pos_needs_grad else None
         ctx.n_grads = 9 if pos_acc is not None else 8  # (apply called without pos_acc: 8 inputs)
         ctx.p_drop = p_drop
+        ctx.gsum = _gsum_tagged(r)
         ctx.save_for_backward(r, y, weight, mean, rstd, seed)
         return out, out16, q16
 
@@ -242,6 +247,9 @@ class _AddLayerNormCarry(Function):
         if rc != 0:
             raise RuntimeError(lib.mfl_add_layernorm_last_error().decode())
         _attach_colsum(dy, ysum)
+        if ctx.gsum:
+            from .linear import grad_sum_give
+            grad_sum_give(True, r, dr)
         return (dr, dy, dw, db, (None if acc is not None else dpos), None, None, None, None)[:ctx.n_grads]
 
 

@@ -32,7 +32,7 @@ from .value_proj import linear_group, linear_group_supported
 from ..ops.functions.ms_deform_attn_func import MSDeformAttnFunction  # reference attention.py:310-328
 from ..ops.modules.ms_deform_attn import stack_sampled_values
 from .linear import (Linear, _AutocastLinear, _accum_group, _addmm, _bias_grad, _claim_group, _defer, _mm_nn,
-                     _weight_grad, linear_pair)
+                     _weight_grad, grad_sum_mm, grad_sum_tagged, linear_pair)
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
            "masked_scores_softmax", "mask_padding_rows", "mha_self_attention"]
@@ -102,6 +102,7 @@ class _QueryPrologue(torch.autograd.Function):
         loc, aw = _msda.prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes, layout)
         ctx.save_for_backward(x2, wc, y, aw, ref)
         ctx.shapes, ctx.x_shape, ctx.layout = shapes, x.shape, layout
+        ctx.gsum = grad_sum_tagged(x)
         ctx.params = (wa, ba, wb, bb)
         return loc, aw
 
@@ -112,7 +113,7 @@ class _QueryPrologue(torch.autograd.Function):
         nig = ctx.needs_input_grad
         g2, g_ref = _msda.prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, ctx.shapes, need_ref=nig[9],
                                                  layout=ctx.layout)
-        gx = _mm_nn(g2, wc).view(ctx.x_shape) if nig[0] else None
+        gx = grad_sum_mm(ctx.gsum, x2, g2, wc, ctx.x_shape) if nig[0] else None
         wa, ba, wb, bb = ctx.params
         na = wa.shape[0]
         rest = (None, None, None, None, g_ref, None, None, None)

@@ -37,7 +37,7 @@ import torch.nn.functional as F
 from torch import nn
 
 __all__ = ["Linear", "split_k_chunks", "linear_pair", "deferred_weight_grads", "flush_point",
-           "flat_grad_destinations", "small_addmm", "small_mm_nn"]
+           "flat_grad_destinations", "small_addmm", "small_mm_nn", "mark_grad_sum"]
 
 # GEMM K (input rows) up to which weight gradients are queued and batched: the decoder's 800 query
 # rows (each GEMM too small for the chip).  Not the caption decoder's ~3,200 word tokens (DVC step):
@@ -365,6 +365,9 @@ _dest = None  # flat_grad_destinations: {"views": {id(param): flat view}, "claim
 # later products of a parameter added into the view / .grad in place (False: autograd's accumulation,
 # for A/B tests)
 ACCUMULATE_IN_PLACE = True
+# a tagged activation's later consumer adds its input gradient into an earlier one's in its dgrad GEMM
+# (mark_grad_sum; False: autograd's bf16 add, for A/B tests)
+GRAD_SUM_IN_GEMM = True
 
 
 @contextlib.contextmanager
@@ -433,6 +436,68 @@ def _accum_group(params):
         from ... import _trace
         _trace.hit("grad_accum_view")
     return v
+
+
+def mark_grad_sum(x):
+    """Declare that EVERY consumer of the 16-bit activation x hands its input gradient through
+    grad_sum_mm / grad_sum_give (the multimodal encoder's bf16 streams: v16 is the value of one
+    cross-modal call and the query of the other; an FFN input is linear1's input and the add +
+    LayerNorm's residual).  In the trainer's backward a later consumer's dgrad GEMM then adds its
+    product into the gradient an earlier consumer produced (C += dY W, one rounding of the fp32 sum)
+    instead of autograd's separate bf16 add of the two (a read of both and a write per pair).
+    Returns x."""
+    if x is not None and x.is_cuda and x.is_contiguous() and x.dtype in (torch.bfloat16, torch.float16):
+        x._mfl_gsum = True
+    return x
+
+
+def grad_sum_tagged(x):
+    return bool(getattr(x, "_mfl_gsum", False))
+
+
+def _gsum_registry():
+    d = _dest
+    if d is None or not GRAD_SUM_IN_GEMM:
+        return None
+    return d.setdefault("gsum", {})
+
+
+def _gsum_key(x):
+    return x if isinstance(x, tuple) else (x.data_ptr(), x.numel(), x.dtype)
+
+
+def grad_sum_mm(tagged, x2, g2, w, x_shape):
+    """A tagged (mark_grad_sum) input's gradient ``g2 @ w``: added in place into the gradient an
+    earlier consumer of the same input produced and still holds pending in autograd (then None is
+    returned: autograd gets no second gradient to add), else computed, registered for the later
+    consumers and returned."""
+    reg = _gsum_registry() if tagged else None
+    if reg is None:
+        return _mm_nn(g2, w).view(x_shape)
+    k = _gsum_key(x2)
+    t = reg.get(k)
+    if t is not None and t.dtype == g2.dtype:
+        from ... import _trace
+        _trace.hit("grad_sum_into")
+        t.view(-1, w.shape[1]).addmm_(g2, w)
+        return None
+    gx = _mm_nn(g2, w).view(x_shape)
+    reg[k] = gx
+    return gx
+
+
+def grad_sum_give(tagged, x, g):
+    """A consumer of tagged input x returning its gradient ``g`` to autograd as usual: g becomes the
+    gradient later consumers add into — or, when an earlier consumer's is registered (autograd now
+    adds the two out of place, leaving that tensor behind), the registration is dropped."""
+    reg = _gsum_registry() if tagged else None
+    if reg is None or g is None:
+        return
+    k = _gsum_key(x)  # (x: the input, or its key taken in the forward)
+    if k in reg:
+        del reg[k]
+    elif g.is_contiguous() and g.dtype == k[2] and g.numel() == k[1]:
+        reg[k] = g
 
 
 def _given_colsum(gy, n):
@@ -567,6 +632,7 @@ class _AutocastLinear(torch.autograd.Function):
         ctx.save_for_backward(x2, wc)
         ctx.has_bias = bias is not None
         ctx.x_shape = x.shape
+        ctx.gsum = grad_sum_tagged(x)
         ctx.weight, ctx.bias = weight, bias  # the parameters a deferred gradient is delivered to
         # not an autograd view of the 2-D GEMM output (as F.linear's 3-D result): callers may
         # modify it in place (MSDeformAttn zeroes the padding rows of value_proj's output)
@@ -580,7 +646,7 @@ class _AutocastLinear(torch.autograd.Function):
         gx = gw = gb = None
         nig = ctx.needs_input_grad
         if nig[0]:
-            gx = _mm_nn(g2, wc).view(ctx.x_shape)
+            gx = grad_sum_mm(ctx.gsum, x2, g2, wc, ctx.x_shape)
         if nig[1] and (not ctx.has_bias or nig[2]) and _defer((g2, x2, ctx.weight, 0, ctx.bias if ctx.has_bias else None,
                                                                 cs)):
             return gx, None, None, None, None
@@ -619,6 +685,7 @@ class _AutocastLinearPair(torch.autograd.Function):
         yb = _addmm(bb.to(dt) if bcb is None else bcb, x2, wcb)
         ctx.save_for_backward(x2, wca, wcb)
         ctx.x_shape = x.shape
+        ctx.gsum = grad_sum_tagged(x)
         ctx.params = (wa, ba, wb, bb)
         lead = x.shape[:-1]
         return ya.view(*lead, wca.shape[0]), yb.view(*lead, wcb.shape[0])
@@ -633,6 +700,7 @@ class _AutocastLinearPair(torch.autograd.Function):
         g2 = torch.cat((ga, gb_), 1)
         nig = ctx.needs_input_grad
         gx = torch.mm(g2, torch.cat((wca, wcb), 0)).view(ctx.x_shape) if nig[0] else None
+        grad_sum_give(ctx.gsum, x2, gx)
         wa, ba, wb, bb = ctx.params
         if all(nig[1:5]) and _defer((ga, x2, wa, 0, ba), (gb_, x2, wb, 0, bb)):
             return gx, None, None, None, None, None, None, None, None

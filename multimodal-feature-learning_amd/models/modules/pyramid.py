@@ -181,7 +181,10 @@ class _PyramidPos(Function):
 
 
 def _pyramid_supported(pos, level_embed):
+    import os
     from .embedding_layers import PositionEmbeddingVideoSine
+    if os.environ.get("MFL_PYRAMID_POS", "1") == "0":  # (A/B: the per-level embeddings + mfl_level_pos_flatten)
+        return False
     mod = pos.pos_embed
     if not (type(mod) is PositionEmbeddingVideoSine and level_embed.is_cuda and level_embed.dtype == torch.float32
             and level_embed.is_contiguous() and level_embed.dim() == 2 and level_embed.shape[0] == len(pos.masks)
@@ -284,7 +287,10 @@ class _GroupNormCL(Function):
 
 
 def group_norm_cl_supported(x, norm):
+    import os
     from ... import _native
+    if os.environ.get("MFL_GROUPNORM_CL", "1") == "0":  # (A/B: the reference's transposes + nn.GroupNorm)
+        return False
     if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 3 and x.is_contiguous()
             and isinstance(norm, torch.nn.GroupNorm) and norm.affine and norm.weight.dtype == torch.float32
             and norm.weight.device == x.device and norm.num_channels == x.shape[2]

@@ -20,12 +20,13 @@ import os
 import torch
 import torch.nn.functional as F
 from torch import nn
+from torch.autograd import Function
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from ..deformable.unimodal_deformable_transformer import encoder_reference_points, level_metadata
 from ..modules.pyramid import flatten_levels, level_pos_flatten
 from ..modules.attention import MSDeformAttn, mha_self_attention
-from ..modules.linear import Linear
+from ..modules.linear import Linear, grad_sum_give, grad_sum_tagged, mark_grad_sum
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 from ..modules.ffn import relu_dropout
 from ..modules.misc_modules import inverse_sigmoid
@@ -35,6 +36,58 @@ __all__ = [
     "DeformableTransformerDecoderLayer", "DeformableTransformerDecoder", "MaskPredictor",
     "build_sparse_deforamble_transformer",
 ]
+
+
+class _GatherRows(Function):
+    """``src.gather(1, topk[..., None].expand(-1, -1, C))`` for src (B, S, C) by flat row index
+    (``rows`` = b * S + topk, unique per clip): index_select over rows instead of an expanded
+    (B, k, C) int64 index (18.9 MB at the bench shape, read by the gather and again by its
+    scatter_add backward); the backward copies the gradient rows into a zeroed (B, S, C)."""
+
+    @staticmethod
+    def forward(ctx, src, rows, k):
+        B, S, C = src.shape
+        ctx.save_for_backward(rows)
+        ctx.shape = (B, S, C)
+        return src.reshape(B * S, C).index_select(0, rows).view(B, k, C)
+
+    @staticmethod
+    def backward(ctx, g):
+        (rows,) = ctx.saved_tensors
+        B, S, C = ctx.shape
+        gs = g.new_zeros(B * S, C)
+        gs.index_copy_(0, rows, g.reshape(-1, C))
+        return gs.view(B, S, C), None, None
+
+
+class _ScatterRows(Function):
+    """``prev.scatter(1, topk[..., None].expand(-1, -1, C), new)`` by flat row index (as _GatherRows):
+    a copy of prev with those rows replaced.  Backward: prev's gradient is a copy with the rows
+    zeroed — handed through ``grad_sum_give`` when prev is tagged (``mark_grad_sum``: the MSDA value
+    projection of the next layer then adds its input gradient into it in its GEMM) — and new's the
+    gathered rows."""
+
+    @staticmethod
+    def forward(ctx, prev, rows, new):
+        B, S, C = prev.shape
+        out = prev.contiguous().clone()
+        out.view(B * S, C).index_copy_(0, rows, new.reshape(-1, C).to(out.dtype))
+        ctx.save_for_backward(rows)
+        ctx.gsum = grad_sum_tagged(prev)
+        ctx.key = (prev.data_ptr(), prev.numel(), prev.dtype)
+        ctx.new_shape, ctx.new_dtype = new.shape, new.dtype
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        (rows,) = ctx.saved_tensors
+        C = g.shape[-1]
+        g = g.contiguous()
+        g_new = g.view(-1, C).index_select(0, rows).view(ctx.new_shape).to(ctx.new_dtype)
+        g_prev = g.clone()
+        g_prev.view(-1, C).index_fill_(0, rows, 0)
+        grad_sum_give(ctx.gsum, ctx.key, g_prev)
+        return g_prev, None, g_new
 
 
 class SparseDeformableTransformer(nn.Module):
@@ -274,8 +327,16 @@ class DeformableTransformerEncoder(nn.Module):
             reference_points = torch.gather(reference_points.view(B, N, -1), 1,
                                             topk.unsqueeze(-1).expand(-1, -1, S_ * P_)).view(B, -1, S_, P_)
             idx = topk.unsqueeze(-1).expand(-1, -1, output.size(-1))
-            tgt = torch.gather(output, 1, idx)
-            pos = torch.gather(pos, 1, topk.unsqueeze(-1).expand(-1, -1, pos.size(-1)))
+            by_rows = (output.is_cuda and os.environ.get("MFL_SPARSE_ROWS", "1") != "0"
+                       and pos is not None and pos.shape == output.shape)
+            if by_rows:
+                # flat row indices b * S + topk (unique per clip): gathers / scatters by row (_GatherRows)
+                rows = (topk + torch.arange(B, device=topk.device)[:, None] * output.shape[1]).reshape(-1)
+                tgt = _GatherRows.apply(output, rows, topk.shape[1])
+                pos = _GatherRows.apply(pos.contiguous(), rows, topk.shape[1])
+            else:
+                tgt = torch.gather(output, 1, idx)
+                pos = torch.gather(pos, 1, topk.unsqueeze(-1).expand(-1, -1, pos.size(-1)))
             if output_proposals is not None:
                 output_proposals = output_proposals.gather(1, topk.unsqueeze(-1).expand(-1, -1,
                                                                                          output_proposals.size(-1)))
@@ -294,6 +355,10 @@ class DeformableTransformerEncoder(nn.Module):
             from ... import _trace
             _trace.hit("sparse_carry")
             value16 = output.to(torch.get_autocast_dtype("cuda"))
+            if by_rows:
+                return self._forward_carry_rows(output, value16, tgt, pos, rows, keep if sparse_token_nums is not None
+                                                else None, reference_points, temporal_shapes, level_start_index,
+                                                padding_mask, inv, output_proposals)
             query = tgt + pos
             for i, layer in enumerate(self.layers):
                 next_pos = pos if i + 1 < len(self.layers) else None
@@ -344,6 +409,45 @@ class DeformableTransformerEncoder(nn.Module):
             outputs_coords = (output_proposals.squeeze(0) + self.segment_embedding(enc_inter_tgt[:-1])).sigmoid()
             return output, sampling_locations_enc, attn_weights_enc, outputs_count, outputs_coords
         return output, sampling_locations_enc, attn_weights_enc, None, None
+
+
+    def _forward_carry_rows(self, src, value16, tgt, pos, rows, keep, reference_points, temporal_shapes,
+                            level_start_index, padding_mask, inv, output_proposals):
+        """The carry loop with the top-k tokens written back by row (_ScatterRows).  The fp32 memory is
+        read by nothing but the next layer's write-back, and every layer writes the same rows, so it is
+        written once, after the last layer: ``src`` with the kept top-k rows replaced by the last
+        layer's output (the same memory the reference's per-layer scatters leave).  The bf16 value
+        copy is rewritten per layer (the next layer's MSDA reads it); the rows a clip does not keep
+        hold bf16(src)'s values throughout (``keep``: reference :445-448)."""
+        from ... import _trace
+        _trace.hit("sparse_rows")
+        first = tgt
+        const16 = first.to(value16.dtype) if keep is not None else None
+        query = tgt + pos
+        locs, weights, inter = [], [], []
+        for i, layer in enumerate(self.layers):
+            next_pos = pos if i + 1 < len(self.layers) else None
+            # value16's two consumers (this layer's value projection, the write-back below) sum its
+            # gradient in the projection's dgrad GEMM (mark_grad_sum)
+            mark_grad_sum(value16)
+            tgt, tgt16, q16, sampling_locations, attn_weights = layer.forward_carry(
+                value16, tgt, query, next_pos, reference_points, temporal_shapes, level_start_index, padding_mask)
+            locs.append(sampling_locations)
+            weights.append(attn_weights)
+            new16 = tgt16.to(value16.dtype)
+            if keep is not None:
+                new16 = torch.where(keep, new16, const16)
+            value16 = _ScatterRows.apply(value16, rows, new16)
+            query = q16
+            if self.aux_heads:
+                inter.append(tgt)
+        new = tgt if keep is None else torch.where(keep, tgt, first)
+        output = _ScatterRows.apply(src, rows, new)
+        output._mfl_bf16 = value16
+        return self._encoder_returns(output, locs, weights, inter, inv, output_proposals)
+
+    def _encoder_returns(self, output, locs, weights, inter, inv, output_proposals):
+        return self._encoder_returns(output, locs, weights, inter, inv, output_proposals)
 
 
 class DeformableTransformerDecoderLayer(nn.Module):

@@ -317,10 +317,11 @@ def test_pyramid_pos_matches_per_level_embeddings(dev, normalize):
         emb_mod.zero_grad(set_to_none=True)
         level_embed.grad = None
         lp = pyr.LevelPositions(emb_mod, srcs, masks, duration, [torch.float32] * len(Ts))
-        if not fused:
-            list(lp)  # materialise: the per-level reference chain
-        PKG._trace.clear()
         with torch.autocast("cuda", dtype=torch.bfloat16):
+            # (the model builds its positions under autocast: the duration embedding's Linear in bf16)
+            if not fused:
+                list(lp)  # materialise: the per-level reference chain
+            PKG._trace.clear()
             out = pyr.level_pos_flatten(lp, level_embed)
         assert (PKG._trace.hits.get("pyramid_pos", 0) == 1) == fused
         (out * go).sum().backward()

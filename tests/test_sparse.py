@@ -143,15 +143,23 @@ def test_sparse_encoder_carry_matches_plain_bf16(dev, monkeypatch):
                                       dec_layers=2, ff_dim=512, dropout=0.0).to(dev)
     video, mask, dur = PKG.dvc_core.synthetic_clips(3, T=128, feature_dim=256, padded=True, seed=7, device=dev)
     res = []
-    for carry in ("1", "0"):
+    # carry with the row write-backs (_ScatterRows: the fp32 memory written once), carry with the
+    # per-layer scatters, the plain layer path
+    for carry, rows_ in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("MFL_SPARSE_CARRY", carry)
+        monkeypatch.setenv("MFL_SPARSE_ROWS", rows_)
         core.zero_grad(set_to_none=True)
+        PKG._trace.clear()
         with torch.autocast("cuda", dtype=torch.bfloat16):
             out = core(video, mask, dur)
             loss = PKG.dvc_core.sparse_workload_loss(out)
         loss.backward()
+        assert (PKG._trace.hits.get("sparse_rows", 0) > 0) == (carry == "1" and rows_ == "1")
         res.append(([out[k].detach().float().clone() for k in ("memory", "hs", "all_segments", "all_counts")],
                     {n: p.grad.detach().clone() for n, p in core.named_parameters() if p.grad is not None}))
+    (fr, gr) = res.pop(0)
+    for x, y in zip(fr, res[0][0]):
+        assert torch.equal(x, y)
     core64 = copy.deepcopy(core).double()
     core64.zero_grad(set_to_none=True)
     torch.set_default_dtype(torch.float64)  # (tensors the model allocates with the default dtype)
@@ -163,18 +171,19 @@ def test_sparse_encoder_carry_matches_plain_bf16(dev, monkeypatch):
     (fa, ga), (fb, gb) = res
     for x, y in zip(fa, fb):
         assert torch.equal(x, y)
-    assert ga.keys() == gb.keys() and len(ga) > 20
+    assert ga.keys() == gb.keys() == gr.keys() and len(ga) > 20
 
     def rel(a, b):
         return ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
 
     rows, bad = [], []
     for n in ga:
-        d_ab = rel(ga[n], gb[n])
-        e_a, e_b = rel(ga[n], g64[n]), rel(gb[n], g64[n])
-        rows.append((n, round(d_ab, 5), round(e_a, 5), round(e_b, 5)))
-        if d_ab >= 2e-3 and e_a > 1.5 * e_b + 2e-3:
-            bad.append(rows[-1])
+        for gx in (ga, gr):  # (both carry paths against the plain one)
+            d_ab = rel(gx[n], gb[n])
+            e_a, e_b = rel(gx[n], g64[n]), rel(gb[n], g64[n])
+            rows.append((n, round(d_ab, 5), round(e_a, 5), round(e_b, 5)))
+            if d_ab >= 2e-3 and e_a > 1.5 * e_b + 2e-3:
+                bad.append(rows[-1])
     print("carry vs plain (name, difference, carry vs fp64, plain vs fp64), largest:",
           sorted(rows, key=lambda r: -r[1])[:6])
     assert not bad, bad

@@ -421,6 +421,48 @@ def test_flat_order_lays_query_projection_pairs_back_to_back():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["multimodal", "sparse"])
+def test_grad_sum_in_gemm(dev, monkeypatch, kind):
+    """linear.mark_grad_sum: an activation whose every consumer takes part (configs[2]'s encoder: each
+    bf16 stream is one cross-modal call's value and the other's query, each FFN input linear1's input
+    and the residual; the Sparse-DETR encoder: the bf16 memory copy is the next layer's MSDA value
+    and its row write-back's input) gets its input gradients summed in the later consumer's dgrad
+    GEMM (C += dY W) instead of autograd's bf16 add.  Same loss; the flat gradient differs from
+    autograd's sums only by that one bf16 rounding per summed pair."""
+    # (d_model 256: the fused carry paths, which tag the activations, need d % 256 == 0)
+    small = dict(d_model=256, num_queries=6, feature_dim=256, num_heads=4, enc_layers=2, dec_layers=2, ff_dim=512,
+                 dropout=0.0)
+    if kind == "multimodal":
+        video, vmask, dur = PKG.dvc_core.synthetic_clips(2, T=256, feature_dim=256, padded=True, device=dev)
+        audio, amask, _ = PKG.dvc_core.synthetic_clips(2, T=16, feature_dim=256, padded=True, seed=9, device=dev)
+        batch = (video, vmask, audio, amask, dur)
+        make = lambda: PKG.dvc_core.MultimodalDVCCore(num_classes=5, **small)  # noqa: E731
+        loss_fn, want = PKG.dvc_core.multimodal_workload_loss, 8  # 2 layers x (v16, a16, two FFN inputs)
+    else:
+        batch = PKG.dvc_core.synthetic_clips(3, T=128, feature_dim=256, padded=True, seed=7, device=dev)
+        make = lambda: PKG.dvc_core.SparseDVCCore(**small)  # noqa: E731
+        loss_fn, want = PKG.dvc_core.sparse_workload_loss, 2  # the bf16 memory copy before each layer
+
+    def run(on):
+        monkeypatch.setattr(PKG.models.modules.linear, "GRAD_SUM_IN_GEMM", on)
+        torch.manual_seed(0)
+        tr = PKG.train_step.FlatGradTrainer(make().to(dev), loss_fn, lr=1e-3, use_bf16=True, graph=False)
+        PKG._trace.clear()
+        loss = tr._forward_backward(batch)
+        torch.cuda.synchronize()
+        return loss, tr.flat_grad.clone(), dict(PKG._trace.hits), [p.numel() for p in tr.params], tr._offs
+
+    loss_r, ref, hits_r, sizes, offs = run(False)
+    loss, got, hits, _, _ = run(True)
+    assert hits_r.get("grad_sum_into", 0) == 0 and hits.get("grad_sum_into", 0) == want, hits
+    assert torch.equal(loss, loss_r)
+    assert ((got - ref).norm() / ref.norm()).item() < 5e-3
+    for i, (n, off) in enumerate(zip(sizes, offs)):
+        a, b = got[off:off + n].double(), ref[off:off + n].double()
+        assert (a - b).norm().item() <= 2e-2 * b.norm().item() + 1e-6, i
+
+
+@pytest.mark.gpu
 def test_shared_layer_gradients_accumulate_into_flat_views(dev, monkeypatch):
     """configs[2]'s encoder calls one self-attention module four times a layer (the two video calls
     take the weight-gradient GEMMs, the two short audio ones the deferred queue) and its decoder one
@@ -436,6 +478,8 @@ def test_shared_layer_gradients_accumulate_into_flat_views(dev, monkeypatch):
 
     def run(in_place):
         monkeypatch.setattr(PKG.models.modules.linear, "ACCUMULATE_IN_PLACE", in_place)
+        # (activation gradients as autograd sums them in both runs: test_grad_sum_in_gemm)
+        monkeypatch.setattr(PKG.models.modules.linear, "GRAD_SUM_IN_GEMM", False)
         torch.manual_seed(0)
         model = PKG.dvc_core.MultimodalDVCCore(num_classes=5, **small).to(dev)
         tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.multimodal_workload_loss, lr=1e-3, use_bf16=True,
@@ -450,6 +494,7 @@ def test_shared_layer_gradients_accumulate_into_flat_views(dev, monkeypatch):
     loss, got, hits, _, _ = run(True)
     assert hits_r.get("grad_accum_view", 0) == 0 and hits_r.get("wgrad_into_grad", 0) == 0, hits_r
     assert hits.get("grad_accum_view", 0) > 0 and hits.get("wgrad_into_grad", 0) > 0, hits
+
     assert torch.equal(loss, loss_r)
     # not bit for bit: the decoders' per-tap MSDA backward sums each value row's list in the order its
     # atomics placed the taps, which varies run to run, and bf16 GEMMs carry that upstream.  So the
