@@ -406,37 +406,57 @@ __device__ __forceinline__ void store_bf16x8(uint16_t* p, const float (&v)[8]) {
   *reinterpret_cast<uint4*>(p) = u;
 }
 
-// partial sums (sum, sum of squares) of every group over one workgroup's rows
+// per-workgroup statistics of every group over the workgroup's rows: (mean, M2 = sum of squared
+// deviations from that mean), two passes over the rows (the second from cache) — merged per (b, g)
+// by gn_cl_apply (Chan et al.'s pairwise update), as robust as ATen's Welford moments when a group's
+// mean is large against its spread (a one-pass E[x^2] - mean^2 cancels there)
 __global__ __launch_bounds__(256) void gn_cl_stats(const uint16_t* __restrict__ x, int T, int C, int G, int nch,
                                                    float* __restrict__ part) {
-  __shared__ float rs[256], rss[256];
+  __shared__ float rs[256], s_m[128];
   const int blk = (int)blockIdx.x;
   const long long b = blk / nch;
   const int r0 = (blk % nch) * kGnRows, r1 = min(T, r0 + kGnRows);
   const int CL = C / 8, RL = 256 / CL;
   const int cl = (int)threadIdx.x % CL, rl = (int)threadIdx.x / CL;
-  float sum = 0.f, sq = 0.f;
+  const int lpg = C / G / 8;
+  const float nb = (float)(r1 - r0) * (float)(C / G);
+  float sum = 0.f;
+  for (int r = r0 + rl; r < r1; r += RL) {
+    float v[8];
+    load_bf16x8(x + ((b * T + r) * C + cl * 8), v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sum += v[k];
+  }
+  rs[threadIdx.x] = sum;
+  __syncthreads();
+  if ((int)threadIdx.x < G) {
+    const int g = (int)threadIdx.x;
+    float a = 0.f;
+    for (int r = 0; r < RL; ++r)
+      for (int l = g * lpg; l < (g + 1) * lpg; ++l) a += rs[r * CL + l];
+    s_m[g] = a / nb;
+  }
+  __syncthreads();
+  const float m = s_m[cl / lpg];
+  float sq = 0.f;
   for (int r = r0 + rl; r < r1; r += RL) {
     float v[8];
     load_bf16x8(x + ((b * T + r) * C + cl * 8), v);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      sum += v[k];
-      sq += v[k] * v[k];
+      const float d = v[k] - m;
+      sq += d * d;
     }
   }
-  rs[threadIdx.x] = sum;
-  rss[threadIdx.x] = sq;
+  __syncthreads();
+  rs[threadIdx.x] = sq;
   __syncthreads();
   if ((int)threadIdx.x < G) {
-    const int g = (int)threadIdx.x, lpg = C / G / 8;
-    float a = 0.f, q = 0.f;
+    const int g = (int)threadIdx.x;
+    float q = 0.f;
     for (int r = 0; r < RL; ++r)
-      for (int l = g * lpg; l < (g + 1) * lpg; ++l) {
-        a += rs[r * CL + l];
-        q += rss[r * CL + l];
-      }
-    part[((long long)blk * G + g) * 2] = a;
+      for (int l = g * lpg; l < (g + 1) * lpg; ++l) q += rs[r * CL + l];
+    part[((long long)blk * G + g) * 2] = s_m[g];
     part[((long long)blk * G + g) * 2 + 1] = q;
   }
 }
@@ -453,14 +473,19 @@ __global__ __launch_bounds__(256) void gn_cl_apply(const uint16_t* __restrict__ 
   const long long b = blk / nch;
   if ((int)threadIdx.x < G) {
     const int g = (int)threadIdx.x;
-    float a = 0.f, q = 0.f;
-    for (int c = 0; c < nch; ++c) {
-      a += part[((b * nch + c) * G + g) * 2];
-      q += part[((b * nch + c) * G + g) * 2 + 1];
-    }
-    const float n = (float)T * (float)(C / G);
+    // merge the workgroups' (mean, M2): the mean weighted by rows, M2 += n_c (mean_c - mean)^2
+    const float per = (float)(C / G);
+    const float n = (float)T * per;
+    float a = 0.f;
+    for (int c = 0; c < nch; ++c) a += part[((b * nch + c) * G + g) * 2] * ((float)(min(T, (c + 1) * kGnRows) - c * kGnRows) * per);
     const float mean = a / n;
-    const float var = fmaxf(q / n - mean * mean, 0.f);
+    float q = 0.f;
+    for (int c = 0; c < nch; ++c) {
+      const float nc = (float)(min(T, (c + 1) * kGnRows) - c * kGnRows) * per;
+      const float d = part[((b * nch + c) * G + g) * 2] - mean;
+      q += part[((b * nch + c) * G + g) * 2 + 1] + nc * d * d;
+    }
+    const float var = fmaxf(q / n, 0.f);
     const float rstd = 1.f / sqrtf(var + eps);
     s_mean[g] = mean;
     s_rstd[g] = rstd;

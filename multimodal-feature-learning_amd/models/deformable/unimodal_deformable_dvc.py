@@ -175,7 +175,10 @@ class UnimodalDeformableDVC(nn.Module):
 
         mask_out = memory_mask_list[-1].squeeze().float() if self.use_differentiable_mask else None
         if is_training:
-            outputs_caption = torch.stack(outputs_captions)
+            # the levels' caption probabilities as the split views of the one decoder call (the
+            # reference stacks them, :281; every consumer reads one level): no (levels, n, L, vocab)
+            # stacking copy, and their gradients meet in the split's one concatenation
+            outputs_caption = outputs_captions
             out['pred_captions'] = outputs_caption[-1]
             outputs_caption_last_layer = torch.argmax(outputs_caption[-1], dim=2)
             indices_aux = []

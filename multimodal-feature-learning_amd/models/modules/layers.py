@@ -12,7 +12,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from .add_norm import add_layer_norm
+from .add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 from .attention import CrossAttention, masked_scores_softmax
 from .linear import Linear
 
@@ -139,12 +139,25 @@ class UnimodalCaptionDecoderLayer(nn.Module):
         # post-norm: norm(x + dropout(branch)) as one fused kernel each way under autocast (the
         # residual add of the fp32 stream and the 16-bit branch alone took ~60 us a call in ATen's
         # mixed-dtype elementwise kernel); exactly the three modules' composition otherwise
-        x = add_layer_norm(x, self.self_attention(x, x, x, attn_mask=tgt_mask, key_padding_mask=tgt_padding_mask)[0],
-                           self.layer_norm_1, self.projection_dropout_1)
+        sa = self.self_attention(x, x, x, attn_mask=tgt_mask, key_padding_mask=tgt_padding_mask)[0]
+        m = self.mlp
+        if carry_supported(x, self.layer_norm_1) and x.dtype == torch.float32:
+            # each fused add + LayerNorm also writes bf16(out): the cross-attention's query projection,
+            # the MLP's first Linear and the next layer's q / k / v projections (value_proj.layer_values
+            # reads ``_mfl_bf16``) take it instead of casting the fp32 stream, and its gradient is summed
+            # into the fp32 one inside the fused backward (no cast-backward and add kernels)
+            x, x16, _ = add_layer_norm_carry(x, sa, self.layer_norm_1, dropout=self.projection_dropout_1)
+            ca = self.cross_attention(x16, memory, memory, attn_mask=memory_mask,
+                                      key_padding_mask=memory_padding_mask)[0]
+            x, x16, _ = add_layer_norm_carry(x, ca, self.layer_norm_2, dropout=self.projection_dropout_2)
+            h = m.dropout_1(m.activation_layer(m.fully_connected_1(x16)))
+            out, out16, _ = add_layer_norm_carry(x, m.fully_connected_2(h), self.layer_norm_3, dropout=m.dropout_2)
+            out._mfl_bf16 = out16
+            return out
+        x = add_layer_norm(x, sa, self.layer_norm_1, self.projection_dropout_1)
         x = add_layer_norm(x, self.cross_attention(x, memory, memory, attn_mask=memory_mask,
                                                    key_padding_mask=memory_padding_mask)[0],
                            self.layer_norm_2, self.projection_dropout_2)
-        m = self.mlp
         h = m.dropout_1(m.activation_layer(m.fully_connected_1(x)))
         return add_layer_norm(x, m.fully_connected_2(h), self.layer_norm_3, m.dropout_2)
 

@@ -27,7 +27,8 @@ from ..deformable.unimodal_deformable_transformer import encoder_reference_point
 from ..modules.pyramid import flatten_levels, level_pos_flatten
 from ..modules.attention import MSDeformAttn, mha_self_attention
 from ..modules.linear import Linear, grad_sum_give, grad_sum_tagged, mark_grad_sum
-from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
+from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_supported, pos_sink
+from ..modules.value_proj import layer_values, layer_values_supported
 from ..modules.ffn import relu_dropout
 from ..modules.misc_modules import inverse_sigmoid
 
@@ -390,26 +391,7 @@ class DeformableTransformerEncoder(nn.Module):
                 output = tgt
             if self.aux_heads:
                 inter.append(tgt)
-        sampling_locations_enc = torch.stack(locs, dim=1)
-        attn_weights_enc = torch.stack(weights, dim=1)
-        if inv is not None:  # back into score order (B, layers, k, ...)
-            def unsort(t, dim):
-                shape = [1] * t.dim()
-                shape[0], shape[dim] = inv.shape[0], inv.shape[1]
-                return t.gather(dim, inv.view(shape).expand(*t.shape[:dim], inv.shape[1], *t.shape[dim + 1:]))
-            sampling_locations_enc = unsort(sampling_locations_enc, 2)
-            attn_weights_enc = unsort(attn_weights_enc, 2)
-            inter = [unsort(t, 1) for t in inter]
-            if output_proposals is not None:
-                output_proposals = unsort(output_proposals, 1)
-        if self.aux_heads:
-            from ..modules.misc_modules import predict_event_num_with_depth
-            enc_inter_tgt = torch.stack(inter)
-            outputs_count = predict_event_num_with_depth(self.count_head, enc_inter_tgt[:-1])
-            outputs_coords = (output_proposals.squeeze(0) + self.segment_embedding(enc_inter_tgt[:-1])).sigmoid()
-            return output, sampling_locations_enc, attn_weights_enc, outputs_count, outputs_coords
-        return output, sampling_locations_enc, attn_weights_enc, None, None
-
+        return self._encoder_returns(output, locs, weights, inter, inv, output_proposals)
 
     def _forward_carry_rows(self, src, value16, tgt, pos, rows, keep, reference_points, temporal_shapes,
                             level_start_index, padding_mask, inv, output_proposals):
@@ -447,7 +429,25 @@ class DeformableTransformerEncoder(nn.Module):
         return self._encoder_returns(output, locs, weights, inter, inv, output_proposals)
 
     def _encoder_returns(self, output, locs, weights, inter, inv, output_proposals):
-        return self._encoder_returns(output, locs, weights, inter, inv, output_proposals)
+        sampling_locations_enc = torch.stack(locs, dim=1)
+        attn_weights_enc = torch.stack(weights, dim=1)
+        if inv is not None:  # back into score order (B, layers, k, ...)
+            def unsort(t, dim):
+                shape = [1] * t.dim()
+                shape[0], shape[dim] = inv.shape[0], inv.shape[1]
+                return t.gather(dim, inv.view(shape).expand(*t.shape[:dim], inv.shape[1], *t.shape[dim + 1:]))
+            sampling_locations_enc = unsort(sampling_locations_enc, 2)
+            attn_weights_enc = unsort(attn_weights_enc, 2)
+            inter = [unsort(t, 1) for t in inter]
+            if output_proposals is not None:
+                output_proposals = unsort(output_proposals, 1)
+        if self.aux_heads:
+            from ..modules.misc_modules import predict_event_num_with_depth
+            enc_inter_tgt = torch.stack(inter)
+            outputs_count = predict_event_num_with_depth(self.count_head, enc_inter_tgt[:-1])
+            outputs_coords = (output_proposals.squeeze(0) + self.segment_embedding(enc_inter_tgt[:-1])).sigmoid()
+            return output, sampling_locations_enc, attn_weights_enc, outputs_count, outputs_coords
+        return output, sampling_locations_enc, attn_weights_enc, None, None
 
 
 class DeformableTransformerDecoderLayer(nn.Module):
@@ -477,14 +477,36 @@ class DeformableTransformerDecoderLayer(nn.Module):
         return add_layer_norm(tgt, self.linear2(hidden), self.norm3, dropout=self.dropout4)
 
     def forward(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
-                src_padding_mask=None, query_mask=None):
-        sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask)
+                src_padding_mask=None, query_mask=None, value=None):
+        """``value``: this layer's cross-attention value, when the decoder computed it (value_proj.py)."""
+        out, _, _, sampling_locations, attn_weights = self.forward_carry(
+            tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index, src_padding_mask,
+            query_mask, value)
+        return out, sampling_locations, attn_weights
+
+    def forward_carry(self, tgt, query_pos, reference_points, src, src_temporal_shapes, level_start_index,
+                      src_padding_mask=None, query_mask=None, value=None, carried=None, pos_acc=None):
+        """``forward`` returning ``(out, out16, q16, sampling_locations, attn_weights)``: as the dense
+        decoder's layer (unimodal_deformable_transformer.py), under bf16 autocast on the GPU the fused
+        add + LayerNorms hand the cross-attention its bf16 query, linear1 its bf16 input and the next
+        layer bf16(out) and bf16(out + query_pos) (``carried``); (out, None, None, ...) otherwise."""
+        sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask, carried)
+        if carry_supported(tgt, self.norm2) and (query_pos is None or query_pos.shape == tgt.shape):
+            tgt, tgt16, q16 = add_layer_norm_carry(tgt, sa, self.norm2, query_pos, self.dropout2, pos_acc=pos_acc)
+            ca, sampling_locations, attn_weights = self.cross_attn(
+                q16 if q16 is not None else tgt16, reference_points, src, src_temporal_shapes, level_start_index,
+                src_padding_mask, is_sparse=True, value=value)
+            tgt, tgt16, _ = add_layer_norm_carry(tgt, ca, self.norm1, dropout=self.dropout1)
+            hidden = relu_dropout(self.linear1(tgt16), self.activation, self.dropout3)
+            out, out16, q16 = add_layer_norm_carry(tgt, self.linear2(hidden), self.norm3, query_pos, self.dropout4,
+                                                   pos_acc=pos_acc)
+            return out, out16, q16, sampling_locations, attn_weights
         tgt = add_layer_norm(tgt, sa, self.norm2, dropout=self.dropout2)
         ca, sampling_locations, attn_weights = self.cross_attn(self.with_pos_embed(tgt, query_pos), reference_points,
                                                                src, src_temporal_shapes, level_start_index,
-                                                               src_padding_mask, is_sparse=True)
+                                                               src_padding_mask, is_sparse=True, value=value)
         tgt = add_layer_norm(tgt, ca, self.norm1, dropout=self.dropout1)
-        return self.forward_ffn(tgt), sampling_locations, attn_weights
+        return self.forward_ffn(tgt), None, None, sampling_locations, attn_weights
 
 
 class DeformableTransformerDecoder(nn.Module):
@@ -497,19 +519,52 @@ class DeformableTransformerDecoder(nn.Module):
         self.return_intermediate = return_intermediate
         self.bbox_head = None
 
+    def flat_groups(self):
+        """Parameters a flat-buffer trainer lays out back to back (train_step._flat_order), as the dense
+        decoder's: each same-shape weight / bias of the layers and the query prologue pairs interleaved,
+        so the batched gradient GEMMs write one view of the flat gradient buffer."""
+        layers = [layer for layer in self.layers if type(layer) is DeformableTransformerDecoderLayer]
+        if len(layers) < 2:
+            return []
+        names = ("linear1.weight", "linear2.weight", "self_attn.out_proj.weight", "cross_attn.value_proj.weight",
+                 "cross_attn.value_proj.bias", "cross_attn.output_proj.weight")
+        groups = [tuple(layer.get_parameter(n) for layer in layers) for n in names]
+        for kind in ("weight", "bias"):
+            groups.append(tuple(layer.get_parameter(f"cross_attn.{n}.{kind}") for layer in layers
+                                for n in ("sampling_offsets", "attention_weights")))
+        return groups
+
     def forward(self, tgt, reference_points, src, src_temporal_shapes, src_level_start_index, src_valid_ratios,
                 query_pos=None, src_padding_mask=None, query_padding_mask=None, disable_iterative_refine=False):
         output = tgt
         hs, refs, locs, weights = [], [], [], []
+        plain = all(type(layer) is DeformableTransformerDecoderLayer for layer in self.layers)
+        values = carried = pos_acc = None
+        if plain:
+            attns = [layer.cross_attn for layer in self.layers]
+            if layer_values_supported(attns, src, src_padding_mask):
+                # every layer projects the same memory (its bf16 copy carried from the encoder): one
+                # batched GEMM each way (value_proj.py), as the dense decoder
+                values = layer_values(attns, src, src_padding_mask)
+            if query_pos is not None and not query_pos.is_contiguous():
+                query_pos = query_pos.contiguous()  # once, not per layer (the fused layers read it flat)
+            query_pos, pos_acc = pos_sink(query_pos)  # its gradient summed in place (add_norm.pos_sink)
         for lid, layer in enumerate(self.layers):
             if reference_points.shape[-1] == 2:
                 ref_in = reference_points[:, :, None] * torch.stack([src_valid_ratios, src_valid_ratios], -1)[:, None]
             else:
                 assert reference_points.shape[-1] == 1
                 ref_in = reference_points[:, :, None] * src_valid_ratios[:, None, :, None]
-            output, sampling_locations, attn_weights = layer(output, query_pos, ref_in, src, src_temporal_shapes,
-                                                             src_level_start_index, src_padding_mask,
-                                                             query_padding_mask)
+            if plain:
+                # bf16 self-attention inputs carried from the previous layer's last add + LayerNorm
+                output, out16, q16, sampling_locations, attn_weights = layer.forward_carry(
+                    output, query_pos, ref_in, src, src_temporal_shapes, src_level_start_index, src_padding_mask,
+                    query_padding_mask, values[lid] if values is not None else None, carried, pos_acc=pos_acc)
+                carried = (out16, q16) if out16 is not None else None
+            else:
+                output, sampling_locations, attn_weights = layer(output, query_pos, ref_in, src, src_temporal_shapes,
+                                                                 src_level_start_index, src_padding_mask,
+                                                                 query_padding_mask)
             locs.append(sampling_locations)
             weights.append(attn_weights)
             if not disable_iterative_refine and self.bbox_head is not None:

@@ -19,6 +19,17 @@ from ..utils.preds_postprocess import SegmentMemory
 __all__ = ["UnimodalCaptionDecoder", "build_unimodal_caption_decoder", "greedy_decode"]
 
 
+def _probs(logits):
+    """``logits.softmax(dim=-1)`` as autocast runs it (softmax is on its fp32 list: the 16-bit logits
+    cast to fp32, then an fp32 softmax): one kernel reading the 16-bit logits and writing fp32 (same
+    values), whose backward writes the logits' 16-bit gradient directly — no (n, L, vocab) fp32 cast
+    pass either way (vocab 10,000: 128 MB a pass at the DVC bench shape)."""
+    if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float16) and torch.is_autocast_enabled("cuda"):
+        with torch.autocast("cuda", enabled=False):
+            return torch.softmax(logits, dim=-1, dtype=torch.float32)
+    return logits.softmax(dim=-1)
+
+
 @torch.no_grad()
 def greedy_decode(decoder, prime, step, n, length, bos, eos, pad, faster_eval, device):
     """Shared greedy loop of both caption decoders (reference unimodal_deformable_dvc.py:304-363).
@@ -91,7 +102,7 @@ class UnimodalCaptionDecoder(nn.Module):
             if self.return_intermediate and not last_only:
                 intermediate.append(tgt)
         tgt = torch.stack(intermediate) if self.return_intermediate and not last_only else tgt.unsqueeze(0)
-        return self.head(tgt).softmax(dim=-1)
+        return _probs(self.head(tgt))
 
     def init_weights(self, embedding_matrix, emb_weights_req_grad):
         self.target_embedding.init_word_embeddings(embedding_matrix, emb_weights_req_grad)

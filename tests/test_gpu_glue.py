@@ -331,7 +331,10 @@ def test_pyramid_pos_matches_per_level_embeddings(dev, normalize):
     o2, l2, w2 = run(False)
     torch.testing.assert_close(o1, o2, rtol=2e-6, atol=2e-6)
     torch.testing.assert_close(l1, l2, rtol=1e-5, atol=1e-3)
-    torch.testing.assert_close(w1, w2, rtol=1e-4, atol=1e-3)
+    # the duration embedding's Linear backward reads its output gradient in bf16 (autocast): the
+    # reference rounds each level's token sum to bf16 and sums the levels' four weight gradients, the
+    # fused path rounds the sum over all levels once — the same terms, one bf16 rounding apart
+    torch.testing.assert_close(w1, w2, rtol=1e-2, atol=1e-2 * w2.abs().max().item())
 
 
 @pytest.mark.gpu
@@ -363,3 +366,47 @@ def test_groupnorm_cl_matches_group_norm(dev, T, C, G):
     torch.testing.assert_close(got[0].float(), want[0].float(), rtol=2e-2, atol=2e-2 * want[0].abs().max().item())
     torch.testing.assert_close(got[1], want[1], rtol=1e-3, atol=1e-3 * want[1].abs().max().item())
     torch.testing.assert_close(got[2], want[2], rtol=1e-3, atol=1e-3 * want[2].abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,T,C", [(2, 64, 256), (8, 1024, 512)])
+def test_base_encoder_channels_last_levels_match_reference_path(dev, monkeypatch, B, T, C):
+    """BaseEncoder under bf16 autocast with the channels-last GroupNorm (rows written into the flattened
+    encoder input, pyramid.flatten_levels joining them without a copy) against the reference's
+    composition (MFL_GROUPNORM_CL=0: nn.GroupNorm on the (B, C, T) transposes, torch.cat): every level,
+    the flattened input and the input / parameter gradients (reference base_encoder.py:62-89,
+    unimodal_deformable_transformer.py:90-134)."""
+    torch.manual_seed(5)
+    enc = PKG.models.base_encoder.BaseEncoder(4, C, C).to(dev)
+    with torch.no_grad():
+        for p in enc.parameters():
+            p.add_(torch.randn_like(p) * 0.3)
+    pos_embed = PKG.models.modules.embedding_layers.PositionEmbeddingVideoSine(C // 2, normalize=True).to(dev)
+    video, mask, dur = PKG.dvc_core.synthetic_clips(B, T=T, feature_dim=C, padded=True, seed=3, device=dev)
+    video = (video * 1.7 + 0.4).requires_grad_(True)
+    pyr = PKG.models.modules.pyramid
+    res = []
+    for on in ("1", "0"):
+        monkeypatch.setenv("MFL_GROUPNORM_CL", on)
+        enc.zero_grad(set_to_none=True)
+        video.grad = None
+        PKG._trace.clear()
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            srcs, masks, _ = enc(video, mask, dur, pos_embed)
+            flat = pyr.flatten_levels(srcs)
+        assert (PKG._trace.hits.get("groupnorm_cl", 0) == 4) == (on == "1"), PKG._trace.hits
+        g = torch.randn(flat.shape, device=dev, generator=torch.Generator(device=dev).manual_seed(9))
+        (flat * g).sum().backward()
+        res.append(([s.detach().float().clone() for s in srcs] + [flat.detach().clone()],
+                    [video.grad.clone()] + [p.grad.clone() for p in enc.parameters()]))
+    (fa, ga), (fb, gb) = res
+    # level 0 as the reference to fp32 summation order; the later levels read the previous level's bf16
+    # copy, where an fp32 difference of one ulp can round the other way (the reference rounds its fp32
+    # GroupNorm output at the next convolution's cast): held to the norm of the level
+    torch.testing.assert_close(fa[0], fb[0], rtol=1e-4, atol=1e-4)
+    for i, (a, b) in enumerate(zip(fa, fb)):
+        err = ((a.double() - b.double()).norm() / b.double().norm()).item()
+        assert err < 1e-3, (i, err)
+    for i, (a, b) in enumerate(zip(ga, gb)):
+        err = ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
+        assert err < 2e-2, (i, err)

@@ -497,9 +497,11 @@ def test_shared_layer_gradients_accumulate_into_flat_views(dev, monkeypatch):
 
     assert torch.equal(loss, loss_r)
     # not bit for bit: the decoders' per-tap MSDA backward sums each value row's list in the order its
-    # atomics placed the taps, which varies run to run, and bf16 GEMMs carry that upstream.  So the
-    # in-place run must be as close to autograd's as two autograd runs are to each other.
+    # atomics placed the taps, which varies run to run, and bf16 GEMMs carry that upstream (a
+    # gradient cast to bf16 may round either way: the duration embedding's, a sum over every token).
+    # So the in-place run must be as close to autograd's as two autograd runs are to each other, up
+    # to 1e-3 of the gradient's norm — far below a missing or doubled contribution of a shared call.
     for i, (n, off) in enumerate(zip(sizes, offs)):
         a, b, c = got[off:off + n].double(), ref[off:off + n].double(), ref2[off:off + n].double()
-        spread = (b - c).abs().max().item()
-        assert (a - b).abs().max().item() <= 4 * spread + 1e-6 * b.abs().max().item() + 1e-9, i
+        spread = (b - c).norm().item()
+        assert (a - b).norm().item() <= 4 * spread + 1e-3 * b.norm().item() + 1e-9, i
