@@ -89,6 +89,9 @@ EXPORTED_SYMBOLS = (
     "mfl_seg_attention_bias_parts",
     "mfl_seg_attention_workspace_bytes",
     "mfl_seg_attention_last_error",
+    # include/host_lsa.h (host code)
+    "mfl_lsa",
+    "mfl_lsa_levels",
     "msda_hip_last_error",
     "msda_hip_abi_version",
 )
@@ -240,6 +243,10 @@ def _declare(lib):
     lib.msda_hip_last_error.argtypes = []
     lib.msda_hip_abi_version.restype = i32
     lib.msda_hip_abi_version.argtypes = []
+    lib.mfl_lsa.restype = i32
+    lib.mfl_lsa.argtypes = [vp, i64, i64, vp, vp]
+    lib.mfl_lsa_levels.restype = i32
+    lib.mfl_lsa_levels.argtypes = [vp, i64, i64, i64, i64, vp, vp, vp, vp]
     return lib
 
 

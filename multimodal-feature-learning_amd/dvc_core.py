@@ -362,8 +362,14 @@ class StagedDVCLoss:
         """get_src_permutation_idx (utils/preds_postprocess.py) of every level, written with numpy
         into the pinned buffer: (clip, prediction) pairs ordered by target within each clip."""
         import numpy as np
-        self.level_indices = self._matcher.solve_levels(cpu, state['cost_meta'])
         ih = self.idx_host.numpy()
+        m = self._matcher
+        if "solve_levels" not in vars(m):
+            # the matching and the index lists in one native call where it applies (solve_levels_into)
+            self.level_indices = type(m).solve_levels_into(cpu, state['cost_meta'], ih)
+            return
+        # (an instance's own solve_levels: a test pinning the assignment)
+        self.level_indices = m.solve_levels(cpu, state['cost_meta'])
         for lvl, ind in enumerate(self.level_indices):
             off = 0
             for b, (src, tgt) in enumerate(ind):

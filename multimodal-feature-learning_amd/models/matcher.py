@@ -64,12 +64,41 @@ class HungarianMatcher(nn.Module):
         """The host half: the reference's syncing asserts (utils/box_ops.py:59-60) and scipy's
         linear_sum_assignment per clip and level (reference :86-94), on numpy views of the one
         copied buffer (the per-clip torch indexing and conversions were most of the host step)."""
+        return HungarianMatcher.solve_levels_into(host, meta, None)
+
+    @staticmethod
+    def solve_levels_into(host, meta, idx_out):
+        """``solve_levels``; with ``idx_out`` (an int64 (levels, 2, n_tgt) array) also writes every
+        level's get_src_permutation_idx (clip, prediction) lists into it.  Every clip's matching in ONE
+        native call (include/host_lsa.h: scipy's algorithm and tie rules) where the levels share their
+        shapes and no clip has more targets than predictions; scipy per clip otherwise (or with
+        MFL_HOST_LSA=0)."""
+        import os
         shapes, sizes, n_tgt, n_flags = meta
         h = host.numpy() if isinstance(host, torch.Tensor) else np.asarray(host)
         ok = h[-n_flags:]
         assert bool(ok[:-1].all()), "Segment start > Segment end (from output)"
         assert bool(ok[-1]), "Segment start > Segment end (from target)"
-        bounds = np.cumsum([0] + list(sizes))
+        bounds = np.cumsum([0] + list(sizes)).astype(np.int64)
+        if (os.environ.get("MFL_HOST_LSA", "1") != "0" and shapes and len(set(shapes)) == 1 and h.dtype == np.float32
+                and max(sizes, default=0) <= shapes[0][1] and n_tgt == int(bounds[-1])):
+            from .. import _native
+            lib = _native.load_library()
+            L = len(shapes)
+            B, Q = shapes[0]
+            cost = np.ascontiguousarray(h[:L * B * Q * n_tgt])
+            src = np.empty((L, n_tgt), np.int64)
+            tgt = np.empty((L, n_tgt), np.int64)
+            idx = idx_out if idx_out is not None else np.empty((L, 2, n_tgt), np.int64)
+            rc = lib.mfl_lsa_levels(cost.ctypes.data, L, B, Q, n_tgt, bounds.ctypes.data, src.ctypes.data,
+                                    tgt.ctypes.data, idx.ctypes.data)
+            if rc == 2:
+                raise ValueError("matrix contains invalid numeric entries")
+            if rc == 3:
+                raise ValueError("cost matrix is infeasible")
+            if rc != 0:
+                raise RuntimeError(f"mfl_lsa_levels failed (status {rc})")
+            return _LevelPairs(src, tgt, bounds, L, B)
         result, off = [], 0
         for B, Q in shapes:
             n = B * Q * n_tgt
@@ -80,7 +109,46 @@ class HungarianMatcher(nn.Module):
                 i, j = linear_sum_assignment(cost[b, :, bounds[b]:bounds[b + 1]])
                 level.append((torch.from_numpy(i.astype(np.int64)), torch.from_numpy(j.astype(np.int64))))
             result.append(level)
+        if idx_out is not None:
+            for lvl, ind in enumerate(result):
+                off = 0
+                for b, (s_, t_) in enumerate(ind):
+                    sv, tv = s_.numpy(), t_.numpy()
+                    k = len(sv)
+                    idx_out[lvl, 0, off:off + k] = b
+                    idx_out[lvl, 1, off:off + k] = sv[np.argsort(tv, kind="stable")]
+                    off += k
         return result
+
+
+class _LevelPairs(list):
+    """solve_levels' result ([level][clip] -> (prediction indices, target indices) int64 tensors) over
+    the native call's flat arrays, built when first read: a replayed DVC step reads only the index
+    lists the call also wrote (the ~200 small tensors cost more host time than the matching)."""
+
+    def __init__(self, src, tgt, bounds, L, B):
+        super().__init__()
+        self._args = (src, tgt, bounds, L, B)
+
+    def _build(self):
+        if self._args is not None:
+            src, tgt, bounds, L, B = self._args
+            self._args = None
+            st, tt = torch.from_numpy(src), torch.from_numpy(tgt)
+            super().extend([[(st[lvl, bounds[b]:bounds[b + 1]], tt[lvl, bounds[b]:bounds[b + 1]]) for b in range(B)]
+                            for lvl in range(L)])
+
+    def __getitem__(self, i):
+        self._build()
+        return super().__getitem__(i)
+
+    def __iter__(self):
+        self._build()
+        return super().__iter__()
+
+    def __len__(self):
+        self._build()
+        return super().__len__()
 
 
 def build_matcher(args):

@@ -7,6 +7,8 @@ Semantics follow the reference's live core ``ms_deform_attn_core_pytorch``
 path: a non-ROCm tensor raises, like the reference extension's CPU stub
 (models/ops/src/cpu/ms_deform_attn_cpu.cpp:17-41).
 """
+import functools
+
 import torch
 from torch.autograd import Function
 from torch.autograd.function import once_differentiable
@@ -48,6 +50,7 @@ class KernelTimer:
 
     def __init__(self):
         self.records = []
+        self.calls = {}
 
     def __enter__(self):
         global _timer
@@ -74,10 +77,32 @@ class KernelTimer:
         ev.record()
         return ev
 
-    def _end(self, kind, key, nbytes, ev0, gathered=0):
+    def _end(self, kind, key, nbytes, ev0, gathered=0, call=None, keep=()):
         ev1 = torch.cuda.Event(enable_timing=True)
         ev1.record()
         self.records.append((kind, key, nbytes, gathered, ev0, ev1))
+        if call is not None:
+            self.calls[(kind, key)] = (call, keep)  # the last call of each shape, for burst()
+
+    BURST = 20
+
+    def burst(self, n=BURST):
+        """Re-issue the last recorded C-ABI call of every (kind, shape) n times back to back between
+        two events on the same stream: {(kind, key): average ms a launch}.  One pair of events around a
+        single launch also holds the ~6 us between the start event and the kernel's dispatch (rocprof
+        shows the gap); n launches in a row amortise it, so this average is the kernel's own duration
+        (the outputs are rewritten with the same values)."""
+        out = {}
+        for k, (call, _keep) in self.calls.items():
+            call()  # (warm)
+            ev0 = self._begin()
+            for _ in range(n):
+                call()
+            ev1 = torch.cuda.Event(enable_timing=True)
+            ev1.record()
+            out[k] = (ev0, ev1, n)
+        torch.cuda.synchronize()
+        return {k: ev0.elapsed_time(ev1) / n for k, (ev0, ev1, n) in out.items()}
 
     def summary(self):
         """{(kind, key): {"launches", "total_ms", "avg_ms", "bytes_per_launch", "gather_bytes_per_launch"}}"""
@@ -226,15 +251,17 @@ def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_til
     if layout == LEVEL_MAJOR:
         if tiles is None:
             raise RuntimeError("MSDA: the level-major coordinate layout needs a row-block call (level_major_ok)")
-        rc = lib.msda_hip_forward_tiles_layout(*args, tiles.data_ptr(), *tail[:-1], layout, tail[-1])
+        call = functools.partial(lib.msda_hip_forward_tiles_layout, *args, tiles.data_ptr(), *tail[:-1], layout,
+                                 tail[-1])
     elif tiles is None:
-        rc = lib.msda_hip_forward(*args, *tail)
+        call = functools.partial(lib.msda_hip_forward, *args, *tail)
     else:
-        rc = lib.msda_hip_forward_tiles(*args, tiles.data_ptr(), *tail)
+        call = functools.partial(lib.msda_hip_forward_tiles, *args, tiles.data_ptr(), *tail)
+    rc = call()
     _native.check(rc, "msda_hip_forward")
     if timer is not None:
         timer._end("fwd", (S, Lq), algorithmic_bytes("fwd", B, S, M, D, Lq, L, P, value.element_size()), ev0,
-                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()))
+                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()), call, (value, loc, aw, out, tiles))
     return (out, tiles) if want_tiles else out
 
 
@@ -288,16 +315,18 @@ def _backward_ex(value, shapes, starts, loc, aw, grad_output, padding_mode, need
     timer = _timer
     if timer is not None:
         ev0 = timer._begin()
-    rc = lib.msda_hip_backward_ex(value.data_ptr(), _native.DTYPE_TAGS[value.dtype], _native.host_i64_array(shapes),
-                                  _native.host_i64_array(starts), L, loc.data_ptr(), aw.data_ptr(),
-                                  grad_output.data_ptr(), gv.data_ptr(), ptr(gl), ptr(ga), ptr(ws), B, S, M, D, Lq, P,
-                                  _native.PAD_TAGS[padding_mode], rs, _native.stream_handle(value.device))
+    call = functools.partial(lib.msda_hip_backward_ex, value.data_ptr(), _native.DTYPE_TAGS[value.dtype],
+                             _native.host_i64_array(shapes), _native.host_i64_array(starts), L, loc.data_ptr(),
+                             aw.data_ptr(), grad_output.data_ptr(), gv.data_ptr(), ptr(gl), ptr(ga), ptr(ws), B, S, M,
+                             D, Lq, P, _native.PAD_TAGS[padding_mode], rs, _native.stream_handle(value.device))
+    rc = call()
     if rc == _native.MSDA_ERR_UNSUPPORTED:
         return None
     _native.check(rc, "msda_hip_backward_ex")
     if timer is not None:
         timer._end("bwd", (S, Lq), algorithmic_bytes("bwd", B, S, M, D, Lq, L, P, value.element_size()), ev0,
-                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()))
+                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()), call,
+                   (value, loc, aw, grad_output, gv, gl, ga, ws))
     from . import _trace
     _trace.hit("msda_grad_value_slot")
     return gv, gl, ga
@@ -333,15 +362,18 @@ def _backward(value, shapes, starts, loc, aw, grad_output, padding_mode, need_va
     if layout == LEVEL_MAJOR:
         if tiles is None:
             raise RuntimeError("MSDA: a level-major backward needs the forward's tile intervals")
-        rc = lib.msda_hip_backward_tiles_layout(*args, tiles.data_ptr(), *tail[:-1], layout, tail[-1])
+        call = functools.partial(lib.msda_hip_backward_tiles_layout, *args, tiles.data_ptr(), *tail[:-1], layout,
+                                 tail[-1])
     elif tiles is None:
-        rc = lib.msda_hip_backward(*args, *tail)
+        call = functools.partial(lib.msda_hip_backward, *args, *tail)
     else:
-        rc = lib.msda_hip_backward_tiles(*args, tiles.data_ptr(), *tail)
+        call = functools.partial(lib.msda_hip_backward_tiles, *args, tiles.data_ptr(), *tail)
+    rc = call()
     _native.check(rc, "msda_hip_backward")
     if timer is not None:
         timer._end("bwd", (S, Lq), algorithmic_bytes("bwd", B, S, M, D, Lq, L, P, value.element_size()), ev0,
-                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()))
+                   gathered_bytes(B, M, D, Lq, L, P, value.element_size()), call,
+                   (value, loc, aw, grad_output, gv, gl, ga, ws, tiles))
     return gv, gl, ga
 
 

@@ -559,6 +559,13 @@ class FlatGradTrainer:
                 self.eager_step(batch)
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
+        if self.world > 1 or (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"):
+            # let the RCCL watchdog retire the warm-up collectives (it polls their events every
+            # ~100 ms): a poll of one of them while this thread's stream captures failed the
+            # process group once in the one-rank smoke ("operation not permitted on an event last
+            # recorded in a capturing stream")
+            import time
+            time.sleep(0.5)
         # capture_error_mode "thread_local": the RCCL process group's watchdog thread polls the
         # events of the warm-up collectives (hipEventQuery) while this thread captures; under the
         # default global mode that poll is refused and the watchdog aborts the process

@@ -1,5 +1,6 @@
 """The C-ABI library: loads without a GPU, exports every symbol include/msda_hip.h,
-include/flat_adamw.h, include/add_layernorm.h, include/ffn_glue.h and include/gemm_small.h declare, and rejects bad arguments with a status + message before
+include/flat_adamw.h, include/add_layernorm.h, include/ffn_glue.h, include/gemm_small.h,
+include/seg_attention.h and include/host_lsa.h declare, and rejects bad arguments with a status + message before
 touching a device."""
 import ctypes
 import os
@@ -10,7 +11,8 @@ import pytest
 from conftest import PKG, ROOT
 
 HEADERS = [os.path.join(ROOT, "include", h)
-           for h in ("msda_hip.h", "flat_adamw.h", "add_layernorm.h", "ffn_glue.h", "gemm_small.h", "seg_attention.h")]
+           for h in ("msda_hip.h", "flat_adamw.h", "add_layernorm.h", "ffn_glue.h", "gemm_small.h", "seg_attention.h",
+                     "host_lsa.h")]
 
 
 def declared_symbols():

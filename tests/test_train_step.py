@@ -500,8 +500,10 @@ def test_shared_layer_gradients_accumulate_into_flat_views(dev, monkeypatch):
     # atomics placed the taps, which varies run to run, and bf16 GEMMs carry that upstream (a
     # gradient cast to bf16 may round either way: the duration embedding's, a sum over every token).
     # So the in-place run must be as close to autograd's as two autograd runs are to each other, up
-    # to 1e-3 of the gradient's norm — far below a missing or doubled contribution of a shared call.
+    # to 5e-3 of the gradient's norm (such flips reach the BaseEncoder's first convolution at ~1e-3
+    # even when two runs happen to agree there) — far below a missing or doubled contribution of a
+    # shared call (the audio stream's share of a shared weight's gradient is several percent).
     for i, (n, off) in enumerate(zip(sizes, offs)):
         a, b, c = got[off:off + n].double(), ref[off:off + n].double(), ref2[off:off + n].double()
         spread = (b - c).norm().item()
-        assert (a - b).norm().item() <= 4 * spread + 1e-3 * b.norm().item() + 1e-9, i
+        assert (a - b).norm().item() <= 4 * spread + 5e-3 * b.norm().item() + 1e-9, i
