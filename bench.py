@@ -434,7 +434,8 @@ def main():
     if trainer.phase_events:
         graph_phases = {}
         for name, e0, e1 in trainer.phase_events:
-            graph_phases[name] = graph_phases.get(name, 0.0) + e0.elapsed_time(e1) / args.steps
+            dt = 1e3 * (e1 - e0) if isinstance(e0, float) else e0.elapsed_time(e1)  # (host-clock entries)
+            graph_phases[name] = graph_phases.get(name, 0.0) + dt / args.steps
         graph_phases = {k: round(v, 3) for k, v in graph_phases.items()}
         trainer.phase_events = None
     if world > 1:

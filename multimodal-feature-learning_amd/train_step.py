@@ -31,6 +31,8 @@ the MI355X the way the hardware wants it:
 
 ``graph=False`` runs the same three phases eagerly (CPU tests, world_size-2 gloo).
 """
+import time
+
 import torch
 import torch.distributed as dist
 
@@ -615,13 +617,20 @@ class FlatGradTrainer:
         if self.staged:
             self._g_a.replay()
             t1 = mark()
+            c0 = time.perf_counter()
             torch.cuda.current_stream(self.device).synchronize()  # the request is in pinned memory
+            c1 = time.perf_counter()
             self.loss_fn.host(self._stage_state, self._request_host)
+            c2 = time.perf_counter()
             self.loss_fn.upload()
             t2 = mark()
             if ev is not None:
                 ev.append(("graph A: forward to the host step", t0, t1))
                 ev.append(("host step (device->host wait, host work, upload)", t1, t2))
+                # host clock: the wait for graph A (its launch returns before the GPU finishes it) and
+                # the host work alone
+                ev.append(("host: synchronize (ms, host clock)", c0, c1))
+                ev.append(("host: matching + index lists (ms, host clock)", c1, c2))
             t0 = t2
         self._g_fb.replay()
         t1 = mark()
