@@ -27,6 +27,15 @@ int mfl_relu_dropout_forward(const void* x, int64_t n, float p_drop, const int64
 int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float p_drop, int dropped, void* dx,
                               void* stream);
 
+/* dropout(gelu(x)) (exact erf GELU, reference layers.py:827-869 MLP: nn.GELU() then nn.Dropout) on n bf16
+ * elements (n % 8 == 0, 16-byte aligned), rounded as ATen rounds it under bf16 autocast (gelu to bf16,
+ * then the dropout scale); keep bits from `seed` as mfl_relu_dropout_forward (NULL: no dropout).
+ * Backward from x and the same seed: dx = bf16(bf16(dy keep / (1 - p)) gelu'(x)).
+ * (reference: the caption decoder MLP, models/modules/layers.py:827-869) */
+int mfl_gelu_dropout_forward(const void* x, int64_t n, float p_drop, const int64_t* seed, void* out, void* stream);
+int mfl_gelu_dropout_backward(const void* dy, const void* x, int64_t n, float p_drop, const int64_t* seed, void* dx,
+                              void* stream);
+
 /* mfl_relu_dropout_backward on a (rows x cols) row-major matrix (cols % 8 == 0) that also writes
  * colsum[j] = sum over rows of dx[:, j] as stored (bf16, summed in fp32, fixed order): the bias
  * gradient of the Linear layer whose output the activation read (reference linear1.bias.grad).

@@ -67,6 +67,8 @@ EXPORTED_SYMBOLS = (
     # include/ffn_glue.h
     "mfl_relu_dropout_forward",
     "mfl_relu_dropout_backward",
+    "mfl_gelu_dropout_forward",
+    "mfl_gelu_dropout_backward",
     "mfl_relu_dropout_colsum_workspace_bytes",
     "mfl_relu_dropout_backward_colsum",
     "mfl_level_pos_flatten",
@@ -225,6 +227,10 @@ def _declare(lib):
     lib.mfl_relu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]
     lib.mfl_relu_dropout_backward.restype = i32
     lib.mfl_relu_dropout_backward.argtypes = [vp, vp, i64, f32, i32, vp, vp]
+    lib.mfl_gelu_dropout_forward.restype = i32
+    lib.mfl_gelu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]
+    lib.mfl_gelu_dropout_backward.restype = i32
+    lib.mfl_gelu_dropout_backward.argtypes = [vp, vp, i64, f32, vp, vp, vp]
     lib.mfl_relu_dropout_colsum_workspace_bytes.restype = ctypes.c_size_t
     lib.mfl_relu_dropout_colsum_workspace_bytes.argtypes = [i64, i64]
     lib.mfl_relu_dropout_backward_colsum.restype = i32

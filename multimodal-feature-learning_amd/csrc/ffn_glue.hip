@@ -89,6 +89,74 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_bwd(const uint4* __rest
   }
 }
 
+// dropout(gelu(x)) of the caption decoder's MLP (reference layers.py:827-869: fc1 -> nn.GELU() ->
+// dropout), the exact erf form, as ATen computes it under bf16 autocast: gelu in fp32 rounded to bf16,
+// then (dropout) the bf16 value times keep / (1 - p) rounded again; the keep bits as relu_dropout's.
+// Backward from x and the seed: g = bf16(dy * keep / (1 - p)), dx = bf16(g * gelu'(x)) — ATen's
+// dropout backward then gelu_backward, each rounding to bf16.  One pass each way (ATen: gelu, a
+// dropout writing a byte mask, a masked scale and gelu_backward: four full passes and a mask).
+__device__ __forceinline__ float gelu_f(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad_f(float x) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = expf(-0.5f * x * x) * 0.39894228040143268f;
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float bfr(float f) { return __uint_as_float(rne(f) << 16); }
+
+__global__ __launch_bounds__(kThreads) void gelu_dropout_fwd(const uint4* __restrict__ x, long long nvec,
+                                                            const int64_t* __restrict__ seed_ptr, uint32_t thresh,
+                                                            float scale, uint4* __restrict__ out) {
+  const uint64_t seed = seed_ptr ? (uint64_t)seed_ptr[0] : 0;
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (long long)gridDim.x * kThreads) {
+    const uint4 v = x[i];
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+    uint64_t bits[2] = {0ull, 0ull};
+    if (seed_ptr) {
+      bits[0] = drop_bits4(seed, (uint64_t)i * 2);
+      bits[1] = drop_bits4(seed, (uint64_t)i * 2 + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float a = gelu_f(lo(w[j])), b = gelu_f(hi(w[j]));
+      if (seed_ptr) {
+        const uint64_t q = bits[j >> 1] >> (32 * (j & 1));
+        a = bfr(a) * ((uint32_t)(q & 0xffffu) >= thresh ? scale : 0.f);
+        b = bfr(b) * ((uint32_t)((q >> 16) & 0xffffu) >= thresh ? scale : 0.f);
+      }
+      o[j] = rne(a) | (rne(b) << 16);
+    }
+    out[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void gelu_dropout_bwd(const uint4* __restrict__ dy, const uint4* __restrict__ x,
+                                                            long long nvec, const int64_t* __restrict__ seed_ptr,
+                                                            uint32_t thresh, float scale, uint4* __restrict__ dx) {
+  const uint64_t seed = seed_ptr ? (uint64_t)seed_ptr[0] : 0;
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < nvec; i += (long long)gridDim.x * kThreads) {
+    const uint4 g = dy[i], v = x[i];
+    const uint32_t gw[4] = {g.x, g.y, g.z, g.w}, xw[4] = {v.x, v.y, v.z, v.w};
+    uint32_t o[4];
+    uint64_t bits[2] = {0ull, 0ull};
+    if (seed_ptr) {
+      bits[0] = drop_bits4(seed, (uint64_t)i * 2);
+      bits[1] = drop_bits4(seed, (uint64_t)i * 2 + 1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      float ga = lo(gw[j]), gb = hi(gw[j]);
+      if (seed_ptr) {
+        const uint64_t q = bits[j >> 1] >> (32 * (j & 1));
+        ga = bfr(ga * ((uint32_t)(q & 0xffffu) >= thresh ? scale : 0.f));
+        gb = bfr(gb * ((uint32_t)((q >> 16) & 0xffffu) >= thresh ? scale : 0.f));
+      }
+      o[j] = rne(ga * gelu_grad_f(lo(xw[j]))) | (rne(gb * gelu_grad_f(hi(xw[j]))) << 16);
+    }
+    dx[i] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 // relu_dropout_bwd on a (rows x cols) matrix that also sums each column of dx as stored (bf16): the
 // bias gradient of the Linear layer that produced the hidden (linear1), which then needs no
 // column-sum pass over dx.  One block = kRdRows rows x 256 vectors of 8 columns; per-block column
@@ -511,6 +579,32 @@ int mfl_relu_dropout_backward(const void* dy, const void* out, int64_t n, float 
                      static_cast<const uint4*>(dy), static_cast<const uint4*>(out), nvec, scale,
                      static_cast<uint4*>(dx));
   return status("backward");
+}
+
+int mfl_gelu_dropout_forward(const void* x, int64_t n, float p_drop, const int64_t* seed, void* out, void* stream) {
+  g_err[0] = 0;
+  if (!args_ok("mfl_gelu_dropout_forward", n, x, out, out, p_drop)) return 1;
+  if (n == 0) return 0;
+  const long long nvec = n / 8;
+  const uint32_t thresh = (uint32_t)fminf(p_drop * 65536.f + 0.5f, 65536.f);
+  const float scale = seed ? 1.f / (1.f - p_drop) : 1.f;
+  hipLaunchKernelGGL(gelu_dropout_fwd, dim3(grid_for(nvec)), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint4*>(x), nvec, seed, thresh, scale, static_cast<uint4*>(out));
+  return status("gelu forward");
+}
+
+int mfl_gelu_dropout_backward(const void* dy, const void* x, int64_t n, float p_drop, const int64_t* seed, void* dx,
+                              void* stream) {
+  g_err[0] = 0;
+  if (!args_ok("mfl_gelu_dropout_backward", n, dy, x, dx, p_drop)) return 1;
+  if (n == 0) return 0;
+  const long long nvec = n / 8;
+  const uint32_t thresh = (uint32_t)fminf(p_drop * 65536.f + 0.5f, 65536.f);
+  const float scale = seed ? 1.f / (1.f - p_drop) : 1.f;
+  hipLaunchKernelGGL(gelu_dropout_bwd, dim3(grid_for(nvec)), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     static_cast<const uint4*>(dy), static_cast<const uint4*>(x), nvec, seed, thresh, scale,
+                     static_cast<uint4*>(dx));
+  return status("gelu backward");
 }
 
 size_t mfl_relu_dropout_colsum_workspace_bytes(int64_t rows, int64_t cols) {

@@ -17,7 +17,7 @@ from torch.autograd import Function
 
 from .add_norm import _attach_colsum, _drop_args, _ptr
 
-__all__ = ["relu_dropout"]
+__all__ = ["relu_dropout", "gelu_dropout"]
 
 
 class _ReluDropout(Function):
@@ -70,4 +70,48 @@ def relu_dropout(h, activation, dropout: nn.Dropout):
             and h.numel() % 8 == 0 and h.data_ptr() % 16 == 0 and isinstance(dropout, nn.Dropout)):
         p_drop, seed = _drop_args(dropout, h.device)
         return _ReluDropout.apply(h, p_drop, seed)
+    return dropout(activation(h))
+
+
+class _GeluDropout(Function):
+    """dropout(gelu(h)) of the caption decoder's MLP (include/ffn_glue.h mfl_gelu_dropout_*): saves h
+    and the dropout seed; the backward regenerates the keep bits."""
+
+    @staticmethod
+    def forward(ctx, h, p_drop, seed):
+        from ... import _native, _trace
+        _trace.hit("gelu_dropout")
+        lib = _native.load_library()
+        out = torch.empty_like(h)
+        rc = lib.mfl_gelu_dropout_forward(h.data_ptr(), h.numel(), p_drop, _ptr(seed), out.data_ptr(),
+                                          _native.stream_handle(h.device))
+        if rc != 0:
+            raise RuntimeError(lib.mfl_relu_dropout_last_error().decode())
+        ctx.p_drop = p_drop
+        ctx.save_for_backward(h, seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        from ... import _native
+        lib = _native.load_library()
+        h, seed = ctx.saved_tensors
+        dy = dy.to(h.dtype).contiguous()
+        dx = torch.empty_like(h)
+        rc = lib.mfl_gelu_dropout_backward(dy.data_ptr(), h.data_ptr(), h.numel(), ctx.p_drop, _ptr(seed),
+                                           dx.data_ptr(), _native.stream_handle(h.device))
+        if rc != 0:
+            raise RuntimeError(lib.mfl_relu_dropout_last_error().decode())
+        return dx, None, None
+
+
+def gelu_dropout(h, activation, dropout: nn.Dropout):
+    """``dropout(activation(h))`` for ``activation`` an exact-erf ``nn.GELU``: one HIP kernel each way
+    for a bf16 ``h`` on the GPU (ATen's roundings, keep bits from a device seed); the modules as they
+    are elsewhere."""
+    if (isinstance(activation, nn.GELU) and activation.approximate == "none" and h.is_cuda
+            and h.dtype == torch.bfloat16 and h.is_contiguous() and h.numel() % 8 == 0 and h.data_ptr() % 16 == 0
+            and isinstance(dropout, nn.Dropout)):
+        p_drop, seed = _drop_args(dropout, h.device)
+        return _GeluDropout.apply(h, p_drop, seed)
     return dropout(activation(h))

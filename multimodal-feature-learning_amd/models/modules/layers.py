@@ -14,6 +14,7 @@ from torch import nn
 
 from .add_norm import add_layer_norm, add_layer_norm_carry, carry_supported
 from .attention import CrossAttention, masked_scores_softmax
+from .ffn import gelu_dropout
 from .linear import Linear
 
 __all__ = ["MLP", "FFN", "ContextMaskModel", "UnimodalCaptionDecoderLayer", "MultimodalCaptionDecoderLayer",
@@ -150,7 +151,7 @@ class UnimodalCaptionDecoderLayer(nn.Module):
             ca = self.cross_attention(x16, memory, memory, attn_mask=memory_mask,
                                       key_padding_mask=memory_padding_mask)[0]
             x, x16, _ = add_layer_norm_carry(x, ca, self.layer_norm_2, dropout=self.projection_dropout_2)
-            h = m.dropout_1(m.activation_layer(m.fully_connected_1(x16)))
+            h = gelu_dropout(m.fully_connected_1(x16), m.activation_layer, m.dropout_1)
             out, out16, _ = add_layer_norm_carry(x, m.fully_connected_2(h), self.layer_norm_3, dropout=m.dropout_2)
             out._mfl_bf16 = out16
             return out

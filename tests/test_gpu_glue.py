@@ -410,3 +410,45 @@ def test_base_encoder_channels_last_levels_match_reference_path(dev, monkeypatch
     for i, (a, b) in enumerate(zip(ga, gb)):
         err = ((a.double() - b.double()).norm() / b.double().norm().clamp_min(1e-30)).item()
         assert err < 2e-2, (i, err)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gelu_dropout_matches_aten(dev, p):
+    """ffn.gelu_dropout (mfl_gelu_dropout_*): dropout(gelu(h)) of the caption decoder's MLP (reference
+    layers.py:827-869, exact erf GELU) with ATen's bf16 roundings — without dropout equal to F.gelu's
+    forward and gelu_backward (to one bf16 ulp on a few elements: erf / exp of another math library
+    build); with dropout the kept elements are bf16(bf16(gelu) / (1 - p)), about p of them dropped, and
+    the backward passes the gradient exactly where the forward kept."""
+    ffn = PKG.models.modules.ffn
+    g = torch.Generator(device=dev).manual_seed(3)
+    h = (torch.randn(3192, 2048, device=dev, generator=g) * 2).bfloat16().requires_grad_(True)
+    dy = torch.randn(3192, 2048, device=dev, generator=g).bfloat16()
+    drop = torch.nn.Dropout(p).train()
+    PKG._trace.clear()
+    out = ffn.gelu_dropout(h, torch.nn.GELU(), drop)
+    assert PKG._trace.hits.get("gelu_dropout", 0) == 1
+    (dx,) = torch.autograd.grad(out, h, dy)
+    ref = torch.nn.functional.gelu(h.detach().float()).bfloat16()
+    rdx = torch.ops.aten.gelu_backward(dy, h.detach(), approximate="none")
+
+    def ulps(a, b):
+        ai = a.view(torch.int16).int()
+        bi = b.view(torch.int16).int()
+        return (ai - bi).abs()
+
+    if p == 0.0:
+        assert (ulps(out, ref) > 1).sum().item() == 0 and (ulps(out, ref) > 0).float().mean().item() < 1e-3
+        assert (ulps(dx, rdx) > 1).sum().item() == 0 and (ulps(dx, rdx) > 0).float().mean().item() < 1e-3
+    else:
+        kept = out != 0
+        frac = 1 - kept.float().mean().item()
+        assert abs(frac - p) < 0.01, frac
+        want = (ref.float() / (1 - p)).bfloat16()
+        nz = kept & (ref != 0)
+        assert (ulps(out[nz], want[nz]) > 1).sum().item() == 0
+        # the backward keeps exactly the forward's elements (where gelu(h) != 0)
+        dmask = (dy.float() / (1 - p)).bfloat16()
+        want_dx = torch.ops.aten.gelu_backward(dmask, h.detach(), approximate="none")
+        assert torch.equal(dx[~kept & (ref != 0)], torch.zeros_like(dx[~kept & (ref != 0)]))
+        assert (ulps(dx[nz], want_dx[nz]) > 1).sum().item() == 0
