@@ -27,14 +27,15 @@ extern "C" {
  * min(nr, nc) pairs: rows[k] ascending, cols[k] the matched column. */
 int mfl_lsa(const double* cost, int64_t nr, int64_t nc, int64_t* rows, int64_t* cols);
 
-/* Every level's matching of the staged DVC loss.  cost: L blocks of (B, Q, n_tgt) float32 (the
- * copied request); clip b's targets are columns [bounds[b], bounds[b+1]).  Per level and clip the
+/* Every level's matching of the staged DVC loss.  cost: L blocks of (B, Q, n_tgt) float64 (the
+ * copied request, as HungarianMatcher.level_costs concatenates it); clip b's targets are columns
+ * [bounds[b], bounds[b+1]).  Per level and clip the
  * assignment of cost[l, b, :, bounds[b]:bounds[b+1]] is written as
  *   src[l * n_tgt + bounds[b] + k], tgt[...]: prediction and target (rows ascending, scipy's order);
  *   idx[(l * 2 + 0) * n_tgt + o], idx[(l * 2 + 1) * n_tgt + o]: clip b and the prediction matched
  *   to the clip's targets in target order (get_src_permutation_idx), o = bounds[b] + t.
  * Requires Q >= the clip's target count (every target matched, as the DVC loss assumes). */
-int mfl_lsa_levels(const float* cost, int64_t L, int64_t B, int64_t Q, int64_t n_tgt, const int64_t* bounds,
+int mfl_lsa_levels(const double* cost, int64_t L, int64_t B, int64_t Q, int64_t n_tgt, const int64_t* bounds,
                    int64_t* src, int64_t* tgt, int64_t* idx);
 
 #ifdef __cplusplus

@@ -146,7 +146,7 @@ extern "C" int mfl_lsa(const double* cost, int64_t nr, int64_t nc, int64_t* rows
   return assign(s, buf, nr, nc, [&](int64_t i, int64_t j) { return cost[i * nc + j]; }, rows, cols);
 }
 
-extern "C" int mfl_lsa_levels(const float* cost, int64_t L, int64_t B, int64_t Q, int64_t n_tgt,
+extern "C" int mfl_lsa_levels(const double* cost, int64_t L, int64_t B, int64_t Q, int64_t n_tgt,
                               const int64_t* bounds, int64_t* src, int64_t* tgt, int64_t* idx) {
   if (L < 0 || B < 0 || Q <= 0 || n_tgt < 0 || cost == nullptr || bounds == nullptr || src == nullptr ||
       tgt == nullptr || idx == nullptr || bounds[0] != 0 || bounds[B] != n_tgt)
@@ -159,10 +159,10 @@ extern "C" int mfl_lsa_levels(const float* cost, int64_t L, int64_t B, int64_t Q
     for (int64_t b = 0; b < B; ++b) {
       const int64_t t0 = bounds[b], nt = bounds[b + 1] - t0;
       if (nt == 0) continue;
-      const float* blk = cost + ((l * B + b) * Q) * n_tgt + t0;  // (Q, nt) with row stride n_tgt
+      const double* blk = cost + ((l * B + b) * Q) * n_tgt + t0;  // (Q, nt) with row stride n_tgt
       int64_t* rs = src + l * n_tgt + t0;
       int64_t* cs = tgt + l * n_tgt + t0;
-      const int rc = assign(s, buf, Q, nt, [&](int64_t i, int64_t j) { return (double)blk[i * n_tgt + j]; }, rs, cs);
+      const int rc = assign(s, buf, Q, nt, [&](int64_t i, int64_t j) { return blk[i * n_tgt + j]; }, rs, cs);
       if (rc != MFL_LSA_OK) return rc;
       // get_src_permutation_idx: the clip's matched predictions in target order
       int64_t* ib = idx + (l * 2) * n_tgt + t0;

@@ -80,13 +80,14 @@ class HungarianMatcher(nn.Module):
         assert bool(ok[:-1].all()), "Segment start > Segment end (from output)"
         assert bool(ok[-1]), "Segment start > Segment end (from target)"
         bounds = np.cumsum([0] + list(sizes)).astype(np.int64)
-        if (os.environ.get("MFL_HOST_LSA", "1") != "0" and shapes and len(set(shapes)) == 1 and h.dtype == np.float32
-                and max(sizes, default=0) <= shapes[0][1] and n_tgt == int(bounds[-1])):
+        if (os.environ.get("MFL_HOST_LSA", "1") != "0" and shapes and len(set(shapes)) == 1
+                and h.dtype in (np.float32, np.float64) and max(sizes, default=0) <= shapes[0][1]
+                and n_tgt == int(bounds[-1])):
             from .. import _native
             lib = _native.load_library()
             L = len(shapes)
             B, Q = shapes[0]
-            cost = np.ascontiguousarray(h[:L * B * Q * n_tgt])
+            cost = np.ascontiguousarray(h[:L * B * Q * n_tgt], dtype=np.float64)  # (scipy solves in float64)
             src = np.empty((L, n_tgt), np.int64)
             tgt = np.empty((L, n_tgt), np.int64)
             idx = idx_out if idx_out is not None else np.empty((L, 2, n_tgt), np.int64)

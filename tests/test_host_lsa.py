@@ -51,13 +51,13 @@ def test_lsa_infeasible_and_invalid():
 def test_lsa_levels_matches_python_host_step():
     """mfl_lsa_levels on a request buffer of the staged DVC loss equals solve_levels' per-clip scipy
     calls and the Python index building of StagedDVCLoss.host (bench shape: 6 levels, 8 clips, 100
-    predictions, 1-7 targets a clip; float32 costs with ties)."""
+    predictions, 1-7 targets a clip; float64 costs with ties, as the request is)."""
     rng = np.random.default_rng(11)
     L, B, Q = 6, 8, 100
     counts = rng.integers(1, 8, B)
     bounds = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     n_tgt = int(bounds[-1])
-    cost = rng.standard_normal((L, B, Q, n_tgt)).astype(np.float32)
+    cost = rng.standard_normal((L, B, Q, n_tgt))
     cost[..., : n_tgt // 3] = np.round(cost[..., : n_tgt // 3])  # ties
     lib = PKG._native.load_library()
     src, tgt = np.zeros((L, n_tgt), np.int64), np.zeros((L, n_tgt), np.int64)
@@ -88,7 +88,7 @@ def test_solve_levels_native_matches_scipy_path(monkeypatch):
     sizes = [3, 1, 5, 2]
     n_tgt = sum(sizes)
     shapes = [(B, Q)] * 3
-    h = np.concatenate([rng.random(3 * B * Q * n_tgt).astype(np.float32), np.ones(2, np.float32)])
+    h = np.concatenate([rng.random(3 * B * Q * n_tgt), np.ones(2)])  # (float64, as level_costs' request)
     meta = (shapes, sizes, n_tgt, 2)
     monkeypatch.setenv("MFL_HOST_LSA", "0")
     want = HM.solve_levels(torch.from_numpy(h), meta)
