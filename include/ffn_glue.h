@@ -36,6 +36,13 @@ int mfl_gelu_dropout_forward(const void* x, int64_t n, float p_drop, const int64
 int mfl_gelu_dropout_backward(const void* dy, const void* x, int64_t n, float p_drop, const int64_t* seed, void* dx,
                               void* stream);
 
+/* The logits' gradient when a loss reads one word's probability a row, p_w = softmax(x)[row, words[row]]
+ * (the caption loss's gather of the decoder's probabilities, reference criterion over
+ * unimodal_caption_decoder.py's softmax): dx[row, j] = coef[row] (delta_{j, w} - probs[row, j]) as bf16,
+ * coef = dL/dp_w * p_w; probs (rows x vocab) fp32, vocab % 4 == 0, dx rows 8-byte aligned. */
+int mfl_word_prob_backward(const float* probs, const int64_t* words, const float* coef, int64_t rows, int64_t vocab,
+                           void* dx, void* stream);
+
 /* mfl_relu_dropout_backward on a (rows x cols) row-major matrix (cols % 8 == 0) that also writes
  * colsum[j] = sum over rows of dx[:, j] as stored (bf16, summed in fp32, fixed order): the bias
  * gradient of the Linear layer whose output the activation read (reference linear1.bias.grad).

@@ -69,6 +69,7 @@ EXPORTED_SYMBOLS = (
     "mfl_relu_dropout_backward",
     "mfl_gelu_dropout_forward",
     "mfl_gelu_dropout_backward",
+    "mfl_word_prob_backward",
     "mfl_relu_dropout_colsum_workspace_bytes",
     "mfl_relu_dropout_backward_colsum",
     "mfl_level_pos_flatten",
@@ -231,6 +232,8 @@ def _declare(lib):
     lib.mfl_gelu_dropout_forward.argtypes = [vp, i64, f32, vp, vp, vp]
     lib.mfl_gelu_dropout_backward.restype = i32
     lib.mfl_gelu_dropout_backward.argtypes = [vp, vp, i64, f32, vp, vp, vp]
+    lib.mfl_word_prob_backward.restype = i32
+    lib.mfl_word_prob_backward.argtypes = [vp, vp, vp, i64, i64, vp, vp]
     lib.mfl_relu_dropout_colsum_workspace_bytes.restype = ctypes.c_size_t
     lib.mfl_relu_dropout_colsum_workspace_bytes.argtypes = [i64, i64]
     lib.mfl_relu_dropout_backward_colsum.restype = i32

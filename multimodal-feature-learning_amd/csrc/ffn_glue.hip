@@ -157,6 +157,27 @@ __global__ __launch_bounds__(kThreads) void gelu_dropout_bwd(const uint4* __rest
   }
 }
 
+// Gradient of the caption logits when a loss reads one word's probability a row (p_w = softmax(x)_w,
+// the caption loss's gather): dx_j = c (delta_jw - p_j), c = dL/dp_w * p_w, from the stored fp32
+// probabilities; one workgroup a row, float4 reads, bf16 writes.  The dense path (the gather's
+// scatter_add into zeros, the level split's concatenation, softmax's backward, the bf16 cast) makes
+// ~8 passes over the (rows x vocabulary) tensor; this one reads it once.
+__global__ __launch_bounds__(kThreads) void word_prob_bwd(const float4* __restrict__ probs, const int64_t* __restrict__ words,
+                                                         const float* __restrict__ coef, int v4, uint2* __restrict__ dx) {
+  const long long r = blockIdx.x;
+  const float c = coef[r];
+  const long long w = words[r];
+  const float4* pr = probs + r * v4;
+  uint2* out = dx + r * v4;
+  for (int i = threadIdx.x; i < v4; i += kThreads) {
+    const float4 p = pr[i];
+    float o[4] = {-c * p.x, -c * p.y, -c * p.z, -c * p.w};
+    const long long j0 = 4ll * i;
+    if (w >= j0 && w < j0 + 4) o[w - j0] += c;  // c (1 - p_w) as c - c p_w
+    out[i] = make_uint2(rne(o[0]) | (rne(o[1]) << 16), rne(o[2]) | (rne(o[3]) << 16));
+  }
+}
+
 // relu_dropout_bwd on a (rows x cols) matrix that also sums each column of dx as stored (bf16): the
 // bias gradient of the Linear layer that produced the hidden (linear1), which then needs no
 // column-sum pass over dx.  One block = kRdRows rows x 256 vectors of 8 columns; per-block column
@@ -605,6 +626,19 @@ int mfl_gelu_dropout_backward(const void* dy, const void* x, int64_t n, float p_
                      static_cast<const uint4*>(dy), static_cast<const uint4*>(x), nvec, seed, thresh, scale,
                      static_cast<uint4*>(dx));
   return status("gelu backward");
+}
+
+int mfl_word_prob_backward(const float* probs, const int64_t* words, const float* coef, int64_t rows, int64_t vocab,
+                           void* dx, void* stream) {
+  g_err[0] = 0;
+  if (rows < 0 || vocab <= 0 || vocab % 4 != 0 || (rows > 0 && (!probs || !words || !coef || !dx))) {
+    snprintf(g_err, sizeof(g_err), "mfl_word_prob_backward: bad arguments (vocab %% 4 == 0, non-null buffers)");
+    return 1;
+  }
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(word_prob_bwd, dim3((unsigned)rows), dim3(kThreads), 0, static_cast<hipStream_t>(stream),
+                     reinterpret_cast<const float4*>(probs), words, coef, (int)(vocab / 4), static_cast<uint2*>(dx));
+  return status("word prob backward");
 }
 
 size_t mfl_relu_dropout_colsum_workspace_bytes(int64_t rows, int64_t cols) {

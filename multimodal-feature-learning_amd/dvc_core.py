@@ -20,6 +20,7 @@ from .models.deformable.unimodal_deformable_transformer import DeformableTransfo
 from .models.sparse.unimodal_sparse_deformable_transformer import SparseDeformableTransformer
 from .models.modules.embedding_layers import FFN, PositionEmbeddingVideoSine
 from .models.modules.misc_modules import inverse_sigmoid, level_heads, predict_event_num, predict_event_num_with_depth
+from .models.unimodal_caption_decoder import word_probs
 from .utils.dam import attn_map_to_flat_grid
 from .models.modules.linear import Linear
 
@@ -307,7 +308,7 @@ def dvc_workload_loss(result, obj):
         total = total - torch.log(o['pred_logits'][bidx, sidx, 0].float().clamp_min(1e-9)).mean()
         total = total + 2 * F.cross_entropy(o['pred_count'].float(), n_events.clamp_max(o['pred_count'].shape[-1] - 1))
         if o.get('pred_captions') is not None:
-            p = o['pred_captions'].float().gather(-1, words[..., None])[..., 0]
+            p = word_probs(o['pred_captions'], words)
             total = total - (torch.log(p.clamp_min(1e-9)) * live).sum() / live.sum()
     if 'pred_memory_mask' in out:
         # the crop's kept tokens as the context target (criterion.py loss_contexts)
@@ -401,7 +402,7 @@ class StagedDVCLoss:
             total = total + 2 * F.cross_entropy(o['pred_count'].float(),
                                                 self.n_events.clamp_max(o['pred_count'].shape[-1] - 1))
             if o.get('pred_captions') is not None:
-                p = o['pred_captions'].float().gather(-1, self.words[..., None])[..., 0]
+                p = word_probs(o['pred_captions'], self.words)
                 total = total - (torch.log(p.clamp_min(1e-9)) * self.live).sum() / self.live_sum
         if 'pred_memory_mask' in out:
             total = total + 3 * F.binary_cross_entropy_with_logits(out['pred_memory_mask'].float(),

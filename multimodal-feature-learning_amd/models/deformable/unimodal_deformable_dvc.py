@@ -172,6 +172,10 @@ class UnimodalDeformableDVC(nn.Module):
                 captions.repeat(reps, 1), stacked, tgt_mask=tgt_mask.repeat(reps, 1, 1, 1),
                 memory_mask=torch.cat(cross), tgt_padding_mask=padding_mask.repeat(reps, 1), last_only=True)
             outputs_captions = list(output_caption[-1].split(counts))
+            lg = getattr(output_caption, "_mfl_logits", None)
+            if lg is not None:  # (each level's logits, for a loss's fused word gather: word_probs)
+                for piece, lgp in zip(outputs_captions, lg[-1].split(counts)):
+                    piece._mfl_logits = lgp
 
         mask_out = memory_mask_list[-1].squeeze().float() if self.use_differentiable_mask else None
         if is_training:

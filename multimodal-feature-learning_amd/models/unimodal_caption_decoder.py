@@ -26,8 +26,49 @@ def _probs(logits):
     pass either way (vocab 10,000: 128 MB a pass at the DVC bench shape)."""
     if logits.is_cuda and logits.dtype in (torch.bfloat16, torch.float16) and torch.is_autocast_enabled("cuda"):
         with torch.autocast("cuda", enabled=False):
-            return torch.softmax(logits, dim=-1, dtype=torch.float32)
+            probs = torch.softmax(logits, dim=-1, dtype=torch.float32)
+        probs._mfl_logits = logits  # (word_probs: a loss's gather of one word a row, fused backward)
+        return probs
     return logits.softmax(dim=-1)
+
+
+class _WordProbs(torch.autograd.Function):
+    """probs[..., words] of softmax probabilities computed from ``logits``, the gradient going to the
+    logits directly (include/ffn_glue.h mfl_word_prob_backward) instead of through a dense
+    (rows x vocabulary) gradient of the probabilities and softmax's backward."""
+
+    @staticmethod
+    def forward(ctx, logits, probs, words):
+        p = probs.gather(-1, words[..., None])[..., 0]
+        ctx.save_for_backward(probs, words, p)
+        ctx.logits_shape, ctx.logits_dtype = logits.shape, logits.dtype
+        return p
+
+    @staticmethod
+    def backward(ctx, g):
+        from .. import _native
+        probs, words, p = ctx.saved_tensors
+        lib = _native.load_library()
+        V = probs.shape[-1]
+        coef = (g.float() * p).contiguous()
+        dx = torch.empty(ctx.logits_shape, dtype=ctx.logits_dtype, device=probs.device)
+        rc = lib.mfl_word_prob_backward(probs.data_ptr(), words.data_ptr(), coef.data_ptr(), probs.numel() // V, V,
+                                        dx.data_ptr(), _native.stream_handle(probs.device))
+        if rc != 0:
+            raise RuntimeError(lib.mfl_relu_dropout_last_error().decode())
+        return dx, None, None
+
+
+def word_probs(probs, words):
+    """``probs.float().gather(-1, words[..., None])[..., 0]`` — one word's probability a row, the caption
+    loss's read of the decoder's output.  When ``probs`` came from ``_probs`` on the GPU (it carries
+    its logits), the gradient is written to the logits in one pass (``_WordProbs``); the value is the
+    same."""
+    lg = getattr(probs, "_mfl_logits", None)
+    if (lg is None or not probs.is_cuda or probs.dtype != torch.float32 or not probs.is_contiguous()
+            or lg.shape != probs.shape or probs.shape[-1] % 4 or words.shape != probs.shape[:-1]):
+        return probs.float().gather(-1, words[..., None])[..., 0]
+    return _WordProbs.apply(lg, probs.detach(), words.contiguous().to(torch.int64))
 
 
 @torch.no_grad()

@@ -452,3 +452,31 @@ def test_gelu_dropout_matches_aten(dev, p):
         want_dx = torch.ops.aten.gelu_backward(dmask, h.detach(), approximate="none")
         assert torch.equal(dx[~kept & (ref != 0)], torch.zeros_like(dx[~kept & (ref != 0)]))
         assert (ulps(dx[nz], want_dx[nz]) > 1).sum().item() == 0
+
+
+@pytest.mark.gpu
+def test_word_probs_fused_backward_matches_dense(dev):
+    """unimodal_caption_decoder.word_probs (mfl_word_prob_backward): the caption loss's gather of one
+    word's probability a row from the bf16-logit softmax, its gradient written to the logits in one
+    pass, equals the dense path's (the gather's scatter into zeros, softmax's backward, the bf16 cast) —
+    the same formula c (delta - p) in fp32, one bf16 rounding."""
+    ucd = PKG.models.unimodal_caption_decoder
+    g = torch.Generator(device=dev).manual_seed(4)
+    rows, V = (6, 28, 19), 10000
+    x = (torch.randn(*rows, V, device=dev, generator=g) * 3).bfloat16()
+    words = torch.randint(0, V, rows, device=dev, generator=g)
+    live = (torch.rand(rows, device=dev, generator=g) > 0.2).float()
+    res = []
+    for fused in (True, False):
+        lg = x.clone().requires_grad_(True)
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            probs = ucd._probs(lg)
+        assert hasattr(probs, "_mfl_logits")
+        p = ucd.word_probs(probs, words) if fused else probs.float().gather(-1, words[..., None])[..., 0]
+        loss = -(torch.log(p.clamp_min(1e-9)) * live).sum() / live.sum()
+        loss.backward()
+        res.append((p.detach(), lg.grad.float()))
+    (pa, ga), (pb, gb) = res
+    assert torch.equal(pa, pb)
+    torch.testing.assert_close(ga, gb, rtol=1e-2, atol=1e-2 * gb.abs().max().item())
+    assert ((ga - gb).norm() / gb.norm()).item() < 1e-3
