@@ -71,6 +71,7 @@ def main():
                                                        "selects; not the GPU fast paths)")
     ap.add_argument("--extra", default="", help="more bench.py arguments, e.g. '--batch 1 --T 256'")
     ap.add_argument("--ops", default="", help="comma list: only these aten ops (e.g. sum,mean,norm)")
+    ap.add_argument("--by", default="bytes", choices=["bytes", "count"], help="order of the listing")
     a = ap.parse_args()
     sys.argv = [sys.argv[0], "--config", a.config, "--graph", "0", "--cpu-baseline", "0"] + a.extra.split()
     import bench
@@ -100,7 +101,8 @@ def main():
     print(f"{a.config}: {tot_n} glue ops in one step, {sum(v[1] for v in c.rows.values()) / 1e6:.1f} MB written")
     keep = set(a.ops.split(",")) if a.ops else None
     items = [kv for kv in c.rows.items() if keep is None or kv[0][0] in keep]
-    for (name, s, where), (n, b) in sorted(items, key=lambda kv: -kv[1][1])[:a.top]:
+    order = (lambda kv: -kv[1][1]) if a.by == "bytes" else (lambda kv: (-kv[1][0], -kv[1][1]))
+    for (name, s, where), (n, b) in sorted(items, key=order)[:a.top]:
         print(f"{b / 1e6:8.2f} MB {n:4d}x  {name} {s[:110]}\n              {where}")
 
 
