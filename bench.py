@@ -292,7 +292,7 @@ def msda_source_sha16():
     return h.hexdigest()[:16]
 
 
-def roofline(summary, traffic, bursts=None):
+def roofline(summary, traffic, bursts=None, bf16=True):
     """Dominant MSDA launch kind (largest total time) -> achieved algorithmic GB/s vs HBM peak.  The
     launch duration is the burst average (KernelTimer.burst: the call re-issued back to back between
     two events) where there is one, else the single-launch event average."""
@@ -305,7 +305,8 @@ def roofline(summary, traffic, bursts=None):
         d["avg_ms"] = bursts[(kind, key)]
     achieved = d["bytes_per_launch"] / (d["avg_ms"] * 1e-3) / 1e9
     name = f"msda_{kind}_S{key[0]}_Lq{key[1]}"
-    tr = traffic.get(name) if traffic else None
+    # (the PMC passes run the bf16 kernels: no HBM figure for an fp32 run's launch of the same shape)
+    tr = traffic.get(name) if traffic and bf16 else None
     gathered = d["gather_bytes_per_launch"]
     return {"bound": "hbm", "kernel": name,
             "timing": "HIP events on the launch stream, eager steps after the timed region: around every MSDA "
@@ -475,7 +476,7 @@ def main():
                        "d_model": 512, "levels": 4, "queries": args.queries, "parallelism": f"dp{world}",
                        "execution": "hip_graph" if graph else "eager", "gemm_solutions": gemm_sel,
                        "conv_solver": "MIOpen find (cudnn.benchmark)" if args.conv_find else "MIOpen immediate"},
-            "roofline": roofline(summary, traffic, bursts),
+            "roofline": roofline(summary, traffic, bursts, bf16=use_bf16),
             "cpu_baseline": None,
         }
         if phases is not None:

@@ -55,6 +55,25 @@ def level_token_ranges(num_feature_levels, video_rescale_len):
     return out
 
 
+_RANGES = {}
+
+
+def _range_tensors(num_feature_levels, video_rescale_len, dev):
+    """level_token_ranges as device tensors (lower, upper - lower as float32; lower, upper - 1 as int64),
+    made once per device (the first, eager step: nothing is copied from the host inside a captured
+    graph)."""
+    key = (num_feature_levels, video_rescale_len, str(dev))
+    t = _RANGES.get(key)
+    if t is None:
+        rng = level_token_ranges(num_feature_levels, video_rescale_len)
+        t = (torch.tensor([lo for lo, _ in rng], dtype=torch.float32, device=dev),
+             torch.tensor([up - lo for lo, up in rng], dtype=torch.float32, device=dev),
+             torch.tensor([lo for lo, _ in rng], dtype=torch.int64, device=dev),
+             torch.tensor([up - 1 for _, up in rng], dtype=torch.int64, device=dev))
+        _RANGES[key] = t
+    return t
+
+
 def crop_segments(features, denormalized_segments, segment_batch_id, video_durations, num_feature_levels,
                   video_rescale_len):
     """Memory rows of each matched segment: per level, tokens [start, end) with
@@ -67,12 +86,14 @@ def crop_segments(features, denormalized_segments, segment_batch_id, video_durat
     bid = segment_batch_id.to(dev)
     dur = _durations(video_durations, dev)[bid]  # its own dtype: the reference promotes seg / dur the same way
     tok = torch.arange(K, device=dev)
-    keep = torch.zeros(n, K, dtype=torch.bool, device=dev)
-    for lower, upper in level_token_ranges(num_feature_levels, video_rescale_len):
-        diff = upper - lower
-        s = torch.clamp((lower + (diff * seg[:, 0] / dur)).round().long(), min=lower, max=upper - 1)
-        e = torch.clamp((lower + (diff * seg[:, 1] / dur)).round().long(), min=lower, max=upper - 1)
-        keep |= (tok[None, :] >= s[:, None]) & (tok[None, :] < e[:, None])
+    # every level's token range at once, (n, levels) bounds (the reference loops over the levels,
+    # :481-490; ~12 small kernels a level and decoder level in a step): the same float32 / float64
+    # arithmetic per element, the same rounding and clamps, the union of the ranges
+    lower, diff, lo_i, hi_i = _range_tensors(num_feature_levels, video_rescale_len, dev)
+    dcol = dur[:, None] if dur.dim() == 1 else dur
+    s = torch.clamp((lower + (diff * seg[:, 0:1] / dcol)).round().long(), min=lo_i, max=hi_i)
+    e = torch.clamp((lower + (diff * seg[:, 1:2] / dcol)).round().long(), min=lo_i, max=hi_i)
+    keep = ((tok[None, None, :] >= s[:, :, None]) & (tok[None, None, :] < e[:, :, None])).any(1)
     if isinstance(features, SegmentMemory):
         return features.select(bid, keep), ~keep
     cropped = torch.where(keep[..., None], features[bid], features.new_zeros(()))
