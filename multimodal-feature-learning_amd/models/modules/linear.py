@@ -352,6 +352,12 @@ def _addmm(bias, x2, w):
     return torch.mm(x2, w.t()) if bias is None else torch.addmm(bias, x2, w.t())
 
 
+# (min_chunk, max_split) for weight gradients of at most _SPLITK_SMALL elements (e.g. 512 x 512: 8
+# chunks of a 15,360-token K give only 8 x 32 output tiles); MFL_SPLITK_SMALL="min,max" for A/B runs
+_SPLITK = tuple(int(v) for v in os.environ.get("MFL_SPLITK_SMALL", "1024,8").split(","))
+_SPLITK_SMALL = 512 * 512
+
+
 def split_k_chunks(k, min_chunk=1024, max_split=8):
     """Number of K chunks for the weight-gradient GEMM: the largest s <= max_split dividing K
     with K / s >= min_chunk (1 = no split)."""
@@ -612,7 +618,7 @@ def _weight_grad(g2, x2, out=None, accumulate=False):
     GEMM with fp32 partial outputs, then their sum (into ``out`` if given; added into it with
     ``accumulate``)."""
     k, n_out, n_in = x2.shape[0], g2.shape[1], x2.shape[1]
-    s = split_k_chunks(k)
+    s = split_k_chunks(k, *_SPLITK) if n_out * n_in <= _SPLITK_SMALL else split_k_chunks(k)
     if s > 1:
         # (bmm, not baddbmm(out=part, beta=0): that form first copies `part` into the output — an
         # extra 8-32 MB pass per call, ~0.3 ms per step, tools/op_census.py)
