@@ -238,3 +238,28 @@ def test_conv1d_as_gemm_equals_conv1d(k, T):
     want = (y2,) + torch.autograd.grad(y2, (x2, conv.weight, conv.bias), g)
     for a, b in zip(got, want):
         torch.testing.assert_close(a, b, rtol=1e-13, atol=1e-13)
+
+
+@pytest.mark.parametrize("dur_dtype", [torch.float32, torch.float64])
+def test_crop_masks_of_all_levels_equal_the_level_loop(dur_dtype):
+    """preds_postprocess.crop_segments builds every pyramid level's token range at once; it equals the
+    reference's loop over the levels (crop_segments :481-490: per level, start / end =
+    clamp(round(lower + diff * t / duration)), the union of the ranges) element for element, with
+    float32 and float64 durations (the arithmetic promotes the same way)."""
+    pp = PKG.utils.preds_postprocess
+    g = torch.Generator().manual_seed(2)
+    B, n, K, L, R = 8, 60, 1920, 4, 1024
+    durs = torch.rand(B, generator=g, dtype=dur_dtype) * 230 + 10
+    bid = torch.randint(0, B, (n,), generator=g)
+    seg = torch.sort(torch.rand(n, 2, generator=g) * durs[bid][:, None].float() * 1.1, 1)[0]
+    seg[:3] = torch.tensor([[0.0, 0.0], [5.0, 5.0], [0.0, 1e4]])  # empty, point, past the end
+    dur = pp._durations(durs, seg.device)[bid]
+    tok = torch.arange(K)
+    want = torch.zeros(n, K, dtype=torch.bool)
+    for lower, upper in pp.level_token_ranges(L, R):
+        diff = upper - lower
+        s = torch.clamp((lower + (diff * seg[:, 0] / dur)).round().long(), min=lower, max=upper - 1)
+        e = torch.clamp((lower + (diff * seg[:, 1] / dur)).round().long(), min=lower, max=upper - 1)
+        want |= (tok[None, :] >= s[:, None]) & (tok[None, :] < e[:, None])
+    _, key_mask = pp.crop_segments(torch.zeros(B, K, 4), seg, bid, durs, L, R)
+    assert torch.equal(~key_mask, want)
