@@ -368,7 +368,7 @@ def mha_self_attention(mha, tgt, query_pos, query_mask, carried=None):
     H = mha.num_heads
     hd = E // H
     w, b = mha.in_proj_weight, mha.in_proj_bias
-    x_qk = tgt if query_pos is None else tgt + query_pos
+    with_pos = (lambda: tgt if query_pos is None else tgt + query_pos)  # noqa: E731 (not built when carried)
     if (tgt.is_cuda and torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
             and w.dtype == torch.float32 and mha.out_proj.bias is not None and w.device == tgt.device):
         # the projections as the autocast Linear's: bf16 weights from the trainer's shadow, fp32
@@ -379,7 +379,7 @@ def mha_self_attention(mha, tgt, query_pos, query_mask, carried=None):
                 and carried[0].dtype == carried[1].dtype == torch.bfloat16):
             v16, qk16 = carried
         else:
-            qk16, v16 = x_qk.to(torch.bfloat16), tgt.to(torch.bfloat16)
+            qk16, v16 = with_pos().to(torch.bfloat16), tgt.to(torch.bfloat16)
         with torch.autocast("cuda", enabled=False):
             qk, v = _InProjection.apply(qk16, v16, w, b, sh[0] if ok else None, sh[1] if ok else None)
             q, k = qk.view(B, L, 2, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
@@ -388,7 +388,7 @@ def mha_self_attention(mha, tgt, query_pos, query_mask, carried=None):
                                                  dropout_p=mha.dropout if mha.training else 0.0)
             return _AutocastLinear.apply(out.transpose(1, 2).reshape(B, L, E), mha.out_proj.weight,
                                          mha.out_proj.bias, sh[2] if ok else None, sh[3] if ok else None)
-    qk = F.linear(x_qk, w[:2 * E], b[:2 * E])
+    qk = F.linear(with_pos(), w[:2 * E], b[:2 * E])
     v = F.linear(tgt, w[2 * E:], b[2 * E:])
     q, k = qk.view(B, L, 2, H, hd).permute(2, 0, 3, 1, 4).unbind(0)
     v = v.view(B, L, H, hd).transpose(1, 2)
