@@ -74,7 +74,9 @@ __device__ __forceinline__ uint16_t f2bf(float x) {
   const uint32_t u = __float_as_uint(x);
   return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
-__device__ __forceinline__ __bf16 tobf(float x) { return __builtin_bit_cast(__bf16, f2bf(x)); }
+// the MFMA operands' rounding: gfx950's v_cvt_pk_bf16_f32 (round to nearest even, two values an
+// instruction) — bitwise f2bf for every finite input, against f2bf's ~5 integer ops a value
+__device__ __forceinline__ __bf16 tobf(float x) { return (__bf16)x; }
 __device__ __forceinline__ float bf2f(uint16_t u) { return __uint_as_float((uint32_t)u << 16); }
 
 __device__ __forceinline__ bf16x8 zero8() {

@@ -57,13 +57,21 @@ def run(name, p, sort=True, **kw):
     print(f"{name:34s} fwd+bwd {start.elapsed_time(end) / 4 * 1e3:8.1f} us", flush=True)
 
 
+VARIANTS = [
+    ("uniform, all live, p=0, unsorted", 0.0, dict(sort=False)),
+    ("uniform, all live, p=0", 0.0, {}),
+    ("uniform, all live, p=0.1", 0.1, {}),
+    ("skewed, all live, p=0.1", 0.1, dict(skew=True)),
+    ("skewed, windows, p=0.1", 0.1, dict(skew=True, windows=True)),
+    ("uniform, windows, p=0", 0.0, dict(windows=True)),
+]
+
+
 def main():
-    run("uniform, all live, p=0, unsorted", 0.0, sort=False)
-    run("uniform, all live, p=0", 0.0)
-    run("uniform, all live, p=0.1", 0.1)
-    run("skewed, all live, p=0.1", 0.1, skew=True)
-    run("skewed, windows, p=0.1", 0.1, skew=True, windows=True)
-    run("uniform, windows, p=0", 0.0, windows=True)
+    only = os.environ.get("SEG_MB_VARIANT")  # an index into VARIANTS (PMC passes: one variant)
+    for i, (name, p, kw) in enumerate(VARIANTS):
+        if only is None or int(only) == i:
+            run(name, p, **kw)
 
 
 if __name__ == "__main__":
