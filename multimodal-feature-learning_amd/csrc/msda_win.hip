@@ -160,6 +160,12 @@ __device__ __forceinline__ short bf16_bits(float x) {  // round to nearest even 
   const uint32_t u = __float_as_uint(x);
   return (short)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
+// two values rounded to nearest even by one v_cvt_pk_bf16_f32 (bitwise bf16_bits for finite inputs),
+// x in the low half
+__device__ __forceinline__ uint32_t bf16_pair(float x, float y) {
+  typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+  return __builtin_bit_cast(uint32_t, bf16x2{(__bf16)x, (__bf16)y});
+}
 __device__ __forceinline__ float bf16_val(short h) { return __uint_as_float(((uint32_t)(uint16_t)h) << 16); }
 
 // One wave per 16-row block of one (b, m, level): barrier-free (every LDS exchange is inside the
@@ -383,8 +389,7 @@ __global__ __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(P >= 8 ?
       // bf16 — |c - hi - lo| <= 2^-16 |c|, far below the bf16 rounding of grad_value
       const uint32_t u0 = __float_as_uint(c0) & 0xffff0000u, u1 = __float_as_uint(c1) & 0xffff0000u;
       ch[j] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);  // hi halves: c0 low, c1 high
-      cl[j] = (uint32_t)(uint16_t)bf16_bits(c0 - __uint_as_float(u0)) |
-              ((uint32_t)(uint16_t)bf16_bits(c1 - __uint_as_float(u1)) << 16);
+      cl[j] = bf16_pair(c0 - __uint_as_float(u0), c1 - __uint_as_float(u1));
       if (sel) s_q[kp[j]] = s / P;
       n += __popcll(bal);
     }
@@ -708,8 +713,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
           const float c1 = tp[jj].ok1 ? a[jj] * tp[jj].w1 : 0.f;
           const uint32_t u0 = __float_as_uint(c0) & 0xffff0000u, u1 = __float_as_uint(c1) & 0xffff0000u;
           ch[jj] = __builtin_amdgcn_perm(u1, u0, 0x07060302u);
-          cl[jj] = (uint32_t)(uint16_t)bf16_bits(c0 - __uint_as_float(u0)) |
-                   ((uint32_t)(uint16_t)bf16_bits(c1 - __uint_as_float(u1)) << 16);
+          cl[jj] = bf16_pair(c0 - __uint_as_float(u0), c1 - __uint_as_float(u1));
           if (sel) s_q[kp[jj]] = s / P;
           n += __popcll(bal);
         }
