@@ -89,6 +89,9 @@ EXPORTED_SYMBOLS = (
     "mfl_seg_attention_forward",
     "mfl_seg_attention_backward",
     "mfl_seg_attention_backward_ex",
+    "mfl_seg_attention_forward_ex",
+    "mfl_seg_attention_backward_ex2",
+    "mfl_seg_attention_drop_bits_bytes",
     "mfl_seg_attention_bias_parts",
     "mfl_seg_attention_workspace_bytes",
     "mfl_seg_attention_last_error",
@@ -218,6 +221,14 @@ def _declare(lib):
     lib.mfl_seg_attention_backward_ex.restype = i32
     lib.mfl_seg_attention_backward_ex.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32,
                                                   f32, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp]
+    lib.mfl_seg_attention_forward_ex.restype = i32
+    lib.mfl_seg_attention_forward_ex.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32,
+                                                 f32, vp, vp, vp, vp, vp]
+    lib.mfl_seg_attention_backward_ex2.restype = i32
+    lib.mfl_seg_attention_backward_ex2.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, i64, i64, i64, i64, i64, f32,
+                                                   f32, vp, vp, vp, vp, vp, vp, vp, i64, i64, vp, vp, vp, vp]
+    lib.mfl_seg_attention_drop_bits_bytes.restype = i64
+    lib.mfl_seg_attention_drop_bits_bytes.argtypes = [i64, i64, i64]
     lib.mfl_seg_attention_bias_parts.restype = i64
     lib.mfl_seg_attention_bias_parts.argtypes = [i64]
     lib.mfl_seg_attention_workspace_bytes.restype = i64

@@ -66,7 +66,14 @@ struct Args {
   float* dbias;  // (H, P, 2, 64)
   float* D;      // (n, H, 32)
   int* dead;     // (n)
+  uint16_t* dbits;  // dropout keep bits, (n, H, nblk, 64) words: written by the forward, read by the backward, or null
 };
+
+// the word of (segment s, head h, key block blk) in the dropout keep-bit buffer: lane (g, li) of the
+// forward's block holds bit kt*8 + qt*4 + r for key kt*16 + 4g + r, query qt*16 + li
+__device__ __forceinline__ long long dbits_at(const Args& a, int s, int h, int blk, int nblk) {
+  return ((long long)(s * a.H + h) * nblk + blk) * 64;
+}
 
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("" ::: "memory"); }
 
@@ -336,6 +343,7 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
       m[qt] = mn;
     }
     bf16x8 pa[2];  // A operand of O += P' V: row = query qt*16 + li, k slots = keys 4g.. | 16+4g..
+    uint32_t kept = 0u;  // the block's keep bits of this lane (dbits_at)
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const int qi = qt * 16 + li;
@@ -346,11 +354,14 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
           float p = sc[kt][qt][r];
           if (a.seed) {
             const uint32_t e = ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kt * 16 + 4 * g + r);
-            p *= drop_mul(seed, thresh, dscale, e);
+            const bool k = (drop_bits(seed, e) >> 8) >= thresh;
+            kept |= (uint32_t)k << (kt * 8 + qt * 4 + r);
+            p *= k ? dscale : 0.f;  // (= drop_mul)
           }
           pa[qt][kt * 4 + r] = tobf(p);
         }
     }
+    if (a.seed && a.dbits) a.dbits[dbits_at(a, s, h, blk, nblk) + lane] = (uint16_t)kept;
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
@@ -414,6 +425,8 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
   }
 }
 
+// kBits: the forward's recorded keep bits are read (a.seed and a.dbits set), else drawn from the seed
+template <bool kBits>
 __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   __shared__ __attribute__((aligned(16))) unsigned char s_raw[kRawBytes];  // staging tiles, then partial dQ
   float(*const s_dq)[QT][HD + 1] = reinterpret_cast<float(*)[QT][HD + 1]>(s_raw);
@@ -479,6 +492,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
     for (int bb = wave; bb < nblk; bb += kWaves) {
       const uint32_t zr = in_mask(bb * KB, a.K) & ~s_keep[bb];
       if (zr == 0u) continue;
+      const uint32_t wd = kBits ? a.dbits[dbits_at(a, s, h, bb, nblk) + lane] : 0u;
 #pragma unroll
       for (int qt = 0; qt < 2; ++qt) {
         const int qi = qt * 16 + li;
@@ -489,9 +503,10 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
           for (int r = 0; r < 4; ++r) {
             const int kk = kt * 16 + 4 * g + r;
             if (!((zr >> kk) & 1u)) continue;
-            cA[qt] += a.seed ? p * drop_mul(seed, thresh, dscale, ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K +
-                                                                      (bb * KB + kk))
-                             : p;
+            cA[qt] += kBits     ? p * (((wd >> (kt * 8 + qt * 4 + r)) & 1u) ? dscale : 0.f)
+                      : !a.seed ? p
+                                : p * drop_mul(seed, thresh, dscale, ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K +
+                                                                         (bb * KB + kk));
           }
       }
     }
@@ -499,11 +514,14 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   // a segment with every key masked has constant scores: no gradient reaches q (nor k)
   int blk = dead ? nblk : next_active(s_live, wave, nblk, false);
   bf16x8 kf[2][2], vf[2][2];
+  constexpr bool bits = kBits;
+  uint32_t wb = 0u;  // the block's keep bits (the forward's), loaded with its rows
   if (blk < nblk) {
     const BlockMasks mk{in_mask(blk * KB, a.K), s_live[blk], s_keep[blk]};
     const long long rbase = (b * a.K + blk * KB) * d + h * HD;
     row_frags(kf, a.pk + rbase, bk, mk, d, g, li);
     row_frags(vf, a.pv + rbase, bv, mk, d, g, li);
+    if (bits) wb = a.dbits[dbits_at(a, s, h, blk, nblk) + lane];
   }
   while (blk < nblk) {
     const int j0 = blk * KB;
@@ -522,11 +540,13 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
         dp[kt][qt] = mfma(vf[kt][1], df[qt][1], dp[kt][qt]);
       }
     const int nb = next_active(s_live, blk + kWaves, nblk, false);
+    const uint32_t wc = wb;
     if (nb < nblk) {
       const BlockMasks mn{in_mask(nb * KB, a.K), s_live[nb], s_keep[nb]};
       const long long rbase = (b * a.K + nb * KB) * d + h * HD;
       row_frags(kf, a.pk + rbase, bk, mn, d, g, li);
       row_frags(vf, a.pv + rbase, bv, mn, d, g, li);
+      if (bits) wb = a.dbits[dbits_at(a, s, h, nb, nblk) + lane];
     }
     bf16x8 da[2];  // A operand of dQ += dS K: row = query qt*16 + li, k slots = keys 4g.. | 16+4g..
 #pragma unroll
@@ -540,7 +560,9 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
           const bool live = (mk.live >> kk) & 1u;
           const float p = live ? __expf(st[kt][qt][r] * a.scale - lse[qt]) : 0.f;
           const float dm =
-              a.seed ? drop_mul(seed, thresh, dscale, ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk)) : 1.f;
+              bits      ? (((wc >> (kt * 8 + qt * 4 + r)) & 1u) ? dscale : 0.f)
+              : !a.seed ? 1.f
+                        : drop_mul(seed, thresh, dscale, ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk));
           const float ds = p * (dp[kt][qt][r] * dm - Dq[qt]) * a.scale;
           da[qt][kt * 4 + r] = tobf(ds);
           if (!((mk.keep >> kk) & 1u)) {
@@ -626,6 +648,7 @@ struct SegPrefetch {
   bf16x8 q[2][2], o[2][2];
   float lse, D;
   uint32_t mb, kb;
+  uint32_t db;  // the forward's keep-bit word of (s, h, this block), lane's own (dbits_at)
   int dead;
 };
 
@@ -644,6 +667,7 @@ __device__ __forceinline__ void load_segment(const Args& a, int s, int h, int d,
   p.lse = a.lse[((long long)s * a.H + h) * QT + (lane & 31)];
   p.D = a.D[((long long)s * a.H + h) * QT + (lane & 31)];
   p.dead = a.dead[s];
+  p.db = a.dbits ? a.dbits[dbits_at(a, s, h, j0 / KB, (a.K + KB - 1) / KB) + lane] : 0u;
   const int j = j0 + (lane & 31);
   p.mb = 1u;
   p.kb = 0u;
@@ -659,6 +683,7 @@ __device__ __forceinline__ void load_segment(const Args& a, int s, int h, int d,
 // clip's segments alone) without block barriers — each stages its own copy of a segment's Q / dO
 // rows in LDS and prefetches its next segment's while it computes — and add their partial dK / dV
 // through LDS at the end
+template <bool kBits>
 __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
   constexpr int kStage = 2 * QT * kRS;                  // a wave's Q + dO rows
   constexpr int kPart = 2 * 2 * 4 * 64 * 16;            // a wave's dK + dV tiles (f32x4 a lane)
@@ -746,6 +771,12 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
       const bool lo = lane < 32;
       const uint32_t live = (uint32_t)__ballot(lo && pf.mb == 0u) & inm;
       const uint32_t keep = (uint32_t)__ballot(lo && pf.kb != 0u) & inm;
+      // keep bit of (query qt*16 + 4g + r, key kt*16 + li): bit kt*8 + qt*4 + (li & 3) of the forward
+      // lane (li >> 2, 4g + r)'s word, gathered into bit kt*8 + qt*4 + r of one register
+      uint32_t dmk = 0u;
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (kBits) dmk |= ((__shfl(pf.db, (li >> 2) * 16 + 4 * g + r) >> (li & 3)) & 0x1111u) << r;
       if (it + kWaves < total) load_segment(a, s_list[it + kWaves], h, d, j0, g, li, lane, pf);  // in flight meanwhile
       const uint32_t wts = (dead ? inm : live) & keep;  // kept keys with a non-zero weight
       if (wts == 0u) continue;
@@ -773,9 +804,10 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
           for (int r = 0; r < 4; ++r) {
             const int qi = qt * 16 + 4 * g + r;
             const float p = !w ? 0.f : __expf((dead ? 0.f : st[r] * a.scale) - s_lse[wave][qi]);
-            const float dm = a.seed ? drop_mul(seed, thresh, dscale,
-                                               ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk))
-                                    : 1.f;
+            const float dm = kBits     ? (((dmk >> (kt * 8 + qt * 4 + r)) & 1u) ? dscale : 0.f)
+                             : !a.seed ? 1.f
+                                       : drop_mul(seed, thresh, dscale,
+                                                  ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk));
             aa[kt][qt * 4 + r] = tobf(p * dm);
             sa[kt][qt * 4 + r] = tobf(dead ? 0.f : p * (dp[r] * dm - s_D[wave][qi]) * a.scale);
           }
@@ -858,7 +890,21 @@ int mfl_seg_attention_forward(const void* q, const void* pk, const void* pv, con
                               int64_t n, int64_t B,
                               int64_t K, int64_t Lq, int64_t H, float scale, float p_drop, const int64_t* seed,
                               void* out, float* lse, void* stream) {
+  return mfl_seg_attention_forward_ex(q, pk, pv, bias_k, bias_v, index, order, keep, masked, n, B, K, Lq, H, scale,
+                                      p_drop, seed, out, lse, nullptr, stream);
+}
+
+int64_t mfl_seg_attention_drop_bits_bytes(int64_t n, int64_t K, int64_t H) {
+  return n * H * ((K + KB - 1) / KB) * 64 * 2;
+}
+
+int mfl_seg_attention_forward_ex(const void* q, const void* pk, const void* pv, const void* bias_k,
+                                 const void* bias_v, const int64_t* index, const int32_t* order, const uint8_t* keep,
+                                 const uint8_t* masked, int64_t n, int64_t B, int64_t K, int64_t Lq, int64_t H,
+                                 float scale, float p_drop, const int64_t* seed, void* out, float* lse,
+                                 uint16_t* drop_bits, void* stream) {
   Args a{};
+  a.dbits = drop_bits;
   a.q = static_cast<const uint16_t*>(q);
   a.pk = static_cast<const uint16_t*>(pk);
   a.pv = static_cast<const uint16_t*>(pv);
@@ -891,9 +937,9 @@ int mfl_seg_attention_backward(const void* q, const void* pk, const void* pv, co
                                int64_t K, int64_t Lq, int64_t H, float scale, float p_drop, const int64_t* seed,
                                const void* out, const float* lse, const void* dout, void* dq, void* dpk, void* dpv,
                                float* dbias_part, void* workspace, void* stream) {
-  return mfl_seg_attention_backward_ex(q, pk, pv, bias_k, bias_v, index, order, keep, masked, n, B, K, Lq, H, scale,
-                                       p_drop, seed, out, lse, dout, dq, dpk, dpv, 0, 0, dbias_part, workspace,
-                                       stream);
+  return mfl_seg_attention_backward_ex2(q, pk, pv, bias_k, bias_v, index, order, keep, masked, n, B, K, Lq, H, scale,
+                                        p_drop, seed, out, lse, dout, dq, dpk, dpv, 0, 0, dbias_part, workspace,
+                                        nullptr, stream);
 }
 
 int mfl_seg_attention_backward_ex(const void* q, const void* pk, const void* pv, const void* bias_k,
@@ -903,7 +949,20 @@ int mfl_seg_attention_backward_ex(const void* q, const void* pk, const void* pv,
                                   const void* out, const float* lse, const void* dout, void* dq, void* dpk,
                                   void* dpv, int64_t dpk_row_stride, int64_t dpv_row_stride, float* dbias_part,
                                   void* workspace, void* stream) {
+  return mfl_seg_attention_backward_ex2(q, pk, pv, bias_k, bias_v, index, order, keep, masked, n, B, K, Lq, H, scale,
+                                        p_drop, seed, out, lse, dout, dq, dpk, dpv, dpk_row_stride, dpv_row_stride,
+                                        dbias_part, workspace, nullptr, stream);
+}
+
+int mfl_seg_attention_backward_ex2(const void* q, const void* pk, const void* pv, const void* bias_k,
+                                   const void* bias_v, const int64_t* index, const int32_t* order,
+                                   const uint8_t* keep, const uint8_t* masked, int64_t n, int64_t B, int64_t K,
+                                   int64_t Lq, int64_t H, float scale, float p_drop, const int64_t* seed,
+                                   const void* out, const float* lse, const void* dout, void* dq, void* dpk,
+                                   void* dpv, int64_t dpk_row_stride, int64_t dpv_row_stride, float* dbias_part,
+                                   void* workspace, const uint16_t* drop_bits, void* stream) {
   Args a{};
+  a.dbits = const_cast<uint16_t*>(drop_bits);
   const long long dmod = H * HD;
   a.rs_k = dpk_row_stride > 0 ? dpk_row_stride : dmod;
   a.rs_v = dpv_row_stride > 0 ? dpv_row_stride : dmod;
@@ -934,9 +993,15 @@ int mfl_seg_attention_backward_ex(const void* q, const void* pk, const void* pv,
   if (!aligned16(out) || !aligned16(dout) || !aligned16(dq) || !aligned16(workspace))
     return fail("seg_attention: operands must be 16-byte aligned");
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (n > 0) hipLaunchKernelGGL(seg_attn_bwd_dq, dim3((unsigned)(n * H)), dim3(kThreads), 0, st, a);
+  if (!a.seed) a.dbits = nullptr;
   const int nblk = (int)((K + KB - 1) / KB);
-  hipLaunchKernelGGL(seg_attn_bwd_dkv, dim3((unsigned)(B * H * nblk)), dim3(kThreads), 0, st, a);
+  if (a.dbits) {
+    if (n > 0) hipLaunchKernelGGL(seg_attn_bwd_dq<true>, dim3((unsigned)(n * H)), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(seg_attn_bwd_dkv<true>, dim3((unsigned)(B * H * nblk)), dim3(kThreads), 0, st, a);
+  } else {
+    if (n > 0) hipLaunchKernelGGL(seg_attn_bwd_dq<false>, dim3((unsigned)(n * H)), dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL(seg_attn_bwd_dkv<false>, dim3((unsigned)(B * H * nblk)), dim3(kThreads), 0, st, a);
+  }
   const hipError_t e = hipGetLastError();
   return e == hipSuccess ? 0 : fail(hipGetErrorString(e));
 }

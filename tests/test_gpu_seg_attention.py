@@ -117,6 +117,30 @@ def test_segment_attention_dropout_bits():
     _run(CASES[0], p=0.1)
 
 
+@pytest.mark.parametrize("ci", [0, 1, 3, 4])
+def test_segment_attention_recorded_drop_bits_equal_redrawn(ci, monkeypatch):
+    """The backward reading the forward's recorded keep bits (mfl_seg_attention_forward_ex /
+    backward_ex2, the default) gives the same output and gradients, bit for bit, as re-drawing them
+    from the seed (MFL_SEG_DROP_BITS=0) — dead segments, ragged K and one-query tiles included."""
+    dev = torch.device("cuda")
+    n, B, K, Lq, H, dead = CASES[ci]
+    q, pk, pv, bk, bv, index, keep, masked = _case(n, B, K, Lq, H, seed=n * 131 + K, dead=dead)
+    bf = [t.to(dev, torch.bfloat16) for t in (q, pk, pv, bk, bv)]
+    seed_t = torch.tensor([24681357], dtype=torch.int64, device=dev)
+    gout = torch.randn(n, Lq, 64 * H, generator=torch.Generator().manual_seed(9)).to(dev, torch.bfloat16)
+    res = {}
+    for mode in ("1", "0"):
+        monkeypatch.setenv("MFL_SEG_DROP_BITS", mode)
+        leaves = [t.clone().requires_grad_(True) for t in bf]
+        out = PKG.models.modules.seg_attention._SegmentAttention.apply(
+            *leaves, index.to(dev), keep.to(dev), masked.to(dev), H, 64 ** -0.5, 0.1, seed_t)
+        out.backward(gout)
+        torch.cuda.synchronize()
+        res[mode] = [out.detach()] + [t.grad for t in leaves]
+    for name, a, b in zip(("out", "dq", "dpk", "dpv", "dbk", "dbv"), res["1"], res["0"]):
+        assert torch.equal(a, b), name
+
+
 def test_segment_attention_no_bias_no_mask():
     _run(CASES[1], with_bias=False, with_mask=False)
 
