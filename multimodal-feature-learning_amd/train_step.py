@@ -179,6 +179,7 @@ class FlatGradTrainer:
         self._pending = None
         self._overlap_now = self.overlap  # eager steps; capture() decides for the graph
         self._fb_reduces = False          # the captured fwd+bwd graph all-reduces the buckets
+        self._capturing_now = False       # inside capture()'s fwd+bwd graph capture
         # parameters that no rank gave a gradient are left untouched, as torch AdamW leaves a
         # parameter whose grad is None (reference DDP find_unused_parameters=True, main.py:85):
         # found again after every eager step; the captured graphs keep the set of their capture
@@ -561,13 +562,6 @@ class FlatGradTrainer:
                 self.eager_step(batch)
         torch.cuda.current_stream(self.device).wait_stream(side)
         torch.cuda.synchronize(self.device)
-        if self.world > 1 or (dist.is_available() and dist.is_initialized() and dist.get_backend() == "nccl"):
-            # let the RCCL watchdog retire the warm-up collectives (it polls their events every
-            # ~100 ms): a poll of one of them while this thread's stream captures failed the
-            # process group once in the one-rank smoke ("operation not permitted on an event last
-            # recorded in a capturing stream")
-            import time
-            time.sleep(0.5)
         # capture_error_mode "thread_local": the RCCL process group's watchdog thread polls the
         # events of the warm-up collectives (hipEventQuery) while this thread captures; under the
         # default global mode that poll is refused and the watchdog aborts the process
@@ -591,9 +585,11 @@ class FlatGradTrainer:
         # all-reduce between the two graphs instead of the overlapped bucket collectives
         self._overlap_now = self.overlap and self.capture_collectives and not self._late_global
         try:
+            self._capturing_now = True
             with torch.cuda.graph(self._g_fb, pool=pool, capture_error_mode="thread_local"):
                 self._loss = self._forward_backward(batch, cache_casts=False, stage_state=self._stage_state)
         finally:
+            self._capturing_now = False
             self._fb_reduces, self._overlap_now = self._overlap_now, self.overlap
         if self._fb_reduces and self._late:
             # (the captured bucket reduces would replay without this rank's late gradients)

@@ -53,6 +53,9 @@ Fixtures:
                              of 64, ff 1024), T=64, B=2 (one padded clip), dropout 0: fp64 and bf16 autocast,
                              the seed chosen so that both runs select the same top-k tokens with a margin;
                              outputs, mask prediction, top-k, sampled gradients.
+  multimodal_bf16_d256.pt    shared BaseEncoder + MultimodalDeformableTransformer (2 enc + 2 dec, d=256, 4 heads
+                             of 64, ff 1024), video T=64 + audio T=16, B=2 (one padded clip), dropout 0: fp64 and
+                             bf16 autocast; both memories, hs, input gradients, sampled parameter gradients.
 
 usage: make_golden.py [case ...]   (default: every case; e.g. ``make_golden.py dam sparse``)
 """
@@ -785,6 +788,102 @@ def sparse_bf16_d256_case(ref):
                 margin=torch.tensor(margin), truth=truth, bf16=bf16)
 
 
+MM256 = dict(d_model=256, heads=4, ff=1024, Q=10, B=2, T=64, Ta=16, seed=131)
+
+
+def mm256_inputs():
+    """Inputs of multimodal_bf16_d256 (regenerable: the GPU test calls this too): video (B, 64, d) and
+    audio (B, 16, d) features, the second clip padded from video frame 48 / audio frame 12."""
+    c = MM256
+    gen = torch.Generator().manual_seed(c["seed"])
+    video = torch.randn((c["B"], c["T"], c["d_model"]), generator=gen, dtype=torch.float64).float()
+    audio = torch.randn((c["B"], c["Ta"], c["d_model"]), generator=gen, dtype=torch.float64).float()
+    vmask = torch.zeros(c["B"], c["T"], dtype=torch.bool)
+    vmask[1, 48:] = True
+    amask = torch.zeros(c["B"], c["Ta"], dtype=torch.bool)
+    amask[1, 12:] = True
+    durations = torch.tensor([52.5, 133.75], dtype=torch.float32)
+    return video, vmask, audio, amask, durations, gen
+
+
+def mm256_modules(mm_cls, embedding_layers, base_encoder):
+    """The multimodal stack of MultimodalDeformableDVC's proposal path (multimodal_deformable_dvc.py:
+    112-170): one PositionEmbeddingVideoSine and one BaseEncoder shared by the video and audio
+    streams, MultimodalDeformableTransformer (2 + 2 layers, d=256, 4 heads of 64, ff 1024, dropout 0)."""
+    c = MM256
+    d = c["d_model"]
+    return torch.nn.ModuleDict(dict(
+        pos_embed=embedding_layers.PositionEmbeddingVideoSine(d // 2, normalize=True),
+        base_encoder=base_encoder.BaseEncoder(4, d, d),
+        transformer=mm_cls(d_model=d, num_head=c["heads"], num_encoder_layers=2, num_decoder_layers=2,
+                           dim_feedforward=c["ff"], dropout=0.0, return_intermediate_dec=True, num_feature_levels=4,
+                           dec_n_points=4, enc_n_points=4),
+        query_embedding=torch.nn.Embedding(c["Q"], 2 * d)))
+
+
+def mm256_forward(mods, video, vmask, audio, amask, durations):
+    """Reference multimodal_deformable_transformer.py:237-277 (encoder: per layer video->video,
+    audio->audio and both cross-modal MSDA calls through the shared layers) and :380-432 (decoder:
+    cross-attention into both memories + the fusion bridge), behind the shared BaseEncoder.
+    Returns (memory_video, memory_audio, hs)."""
+    tr = mods["transformer"]
+    v_srcs, v_masks, v_pos = mods["base_encoder"](video, vmask, durations, mods["pos_embed"])
+    a_srcs, a_masks, a_pos = mods["base_encoder"](audio, amask, durations, mods["pos_embed"])
+    v = tr.prepare_encoder_inputs(v_srcs, v_masks, v_pos)
+    a = tr.prepare_encoder_inputs(a_srcs, a_masks, a_pos)
+    mem_v, mem_a = tr.forward_encoder(*v, *a)
+    B = video.shape[0]
+    qw = mods["query_embedding"].weight
+    qmask = torch.ones(B, qw.shape[0], dtype=torch.bool, device=video.device)
+    _, tgt, refp, qpos = tr.prepare_decoder_input_query(B, qw)
+    hs, _ = tr.forward_decoder(tgt, refp, qpos, qmask, mem_v, v[1], v[2], v[3], v[5], mem_a, a[1], a[2], a[3], a[5],
+                               False)
+    return mem_v, mem_a, hs
+
+
+def multimodal_bf16_d256_case(ref):
+    """configs[2]'s composition at a size where the bench's fused bf16 paths engage (d % 256 == 0,
+    2 + 2 layers): the shared BaseEncoder over video (T=64) and audio (T=16) and the reference's
+    MultimodalDeformableTransformer (4 heads of 64 channels: the bench kernels' D), B=2 with one padded
+    clip, dropout 0 — in fp64 (the truth) and in fp32 under torch.autocast('cpu', bfloat16) (the
+    reference's own bf16 run).  Loss (hs w_hs).sum() + (memory_video w_v).sum() + (memory_audio w_a).sum().
+    Parameters from regen_parameters; gradients on fixed samples plus their norms."""
+    import copy
+    c = MM256
+    named = mm256_modules(ref.mm.MultimodalDeformableTransformer, ref.embedding_layers, ref.base_encoder)
+    sums = regen_parameters(named, c["seed"])
+    video, vmask, audio, amask, durations, gen = mm256_inputs()
+    Sv = sum(c["T"] >> l for l in range(4))
+    Sa = sum(c["Ta"] >> l for l in range(4))
+    w = [torch.randn(sh, generator=gen, dtype=torch.float64).float()
+         for sh in ((2, c["B"], c["Q"], c["d_model"]), (c["B"], Sv, c["d_model"]), (c["B"], Sa, c["d_model"]))]
+
+    def run(mods, dtype, autocast):
+        v = video.to(dtype).requires_grad_(True)
+        a = audio.to(dtype).requires_grad_(True)
+        with torch.autocast("cpu", dtype=torch.bfloat16, enabled=autocast):
+            mem_v, mem_a, hs = mm256_forward(mods, v, vmask, a, amask, durations.to(dtype))
+        loss = ((hs.to(dtype) * w[0].to(dtype)).sum() + (mem_v.to(dtype) * w[1].to(dtype)).sum()
+                + (mem_a.to(dtype) * w[2].to(dtype)).sum())
+        loss.backward()
+        return dict(memory_video=mem_v.detach().float(), memory_audio=mem_a.detach().float(), hs=hs.detach().float(),
+                    grad_video=v.grad.float(), grad_audio=a.grad.float(), loss=loss.detach().double(),
+                    grads=sampled_grads(dict(mods.items())))
+
+    m64 = copy.deepcopy(named).double()
+    torch.set_default_dtype(torch.float64)  # the duration embedding allocates with the default dtype
+    try:
+        truth = run(m64, torch.float64, False)
+    finally:
+        torch.set_default_dtype(torch.float32)
+    bf16 = run(named, torch.float32, True)
+    rel = lambda a, b: ((a.double() - b.double()).norm() / b.double().norm()).item()  # noqa: E731
+    print("mm256: reference bf16 vs fp64: " + " ".join(
+        f"{k} {rel(bf16[k], truth[k]):.3e}" for k in ("memory_video", "memory_audio", "hs", "grad_video", "grad_audio")))
+    return dict(config={k: torch.tensor(v) for k, v in c.items()}, param_abs_sums=sums, weights=w, truth=truth,
+                bf16=bf16)
+
+
 CAPTION = dict(vocab=10000, seq_len=20, d_model=512, depth=2, heads=8, N=6, K=40, seed=101, head_scale=8.0,
                bos=2, eos=3, pad=1)
 
@@ -1383,6 +1482,7 @@ def main():
         "caption_bf16": lambda: caption_bf16_case(ref),
         "deformable_dvc_bf16_d256": lambda: deformable_dvc_bf16_d256_case(ref),
         "sparse_bf16_d256": lambda: sparse_bf16_d256_case(ref),
+        "multimodal_bf16_d256": lambda: multimodal_bf16_d256_case(ref),
     }
     wanted = sys.argv[1:] or list(cases)
     for name, fn in cases.items():

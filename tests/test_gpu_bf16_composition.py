@@ -286,6 +286,82 @@ def test_dvc_training_step_bf16_matches_reference_bf16(golden, dev):
     assert not fails, fails
 
 
+MM_EXPECTED_PATHS = ("carry_entry", "add_ln_carry", "grad_sum_into", "grad_accum_view", "relu_dropout",
+                     "linear_shadow", "query_prologue", "zero_rows", "msda_bfloat16", "msda_level_major")
+
+
+def test_multimodal_step_bf16_matches_reference_bf16(golden, dev):
+    """multimodal_bf16_d256: the shared BaseEncoder over video (T=64) and audio (T=16) and the reference's
+    MultimodalDeformableTransformer (2 + 2 layers, d=256, 4 heads of 64, ff 1024, one padded clip), fp64
+    and under bf16 autocast (reference multimodal_deformable_transformer.py:237-277 — four MSDA calls a
+    layer through shared weights, :256,262,268,270 — and :380-432).  Ours runs as bench.py --config
+    multimodal does: FlatGradTrainer (bf16 shadow weights), bf16 autocast, and the paths configs[2]
+    benchmarks — the bf16 carry between the fused add + LayerNorms (carry_entry / add_ln_carry), the
+    activation gradients summed inside the consumer's dgrad GEMM (grad_sum_into) and the shared layers'
+    gradients accumulated in place into their flat views (grad_accum_view) — asserted by trace.  Both
+    memories, hs, both input gradients and >= 60 sampled parameter gradients (with their full norms) must
+    be as close to the fp64 run as the reference's own bf16 run is (check(): <= 1.5 x its error + slack)."""
+    g = golden("multimodal_bf16_d256")
+    c = {k: int(v) for k, v in g["config"].items()}
+    mods = MG.mm256_modules(M.deformable.multimodal_deformable_transformer.MultimodalDeformableTransformer,
+                            M.modules.embedding_layers, M.base_encoder)
+    _check_param_sums(mods, c["seed"], g["param_abs_sums"])
+
+    class _MMStack(nn.Module):
+        def __init__(self, m):
+            super().__init__()
+            self.mods = m
+
+        def forward(self, video, vmask, audio, amask, durations):
+            return MG.mm256_forward(self.mods, video, vmask, audio, amask, durations)
+
+    stack = _MMStack(mods).to(dev)
+    video, vmask, audio, amask, durations, _ = MG.mm256_inputs()
+    video = video.to(dev).requires_grad_(True)
+    audio = audio.to(dev).requires_grad_(True)
+    w = [t.to(dev) for t in g["weights"]]
+    outs = {}
+
+    def loss_fn(out):
+        outs["memory_video"], outs["memory_audio"], outs["hs"] = out
+        return (out[2].float() * w[0]).sum() + (out[0].float() * w[1]).sum() + (out[1].float() * w[2]).sum()
+
+    trainer = PKG.train_step.FlatGradTrainer(stack, loss_fn, use_bf16=True, graph=False)
+    PKG._trace.clear()
+    trainer._forward_backward((video, vmask.to(dev), audio, amask.to(dev), durations.to(dev)))
+    torch.cuda.synchronize()
+    hits = dict(PKG._trace.hits)
+    for path in MM_EXPECTED_PATHS:
+        assert hits.get(path, 0) > 0, (path, hits)
+    assert not any(k.endswith("_cast") for k in hits), hits  # every Linear read the trainer's shadow
+
+    truth, ref16 = g["truth"], g["bf16"]
+    report, fails = [], []
+    for k in ("memory_video", "memory_audio", "hs"):
+        check(k, outs[k].float(), truth[k], ref16[k], report=report, fails=fails)
+    check("grad_video", video.grad, truth["grad_video"], ref16["grad_video"], report=report, fails=fails)
+    check("grad_audio", audio.grad, truth["grad_audio"], ref16["grad_audio"], report=report, fails=fails)
+    named = dict(mods.items())
+    n = 0
+    for mname, grads in truth["grads"].items():
+        params = dict(named[mname].named_parameters())
+        for k, t in grads.items():
+            if t["norm"].item() < 1e-9:
+                continue
+            flat = params[k].grad.reshape(-1)
+            s = flat[MG.grad_sample_index(mname + "." + k, flat.numel()).to(dev)]
+            bound = check(f"{mname}.{k}", s, t["sample"], ref16["grads"][mname][k]["sample"], slack=5e-3,
+                          report=report, fails=fails)
+            e_norm = abs(flat.double().norm().item() / t["norm"].item() - 1)
+            if e_norm > bound:
+                fails.append((f"{mname}.{k}", "norm", e_norm, bound))
+            n += 1
+    for r in report:
+        print("multimodal bf16 (name, ours vs fp64, reference bf16 vs fp64):", r)
+    assert n >= 60, n
+    assert not fails, fails
+
+
 def test_sparse_step_bf16_matches_reference_bf16(golden, dev, monkeypatch):
     """sparse_bf16_d256: the reference's default-active Sparse-DETR transformer (rho 0.3: mask
     predictor, top-k encoder tokens scattered back into the memory; 2 + 2 layers, d=256, 4 heads of
