@@ -54,6 +54,13 @@ int mfl_sum_slabs(const float* part, int64_t s, int64_t n, float* out, void* str
 int mfl_sum_slabs_ex(const float* part, int64_t groups, int64_t s, int64_t n, float* out, int accumulate,
                      void* stream);
 
+/* A HIP stream of its own on `device` (hipStreamNonBlocking), outside PyTorch's round-robin stream pool:
+ * the trainer's capture / comm streams (train_step.py).  A pool stream can be the RCCL process group's
+ * own NCCL stream, and HIP refuses hipEventQuery of an event whose stream is capturing — even one
+ * recorded before the capture — which the RCCL watchdog takes as fatal.  Lives for the
+ * process. */
+int mfl_stream_create(int device, void** stream);
+
 /* Text of the last error of flat_adamw_step / mfl_colsum / mfl_sum_slabs on the calling thread. */
 const char* flat_adamw_last_error(void);
 

@@ -51,6 +51,7 @@ EXPORTED_SYMBOLS = (
     "mfl_colsum_ex",
     "mfl_sum_slabs",
     "mfl_sum_slabs_ex",
+    "mfl_stream_create",
     # include/add_layernorm.h
     "mfl_add_layernorm_workspace_bytes",
     "mfl_add_layernorm_forward",
@@ -155,6 +156,8 @@ def _declare(lib):
     lib.msda_hip_dam_flat_grid.restype = i32
     lib.msda_hip_dam_flat_grid.argtypes = [vp, vp, p64, p64, i64, i64, i64, i64, i64, vp, vp]
     f32 = ctypes.c_float
+    lib.mfl_stream_create.restype = ctypes.c_int
+    lib.mfl_stream_create.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
     lib.flat_adamw_workspace_bytes.restype = ctypes.c_size_t
     lib.flat_adamw_workspace_bytes.argtypes = []
     lib.flat_adamw_step.restype = i32
@@ -308,3 +311,23 @@ def host_i64_array(values):
 
 def stream_handle(device):
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+_own_streams = {}
+
+
+def own_stream(device, tag):
+    """A HIP stream of the package's own on ``device`` (include/flat_adamw.h mfl_stream_create), wrapped as
+    a torch stream, one per (device, tag) for the process: the trainer's capture and bucket-collective
+    streams, which must never be a pool stream that the RCCL process group also uses."""
+    device = torch.device(device)
+    key = (device.index if device.index is not None else torch.cuda.current_device(), tag)
+    s = _own_streams.get(key)
+    if s is None:
+        ptr = ctypes.c_void_p()
+        rc = load_library().mfl_stream_create(key[0], ctypes.byref(ptr))
+        if rc != 0:
+            raise RuntimeError(load_library().flat_adamw_last_error().decode())
+        s = torch.cuda.ExternalStream(ptr.value, device=torch.device("cuda", key[0]))
+        _own_streams[key] = s
+    return s

@@ -463,6 +463,28 @@ int mfl_sum_slabs_ex(const float* part, int64_t groups, int64_t s, int64_t n, fl
   return status("sum slabs");
 }
 
+int mfl_stream_create(int device, void** stream) {
+  g_err[0] = 0;
+  if (stream == nullptr) {
+    snprintf(g_err, sizeof(g_err), "mfl_stream_create: stream is NULL");
+    return 1;
+  }
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "mfl_stream_create: bad device %d", device);
+    return 1;
+  }
+  hipStream_t s = nullptr;
+  const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  (void)hipSetDevice(prev);
+  if (e != hipSuccess) {
+    snprintf(g_err, sizeof(g_err), "mfl_stream_create: %s", hipGetErrorString(e));
+    return 1;
+  }
+  *stream = s;
+  return 0;
+}
+
 const char* flat_adamw_last_error(void) { return g_err; }
 
 }  // extern "C"

@@ -5,6 +5,8 @@ scipy's ``linear_sum_assignment`` on the host, as in the reference.  The referen
 device->host copy per call (``.cpu()`` :86) plus two syncing asserts (utils/box_ops.py:59-60), once
 per decoder level; ``match_levels`` builds every level's cost matrix and the well-formedness flags
 on the device and moves them in ONE copy."""
+from collections.abc import Sequence
+
 import numpy as np
 import torch
 from scipy.optimize import linear_sum_assignment
@@ -64,7 +66,8 @@ class HungarianMatcher(nn.Module):
         """The host half: the reference's syncing asserts (utils/box_ops.py:59-60) and scipy's
         linear_sum_assignment per clip and level (reference :86-94), on numpy views of the one
         copied buffer (the per-clip torch indexing and conversions were most of the host step)."""
-        return HungarianMatcher.solve_levels_into(host, meta, None)
+        res = HungarianMatcher.solve_levels_into(host, meta, None)
+        return res.materialize() if isinstance(res, _LevelPairs) else res  # a plain list leaves the public API
 
     @staticmethod
     def solve_levels_into(host, meta, idx_out):
@@ -122,34 +125,36 @@ class HungarianMatcher(nn.Module):
         return result
 
 
-class _LevelPairs(list):
-    """solve_levels' result ([level][clip] -> (prediction indices, target indices) int64 tensors) over
-    the native call's flat arrays, built when first read: a replayed DVC step reads only the index
-    lists the call also wrote (the ~200 small tensors cost more host time than the matching)."""
+class _LevelPairs(Sequence):
+    """solve_levels_into's result ([level][clip] -> (prediction indices, target indices) int64 tensors)
+    over the native call's flat arrays, built when first read: a replayed DVC step reads only the index
+    lists the call also wrote (the ~200 small tensors cost more host time than the matching).  A
+    read-only Sequence, not a list subclass (C-level list operations would see the empty storage);
+    the public ``solve_levels`` hands out ``materialize()``'s plain list."""
 
     def __init__(self, src, tgt, bounds, L, B):
-        super().__init__()
         self._args = (src, tgt, bounds, L, B)
+        self._levels = None
 
-    def _build(self):
-        if self._args is not None:
+    def materialize(self):
+        if self._levels is None:
             src, tgt, bounds, L, B = self._args
-            self._args = None
             st, tt = torch.from_numpy(src), torch.from_numpy(tgt)
-            super().extend([[(st[lvl, bounds[b]:bounds[b + 1]], tt[lvl, bounds[b]:bounds[b + 1]]) for b in range(B)]
-                            for lvl in range(L)])
+            self._levels = [[(st[lvl, bounds[b]:bounds[b + 1]], tt[lvl, bounds[b]:bounds[b + 1]]) for b in range(B)]
+                            for lvl in range(L)]
+        return self._levels
 
     def __getitem__(self, i):
-        self._build()
-        return super().__getitem__(i)
-
-    def __iter__(self):
-        self._build()
-        return super().__iter__()
+        return self.materialize()[i]
 
     def __len__(self):
-        self._build()
-        return super().__len__()
+        return self._args[3]
+
+    def __eq__(self, other):
+        return self.materialize() == (other.materialize() if isinstance(other, _LevelPairs) else other)
+
+    def __repr__(self):
+        return repr(self.materialize())
 
 
 def build_matcher(args):

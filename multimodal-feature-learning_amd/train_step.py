@@ -31,7 +31,9 @@ the MI355X the way the hardware wants it:
 
 ``graph=False`` runs the same three phases eagerly (CPU tests, world_size-2 gloo).
 """
+import os
 import time
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -72,6 +74,80 @@ def _flat_order(model, params):
             seen.add(id(p))
             out.append(p)
     return out
+
+
+_CAPTURE_GROUPS = {}
+
+
+def _capture_group(pg, device):
+    """The process group the captured bucket all-reduces run on: the trainer's group's ranks again, as a
+    group used ONLY inside graph captures (one per (group, device) for the process).
+
+    The RCCL process group's watchdog thread polls the end event of every eager collective
+    (WorkNCCL::isCompleted -> hipEventQuery) until it retires it, ~100 ms later.  HIP refuses that query
+    (hipErrorCapturedEvent) whenever the stream the event was recorded on is capturing at the time of
+    the query — even for an event recorded and completed before the capture began
+    (tools/probes/event_capture_probe.py) — and the watchdog takes the refusal as fatal.  Captured
+    collectives join their group's NCCL stream into the capture, so captured and eager collectives on
+    one group abort the process whenever a poll of a not-yet-retired eager collective falls inside the
+    capture (the warm-up steps' collectives right before it).  This group never runs an eager collective:
+    its communicator is connected eagerly (device_id) and its first collective runs inside a throwaway
+    relaxed-mode capture, so its watchdog never holds a Work.  Its NCCL stream comes from the
+    high-priority pool, apart from the default group's and torch's default-priority streams."""
+    key = (id(pg), device.index)
+    entry = _CAPTURE_GROUPS.get(key)
+    if entry is None:
+        from . import _native
+        ranks = dist.get_process_group_ranks(pg if pg is not None else dist.group.WORLD)
+        opts = dist.ProcessGroupNCCL.Options()
+        opts.is_high_priority_stream = True
+        if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") != "0":
+            raise RuntimeError(
+                "FlatGradTrainer: captured RCCL collectives need TORCH_NCCL_CUDA_EVENT_CACHE=0 when the process "
+                "groups are created (the package sets it at import: import it before init_process_group); with the "
+                "cache a captured collective's end event reaches an eager collective and the RCCL watchdog aborts")
+        grp = dist.new_group(ranks, backend="nccl", pg_options=opts, device_id=device)
+        _drain_watchdogs(exclude=(grp,))
+        buf = torch.zeros(64, dtype=torch.float32, device=device)
+        stream = _native.own_stream(device, "capture")
+        stream.wait_stream(torch.cuda.current_stream(device))
+        g = torch.cuda.CUDAGraph()
+        with warnings.catch_warnings():
+            warnings.filterwarnings("ignore", message="The CUDA Graph is empty")  # (one rank: nothing to reduce)
+            with torch.cuda.graph(g, stream=stream, capture_error_mode="relaxed"):
+                dist.all_reduce(buf, group=grp)
+        g.replay()
+        torch.cuda.synchronize(device)
+        entry = _CAPTURE_GROUPS[key] = (grp, g, buf)  # (the warm graph and its buffer stay alive)
+    return entry[0]
+
+
+def _drain_watchdogs(exclude=(), timeout_s=120.0):
+    """Wait until the RCCL watchdogs have retired every collective they poll (except those of the groups
+    in ``exclude``), read from the flight recorder's record of which collectives are still active.
+
+    A graph capture must not begin while the watchdog of a group still holds one of its eager
+    collectives: HIP refuses hipEventQuery of an event whose stream joins a capture, and the watchdog
+    takes the refusal as fatal (_capture_group).  The watchdog retires a finished collective on its next
+    poll (~100 ms); this waits for exactly that condition instead of sleeping."""
+    import json
+    from torch._C._distributed_c10d import _dump_nccl_trace_json
+    if int(os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE", "0") or 0) <= 0:
+        raise RuntimeError("FlatGradTrainer: captured RCCL collectives need TORCH_NCCL_TRACE_BUFFER_SIZE > 0 when the "
+                           "process groups are created (the package sets it at import: import it before "
+                           "init_process_group)")
+    skip = {dist.distributed_c10d._get_process_group_name(g) for g in exclude}
+    t0 = time.monotonic()
+    while True:
+        dump = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
+        active = [e for e in dump.get("entries", []) if (e.get("process_group") or [None])[0] not in skip]
+        if not active:
+            return
+        if time.monotonic() - t0 > timeout_s:
+            raise RuntimeError(f"FlatGradTrainer.capture: {len(active)} collectives not retired by the RCCL watchdog "
+                               f"after {timeout_s:.0f} s (first: {active[0].get('profiling_name')}, "
+                               f"state {active[0].get('state')})")
+        time.sleep(0.005)
 
 
 def _record(events):
@@ -180,6 +256,7 @@ class FlatGradTrainer:
         self._overlap_now = self.overlap  # eager steps; capture() decides for the graph
         self._fb_reduces = False          # the captured fwd+bwd graph all-reduces the buckets
         self._capturing_now = False       # inside capture()'s fwd+bwd graph capture
+        self._capture_pg = None           # the group of the captured bucket all-reduces (_capture_group)
         # parameters that no rank gave a gradient are left untouched, as torch AdamW leaves a
         # parameter whose grad is None (reference DDP find_unused_parameters=True, main.py:85):
         # found again after every eager step; the captured graphs keep the set of their capture
@@ -293,10 +370,13 @@ class FlatGradTrainer:
             cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
             if cur is not None:
                 if self._comm_stream is None:
-                    self._comm_stream = torch.cuda.Stream(self.device)
+                    from . import _native
+                    self._comm_stream = _native.own_stream(self.device, "comm")  # (never a pool stream, _capture_group)
                 self._comm_stream.wait_stream(cur)
+                # inside capture() the collectives go to the capture-only group (_capture_group)
+                group = self._capture_pg if self._capturing_now and self._capture_pg is not None else self.pg
                 with torch.cuda.stream(self._comm_stream):
-                    dist.all_reduce(self.flat_grad[start:end], group=self.pg)
+                    dist.all_reduce(self.flat_grad[start:end], group=group)
             else:
                 self._works.append(dist.all_reduce(self.flat_grad[start:end], group=self.pg, async_op=True))
 
@@ -555,7 +635,10 @@ class FlatGradTrainer:
                 "(DEBUG_CLR_GRAPH_PACKET_CAPTURE must be '0' before HIP initialises: import the package "
                 "before any device call, or export the variable); with it on, replays after allocating "
                 "eager work produced corrupted gradients (DESIGN.md §6)")
-        side = torch.cuda.Stream(self.device)
+        from . import _native
+        # the warm-up and the captures run on the package's own stream: never a pool stream that the
+        # RCCL process group's NCCL stream can be (_capture_group)
+        side = _native.own_stream(self.device, "capture")
         side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(side):
             for _ in range(warmup):
@@ -564,8 +647,14 @@ class FlatGradTrainer:
         torch.cuda.synchronize(self.device)
         # capture_error_mode "thread_local": the RCCL process group's watchdog thread polls the
         # events of the warm-up collectives (hipEventQuery) while this thread captures; under the
-        # default global mode that poll is refused and the watchdog aborts the process
+        # default global mode that poll is refused.  The captured collectives themselves run on a
+        # group of their own (_capture_group), whose NCCL stream no eager collective ever used
         pool = None
+        if (self.overlap and self.capture_collectives and not self._late_global and dist.is_available()
+                and dist.is_initialized() and dist.get_backend(self.pg) == "nccl"):
+            self._capture_pg = _capture_group(self.pg, self.device)
+            # no eager collective (the warm-up's) left for a watchdog to poll during the captures
+            _drain_watchdogs(exclude=(self._capture_pg,))
         if self.staged:
             # graph A: the forward up to the host step and the copy of its request into pinned
             # host memory; graph B (same memory pool) runs the rest of the forward and the whole
@@ -573,7 +662,7 @@ class FlatGradTrainer:
             shape, dtype = self._request_like  # from the eager warm-up
             self._request_host = torch.empty(shape, dtype=dtype, device="cpu").pin_memory()
             self._g_a = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self._g_a, capture_error_mode="thread_local"):
+            with torch.cuda.graph(self._g_a, stream=side, capture_error_mode="thread_local"):
                 with torch.autocast(self.device.type, dtype=torch.bfloat16, enabled=self.use_bf16,
                                     cache_enabled=False), seed_pool(self.device):
                     self._stage_state = self.loss_fn.stage_a(self.model, batch)
@@ -586,7 +675,7 @@ class FlatGradTrainer:
         self._overlap_now = self.overlap and self.capture_collectives and not self._late_global
         try:
             self._capturing_now = True
-            with torch.cuda.graph(self._g_fb, pool=pool, capture_error_mode="thread_local"):
+            with torch.cuda.graph(self._g_fb, pool=pool, stream=side, capture_error_mode="thread_local"):
                 self._loss = self._forward_backward(batch, cache_casts=False, stage_state=self._stage_state)
         finally:
             self._capturing_now = False
@@ -596,7 +685,7 @@ class FlatGradTrainer:
             raise RuntimeError("FlatGradTrainer.capture: a gradient arrived after its bucket was reduced inside the "
                                "captured backward; capture with capture_collectives=False")
         self._g_up = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self._g_up, pool=self._g_fb.pool(), capture_error_mode="thread_local"):
+        with torch.cuda.graph(self._g_up, pool=self._g_fb.pool(), stream=side, capture_error_mode="thread_local"):
             self._update()
         torch.cuda.synchronize(self.device)
 

@@ -165,7 +165,11 @@ def test_caption_decoder_bf16_matches_reference_bf16(golden, dev):
     with torch.autocast("cuda", dtype=torch.bfloat16):
         out = dec(tgt, mem, tgt_mask=tgt_mask, memory_mask=kmask[:, None, None, :], tgt_padding_mask=padding)
     out = out.float()
-    p_t = out.gather(-1, nxt[None, :, :, None].expand(out.shape[0], -1, -1, 1))[..., 0]
+    # the caption loss's word read as the DVC step takes it: word_probs' one-pass logits gradient
+    # (mfl_word_prob_backward) in place of gather -> softmax backward -> cast
+    PKG._trace.clear()
+    p_t = M.unimodal_caption_decoder.word_probs(out, nxt[None].expand(out.shape[0], -1, -1))
+    assert PKG._trace.hits.get("word_prob_fused", 0) > 0, dict(PKG._trace.hits)
     (-(p_t * live).sum()).backward()
     truth, ref16 = g["truth"], g["bf16"]
     report, fails = [], []
@@ -257,17 +261,28 @@ def test_dvc_training_step_bf16_matches_reference_bf16(golden, dev):
                 for la, lb in zip(own[0], levels) for a, b in zip(la, lb))
     assert agree, f"our bf16 matching costs give another assignment (fixture margin {g['margin'].item():.4f})"
     report, fails = [], []
+    # the loss is a sum of random-signed products of these outputs (w ~ N(0, 1)), so its scalar error is a
+    # cancellation (the reference bf16 run's 9e-5 is luck, not a bound).  Every weighted term is pinned
+    # element by element at the outputs' own tolerance (check()), so no term can hide behind the sum; the
+    # scalar loss is held to what our measured element errors e_k allow: they do not depend on w, so
+    # sum_k w_k . e_k ~ N(0, sum_k |e_k|^2) — 4 standard deviations — plus the aux terms' Cauchy-Schwarz
+    # bound (constant weights 0.5)
+    var = 0.0
     for k in MG.DVC256_KEYS:
         check(k, out[k].float(), truth["out"][k], ref16["out"][k], report=report, fails=fails)
-    check("aux_captions", torch.stack([o["pred_captions"].float() for o in out["aux_outputs"]]), truth["aux_captions"],
-          ref16["aux_captions"], report=report, fails=fails)
+        var += (out[k].double().cpu() - truth["out"][k].double()).norm().item() ** 2
+        wk = w[k].double().cpu()
+        check("term " + k, out[k].double().cpu() * wk, truth["out"][k] * wk, ref16["out"][k] * wk, report=report,
+              fails=fails)
+    aux = torch.stack([o["pred_captions"].float() for o in out["aux_outputs"]])
+    check("aux_captions", aux, truth["aux_captions"], ref16["aux_captions"], report=report, fails=fails)
     loss = MG.dvc256_loss(out, {k: v.double() for k, v in w.items()})
-    # the loss is a weighted sum of the outputs above, whose bf16 errors are ~1-4 % an element: the
-    # reference run's 9e-5 is a cancellation, not a bound — two of our runs whose encoder inputs differ
-    # by 7e-8 relative (the channels-last GroupNorm on / off; their memories agree to 2e-4) differ by
-    # 0.6 % in it.  Held to 1 %, as the outputs' own spread allows
-    check("loss", loss.reshape(1), truth["loss"].reshape(1), ref16["loss"].reshape(1), slack=1e-2, report=report,
-          fails=fails)
+    e_loss = abs(loss.item() - truth["loss"].item())
+    ta = truth["aux_captions"].double()
+    allowed = 4.0 * var ** 0.5 + 0.5 * (aux.double().cpu() - ta).norm().item() * ta.numel() ** 0.5
+    report.append(("loss abs error (allowed)", round(e_loss, 5), round(allowed, 5)))
+    if e_loss > allowed:
+        fails.append(("loss", e_loss, allowed))
     params = dict(model.named_parameters())
     n = 0
     for k, t in truth["grads"]["dvc"].items():
@@ -287,7 +302,7 @@ def test_dvc_training_step_bf16_matches_reference_bf16(golden, dev):
 
 
 MM_EXPECTED_PATHS = ("carry_entry", "add_ln_carry", "grad_sum_into", "grad_accum_view", "relu_dropout",
-                     "linear_shadow", "query_prologue", "zero_rows", "msda_bfloat16", "msda_level_major")
+                     "linear_shadow", "query_prologue", "zero_rows", "msda_bfloat16")
 
 
 def test_multimodal_step_bf16_matches_reference_bf16(golden, dev):

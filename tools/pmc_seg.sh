@@ -9,6 +9,7 @@ run() { local name=$1; shift; rm -rf $OUT/$name
 run sq1 SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU
 run sq2 SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_VALU_MFMA_BUSY_CYCLES
 run fetch FETCH_SIZE
+run write WRITE_SIZE
 python3 - $OUT <<'PY'
 import csv, glob, os, sys
 from collections import defaultdict

@@ -9,7 +9,7 @@ current stream is capturing, whether the comm stream is capturing once it has wa
 stream ids.  A flush issued during capture from a thread whose current stream is not capturing would
 enqueue its Work to the watchdog while its end event is recorded inside the capture.
 
-usage: python tools/rccl_capture_diag.py [rounds]   (prints a summary; exits 1 if such a flush occurred)
+usage: python tools/rccl_capture_diag.py [rounds] [capture|eager]   (eager: capture_collectives=False)   (prints a summary; exits 1 if such a flush occurred)
 """
 import copy
 import os
@@ -28,11 +28,15 @@ def main():
     import importlib
     pkg = importlib.import_module("multimodal-feature-learning_amd")
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 10
+    capcoll = (sys.argv[2] if len(sys.argv) > 2 else "capture") == "capture"
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     dist.init_process_group("nccl", rank=0, world_size=1)
+    print("stream priority range", torch.cuda.Stream.priority_range(), "pool ids (default / high):",
+          [torch.cuda.Stream(dev).stream_id for _ in range(3)], [torch.cuda.Stream(dev, priority=-1).stream_id
+                                                                  for _ in range(3)], flush=True)
     T = pkg.train_step.FlatGradTrainer
     log = []
     orig = T._flush_bucket
@@ -45,6 +49,19 @@ def main():
         return orig(self, b)
 
     T._flush_bucket = flush
+    ts = pkg.train_step
+    orig_drain = ts._drain_watchdogs
+
+    def drain(exclude=(), timeout_s=120.0):
+        import json
+        import time
+        from torch._C._distributed_c10d import _dump_nccl_trace_json
+        n = len(json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True)).get("entries", []))
+        t0 = time.monotonic()
+        orig_drain(exclude, timeout_s)
+        print(f"  drain: {n} active entries, waited {1e3 * (time.monotonic() - t0):.1f} ms", flush=True)
+
+    ts._drain_watchdogs = drain
     small = dict(d_model=64, num_queries=6, feature_dim=64, enc_layers=2, dec_layers=2, ff_dim=128, dropout=0.0)
     torch.manual_seed(0)
     base = pkg.dvc_core.DeformableDVCCore(**small)
@@ -52,8 +69,13 @@ def main():
     try:
         for r in range(rounds):
             tr = T(copy.deepcopy(base).to(dev), pkg.dvc_core.workload_loss, lr=1e-3, use_bf16=(r % 2 == 0),
-                   graph=True, overlap="force", bucket_mb=0.05)
+                   graph=True, overlap="force", bucket_mb=0.05, capture_collectives=capcoll)
+            n0 = len(log)
             tr.capture(batch, warmup=1)
+            cap = [e for e in log[n0:] if e["capturing_trainer"]]
+            print(f"round {r}: capture flushes {len(cap)}, threads {sorted({e['thread'] for e in cap})}, "
+                  f"not capturing {sum(1 for e in cap if not e['cur_capturing'])}, "
+                  f"streams {sorted({e['cur_stream'] for e in cap})}", flush=True)
             for _ in range(3):
                 tr.step(batch)
             torch.cuda.synchronize()
