@@ -14,7 +14,8 @@ from torch import nn
 from torch.nn.init import constant_, normal_, xavier_uniform_
 
 from ..modules.pyramid import flatten_levels, level_pos_flatten
-from ..modules.attention import MSDeformAttn, mha_self_attention
+from ... import msda as _msda
+from ..modules.attention import MSDeformAttn, joint_supported, mha_self_attention
 from ..modules.misc_modules import inverse_sigmoid
 from ..modules.linear import Linear, mark_grad_sum
 from ..modules.add_norm import add_layer_norm, add_layer_norm_carry, carry_entry, carry_supported, pos_sink
@@ -173,6 +174,26 @@ class MultimodalDeformableTransformerEncoderLayer(nn.Module):
         return (ffn(audio_attended_visual, video_next_pos, pos_accs[0]),
                 ffn(visual_attended_audio, audio_next_pos, pos_accs[1]))
 
+    def forward_joint(self, stream, next_pos, pos_acc, self_calls, cross_calls, padding_mask):
+        """``forward_carry`` with the video and audio rows in ONE tensor each (``stream`` = (src, value,
+        query) of the joint rows, video rows first): the shared self_attn runs both streams' self calls,
+        then both cross-modal calls, as ONE value projection, ONE query projection and ONE output
+        projection over all the rows (MSDeformAttn.forward_joint, one MSDA launch per call); the add +
+        LayerNorms and the FFN run once over all the rows.  Same math per row as ``forward_carry``
+        (reference :237-277): the cross calls' outputs come back in query row order, i.e. the video rows
+        hold audio_attended_visual and the audio rows visual_attended_audio, each stream's FFN input."""
+        src, value, query = stream
+        attn = self.self_attn.forward_joint(query, value, padding_mask, self_calls)
+        x16 = add_layer_norm_carry(src, attn, self.norm1, dropout=self.dropout1)[1]
+        # x16 is the cross calls' value and their query: both input gradients summed in one GEMM
+        mark_grad_sum(x16)
+        x = self.self_attn.forward_joint(x16, x16, padding_mask, cross_calls)
+        mark_grad_sum(x)  # (linear1's input and the add + LayerNorm's residual)
+        hidden = relu_dropout(self.linear1(x), self.activation, self.dropout2)
+        out, out16, q16 = add_layer_norm_carry(x, self.linear2(hidden), self.norm2, next_pos, self.dropout3,
+                                               pos_acc=pos_acc)
+        return out, out16, (q16 if q16 is not None else out16)
+
     def _self_block(self, src, pos, ref, shapes, starts, mask):
         """``norm1(src + dropout1(self_attn(src + pos, src)))`` as its bf16 copy (under bf16 autocast
         on the GPU, from the fused add + LayerNorm; else the fp32 tensor itself): its only
@@ -214,9 +235,14 @@ class MultimodalDeformableTransformerEncoder(nn.Module):
         video_ref = self.get_reference_points(video_temporal_shapes, video_valid_ratios, device=video_src.device)
         audio_ref = self.get_reference_points(audio_temporal_shapes, audio_valid_ratios, device=audio_src.device)
         output = video_src, audio_src
-        if (self.layers and all(type(layer) is MultimodalDeformableTransformerEncoderLayer for layer in self.layers)
-                and carry_supported(video_src, self.layers[0].norm2) and carry_supported(audio_src, self.layers[0].norm2)
-                and all(p is None or p.dtype == torch.float32 for p in (video_pos, audio_pos))):
+        carry = (self.layers and all(type(layer) is MultimodalDeformableTransformerEncoderLayer for layer in self.layers)
+                 and carry_supported(video_src, self.layers[0].norm2) and carry_supported(audio_src, self.layers[0].norm2)
+                 and all(p is None or p.dtype == torch.float32 for p in (video_pos, audio_pos)))
+        if carry and _joint_ok(self, video_src, audio_src, video_pos, audio_pos):
+            return self._forward_joint(video_src, video_temporal_shapes, video_level_start_index, video_pos,
+                                       video_padding_mask, video_ref, audio_src, audio_temporal_shapes,
+                                       audio_level_start_index, audio_pos, audio_padding_mask, audio_ref)
+        if carry:
             # bf16 MSDA operands carried from each layer's fused FFN add + LayerNorm to the next;
             # each pos's gradient summed in place by those fused backwards (add_norm.pos_sink)
             wp = MultimodalDeformableTransformerEncoderLayer.with_pos_embed
@@ -238,6 +264,79 @@ class MultimodalDeformableTransformerEncoder(nn.Module):
             output = layer(v, video_pos, video_ref, video_temporal_shapes, video_level_start_index, video_padding_mask,
                            a, audio_pos, audio_ref, audio_temporal_shapes, audio_level_start_index, audio_padding_mask)
         return output
+
+
+    def _forward_joint(self, video_src, video_temporal_shapes, video_level_start_index, video_pos, video_padding_mask,
+                       video_ref, audio_src, audio_temporal_shapes, audio_level_start_index, audio_pos,
+                       audio_padding_mask, audio_ref):
+        """The carried layers on the joint rows (``forward_joint``): both streams' rows and position
+        embeddings concatenated once (video first), split back into the two memories at the end."""
+        B, Sv, d = video_src.shape
+        Sa = audio_src.shape[1]
+        nv, na = B * Sv, B * Sa
+        v_shapes, v_starts = _msda.host_levels(video_temporal_shapes, video_level_start_index)
+        a_shapes, a_starts = _msda.host_levels(audio_temporal_shapes, audio_level_start_index)
+        src = torch.cat([video_src.reshape(nv, d), audio_src.reshape(na, d)])
+        pos = None if video_pos is None else torch.cat([video_pos.reshape(nv, d), audio_pos.reshape(na, d)])
+        mask = None
+        if video_padding_mask is not None or audio_padding_mask is not None:
+            vm = (video_padding_mask if video_padding_mask is not None
+                  else torch.zeros((B, Sv), dtype=torch.bool, device=video_src.device))
+            am = (audio_padding_mask if audio_padding_mask is not None
+                  else torch.zeros((B, Sa), dtype=torch.bool, device=audio_src.device))
+            mask = torch.cat([vm.reshape(nv), am.reshape(na)])
+        # (q0, q1, v0, v1, B, reference points, value level shapes, starts): video rows first
+        self_calls = ((0, nv, 0, nv, B, video_ref, v_shapes, v_starts),
+                      (nv, nv + na, nv, nv + na, B, audio_ref, a_shapes, a_starts))
+        cross_calls = ((0, nv, nv, nv + na, B, video_ref, a_shapes, a_starts),
+                       (nv, nv + na, 0, nv, B, audio_ref, v_shapes, v_starts))
+        pos, acc = pos_sink(pos)
+        wp = MultimodalDeformableTransformerEncoderLayer.with_pos_embed
+        stream = carry_entry(src, pos, acc) or (src, src, wp(src, pos))
+        for i, layer in enumerate(self.layers):
+            last = i + 1 == len(self.layers)
+            stream = layer.forward_joint(stream, None if last else pos, acc, self_calls, cross_calls, mask)
+        v_out, a_out = _SplitRows.apply(stream[0], nv, (B, Sv, d), (B, Sa, d))
+        v16, a16 = _SplitRows.apply(stream[1], nv, (B, Sv, d), (B, Sa, d))
+        v_out._mfl_bf16, a_out._mfl_bf16 = v16, a16  # bf16(out): the decoder's value projections read them
+        return v_out, a_out
+
+
+def _joint_ok(encoder, video_src, audio_src, video_pos, audio_pos):
+    """Whether the encoder runs both streams on joint rows (``_forward_joint``; MFL_MM_JOINT=0 keeps the
+    per-stream calls for A/B)."""
+    import os
+    if os.environ.get("MFL_MM_JOINT", "1") == "0":
+        return False
+    attn = encoder.layers[0].self_attn
+    return (video_src.dim() == 3 and audio_src.dim() == 3 and video_src.shape[0] == audio_src.shape[0]
+            and video_src.shape[2] == audio_src.shape[2] and video_src.dtype == audio_src.dtype == torch.float32
+            and (video_pos is None) == (audio_pos is None)
+            and all(p is None or p.shape == s.shape for p, s in ((video_pos, video_src), (audio_pos, audio_src)))
+            and joint_supported(attn, video_src.reshape(-1, video_src.shape[-1]),
+                                audio_src.reshape(-1, audio_src.shape[-1])))
+
+
+class _SplitRows(torch.autograd.Function):
+    """(x[:n] as shape_a, x[n:] as shape_b) of joint rows; backward ONE concatenation of the two
+    gradients (zeros for a part that got none) instead of autograd's two zero-filled full-size slice
+    gradients and their sum."""
+
+    @staticmethod
+    def forward(ctx, x, n, shape_a, shape_b):
+        ctx.set_materialize_grads(False)
+        ctx.n, ctx.shape, ctx.dtype = n, x.shape, x.dtype
+        return x[:n].view(shape_a), x[n:].view(shape_b)
+
+    @staticmethod
+    def backward(ctx, ga, gb):
+        if ga is None and gb is None:
+            return None, None, None, None
+        n, (R, d) = ctx.n, ctx.shape
+        ref = ga if ga is not None else gb
+        ga = ga.reshape(n, d) if ga is not None else ref.new_zeros((n, d))
+        gb = gb.reshape(R - n, d) if gb is not None else ref.new_zeros((R - n, d))
+        return torch.cat([ga, gb]), None, None, None
 
 
 class MultimodalDeformableTransformerDecoderLayer(nn.Module):

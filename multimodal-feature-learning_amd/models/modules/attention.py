@@ -35,7 +35,7 @@ from .linear import (Linear, _AutocastLinear, _accum_group, _addmm, _bias_grad, 
                      _weight_grad, grad_sum_mm, grad_sum_tagged, linear_pair)
 
 __all__ = ["MSDeformAttnFunction", "ms_deform_attn_core_pytorch", "MSDeformAttn", "CrossAttention",
-           "masked_scores_softmax", "mask_padding_rows", "mha_self_attention"]
+           "masked_scores_softmax", "mask_padding_rows", "mha_self_attention", "joint_supported"]
 
 
 def _loc5(sampling_locations):
@@ -113,32 +113,127 @@ class _QueryPrologue(torch.autograd.Function):
         nig = ctx.needs_input_grad
         g2, g_ref = _msda.prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, ctx.shapes, need_ref=nig[9],
                                                  layout=ctx.layout)
-        gx = grad_sum_mm(ctx.gsum, x2, g2, wc, ctx.x_shape) if nig[0] else None
-        wa, ba, wb, bb = ctx.params
-        na = wa.shape[0]
-        rest = (None, None, None, None, g_ref, None, None, None)
-        if all(nig[1:5]) and _defer((g2[:, :na], x2, wa, 0, ba), (g2[:, na:], x2, wb, 0, bb)):
-            return (gx, None, None, None, None) + rest
-        gwa = gwb = gba = gbb = None
-        # [W_off; W_aw] and [b_off; b_aw] lie back to back in the trainer's flat gradient buffer
-        # (flat_groups): the products are written straight into those views when they can be claimed
-        # (a module called several times in one backward — the multimodal encoder's shared
-        # self-attention: a later call adds its products into the view an earlier one claimed)
-        if nig[1] or nig[3]:
-            acc = _accum_group((wa, wb)) if nig[1] and nig[3] else None
-            if acc is not None:
-                _weight_grad(g2, x2, acc, accumulate=True)
-            else:
-                gw = _weight_grad(g2, x2, _claim_group((wa, wb)) if nig[1] and nig[3] else None)
-                gwa, gwb = gw[:na], gw[na:]
-        if nig[2] or nig[4]:
-            acc = _accum_group((ba, bb)) if nig[2] and nig[4] else None
-            if acc is not None:
-                _bias_grad(g2, acc, accumulate=True)
-            else:
-                gbias = _bias_grad(g2, _claim_group((ba, bb)) if nig[2] and nig[4] else None)
-                gba, gbb = gbias[:na], gbias[na:]
-        return (gx, gwa, gba, gwb, gbb) + rest
+        return _prologue_grads(ctx, nig, g2, x2, wc) + (None, None, None, None, g_ref, None, None, None)
+
+
+def _prologue_grads(ctx, nig, g2, x2, wc):
+    """(gx, g W_off, g b_off, g W_aw, g b_aw) of a query prologue from its [offsets | logits] rows' gradient
+    g2: one dgrad GEMM, the weight / bias products queued with the short-K layers' or written into the
+    trainer's flat views (_QueryPrologue, _QueryPrologueJoint)."""
+    gx = grad_sum_mm(ctx.gsum, x2, g2, wc, ctx.x_shape) if nig[0] else None
+    wa, ba, wb, bb = ctx.params
+    na = wa.shape[0]
+    if all(nig[1:5]) and _defer((g2[:, :na], x2, wa, 0, ba), (g2[:, na:], x2, wb, 0, bb)):
+        return (gx, None, None, None, None)
+    gwa = gwb = gba = gbb = None
+    # [W_off; W_aw] and [b_off; b_aw] lie back to back in the trainer's flat gradient buffer
+    # (flat_groups): the products are written straight into those views when they can be claimed
+    # (a module called several times in one backward — the multimodal encoder's shared
+    # self-attention: a later call adds its products into the view an earlier one claimed)
+    if nig[1] or nig[3]:
+        acc = _accum_group((wa, wb)) if nig[1] and nig[3] else None
+        if acc is not None:
+            _weight_grad(g2, x2, acc, accumulate=True)
+        else:
+            gw = _weight_grad(g2, x2, _claim_group((wa, wb)) if nig[1] and nig[3] else None)
+            gwa, gwb = gw[:na], gw[na:]
+    if nig[2] or nig[4]:
+        acc = _accum_group((ba, bb)) if nig[2] and nig[4] else None
+        if acc is not None:
+            _bias_grad(g2, acc, accumulate=True)
+        else:
+            gbias = _bias_grad(g2, _claim_group((ba, bb)) if nig[2] and nig[4] else None)
+            gba, gbb = gbias[:na], gbias[na:]
+    return (gx, gwa, gba, gwb, gbb)
+
+
+class _QueryPrologueJoint(torch.autograd.Function):
+    """_QueryPrologue over the rows of several MSDA calls of one module at once (the multimodal
+    encoder's video and audio streams, MSDeformAttn.forward_joint): ONE [offsets | logits] GEMM over
+    all the query rows, then each call's prologue on its row range (its reference points and its value
+    pyramid's level shapes); backward: each call's prologue backward into its rows of one gradient
+    buffer, ONE dgrad GEMM and one weight / bias product.  ``metas``: per call (q0, q1, B, Lq, shapes,
+    layout); ``refs``: the calls' reference points.  Returns loc_0, aw_0, loc_1, aw_1, ..."""
+
+    @staticmethod
+    def forward(ctx, x, wa, ba, wb, bb, wca, bca, wcb, bcb, dims, metas, *refs):
+        from ... import _trace
+        _trace.hit("query_prologue")
+        _trace.hit("query_prologue_joint")
+        M, L, P = dims
+        wc, bc = _rows_view(wca, wcb), _rows_view(bca, bcb)
+        x2 = x.reshape(-1, x.shape[-1])
+        y = _addmm(bc, x2, wc)
+        outs, saved = [], []
+        for (q0, q1, B, Lq, shapes, layout), ref in zip(metas, refs):
+            loc, aw = _msda.prologue_forward_rows(y[q0:q1], B, Lq, M, L, P, ref, shapes, layout)
+            outs += [loc, aw]
+            saved.append(aw)
+        ctx.save_for_backward(x2, wc, y, *saved, *refs)
+        ctx.metas, ctx.x_shape, ctx.n = metas, x.shape, len(metas)
+        ctx.gsum = grad_sum_tagged(x)
+        ctx.params = (wa, ba, wb, bb)
+        return tuple(outs)
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, *grads):
+        x2, wc, y = ctx.saved_tensors[:3]
+        n = ctx.n
+        aws, refs = ctx.saved_tensors[3:3 + n], ctx.saved_tensors[3 + n:]
+        nig = ctx.needs_input_grad
+        g2 = torch.empty_like(y)
+        g_refs = []
+        for i, (q0, q1, B, Lq, shapes, layout) in enumerate(ctx.metas):
+            _, g_ref = _msda.prologue_backward_rows(grads[2 * i], grads[2 * i + 1], aws[i], y[q0:q1], refs[i], shapes,
+                                                    need_ref=nig[11 + i], layout=layout, g2_out=g2[q0:q1])
+            g_refs.append(g_ref)
+        return _prologue_grads(ctx, nig, g2, x2, wc) + (None,) * 6 + tuple(g_refs)
+
+
+class _JointMSDA(torch.autograd.Function):
+    """Several MSDA calls on row ranges of ONE projected value (B rows first within each range) writing
+    row ranges of ONE output (MSDeformAttn.forward_joint): the calls' value ranges cover the value rows
+    once, so the backward writes every row of one grad_value (each call its range, no adds).  ``metas``:
+    per call (q0, q1, v0, v1, B, Lq, S, shapes, starts, layout); ``coords``: loc_0, aw_0, loc_1, aw_1, ..."""
+
+    @staticmethod
+    def forward(ctx, value, heads, n_rows, metas, *coords):
+        from ... import _trace
+        M, Dh = heads
+        out = torch.empty((n_rows, M * Dh), dtype=value.dtype, device=value.device)
+        tiles = []
+        for i, (q0, q1, v0, v1, B, Lq, S, shapes, starts, layout) in enumerate(metas):
+            _trace.hit("msda_" + str(value.dtype).replace("torch.", ""))
+            if layout == _msda.LEVEL_MAJOR:
+                _trace.hit("msda_level_major")
+            _, t = _msda.msda_forward(value[v0:v1].view(B, S, M, Dh), shapes, starts, coords[2 * i], coords[2 * i + 1],
+                                      "border", want_tiles=True, layout=layout, out=out[q0:q1].view(B, Lq, M * Dh))
+            tiles.append(t)
+        _trace.hit("msda_joint")
+        ctx.tiles, ctx.metas, ctx.heads = tiles, metas, heads
+        ctx.save_for_backward(value, *coords)
+        return out
+
+    @staticmethod
+    @once_differentiable
+    def backward(ctx, grad_out):
+        value, *coords = ctx.saved_tensors
+        M, Dh = ctx.heads
+        nig = ctx.needs_input_grad
+        gv = torch.empty_like(value) if nig[0] else None
+        grads = []
+        for i, (q0, q1, v0, v1, B, Lq, S, shapes, starts, layout) in enumerate(ctx.metas):
+            vi = value[v0:v1].view(B, S, M, Dh)
+            _, gl, ga = _msda.msda_backward(vi, shapes, starts, coords[2 * i], coords[2 * i + 1],
+                                            grad_out[q0:q1].view(B, Lq, M * Dh), "border", need_value=nig[0],
+                                            need_loc=nig[4 + 2 * i], need_aw=nig[5 + 2 * i], tiles=ctx.tiles[i],
+                                            layout=layout, gv_out=None if gv is None else gv[v0:v1].view(vi.shape))
+            grads += [gl, ga]
+        ctx.tiles = None
+        if gv is not None:
+            gv._mfl_private = True  # fresh, referenced by nothing else (attention.private_grad)
+        return (gv, None, None, None) + tuple(grads)
 
 
 class MSDeformAttn(nn.Module):
@@ -191,6 +286,10 @@ class MSDeformAttn(nn.Module):
         constant_(self.value_proj.bias.data, 0.)
         xavier_uniform_(self.output_proj.weight.data)
         constant_(self.output_proj.bias.data, 0.)
+
+    def forward_joint(self, query, value_in, padding_mask, calls):
+        """Several calls of this module on joint row tensors (``_forward_joint``)."""
+        return _forward_joint(self, query, value_in, padding_mask, calls)
 
     def forward(self, query, reference_points, input_flatten, input_spatial_shapes,
                 input_level_start_index, input_padding_mask=None, is_sparse=False, value=None):
@@ -291,6 +390,58 @@ class MSDeformAttn(nn.Module):
         if is_sparse:
             return output, sampling_locations.unsqueeze(-1), attention_weights
         return output
+
+
+def joint_supported(attn, query, value_in):
+    """Whether MSDeformAttn.forward_joint runs fused for these joint rows (bf16 autocast on the GPU, the
+    bf16 query prologue, D = d / M)."""
+    a, b = attn.sampling_offsets, attn.attention_weights
+    return (query.is_cuda and value_in.is_cuda and query.dim() == 2 and value_in.dim() == 2
+            and isinstance(a, Linear) and isinstance(b, Linear) and a.bias is not None and b.bias is not None
+            and a._autocast_dtype(query) == torch.bfloat16
+            and _msda.prologue_supported(attn.n_heads, attn.n_levels, attn.n_points))
+
+
+def _forward_joint(self, query, value_in, padding_mask, calls):
+    """Several calls of this module at once, on ONE tensor of query rows and ONE tensor of value-input
+    rows (the multimodal encoder's video and audio streams, models/deformable/multimodal_deformable_
+    transformer.py): ``value_proj`` and the masking once over all the value rows, the two query
+    projections as one GEMM over all the query rows (_QueryPrologueJoint), each call's MSDA on its row
+    ranges into one output (_JointMSDA), ``output_proj`` once.  The same arithmetic as one ``forward``
+    per call (reference attention.py:446-511; each GEMM output element is its own dot product).
+
+    query (Rq, C) bf16 rows, value_in (Rv, C) rows, padding_mask (Rv,) bool or None; ``calls``: per call
+    (q0, q1, v0, v1, B, reference_points (B, Lq, L, 1|2), level shapes, level starts) — query rows
+    [q0, q1) = B x Lq, value rows [v0, v1) = B x sum(shapes), the value ranges covering [0, Rv) once."""
+    M, L, P = self.n_heads, self.n_levels, self.n_points
+    Dh = self.d_model // M
+    value = self.value_proj(value_in)
+    if padding_mask is not None:
+        value = mask_padding_rows(value, padding_mask)
+    cover = sorted((c[2], c[3]) for c in calls)
+    if cover[0][0] != 0 or cover[-1][1] != value.shape[0] or any(x[1] != y[0] for x, y in zip(cover, cover[1:])):
+        raise ValueError("MSDeformAttn.forward_joint: the calls' value ranges must cover the value rows once")
+    a, b = self.sampling_offsets, self.attention_weights
+    dt = torch.bfloat16
+    wca, bca = a._low(dt)
+    wcb, bcb = b._low(dt)
+    if wca is None or wcb is None:
+        wca, bca, wcb, bcb = a.weight.to(dt), a.bias.to(dt), b.weight.to(dt), b.bias.to(dt)
+    pmetas, mmetas, refs = [], [], []
+    for q0, q1, v0, v1, B, ref, shapes, starts in calls:
+        shapes = tuple(int(t) for t in shapes)
+        starts = tuple(int(t) for t in starts)
+        Lq, S = (q1 - q0) // B, (v1 - v0) // B
+        layout = (_msda.LEVEL_MAJOR if torch.is_grad_enabled()
+                  and _msda.level_major_ok(value[v0:v1].view(B, S, M, Dh), shapes, Lq, P) else 0)
+        pmetas.append((q0, q1, B, Lq, shapes, layout))
+        mmetas.append((q0, q1, v0, v1, B, Lq, S, shapes, starts, layout))
+        refs.append(ref.float().contiguous())
+    with torch.autocast("cuda", enabled=False):
+        coords = _QueryPrologueJoint.apply(query.to(dt), a.weight, a.bias, b.weight, b.bias, wca, bca, wcb, bcb,
+                                           (M, L, P), tuple(pmetas), *refs)
+        out = _JointMSDA.apply(value.contiguous(), (M, Dh), query.shape[0], tuple(mmetas), *coords)
+    return self.output_proj(out)
 
 
 def private_grad(grad):

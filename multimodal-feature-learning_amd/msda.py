@@ -223,18 +223,23 @@ def _check_inputs(value, loc, aw, shapes, starts, layout=0):
         raise ValueError(f"levels {shapes} starting at {starts} exceed spatial size {S}")
 
 
-def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_tiles=False, layout=0):
+def msda_forward(value, shapes, starts, loc, aw, padding_mode="border", want_tiles=False, layout=0, out=None):
     """out (B, Lq, M*D) = MSDA(value (B,S,M,D), loc/aw (B,Lq,M,L,P)) on the HIP kernel.
 
     ``want_tiles``: also return the backward's row intervals when the call's backward takes the
     row-block path (``msda_hip_forward_tiles``; None otherwise): ``(out, tiles)``.
     ``layout=LEVEL_MAJOR``: loc / aw are (B, M, L, Lq, P) (``msda_hip_forward_tiles_layout``; the
-    call must satisfy ``level_major_ok``; tiles are always written)."""
+    call must satisfy ``level_major_ok``; tiles are always written).  ``out``: a contiguous
+    (B, Lq, M*D) tensor of value's dtype to write into (a row range of a joint output)."""
     _check_inputs(value, loc, aw, shapes, starts, layout)
     lib = _native.load_library()
     B, S, M, D = value.shape
     Lq, _, L, P = _coord_dims(loc, layout)
-    out = torch.empty((B, Lq, M * D), dtype=value.dtype, device=value.device)
+    if out is None:
+        out = torch.empty((B, Lq, M * D), dtype=value.dtype, device=value.device)
+    elif (tuple(out.shape) != (B, Lq, M * D) or out.dtype != value.dtype or not out.is_contiguous()
+          or out.device != value.device):
+        raise ValueError(f"MSDA: out must be a contiguous {(B, Lq, M * D)} {value.dtype} tensor")
     tiles = None
     if want_tiles or layout == LEVEL_MAJOR:
         nb = lib.msda_hip_forward_tiles_bytes(_native.DTYPE_TAGS[value.dtype], _native.host_i64_array(shapes), L,
@@ -279,13 +284,15 @@ def _strided_slot(dest, value):
 
 
 def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="border",
-                  need_value=True, need_loc=True, need_aw=True, tiles=None, layout=0, grad_value_out=None):
+                  need_value=True, need_loc=True, need_aw=True, tiles=None, layout=0, grad_value_out=None,
+                  gv_out=None):
     """(grad_value, grad_loc, grad_aw) of msda_forward; unneeded ones come back None.
     ``tiles``: the row intervals ``msda_forward(..., want_tiles=True)`` returned for these inputs
     (required with ``layout=LEVEL_MAJOR``; grad_loc / grad_aw then come back level-major too).
     ``grad_value_out``: a strided (B, S, M, D) slot to write grad_value into (msda_hip_backward_ex;
     the decoder layers' stacked value gradients): returned as grad_value when the call's kernel path
-    writes it, else ignored (a fresh grad_value comes back)."""
+    writes it, else ignored (a fresh grad_value comes back).  ``gv_out``: a contiguous tensor of value's
+    shape and dtype the other paths write grad_value into (a row range of a joint value's gradient)."""
     rs = _strided_slot(grad_value_out, value) if need_value and layout == 0 and tiles is None else 0
     if rs:
         rc_ex = _backward_ex(value, shapes, starts, loc, aw, grad_output, padding_mode, need_loc, need_aw,
@@ -293,7 +300,7 @@ def msda_backward(value, shapes, starts, loc, aw, grad_output, padding_mode="bor
         if rc_ex is not None:
             return rc_ex
     return _backward(value, shapes, starts, loc, aw, grad_output, padding_mode, need_value, need_loc, need_aw,
-                     tiles, layout)
+                     tiles, layout, gv_out)
 
 
 def _backward_ex(value, shapes, starts, loc, aw, grad_output, padding_mode, need_loc, need_aw, gv, rs):
@@ -333,7 +340,7 @@ def _backward_ex(value, shapes, starts, loc, aw, grad_output, padding_mode, need
 
 
 def _backward(value, shapes, starts, loc, aw, grad_output, padding_mode, need_value, need_loc, need_aw, tiles,
-              layout):
+              layout, gv_out=None):
     _check_inputs(value, loc, aw, shapes, starts, layout)
     grad_output = grad_output.to(value.dtype).contiguous()
     B, S, M, D = value.shape
@@ -341,7 +348,12 @@ def _backward(value, shapes, starts, loc, aw, grad_output, padding_mode, need_va
     if tuple(grad_output.shape) != (B, Lq, M * D):
         raise ValueError(f"grad_output must be {(B, Lq, M * D)}, got {tuple(grad_output.shape)}")
     lib = _native.load_library()
-    gv = torch.empty_like(value) if need_value else None
+    if need_value and gv_out is not None:
+        if gv_out.shape != value.shape or gv_out.dtype != value.dtype or not gv_out.is_contiguous():
+            raise ValueError(f"MSDA: gv_out must be a contiguous {tuple(value.shape)} {value.dtype} tensor")
+        gv = gv_out
+    else:
+        gv = torch.empty_like(value) if need_value else None
     gl = torch.empty_like(loc) if need_loc else None
     ga = torch.empty_like(aw) if need_aw else None
     ws = None
@@ -519,9 +531,10 @@ def prologue_forward_rows(y, B, Lq, M, L, P, ref, shapes, layout=0):
     return loc, aw
 
 
-def prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, shapes, need_ref=True, layout=0):
+def prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, shapes, need_ref=True, layout=0, g2_out=None):
     """``prologue_backward`` into ONE (B*Lq, 2*M*L*P) buffer of [grad offsets | grad logits] rows
-    (the dgrad GEMM's input) -> (g2, grad_ref or None); grad_loc / grad_aw / aw in ``layout``."""
+    (the dgrad GEMM's input) -> (g2, grad_ref or None); grad_loc / grad_aw / aw in ``layout``.
+    ``g2_out``: a contiguous tensor like y to write into (a row range of a joint buffer)."""
     B = aw.shape[0]
     Lq, M, L, P = _coord_dims(aw, layout)
     n = M * L * P
@@ -529,7 +542,12 @@ def prologue_backward_rows(grad_loc, grad_aw, aw, y, ref, shapes, need_ref=True,
     lib = _native.load_library()
     grad_loc = torch.zeros_like(aw) if grad_loc is None else grad_loc.to(cd).contiguous()
     grad_aw = torch.zeros_like(aw) if grad_aw is None else grad_aw.to(cd).contiguous()
-    g2 = torch.empty_like(y)
+    if g2_out is not None:
+        if g2_out.shape != y.shape or g2_out.dtype != y.dtype or not g2_out.is_contiguous():
+            raise ValueError(f"MSDA prologue rows: g2_out must be a contiguous {tuple(y.shape)} {y.dtype} tensor")
+        g2 = g2_out
+    else:
+        g2 = torch.empty_like(y)
     g_ref = torch.empty_like(ref) if need_ref else None
     base, ybase = g2.data_ptr(), y.data_ptr()
     rc = lib.msda_hip_prologue_backward_layout(

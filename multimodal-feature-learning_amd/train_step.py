@@ -33,7 +33,6 @@ the MI355X the way the hardware wants it:
 """
 import os
 import time
-import warnings
 
 import torch
 import torch.distributed as dist
@@ -81,23 +80,23 @@ _CAPTURE_GROUPS = {}
 
 def _capture_group(pg, device):
     """The process group the captured bucket all-reduces run on: the trainer's group's ranks again, as a
-    group used ONLY inside graph captures (one per (group, device) for the process).
+    group whose collectives run only inside graph captures after its first one (one per (group, device)
+    for the process).
 
     The RCCL process group's watchdog thread polls the end event of every eager collective
     (WorkNCCL::isCompleted -> hipEventQuery) until it retires it, ~100 ms later.  HIP refuses that query
-    (hipErrorCapturedEvent) whenever the stream the event was recorded on is capturing at the time of
-    the query — even for an event recorded and completed before the capture began
-    (tools/probes/event_capture_probe.py) — and the watchdog takes the refusal as fatal.  Captured
+    (hipErrorCapturedEvent, and invalidates the capture) whenever the stream the event was recorded on
+    is capturing at the time of the query — even for an event recorded and completed before the capture
+    began (tools/probes/event_capture_probe.py) — and the watchdog takes the refusal as fatal.  Captured
     collectives join their group's NCCL stream into the capture, so captured and eager collectives on
     one group abort the process whenever a poll of a not-yet-retired eager collective falls inside the
-    capture (the warm-up steps' collectives right before it).  This group never runs an eager collective:
-    its communicator is connected eagerly (device_id) and its first collective runs inside a throwaway
-    relaxed-mode capture, so its watchdog never holds a Work.  Its NCCL stream comes from the
+    capture.  This group runs one eager collective, right here (its communicator's
+    connections), which capture() waits to see retired (_drain_watchdogs) before it captures; the
+    trainer's eager steps keep using the trainer's own group.  Its NCCL stream comes from the
     high-priority pool, apart from the default group's and torch's default-priority streams."""
     key = (id(pg), device.index)
     entry = _CAPTURE_GROUPS.get(key)
     if entry is None:
-        from . import _native
         ranks = dist.get_process_group_ranks(pg if pg is not None else dist.group.WORLD)
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
@@ -107,24 +106,18 @@ def _capture_group(pg, device):
                 "groups are created (the package sets it at import: import it before init_process_group); with the "
                 "cache a captured collective's end event reaches an eager collective and the RCCL watchdog aborts")
         grp = dist.new_group(ranks, backend="nccl", pg_options=opts, device_id=device)
-        _drain_watchdogs(exclude=(grp,))
         buf = torch.zeros(64, dtype=torch.float32, device=device)
-        stream = _native.own_stream(device, "capture")
-        stream.wait_stream(torch.cuda.current_stream(device))
-        g = torch.cuda.CUDAGraph()
-        with warnings.catch_warnings():
-            warnings.filterwarnings("ignore", message="The CUDA Graph is empty")  # (one rank: nothing to reduce)
-            with torch.cuda.graph(g, stream=stream, capture_error_mode="relaxed"):
-                dist.all_reduce(buf, group=grp)
-        g.replay()
+        dist.all_reduce(buf, group=grp)  # (connects the communicator)
         torch.cuda.synchronize(device)
-        entry = _CAPTURE_GROUPS[key] = (grp, g, buf)  # (the warm graph and its buffer stay alive)
+        _drain_watchdogs(only=(grp,))  # this group's one eager collective retired: it never polls again
+        entry = _CAPTURE_GROUPS[key] = (grp,)
     return entry[0]
 
 
-def _drain_watchdogs(exclude=(), timeout_s=120.0):
-    """Wait until the RCCL watchdogs have retired every collective they poll (except those of the groups
-    in ``exclude``), read from the flight recorder's record of which collectives are still active.
+def _drain_watchdogs(exclude=(), only=None, timeout_s=120.0):
+    """Wait until the RCCL watchdogs have retired every collective they poll (of the groups in ``only``,
+    or of all groups but those in ``exclude``), read from the flight recorder's record of which
+    collectives are still active.
 
     A graph capture must not begin while the watchdog of a group still holds one of its eager
     collectives: HIP refuses hipEventQuery of an event whose stream joins a capture, and the watchdog
@@ -136,11 +129,14 @@ def _drain_watchdogs(exclude=(), timeout_s=120.0):
         raise RuntimeError("FlatGradTrainer: captured RCCL collectives need TORCH_NCCL_TRACE_BUFFER_SIZE > 0 when the "
                            "process groups are created (the package sets it at import: import it before "
                            "init_process_group)")
-    skip = {dist.distributed_c10d._get_process_group_name(g) for g in exclude}
+    name = dist.distributed_c10d._get_process_group_name
+    skip = {name(g) for g in exclude}
+    keep = None if only is None else {name(g) for g in only}
     t0 = time.monotonic()
     while True:
         dump = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
-        active = [e for e in dump.get("entries", []) if (e.get("process_group") or [None])[0] not in skip]
+        active = [e for e in dump.get("entries", []) if (e.get("process_group") or [None])[0] not in skip
+                  and (keep is None or (e.get("process_group") or [None])[0] in keep)]
         if not active:
             return
         if time.monotonic() - t0 > timeout_s:

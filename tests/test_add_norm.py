@@ -375,6 +375,7 @@ def test_multimodal_encoder_carry_matches_uncarried(dev, monkeypatch):
         return (ov.detach(), oa.detach()), [v.grad, a.grad, vp.grad, ap.grad] + [
             p.grad.clone() for p in enc.parameters()]
 
+    monkeypatch.setenv("MFL_MM_JOINT", "0")  # the per-stream carried layers (the joint rows: the next test)
     o1, g1 = run()
     monkeypatch.setattr(MT, "carry_supported", lambda *a: False)
     o2, g2 = run()
@@ -383,6 +384,62 @@ def test_multimodal_encoder_carry_matches_uncarried(dev, monkeypatch):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
     for a, b, c in zip(g1, g2, g3):
         torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -7 * b.abs().max().item())
+        assert (a - c).norm() <= 1.25 * (b - c).norm() + 1e-6 * c.norm()
+
+
+@pytest.mark.gpu
+def test_multimodal_encoder_joint_rows_match_per_stream(dev, monkeypatch):
+    """The multimodal encoder on joint rows (MultimodalDeformableTransformerEncoder._forward_joint: both
+    streams' rows in one tensor; per layer ONE value / query / output projection of the shared self_attn
+    for the two self calls and ONE for the two cross-modal calls, one MSDA launch per call, the add +
+    LayerNorms and the FFN once over all rows) against the per-stream carried layers.  A GEMM over more
+    rows may pick another kernel (another bf16 rounding), so both are held to the fp32 run of the same
+    stack: outputs and gradients (inputs, positional embeddings, every parameter) no further from it than
+    the per-stream path (x1.25), and the two within bf16-ulp tolerance of each other; the joint path's
+    launches asserted by trace."""
+    MT = PKG.models.deformable.multimodal_deformable_transformer
+    torch.manual_seed(4)
+    B, d, vs, as_ = 2, 512, [128, 64, 32, 16], [50, 25, 13, 7]
+    layer = MT.MultimodalDeformableTransformerEncoderLayer(d, 1024, 0.0, "relu", 4, 8, 4)
+    enc = MT.MultimodalDeformableTransformerEncoder(layer, 3).to(dev)
+
+    def meta(shapes):
+        ts = torch.tensor(shapes, device=dev)
+        return ts, torch.cat([ts.new_zeros(1), ts.cumsum(0)[:-1]])
+    vts, vlsi = meta(vs)
+    ats, alsi = meta(as_)
+    ones = torch.ones(B, 4, device=dev)
+    v0, a0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
+    vp0, ap0 = torch.randn(B, sum(vs), d, device=dev), torch.randn(B, sum(as_), d, device=dev)
+    vmask = torch.zeros(B, sum(vs), dtype=torch.bool, device=dev)
+    amask = torch.zeros(B, sum(as_), dtype=torch.bool, device=dev)
+    for l, (t, s0) in enumerate(zip(vs, vlsi.tolist())):
+        vmask[1, s0 + (3 * t) // 4:s0 + t] = True
+    for l, (t, s0) in enumerate(zip(as_, alsi.tolist())):
+        amask[1, s0 + (3 * t) // 4:s0 + t] = True
+    vr = torch.tensor([[1.0] * 4, [0.75] * 4], device=dev)
+    wv, wa = torch.randn(d, device=dev), torch.randn(d, device=dev)
+
+    def run(amp=True):
+        enc.zero_grad(set_to_none=True)
+        v, a = v0.clone().requires_grad_(True), a0.clone().requires_grad_(True)
+        vp, ap = vp0.clone().requires_grad_(True), ap0.clone().requires_grad_(True)
+        PKG._trace.clear()
+        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=amp):
+            ov, oa = enc(v, vts, vlsi, vr, vp, vmask, a, ats, alsi, vr, ap, amask)
+        hits = dict(PKG._trace.hits)
+        (ov.float() * wv).sum().add_((oa.float() * wa).sum()).backward()
+        return [ov.detach().float(), oa.detach().float()], [v.grad, a.grad, vp.grad, ap.grad] + [
+            p.grad.clone() for p in enc.parameters()], hits
+
+    o1, g1, hits = run()
+    assert hits.get("msda_joint", 0) == 6 and hits.get("query_prologue_joint", 0) == 6, hits
+    monkeypatch.setenv("MFL_MM_JOINT", "0")
+    o2, g2, hits2 = run()
+    assert hits2.get("msda_joint", 0) == 0, hits2
+    o3, g3, _ = run(amp=False)
+    for a, b, c in zip(o1 + g1, o2 + g2, o3 + g3):
+        torch.testing.assert_close(a, b, rtol=2 ** -6, atol=2 ** -6 * b.abs().max().item())
         assert (a - c).norm() <= 1.25 * (b - c).norm() + 1e-6 * c.norm()
 
 

@@ -52,13 +52,13 @@ def main():
     ts = pkg.train_step
     orig_drain = ts._drain_watchdogs
 
-    def drain(exclude=(), timeout_s=120.0):
+    def drain(exclude=(), only=None, timeout_s=120.0):
         import json
         import time
         from torch._C._distributed_c10d import _dump_nccl_trace_json
         n = len(json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True)).get("entries", []))
         t0 = time.monotonic()
-        orig_drain(exclude, timeout_s)
+        orig_drain(exclude, only, timeout_s)
         print(f"  drain: {n} active entries, waited {1e3 * (time.monotonic() - t0):.1f} ms", flush=True)
 
     ts._drain_watchdogs = drain
