@@ -38,7 +38,8 @@ _os.environ.setdefault(_EVENT_CACHE_VAR, "0")
 # Also read at ProcessGroupNCCL construction: the flight recorder, whose record of which collectives the
 # watchdog has retired lets FlatGradTrainer.capture() wait until no eager collective is left for the
 # watchdog to poll before it captures (train_step._drain_watchdogs)
-_os.environ.setdefault("TORCH_NCCL_TRACE_BUFFER_SIZE", "2048")
+if "TORCH_NCCL_TRACE_BUFFER_SIZE" not in _os.environ:  # (its older name, still honoured)
+    _os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "2048")
 
 
 def graph_packet_capture_off():

@@ -125,10 +125,11 @@ def _drain_watchdogs(exclude=(), only=None, timeout_s=120.0):
     poll (~100 ms); this waits for exactly that condition instead of sleeping."""
     import json
     from torch._C._distributed_c10d import _dump_nccl_trace_json
-    if int(os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE", "0") or 0) <= 0:
-        raise RuntimeError("FlatGradTrainer: captured RCCL collectives need TORCH_NCCL_TRACE_BUFFER_SIZE > 0 when the "
-                           "process groups are created (the package sets it at import: import it before "
-                           "init_process_group)")
+    size = os.environ.get("TORCH_FR_BUFFER_SIZE") or os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE") or "0"
+    if int(size) <= 0:
+        raise RuntimeError("FlatGradTrainer: captured RCCL collectives need the flight recorder (TORCH_FR_BUFFER_SIZE "
+                           "> 0) when the process groups are created (the package sets it at import: import it "
+                           "before init_process_group)")
     name = dist.distributed_c10d._get_process_group_name
     skip = {name(g) for g in exclude}
     keep = None if only is None else {name(g) for g in only}
