@@ -30,16 +30,10 @@ _HIP_UP_AT_IMPORT = _torch.cuda.is_initialized()
 _PACKET_CAPTURE_AT_IMPORT = _os.environ.get(_PACKET_CAPTURE_VAR)
 _os.environ.setdefault(_PACKET_CAPTURE_VAR, "0")
 # Read when a ProcessGroupNCCL is constructed: its per-device event cache hands the end event of a
-# collective captured in a HIP graph to a later eager collective of ANY group, and HIP keeps treating
-# that event as the captured stream's (hipEventQuery refuses it while that stream captures again), which
-# the RCCL watchdog takes as fatal (train_step._capture_group)
+# collective captured in a HIP graph to a later eager collective; kept off, so an event the RCCL watchdog
+# polls has only ever been recorded on the eager collectives' stream (train_step._capture_group)
 _EVENT_CACHE_VAR = "TORCH_NCCL_CUDA_EVENT_CACHE"
 _os.environ.setdefault(_EVENT_CACHE_VAR, "0")
-# Also read at ProcessGroupNCCL construction: the flight recorder, whose record of which collectives the
-# watchdog has retired lets FlatGradTrainer.capture() wait until no eager collective is left for the
-# watchdog to poll before it captures (train_step._drain_watchdogs)
-if "TORCH_NCCL_TRACE_BUFFER_SIZE" not in _os.environ:  # (its older name, still honoured)
-    _os.environ.setdefault("TORCH_FR_BUFFER_SIZE", "2048")
 
 
 def graph_packet_capture_off():

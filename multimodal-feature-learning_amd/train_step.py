@@ -80,71 +80,30 @@ _CAPTURE_GROUPS = {}
 
 def _capture_group(pg, device):
     """The process group the captured bucket all-reduces run on: the trainer's group's ranks again, as a
-    group whose collectives run only inside graph captures after its first one (one per (group, device)
-    for the process).
+    group that runs nothing eagerly but its first collective (one per (group, device) for the process).
 
     The RCCL process group's watchdog thread polls the end event of every eager collective
     (WorkNCCL::isCompleted -> hipEventQuery) until it retires it, ~100 ms later.  HIP refuses that query
     (hipErrorCapturedEvent, and invalidates the capture) whenever the stream the event was recorded on
     is capturing at the time of the query — even for an event recorded and completed before the capture
-    began (tools/probes/event_capture_probe.py) — and the watchdog takes the refusal as fatal.  Captured
-    collectives join their group's NCCL stream into the capture, so captured and eager collectives on
-    one group abort the process whenever a poll of a not-yet-retired eager collective falls inside the
-    capture.  This group runs one eager collective, right here (its communicator's
-    connections), which capture() waits to see retired (_drain_watchdogs) before it captures; the
-    trainer's eager steps keep using the trainer's own group.  Its NCCL stream comes from the
-    high-priority pool, apart from the default group's and torch's default-priority streams."""
+    began (tools/probes/event_capture_probe.py) — and the watchdog takes the refusal as fatal.  A
+    blocking collective runs on, and records its end event on, the CURRENT stream; so no stream that
+    carries an eager collective may ever capture: the trainer's warm-up, its captures, its
+    eager and its captured bucket collectives each run on a stream of their own (``_native.own_stream``),
+    and the captured collectives on this group, whose NCCL stream (high-priority pool) no eager
+    collective of the trainer's group uses.  Its first collective, which connects the communicator, runs
+    eagerly on the caller's current stream, which never captures."""
     key = (id(pg), device.index)
-    entry = _CAPTURE_GROUPS.get(key)
-    if entry is None:
+    grp = _CAPTURE_GROUPS.get(key)
+    if grp is None:
         ranks = dist.get_process_group_ranks(pg if pg is not None else dist.group.WORLD)
         opts = dist.ProcessGroupNCCL.Options()
         opts.is_high_priority_stream = True
-        if os.environ.get("TORCH_NCCL_CUDA_EVENT_CACHE") != "0":
-            raise RuntimeError(
-                "FlatGradTrainer: captured RCCL collectives need TORCH_NCCL_CUDA_EVENT_CACHE=0 when the process "
-                "groups are created (the package sets it at import: import it before init_process_group); with the "
-                "cache a captured collective's end event reaches an eager collective and the RCCL watchdog aborts")
         grp = dist.new_group(ranks, backend="nccl", pg_options=opts, device_id=device)
-        buf = torch.zeros(64, dtype=torch.float32, device=device)
-        dist.all_reduce(buf, group=grp)  # (connects the communicator)
+        dist.all_reduce(torch.zeros(64, dtype=torch.float32, device=device), group=grp)  # (connects it)
         torch.cuda.synchronize(device)
-        _drain_watchdogs(only=(grp,))  # this group's one eager collective retired: it never polls again
-        entry = _CAPTURE_GROUPS[key] = (grp,)
-    return entry[0]
-
-
-def _drain_watchdogs(exclude=(), only=None, timeout_s=120.0):
-    """Wait until the RCCL watchdogs have retired every collective they poll (of the groups in ``only``,
-    or of all groups but those in ``exclude``), read from the flight recorder's record of which
-    collectives are still active.
-
-    A graph capture must not begin while the watchdog of a group still holds one of its eager
-    collectives: HIP refuses hipEventQuery of an event whose stream joins a capture, and the watchdog
-    takes the refusal as fatal (_capture_group).  The watchdog retires a finished collective on its next
-    poll (~100 ms); this waits for exactly that condition instead of sleeping."""
-    import json
-    from torch._C._distributed_c10d import _dump_nccl_trace_json
-    size = os.environ.get("TORCH_FR_BUFFER_SIZE") or os.environ.get("TORCH_NCCL_TRACE_BUFFER_SIZE") or "0"
-    if int(size) <= 0:
-        raise RuntimeError("FlatGradTrainer: captured RCCL collectives need the flight recorder (TORCH_FR_BUFFER_SIZE "
-                           "> 0) when the process groups are created (the package sets it at import: import it "
-                           "before init_process_group)")
-    name = dist.distributed_c10d._get_process_group_name
-    skip = {name(g) for g in exclude}
-    keep = None if only is None else {name(g) for g in only}
-    t0 = time.monotonic()
-    while True:
-        dump = json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True))
-        active = [e for e in dump.get("entries", []) if (e.get("process_group") or [None])[0] not in skip
-                  and (keep is None or (e.get("process_group") or [None])[0] in keep)]
-        if not active:
-            return
-        if time.monotonic() - t0 > timeout_s:
-            raise RuntimeError(f"FlatGradTrainer.capture: {len(active)} collectives not retired by the RCCL watchdog "
-                               f"after {timeout_s:.0f} s (first: {active[0].get('profiling_name')}, "
-                               f"state {active[0].get('state')})")
-        time.sleep(0.005)
+        _CAPTURE_GROUPS[key] = grp
+    return grp
 
 
 def _record(events):
@@ -366,14 +325,15 @@ class FlatGradTrainer:
         if self._overlap_now:
             cur = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
             if cur is not None:
-                if self._comm_stream is None:
-                    from . import _native
-                    self._comm_stream = _native.own_stream(self.device, "comm")  # (never a pool stream, _capture_group)
+                from . import _native
+                # eager and captured collectives on streams of their own, the captured ones on the
+                # capture-only group: no stream that carries an eager collective ever captures
+                # (_capture_group)
+                captured = self._capturing_now and self._capture_pg is not None
+                self._comm_stream = _native.own_stream(self.device, "comm_capture" if captured else "comm")
                 self._comm_stream.wait_stream(cur)
-                # inside capture() the collectives go to the capture-only group (_capture_group)
-                group = self._capture_pg if self._capturing_now and self._capture_pg is not None else self.pg
                 with torch.cuda.stream(self._comm_stream):
-                    dist.all_reduce(self.flat_grad[start:end], group=group)
+                    dist.all_reduce(self.flat_grad[start:end], group=self._capture_pg if captured else self.pg)
             else:
                 self._works.append(dist.all_reduce(self.flat_grad[start:end], group=self.pg, async_op=True))
 
@@ -634,24 +594,25 @@ class FlatGradTrainer:
                 "eager work produced corrupted gradients (DESIGN.md §6)")
         from . import _native
         # the warm-up and the captures run on the package's own stream: never a pool stream that the
-        # RCCL process group's NCCL stream can be (_capture_group)
+        # RCCL process group's NCCL stream can be; the warm-up's eager collectives on another stream than
+        # the captures (_capture_group)
         side = _native.own_stream(self.device, "capture")
-        side.wait_stream(torch.cuda.current_stream(self.device))
-        with torch.cuda.stream(side):
+        warm = _native.own_stream(self.device, "warmup")
+        warm.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(warm):
             for _ in range(warmup):
                 self.eager_step(batch)
-        torch.cuda.current_stream(self.device).wait_stream(side)
+        torch.cuda.current_stream(self.device).wait_stream(warm)
         torch.cuda.synchronize(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
         # capture_error_mode "thread_local": the RCCL process group's watchdog thread polls the
         # events of the warm-up collectives (hipEventQuery) while this thread captures; under the
-        # default global mode that poll is refused.  The captured collectives themselves run on a
-        # group of their own (_capture_group), whose NCCL stream no eager collective ever used
+        # default global mode that poll is refused.  Those events sit on streams that never capture,
+        # and the captured collectives run on a group of their own (_capture_group)
         pool = None
         if (self.overlap and self.capture_collectives and not self._late_global and dist.is_available()
                 and dist.is_initialized() and dist.get_backend(self.pg) == "nccl"):
             self._capture_pg = _capture_group(self.pg, self.device)
-            # no eager collective (the warm-up's) left for a watchdog to poll during the captures
-            _drain_watchdogs(exclude=(self._capture_pg,))
         if self.staged:
             # graph A: the forward up to the host step and the copy of its request into pinned
             # host memory; graph B (same memory pool) runs the rest of the forward and the whole

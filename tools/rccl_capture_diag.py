@@ -49,19 +49,6 @@ def main():
         return orig(self, b)
 
     T._flush_bucket = flush
-    ts = pkg.train_step
-    orig_drain = ts._drain_watchdogs
-
-    def drain(exclude=(), only=None, timeout_s=120.0):
-        import json
-        import time
-        from torch._C._distributed_c10d import _dump_nccl_trace_json
-        n = len(json.loads(_dump_nccl_trace_json(includeCollectives=True, onlyActive=True)).get("entries", []))
-        t0 = time.monotonic()
-        orig_drain(exclude, only, timeout_s)
-        print(f"  drain: {n} active entries, waited {1e3 * (time.monotonic() - t0):.1f} ms", flush=True)
-
-    ts._drain_watchdogs = drain
     small = dict(d_model=64, num_queries=6, feature_dim=64, enc_layers=2, dec_layers=2, ff_dim=128, dropout=0.0)
     torch.manual_seed(0)
     base = pkg.dvc_core.DeformableDVCCore(**small)
