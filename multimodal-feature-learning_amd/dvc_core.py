@@ -25,7 +25,7 @@ from .utils.dam import attn_map_to_flat_grid
 from .models.modules.linear import Linear
 
 __all__ = ["DeformableDVCCore", "MultimodalDVCCore", "SparseDVCCore", "synthetic_clips", "workload_loss",
-           "multimodal_workload_loss", "sparse_workload_loss", "StagedDVCLoss"]
+           "multimodal_workload_loss", "sparse_workload_loss", "StagedDVCLoss", "level_terms"]
 
 
 class DeformableDVCCore(nn.Module):
@@ -286,6 +286,40 @@ def synthetic_dvc_batch(batch, T=1024, feature_dim=512, vocab_size=10000, seq_le
             'video_target': targets, 'cap_tensor': cap.to(device), 'cap_mask': (cap == 1).to(device)}
 
 
+def level_terms(levels, lidx, tgt_seg, n_events, words, live, live_sum):
+    """The per-level terms of ``dvc_workload_loss`` summed over every decoder level at once: the heads
+    stacked over the levels (``levels['segments' / 'logits' / 'counts']``, (L, B, Q, .), as
+    misc_modules.level_heads makes them) and the levels' caption probabilities stacked along the
+    segments (``levels['captions']``, (L n, W, V), the one caption decoder call), with ``lidx`` (L, 2, n)
+    the (clip, prediction) pairs matched at each level.  Per level the same terms as the loop — L1 of the
+    matched segments (x5), -log p(label) (x1), the count head's cross-entropy (x2), the captions' -log
+    p(word) over non-pad words — each gather / reduction one launch for all levels instead of one per
+    level (the loss had ~50 launches a level each way at the DVC bench shape)."""
+    import torch.nn.functional as F
+    L, n = lidx.shape[0], lidx.shape[2]
+    lv = torch.arange(L, device=lidx.device)[:, None].expand(L, n)
+    b, s = lidx[:, 0], lidx[:, 1]
+    total = 5 * (levels['segments'][lv, b, s].float() - tgt_seg).abs().mean(dim=(1, 2)).sum()
+    total = total - torch.log(levels['logits'][lv, b, s, 0].float().clamp_min(1e-9)).mean(dim=1).sum()
+    counts = levels['counts']
+    C = counts.shape[-1]
+    ce = F.cross_entropy(counts.float().reshape(-1, C), n_events.clamp_max(C - 1).repeat(L), reduction='none')
+    total = total + 2 * ce.view(L, -1).mean(dim=1).sum()
+    caps = levels.get('captions')
+    if caps is not None:
+        p = word_probs(caps, words.repeat(L, 1))
+        total = total - (torch.log(p.clamp_min(1e-9)) * live.repeat(L, 1)).view(L, -1).sum(dim=1).div(live_sum).sum()
+    return total
+
+
+def _stacked_levels(out):
+    """``out['_levels']`` when it covers every level the loss reads (the aux levels present), else None."""
+    lv = out.get('_levels')
+    if lv is None or len(out.get('aux_outputs', [])) + 1 != lv['segments'].shape[0]:
+        return None
+    return lv
+
+
 def dvc_workload_loss(result, obj):
     """A loss over every output of UnimodalDeformableDVC's training forward, shaped like the
     reference criterion's terms (models/criterion.py, coefficients of config_dvc_train.py): L1 of
@@ -301,6 +335,16 @@ def dvc_workload_loss(result, obj):
     live = (~obj['cap_mask'][:, 1:]).float()
     n_events = torch.tensor([len(t['segments']) for t in obj['video_target']], device=dev)
     total = 0.0
+    stacked = _stacked_levels(out)
+    if stacked is not None:
+        # every level at once (level_terms): level l's pairs, the last level's being ``indices``
+        lidx = torch.stack([torch.stack([t.to(dev) for t in get_src_permutation_idx(ind)])
+                            for ind in list(indices_aux) + [indices]])
+        total = level_terms(stacked, lidx, tgt_seg, n_events, words, live, live.sum())
+        if 'pred_memory_mask' in out:
+            total = total + 3 * F.binary_cross_entropy_with_logits(out['pred_memory_mask'].float(),
+                                                                  (out['pred_memory_mask'].detach() > 0).float())
+        return total
     levels = [(out, indices)] + list(zip(out.get('aux_outputs', []), indices_aux))
     for o, ind in levels:
         bidx, sidx = (t.to(dev) for t in get_src_permutation_idx(ind))
@@ -394,6 +438,14 @@ class StagedDVCLoss:
         import torch.nn.functional as F
         out = result[0]
         total = 0.0
+        stacked = _stacked_levels(out)
+        if stacked is not None:
+            total = level_terms(stacked, self.idx_dev, self.tgt_seg, self.n_events, self.words, self.live,
+                                self.live_sum)
+            if 'pred_memory_mask' in out:
+                total = total + 3 * F.binary_cross_entropy_with_logits(out['pred_memory_mask'].float(),
+                                                                      (out['pred_memory_mask'].detach() > 0).float())
+            return total
         outs = [out] + list(out.get('aux_outputs', []))
         lv = [levels[-1]] + levels[:len(outs) - 1]
         for o, (bidx, sidx) in zip(outs, lv):

@@ -189,6 +189,13 @@ class UnimodalDeformableDVC(nn.Module):
             if self.aux_loss:
                 out['aux_outputs'] = self._set_aux_loss(outputs_class, outputs_segment, outputs_count, outputs_caption)
                 indices_aux = level_indices[:len(out['aux_outputs'])]  # same segments -> same assignment
+            # the same outputs stacked over the levels (a loss may read every level at once:
+            # dvc_core.level_terms); private key, the reference's keys are untouched
+            caps_all = output_caption[-1]
+            if lg is not None:
+                caps_all._mfl_logits = lg[-1]
+            out['_levels'] = {'logits': outputs_class, 'segments': outputs_segment, 'counts': outputs_count,
+                              'captions': caps_all}
             return out, outputs_caption_last_layer, indices, indices_aux, mask_out
 
         # inference: greedy decode of the last level (the reference's token choice reads only it, :334-338)

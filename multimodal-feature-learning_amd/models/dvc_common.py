@@ -51,8 +51,9 @@ def context_mask(model, denorm, query_features_selected, key_mask):
     criterion) and the boolean mask the caption decoder reads (sigmoid > 0.5)."""
     x = torch.cat([denorm.to(query_features_selected.dtype), query_features_selected], 1)
     pred = model(x)
-    seg_confidence = torch.ones([pred.shape[0], 1], device=pred.device, dtype=pred.dtype)
-    pred = seg_confidence * pred + (1 - seg_confidence) * key_mask.to(pred.dtype)
+    # the reference blends ``seg_confidence * pred + (1 - seg_confidence) * key_mask`` with
+    # seg_confidence = ones (:255-257): exactly pred (1 * p = p, (1 - 1) * m = 0, p + 0 = p) and a gradient
+    # of exactly 1 — five launches each way per level that change nothing, so pred is used as it is
     return pred, pred.sigmoid() > 0.5
 
 

@@ -372,6 +372,32 @@ def test_staged_dvc_loss_equals_eager_loss_cpu():
     assert torch.isfinite(tr.flat_grad).all() and tr.flat_grad.abs().sum() > 0
 
 
+def test_level_terms_equal_per_level_loop_cpu():
+    """dvc_core.level_terms (every decoder level's loss terms in one launch each, from the heads and
+    caption probabilities stacked over the levels, ``out['_levels']``) equals the per-level loop of
+    dvc_workload_loss on the same forward result, value and gradients (fp32, CPU, oracle MSDA core)."""
+    torch.manual_seed(1)
+    model = PKG.dvc_core.build_dvc(d_model=64, num_queries=10, T=32, enc_layers=1, dec_layers=3, caption_depth=1,
+                                   dropout=0.0, vocab_size=100, ff_dim=128)
+    obj = PKG.dvc_core.synthetic_dvc_batch(3, T=32, feature_dim=64, vocab_size=100, seed=5)
+    grads = []
+    with oracle_core(PKG):
+        for vectorized in (True, False):
+            model.zero_grad(set_to_none=True)
+            res = model(obj, is_training=True)
+            assert '_levels' in res[0] and res[0]['_levels']['segments'].shape[0] == 3
+            if not vectorized:
+                res[0].pop('_levels')
+            loss = PKG.dvc_core.dvc_workload_loss(res, obj)
+            loss.backward()
+            grads.append((loss.detach(), [p.grad.clone() for p in model.parameters() if p.grad is not None]))
+    (l1, g1), (l2, g2) = grads
+    torch.testing.assert_close(l1, l2, rtol=1e-6, atol=1e-6)
+    assert len(g1) == len(g2) > 0
+    for a, b in zip(g1, g2):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-7)
+
+
 @pytest.mark.parametrize("faster_eval", [False, True])
 def test_oracle_redecode_loop_matches_kv_cached_decode(faster_eval):
     """bench.py --config decode's CPU leg decodes with oracle/cpu_model.redecode_greedy (the
