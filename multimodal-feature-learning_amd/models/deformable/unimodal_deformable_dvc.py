@@ -30,7 +30,7 @@ from ..modules.embedding_layers import PositionEmbeddingVideoSine
 from ..modules.layers import FFN, ContextMaskModel
 from ..modules.linear import Linear
 from ..modules.misc_modules import level_heads
-from ...utils.preds_postprocess import SegmentMemory
+from ...utils.preds_postprocess import SegmentMemory, crop_keep, denormalize_segments, get_src_permutation_idx
 from ..unimodal_caption_decoder import build_unimodal_caption_decoder
 from .unimodal_deformable_transformer import build_unimodal_deformable_transformer
 
@@ -138,7 +138,13 @@ class UnimodalDeformableDVC(nn.Module):
             memory = SegmentMemory.of(memory)
 
         outputs_captions, memory_list, memory_mask_list, pred_memory_mask_list = [], [], [], []
-        for lvl in range(num_pred):
+        levels = self._level_crops(memory, outputs_segment, query_features, level_indices, level_idx_dev,
+                                   video_durations) if is_training else None
+        if levels is not None:
+            memory_list, memory_mask_list, pred_memory_mask_list, pred_logits = levels
+            if pred_logits is not None:
+                out['pred_memory_mask'] = pred_logits
+        for lvl in range(num_pred if levels is None else 0):
             # as the reference (:235): ``memory`` is rebound to this level's crop, which the next level crops
             idx, idx_dev, denorm, memory, key_mask = segment_memory(
                 memory, out_aux[lvl], level_indices[lvl], video_durations, self.num_feature_levels,
@@ -215,6 +221,48 @@ class UnimodalDeformableDVC(nn.Module):
             out['aux_outputs'] = self._set_aux_loss(outputs_class, outputs_segment, outputs_count, aux_caps + [None])
             indices_aux = level_indices[:len(out['aux_outputs'])]
         return out, captions_with_eos, indices, indices_aux, mask_out
+
+    def _level_crops(self, memory, outputs_segment, query_features, level_indices, level_idx_dev, video_durations):
+        """The per-level loop of ``forward_stage_captions`` (reference :227-260: each decoder level's matched
+        segments denormalised, the memory cropped — level l cropping level l-1's crop — and the context
+        mask predicted) with everything that does not chain from level to level run over all the levels'
+        segments at once: the segment gathers, the denormalisation, the crop bounds and the context-mask
+        model (row-wise: the same value per row; only the last level's logits reach the loss, the others
+        feed the boolean mask).  The crops still compose level by level (``SegmentMemory.select``).  None
+        (the loop runs) unless the memory is a SegmentMemory and every level matched the same number of
+        segments.  -> (memories, key masks, predicted masks or Nones, last level's mask logits or None)"""
+        if not isinstance(memory, SegmentMemory):
+            return None
+        L = query_features.shape[0]
+        dev = outputs_segment.device
+        idxs = []
+        for lvl in range(L):
+            if level_idx_dev is not None:
+                idxs.append(level_idx_dev[lvl])
+            else:
+                idxs.append(tuple(t.to(dev) for t in get_src_permutation_idx(level_indices[lvl])))
+        n = int(idxs[0][0].shape[0])
+        if n == 0 or any(int(i[0].shape[0]) != n for i in idxs):
+            return None
+        from ... import _trace
+        _trace.hit("level_crops_batched")
+        b_all = torch.cat([i[0] for i in idxs])
+        s_all = torch.cat([i[1] for i in idxs])
+        lv_all = torch.arange(L, device=dev).repeat_interleave(n)
+        denorm = denormalize_segments(outputs_segment[lv_all, b_all, s_all], video_durations, b_all)
+        keep = crop_keep(denorm, b_all, video_durations, memory.shape[1], self.num_feature_levels,
+                         self.video_rescale_len, dev)
+        memories, key_masks = [], []
+        for lvl in range(L):
+            memory = memory.select(idxs[lvl][0], keep[lvl * n:(lvl + 1) * n])
+            memories.append(memory)
+            key_masks.append((~keep[lvl * n:(lvl + 1) * n]).unsqueeze(1).unsqueeze(1))
+        if not self.use_differentiable_mask:
+            return memories, key_masks, [None] * L, None
+        pred_logits, pred_bool = context_mask(self.context_mask_model, denorm, query_features[lv_all, b_all, s_all],
+                                              ~keep)
+        preds = [pred_bool[lvl * n:(lvl + 1) * n].unsqueeze(1).unsqueeze(1) for lvl in range(L)]
+        return memories, key_masks, preds, pred_logits[(L - 1) * n:]
 
     @torch.no_grad()
     def _caption_probs(self, captions, mem, cross_mask):

@@ -11,7 +11,8 @@ from math import floor
 
 import torch
 
-__all__ = ["get_src_permutation_idx", "denormalize_segments", "crop_segments", "SegmentMemory", "level_token_ranges",
+__all__ = ["get_src_permutation_idx", "denormalize_segments", "crop_segments", "crop_keep", "SegmentMemory",
+           "level_token_ranges",
            "captions_to_string", "pre_process"]
 
 
@@ -79,11 +80,20 @@ def crop_segments(features, denormalized_segments, segment_batch_id, video_durat
     """Memory rows of each matched segment: per level, tokens [start, end) with
     start / end = clamp(round(lower + diff * t / duration), lower, upper - 1) (reference :457-493);
     other rows 0 and masked.  -> (features (n, K, d), padding mask (n, K) bool, True = masked)."""
-    n = denormalized_segments.shape[0]
-    K = features.shape[1]
-    dev = features.device
+    bid = segment_batch_id.to(features.device)
+    keep = crop_keep(denormalized_segments, bid, video_durations, features.shape[1], num_feature_levels,
+                     video_rescale_len, features.device)
+    if isinstance(features, SegmentMemory):
+        return features.select(bid, keep), ~keep
+    cropped = torch.where(keep[..., None], features[bid], features.new_zeros(()))
+    return cropped, ~keep
+
+
+def crop_keep(denormalized_segments, bid, video_durations, K, num_feature_levels, video_rescale_len, dev):
+    """crop_segments' (n, K) bool mask of the tokens each segment keeps (any row count: the DVC wrapper
+    computes every decoder level's segments at once)."""
     seg = denormalized_segments.to(dev, torch.float32)
-    bid = segment_batch_id.to(dev)
+    bid = bid.to(dev)
     dur = _durations(video_durations, dev)[bid]  # its own dtype: the reference promotes seg / dur the same way
     tok = torch.arange(K, device=dev)
     # every level's token range at once, (n, levels) bounds (the reference loops over the levels,
@@ -93,11 +103,7 @@ def crop_segments(features, denormalized_segments, segment_batch_id, video_durat
     dcol = dur[:, None] if dur.dim() == 1 else dur
     s = torch.clamp((lower + (diff * seg[:, 0:1] / dcol)).round().long(), min=lo_i, max=hi_i)
     e = torch.clamp((lower + (diff * seg[:, 1:2] / dcol)).round().long(), min=lo_i, max=hi_i)
-    keep = ((tok[None, None, :] >= s[:, :, None]) & (tok[None, None, :] < e[:, :, None])).any(1)
-    if isinstance(features, SegmentMemory):
-        return features.select(bid, keep), ~keep
-    cropped = torch.where(keep[..., None], features[bid], features.new_zeros(()))
-    return cropped, ~keep
+    return ((tok[None, None, :] >= s[:, :, None]) & (tok[None, None, :] < e[:, :, None])).any(1)
 
 
 class SegmentMemory:

@@ -252,7 +252,8 @@ def test_dvc_training_step_bf16_matches_reference_bf16(golden, dev):
     trainer._forward_backward((obj,))
     torch.cuda.synchronize()
     hits = dict(PKG._trace.hits)
-    for path in ("add_ln_carry", "linear_shadow", "query_prologue", "msda_bfloat16", "seg_attention"):
+    for path in ("add_ln_carry", "linear_shadow", "query_prologue", "msda_bfloat16", "seg_attention",
+                 "level_crops_batched"):
         assert hits.get(path, 0) > 0, (path, hits)
     out, _, indices, indices_aux, _ = res["r"]
     # the fixture's seed gives the fp64 and the reference's bf16 matching with a margin (0.019 in the
