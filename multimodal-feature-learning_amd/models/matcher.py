@@ -47,6 +47,20 @@ class HungarianMatcher(nn.Module):
         tgt_segments = torch.cat([v["segments"] for v in targets])
         tgt_xy = segment_cl_to_xy(tgt_segments)
         sizes = [len(v["segments"]) for v in targets]
+        shapes = [tuple(o["pred_segments"].shape[:2]) for o in outputs_list]
+        if len(outputs_list) > 1 and len(set(shapes)) == 1 and len(set(o["pred_segments"].dtype
+                                                                      for o in outputs_list)) == 1:
+            # every level's rows in one matrix: the costs are row-wise (cdist p=1, gIoU), so each
+            # element is the per-level one and the flattened (levels * B * Q, n) matrix is the
+            # concatenation of the per-level flattened costs — a few launches instead of ~20 a level
+            out_segments = torch.stack([o["pred_segments"] for o in outputs_list]).flatten(0, 2)
+            out_xy = segment_cl_to_xy(out_segments)
+            c = (self.cost_segment * torch.cdist(out_segments, tgt_segments, p=1)
+                 - self.cost_giou * generalized_box_iou_unchecked(out_xy, tgt_xy))
+            flags = (out_xy[:, 1] >= out_xy[:, 0]).view(len(outputs_list), -1).all(1)
+            flags = torch.cat([flags, (tgt_xy[:, 1] >= tgt_xy[:, 0]).all().reshape(1)])
+            return (torch.cat([c.reshape(-1).double(), flags.double()]),
+                    (shapes, sizes, len(tgt_segments), len(outputs_list) + 1))
         costs, flags, shapes = [], [], []
         for outputs in outputs_list:
             B, Q = outputs["pred_segments"].shape[:2]

@@ -98,3 +98,21 @@ def test_solve_levels_native_matches_scipy_path(monkeypatch):
     for lg, lw in zip(got, want):
         for (gi, gj), (wi, wj) in zip(lg, lw):
             assert torch.equal(gi, wi) and torch.equal(gj, wj) and gi.dtype == torch.int64
+
+
+def test_level_costs_all_levels_at_once_equal_per_level():
+    """HungarianMatcher.level_costs over several decoder levels builds every level's cost rows in one
+    matrix: bit for bit the per-level costs (each computed alone) concatenated, and the same flags."""
+    import torch
+    from conftest import PKG
+    g = torch.Generator().manual_seed(3)
+    m = PKG.models.matcher.HungarianMatcher(cost_class=1, cost_segment=5, cost_giou=2)
+    B, Q, L = 3, 7, 4
+    outs = [{"pred_segments": torch.rand(B, Q, 2, generator=g)} for _ in range(L)]
+    targets = [{"segments": torch.rand(n, 2, generator=g) * 0.5 + 0.1} for n in (2, 3, 1)]
+    joint, meta = m.level_costs(outs, targets)
+    parts = [m.level_costs([o], targets)[0] for o in outs]
+    n = B * Q * sum(len(t["segments"]) for t in targets)
+    assert torch.equal(joint[:L * n], torch.cat([p[:n] for p in parts]))
+    assert torch.equal(joint[L * n:], torch.cat([p[n:n + 1] for p in parts] + [parts[0][n + 1:]]))
+    assert meta[3] == L + 1 and meta[0] == [(B, Q)] * L
