@@ -38,8 +38,12 @@ def denormalize_segments(segments, video_durations, segment_batch_id):
     segments = segments.detach()  # the reference rebuilds them with torch.tensor(...): no gradient (:70-78)
     d = _durations(video_durations, dev)[segment_batch_id.to(dev)]
     c, l = segments[:, 0], segments[:, 1]
-    start = torch.minimum(torch.clamp(d / 2 * (2 * c - l), min=0), d)
-    end = torch.clamp(torch.minimum(d / 2 * (2 * c + l), d), min=0)
+    # the 16-bit (2c - l) / (2c + l) converted to the promoted dtype explicitly (exact: the values the
+    # mixed-dtype multiply promotes to), so the multiply is a same-dtype kernel — ROCm's mixed-dtype
+    # elementwise path took ~40 us a call here for a few dozen elements
+    pt = torch.promote_types(c.dtype, d.dtype)
+    start = torch.minimum(torch.clamp(d / 2 * (2 * c - l).to(pt), min=0), d)
+    end = torch.clamp(torch.minimum(d / 2 * (2 * c + l).to(pt), d), min=0)
     seg = torch.stack([start, end], 1).float()
     swap = ~(seg[:, 0] < seg[:, 1])
     return torch.where(swap[:, None], seg.flip(1), seg)

@@ -423,9 +423,9 @@ def test_flat_order_lays_query_projection_pairs_back_to_back():
 @pytest.mark.gpu
 @pytest.mark.parametrize("kind", ["multimodal", "sparse"])
 def test_grad_sum_in_gemm(dev, monkeypatch, kind):
-    """linear.mark_grad_sum: an activation whose every consumer takes part (configs[2]'s encoder: each
-    bf16 stream is one cross-modal call's value and the other's query, each FFN input linear1's input
-    and the residual; the Sparse-DETR encoder: the bf16 memory copy is the next layer's MSDA value
+    """linear.mark_grad_sum: an activation whose every consumer takes part (configs[2]'s encoder: the
+    joint rows' bf16 self-block output is the cross-modal calls' value and their query, the FFN input
+    linear1's input and the residual; the Sparse-DETR encoder: the bf16 memory copy is the next layer's MSDA value
     and its row write-back's input) gets its input gradients summed in the later consumer's dgrad
     GEMM (C += dY W) instead of autograd's bf16 add.  Same loss; the flat gradient differs from
     autograd's sums only by that one bf16 rounding per summed pair."""
@@ -437,7 +437,9 @@ def test_grad_sum_in_gemm(dev, monkeypatch, kind):
         audio, amask, _ = PKG.dvc_core.synthetic_clips(2, T=16, feature_dim=256, padded=True, seed=9, device=dev)
         batch = (video, vmask, audio, amask, dur)
         make = lambda: PKG.dvc_core.MultimodalDVCCore(num_classes=5, **small)  # noqa: E731
-        loss_fn, want = PKG.dvc_core.multimodal_workload_loss, 8  # 2 layers x (v16, a16, two FFN inputs)
+        # 2 layers x (the joint rows' bf16 self-block output x16 — both cross calls' value and query —,
+        # and the joint FFN input): the encoder runs both streams on joint rows (_forward_joint)
+        loss_fn, want = PKG.dvc_core.multimodal_workload_loss, 4
     else:
         batch = PKG.dvc_core.synthetic_clips(3, T=128, feature_dim=256, padded=True, seed=7, device=dev)
         make = lambda: PKG.dvc_core.SparseDVCCore(**small)  # noqa: E731
