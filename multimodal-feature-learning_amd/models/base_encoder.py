@@ -31,7 +31,9 @@ class _Conv1dGemm(torch.autograd.Function):
         B, T, C = x.shape
         O, _, k = weight.shape
         dt = x.dtype
-        w2 = weight.permute(0, 2, 1).reshape(O, k * C).to(dt)  # [o][tap][c]
+        # [o][tap][c] in the input dtype: the permute and the cast in one copy kernel (reshape of the
+        # permuted fp32 weight would first clone it in fp32)
+        w2 = torch.empty((O, k, C), dtype=dt, device=weight.device).copy_(weight.permute(0, 2, 1)).view(O, k * C)
         if k == 1:
             t_out = T
             cols = x.reshape(B * T, C)

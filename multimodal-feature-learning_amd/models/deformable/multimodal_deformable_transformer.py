@@ -385,6 +385,8 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
         sa = mha_self_attention(self.self_attn, tgt, query_pos, query_mask, carried)
         tgt, _, q16 = add_layer_norm_carry(tgt, sa, self.norm2, query_pos, self.dropout2, pos_acc=pos_acc)
         query = q16 if q16 is not None else tgt
+        # the one query of both cross-attentions: their two prologue input gradients summed in one GEMM
+        mark_grad_sum(query)
         ca_v = self.cross_attn(query, reference_points_input_video, video_src, video_temporal_shapes,
                                video_level_start_index, video_src_padding_mask, value=video_value)
         tgt_video = add_layer_norm(tgt, ca_v, self.norm1, dropout=self.dropout1)
@@ -393,6 +395,7 @@ class MultimodalDeformableTransformerDecoderLayer(nn.Module):
         tgt_audio = add_layer_norm(tgt, ca_a, self.norm1, dropout=self.dropout1)
         bridged = self.linear3(self.norm4(torch.cat([tgt_video, tgt_audio], dim=-1)))
         t = relu_dropout(bridged, self.activation, self.dropout5)
+        mark_grad_sum(t)  # (linear1's input and the add + LayerNorm's residual)
         hidden = relu_dropout(self.linear1(t), self.activation, self.dropout3)
         return add_layer_norm_carry(t, self.linear2(hidden), self.norm3, query_pos, self.dropout4, pos_acc=pos_acc)
 

@@ -194,10 +194,18 @@ class _WgradQueue:
                 # row blocks tiling the weight (in_proj q / k | v): concatenated straight into its flat view
                 v = _claim(prm, returned=False) if ps[0][1].is_cuda else None
                 grad = torch.cat([g for _, g in ps]) if v is None else torch.cat([g for _, g in ps], out=v)
-            else:  # a weight used several times
+            elif all(r == 0 and g.shape == prm.shape for r, g in ps):
+                # a whole weight used several times (the multimodal decoder's cross-attention over both
+                # memories): its products summed into its flat view in list order (one slab-sum kernel
+                # when they are slabs of one batched GEMM's output)
+                v = _claim(prm, returned=False) if ps[0][1].is_cuda else None
+                out = v.view_as(prm) if v is not None else torch.empty(prm.shape, dtype=torch.float32,
+                                                                         device=prm.device)
+                grad = _sum_into([g for _, g in ps], out, accumulate=False)
+            else:  # row blocks of a weight used several times
                 grad = torch.zeros(prm.shape, dtype=torch.float32, device=prm.device)
                 for row, g in ps:
-                    grad[row:row + g.shape[0]] += g
+                    grad[row:row + g.shape[0]].add_(g)  # (in place: no write-back copy of the slice)
             self.deliver(prm, grad)
 
 
@@ -368,6 +376,16 @@ def split_k_chunks(k, min_chunk=1024, max_split=8):
             return s
         s //= 2
     return 1
+
+
+def _split_k_ragged(k, out_elems):
+    """(s, r): s chunks of K // s rows (a power of two, the chunk sizes split_k_chunks asks for) and r
+    leftover rows, for a K that split_k_chunks cannot divide; (1, 0) when not worth it."""
+    min_chunk, max_split = _SPLITK if out_elems <= _SPLITK_SMALL else (1024, 8)
+    s = max_split
+    while s > 1 and k // s < min_chunk:
+        s //= 2
+    return (s, k - s * (k // s)) if s > 1 else (1, 0)
 
 
 _dest = None  # flat_grad_destinations: {"views": {id(param): flat view}, "claimed": set(), ...}
@@ -620,11 +638,22 @@ def _weight_grad(g2, x2, out=None, accumulate=False):
     ``accumulate``)."""
     k, n_out, n_in = x2.shape[0], g2.shape[1], x2.shape[1]
     s = split_k_chunks(k, *_SPLITK) if n_out * n_in <= _SPLITK_SMALL else split_k_chunks(k)
-    if s > 1:
+    s2, r = _split_k_ragged(k, n_out * n_in)
+    if s > 1 and not (s2 > s and g2.is_cuda):
         # (bmm, not baddbmm(out=part, beta=0): that form first copies `part` into the output — an
         # extra 8-32 MB pass per call, ~0.3 ms per step, tools/op_census.py)
         part = torch.bmm(g2.view(s, k // s, n_out).transpose(1, 2), x2.view(s, k // s, n_in),
                          out_dtype=torch.float32)
+        return _sum_slabs(part, out, accumulate)
+    s = s2
+    if s > 1 and g2.is_cuda:
+        # K not divisible by a useful chunk count (the multimodal encoder's joint rows: 16,120): s equal
+        # chunks in one strided-batched GEMM plus the last r rows as one more slab, summed together
+        c = k // s
+        part = torch.empty((s + 1, n_out, n_in), dtype=torch.float32, device=g2.device)
+        torch.bmm(g2[:s * c].view(s, c, n_out).transpose(1, 2), x2[:s * c].view(s, c, n_in), out_dtype=torch.float32,
+                  out=part[:s])
+        torch.mm(g2[s * c:].t(), x2[s * c:], out_dtype=torch.float32, out=part[s])
         return _sum_slabs(part, out, accumulate)
     r = torch.mm(g2.t(), x2, out_dtype=torch.float32)
     if out is None:

@@ -437,9 +437,10 @@ def test_grad_sum_in_gemm(dev, monkeypatch, kind):
         audio, amask, _ = PKG.dvc_core.synthetic_clips(2, T=16, feature_dim=256, padded=True, seed=9, device=dev)
         batch = (video, vmask, audio, amask, dur)
         make = lambda: PKG.dvc_core.MultimodalDVCCore(num_classes=5, **small)  # noqa: E731
-        # 2 layers x (the joint rows' bf16 self-block output x16 — both cross calls' value and query —,
-        # and the joint FFN input): the encoder runs both streams on joint rows (_forward_joint)
-        loss_fn, want = PKG.dvc_core.multimodal_workload_loss, 4
+        # encoder: 2 layers x (the joint rows' bf16 self-block output x16 — both cross calls' value and
+        # query — and the joint FFN input; _forward_joint); decoder: 2 layers x (the one bf16 query of
+        # both cross-attentions, the bridge output t: linear1's input and the residual)
+        loss_fn, want = PKG.dvc_core.multimodal_workload_loss, 8
     else:
         batch = PKG.dvc_core.synthetic_clips(3, T=128, feature_dim=256, padded=True, seed=7, device=dev)
         make = lambda: PKG.dvc_core.SparseDVCCore(**small)  # noqa: E731
