@@ -75,6 +75,16 @@ int mfl_gather_keep_backward(const void* grad, const int64_t* index, const void*
 int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t row_bytes, const uint8_t* mask,
                                  void* stream);
 
+/* The augmented operands of the batched value / key projections' bias-in-K GEMM
+ * (models/modules/value_proj.py layer_values, y_i = [x | 1] . [W_i^T ; b_i] with K padded to ca):
+ *   mfl_augment_rows:    out (k, ca) bf16 = [x (k, c) | 1 | 0 ...]                  (c, ca multiples of 8, 16-B aligned)
+ *   mfl_augment_weights: out (n, ca, co) bf16, out[i][j][o] = w[i][o][j] (j < c), b[i][o] (j == c), 0 (j > c),
+ *                        w (n, co, c) / b (n, co) bf16 contiguous.
+ * One pass each. */
+int mfl_augment_rows(const void* x, int64_t k, int64_t c, int64_t ca, void* out, void* stream);
+int mfl_augment_weights(const void* w, const void* b, int64_t n, int64_t c, int64_t ca, int64_t co, void* out,
+                        void* stream);
+
 /* The flattened level position embedding of prepare_encoder_inputs (reference
  * models/deformable/unimodal_deformable_transformer.py:90-134, `torch.cat([pos_l.transpose(1, 2) +
  * level_embed[l].view(1, 1, -1) for l], 1)`): out[b, start_l + t, c] = pos[l][b, c, t] +

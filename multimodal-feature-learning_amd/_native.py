@@ -81,6 +81,8 @@ EXPORTED_SYMBOLS = (
     "mfl_relu_dropout_last_error",
     "mfl_zero_masked_rows",
     "mfl_zero_masked_rows_batched",
+    "mfl_augment_rows",
+    "mfl_augment_weights",
     "mfl_gather_keep_backward",
     # include/gemm_small.h
     "mfl_gemm_nt_bf16",
@@ -256,6 +258,10 @@ def _declare(lib):
     lib.mfl_zero_masked_rows.argtypes = [vp, i64, i64, vp, vp]
     lib.mfl_zero_masked_rows_batched.restype = i32
     lib.mfl_zero_masked_rows_batched.argtypes = [vp, i64, i64, i64, vp, vp]
+    lib.mfl_augment_rows.restype = i32
+    lib.mfl_augment_rows.argtypes = [vp, i64, i64, i64, vp, vp]
+    lib.mfl_augment_weights.restype = i32
+    lib.mfl_augment_weights.argtypes = [vp, vp, i64, i64, i64, i64, vp, vp]
     lib.mfl_relu_dropout_last_error.restype = ctypes.c_char_p
     lib.mfl_relu_dropout_last_error.argtypes = []
     lib.mfl_add_layernorm_last_error.restype = ctypes.c_char_p

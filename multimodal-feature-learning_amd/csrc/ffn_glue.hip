@@ -573,6 +573,38 @@ bool level_table(const int64_t* T, int64_t L, int64_t B, int64_t N, int rows_per
   tb.blk0[L] = (int)blk;
   return true;
 }
+
+// The augmented operands of value_proj.layer_values' bias-in-K GEMM (models/modules/value_proj.py):
+// x_aug (k, ca) = [x | 1 | 0 ...] and w_aug (n, ca, co) = [W_i^T ; b_i ; 0 ...], each in ONE pass
+// (against zeros + a strided copy + a column fill, and zeros + two stacks + two strided copies).
+// One thread a 16-B chunk of an x_aug row (c % 8 == 0, ca % 8 == 0).
+__global__ __launch_bounds__(kThreads) void augment_rows_kernel(const uint4* __restrict__ x, long long k, int cv,
+                                                                int cav, uint4* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= k * cav) return;
+  const long long r = i / cav;
+  const int v = (int)(i - r * cav);
+  uint4 o = make_uint4(0u, 0u, 0u, 0u);
+  if (v < cv) o = x[r * cv + v];
+  else if (v == cv) o.x = 0x3F80u;  // bf16 1.0 in the chunk's first element
+  out[i] = o;
+}
+
+// w_aug[i][j][o] = j < c ? w[i][o][j] : (j == c ? b[i][o] : 0): one thread an output element (bf16;
+// the (n x ca x co) operand is at most a few MB)
+__global__ __launch_bounds__(kThreads) void augment_weights_kernel(const uint16_t* __restrict__ w,
+                                                                   const uint16_t* __restrict__ b, int n, int c,
+                                                                   int ca, int co, uint16_t* __restrict__ out) {
+  const long long e = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (e >= (long long)n * ca * co) return;
+  const int o = (int)(e % co);
+  const long long ij = e / co;
+  const int j = (int)(ij % ca), i = (int)(ij / ca);
+  uint16_t v = 0;
+  if (j < c) v = w[((long long)i * co + o) * c + j];
+  else if (j == c) v = b[(long long)i * co + o];
+  out[e] = v;
+}
 }  // namespace
 
 extern "C" {
@@ -672,6 +704,36 @@ int mfl_relu_dropout_backward_colsum(const void* dy, const void* out, int64_t ro
   hipLaunchKernelGGL(relu_dropout_colsum_final, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st,
                      static_cast<const float*>(workspace), (int)groups, (int)cols, colsum);
   return status("backward (column sums, final)");
+}
+
+int mfl_augment_rows(const void* x, int64_t k, int64_t c, int64_t ca, void* out, void* stream) {
+  g_err[0] = 0;
+  if (k < 0 || c <= 0 || ca <= c || c % 8 || ca % 8 || !x || !out || ((uintptr_t)x & 15u) || ((uintptr_t)out & 15u) ||
+      k * (ca / 8) >= (1LL << 40)) {
+    snprintf(g_err, sizeof(g_err), "mfl_augment_rows: bad arguments (c %% 8 == 0, ca %% 8 == 0, ca > c, 16-B aligned)");
+    return 1;
+  }
+  const long long total = k * (ca / 8);
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(augment_rows_kernel, dim3((unsigned)((total + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint4*>(x), k, (int)(c / 8), (int)(ca / 8),
+                     static_cast<uint4*>(out));
+  return status("augment rows");
+}
+
+int mfl_augment_weights(const void* w, const void* b, int64_t n, int64_t c, int64_t ca, int64_t co, void* out,
+                        void* stream) {
+  g_err[0] = 0;
+  if (n < 0 || c <= 0 || ca <= c || co <= 0 || !w || !b || !out || n * ca * co >= (1LL << 31)) {
+    snprintf(g_err, sizeof(g_err), "mfl_augment_weights: bad arguments (ca > c, n * ca * co < 2^31)");
+    return 1;
+  }
+  const long long total = n * ca * co;
+  if (total == 0) return 0;
+  hipLaunchKernelGGL(augment_weights_kernel, dim3((unsigned)((total + kThreads - 1) / kThreads)), dim3(kThreads), 0,
+                     static_cast<hipStream_t>(stream), static_cast<const uint16_t*>(w),
+                     static_cast<const uint16_t*>(b), (int)n, (int)c, (int)ca, (int)co, static_cast<uint16_t*>(out));
+  return status("augment weights");
 }
 
 int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t row_bytes, const uint8_t* mask,

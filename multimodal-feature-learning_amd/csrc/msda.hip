@@ -2557,6 +2557,8 @@ int fast16_group(const Problem& pr) {
 }
 
 int env_int(const char* name, int dflt);
+bool dense_takes(const Problem& pr, int value_dtype);
+WinShape dense_win_shape(const Problem& pr);
 
 template <typename scalar_t, typename coord_t, int VEC>
 int run_forward(const Problem& pr, const void* value, const void* loc, const void* aw, void* out,
@@ -2573,6 +2575,16 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
   auto* o = static_cast<scalar_t*>(out);
   if constexpr (!std::is_same<coord_t, double>::value && VEC * sizeof(scalar_t) == 16) {
     const int G = fast16_group<scalar_t>(pr);
+    if constexpr (std::is_same<scalar_t, bf16_t>::value) {
+      if (dense_takes(pr, MSDA_DTYPE_BF16)) {  // (tiles, when handed over, are not needed by its backward)
+        const WinShape sh = dense_win_shape(pr);
+        if (msda_dense_forward(value, loc, aw, out, &sh, pad == MSDA_PAD_ZEROS, lm ? 1 : 0, st) != 0) {
+          set_error("msda forward: the dense small-pyramid kernel could not be launched");
+          return MSDA_ERR_LAUNCH;
+        }
+        return launch_status("forward (dense)");
+      }
+    }
     if constexpr (sizeof(scalar_t) == 2) {
     if (tiles != nullptr) {  // the caller checked forward_tiles_ok: 16-bit values, D = 64 (G = 8)
       const int ntile = (int)((pr.Lq + kWinQT - 1) / kWinQT);
@@ -3250,6 +3262,25 @@ bool forward_tiles_ok(const Problem& pr, int value_dtype) {
   return win_takes(pr, value_dtype);
 }
 
+// The dense small-pyramid kernels (msda_win.hip) take the call: bf16 values, D = 64, a pyramid of at
+// most 128 rows (configs[2]'s audio pyramid: the video queries' cross-modal call and the audio
+// self-attention), L <= 4, P <= 4; both coordinate layouts, the forward's tiles unused
+bool dense_takes(const Problem& pr, int value_dtype) {
+  return pr.B * pr.M * pr.S > 0 && pr.Lq > 0 &&
+         msda_dense_supported(value_dtype == MSDA_DTYPE_BF16, pr.D, pr.S, pr.L, pr.P) != 0;
+}
+
+WinShape dense_win_shape(const Problem& pr) {
+  WinShape sh{};
+  sh.B = pr.B; sh.S = pr.S; sh.M = pr.M; sh.Lq = pr.Lq; sh.L = (int)pr.L; sh.P = (int)pr.P;
+  for (int l = 0; l < pr.L; ++l) {
+    sh.T[l] = pr.lv.T[l];
+    sh.start[l] = pr.lv.start[l];
+  }
+  sh.gv_rs = pr.gv_rs;
+  return sh;
+}
+
 template <typename scalar_t, typename coord_t>
 int run_backward(const Problem& pr, const void* value, const void* loc, const void* aw,
                  const void* gout, void* gval, void* gloc, void* gaw, void* workspace,
@@ -3263,6 +3294,19 @@ int run_backward(const Problem& pr, const void* value, const void* loc, const vo
     int minT = 1 << 30;
     for (int l = 0; l < pr.L; ++l) minT = min(minT, pr.lv.T[l]);
     const bool sparse = pr.Lq * pr.P <= 4LL * (minT + 1) || pr.Lq * pr.P <= 512;
+    if constexpr (std::is_same<scalar_t, bf16_t>::value) {
+      // the dense small-pyramid kernels (any of gval / gloc / gaw may be null; a strided grad_value too:
+      // configs[2]'s decoder cross-attention into the audio memory writes layer_values' G in place)
+      if (dense_takes(pr, value_dtype)) {
+        const WinShape sh = dense_win_shape(pr);
+        if (msda_dense_backward(value, loc, aw, gout, gval, gloc, gaw, workspace, &sh, pad == MSDA_PAD_ZEROS, layout,
+                                st) != 0) {
+          set_error("msda backward: the dense small-pyramid kernel could not be launched");
+          return MSDA_ERR_LAUNCH;
+        }
+        return launch_status("backward (dense)");
+      }
+    }
     if (pr.gv_rs > 0 && pr.gv_rs != pr.M * pr.D) {
       // a strided grad_value: only the per-tap fused kernel writes it (the calls that ask for it,
       // the decoders' cross-attentions, take that path); others report it unsupported
@@ -4165,6 +4209,9 @@ size_t msda_hip_backward_workspace_bytes(int value_dtype, int64_t batch, int64_t
                                          int64_t num_levels, int64_t num_point) {
   (void)channels;
   if (batch <= 0 || spatial_size <= 0 || num_heads <= 0) return 0;
+  if (value_dtype == MSDA_DTYPE_BF16 && num_query > 0 &&
+      msda_dense_supported(1, channels, spatial_size, num_levels, num_point) != 0)
+    return msda_dense_workspace_bytes(batch, spatial_size, num_heads, num_query);  // (dense_takes: its partial sums)
   PairPlan pp;
   // the row-block MFMA path's tile intervals (when it may run: the levels are not known here)
   const bool may_win = win_supported_call(value_dtype, channels, num_query, num_point, num_heads, num_levels);

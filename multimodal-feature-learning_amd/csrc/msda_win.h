@@ -96,6 +96,8 @@ struct WinShape {
   QOrder qo;  // tile order of the queries (set by the caller: make_qorder; ignored when qo_dev)
   int qo_dev;  // 1: the tiles came from the forward, which stored its QOrder in the tiles tail
   int exp;  // profiling only (MSDA_HIP_WIN_EXP bitmask, 0 in production): skip parts of win_bwd_kernel
+  long long gv_rs;  // dense kernels: grad_value row stride in elements (0: M * 64)
+  int wsplit[16];  // win_lm_kernel split mode: waves per row block of each level (1, 2 or 4; set by msda_win_backward)
   unsigned short cs[kWinMaxChunks + 1];
   unsigned short seq[kWinMaxSeq];
 };
@@ -153,3 +155,20 @@ __attribute__((visibility("hidden"))) int msda_win_backward(const void* value, c
                                                             void* workspace, const void* tiles_ready,
                                                             const WinShape* shape, int zeros, int coord_layout,
                                                             hipStream_t st);
+
+// The dense small-pyramid kernels (msda_win.hip): 16-bit values, D = 64, at most 128 pyramid rows per
+// (b, m), L <= 4, P in {1, 2, 4}; MSDA_HIP_DENSE=0 turns them off (A/B).  Shape fields used: B, S, M,
+// Lq, L, P, T, start.  Return 0, or -1 when the shape does not fit (nothing launched).
+__attribute__((visibility("hidden"))) int msda_dense_supported(int value_dtype_is_bf16, long long D, long long S,
+                                                               long long L, long long P);
+__attribute__((visibility("hidden"))) int msda_dense_forward(const void* value, const void* loc, const void* aw,
+                                                             void* out, const WinShape* shape, int zeros,
+                                                             int coord_layout, hipStream_t st);
+// workspace: msda_dense_workspace_bytes (the groups' fp32 partial sums of grad_value), or null (one
+// workgroup a (b, m), slower)
+__attribute__((visibility("hidden"))) int msda_dense_backward(const void* value, const void* loc, const void* aw,
+                                                              const void* gout, void* gval, void* gloc, void* gaw,
+                                                              void* workspace, const WinShape* shape, int zeros,
+                                                              int coord_layout, hipStream_t st);
+__attribute__((visibility("hidden"))) size_t msda_dense_workspace_bytes(long long B, long long S, long long M,
+                                                                       long long Lq);

@@ -555,20 +555,30 @@ __device__ __forceinline__ int lm_sw(int r, int c) {
 // different rows; the A-operand reads (rows li, chunk g / 4 + g) still meet 16 distinct bank quads
 __device__ __forceinline__ int lm_csw(int r, int c) { return r * kLmRow + ((c ^ (r & 7)) << 4); }
 
-template <bool ZEROS, bool COORDS, int P>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void win_lm_kernel(
+// NW (round 6): waves per workgroup.  NW = 1: one wave a 16-row block.  NW = 4 (split mode): a
+// workgroup holds 4 / W_l blocks of level l with W_l = sh.wsplit[l] waves each (1, 2 or 4); the
+// waves of one block take its visits round-robin (wave p: visits p, p + W_l, ...) and add their
+// grad_value partials through LDS at the end in wave order.  The coarse levels' blocks meet the most
+// query tiles (bench encoder call: ~12 visits a level-3 block against ~5 a level-0 block,
+// tools/win_visits.py); with one wave each they are the kernel's longest waves.
+template <bool ZEROS, bool COORDS, int P, int NW = 1>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(4))) void win_lm_kernel(
     const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
     const uint16_t* __restrict__ gout, uint16_t* __restrict__ gval, float* __restrict__ gloc,
     float* __restrict__ gaw, const int2* __restrict__ tiles, const WinShape sh) {
   constexpr int NS = kQT * P;                  // samples per tile and level
   constexpr int SPL = NS >= 64 ? NS / 64 : 1;  // samples per lane
-  __shared__ __attribute__((aligned(16))) unsigned char s_g[kQT * kLmRow];  // the tile's grad_out rows
+  __shared__ __attribute__((aligned(16))) unsigned char s_g_w[NW][kQT * kLmRow];  // the tile's grad_out rows
   // dots [row - r0][q] (kVRows x kDQS floats), then, once the coordinate gradients have read them,
   // the coefficient tile C [16 rows][hi 32 | lo 32] bf16 of each MFMA step
-  __shared__ __attribute__((aligned(16))) float s_cd[kVRows * kDQS];
-  __shared__ int s_q[NS + kQT];  // query (in the tile) of each compacted sample, padded
+  __shared__ __attribute__((aligned(16))) float s_cd_w[NW][kVRows * kDQS];
+  __shared__ int s_q_w[NW][NS + kQT];  // query (in the tile) of each compacted sample, padded
+  const int wid = NW > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)) : 0;  // (wave-uniform)
+  unsigned char* const s_g = s_g_w[wid];
+  float* const s_cd = s_cd_w[wid];
+  int* const s_q = s_q_w[wid];
   unsigned char* const s_c = reinterpret_cast<unsigned char*>(s_cd);
-  const int lane = (int)threadIdx.x, g = lane >> 4, li = lane & 15;
+  const int lane = (int)(threadIdx.x & 63), g = lane >> 4, li = lane & 15;
   const int grow = lane >> 3, gch = lane & 7;
   // LDS offsets fixed per lane: grad_out row writes (rows grow, grow + 8), and the row reads of
   // chunks g / 4 + g of row li (the dots' A operand, rows li and 16 + li; the C tile's hi / lo)
@@ -584,17 +594,29 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
   const int cq = qo.cs == 0 ? 1 : 0;  // (uniform) consecutive tiles
 
   const unsigned slot = blockIdx.x >> 3;
+  f32x4 acc[4];
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  int Wl = 1, part = 0;  // waves of this wave's block and its rank among them
+  int j = -1;            // (B M nblk < 2^31: checked by the host)
+  int l = sh.L - 1;
   {
-    int l = sh.L - 1;
-    int j = -1;  // (B M nblk < 2^31: checked by the host)
     {
+      // the workgroups of XCD x8: level l (coarsest first) has cl = ceil(nu / 8) slots of its nu
+      // workgroups (4 / W_l blocks each in split mode), slot i of it is workgroup x8 cl + i
       unsigned s = slot;
       for (; l >= 0; --l) {
+        const int wl = NW > 1 ? sh.wsplit[l] : 1;
+        const unsigned bpu = (unsigned)(NW / wl);
         const unsigned nl = (unsigned)sh.B * (unsigned)sh.M * (unsigned)(sh.blk0[l + 1] - sh.blk0[l]);
-        const unsigned cl = (nl + 7u) / 8u;
+        const unsigned nu = (nl + bpu - 1u) / bpu;
+        const unsigned cl = (nu + 7u) / 8u;
         if (s < cl) {
-          const unsigned jj = x8 * cl + s;
-          j = jj < nl ? (int)jj : -1;  // (past the level's end on this XCD: none)
+          const unsigned uu = x8 * cl + s;
+          const unsigned jj = uu * bpu + (unsigned)(wid / wl);
+          j = uu < nu && jj < nl ? (int)jj : -1;  // (past the level's end on this XCD: none)
+          Wl = wl;
+          part = wid % wl;
           break;
         }
         s -= cl;
@@ -632,7 +654,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
       };
       int cur_t0 = 0;
       unsigned long long mask = chunk_mask(0);
-      auto next_tile = [&]() -> int {
+      auto pop_tile = [&]() -> int {
         while (mask == 0ull) {
           cur_t0 += 64;
           if (cur_t0 >= sh.ntile) return -1;
@@ -642,12 +664,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
         mask &= mask - 1ull;
         return t;
       };
+      bool first_pop = true;
+      auto next_tile = [&]() -> int {  // this wave's visits: part, part + Wl, ... of the block's
+        if constexpr (NW > 1) {
+          const int skip = first_pop ? part : Wl - 1;
+          first_pop = false;
+          for (int i = 0; i < skip; ++i)
+            if (pop_tile() < 0) return -1;
+        }
+        return pop_tile();
+      };
       // the query of entry e of the tile order
       auto qry = [&](int e) -> int { return cq ? e : qo_query(qo, e); };
 
-      f32x4 acc[4];
-#pragma unroll
-      for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
       float rl[SPL], ra[SPL];
       uint4 rg[4];
       auto fetch = [&](int tile) {
@@ -806,22 +835,582 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void wi
         wave_lds_fence();  // this visit's LDS reads before the next visit's writes
         tile = next;
       }
-      // grad_value rows r0 + 4g + jj, channels 16 cb + li (every row of the block, zeros included)
-      if (gval != nullptr) {
-        uint16_t* __restrict__ gvl = gval + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
+    }
+  }
+  if constexpr (NW > 1) {
+    // split blocks: waves 1 .. W_l - 1 of a block hand their partial sums to wave 0 through their own
+    // (now idle) grad_out tile; the barriers are reached by every wave of the workgroup
+    __syncthreads();
+    if (j >= 0 && part > 0) {
 #pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int x = r0 + 4 * g + jj;
-          if (x < T) {
+      for (int cb = 0; cb < 4; ++cb) reinterpret_cast<f32x4*>(s_g)[cb * 64 + lane] = acc[cb];
+    }
+    __syncthreads();
+    if (j >= 0 && part == 0) {
+      for (int p = 1; p < Wl; ++p) {
 #pragma unroll
-            for (int cb = 0; cb < 4; ++cb) gvl[x * rs + cb * 16 + li] = (uint16_t)bf16_bits(acc[cb][jj]);
+        for (int cb = 0; cb < 4; ++cb) acc[cb] += reinterpret_cast<const f32x4*>(s_g_w[wid + p])[cb * 64 + lane];
+      }
+    }
+  }
+  // grad_value rows r0 + 4g + jj, channels 16 cb + li (every row of the block, zeros included)
+  if (j >= 0 && part == 0 && gval != nullptr) {
+    const int nbl = sh.blk0[l + 1] - sh.blk0[l];
+    const unsigned bm = (unsigned)j / (unsigned)nbl;
+    const int k = (int)((unsigned)j - bm * (unsigned)nbl);
+    const int m = (int)(bm % (unsigned)sh.M);
+    const long long b = bm / (unsigned)sh.M;
+    const int T = sh.T[l];
+    const int r0 = k * kRW;
+    const int rs = sh.M * 64;
+    uint16_t* __restrict__ gvl = gval + ((b * sh.S + sh.start[l]) * sh.M + m) * 64;
+#pragma unroll
+    for (int jj = 0; jj < 4; ++jj) {
+      const int x = r0 + 4 * g + jj;
+      if (x < T) {
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) gvl[x * rs + cb * 16 + li] = (uint16_t)bf16_bits(acc[cb][jj]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Dense small-pyramid kernels (round 6): calls whose value pyramid has at most kDnMaxRows rows per
+// (b, m) — configs[2]'s video queries on the audio pyramid (S = 95, Lq = 1920) and the audio
+// self-attention (S = Lq = 95).  A 32-query tile's samples there touch about a third of the rows,
+// so the sampling of a tile is a DENSE matrix C (queries x pyramid rows: each sample's aw * w at
+// its two tap rows, the samples of one query on one row summed) and the call is small GEMMs on
+// the matrix cores:
+//   forward    out (q x 64) = C . V                    (V: the (b, m) pyramid, staged in LDS once)
+//   backward   grad_value (rows x 64) += C^T . G       (G: the tile's grad_out rows)
+//              dots D (rows x q) = V . G^T             grad_attn = w0 d0 + w1 d1,
+//                                                      grad_loc = aw (d1 - d0) dy/dloc (two rows of D)
+// instead of the row-block kernel's 8 waves per 16-row block that each stage every tile (all 60
+// tiles meet each of the 8 blocks of the 95-row pyramid: 44 us, 1.49x its algorithmic bytes) and
+// the gathering forward's 2 x 16 row fragments per query from L2 (34 us).
+// C is built without atomics: thread (q, l) owns query q's coefficients on level l's rows (levels'
+// rows never coincide), sums its 2P taps' coefficients per row in registers in sample order and
+// stores each distinct row once as a bf16 hi + lo pair (|c - hi - lo| <= 2^-16 |c|, as
+// win_lm_kernel), then clears what it stored once the products have read it.  Taps and weights
+// are make_taps' (the other kernels' bit for bit); every grad_value row is written once, every
+// coordinate gradient once: deterministic, no atomics.
+// ---------------------------------------------------------------------------------------------
+constexpr int kDnMaxRows = 128;  // pyramid rows per (b, m)
+constexpr int kDnMaxL = 4;
+constexpr int kDnSub = 2;        // backward: query tiles in flight per workgroup (4 waves each)
+constexpr int kDnDQ = kQT + 4;   // backward dots: [row][q] floats, 16-B rows
+
+struct DenseShape {
+  long long B, S, M, Lq;
+  int L, P;
+  int R;  // rows rounded up to 32 (the MFMA K steps of the forward)
+  int T[kDnMaxL], start[kDnMaxL];
+  long long cb, cm;  // coordinate strides (coord_strides)
+  int cq, cl;
+  int ntile;         // backward: 32-query tiles
+  int ngroup;        // backward: workgroups per (b, m) (query tiles dealt over them; > 1: partial sums)
+  int nchunk;        // forward: query chunks per (b, m) of 64 wt queries (4 waves x wt 16-query tiles)
+  int wt;            // forward: 16-query tiles a wave takes
+  long long gvs;     // grad_value row stride (elements): M * 64, or a caller's strided slot
+};
+
+// the thread's P samples on one level: tap rows (row, row + 1) in the flattened pyramid and weights
+template <int P>
+struct DnTaps {
+  int row[P];
+  float w0[P], w1[P], a[P], gmul[P];
+  bool ok0[P], ok1[P];
+};
+
+template <int P>
+__device__ __forceinline__ void dn_load4(const float* __restrict__ p, float (&x)[P]) {
+  if constexpr (P == 4) {
+    const float4 v = *reinterpret_cast<const float4*>(p);
+    x[0] = v.x; x[1] = v.y; x[2] = v.z; x[3] = v.w;
+  } else if constexpr (P == 2) {
+    const float2 v = *reinterpret_cast<const float2*>(p);
+    x[0] = v.x; x[1] = v.y;
+  } else {
+    x[0] = p[0];
+  }
+}
+
+template <int P>
+__device__ __forceinline__ void dn_store4(float* __restrict__ p, const float (&x)[P]) {
+  if constexpr (P == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+  } else if constexpr (P == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(x[0], x[1]);
+  } else {
+    p[0] = x[0];
+  }
+}
+
+template <bool ZEROS, int P>
+__device__ __forceinline__ void dn_taps(const float* __restrict__ lp, const float* __restrict__ ap, int T, int st,
+                                        DnTaps<P>& tp) {
+  float lc[P], ac[P];
+  dn_load4<P>(lp, lc);
+  dn_load4<P>(ap, ac);
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    const Taps t = make_taps<ZEROS>(lc[p], T);
+    tp.row[p] = st + t.base;
+    tp.w0[p] = t.w0;
+    tp.w1[p] = t.w1;
+    tp.ok0[p] = t.ok0;
+    tp.ok1[p] = t.ok1;
+    tp.a[p] = ac[p];
+    tp.gmul[p] = t.gmul;
+  }
+}
+
+// the distinct rows of the thread's 2P taps with their summed coefficients (sample order), each
+// handed to f(row, coefficient) once; clear(row) variants hand the same rows only
+template <int P, typename F>
+__device__ __forceinline__ void dn_rows(const DnTaps<P>& tp, F f) {
+  int r[2 * P];
+  float c[2 * P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    r[2 * p] = tp.ok0[p] ? tp.row[p] : -1;
+    c[2 * p] = tp.ok0[p] ? tp.a[p] * tp.w0[p] : 0.f;
+    r[2 * p + 1] = tp.ok1[p] ? tp.row[p] + 1 : -1;
+    c[2 * p + 1] = tp.ok1[p] ? tp.a[p] * tp.w1[p] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < 2 * P; ++j) {
+    bool first = r[j] >= 0;
+#pragma unroll
+    for (int k = 0; k < j; ++k) first = first && r[k] != r[j];
+    if (first) {
+      float s = c[j];
+#pragma unroll
+      for (int k = j + 1; k < 2 * P; ++k) s += r[k] == r[j] ? c[k] : 0.f;
+      f(r[j], s);
+    }
+  }
+}
+
+__device__ __forceinline__ uint16_t dn_hi(float c) { return (uint16_t)(__float_as_uint(c) >> 16); }
+__device__ __forceinline__ uint16_t dn_lo(float c) {
+  return __builtin_bit_cast(uint16_t, (__bf16)(c - __uint_as_float(__float_as_uint(c) & 0xffff0000u)));
+}
+
+// backward C tile: [row][32 queries] bf16, 64-B rows, 16-B chunk (8 queries) c at c ^ ((row >> 1) & 3):
+// the A-operand reads (16 rows, one chunk) meet 16 distinct bank quads
+__device__ __forceinline__ int dn_bc(int row, int q) {
+  return row * 64 + ((((q >> 3) ^ (row >> 1)) & 3) << 4) + (q & 7) * 2;
+}
+// forward C tile: [16 queries][128 rows] bf16, 256-B rows, chunk (8 rows) c at c ^ (q & 7)
+__device__ __forceinline__ int dn_fc(int q, int row) { return q * 256 + ((((row >> 3) ^ q) & 15) << 4) + (row & 7) * 2; }
+
+// sh.ngroup workgroups per (b, m), kDnSub x 4 waves each: sub-group s of group r takes query tiles
+// (r kDnSub + s) + i ngroup kDnSub; in a tile, threads (q, l) of the sub-group build C, wave w then owns
+// row blocks w and w + 4 (16 rows each: grad_value += C^T G, dots D = V G^T), threads (q, l) write
+// their coordinate gradients from D; at the end the sub-groups' grad_value partials meet in LDS in a
+// fixed order, and with several groups each group's sum goes to `part` (fp32, group-major) for
+// dense_sum_kernel to add in group order.
+template <bool ZEROS, bool COORDS, int P>
+__global__ __launch_bounds__(256 * kDnSub) void dense_bwd_kernel(
+    const uint16_t* __restrict__ value, const float* __restrict__ loc, const float* __restrict__ aw,
+    const uint16_t* __restrict__ gout, uint16_t* __restrict__ gval, float* __restrict__ gloc,
+    float* __restrict__ gaw, float* __restrict__ gpart, const DenseShape sh) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  const int R = sh.R, nrb = (int)((sh.S + 15) / 16);
+  const int sub_bytes = kQT * kLmRow + 128 * R + 4 * kDnDQ * R;  // G | C hi, lo | D
+  const int tid = (int)threadIdx.x, sub = tid >> 8, t = tid & 255, wave = t >> 6, lane = t & 63;
+  const int g = lane >> 4, li = lane & 15;
+  unsigned char* const s_g = s_dyn + sub * sub_bytes;
+  unsigned char* const s_chi = s_g + kQT * kLmRow;
+  unsigned char* const s_clo = s_chi + 64 * R;
+  float* const s_d = reinterpret_cast<float*>(s_clo + 64 * R);
+  const int grp = (int)(blockIdx.x % (unsigned)sh.ngroup);
+  const unsigned bm = blockIdx.x / (unsigned)sh.ngroup;
+  const int m = (int)(bm % (unsigned)sh.M);
+  const long long b = bm / (unsigned)sh.M;
+  const int rs = (int)sh.M * 64;  // value / grad_out row stride (elements)
+  const uint16_t* __restrict__ vb = value + (b * sh.S * sh.M + m) * 64;
+  const uint16_t* __restrict__ gb = gout + (b * sh.Lq * sh.M + m) * 64;
+  const long long cbase = b * sh.cb + m * sh.cm;
+  // the dots' B operands: value rows r0 + li of the wave's blocks (zeros past S)
+  bf16x8 vr[2][2];
+#pragma unroll
+  for (int o = 0; o < 2; ++o) {
+    const int x = (wave + 4 * o) * 16 + li;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (x < sh.S) v = *reinterpret_cast<const uint4*>(vb + x * rs + ks * 32 + 8 * g);
+      vr[o][ks] = __builtin_bit_cast(bf16x8, v);
+    }
+  }
+  f32x4 acc[2][4];
+#pragma unroll
+  for (int o = 0; o < 2; ++o)
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[o][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = t; i < 128 * R / 16; i += 256) reinterpret_cast<uint4*>(s_chi)[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  const int cqi = t >> 2, cli = t & 3;  // the C / coordinate thread's query in the tile and level
+  const int span = kDnSub * sh.ngroup;  // tiles a round of every group's sub-groups takes
+  const int nit = (sh.ntile + span - 1) / span;
+  const int qq = li >> 2, pp = li & 3;
+  for (int it = 0; it < nit; ++it) {
+    const int tile = it * span + grp * kDnSub + sub;
+    const int q0 = tile * kQT;
+    {  // the tile's grad_out rows: one 16-B chunk a thread
+      const int row = t >> 3, ch = t & 7, q = q0 + row;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (tile < sh.ntile && q < sh.Lq) v = *reinterpret_cast<const uint4*>(gb + (long long)q * rs + ch * 8);
+      *reinterpret_cast<uint4*>(s_g + lm_sw(row, ch)) = v;
+    }
+    const bool own = tile < sh.ntile && t < 4 * kQT && cli < sh.L && q0 + cqi < sh.Lq;
+    const long long co = cbase + (long long)(q0 + cqi) * sh.cq + (long long)cli * sh.cl;
+    if (own) {
+      DnTaps<P> tp;
+      dn_taps<ZEROS, P>(loc + co, aw + co, sh.T[cli], sh.start[cli], tp);
+      dn_rows<P>(tp, [&](int r, float c) {
+        *reinterpret_cast<uint16_t*>(s_chi + dn_bc(r, cqi)) = dn_hi(c);
+        *reinterpret_cast<uint16_t*>(s_clo + dn_bc(r, cqi)) = dn_lo(c);
+      });
+    }
+    __syncthreads();
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const int rb = wave + 4 * o;
+      if (rb < nrb) {
+        const int r0 = rb * 16;
+        const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(s_chi + dn_bc(r0 + li, 8 * g));
+        const bf16x8 alo = *reinterpret_cast<const bf16x8*>(s_clo + dn_bc(r0 + li, 8 * g));
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) {
+          const int c = 2 * cb + (pp >> 1), w8 = (pp & 1) * 8;
+          const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(s_g + lm_sw(8 * g + qq, c) + w8));
+          const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(s_g + lm_sw(8 * g + 4 + qq, c) + w8));
+          const bf16x8 bv = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[o][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, acc[o][cb], 0, 0, 0);
+          acc[o][cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, acc[o][cb], 0, 0, 0);
+        }
+        if constexpr (COORDS) {
+#pragma unroll
+          for (int qh = 0; qh < 2; ++qh) {
+            const bf16x8 a0 = *reinterpret_cast<const bf16x8*>(s_g + lm_sw(li, g) + qh * 16 * kLmRow);
+            const bf16x8 a1 = *reinterpret_cast<const bf16x8*>(s_g + lm_sw(li, 4 + g) + qh * 16 * kLmRow);
+            f32x4 d = f32x4{0.f, 0.f, 0.f, 0.f};
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, vr[o][0], d, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, vr[o][1], d, 0, 0, 0);
+            *reinterpret_cast<f32x4*>(s_d + (r0 + li) * kDnDQ + qh * 16 + 4 * g) = d;  // rows r0 + li, queries 4g..
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (own) {
+      DnTaps<P> tp;  // (re-read: not held in registers across the products)
+      dn_taps<ZEROS, P>(loc + co, aw + co, sh.T[cli], sh.start[cli], tp);
+      if constexpr (COORDS) {
+        float ga[P], gl[P];
+#pragma unroll
+        for (int p = 0; p < P; ++p) {
+          const float d0 = tp.ok0[p] ? s_d[tp.row[p] * kDnDQ + cqi] : 0.f;
+          const float d1 = tp.ok1[p] ? s_d[(tp.row[p] + 1) * kDnDQ + cqi] : 0.f;
+          ga[p] = d0 * tp.w0[p] + d1 * tp.w1[p];
+          gl[p] = ((d1 - d0) * tp.a[p]) * tp.gmul[p];
+        }
+        if (gaw != nullptr) dn_store4<P>(gaw + co, ga);
+        if (gloc != nullptr) dn_store4<P>(gloc + co, gl);
+      }
+      // clear this tile's coefficients (the next tile's threads write other entries)
+      dn_rows<P>(tp, [&](int r, float) {
+        *reinterpret_cast<uint16_t*>(s_chi + dn_bc(r, cqi)) = 0;
+        *reinterpret_cast<uint16_t*>(s_clo + dn_bc(r, cqi)) = 0;
+      });
+    }
+    __syncthreads();
+  }
+  // the sub-groups' partial sums: 1..kDnSub-1 through LDS, added to sub-group 0's in order
+  f32x4* const part = reinterpret_cast<f32x4*>(s_dyn);
+  if (sub > 0) {
+#pragma unroll
+    for (int o = 0; o < 2; ++o)
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) part[((((sub - 1) * 4 + wave) * 2 + o) * 4 + cb) * 64 + lane] = acc[o][cb];
+  }
+  __syncthreads();
+  if (sub == 0 && gval != nullptr) {
+    uint16_t* __restrict__ gv = gval + b * sh.S * sh.gvs + m * 64;
+    // (several groups: this group's fp32 sum, rows [0, R) x 64 channels)
+    float* __restrict__ gp = gpart + ((long long)bm * sh.ngroup + grp) * sh.R * 64;
+#pragma unroll
+    for (int o = 0; o < 2; ++o) {
+      const int rb = wave + 4 * o;
+      if (rb >= nrb) continue;
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        f32x4 s = acc[o][cb];
+        for (int u = 1; u < kDnSub; ++u) s += part[((((u - 1) * 4 + wave) * 2 + o) * 4 + cb) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int x = rb * 16 + 4 * g + j;
+          if (x < sh.S) {
+            if (sh.ngroup > 1) gp[x * 64 + cb * 16 + li] = s[j];
+            else gv[(long long)x * sh.gvs + cb * 16 + li] = (uint16_t)bf16_bits(s[j]);
           }
         }
       }
     }
   }
 }
+
+// grad_value rows of the (b, m) pairs as the sum of their groups' fp32 partials in group order (one
+// thread a 4-channel piece of a row); bf16 out
+__global__ __launch_bounds__(256) void dense_sum_kernel(const float* __restrict__ gpart, uint16_t* __restrict__ gval,
+                                                        const DenseShape sh) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;  // (bm, row, 4-channel piece)
+  const long long n = sh.B * sh.M * sh.S * 16;
+  if (i >= n) return;
+  const int pc = (int)(i & 15);
+  const long long br = i >> 4;
+  const int row = (int)(br % sh.S);
+  const long long bm = br / sh.S;
+  const int m = (int)(bm % sh.M);
+  const long long b = bm / sh.M;
+  const float4* __restrict__ src = reinterpret_cast<const float4*>(gpart + bm * sh.ngroup * sh.R * 64 + row * 64) + pc;
+  float4 s = src[0];
+  for (int r = 1; r < sh.ngroup; ++r) {
+    const float4 t = src[(long long)r * sh.R * 16];
+    s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+  }
+  uint2 o;
+  o.x = (uint32_t)(uint16_t)bf16_bits(s.x) | ((uint32_t)(uint16_t)bf16_bits(s.y) << 16);
+  o.y = (uint32_t)(uint16_t)bf16_bits(s.z) | ((uint32_t)(uint16_t)bf16_bits(s.w) << 16);
+  *reinterpret_cast<uint2*>(gval + (b * sh.S + row) * sh.gvs + m * 64 + pc * 4) = o;
+}
+
+// One workgroup per (b, m, 128-query chunk), 4 waves: the (b, m) pyramid staged in LDS once (128-B
+// rows, lm_sw), then each wave takes 16-query tiles: threads (q, l) build the tile's C, then
+// out = C . V over the pyramid's rows in 32-row MFMA steps (B operands read transposed).
+template <bool ZEROS, int P>
+__global__ __launch_bounds__(256) void dense_fwd_kernel(const uint16_t* __restrict__ value,
+                                                        const float* __restrict__ loc,
+                                                        const float* __restrict__ aw, uint16_t* __restrict__ out,
+                                                        const DenseShape sh) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  const int R = sh.R;
+  const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  unsigned char* const s_v = s_dyn;
+  unsigned char* const s_chi = s_dyn + R * kLmRow + wave * (2 * 16 * 256);
+  unsigned char* const s_clo = s_chi + 16 * 256;
+  const unsigned chunk = blockIdx.x % (unsigned)sh.nchunk;  // (of 64 sh.wt queries)
+  const unsigned bm = blockIdx.x / (unsigned)sh.nchunk;
+  const int m = (int)(bm % (unsigned)sh.M);
+  const long long b = bm / (unsigned)sh.M;
+  const int rs = (int)sh.M * 64;
+  const uint16_t* __restrict__ vb = value + (b * sh.S * sh.M + m) * 64;
+  for (int i = tid; i < R * 8; i += 256) {
+    const int row = i >> 3, ch = i & 7;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (row < sh.S) v = *reinterpret_cast<const uint4*>(vb + row * rs + ch * 8);
+    *reinterpret_cast<uint4*>(s_v + lm_sw(row, ch)) = v;
+  }
+  for (int i = lane; i < 2 * 16 * 256 / 16; i += 64) reinterpret_cast<uint4*>(s_chi)[i] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  const int cqi = lane >> 2, cli = lane & 3;
+  const int qq = li >> 2, pp = li & 3;
+  const long long cbase = b * sh.cb + m * sh.cm;
+  for (int wt = 0; wt < sh.wt; ++wt) {
+    const int q0 = ((int)chunk * sh.wt + wt) * 64 + wave * 16;
+    if (q0 >= sh.Lq) break;  // (wave-uniform)
+    const bool own = cli < sh.L && q0 + cqi < sh.Lq;
+    DnTaps<P> tp;
+    if (own) {
+      const long long co = cbase + (long long)(q0 + cqi) * sh.cq + (long long)cli * sh.cl;
+      dn_taps<ZEROS, P>(loc + co, aw + co, sh.T[cli], sh.start[cli], tp);
+      dn_rows<P>(tp, [&](int r, float c) {
+        *reinterpret_cast<uint16_t*>(s_chi + dn_fc(cqi, r)) = dn_hi(c);
+        *reinterpret_cast<uint16_t*>(s_clo + dn_fc(cqi, r)) = dn_lo(c);
+      });
+    }
+    wave_lds_fence();
+    f32x4 acc[4];
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) acc[cb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int ks = 0; ks < R / 32; ++ks) {
+      const bf16x8 ahi = *reinterpret_cast<const bf16x8*>(s_chi + dn_fc(li, ks * 32 + 8 * g));
+      const bf16x8 alo = *reinterpret_cast<const bf16x8*>(s_clo + dn_fc(li, ks * 32 + 8 * g));
+#pragma unroll
+      for (int cb = 0; cb < 4; ++cb) {
+        const int c = 2 * cb + (pp >> 1), w8 = (pp & 1) * 8;
+        const bf16x4 x0 =
+            __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(s_v + lm_sw(ks * 32 + 8 * g + qq, c) + w8));
+        const bf16x4 x1 =
+            __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(s_v + lm_sw(ks * 32 + 8 * g + 4 + qq, c) + w8));
+        const bf16x8 bv = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, acc[cb], 0, 0, 0);
+        acc[cb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, acc[cb], 0, 0, 0);
+      }
+    }
+    wave_lds_fence();  // the products' C reads before the clears
+    if (own) {
+      dn_rows<P>(tp, [&](int r, float) {
+        *reinterpret_cast<uint16_t*>(s_chi + dn_fc(cqi, r)) = 0;
+        *reinterpret_cast<uint16_t*>(s_clo + dn_fc(cqi, r)) = 0;
+      });
+    }
+    // out rows q0 + 4g + j, channels 16 cb + li
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = q0 + 4 * g + j;
+      if (q < sh.Lq) {
+        uint16_t* __restrict__ op = out + ((b * sh.Lq + q) * sh.M + m) * 64;
+#pragma unroll
+        for (int cb = 0; cb < 4; ++cb) op[cb * 16 + li] = (uint16_t)bf16_bits(acc[cb][j]);
+      }
+    }
+    wave_lds_fence();  // the clears before the next tile's stores
+  }
+}
 }  // namespace
+
+// the dense kernels' LDS (bytes): backward per workgroup, forward per workgroup
+// (backward: the sub-groups' tiles, or the partial sums they add at the end, whichever is larger)
+static size_t dense_bwd_lds(int R) {
+  const size_t tiles = (size_t)kDnSub * (kQT * kLmRow + 128 * R + 4 * kDnDQ * R);
+  const size_t parts = (size_t)(kDnSub - 1) * 4 * 2 * 4 * 64 * 16;
+  return tiles > parts ? tiles : parts;
+}
+static size_t dense_fwd_lds(int R) { return (size_t)R * kLmRow + 4 * 2 * 16 * 256; }
+
+int msda_dense_supported(int value_dtype_is_bf16, long long D, long long S, long long L, long long P) {
+  const char* e = getenv("MSDA_HIP_DENSE");
+  if (e != nullptr && atoi(e) == 0) return 0;
+  return value_dtype_is_bf16 && D == 64 && S >= 1 && S <= kDnMaxRows && L >= 1 && L <= kDnMaxL &&
+         (P == 1 || P == 2 || P == 4);
+}
+
+static bool dense_shape(const WinShape* in, int coord_layout, DenseShape& sh) {
+  sh.B = in->B; sh.S = in->S; sh.M = in->M; sh.Lq = in->Lq;
+  sh.L = in->L; sh.P = in->P;
+  if (sh.L < 1 || sh.L > kDnMaxL || sh.S > kDnMaxRows || sh.S * sh.M * 64 >= (1LL << 31) ||
+      sh.Lq * sh.M * 64 >= (1LL << 31))
+    return false;
+  for (int l = 0; l < sh.L; ++l) {
+    sh.T[l] = in->T[l];
+    sh.start[l] = in->start[l];
+  }
+  sh.R = (int)((sh.S + 31) / 32) * 32;
+  const CoordStrides cs = coord_strides(coord_layout, sh.Lq, sh.M, sh.L, sh.P);
+  sh.cb = cs.cb; sh.cm = cs.cm; sh.cq = cs.cq; sh.cl = cs.cl;
+  sh.ntile = (int)((sh.Lq + kQT - 1) / kQT);
+  sh.ngroup = 1;
+  // forward chunks: 128 queries a workgroup on long query sets, 64 on short ones (the audio self-
+  // attention's 95 queries: 2 workgroups a (b, m) instead of one)
+  sh.wt = sh.Lq >= 1024 ? 2 : 1;
+  sh.nchunk = (int)((sh.Lq + 64 * sh.wt - 1) / (64 * sh.wt));
+  sh.gvs = in->gv_rs > 0 ? in->gv_rs : sh.M * 64;
+  return true;
+}
+
+// workgroups per (b, m) of the dense backward: about 512 workgroups over the chip, at least one
+// tile a sub-group
+static int dense_groups(long long B, long long M, long long Lq) {
+  const long long ntile = (Lq + kQT - 1) / kQT;
+  long long ng = (512 + B * M - 1) / max(1LL, B * M);
+  ng = min(ng, (ntile + kDnSub - 1) / kDnSub);
+  return (int)max(1LL, min(ng, 64LL));
+}
+
+size_t msda_dense_workspace_bytes(long long B, long long S, long long M, long long Lq) {
+  const int ng = dense_groups(B, M, Lq);
+  if (ng <= 1) return 0;
+  const long long R = (S + 31) / 32 * 32;
+  return (size_t)(B * M * ng * R * 64) * sizeof(float);
+}
+
+template <typename K>
+static int dense_lds_attr(K kernel, size_t bytes) {
+  if (bytes <= 64 * 1024) return 0;
+  return hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             (int)bytes) == hipSuccess
+             ? 0
+             : -1;
+}
+
+int msda_dense_forward(const void* value, const void* loc, const void* aw, void* out, const WinShape* shape, int zeros,
+                       int coord_layout, hipStream_t st) {
+  DenseShape sh{};
+  if (!dense_shape(shape, coord_layout, sh)) return -1;
+  if (sh.B * sh.M == 0 || sh.Lq == 0) return 0;
+  const unsigned grid = (unsigned)(sh.B * sh.M * sh.nchunk);
+  const size_t lds = dense_fwd_lds(sh.R);
+  auto* v = static_cast<const uint16_t*>(value);
+  auto* lc = static_cast<const float*>(loc);
+  auto* a = static_cast<const float*>(aw);
+  auto* o = static_cast<uint16_t*>(out);
+#define DN_FWD(Z, PP)                                                                                   \
+  do {                                                                                                  \
+    if (dense_lds_attr(dense_fwd_kernel<Z, PP>, lds)) return -1;                                        \
+    hipLaunchKernelGGL((dense_fwd_kernel<Z, PP>), dim3(grid), dim3(256), lds, st, v, lc, a, o, sh);      \
+  } while (0)
+#define DN_FWD_P(Z)                     \
+  switch (sh.P) {                       \
+    case 1: DN_FWD(Z, 1); break;        \
+    case 2: DN_FWD(Z, 2); break;        \
+    default: DN_FWD(Z, 4); break;       \
+  }
+  if (zeros) { DN_FWD_P(true) } else { DN_FWD_P(false) }
+#undef DN_FWD_P
+#undef DN_FWD
+  return 0;
+}
+
+int msda_dense_backward(const void* value, const void* loc, const void* aw, const void* gout, void* gval, void* gloc,
+                        void* gaw, void* workspace, const WinShape* shape, int zeros, int coord_layout,
+                        hipStream_t st) {
+  DenseShape sh{};
+  if (!dense_shape(shape, coord_layout, sh)) return -1;
+  if (sh.B * sh.M == 0) return 0;
+  // several workgroups per (b, m) when the caller handed the partial sums' workspace
+  // (msda_dense_workspace_bytes; one workgroup a (b, m) writes grad_value directly otherwise)
+  if (workspace != nullptr && gval != nullptr) sh.ngroup = dense_groups(sh.B, sh.M, sh.Lq);
+  auto* gp = static_cast<float*>(workspace);
+  const unsigned grid = (unsigned)(sh.B * sh.M * sh.ngroup);
+  const size_t lds = dense_bwd_lds(sh.R);
+  const bool coords = gloc != nullptr || gaw != nullptr;
+  auto* v = static_cast<const uint16_t*>(value);
+  auto* lc = static_cast<const float*>(loc);
+  auto* a = static_cast<const float*>(aw);
+  auto* g = static_cast<const uint16_t*>(gout);
+  auto* gv = static_cast<uint16_t*>(gval);
+  auto* gl = static_cast<float*>(gloc);
+  auto* ga = static_cast<float*>(gaw);
+#define DN_BWD(Z, C, PP)                                                                                 \
+  do {                                                                                                   \
+    if (dense_lds_attr(dense_bwd_kernel<Z, C, PP>, lds)) return -1;                                      \
+    hipLaunchKernelGGL((dense_bwd_kernel<Z, C, PP>), dim3(grid), dim3(256 * kDnSub), lds, st, v, lc, a, g, gv, gl, \
+                       ga, gp, sh);                                                                      \
+  } while (0)
+#define DN_BWD_P(Z, C)                  \
+  switch (sh.P) {                       \
+    case 1: DN_BWD(Z, C, 1); break;     \
+    case 2: DN_BWD(Z, C, 2); break;     \
+    default: DN_BWD(Z, C, 4); break;    \
+  }
+  if (zeros) {
+    if (coords) { DN_BWD_P(true, true) } else { DN_BWD_P(true, false) }
+  } else {
+    if (coords) { DN_BWD_P(false, true) } else { DN_BWD_P(false, false) }
+  }
+#undef DN_BWD_P
+#undef DN_BWD
+  if (sh.ngroup > 1) {
+    const long long n = sh.B * sh.M * sh.S * 16;
+    hipLaunchKernelGGL(dense_sum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, gp, gv, sh);
+  }
+  return 0;
+}
 
 size_t msda_win_workspace_bytes(long long B, long long M, long long L, long long Lq) {
   const long long ntile = (Lq + kQT - 1) / kQT;
@@ -903,8 +1492,28 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
   if (lm_kernel) {
     sh.qo_dev = 1;
     sh.exp = 0;
+    // split mode (4-wave workgroups, MSDA_HIP_WIN_LM_SPLIT=1; measured slower, so opt-in): a level
+    // with a quarter / an eighth of the finest level's rows gets 2 / 4 waves a block (its blocks meet
+    // 2-3x the query tiles).  Bench encoder call (tools/msda_microbench.py, r06l): 56.4 / 61.2 us
+    // (init / trained sampling) against 49.4 / 54.8 with one wave a block — the coarse blocks are not
+    // the kernel's critical path; the split adds waves, barriers and the partial-sum exchange
+    const char* spe = getenv("MSDA_HIP_WIN_LM_SPLIT");
+    int tmax = 1;
+    for (int l = 0; l < sh.L; ++l) tmax = max(tmax, sh.T[l]);
+    bool split = false;
+    for (int l = 0; l < sh.L; ++l) {
+      const int ratio = tmax / max(1, sh.T[l]);
+      sh.wsplit[l] = ratio >= 8 ? 4 : ratio >= 4 ? 2 : 1;
+      split = split || sh.wsplit[l] > 1;
+    }
+    if (spe == nullptr || atoi(spe) != 1) split = false;
+    const int nw = split ? 4 : 1;
     unsigned nsx = 0;
-    for (int l = 0; l < sh.L; ++l) nsx += (unsigned)((sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + 7) / 8);
+    for (int l = 0; l < sh.L; ++l) {
+      const long long bpu = split ? 4 / sh.wsplit[l] : 1;
+      const long long nu = (sh.B * sh.M * (sh.blk0[l + 1] - sh.blk0[l]) + bpu - 1) / bpu;
+      nsx += (unsigned)((nu + 7) / 8);
+    }
     auto* tl = static_cast<const int2*>(tiles_ready);
     const bool coords = gloc != nullptr || gaw != nullptr;
     auto* v = static_cast<const uint16_t*>(value);
@@ -914,8 +1523,13 @@ int msda_win_backward(const void* value, const void* loc, const void* aw, const 
     auto* gv = static_cast<uint16_t*>(gval);
     auto* gl = static_cast<float*>(gloc);
     auto* ga = static_cast<float*>(gaw);
-#define WIN_LM(Z, C, N) \
-  hipLaunchKernelGGL((win_lm_kernel<Z, C, N>), dim3(8u * nsx), dim3(64), 0, st, v, lc, a, g, gv, gl, ga, tl, sh)
+#define WIN_LM(Z, C, N)                                                                                      \
+  do {                                                                                                       \
+    if (nw == 4)                                                                                             \
+      hipLaunchKernelGGL((win_lm_kernel<Z, C, N, 4>), dim3(8u * nsx), dim3(256), 0, st, v, lc, a, g, gv, gl, ga, tl, sh); \
+    else                                                                                                     \
+      hipLaunchKernelGGL((win_lm_kernel<Z, C, N, 1>), dim3(8u * nsx), dim3(64), 0, st, v, lc, a, g, gv, gl, ga, tl, sh); \
+  } while (0)
 #define WIN_LM_P(Z, C)                                                  \
   do {                                                                  \
     switch (sh.P) {                                                     \

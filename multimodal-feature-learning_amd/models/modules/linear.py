@@ -639,7 +639,10 @@ def _weight_grad(g2, x2, out=None, accumulate=False):
     k, n_out, n_in = x2.shape[0], g2.shape[1], x2.shape[1]
     s = split_k_chunks(k, *_SPLITK) if n_out * n_in <= _SPLITK_SMALL else split_k_chunks(k)
     s2, r = _split_k_ragged(k, n_out * n_in)
-    if s > 1 and not (s2 > s and g2.is_cuda):
+    # an exact split at least half as wide as the ragged one is taken as it is: the ragged form's
+    # leftover rows cost a GEMM launch of their own (the multimodal joint rows, K = 16,120 = 16 x 1,007
+    # + 8: a (512 x 8) . (8 x 512) product at ~6 us, 36 a step; tools/splitk_probe.py)
+    if s > 1 and not (s2 > 2 * s and g2.is_cuda):
         # (bmm, not baddbmm(out=part, beta=0): that form first copies `part` into the output — an
         # extra 8-32 MB pass per call, ~0.3 ms per step, tools/op_census.py)
         part = torch.bmm(g2.view(s, k // s, n_out).transpose(1, 2), x2.view(s, k // s, n_in),

@@ -51,16 +51,32 @@ class _LayerValues(Function):
         wcs = [wc[i] if wc[i] is not None else w[i].to(dt) for i in range(n)]
         bcs = [bc[i] if bc[i] is not None else b[i].to(dt) for i in range(n)]
         c_out = wcs[0].shape[0]
-        x_aug = torch.zeros(k, c + _PAD, dtype=dt, device=x.device)
-        x_aug[:, :c] = x16
-        x_aug[:, c] = 1
-        w_aug = torch.zeros(n, c + _PAD, c_out, dtype=dt, device=x.device)
-        w_aug[:, :c] = torch.stack(wcs).transpose(1, 2)
-        w_aug[:, c] = torch.stack(bcs)
+        wcat = torch.cat(wcs, 0)
+        if x16.is_cuda and c % 8 == 0 and x16.is_contiguous():
+            # [x | 1 | 0 ...] and [W_i^T ; b_i ; 0 ...] in one pass each (include/ffn_glue.h)
+            from ... import _native
+            lib = _native.load_library()
+            x16 = x16.contiguous()
+            bcat = torch.cat(bcs, 0)
+            x_aug = torch.empty(k, c + _PAD, dtype=dt, device=x.device)
+            w_aug = torch.empty(n, c + _PAD, c_out, dtype=dt, device=x.device)
+            st = _native.stream_handle(x.device)
+            rc = lib.mfl_augment_rows(x16.data_ptr(), k, c, c + _PAD, x_aug.data_ptr(), st)
+            rc = rc or lib.mfl_augment_weights(wcat.data_ptr(), bcat.data_ptr(), n, c, c + _PAD, c_out,
+                                               w_aug.data_ptr(), st)
+            if rc != 0:
+                raise RuntimeError("mfl_augment_rows / weights failed: " + lib.mfl_relu_dropout_last_error().decode())
+        else:
+            x_aug = torch.zeros(k, c + _PAD, dtype=dt, device=x.device)
+            x_aug[:, :c] = x16
+            x_aug[:, c] = 1
+            w_aug = torch.zeros(n, c + _PAD, c_out, dtype=dt, device=x.device)
+            w_aug[:, :c] = torch.stack(wcs).transpose(1, 2)
+            w_aug[:, c] = torch.stack(bcs)
         y = torch.bmm(x_aug.expand(n, k, c + _PAD), w_aug)  # (n, k, c_out); A shared (batch stride 0)
         if mask is not None:
             _zero_rows(y, n, k, mask)
-        ctx.save_for_backward(x16, torch.cat(wcs, 0), mask)
+        ctx.save_for_backward(x16, wcat, mask)
         ctx.n, ctx.x_shape, ctx.x_dtype, ctx.c_out = n, x.shape, x.dtype, c_out
         ctx.params = (w, b)  # (the parameters whose flat gradient views the backward may claim)
         outs = tuple(torch.ops.aten._unsafe_view(y[i], (*lead, c_out)) for i in range(n))

@@ -355,8 +355,11 @@ def test_forward_tiles_equal_backward_prepass(dev, monkeypatch, case, padding):
     backward's tile intervals reduced in the workgroup) gives the plain forward's output bit for
     bit, and the backward fed those intervals (msda_hip_backward_tiles) gives the gradients of
     the backward that computes them in its own prepass bit for bit — both see the same rows
-    (msda_win.h win_sample_rows), so every row block visits the same tiles in the same order."""
+    (msda_win.h win_sample_rows), so every row block visits the same tiles in the same order.
+    (The row-block protocol: the audio-pyramid cases would otherwise take the dense small-pyramid
+    kernels, which neither write nor read tile intervals — tests/test_gpu_dense.py.)"""
     monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
+    monkeypatch.setenv("MSDA_HIP_DENSE", "0")
     shapes, B, M, Lq, P, kind = WIN_CASES[case]
     D = 64
     value, loc, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=70 + case)
@@ -547,6 +550,7 @@ def test_level_major_row_kernel_equals_per_block_kernel(dev, monkeypatch, case, 
     for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH", "MSDA_HIP_QORDER",
               "MSDA_HIP_WIN_LM"):
         monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("MSDA_HIP_WIN_LM_SPLIT", "0")  # (one wave a block: the per-block kernel's sum order)
     shapes, B, M, P = LM_CASES[case]
     D, Lq = 64, sum(shapes)
     value, _, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=120 + case, lo=0.0, hi=1.0)
@@ -566,6 +570,38 @@ def test_level_major_row_kernel_equals_per_block_kernel(dev, monkeypatch, case, 
     for run in runs:
         for r, x in zip(ref, run):
             assert torch.equal(r, x)
+
+
+@pytest.mark.parametrize("padding", ["border", "zeros"])
+@pytest.mark.parametrize("case", range(len(LM_CASES)))
+def test_level_major_split_blocks_equal_single_wave_blocks(dev, monkeypatch, case, padding):
+    """win_lm_kernel's split mode (round 6, opt-in MSDA_HIP_WIN_LM_SPLIT=1: 4-wave workgroups, the coarse
+    levels' blocks shared by 2 / 4 waves that take the block's visits round-robin and add their
+    grad_value partials in wave order) against one wave a block (the default): the coordinate gradients bit for bit (each
+    visit's arithmetic is unchanged), grad_value within one bf16 rounding (fp32 partial sums added in
+    another order); the split backward is reproducible bit for bit."""
+    for k in ("MSDA_HIP_BWD_WIN", "MSDA_HIP_WIN_SPLIT", "MSDA_HIP_WIN_ORDER", "MSDA_HIP_BWD_PATH", "MSDA_HIP_QORDER",
+              "MSDA_HIP_WIN_LM", "MSDA_HIP_WIN_LM_SPLIT"):
+        monkeypatch.delenv(k, raising=False)
+    shapes, B, M, P = LM_CASES[case]
+    D, Lq = 64, sum(shapes)
+    value, _, aw, gout = rand_case(shapes, B, M, D, Lq, P, torch.bfloat16, seed=140 + case, lo=0.0, hi=1.0)
+    loc = local_locations(B, Lq, M, shapes, P, seed=141 + case)
+    starts = O.level_starts(shapes)
+    v, g = value.cuda(), gout.cuda()
+    lcm, am = _to_level_major(loc).cuda(), _to_level_major(aw).cuda()
+    _, tiles = msda.msda_forward(v, shapes, starts, lcm, am, padding, want_tiles=True, layout=msda.LEVEL_MAJOR)
+    monkeypatch.setenv("MSDA_HIP_WIN_LM_SPLIT", "1")
+    split = [msda.msda_backward(v, shapes, starts, lcm, am, g, padding, tiles=tiles, layout=msda.LEVEL_MAJOR)
+             for _ in range(2)]
+    monkeypatch.setenv("MSDA_HIP_WIN_LM_SPLIT", "0")
+    one = msda.msda_backward(v, shapes, starts, lcm, am, g, padding, tiles=tiles, layout=msda.LEVEL_MAJOR)
+    torch.cuda.synchronize()
+    for x, y in zip(split[0], split[1]):
+        assert torch.equal(x, y)
+    assert torch.equal(split[0][1], one[1]) and torch.equal(split[0][2], one[2])
+    a, b = split[0][0].float(), one[0].float()
+    torch.testing.assert_close(a, b, rtol=2 ** -8, atol=2 ** -8 * b.abs().max().item())
 
 
 @pytest.mark.parametrize("padding", ["border", "zeros"])

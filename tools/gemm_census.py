@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-GEMM efficiency of one bench step (bf16 autocast, B=8, T=1024, eager so every GEMM is
-attributable): every aten mm / addmm / bmm / baddbmm / convolution call grouped by input shapes,
+attributable; argv[2] "multimodal" for configs[2]): every aten mm / addmm / bmm / baddbmm / convolution call grouped by input shapes,
 its device time and its TFLOP/s against the bf16 dense MFMA peak (2.5 PFLOP/s,
 MI355X_MICROARCH.md).  Writes a CSV (argv[1]) and prints the table.  Diagnostic only."""
 import csv
@@ -36,12 +36,20 @@ def flops(name, shapes):
     return None
 
 
-def main(out_csv):
+def main(out_csv, config="video"):
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    model = PKG.dvc_core.DeformableDVCCore(d_model=512, num_queries=100, dropout=0.1).to(dev)
-    tr = PKG.train_step.FlatGradTrainer(model, PKG.dvc_core.workload_loss, graph=False)
-    batch = PKG.dvc_core.synthetic_clips(8, T=1024, device=dev)
+    dc = PKG.dvc_core
+    if config == "multimodal":  # configs[2]: bench.py --config multimodal's model and batch
+        model = dc.MultimodalDVCCore(d_model=512, num_queries=100, dropout=0.1).to(dev)
+        tr = PKG.train_step.FlatGradTrainer(model, dc.multimodal_workload_loss, graph=False)
+        video, mask, dur = dc.synthetic_clips(8, T=1024, device=dev)
+        audio, amask, _ = dc.synthetic_clips(8, T=50, seed=2000, device=dev)
+        batch = (video, mask, audio, amask, dur)
+    else:
+        model = dc.DeformableDVCCore(d_model=512, num_queries=100, dropout=0.1).to(dev)
+        tr = PKG.train_step.FlatGradTrainer(model, dc.workload_loss, graph=False)
+        batch = dc.synthetic_clips(8, T=1024, device=dev)
     for _ in range(3):
         tr.eager_step(batch)
     torch.cuda.synchronize()
@@ -79,4 +87,4 @@ def main(out_csv):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/gemm_census.csv")
+    main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/gemm_census.csv", sys.argv[2] if len(sys.argv) > 2 else "video")
