@@ -180,26 +180,35 @@ __global__ __launch_bounds__(kThreads) void word_prob_bwd(const float4* __restri
 
 // relu_dropout_bwd on a (rows x cols) matrix that also sums each column of dx as stored (bf16): the
 // bias gradient of the Linear layer that produced the hidden (linear1), which then needs no
-// column-sum pass over dx.  One block = kRdRows rows x 256 vectors of 8 columns; per-block column
+// column-sum pass over dx.  One block = rpb rows x blockDim.x vectors of 8 columns; per-block column
 // partials in fixed order, summed by relu_dropout_colsum_final in fixed order (deterministic).
+// rpb = 32 rows and 256-thread blocks for the encoder's ~16 K rows; the decoder / audio calls (760-800
+// rows) take 8 rows and one-wave blocks (rd_rows_per_block): with 32 they ran 25 blocks of 32
+// dependent-row rounds (15-20 us for 3 MB; 4-5 us now)
 constexpr int kRdRows = 32;
+constexpr int kRdRowsSmall = 8;
 constexpr int kRdUnroll = 8;  // rows whose loads are in flight together (one dependent row at a time: 2x slower)
+
+int rd_rows_per_block(long long rows, long long cvec) {
+  const long long waves = (rows + kRdRows - 1) / kRdRows * ((cvec + 63) / 64);
+  return waves >= 1024 ? kRdRows : kRdRowsSmall;
+}
 
 __global__ __launch_bounds__(kThreads) void relu_dropout_bwd_colsum(const uint4* __restrict__ dy,
                                                                    const uint4* __restrict__ out, long long rows,
-                                                                   int cvec, float scale, uint4* __restrict__ dx,
-                                                                   float* __restrict__ part) {
-  const int c = blockIdx.y * kThreads + threadIdx.x;
+                                                                   int cvec, int rpb, float scale,
+                                                                   uint4* __restrict__ dx, float* __restrict__ part) {
+  const int c = blockIdx.y * blockDim.x + threadIdx.x;
   if (c >= cvec) return;
-  const long long r0 = (long long)blockIdx.x * kRdRows;
+  const long long r0 = (long long)blockIdx.x * rpb;
   // (the last block's rows past the end re-read its last row and add nothing: branch-free loads, so
   // the compiler keeps kRdUnroll rows of loads in flight — with guarded loads it waited on each)
-  const int nr = (int)min((long long)kRdRows, rows - r0);
+  const int nr = (int)min((long long)rpb, rows - r0);
   float sum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const uint4* __restrict__ dyc = dy + r0 * cvec + c;
   const uint4* __restrict__ outc = out + r0 * cvec + c;
   uint4* __restrict__ dxc = dx + r0 * cvec + c;
-  for (int rr = 0; rr < kRdRows; rr += kRdUnroll) {
+  for (int rr = 0; rr < rpb; rr += kRdUnroll) {
     uint4 g[kRdUnroll], y[kRdUnroll];
 #pragma unroll
     for (int u = 0; u < kRdUnroll; ++u) {
@@ -229,22 +238,24 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_bwd_colsum(const uint4*
 }
 
 // colsum[j] = sum over the row groups' partials: a block = 16 row strides x 64 columns (the row
-// groups dealt over the 16, two independent chains each, then the 16 added in LDS; fixed order)
+// groups dealt over the 16, four independent chains each, then the 16 added in LDS; fixed order)
 __global__ __launch_bounds__(1024) void relu_dropout_colsum_final(const float* __restrict__ part, int ngroups,
                                                                  int cols, float* __restrict__ colsum) {
   __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + cl;
-  float s0 = 0.f, s1 = 0.f;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   if (j < cols) {
     int k = grp;
-    for (; k + 16 < ngroups; k += 32) {
+    for (; k + 48 < ngroups; k += 64) {
       s0 += part[(long long)k * cols + j];
       s1 += part[(long long)(k + 16) * cols + j];
+      s2 += part[(long long)(k + 32) * cols + j];
+      s3 += part[(long long)(k + 48) * cols + j];
     }
     for (; k < ngroups; k += 16) s0 += part[(long long)k * cols + j];
   }
-  red[grp][cl] = s0 + s1;
+  red[grp][cl] = (s0 + s1) + (s2 + s3);
   __syncthreads();
   if (grp == 0 && j < cols) {
     float t = 0.f;
@@ -675,7 +686,8 @@ int mfl_word_prob_backward(const float* probs, const int64_t* words, const float
 
 size_t mfl_relu_dropout_colsum_workspace_bytes(int64_t rows, int64_t cols) {
   if (rows <= 0 || cols <= 0) return 0;
-  return (size_t)((rows + kRdRows - 1) / kRdRows) * (size_t)cols * sizeof(float);
+  const int rpb = rd_rows_per_block(rows, cols / 8);
+  return (size_t)((rows + rpb - 1) / rpb) * (size_t)cols * sizeof(float);
 }
 
 int mfl_relu_dropout_backward_colsum(const void* dy, const void* out, int64_t rows, int64_t cols, float p_drop,
@@ -693,11 +705,13 @@ int mfl_relu_dropout_backward_colsum(const void* dy, const void* out, int64_t ro
   hipStream_t st = static_cast<hipStream_t>(stream);
   const float scale = dropped ? 1.f / (1.f - p_drop) : 1.f;
   const int cvec = (int)(cols / 8);
-  const long long groups = (rows + kRdRows - 1) / kRdRows;
+  const int rpb = rd_rows_per_block(rows, cvec);
+  const int bt = rpb == kRdRows ? kThreads : 64;
+  const long long groups = (rows + rpb - 1) / rpb;
   if (groups > 0) {
-    hipLaunchKernelGGL(relu_dropout_bwd_colsum, dim3((unsigned)groups, (unsigned)((cvec + kThreads - 1) / kThreads)),
-                       dim3(kThreads), 0, st, static_cast<const uint4*>(dy), static_cast<const uint4*>(out),
-                       (long long)rows, cvec, scale, static_cast<uint4*>(dx), static_cast<float*>(workspace));
+    hipLaunchKernelGGL(relu_dropout_bwd_colsum, dim3((unsigned)groups, (unsigned)((cvec + bt - 1) / bt)), dim3(bt), 0,
+                       st, static_cast<const uint4*>(dy), static_cast<const uint4*>(out), (long long)rows, cvec, rpb,
+                       scale, static_cast<uint4*>(dx), static_cast<float*>(workspace));
     int rc;
     if ((rc = status("backward (column sums)"))) return rc;
   }

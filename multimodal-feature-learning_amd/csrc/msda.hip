@@ -2576,9 +2576,9 @@ int run_forward(const Problem& pr, const void* value, const void* loc, const voi
   if constexpr (!std::is_same<coord_t, double>::value && VEC * sizeof(scalar_t) == 16) {
     const int G = fast16_group<scalar_t>(pr);
     if constexpr (std::is_same<scalar_t, bf16_t>::value) {
-      if (dense_takes(pr, MSDA_DTYPE_BF16)) {  // (tiles, when handed over, are not needed by its backward)
+      if (dense_takes(pr, MSDA_DTYPE_BF16)) {  // (tiles, when handed over, written as the tiles forward does)
         const WinShape sh = dense_win_shape(pr);
-        if (msda_dense_forward(value, loc, aw, out, &sh, pad == MSDA_PAD_ZEROS, lm ? 1 : 0, st) != 0) {
+        if (msda_dense_forward(value, loc, aw, out, tiles, &sh, pad == MSDA_PAD_ZEROS, lm ? 1 : 0, st) != 0) {
           set_error("msda forward: the dense small-pyramid kernel could not be launched");
           return MSDA_ERR_LAUNCH;
         }

@@ -161,8 +161,10 @@ __attribute__((visibility("hidden"))) int msda_win_backward(const void* value, c
 // Lq, L, P, T, start.  Return 0, or -1 when the shape does not fit (nothing launched).
 __attribute__((visibility("hidden"))) int msda_dense_supported(int value_dtype_is_bf16, long long D, long long S,
                                                                long long L, long long P);
+// tiles (may be null): the forward's tile buffer (msda_hip_forward_tiles_bytes), written as the tiles
+// forward writes it (consecutive tiles)
 __attribute__((visibility("hidden"))) int msda_dense_forward(const void* value, const void* loc, const void* aw,
-                                                             void* out, const WinShape* shape, int zeros,
+                                                             void* out, void* tiles, const WinShape* shape, int zeros,
                                                              int coord_layout, hipStream_t st);
 // workspace: msda_dense_workspace_bytes (the groups' fp32 partial sums of grad_value), or null (one
 // workgroup a (b, m), slower)

@@ -921,6 +921,7 @@ struct DnTaps {
   int row[P];
   float w0[P], w1[P], a[P], gmul[P];
   bool ok0[P], ok1[P];
+  int ivlo, ivhi;  // the rows the samples touch or own on their level (win_sample_rows: the tile intervals)
 };
 
 template <int P>
@@ -953,8 +954,13 @@ __device__ __forceinline__ void dn_taps(const float* __restrict__ lp, const floa
   float lc[P], ac[P];
   dn_load4<P>(lp, lc);
   dn_load4<P>(ap, ac);
+  tp.ivlo = kNone;
+  tp.ivhi = -kNone;
 #pragma unroll
   for (int p = 0; p < P; ++p) {
+    const int2 iv = win_sample_rows(lc[p], T, ZEROS);
+    tp.ivlo = min(tp.ivlo, iv.x);
+    tp.ivhi = max(tp.ivhi, iv.y);
     const Taps t = make_taps<ZEROS>(lc[p], T);
     tp.row[p] = st + t.base;
     tp.w0[p] = t.w0;
@@ -1192,12 +1198,17 @@ __global__ __launch_bounds__(256) void dense_sum_kernel(const float* __restrict_
 // One workgroup per (b, m, 128-query chunk), 4 waves: the (b, m) pyramid staged in LDS once (128-B
 // rows, lm_sw), then each wave takes 16-query tiles: threads (q, l) build the tile's C, then
 // out = C . V over the pyramid's rows in 32-row MFMA steps (B operands read transposed).
+// With `tiles` (the level-major calls' buffer, msda_hip_forward_tiles_bytes) it also writes the row
+// intervals of every (b, m, level, 32-query tile) and the buffer's tail as msda_fwd16_tiles_kernel
+// does for consecutive tiles (win_sample_rows, zero tail), so the buffer is defined whichever backward
+// later reads it.
 template <bool ZEROS, int P>
 __global__ __launch_bounds__(256) void dense_fwd_kernel(const uint16_t* __restrict__ value,
                                                         const float* __restrict__ loc,
                                                         const float* __restrict__ aw, uint16_t* __restrict__ out,
-                                                        const DenseShape sh) {
+                                                        int2* __restrict__ tiles, const DenseShape sh) {
   extern __shared__ __attribute__((aligned(16))) unsigned char s_dyn[];
+  __shared__ int2 s_iv[4][kDnMaxL];
   const int R = sh.R;
   const int tid = (int)threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
   unsigned char* const s_v = s_dyn;
@@ -1209,6 +1220,8 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(const uint16_t* __restri
   const long long b = bm / (unsigned)sh.M;
   const int rs = (int)sh.M * 64;
   const uint16_t* __restrict__ vb = value + (b * sh.S * sh.M + m) * 64;
+  if (tiles != nullptr && blockIdx.x == 0 && tid < (int)(kWinTailBytes / 16))  // the tail: zero (consecutive tiles)
+    reinterpret_cast<uint4*>(tiles + sh.B * sh.M * sh.L * sh.ntile)[tid] = make_uint4(0u, 0u, 0u, 0u);
   for (int i = tid; i < R * 8; i += 256) {
     const int row = i >> 3, ch = i & 7;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
@@ -1222,9 +1235,10 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(const uint16_t* __restri
   const long long cbase = b * sh.cb + m * sh.cm;
   for (int wt = 0; wt < sh.wt; ++wt) {
     const int q0 = ((int)chunk * sh.wt + wt) * 64 + wave * 16;
-    if (q0 >= sh.Lq) break;  // (wave-uniform)
     const bool own = cli < sh.L && q0 + cqi < sh.Lq;
     DnTaps<P> tp;
+    tp.ivlo = kNone;
+    tp.ivhi = -kNone;
     if (own) {
       const long long co = cbase + (long long)(q0 + cqi) * sh.cq + (long long)cli * sh.cl;
       dn_taps<ZEROS, P>(loc + co, aw + co, sh.T[cli], sh.start[cli], tp);
@@ -1233,6 +1247,25 @@ __global__ __launch_bounds__(256) void dense_fwd_kernel(const uint16_t* __restri
         *reinterpret_cast<uint16_t*>(s_clo + dn_fc(cqi, r)) = dn_lo(c);
       });
     }
+    if (tiles != nullptr) {
+      // the wave's 16 queries' intervals per level (lanes q * 4 + l), then the two waves of a 32-query
+      // tile combined through LDS (the barriers: every wave runs every wt)
+      int lo = tp.ivlo, hi = tp.ivhi;
+#pragma unroll
+      for (int o = 4; o < 64; o <<= 1) {
+        lo = min(lo, __shfl_xor(lo, o));
+        hi = max(hi, __shfl_xor(hi, o));
+      }
+      if (lane < kDnMaxL) s_iv[wave][lane] = make_int2(lo, hi);
+      __syncthreads();
+      const int tile = q0 / kQT;
+      if ((wave & 1) == 0 && lane < sh.L && tile < sh.ntile) {
+        const int2 o = s_iv[wave + 1][lane];
+        tiles[((long long)bm * sh.L + lane) * sh.ntile + tile] = make_int2(min(lo, o.x), max(hi, o.y));
+      }
+      __syncthreads();
+    }
+    if (q0 >= sh.Lq) continue;  // (wave-uniform: no products for a tile past the queries)
     wave_lds_fence();
     f32x4 acc[4];
 #pragma unroll
@@ -1338,8 +1371,8 @@ static int dense_lds_attr(K kernel, size_t bytes) {
              : -1;
 }
 
-int msda_dense_forward(const void* value, const void* loc, const void* aw, void* out, const WinShape* shape, int zeros,
-                       int coord_layout, hipStream_t st) {
+int msda_dense_forward(const void* value, const void* loc, const void* aw, void* out, void* tiles,
+                       const WinShape* shape, int zeros, int coord_layout, hipStream_t st) {
   DenseShape sh{};
   if (!dense_shape(shape, coord_layout, sh)) return -1;
   if (sh.B * sh.M == 0 || sh.Lq == 0) return 0;
@@ -1349,10 +1382,11 @@ int msda_dense_forward(const void* value, const void* loc, const void* aw, void*
   auto* lc = static_cast<const float*>(loc);
   auto* a = static_cast<const float*>(aw);
   auto* o = static_cast<uint16_t*>(out);
+  auto* tl = static_cast<int2*>(tiles);
 #define DN_FWD(Z, PP)                                                                                   \
   do {                                                                                                  \
     if (dense_lds_attr(dense_fwd_kernel<Z, PP>, lds)) return -1;                                        \
-    hipLaunchKernelGGL((dense_fwd_kernel<Z, PP>), dim3(grid), dim3(256), lds, st, v, lc, a, o, sh);      \
+    hipLaunchKernelGGL((dense_fwd_kernel<Z, PP>), dim3(grid), dim3(256), lds, st, v, lc, a, o, tl, sh);  \
   } while (0)
 #define DN_FWD_P(Z)                     \
   switch (sh.P) {                       \

@@ -624,11 +624,35 @@ class CrossAttention(nn.Module):
         self.projection_layer = Linear(d_model, d_model)
 
     def _mask(self, attn_mask, key_padding_mask):
-        m = attn_mask
-        if key_padding_mask is not None:
-            kpm = key_padding_mask.unsqueeze(1).unsqueeze(1)
-            m = kpm if m is None else (m | kpm)
+        """attn_mask | key_padding_mask (broadcast), built once per pair of mask tensors: the caption
+        decoder's layers all pass the step's same two masks, so its later layers reuse the first
+        one's (the key holds both tensors' identities and versions)."""
+        if key_padding_mask is None:
+            return attn_mask
+        key = (None if attn_mask is None else attn_mask._version, key_padding_mask._version)
+        cached = getattr(key_padding_mask, "_mfl_mask", None)
+        if cached is not None and cached[0] == key and cached[2] is attn_mask:  # (the entry holds attn_mask)
+            return cached[1]
+        kpm = key_padding_mask.unsqueeze(1).unsqueeze(1)
+        m = kpm if attn_mask is None else (attn_mask | kpm)
+        key_padding_mask._mfl_mask = (key, m, attn_mask)
         return m
+
+    def _sdpa_bias(self, masked, dtype):
+        """The additive -1e20*scale bias of a boolean mask for SDPA, once per mask tensor (the caption
+        decoder's layers share the step's mask, _mask), its last dimension padded to a multiple of 16
+        elements and handed over as a view: the fused kernel's alignment rule then needs no padded
+        copy per call."""
+        key = (dtype, self.scale, masked._version)
+        cached = getattr(masked, "_mfl_sdpa_bias", None)
+        if cached is not None and cached[0] == key:
+            return cached[1]
+        lk = masked.shape[-1]
+        full = torch.zeros(masked.shape[:-1] + ((lk + 15) // 16 * 16,), dtype=dtype, device=masked.device)
+        bias = full[..., :lk]
+        bias.masked_fill_(masked, -1e20 * self.scale)
+        masked._mfl_sdpa_bias = (key, bias)
+        return bias
 
     def forward(self, q, k, v, attn_mask=None, key_padding_mask=None, need_weights=False):
         assert k.shape == v.shape, (f"The keys and values inputted to the cross attention module should have the same "
@@ -672,7 +696,7 @@ class CrossAttention(nn.Module):
         else:
             bias = None
             if masked is not None:
-                bias = torch.zeros(masked.shape, dtype=q.dtype, device=q.device).masked_fill(masked, -1e20 * self.scale)
+                bias = self._sdpa_bias(masked, q.dtype)
             out = F.scaled_dot_product_attention(q, k, v, attn_mask=bias, scale=self.scale,
                                                  dropout_p=self.attention_dropout.p if self.training else 0.0)
             att = None

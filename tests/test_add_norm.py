@@ -297,7 +297,14 @@ def test_decoder_carry_matches_uncarried(dev, monkeypatch):
 def test_multimodal_layer_carry_matches_uncarried(dev, monkeypatch):
     """Multimodal encoder layer whose self blocks hand the cross-modal MSDA calls bf16(out) from the
     fused add + LayerNorm, against the same layer with the fp32 output (autocast casts it per call):
-    forward bit-identical (dropout 0), gradients to bf16-ulp tolerance."""
+    forward bit-identical (dropout 0), gradients to bf16-ulp tolerance.
+
+    Gradient bounds: 2^-7 of the norm, 2^-6 of the max element-wise.  Each path's gradient carries its
+    own bf16 rounding noise; against an fp64 truth of this layer (tools/mm_layer_dense_diag.py, run
+    r06o) the carried, uncarried, dense and non-dense runs are equally accurate (attention_weights
+    gradients 1.0e-2 off in norm for every one, the worst attention_weights.bias element 2.8-3.1 off
+    a max of 504), so two such paths differ by up to twice one path's error: 4.6 (0.9 % of the max)
+    at one bias element with the dense small-pyramid kernels, above the 2^-7 element bound."""
     MT = PKG.models.deformable.multimodal_deformable_transformer
     torch.manual_seed(2)
     B, d, vs, as_ = 2, 512, [128, 64, 32, 16], [50, 25, 13, 7]
@@ -335,7 +342,7 @@ def test_multimodal_layer_carry_matches_uncarried(dev, monkeypatch):
     for a, b in zip(o1, o2):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
     for a, b in zip(g1, g2):
-        torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -7 * b.abs().max().item())
+        torch.testing.assert_close(a, b, rtol=2 ** -7, atol=2 ** -6 * b.abs().max().item())
         # the FFN residual add is bf16 + bf16 (rounded to bf16 as autocast's add): one more bf16
         # rounding on both paths, so the carried / uncarried gradient noise is ~2^-8 of the norm
         assert (a - b).norm() <= 2 ** -7 * b.norm()

@@ -118,7 +118,7 @@ def test_graph_replays_draw_fresh_masks(dev):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("rows,cols", [(15360, 2048), (800, 2048), (37, 1024)])
+@pytest.mark.parametrize("rows,cols", [(15360, 2048), (16120, 2048), (800, 2048), (1001, 1032), (37, 1024)])
 def test_backward_hands_over_column_sums(dev, rows, cols):
     """The backward writes dx and its column sums in one pass (mfl_relu_dropout_backward_colsum) and
     hands them to the Linear that produced h (linear1's bias gradient, linear._given_colsum): dx equal

@@ -612,6 +612,7 @@ def test_staged_forward_equals_gathering_forward(dev, monkeypatch, case, padding
     fits, 48 / 32 rows; global gathers otherwise) gives the gathering tiles forward's output and tile
     intervals bit for bit, in both coordinate layouts — on encoder-like local sampling (windows
     staged) and on uniform / clustered sampling (windows over the cap: the fallback)."""
+    monkeypatch.setenv("MSDA_HIP_DENSE", "0")  # (the gathering forwards' tile protocol; tests/test_gpu_dense.py)
     for k in ("MSDA_HIP_FWD_LDS", "MSDA_HIP_QORDER", "MSDA_HIP_BWD_WIN"):
         monkeypatch.delenv(k, raising=False)
     monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
@@ -777,6 +778,7 @@ def test_lds_staged_forward_equals_gather_forward(dev, monkeypatch, case, paddin
     """The LDS-staged tiles forward (msda_fwd16_lds_kernel: each workgroup's per-level row
     intervals staged in LDS, taps read there; levels over the row budget gathered from global)
     gives the gathering tiles forward's output and tile intervals bit for bit."""
+    monkeypatch.setenv("MSDA_HIP_DENSE", "0")  # (the gathering forwards' tile protocol; tests/test_gpu_dense.py)
     monkeypatch.setenv("MSDA_HIP_BWD_WIN", "1")
     shapes, B, M, Lq, P, kind = WIN_CASES[case]
     value, loc, aw, _ = rand_case(shapes, B, M, 64, Lq, P, torch.bfloat16, seed=100 + case)

@@ -51,10 +51,11 @@ def main():
         torch.cuda.synchronize()
         return [("v.grad", v.grad), ("a.grad", a.grad)] + [(n, p.grad.clone()) for n, p in layer.named_parameters()]
 
-    base = run(True, False)
-    for name, (c, dn) in {"uncarried/nondense": (False, False), "carried/dense": (True, True),
-                          "uncarried/dense": (False, True), "carried/dense again": (True, True)}.items():
-        other = run(c, dn)
+    runs = {name: run(c, dn) for name, (c, dn) in {
+        "carried/nondense": (True, False), "uncarried/nondense": (False, False), "carried/dense": (True, True),
+        "uncarried/dense": (False, True), "carried/dense again": (True, True)}.items()}
+    base = runs["carried/nondense"]
+    for name, other in runs.items():
         print(f"== {name} vs carried/nondense")
         for (n, a), (_, b) in zip(base, other):
             rel = ((a - b).norm() / a.norm().clamp_min(1e-30)).item()
@@ -62,6 +63,34 @@ def main():
             if rel > 1e-3 or mx > 4e-3:
                 print(f"   {n:45s} rel {rel:.2e}  max/max {mx:.2e}")
     os.environ.pop("MSDA_HIP_DENSE", None)
+    MT.add_layer_norm_carry = carry_fn
+    # fp64 truth on the host (the oracle grid_sample core, oracle/cpu_model.py)
+    import copy
+    from oracle.cpu_model import oracle_core
+    cpu = torch.device("cpu")
+    lay64 = copy.deepcopy(layer).to(cpu).double()
+    d64 = lambda t: t.detach().to(cpu).double()  # noqa: E731
+    v, a = d64(v0).requires_grad_(True), d64(a0).requires_grad_(True)
+    with oracle_core(PKG):
+        ov, oa = lay64(v, d64(vp0), d64(vref), vts.cpu(), vlsi.cpu(), None, a, d64(ap0), d64(aref), ats.cpu(),
+                       alsi.cpu(), None)
+        (ov * d64(wv)).sum().add_((oa * d64(wa)).sum()).backward()
+    truth = [("v.grad", v.grad), ("a.grad", a.grad)] + [(n, p.grad) for n, p in lay64.named_parameters()]
+    print("== errors against the fp64 truth: |a - t| / |t| (norm), max |a - t| / max |t|")
+    for name, other in runs.items():
+        worst = []
+        for (n, t), (_, g) in zip(truth, other):
+            g = g.detach().to(cpu).double()
+            rel = ((g - t).norm() / t.norm().clamp_min(1e-30)).item()
+            mx = ((g - t).abs().max() / t.abs().max().clamp_min(1e-30)).item()
+            worst.append((rel, mx, n))
+        worst.sort(reverse=True)
+        print(f"   {name:22s} " + "; ".join(f"{n} {r:.1e}/{m:.1e}" for r, m, n in worst[:4]))
+        ab = dict((n, (g.detach().to(cpu).double(), t)) for (n, t), (_, g) in zip(truth, other))
+        g, t = ab["self_attn.attention_weights.bias"]
+        i = int((g - t).abs().argmax())
+        print(f"      attention_weights.bias worst element {i}: got {g[i]:.4f} truth {t[i]:.4f} "
+              f"(max |t| {t.abs().max():.2f})")
 
 
 if __name__ == "__main__":
