@@ -92,9 +92,12 @@ __device__ __forceinline__ bf16x8 zero8() {
 }
 __device__ __forceinline__ bf16x8 load8(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
 
-// the attention-dropout keep bits: a 32-bit mix (murmur3's finaliser) of the element index and the
-// seed folded to 32 bits — a few full-rate integer ops per element (the scores of one block take 32
-// draws a lane); the index ((s * H + h) * Lq + i) * K + j fits 32 bits (checked on the host)
+// the attention-dropout keep bits: a 32-bit mix (murmur3's finaliser) of a key-pair index and the
+// seed folded to 32 bits.  One draw covers keys 2i and 2i + 1 of a query row (row = (s * H + h) *
+// Lq + q): its low 16 bits decide key 2i, its high 16 bits key 2i + 1, kept iff >= p * 2^16.  The
+// finaliser's three 32-bit multiplies run at a quarter of the VALU rate, so a draw per key was ~17 us
+// of the DVC step's forward call; a draw per pair halves that.  The index row * ceil(K / 2) + i fits
+// 32 bits (n * H * Lq * K < 2^32 is checked on the host)
 __device__ __forceinline__ uint32_t drop_bits(uint32_t key, uint32_t e) {
   uint32_t x = e * 0x9E3779B1u + key;
   x ^= x >> 16;
@@ -104,9 +107,17 @@ __device__ __forceinline__ uint32_t drop_bits(uint32_t key, uint32_t e) {
   x ^= x >> 16;
   return x;
 }
-__device__ __forceinline__ float drop_mul(uint32_t key, uint32_t thresh, float dscale, uint32_t e) {
-  return (drop_bits(key, e) >> 8) >= thresh ? dscale : 0.f;
+__device__ __forceinline__ uint32_t drop_pair(uint32_t key, uint32_t row, int j, uint32_t k2) {
+  return drop_bits(key, row * k2 + ((uint32_t)j >> 1));
 }
+__device__ __forceinline__ bool pair_keep(uint32_t x, int j, uint32_t thresh) {
+  return ((j & 1) ? x >> 16 : x & 0xffffu) >= thresh;
+}
+__device__ __forceinline__ float drop_mul(uint32_t key, uint32_t thresh, float dscale, uint32_t row, int j,
+                                          uint32_t k2) {
+  return pair_keep(drop_pair(key, row, j, k2), j, thresh) ? dscale : 0.f;
+}
+__device__ __forceinline__ uint32_t drop_thresh(float p) { return (uint32_t)fminf(p * 65536.f, 65536.f); }
 __device__ __forceinline__ uint32_t drop_key(const int64_t* seed) {
   if (!seed) return 0u;
   const uint64_t v = (uint64_t)seed[0];
@@ -274,7 +285,7 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) o[qt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t seed = drop_key(a.seed);
-  const uint32_t thresh = (uint32_t)fminf(a.p * 16777216.f, 16777216.f);
+  const uint32_t thresh = drop_thresh(a.p), k2 = (uint32_t)(a.K + 1) >> 1;
   const float dscale = 1.f / (1.f - a.p);
   const uint16_t* bk = a.bk ? a.bk + h * HD : nullptr;
   const uint16_t* bv = a.bv ? a.bv + h * HD : nullptr;
@@ -346,30 +357,39 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
     uint32_t kept = 0u;  // the block's keep bits of this lane (dbits_at)
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
-      const int qi = qt * 16 + li;
+      const uint32_t row = (uint32_t)(s * a.H + h) * a.Lq + qt * 16 + li;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
+      for (int kt = 0; kt < 2; ++kt) {
+        uint32_t x[2] = {0u, 0u};  // keys j0 + kt*16 + 4g + {0, 1} and {2, 3}: one draw a pair
+        if (a.seed) {
+#pragma unroll
+          for (int rp = 0; rp < 2; ++rp) x[rp] = drop_pair(seed, row, j0 + kt * 16 + 4 * g + 2 * rp, k2);
+        }
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           float p = sc[kt][qt][r];
           if (a.seed) {
-            const uint32_t e = ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kt * 16 + 4 * g + r);
-            const bool k = (drop_bits(seed, e) >> 8) >= thresh;
+            const bool k = pair_keep(x[r >> 1], r, thresh);  // (= drop_mul: the key's parity is r's)
             kept |= (uint32_t)k << (kt * 8 + qt * 4 + r);
-            p *= k ? dscale : 0.f;  // (= drop_mul)
+            p *= k ? dscale : 0.f;
           }
           pa[qt][kt * 4 + r] = tobf(p);
         }
+      }
     }
     if (a.seed && a.dbits) a.dbits[dbits_at(a, s, h, blk, nblk) + lane] = (uint16_t)kept;
+    // rescale O only when some query's running max moved (alpha = exp(0) = 1 exactly otherwise, so
+    // skipping the multiplies is bitwise the same; after the first blocks the max rarely moves)
+    if (__ballot(alpha[0] != 1.f || alpha[1] != 1.f) != 0ull) {
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt)
+      for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float al = __shfl(alpha[qt], 4 * g + r);  // alpha of query qt*16 + 4g + r (lane li = 4g + r)
+        for (int r = 0; r < 4; ++r) {
+          const float al = __shfl(alpha[qt], 4 * g + r);  // alpha of query qt*16 + 4g + r (lane li = 4g + r)
 #pragma unroll
-        for (int cb = 0; cb < 4; ++cb) o[qt][cb][r] *= al;
-      }
+          for (int cb = 0; cb < 4; ++cb) o[qt][cb][r] *= al;
+        }
+    }
     wave_lds_fence();
 #pragma unroll
     for (int cb = 0; cb < 4; ++cb) {
@@ -483,7 +503,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   // dS and of P' — the bias gradients are sum_q cS[q] Q[q] and sum_q cA[q] dO[q]
   float cS[2] = {0.f, 0.f}, cA[2] = {0.f, 0.f};
   const uint32_t seed = drop_key(a.seed);
-  const uint32_t thresh = (uint32_t)fminf(a.p * 16777216.f, 16777216.f);
+  const uint32_t thresh = drop_thresh(a.p), k2 = (uint32_t)(a.K + 1) >> 1;
   const float dscale = 1.f / (1.f - a.p);
   const uint16_t* bk = a.bk ? a.bk + h * HD : nullptr;
   const uint16_t* bv = a.bv ? a.bv + h * HD : nullptr;
@@ -505,8 +525,8 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
             if (!((zr >> kk) & 1u)) continue;
             cA[qt] += kBits     ? p * (((wd >> (kt * 8 + qt * 4 + r)) & 1u) ? dscale : 0.f)
                       : !a.seed ? p
-                                : p * drop_mul(seed, thresh, dscale, ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K +
-                                                                         (bb * KB + kk));
+                                : p * drop_mul(seed, thresh, dscale, (uint32_t)(s * a.H + h) * a.Lq + qi,
+                                               bb * KB + kk, k2);
           }
       }
     }
@@ -549,6 +569,9 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
       if (bits) wb = a.dbits[dbits_at(a, s, h, nb, nblk) + lane];
     }
     bf16x8 da[2];  // A operand of dQ += dS K: row = query qt*16 + li, k slots = keys 4g.. | 16+4g..
+    // (wave-uniform) some key of the block reads the bias row: only then the per-score bias sums, and
+    // branch-free (a 0 / 1 factor in an fma: bitwise the conditional add)
+    const bool bias_rows = (mk.in & ~mk.keep) != 0u;
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
@@ -562,12 +585,13 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
           const float dm =
               bits      ? (((wc >> (kt * 8 + qt * 4 + r)) & 1u) ? dscale : 0.f)
               : !a.seed ? 1.f
-                        : drop_mul(seed, thresh, dscale, ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk));
+                        : drop_mul(seed, thresh, dscale, (uint32_t)(s * a.H + h) * a.Lq + qi, j0 + kk, k2);
           const float ds = p * (dp[kt][qt][r] * dm - Dq[qt]) * a.scale;
           da[qt][kt * 4 + r] = tobf(ds);
-          if (!((mk.keep >> kk) & 1u)) {
-            cS[qt] += ds;
-            cA[qt] += p * dm;
+          if (bias_rows) {
+            const float nk = ((mk.keep >> kk) & 1u) ? 0.f : 1.f;
+            cS[qt] = fmaf(nk, ds, cS[qt]);
+            cA[qt] = fmaf(nk, p * dm, cA[qt]);
           }
         }
       }
@@ -689,6 +713,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
   constexpr int kPart = 2 * 2 * 4 * 64 * 16;            // a wave's dK + dV tiles (f32x4 a lane)
   constexpr int kUnion = (kWaves - 1) * kPart > kWaves * kStage ? (kWaves - 1) * kPart : kWaves * kStage;
   __shared__ __attribute__((aligned(16))) unsigned char s_buf[kUnion];
+  __shared__ __attribute__((aligned(16))) unsigned char s_kv[2 * KB * kRS];  // the block's K, V rows
   __shared__ float s_lse[kWaves][QT], s_D[kWaves][QT];
   __shared__ int s_list[kListChunk];
   __shared__ int s_wcnt[kWaves];
@@ -705,18 +730,16 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
   const long long rbase = ((long long)b * a.K + j0) * d + h * HD;
   unsigned char* const sq = s_buf + wave * kStage;
   unsigned char* const sd = sq + QT * kRS;
-  // B operands of S = Q K^T and dP = dO V^T: column = key kt*16 + li (the projected rows; keys a
-  // segment reads as the bias row get no contribution here — seg_attn_bwd_dq sums those)
-  bf16x8 kP[2][2], vP[2][2];
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt) {
-    const bool ok = on && j0 + kt * 16 + li < a.K;
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const long long off = rbase + (long long)(kt * 16 + li) * d + ks * 32 + 8 * g;
-      kP[kt][ks] = ok ? load8(a.pk + off) : zero8();
-      vP[kt][ks] = ok ? load8(a.pv + off) : zero8();
-    }
+  // the block's projected K and V rows (B operands of S = Q K^T and dP = dO V^T: column = key kt*16
+  // + li; keys a segment reads as the bias row get no contribution here — seg_attn_bwd_dq sums
+  // those) staged once in LDS for the 4 waves, 16 bytes a thread: per-wave register copies cost 32
+  // VGPRs and made the kernel spill at 256
+  {
+    const int row = tid >> 3, ch = tid & 7;
+    const bool ok = on && j0 + row < a.K;
+    const long long off = rbase + (long long)row * d + ch * 8;
+    *reinterpret_cast<bf16x8*>(s_kv + row * kRS + ch * 16) = ok ? load8(a.pk + off) : zero8();
+    *reinterpret_cast<bf16x8*>(s_kv + (KB + row) * kRS + ch * 16) = ok ? load8(a.pv + off) : zero8();
   }
   f32x4 dk[2][4], dv[2][4];
 #pragma unroll
@@ -724,7 +747,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt) dk[kt][cb] = dv[kt][cb] = f32x4{0.f, 0.f, 0.f, 0.f};
   const uint32_t seed = drop_key(a.seed);
-  const uint32_t thresh = (uint32_t)fminf(a.p * 16777216.f, 16777216.f);
+  const uint32_t thresh = drop_thresh(a.p), k2 = (uint32_t)(a.K + 1) >> 1;
   const float dscale = 1.f / (1.f - a.p);
   for (int c0 = 0; c0 < a.n; c0 += kListChunk) {
     // the segments of this chunk that read clip b, in order (4 candidates a thread, block prefix sum)
@@ -782,22 +805,30 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
       if (wts == 0u) continue;
       wave_lds_fence();
       bf16x8 aa[2], sa[2];  // A operands (row = key kt*16 + li, k slots = queries 4g.. | 16+4g..): P', dS
+      bf16x8 qa[2][2], oa[2][2];
 #pragma unroll
-      for (int qt = 0; qt < 2; ++qt) {
-        bf16x8 qa[2], oa[2];
+      for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const int row = perm_row(qt * 16 + li);
-          qa[ks] = *reinterpret_cast<const bf16x8*>(sq + row * kRS + (ks * 32 + 8 * g) * 2);
-          oa[ks] = *reinterpret_cast<const bf16x8*>(sd + row * kRS + (ks * 32 + 8 * g) * 2);
+          qa[qt][ks] = *reinterpret_cast<const bf16x8*>(sq + row * kRS + (ks * 32 + 8 * g) * 2);
+          oa[qt][ks] = *reinterpret_cast<const bf16x8*>(sd + row * kRS + (ks * 32 + 8 * g) * 2);
         }
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt) {
+      for (int kt = 0; kt < 2; ++kt) {
+        bf16x8 kb[2], vb[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          kb[ks] = *reinterpret_cast<const bf16x8*>(s_kv + (kt * 16 + li) * kRS + (ks * 32 + 8 * g) * 2);
+          vb[ks] = *reinterpret_cast<const bf16x8*>(s_kv + (KB + kt * 16 + li) * kRS + (ks * 32 + 8 * g) * 2);
+        }
+#pragma unroll
+        for (int qt = 0; qt < 2; ++qt) {
           f32x4 st = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-          st = mfma(qa[0], kP[kt][0], st);
-          st = mfma(qa[1], kP[kt][1], st);
-          dp = mfma(oa[0], vP[kt][0], dp);
-          dp = mfma(oa[1], vP[kt][1], dp);
+          st = mfma(qa[qt][0], kb[0], st);
+          st = mfma(qa[qt][1], kb[1], st);
+          dp = mfma(oa[qt][0], vb[0], dp);
+          dp = mfma(oa[qt][1], vb[1], dp);
           const int kk = kt * 16 + li;
           const bool w = (wts >> kk) & 1u;
 #pragma unroll
@@ -806,8 +837,8 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
             const float p = !w ? 0.f : __expf((dead ? 0.f : st[r] * a.scale) - s_lse[wave][qi]);
             const float dm = kBits     ? (((dmk >> (kt * 8 + qt * 4 + r)) & 1u) ? dscale : 0.f)
                              : !a.seed ? 1.f
-                                       : drop_mul(seed, thresh, dscale,
-                                                  ((uint32_t)(s * a.H + h) * a.Lq + qi) * a.K + (j0 + kk));
+                                       : drop_mul(seed, thresh, dscale, (uint32_t)(s * a.H + h) * a.Lq + qi,
+                                                  j0 + kk, k2);
             aa[kt][qt * 4 + r] = tobf(p * dm);
             sa[kt][qt * 4 + r] = tobf(dead ? 0.f : p * (dp[r] * dm - s_D[wave][qi]) * a.scale);
           }

@@ -15,17 +15,21 @@ pytestmark = pytest.mark.gpu
 
 
 def _drop_keep(seed, n, H, Lq, K, p):
-    """The kernels' keep bits (seg_attention.hip drop_bits) for element ((s*H + h)*Lq + i)*K + j."""
+    """The kernels' keep bits (seg_attention.hip drop_pair / pair_keep): one 32-bit draw per key pair
+    (2i, 2i + 1) of query row r = (s*H + h)*Lq + q, at index r * ceil(K / 2) + i; its low 16 bits
+    decide key 2i, its high 16 bits key 2i + 1 (kept iff >= p * 2^16)."""
     key = np.uint32((seed & 0xffffffff) ^ (seed >> 32))
+    k2 = (K + 1) // 2
     with np.errstate(over="ignore"):
-        x = np.arange(n * H * Lq * K, dtype=np.uint32) * np.uint32(0x9E3779B1) + key
+        x = np.arange(n * H * Lq * k2, dtype=np.uint32) * np.uint32(0x9E3779B1) + key
         x ^= x >> np.uint32(16)
         x *= np.uint32(0x85EBCA6B)
         x ^= x >> np.uint32(13)
         x *= np.uint32(0xC2B2AE35)
         x ^= x >> np.uint32(16)
-    thresh = np.uint32(min(p * 16777216.0, 16777216.0))
-    return torch.from_numpy(((x >> np.uint32(8)) >= thresh).reshape(n, H, Lq, K))
+    half = np.stack([x & np.uint32(0xffff), x >> np.uint32(16)], axis=-1).reshape(n * H * Lq, 2 * k2)[:, :K]
+    thresh = np.uint32(min(p * 65536.0, 65536.0))
+    return torch.from_numpy((half >= thresh).reshape(n, H, Lq, K))
 
 
 def _reference(q, pk, pv, bk, bv, index, keep, masked, H, scale, drop=None, p=0.0):

@@ -15,8 +15,10 @@ from collections import defaultdict
 
 
 def short(name):
-    m = re.search(r"((?:msda|win)_\w+?)<(.*?)>\(", name)
-    return None if not m else f"{m.group(1)}<{m.group(2).replace('(anonymous namespace)::', '')}>"
+    m = re.search(r"((?:msda|win|dense)_\w+?)(?:<(.*?)>)?\(", name)
+    if not m:
+        return None
+    return f"{m.group(1)}<{(m.group(2) or '').replace('(anonymous namespace)::', '')}>"
 
 
 def main(root):
