@@ -306,9 +306,18 @@ __global__ __launch_bounds__(256) void sum_slabs_kernel(const float4* __restrict
   for (long long j = (long long)blockIdx.x * 256 + threadIdx.x; j < n4; j += (long long)gridDim.x * 256) {
     const long long i = j;
     float4 a = pg[i];
-    for (int k = 1; k < s; ++k) {
-      const float4 b = pg[(long long)k * n4 + i];
-      a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+    // slabs 8 at a time: the 8 loads issued together (branch-free: a slab index past the end re-reads
+    // the last slab and is not added), then added in slab order — bitwise the sequential sum.  One
+    // dependent load per slab made a 512 x 512 sum of 8 slabs take ~5 us for 9 MB
+    for (int k = 1; k < s; k += 8) {
+      float4 b[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) b[u] = pg[(long long)min(k + u, s - 1) * n4 + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (k + u < s) {
+          a.x += b[u].x; a.y += b[u].y; a.z += b[u].z; a.w += b[u].w;
+        }
     }
     if (accumulate) {
       const float4 o = out[j];

@@ -310,3 +310,17 @@ def test_slab_and_column_sums_accumulate(dev):
         want = base + g2.float().sum(0)
         L._bias_grad(g2, base, accumulate=True)
         torch.testing.assert_close(base, want, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("s", [1, 2, 7, 8, 9, 16, 17])
+def test_slab_sum_is_the_sequential_sum(dev, s):
+    """sum_slabs_kernel loads up to 8 slabs at once but adds them in slab order: bitwise the
+    sequential fp32 sum part[0] + part[1] + ... for any slab count (partial last group of 8)."""
+    L = PKG.models.modules.linear
+    g = torch.Generator(device=dev).manual_seed(s)
+    part = torch.randn(s, 96, 40, device=dev, generator=g) * torch.logspace(-3, 3, 40, device=dev)
+    want = part[0].clone()
+    for k in range(1, s):
+        want += part[k]
+    torch.testing.assert_close(L._sum_slabs(part), want, rtol=0, atol=0)
