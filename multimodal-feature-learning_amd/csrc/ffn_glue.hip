@@ -266,17 +266,25 @@ __global__ __launch_bounds__(1024) void relu_dropout_colsum_final(const float* _
 }
 
 // value.masked_fill(padding_mask[..., None], 0) of MSDeformAttn (reference attention.py:462-463) in
-// place, and the same on its gradient: one wave per row reads the row's mask byte and stores zeros
-// only when the row is padding, so an all-valid batch costs the mask read, not a pass over value.
-// Row i of x uses mask[i % mask_rows] (a batch of matrices sharing one token mask).
+// place, and the same on its gradient: a wave reads the mask bytes of 64 rows (one a lane) and zeroes
+// only the padding rows among them, one row at a time with all its lanes, so an all-valid batch
+// costs the mask read, not a pass over value.  (One wave per row before: 16 K waves that each read
+// one byte, ~5 us a call at the encoder's 15,360 rows.)  Row i of x uses mask[i % mask_rows] (a batch
+// of matrices sharing one token mask).
 __global__ __launch_bounds__(kThreads) void zero_masked_rows_kernel(uint4* __restrict__ x, long long rows,
                                                                    int vec_per_row,
                                                                    const uint8_t* __restrict__ mask,
                                                                    long long mask_rows) {
-  const long long row = (long long)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
-  if (row >= rows || mask[row % mask_rows] == 0) return;  // wave-uniform
-  uint4* p = x + row * vec_per_row;
-  for (int i = threadIdx.x & 63; i < vec_per_row; i += 64) p[i] = make_uint4(0u, 0u, 0u, 0u);
+  const int lane = threadIdx.x & 63;
+  const long long row0 = ((long long)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6)) * 64;
+  const long long row = row0 + lane;
+  unsigned long long pad = __ballot(row < rows && mask[row % mask_rows] != 0);
+  while (pad != 0ull) {  // (wave-uniform)
+    const int r = __builtin_ctzll(pad);
+    pad &= pad - 1ull;
+    uint4* p = x + (row0 + r) * vec_per_row;
+    for (int i = lane; i < vec_per_row; i += 64) p[i] = make_uint4(0u, 0u, 0u, 0u);
+  }
 }
 
 unsigned grid_for(long long nvec) {
@@ -763,7 +771,7 @@ int mfl_zero_masked_rows_batched(void* x, int64_t nbatch, int64_t rows, int64_t 
     return 1;
   }
   const long long total = nbatch * rows;
-  const long long blocks = (total + kThreads / 64 - 1) / (kThreads / 64);
+  const long long blocks = (total + kThreads - 1) / kThreads;  // 64 rows a wave
   hipLaunchKernelGGL(zero_masked_rows_kernel, dim3((unsigned)blocks), dim3(kThreads), 0,
                      static_cast<hipStream_t>(stream), static_cast<uint4*>(x), total, (int)(row_bytes / 16), mask,
                      (long long)rows);
