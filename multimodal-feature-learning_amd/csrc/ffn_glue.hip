@@ -238,24 +238,22 @@ __global__ __launch_bounds__(kThreads) void relu_dropout_bwd_colsum(const uint4*
 }
 
 // colsum[j] = sum over the row groups' partials: a block = 16 row strides x 64 columns (the row
-// groups dealt over the 16, four independent chains each, then the 16 added in LDS; fixed order)
+// groups dealt over the 16, eight independent chains each, then the 16 added in LDS; fixed order)
 __global__ __launch_bounds__(1024) void relu_dropout_colsum_final(const float* __restrict__ part, int ngroups,
                                                                  int cols, float* __restrict__ colsum) {
   __shared__ float red[16][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + cl;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  float sc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   if (j < cols) {
     int k = grp;
-    for (; k + 48 < ngroups; k += 64) {
-      s0 += part[(long long)k * cols + j];
-      s1 += part[(long long)(k + 16) * cols + j];
-      s2 += part[(long long)(k + 32) * cols + j];
-      s3 += part[(long long)(k + 48) * cols + j];
+    for (; k + 112 < ngroups; k += 128) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sc[u] += part[(long long)(k + 16 * u) * cols + j];
     }
-    for (; k < ngroups; k += 16) s0 += part[(long long)k * cols + j];
+    for (; k < ngroups; k += 16) sc[0] += part[(long long)k * cols + j];
   }
-  red[grp][cl] = (s0 + s1) + (s2 + s3);
+  red[grp][cl] = ((sc[0] + sc[1]) + (sc[2] + sc[3])) + ((sc[4] + sc[5]) + (sc[6] + sc[7]));
   __syncthreads();
   if (grp == 0 && j < cols) {
     float t = 0.f;

@@ -264,7 +264,7 @@ __global__ __launch_bounds__(kSmallCL * kSmallRL) void colsum_small(const T* __r
 }
 
 // out[c] = sum over chunks of part[k][c]: 16 chunk groups x 64 columns per 1024-thread block,
-// each thread a strided quarter-unrolled run over its chunks, then an LDS reduction over the
+// each thread a strided run over its chunks in eight independent chains, then an LDS reduction over the
 // groups (fixed order: deterministic).
 constexpr int kFinGroups = 16;
 __global__ __launch_bounds__(kFinGroups * 64) void colsum_final(const float* __restrict__ part, int nchunks, int N,
@@ -272,18 +272,16 @@ __global__ __launch_bounds__(kFinGroups * 64) void colsum_final(const float* __r
   __shared__ float red[kFinGroups][64];
   const int c_l = threadIdx.x & 63, g = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + c_l;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  float sc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // eight independent chains, fixed order
   if (c < N) {
     int k = g;
-    for (; k + 3 * kFinGroups < nchunks; k += 4 * kFinGroups) {
-      s0 += part[(long long)k * N + c];
-      s1 += part[(long long)(k + kFinGroups) * N + c];
-      s2 += part[(long long)(k + 2 * kFinGroups) * N + c];
-      s3 += part[(long long)(k + 3 * kFinGroups) * N + c];
+    for (; k + 7 * kFinGroups < nchunks; k += 8 * kFinGroups) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) sc[u] += part[(long long)(k + u * kFinGroups) * N + c];
     }
-    for (; k < nchunks; k += kFinGroups) s0 += part[(long long)k * N + c];
+    for (; k < nchunks; k += kFinGroups) sc[0] += part[(long long)k * N + c];
   }
-  red[g][c_l] = (s0 + s1) + (s2 + s3);
+  red[g][c_l] = ((sc[0] + sc[1]) + (sc[2] + sc[3])) + ((sc[4] + sc[5]) + (sc[6] + sc[7]));
   __syncthreads();
   if (g == 0 && c < N) {
     float t = 0.f;
