@@ -118,6 +118,11 @@ __device__ __forceinline__ float drop_mul(uint32_t key, uint32_t thresh, float d
   return pair_keep(drop_pair(key, row, j, k2), j, thresh) ? dscale : 0.f;
 }
 __device__ __forceinline__ uint32_t drop_thresh(float p) { return (uint32_t)fminf(p * 65536.f, 65536.f); }
+// bit i of w ? dscale : 0 — the bit sign-extended to an all-ones / zero mask over dscale's bits (two
+// VALU ops against the compare-and-select's three; bitwise the same value)
+__device__ __forceinline__ float bit_scale(uint32_t w, int i, float dscale) {
+  return __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)w, i, 1) & __float_as_uint(dscale));
+}
 __device__ __forceinline__ uint32_t drop_key(const int64_t* seed) {
   if (!seed) return 0u;
   const uint64_t v = (uint64_t)seed[0];
@@ -287,6 +292,7 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
   const uint32_t seed = drop_key(a.seed);
   const uint32_t thresh = drop_thresh(a.p), k2 = (uint32_t)(a.K + 1) >> 1;
   const float dscale = 1.f / (1.f - a.p);
+  const float sce = dead ? 0.f : a.scale;  // (wave-uniform)
   const uint16_t* bk = a.bk ? a.bk + h * HD : nullptr;
   const uint16_t* bv = a.bv ? a.bv + h * HD : nullptr;
   unsigned char* const sv = s_raw + wave * KB * kRS;
@@ -304,6 +310,9 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
     const BlockMasks mk{in_mask(j0, a.K), s_live[blk], s_keep[blk]};
     wave_lds_fence();
     store_frags(sv, vf, g, li);
+    // keys with a score: the unmasked ones, or every existing key of a dead segment, whose scores are
+    // all 0 (t * 0: the same softmax as the constant 0 — a signed zero changes no exp or max result)
+    const uint32_t ok = dead ? mk.in : (mk.in & mk.live);
     float sc[2][2][4];  // [kt][qt][r]: key kt*16 + 4g + r, query qt*16 + li
 #pragma unroll
     for (int kt = 0; kt < 2; ++kt)
@@ -315,8 +324,7 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int kk = kt * 16 + 4 * g + r;
-          const bool in = (mk.in >> kk) & 1u, live = (mk.live >> kk) & 1u;
-          sc[kt][qt][r] = !in ? kNegInf : dead ? 0.f : live ? t[r] * a.scale : kNegInf;
+          sc[kt][qt][r] = ((ok >> kk) & 1u) ? t[r] * sce : kNegInf;
         }
       }
     const int nb = next_active(s_live, blk + kWaves, nblk, dead);
@@ -580,10 +588,10 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int kk = kt * 16 + 4 * g + r;
-          const bool live = (mk.live >> kk) & 1u;
-          const float p = live ? __expf(st[kt][qt][r] * a.scale - lse[qt]) : 0.f;
+          const uint32_t lm = (uint32_t)__builtin_amdgcn_sbfe((int)mk.live, kk, 1);  // (masked exp: see dK / dV)
+          const float p = __uint_as_float(__float_as_uint(__expf(st[kt][qt][r] * a.scale - lse[qt])) & lm);
           const float dm =
-              bits      ? (((wc >> (kt * 8 + qt * 4 + r)) & 1u) ? dscale : 0.f)
+              bits      ? bit_scale(wc, kt * 8 + qt * 4 + r, dscale)
               : !a.seed ? 1.f
                         : drop_mul(seed, thresh, dscale, (uint32_t)(s * a.H + h) * a.Lq + qi, j0 + kk, k2);
           const float ds = p * (dp[kt][qt][r] * dm - Dq[qt]) * a.scale;
@@ -791,6 +799,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
         s_D[wave][lane] = pf.D;
       }
       const bool dead = pf.dead != 0;
+      const float sc = dead ? 0.f : a.scale;  // (wave-uniform)
       const bool lo = lane < 32;
       const uint32_t live = (uint32_t)__ballot(lo && pf.mb == 0u) & inm;
       const uint32_t keep = (uint32_t)__ballot(lo && pf.kb != 0u) & inm;
@@ -830,17 +839,21 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
           dp = mfma(oa[qt][0], vb[0], dp);
           dp = mfma(oa[qt][1], vb[1], dp);
           const int kk = kt * 16 + li;
-          const bool w = (wts >> kk) & 1u;
+          // all-ones where key kk has a weight: exp is taken for every score and masked (bitwise the
+          // select; as `w ? exp : 0` the compiler branched around each exp under a lane mask)
+          const uint32_t wm = (uint32_t)__builtin_amdgcn_sbfe((int)wts, kk, 1);
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int qi = qt * 16 + 4 * g + r;
-            const float p = !w ? 0.f : __expf((dead ? 0.f : st[r] * a.scale) - s_lse[wave][qi]);
-            const float dm = kBits     ? (((dmk >> (kt * 8 + qt * 4 + r)) & 1u) ? dscale : 0.f)
+            // (sc = 0 for a dead segment: st * 0 and the dS product's * 0 are the zeros the dead
+            // branch gave, bitwise — the finite operands' signed zeros add nothing to dK / dV)
+            const float p = __uint_as_float(__float_as_uint(__expf(st[r] * sc - s_lse[wave][qi])) & wm);
+            const float dm = kBits     ? bit_scale(dmk, kt * 8 + qt * 4 + r, dscale)
                              : !a.seed ? 1.f
                                        : drop_mul(seed, thresh, dscale, (uint32_t)(s * a.H + h) * a.Lq + qi,
                                                   j0 + kk, k2);
             aa[kt][qt * 4 + r] = tobf(p * dm);
-            sa[kt][qt * 4 + r] = tobf(dead ? 0.f : p * (dp[r] * dm - s_D[wave][qi]) * a.scale);
+            sa[kt][qt * 4 + r] = tobf(p * (dp[r] * dm - s_D[wave][qi]) * sc);
           }
         }
       }
