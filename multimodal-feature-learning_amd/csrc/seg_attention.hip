@@ -41,6 +41,7 @@ constexpr int kRS = 144;     // LDS row stride (bytes): 64 bf16 + 16 B, 16-B ali
 constexpr int kMaxBlk = 256;     // key blocks per segment held as LDS bit words: K <= 8192
 constexpr int kListChunk = 1024;  // segments scanned per pass of seg_attn_bwd_dkv's clip list
 constexpr float kNegInf = -INFINITY;
+constexpr float kLog2e = 1.4426950408889634f;
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
@@ -139,6 +140,30 @@ __device__ __forceinline__ bf16x8 tr_b(const unsigned char* tile, int g, int li,
   const int col = (cb * 16 + 4 * pp) * 2;
   const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(tile + (8 * g + qq) * kRS + col));
   const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(tile + (8 * g + 4 + qq) * kRS + col));
+  return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
+// seg_attn_bwd_dkv's Q / dO tiles: 128-B rows, 16-B chunk c of row r at slot c ^ qs_sw(r), qs_sw(r) =
+// bits (0, 3, 1) of r.  A search over the GF(2) maps of the row bits: the one under which the
+// row-fragment writes (rows perm_row(kt*16 + li), chunks ks*4 + g), the A-operand ds_read_b128 reads
+// (the same rows) and the transposed B reads (rows 8g + qq (+4), 8-B pieces) all meet distinct banks
+// in their lane groups — the 144-B padded rows left two lanes on a bank in each of them
+__device__ __forceinline__ int qs_sw(int r) { return (r & 1) | (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2); }
+__device__ __forceinline__ int qs_at(int r, int c) { return r * 128 + ((c ^ qs_sw(r)) << 4); }
+
+__device__ __forceinline__ void store_frags_sw(unsigned char* tile, const bf16x8 (&f)[2][2], int g, int li) {
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+      *reinterpret_cast<bf16x8*>(tile + qs_at(perm_row(kt * 16 + li), ks * 4 + g)) = f[kt][ks];
+}
+
+__device__ __forceinline__ bf16x8 tr_b_sw(const unsigned char* tile, int g, int li, int cb) {
+  const int qq = li >> 2, pp = li & 3;
+  const int c = cb * 2 + (pp >> 1), w8 = (pp & 1) * 8;
+  const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(tile + qs_at(8 * g + qq, c) + w8));
+  const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(tile + qs_at(8 * g + 4 + qq, c) + w8));
   return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
@@ -717,11 +742,14 @@ __device__ __forceinline__ void load_segment(const Args& a, int s, int h, int d,
 // through LDS at the end
 template <bool kBits>
 __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
-  constexpr int kStage = 2 * QT * kRS;                  // a wave's Q + dO rows
+  constexpr int kStage = 2 * QT * 128;                  // a wave's Q + dO rows (qs_at layout)
   constexpr int kPart = 2 * 2 * 4 * 64 * 16;            // a wave's dK + dV tiles (f32x4 a lane)
   constexpr int kUnion = (kWaves - 1) * kPart > kWaves * kStage ? (kWaves - 1) * kPart : kWaves * kStage;
   __shared__ __attribute__((aligned(16))) unsigned char s_buf[kUnion];
-  __shared__ __attribute__((aligned(16))) unsigned char s_kv[2 * KB * kRS];  // the block's K, V rows
+  // the block's K, V rows: 128-B rows, 16-B chunk c of row r at slot c ^ ((r >> 1) & 7) — the B-operand
+  // reads (rows kt*16 + li, chunks ks*4 + g) then meet 16 distinct slots in each ds_read_b128 lane group
+  // (the 144-B padded rows of the Q / dO tiles put two lanes of a group on most slots)
+  __shared__ __attribute__((aligned(16))) unsigned char s_kv[2 * KB * 128];
   __shared__ float s_lse[kWaves][QT], s_D[kWaves][QT];
   __shared__ int s_list[kListChunk];
   __shared__ int s_wcnt[kWaves];
@@ -737,7 +765,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
   const uint32_t inm = in_mask(j0, a.K);
   const long long rbase = ((long long)b * a.K + j0) * d + h * HD;
   unsigned char* const sq = s_buf + wave * kStage;
-  unsigned char* const sd = sq + QT * kRS;
+  unsigned char* const sd = sq + QT * 128;
   // the block's projected K and V rows (B operands of S = Q K^T and dP = dO V^T: column = key kt*16
   // + li; keys a segment reads as the bias row get no contribution here — seg_attn_bwd_dq sums
   // those) staged once in LDS for the 4 waves, 16 bytes a thread: per-wave register copies cost 32
@@ -746,8 +774,9 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
     const int row = tid >> 3, ch = tid & 7;
     const bool ok = on && j0 + row < a.K;
     const long long off = rbase + (long long)row * d + ch * 8;
-    *reinterpret_cast<bf16x8*>(s_kv + row * kRS + ch * 16) = ok ? load8(a.pk + off) : zero8();
-    *reinterpret_cast<bf16x8*>(s_kv + (KB + row) * kRS + ch * 16) = ok ? load8(a.pv + off) : zero8();
+    const int sw = (ch ^ ((row >> 1) & 7)) << 4;
+    *reinterpret_cast<bf16x8*>(s_kv + row * 128 + sw) = ok ? load8(a.pk + off) : zero8();
+    *reinterpret_cast<bf16x8*>(s_kv + (KB + row) * 128 + sw) = ok ? load8(a.pv + off) : zero8();
   }
   f32x4 dk[2][4], dv[2][4];
 #pragma unroll
@@ -792,14 +821,15 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
     for (int it = wave; it < total; it += kWaves) {
       const int s = s_list[it];
       wave_lds_fence();  // the previous segment's LDS reads are issued before these writes
-      store_frags(sq, pf.q, g, li);
-      store_frags(sd, pf.o, g, li);
+      store_frags_sw(sq, pf.q, g, li);
+      store_frags_sw(sd, pf.o, g, li);
       if (lane < QT) {
-        s_lse[wave][lane] = pf.lse;
+        s_lse[wave][lane] = pf.lse * kLog2e;  // (base-2: P = 2^(S sc log2 e - lse log2 e))
         s_D[wave][lane] = pf.D;
       }
       const bool dead = pf.dead != 0;
       const float sc = dead ? 0.f : a.scale;  // (wave-uniform)
+      const float sc2 = sc * kLog2e;
       const bool lo = lane < 32;
       const uint32_t live = (uint32_t)__ballot(lo && pf.mb == 0u) & inm;
       const uint32_t keep = (uint32_t)__ballot(lo && pf.kb != 0u) & inm;
@@ -820,16 +850,17 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const int row = perm_row(qt * 16 + li);
-          qa[qt][ks] = *reinterpret_cast<const bf16x8*>(sq + row * kRS + (ks * 32 + 8 * g) * 2);
-          oa[qt][ks] = *reinterpret_cast<const bf16x8*>(sd + row * kRS + (ks * 32 + 8 * g) * 2);
+          qa[qt][ks] = *reinterpret_cast<const bf16x8*>(sq + qs_at(row, ks * 4 + g));
+          oa[qt][ks] = *reinterpret_cast<const bf16x8*>(sd + qs_at(row, ks * 4 + g));
         }
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         bf16x8 kb[2], vb[2];
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          kb[ks] = *reinterpret_cast<const bf16x8*>(s_kv + (kt * 16 + li) * kRS + (ks * 32 + 8 * g) * 2);
-          vb[ks] = *reinterpret_cast<const bf16x8*>(s_kv + (KB + kt * 16 + li) * kRS + (ks * 32 + 8 * g) * 2);
+          const int r = kt * 16 + li, sw = ((ks * 4 + g) ^ ((r >> 1) & 7)) << 4;
+          kb[ks] = *reinterpret_cast<const bf16x8*>(s_kv + r * 128 + sw);
+          vb[ks] = *reinterpret_cast<const bf16x8*>(s_kv + (KB + r) * 128 + sw);
         }
 #pragma unroll
         for (int qt = 0; qt < 2; ++qt) {
@@ -847,7 +878,9 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
             const int qi = qt * 16 + 4 * g + r;
             // (sc = 0 for a dead segment: st * 0 and the dS product's * 0 are the zeros the dead
             // branch gave, bitwise — the finite operands' signed zeros add nothing to dK / dV)
-            const float p = __uint_as_float(__float_as_uint(__expf(st[r] * sc - s_lse[wave][qi])) & wm);
+            // (one fma + v_exp_f32 on base-2 operands: __expf's x * log2 e multiply folded into them)
+            const float p = __uint_as_float(
+                __float_as_uint(__builtin_amdgcn_exp2f(fmaf(st[r], sc2, -s_lse[wave][qi]))) & wm);
             const float dm = kBits     ? bit_scale(dmk, kt * 8 + qt * 4 + r, dscale)
                              : !a.seed ? 1.f
                                        : drop_mul(seed, thresh, dscale, (uint32_t)(s * a.H + h) * a.Lq + qi,
@@ -859,7 +892,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
       }
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        const bf16x8 ob = tr_b(sd, g, li, cb), qb = tr_b(sq, g, li, cb);
+        const bf16x8 ob = tr_b_sw(sd, g, li, cb), qb = tr_b_sw(sq, g, li, cb);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           dv[kt][cb] = mfma(aa[kt], ob, dv[kt][cb]);
