@@ -750,7 +750,8 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
   // reads (rows kt*16 + li, chunks ks*4 + g) then meet 16 distinct slots in each ds_read_b128 lane group
   // (the 144-B padded rows of the Q / dO tiles put two lanes of a group on most slots)
   __shared__ __attribute__((aligned(16))) unsigned char s_kv[2 * KB * 128];
-  __shared__ float s_lse[kWaves][QT], s_D[kWaves][QT];
+  __shared__ __attribute__((aligned(16))) float s_lse[kWaves][QT];
+  __shared__ __attribute__((aligned(16))) float s_D[kWaves][QT];
   __shared__ int s_list[kListChunk];
   __shared__ int s_wcnt[kWaves];
   const int nblk = (a.K + KB - 1) / KB;
@@ -873,6 +874,10 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
           // all-ones where key kk has a weight: exp is taken for every score and masked (bitwise the
           // select; as `w ? exp : 0` the compiler branched around each exp under a lane mask)
           const uint32_t wm = (uint32_t)__builtin_amdgcn_sbfe((int)wts, kk, 1);
+          // lse / D of queries qt*16 + 4g .. + 3: one 16-B read each
+          const float4 l4 = *reinterpret_cast<const float4*>(&s_lse[wave][qt * 16 + 4 * g]);
+          const float4 d4 = *reinterpret_cast<const float4*>(&s_D[wave][qt * 16 + 4 * g]);
+          const float lr[4] = {l4.x, l4.y, l4.z, l4.w}, dr[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int qi = qt * 16 + 4 * g + r;
@@ -880,13 +885,13 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
             // branch gave, bitwise — the finite operands' signed zeros add nothing to dK / dV)
             // (one fma + v_exp_f32 on base-2 operands: __expf's x * log2 e multiply folded into them)
             const float p = __uint_as_float(
-                __float_as_uint(__builtin_amdgcn_exp2f(fmaf(st[r], sc2, -s_lse[wave][qi]))) & wm);
+                __float_as_uint(__builtin_amdgcn_exp2f(fmaf(st[r], sc2, -lr[r]))) & wm);
             const float dm = kBits     ? bit_scale(dmk, kt * 8 + qt * 4 + r, dscale)
                              : !a.seed ? 1.f
                                        : drop_mul(seed, thresh, dscale, (uint32_t)(s * a.H + h) * a.Lq + qi,
                                                   j0 + kk, k2);
             aa[kt][qt * 4 + r] = tobf(p * dm);
-            sa[kt][qt * 4 + r] = tobf(p * (dp[r] * dm - s_D[wave][qi]) * sc);
+            sa[kt][qt * 4 + r] = tobf(p * (dp[r] * dm - dr[r]) * sc);
           }
         }
       }
