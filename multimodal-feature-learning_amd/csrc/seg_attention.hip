@@ -143,30 +143,6 @@ __device__ __forceinline__ bf16x8 tr_b(const unsigned char* tile, int g, int li,
   return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
-// seg_attn_bwd_dkv's Q / dO tiles: 128-B rows, 16-B chunk c of row r at slot c ^ qs_sw(r), qs_sw(r) =
-// bits (0, 3, 1) of r.  A search over the GF(2) maps of the row bits: the one under which the
-// row-fragment writes (rows perm_row(kt*16 + li), chunks ks*4 + g), the A-operand ds_read_b128 reads
-// (the same rows) and the transposed B reads (rows 8g + qq (+4), 8-B pieces) all meet distinct banks
-// in their lane groups — the 144-B padded rows left two lanes on a bank in each of them
-__device__ __forceinline__ int qs_sw(int r) { return (r & 1) | (((r >> 3) & 1) << 1) | (((r >> 1) & 1) << 2); }
-__device__ __forceinline__ int qs_at(int r, int c) { return r * 128 + ((c ^ qs_sw(r)) << 4); }
-
-__device__ __forceinline__ void store_frags_sw(unsigned char* tile, const bf16x8 (&f)[2][2], int g, int li) {
-#pragma unroll
-  for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      *reinterpret_cast<bf16x8*>(tile + qs_at(perm_row(kt * 16 + li), ks * 4 + g)) = f[kt][ks];
-}
-
-__device__ __forceinline__ bf16x8 tr_b_sw(const unsigned char* tile, int g, int li, int cb) {
-  const int qq = li >> 2, pp = li & 3;
-  const int c = cb * 2 + (pp >> 1), w8 = (pp & 1) * 8;
-  const bf16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(tile + qs_at(8 * g + qq, c) + w8));
-  const bf16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4bf16((lds_bf16x4*)(tile + qs_at(8 * g + 4 + qq, c) + w8));
-  return __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
-}
-
 __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -742,7 +718,7 @@ __device__ __forceinline__ void load_segment(const Args& a, int s, int h, int d,
 // through LDS at the end
 template <bool kBits>
 __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
-  constexpr int kStage = 2 * QT * 128;                  // a wave's Q + dO rows (qs_at layout)
+  constexpr int kStage = 2 * QT * kRS;                  // a wave's Q + dO rows
   constexpr int kPart = 2 * 2 * 4 * 64 * 16;            // a wave's dK + dV tiles (f32x4 a lane)
   constexpr int kUnion = (kWaves - 1) * kPart > kWaves * kStage ? (kWaves - 1) * kPart : kWaves * kStage;
   __shared__ __attribute__((aligned(16))) unsigned char s_buf[kUnion];
@@ -766,7 +742,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
   const uint32_t inm = in_mask(j0, a.K);
   const long long rbase = ((long long)b * a.K + j0) * d + h * HD;
   unsigned char* const sq = s_buf + wave * kStage;
-  unsigned char* const sd = sq + QT * 128;
+  unsigned char* const sd = sq + QT * kRS;
   // the block's projected K and V rows (B operands of S = Q K^T and dP = dO V^T: column = key kt*16
   // + li; keys a segment reads as the bias row get no contribution here — seg_attn_bwd_dq sums
   // those) staged once in LDS for the 4 waves, 16 bytes a thread: per-wave register copies cost 32
@@ -822,8 +798,8 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
     for (int it = wave; it < total; it += kWaves) {
       const int s = s_list[it];
       wave_lds_fence();  // the previous segment's LDS reads are issued before these writes
-      store_frags_sw(sq, pf.q, g, li);
-      store_frags_sw(sd, pf.o, g, li);
+      store_frags(sq, pf.q, g, li);
+      store_frags(sd, pf.o, g, li);
       if (lane < QT) {
         s_lse[wave][lane] = pf.lse * kLog2e;  // (base-2: P = 2^(S sc log2 e - lse log2 e))
         s_D[wave][lane] = pf.D;
@@ -851,8 +827,8 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           const int row = perm_row(qt * 16 + li);
-          qa[qt][ks] = *reinterpret_cast<const bf16x8*>(sq + qs_at(row, ks * 4 + g));
-          oa[qt][ks] = *reinterpret_cast<const bf16x8*>(sd + qs_at(row, ks * 4 + g));
+          qa[qt][ks] = *reinterpret_cast<const bf16x8*>(sq + row * kRS + (ks * 32 + 8 * g) * 2);
+          oa[qt][ks] = *reinterpret_cast<const bf16x8*>(sd + row * kRS + (ks * 32 + 8 * g) * 2);
         }
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
@@ -897,7 +873,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
       }
 #pragma unroll
       for (int cb = 0; cb < 4; ++cb) {
-        const bf16x8 ob = tr_b_sw(sd, g, li, cb), qb = tr_b_sw(sq, g, li, cb);
+        const bf16x8 ob = tr_b(sd, g, li, cb), qb = tr_b(sq, g, li, cb);
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt) {
           dv[kt][cb] = mfma(aa[kt], ob, dv[kt][cb]);
