@@ -117,7 +117,8 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_fwd(const RT* __restrict__
   const int lane = threadIdx.x & 63;
   const uint64_t seed = drop.seed_ptr ? (uint64_t)drop.seed_ptr[0] : 0;
   const uint32_t thresh = drop_thresh(drop.p);
-  const long long row = (long long)blockIdx.x * kWaves + (threadIdx.x >> 6);
+  // (the wave index as a scalar: row, its bounds test and the row's base address stay scalar)
+  const long long row = (long long)blockIdx.x * kWaves + __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   if (row >= rows) return;  // wave-uniform
   const long long base = row * d;
   float z[CH][4];
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(kWaves * 64) void add_ln_bwd(
     long long rows, int d, RT* __restrict__ dr, YT* __restrict__ dy, float* __restrict__ part,
     const uint16_t* __restrict__ dout16, const uint16_t* __restrict__ dq16, float* __restrict__ dpos, Drop drop,
     int dpos_acc, int ysum) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // (scalar)
   const uint64_t seed = drop.seed_ptr ? (uint64_t)drop.seed_ptr[0] : 0;
   const uint32_t thresh = drop_thresh(drop.p);
   float dg[CH][4], db[CH][4], ys[CH][4];

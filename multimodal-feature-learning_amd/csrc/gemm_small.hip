@@ -49,7 +49,7 @@ __global__ __launch_bounds__(64 * KS) void gemm_nt_small_kernel(const uint16_t* 
                                                                  long long lda, long long ldb, long long ldc,
                                                                  int tiles_n) {
   __shared__ __attribute__((aligned(16))) float red[KS > 1 ? KS : 1][4][64][4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // (scalar)
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
   const int m0 = tm * kT, n0 = tn * kT;
   // fragments: lane l reads row (l & 15) of a 16-row block, K offset 8 (l >> 4) of a 32-step
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(64 * KS) void gemm_nn_small_kernel(const uint16_t* 
                                                                  int tiles_n) {
   __shared__ __attribute__((aligned(16))) float red[KS > 1 ? KS : 1][4][64][4];
   __shared__ __attribute__((aligned(16))) unsigned char sb[KS][kU][32 * kBS];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // (scalar)
   const int tm = blockIdx.x / tiles_n, tn = blockIdx.x % tiles_n;
   const int m0 = tm * kT, n0 = tn * kT;
   const int r = lane & 15, kq = (lane >> 4) * 8;

@@ -151,6 +151,12 @@ struct BlockMasks {
   uint32_t in, live, keep;  // bit kk: key j0+kk exists / is unmasked / reads the projected row
 };
 
+// an LDS word every lane reads at the same (wave-uniform) index, as a scalar: the compiler cannot
+// tell it is uniform and branched on conditions derived from it under lane masks
+__device__ __forceinline__ uint32_t uword(const uint32_t* w, int i) {
+  return (uint32_t)__builtin_amdgcn_readfirstlane((int)w[i]);
+}
+
 __device__ __forceinline__ uint32_t in_mask(int j0, int K) {
   return j0 + KB <= K ? 0xffffffffu : (j0 >= K ? 0u : (1u << (K - j0)) - 1u);
 }
@@ -255,7 +261,7 @@ __device__ __forceinline__ void store_frags(unsigned char* tile, const bf16x8 (&
 // the wave's next block at or after `from` (stride kWaves) with a non-zero weight on some key
 __device__ __forceinline__ int next_active(const uint32_t* s_live, int from, int nblk, bool dead) {
   int bb = from;
-  while (bb < nblk && !dead && s_live[bb] == 0u) bb += kWaves;
+  while (bb < nblk && !dead && uword(s_live, bb) == 0u) bb += kWaves;
   return bb;
 }
 
@@ -271,7 +277,7 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
   float(*const s_o)[QT][HD + 1] = reinterpret_cast<float(*)[QT][HD + 1]>(s_raw);
   __shared__ uint32_t s_live[kMaxBlk], s_keep[kMaxBlk];
   const int s = a.order ? a.order[blockIdx.x / a.H] : (int)(blockIdx.x / a.H), h = blockIdx.x % a.H;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, g = lane >> 4, li = lane & 15;  // (wave: scalar)
   const int d = a.H * HD;
   const long long b = a.index[s];
   const int nblk = (a.K + KB - 1) / KB;
@@ -301,14 +307,14 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
   int blk = next_active(s_live, wave, nblk, dead);
   bf16x8 kf[2][2], vf[2][2];
   if (blk < nblk) {
-    const BlockMasks mk{in_mask(blk * KB, a.K), s_live[blk], s_keep[blk]};
+    const BlockMasks mk{in_mask(blk * KB, a.K), uword(s_live, blk), uword(s_keep, blk)};
     const long long rbase = (b * a.K + blk * KB) * d + h * HD;
     row_frags(kf, a.pk + rbase, bk, mk, d, g, li);
     row_frags(vf, a.pv + rbase, bv, mk, d, g, li);
   }
   while (blk < nblk) {
     const int j0 = blk * KB;
-    const BlockMasks mk{in_mask(j0, a.K), s_live[blk], s_keep[blk]};
+    const BlockMasks mk{in_mask(j0, a.K), uword(s_live, blk), uword(s_keep, blk)};
     wave_lds_fence();
     store_frags(sv, vf, g, li);
     // keys with a score: the unmasked ones, or every existing key of a dead segment, whose scores are
@@ -330,7 +336,7 @@ __global__ __launch_bounds__(kThreads, 3) void seg_attn_fwd(Args a) {
       }
     const int nb = next_active(s_live, blk + kWaves, nblk, dead);
     if (nb < nblk) {
-      const BlockMasks mn{in_mask(nb * KB, a.K), s_live[nb], s_keep[nb]};
+      const BlockMasks mn{in_mask(nb * KB, a.K), uword(s_live, nb), uword(s_keep, nb)};
       const long long rbase = (b * a.K + nb * KB) * d + h * HD;
       row_frags(kf, a.pk + rbase, bk, mn, d, g, li);
       row_frags(vf, a.pv + rbase, bv, mn, d, g, li);
@@ -463,7 +469,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   __shared__ uint32_t s_live[kMaxBlk], s_keep[kMaxBlk];
   __shared__ float s_bias[kWaves][2][HD];
   const int s = a.order ? a.order[blockIdx.x / a.H] : (int)(blockIdx.x / a.H), h = blockIdx.x % a.H;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, g = lane >> 4, li = lane & 15;  // (wave: scalar)
   const int d = a.H * HD;
   const long long b = a.index[s];
   const int nblk = (a.K + KB - 1) / KB;
@@ -546,7 +552,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   constexpr bool bits = kBits;
   uint32_t wb = 0u;  // the block's keep bits (the forward's), loaded with its rows
   if (blk < nblk) {
-    const BlockMasks mk{in_mask(blk * KB, a.K), s_live[blk], s_keep[blk]};
+    const BlockMasks mk{in_mask(blk * KB, a.K), uword(s_live, blk), uword(s_keep, blk)};
     const long long rbase = (b * a.K + blk * KB) * d + h * HD;
     row_frags(kf, a.pk + rbase, bk, mk, d, g, li);
     row_frags(vf, a.pv + rbase, bv, mk, d, g, li);
@@ -554,7 +560,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
   }
   while (blk < nblk) {
     const int j0 = blk * KB;
-    const BlockMasks mk{in_mask(j0, a.K), s_live[blk], s_keep[blk]};
+    const BlockMasks mk{in_mask(j0, a.K), uword(s_live, blk), uword(s_keep, blk)};
     wave_lds_fence();
     store_frags(sk, kf, g, li);
     f32x4 st[2][2], dp[2][2];
@@ -571,7 +577,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
     const int nb = next_active(s_live, blk + kWaves, nblk, false);
     const uint32_t wc = wb;
     if (nb < nblk) {
-      const BlockMasks mn{in_mask(nb * KB, a.K), s_live[nb], s_keep[nb]};
+      const BlockMasks mn{in_mask(nb * KB, a.K), uword(s_live, nb), uword(s_keep, nb)};
       const long long rbase = (b * a.K + nb * KB) * d + h * HD;
       row_frags(kf, a.pk + rbase, bk, mn, d, g, li);
       row_frags(vf, a.pv + rbase, bv, mn, d, g, li);
@@ -735,7 +741,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dkv(Args a) {
   const int blk = bid % nblk;
   bid /= nblk;
   const int h = bid % a.H, b = bid / a.H;
-  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63, g = lane >> 4, li = lane & 15;
+  const int tid = threadIdx.x, wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63, g = lane >> 4, li = lane & 15;  // (wave: scalar)
   const int d = a.H * HD;
   const bool on = true;
   const int j0 = blk * KB;
