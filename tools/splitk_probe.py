@@ -35,13 +35,20 @@ def timeit(fn, reps=50):
 
 
 def main():
+    import os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
+    from conftest import PKG
+    global L
+    L = PKG.models.modules.linear
+    PKG._native.load_library()
     k = int(sys.argv[1]) if len(sys.argv) > 1 else 16120
     dev = torch.device("cuda", 0)
-    for n_out, n_in, cands in ((2048, 512, ((8, None), (8, 1984), (7, 2048), (8, 1920), (16, 1007), (16, 960))),
-                               (512, 2048, ((8, None), (8, 1984), (7, 2048), (8, 1920), (16, 1007), (16, 960))),
+    exact = ((8, 2015), (10, 1612), (13, 1240), (20, 806), (26, 620), (31, 520), (40, 403))  # divisors of 16,120
+    for n_out, n_in, cands in ((2048, 512, ((8, None), (8, 1984), (7, 2048), (8, 1920), (16, 1007), (16, 960)) + exact),
+                               (512, 2048, ((8, None), (8, 1984), (7, 2048), (8, 1920), (16, 1007), (16, 960)) + exact),
                                (512, 512, ((16, None), (16, 1000), (16, 960), (15, 1024), (16, 1008), (32, 496),
-                                           (32, 448), (8, 2015), (8, 1984))),
-                               (256, 512, ((16, None), (16, 1000), (16, 960), (15, 1024), (16, 1008), (32, 496)))):
+                                           (32, 448), (8, 1984)) + exact),
+                               (256, 512, ((16, None), (16, 1000), (16, 960), (15, 1024), (16, 1008), (32, 496)) + exact)):
         g2 = torch.randn(k, n_out, device=dev).to(torch.bfloat16)
         x2 = torch.randn(k, n_in, device=dev).to(torch.bfloat16)
         for s, c in cands:
@@ -49,7 +56,10 @@ def main():
             if s * c > k:
                 continue
             t = timeit(layout(g2, x2, s, c))
-            print(f"dW {n_out}x{n_in} K={k}: s={s:2d} c={c:5d} r={k - s * c:5d}  {t:7.2f} us", flush=True)
+            part = torch.randn(s + (1 if k - s * c else 0), n_out * n_in, device=dev)
+            ts = timeit(lambda: L._sum_slabs(part))
+            print(f"dW {n_out}x{n_in} K={k}: s={s:2d} c={c:5d} r={k - s * c:5d}  {t:7.2f} us  "
+                  f"+ slab sum {ts:6.2f} us", flush=True)
 
 
 if __name__ == "__main__":
