@@ -509,6 +509,7 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
       df[qt][ks] = qi < a.Lq ? load8(a.dout + off) : zero8();
     }
   }
+  const float sc2 = a.scale * kLog2e, lse2[2] = {lse[0] * kLog2e, lse[1] * kLog2e};
   f32x4 dq[2][4];
 #pragma unroll
   for (int qt = 0; qt < 2; ++qt)
@@ -596,7 +597,9 @@ __global__ __launch_bounds__(kThreads, 2) void seg_attn_bwd_dq(Args a) {
         for (int r = 0; r < 4; ++r) {
           const int kk = kt * 16 + 4 * g + r;
           const uint32_t lm = (uint32_t)__builtin_amdgcn_sbfe((int)mk.live, kk, 1);  // (masked exp: see dK / dV)
-          const float p = __uint_as_float(__float_as_uint(__expf(st[kt][qt][r] * a.scale - lse[qt])) & lm);
+          // (base-2 operands as in dK / dV: one fma + v_exp_f32)
+          const float p =
+              __uint_as_float(__float_as_uint(__builtin_amdgcn_exp2f(fmaf(st[kt][qt][r], sc2, -lse2[qt]))) & lm);
           const float dm =
               bits      ? bit_scale(wc, kt * 8 + qt * 4 + r, dscale)
               : !a.seed ? 1.f
